@@ -1,0 +1,128 @@
+"""Server process wiring: asyncio loop running the HTTP + gRPC front ends."""
+
+import asyncio
+import socket
+import threading
+
+import grpc
+from aiohttp import web
+
+from tritonclient.grpc import service_pb2_grpc
+
+from .core import InferenceServer
+from .grpc_frontend import GrpcFrontend
+from .http_frontend import HttpFrontend
+
+
+def default_models(gpu=False):
+    from .cpu_models import CPU_MODELS
+
+    models = list(CPU_MODELS)
+    if gpu:
+        from .gpu_models import GPU_MODELS
+
+        models += list(GPU_MODELS)
+    return models
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+GRPC_OPTIONS = [
+    ("grpc.max_send_message_length", 2**31 - 1),
+    ("grpc.max_receive_message_length", 2**31 - 1),
+    ("grpc.so_reuseport", 0),
+]
+
+
+async def serve(server, http_port, grpc_port, host="127.0.0.1", ready_evt=None, stop_evt=None):
+    server.loop = asyncio.get_running_loop()
+    runner = None
+    if http_port is not None:
+        runner = web.AppRunner(HttpFrontend(server).app, access_log=None)
+        await runner.setup()
+        site = web.TCPSite(runner, host, http_port, reuse_address=True)
+        await site.start()
+    gserver = None
+    if grpc_port is not None:
+        gserver = grpc.aio.server(options=GRPC_OPTIONS)
+        service_pb2_grpc.add_GRPCInferenceServiceServicer_to_server(GrpcFrontend(server), gserver)
+        gserver.add_insecure_port("%s:%d" % (host, grpc_port))
+        await gserver.start()
+    if ready_evt is not None:
+        ready_evt.set()
+    stop = stop_evt or asyncio.Event()
+    try:
+        await stop.wait()
+    finally:
+        if gserver is not None:
+            await gserver.stop(0.5)
+        if runner is not None:
+            await runner.cleanup()
+
+
+class ServerHandle:
+    """Runs an InferenceServer on a background thread (tests, benches)."""
+
+    def __init__(self, models=None, http_port=None, grpc_port=None, model_options=None, load=True):
+        self.http_port = http_port or _free_port()
+        self.grpc_port = grpc_port or _free_port()
+        self.server = InferenceServer(models if models is not None else default_models(), model_options)
+        if load:
+            self.server.load_all()
+        self._ready = threading.Event()
+        self._loop = None
+        self._stop = None
+        self._thread = threading.Thread(target=self._run, daemon=True)
+
+    @property
+    def http_url(self):
+        return "127.0.0.1:%d" % self.http_port
+
+    @property
+    def grpc_url(self):
+        return "127.0.0.1:%d" % self.grpc_port
+
+    def _run(self):
+        loop = asyncio.new_event_loop()
+        self._loop = loop
+        asyncio.set_event_loop(loop)
+
+        async def main():
+            self._stop = asyncio.Event()
+            await serve(self.server, self.http_port, self.grpc_port, ready_evt=self._ready, stop_evt=self._stop)
+
+        loop.run_until_complete(main())
+        loop.close()
+
+    def start(self, timeout=30):
+        self._thread.start()
+        if not self._ready.wait(timeout):
+            raise RuntimeError("server failed to start")
+        return self
+
+    def stop(self):
+        if self._loop is not None and self._stop is not None:
+            self._loop.call_soon_threadsafe(self._stop.set)
+            self._thread.join(10)
+        self.server.sys_shm.unregister()
+        try:
+            self.server.dev_shm.unregister()
+        except Exception:
+            pass
+        self.server.executor.shutdown(wait=False)
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *a):
+        self.stop()
+
+
+def start_server(**kw):
+    return ServerHandle(**kw).start()

@@ -1,0 +1,257 @@
+"""CPU model zoo used by the examples and the test-suite.
+
+Behaviour is pinned by the reference's example/test expectations:
+
+* ``simple`` / ``simple_string`` — add/sub of two [1,16] tensors
+  (reference src/python/examples/simple_http_infer_client.py:207-290,
+  simple_http_string_infer_client.py:41-105).
+* ``simple_identity`` — BYTES identity (simple_http_string_infer_client.py:110-141).
+* ``onnx_int32_int32_int32`` v1..3 — add/sub; v2,v3 swap the outputs
+  (reference src/c++/tests/cc_client_test.cc:435-470).
+* ``custom_identity_int32`` — identity with an execution delay, for timeout tests
+  (reference src/c++/tests/client_timeout_test.cc:421).
+* ``simple_sequence`` / ``simple_dyna_sequence`` / ``simple_string_dyna_sequence``
+  — stateful models (simple_grpc_sequence_sync_infer_client.py:186-205).
+* ``repeat_int32`` — decoupled: one response per IN element after DELAY[i] ms
+  (simple_grpc_custom_repeat.py:78-152).
+* ``preprocess_inception`` + ``preprocess_inception_ensemble`` — BYTES image ->
+  tensor -> classifier ensemble (ensemble_image_client.py).
+"""
+
+import threading
+import time
+
+import numpy as np
+
+from .model_base import Model, TensorSpec
+from .types import ServerError
+
+
+class SimpleAddSub(Model):
+    name = "simple"
+    max_batch_size = 8
+    inputs = (TensorSpec("INPUT0", "INT32", [16]), TensorSpec("INPUT1", "INT32", [16]))
+    outputs = (TensorSpec("OUTPUT0", "INT32", [16]), TensorSpec("OUTPUT1", "INT32", [16]))
+    swap_versions = ()
+
+    def execute(self, requests):
+        out = []
+        for r in requests:
+            try:
+                a = r.input("INPUT0").numpy()
+                b = r.input("INPUT1").numpy()
+                s, d = np.add(a, b, dtype=a.dtype), np.subtract(a, b, dtype=a.dtype)
+                if self.version in self.swap_versions:
+                    s, d = d, s
+                out.append([self.out("OUTPUT0", s), self.out("OUTPUT1", d)])
+            except Exception as e:  # per-request failure
+                out.append(e)
+        return out
+
+
+class OnnxInt32(SimpleAddSub):
+    name = "onnx_int32_int32_int32"
+    platform = "onnxruntime_onnx"
+    backend = "onnxruntime"
+    versions = (1, 2, 3)
+    swap_versions = (2, 3)
+
+
+class SimpleString(Model):
+    name = "simple_string"
+    max_batch_size = 8
+    inputs = (TensorSpec("INPUT0", "BYTES", [16]), TensorSpec("INPUT1", "BYTES", [16]))
+    outputs = (TensorSpec("OUTPUT0", "BYTES", [16]), TensorSpec("OUTPUT1", "BYTES", [16]))
+
+    def execute(self, requests):
+        res = []
+        for r in requests:
+            try:
+                a = r.input("INPUT0").numpy()
+                b = r.input("INPUT1").numpy()
+                ai = np.vectorize(lambda x: int(x))(a).astype(np.int64)
+                bi = np.vectorize(lambda x: int(x))(b).astype(np.int64)
+                s = np.array([str(x).encode() for x in (ai + bi).ravel()], dtype=np.object_)
+                d = np.array([str(x).encode() for x in (ai - bi).ravel()], dtype=np.object_)
+                res.append([self.out("OUTPUT0", s.reshape(a.shape)), self.out("OUTPUT1", d.reshape(a.shape))])
+            except Exception as e:
+                res.append(ServerError("simple_string: %s" % e))
+        return res
+
+
+class Identity(Model):
+    """Generic identity over one input (datatype set per instance)."""
+
+    name = "simple_identity"
+    max_batch_size = 8
+    datatype = "BYTES"
+
+    def __init__(self, version=1, **kw):
+        super().__init__(version, **kw)
+        self.inputs = (TensorSpec("INPUT0", self.datatype, [-1]),)
+        self.outputs = (TensorSpec("OUTPUT0", self.datatype, [-1]),)
+
+    def execute(self, requests):
+        delay_ms = float(self.options.get("delay_ms", 0))
+        if delay_ms:
+            time.sleep(delay_ms / 1000.0)
+        return [[self.out("OUTPUT0", r.input("INPUT0").numpy())] for r in requests]
+
+
+class CustomIdentityInt32(Identity):
+    name = "custom_identity_int32"
+    datatype = "INT32"
+
+    def __init__(self, version=1, **kw):
+        kw.setdefault("delay_ms", 500)
+        super().__init__(version, **kw)
+
+
+class IdentityFP32(Identity):
+    name = "identity_fp32"
+    datatype = "FP32"
+    max_batch_size = 0
+
+
+class IdentityBF16(Identity):
+    name = "identity_bf16"
+    datatype = "BF16"
+    max_batch_size = 0
+
+
+class SimpleSequence(Model):
+    """out = in + 1 on the START request, else out = in (int or string corrid)."""
+
+    name = "simple_sequence"
+    max_batch_size = 8
+    sequence_batching = True
+    inputs = (TensorSpec("INPUT", "INT32", [1]),)
+    outputs = (TensorSpec("OUTPUT", "INT32", [1]),)
+
+    def __init__(self, version=1, **kw):
+        super().__init__(version, **kw)
+        self._state = {}
+        self._lock = threading.Lock()
+
+    def _step(self, r, x):
+        return x + (1 if r.sequence_start else 0)
+
+    def execute(self, requests):
+        res = []
+        for r in requests:
+            if r.sequence_id in (0, ""):
+                res.append(ServerError(
+                    "inference request to model '%s' must specify a non-zero or non-empty correlation ID"
+                    % self.name))
+                continue
+            x = r.input("INPUT").numpy()
+            with self._lock:
+                y = self._step(r, x)
+                if r.sequence_end:
+                    self._state.pop(r.sequence_id, None)
+            res.append([self.out("OUTPUT", np.asarray(y, dtype=np.int32))])
+        return res
+
+
+class SimpleDynaSequence(SimpleSequence):
+    """Like simple_sequence, plus the correlation id on the END request."""
+
+    name = "simple_dyna_sequence"
+
+    def _step(self, r, x):
+        y = x + (1 if r.sequence_start else 0)
+        if r.sequence_end:
+            y = y + int(r.sequence_id)
+        return y
+
+
+class SimpleStringDynaSequence(SimpleSequence):
+    """Accumulator keyed by a string correlation id that must decode to int."""
+
+    name = "simple_string_dyna_sequence"
+
+    def _step(self, r, x):
+        try:
+            corr = int(r.sequence_id)
+        except (TypeError, ValueError):
+            raise ServerError("simple_string_dyna_sequence requires an integer-decodable sequence id")
+        if r.sequence_start:
+            acc = x.copy()
+        else:
+            acc = self._state.get(r.sequence_id, np.zeros_like(x)) + x
+        self._state[r.sequence_id] = acc
+        y = acc
+        if r.sequence_end:
+            y = acc + corr
+        return y
+
+
+class RepeatInt32(Model):
+    """Decoupled: for each element i of IN, sleep DELAY[i] ms then emit OUT=[IN[i]]
+    and IDX=[i]; WAIT ms are slept before releasing the request."""
+
+    name = "repeat_int32"
+    decoupled = True
+    inputs = (
+        TensorSpec("IN", "INT32", [-1]),
+        TensorSpec("DELAY", "UINT32", [-1]),
+        TensorSpec("WAIT", "UINT32", [1]),
+    )
+    outputs = (TensorSpec("OUT", "INT32", [1]), TensorSpec("IDX", "UINT32", [1]))
+
+    def execute_decoupled(self, request, emit):
+        vals = request.input("IN").numpy().ravel()
+        d = request.input("DELAY")
+        delays = d.numpy().ravel() if d is not None else np.zeros(len(vals), np.uint32)
+        w = request.input("WAIT")
+        wait = int(w.numpy().ravel()[0]) if w is not None else 0
+        if len(delays) != len(vals):
+            raise ServerError("repeat_int32: IN and DELAY must have the same length")
+        for i, v in enumerate(vals):
+            if delays[i]:
+                time.sleep(delays[i] / 1000.0)
+            emit([
+                self.out("OUT", np.array([v], dtype=np.int32)),
+                self.out("IDX", np.array([i], dtype=np.uint32)),
+            ])
+        if wait:
+            time.sleep(wait / 1000.0)
+
+
+class PreprocessInception(Model):
+    """Decode a raw image (BYTES: PPM/PGM or raw HxWx3 uint8 with a header) and
+    produce INCEPTION-scaled FP32 NCHW [3,224,224]."""
+
+    name = "preprocess_inception"
+    max_batch_size = 8
+    inputs = (TensorSpec("INPUT", "BYTES", [1]),)
+    outputs = (TensorSpec("OUTPUT", "FP32", [3, 224, 224]),)
+
+    def execute(self, requests):
+        from triton_client_amd.utils.image import decode_image, inception_preprocess
+
+        res = []
+        for r in requests:
+            blobs = r.input("INPUT").numpy().reshape(-1)
+            outs = []
+            for b in blobs:
+                img = decode_image(b)
+                outs.append(inception_preprocess(img, 224, 224, "NCHW"))
+            res.append([self.out("OUTPUT", np.stack(outs).astype(np.float32))])
+        return res
+
+
+CPU_MODELS = [
+    SimpleAddSub,
+    OnnxInt32,
+    SimpleString,
+    Identity,
+    CustomIdentityInt32,
+    IdentityFP32,
+    IdentityBF16,
+    SimpleSequence,
+    SimpleDynaSequence,
+    SimpleStringDynaSequence,
+    RepeatInt32,
+    PreprocessInception,
+]
