@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Flagship serving benchmark: perf_analyzer-style inferences/sec + p99 latency
+for ``densenet_onnx`` over gRPC with HIP shared memory (BASELINE.json metric).
+
+One process per GPU (``torch.distributed.run`` for N>1; RCCL over xGMI):
+
+  rank r: spawns the KServe-v2 bench server pinned to GPU r (child process,
+          HIP IPC needs two processes), allocates a HIP shm input region and
+          one output region per in-flight slot, receives the synthetic input
+          batch (K1 Philox on rank 0 -> RCCL broadcast into every rank's
+          region), registers the regions, then drives `concurrency` requests
+          in flight (closed loop) against its own server.
+
+A "step" = every in-flight slot completes one request (concurrency requests,
+each carrying `--batch` images).  W warmup steps, then EXACTLY K timed steps
+between barrier + device sync; elapsed = MAX over ranks; value = total images
+per second over all ranks (weak scaling: per-GPU work is fixed).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+
+def log(*a):
+    print("[bench rank %s]" % os.environ.get("RANK", "0"), *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=8, help="images per request (densenet_onnx bs)")
+    ap.add_argument("--concurrency", type=int, default=16, help="requests in flight per GPU")
+    ap.add_argument("--fanout", default="rccl", choices=["rccl", "p2p", "local"])
+    ap.add_argument("--instance-count", type=int, default=2)
+    ap.add_argument("--max-queue-delay-us", type=int, default=500)
+    ap.add_argument("--server-log", default="")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import tritonclient.grpc as grpcclient
+    from tritonclient.utils import hip_shared_memory as hipshm
+    from triton_client_amd.parallel import fanout
+    from triton_client_amd.perf.harness import ServerProcess
+    from triton_client_amd.perf.loadgen import ConcurrencyRun, percentile_us
+
+    bs, conc = args.batch, args.concurrency
+    log_path = args.server_log or os.path.join(REPO, "gpurun_out", "bench_server_r%d.log" % rank)
+    os.makedirs(os.path.dirname(log_path), exist_ok=True)
+    srv = ServerProcess(
+        device=local_rank,
+        models="densenet_onnx",
+        extra_args=["--instance-count", str(args.instance_count),
+                    "--max-queue-delay-us", str(args.max_queue_delay_us)],
+        log_path=log_path,
+    )
+    regions = []
+    client = None
+    try:
+        log("waiting for server (log %s)" % log_path)
+        srv.wait_ready(timeout=1500, model="densenet_onnx")
+        log("server ready")
+        client = grpcclient.InferenceServerClient(srv.grpc_url)
+
+        in_elems = bs * 3 * 224 * 224
+        in_bytes = in_elems * 4
+        out_bytes = bs * 1000 * 4
+        inp = hipshm.create_shared_memory_region("data_0_in", in_bytes, local_rank)
+        regions.append(inp)
+        method = fanout.fill_and_fanout(inp, "FP32", in_elems, seed=1234, mode="normal", lo=0.0, hi=1.0,
+                                        method=args.fanout)
+        if not fanout.verify_replicas(inp, in_bytes):
+            raise RuntimeError("fan-out replicas differ across ranks")
+        client.register_cuda_shared_memory("data_0_in", hipshm.get_raw_handle(inp), local_rank, in_bytes)
+        outs = []
+        for s in range(conc):
+            name = "fc6_1_out_%d" % s
+            r = hipshm.create_shared_memory_region(name, out_bytes, local_rank)
+            regions.append(r)
+            client.register_cuda_shared_memory(name, hipshm.get_raw_handle(r), local_rank, out_bytes)
+            o = grpcclient.InferRequestedOutput("fc6_1")
+            o.set_shared_memory(name, out_bytes)
+            outs.append([o])
+        x = grpcclient.InferInput("data_0", [bs, 3, 224, 224], "FP32")
+        x.set_shared_memory("data_0_in", in_bytes)
+        runner = ConcurrencyRun(client, "densenet_onnx", [x], outs, conc)
+
+        lat, errs, _ = runner.run(max(args.warmup, 1))
+        if errs:
+            raise RuntimeError("warmup errors: %s" % errs[0])
+        # sanity: outputs are finite logits
+        o0 = hipshm.get_contents_as_numpy(regions[1], np.float32, [bs, 1000])
+        if not np.isfinite(o0).all():
+            raise RuntimeError("non-finite logits in output region")
+        log("warmup done: p50 %.0f us" % percentile_us(lat, 50))
+
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lat, errs, _ = runner.run(args.steps)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if errs:
+            raise RuntimeError("%d request errors, first: %s" % (len(errs), errs[0]))
+        elapsed_max = fanout.max_over_ranks(elapsed)
+        all_lat = fanout.gather_arrays(lat)
+        images = world * args.steps * conc * bs
+        value = images / elapsed_max
+        stats = client.get_inference_statistics("densenet_onnx", as_json=True)
+        if rank == 0:
+            ms = stats["model_stats"][0]
+            execs = int(ms.get("execution_count", 0))
+            infers = int(ms.get("inference_count", 0))
+            res = {
+                "metric": "perf_analyzer inferences/sec (densenet_onnx, HIP shm)",
+                "value": round(value, 2),
+                "unit": "infer/sec",
+                "n_gpus": world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": round(1000.0 * elapsed_max / args.steps, 3),
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "bf16",
+                "data": "synthetic (K1 Philox normal on device, fanned out by %s), random-init weights" % method,
+                "config": {
+                    "model": "densenet_onnx",
+                    "global_batch": world * conc * bs,
+                    "seq_len": None,
+                    "parallelism": "dp%d" % world,
+                    "batch_size": bs,
+                    "concurrency_per_gpu": conc,
+                    "protocol": "grpc",
+                    "shared_memory": "hip",
+                },
+                "p50_latency_us": round(percentile_us(all_lat, 50), 1),
+                "p90_latency_us": round(percentile_us(all_lat, 90), 1),
+                "p99_latency_us": round(percentile_us(all_lat, 99), 1),
+                "requests_per_sec": round(value / bs, 2),
+                "server_avg_batch_rows_rank0": round(infers / max(execs, 1), 2),
+            }
+            print(json.dumps(res), flush=True)
+        return 0
+    finally:
+        try:
+            if client is not None:
+                client.unregister_cuda_shared_memory()
+                client.close()
+        except Exception as e:  # noqa: BLE001
+            log("cleanup error: %s" % e)
+        for r in regions:
+            try:
+                hipshm.destroy_shared_memory_region(r)
+            except Exception:
+                pass
+        srv.stop()
+        if world > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,178 @@
+"""HIP shared memory (the cuda_shared_memory replacement) and the zero-copy
+inference path through the GPU bench server.  Mirrors reference
+src/python/library/tests/test_cuda_shared_memory.py:37-168 plus the
+simple_*_cudashm_client examples."""
+
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hipshm():
+    import torch
+
+    torch.cuda.set_device(0)
+    from tritonclient.utils import hip_shared_memory
+
+    return hip_shared_memory
+
+
+def test_create_set_get_destroy(hipshm):
+    h = hipshm.create_shared_memory_region("r0", 256, 0)
+    assert "r0" in hipshm.allocated_shared_memory_regions()
+    a = np.arange(16, dtype=np.int32)
+    b = np.arange(16, 32, dtype=np.int32)
+    hipshm.set_shared_memory_region(h, [a, b])
+    np.testing.assert_array_equal(hipshm.get_contents_as_numpy(h, np.int32, [16]), a)
+    np.testing.assert_array_equal(hipshm.get_contents_as_numpy(h, np.int32, [16], offset=64), b)
+    raw = hipshm.get_raw_handle(h)
+    import base64
+
+    assert len(base64.b64decode(raw)) == 64
+    hipshm.destroy_shared_memory_region(h)
+    assert "r0" not in hipshm.allocated_shared_memory_regions()
+
+
+def test_bytes_roundtrip(hipshm):
+    from tritonclient.utils import serialize_byte_tensor
+
+    data = np.array([b"hello", b"", b"mi355x" * 10], dtype=np.object_)
+    ser = serialize_byte_tensor(data)
+    h = hipshm.create_shared_memory_region("rb", len(ser.item()), 0)
+    hipshm.set_shared_memory_region(h, [ser])
+    out = hipshm.get_contents_as_numpy(h, np.object_, [3])
+    assert list(out) == list(data)
+    hipshm.destroy_shared_memory_region(h)
+
+
+def test_dlpack_roundtrip_torch(hipshm):
+    import torch
+
+    h = hipshm.create_shared_memory_region("rd", 4 * 64, 0)
+    src = torch.arange(32, dtype=torch.float32, device="cuda")
+    host = torch.arange(32, 64, dtype=torch.float32)
+    hipshm.set_shared_memory_region_from_dlpack(h, [src, host])
+    view = torch.from_dlpack(hipshm.as_shared_memory_tensor(h, "FP32", [64]))
+    assert view.device.type == "cuda"
+    assert torch.equal(view.cpu(), torch.arange(64, dtype=torch.float32))
+    view[0] = 42.0  # zero-copy: writes land in the region
+    torch.cuda.synchronize()
+    assert hipshm.get_contents_as_numpy(h, np.float32, [1])[0] == 42.0
+    del view
+    hipshm.destroy_shared_memory_region(h)
+
+
+def test_device_side_synthetic_and_bf16(hipshm):
+    h = hipshm.create_shared_memory_region("rs", 4096, 0)
+    hipshm.fill_synthetic_data(h, "FP32", 1024, "constant", 1.5)
+    assert (hipshm.get_contents_as_numpy(h, np.float32, [1024]) == 1.5).all()
+    x = np.linspace(-3, 3, 512).astype(np.float32)
+    hipshm.set_shared_memory_region_from_fp32(h, x, "BF16")
+    from tritonclient.utils import deserialize_bf16_tensor, serialize_bf16_tensor
+
+    raw = hipshm.get_contents_as_numpy(h, np.uint8, [1024])
+    assert raw.tobytes() == serialize_bf16_tensor(x).item()
+    np.testing.assert_array_equal(deserialize_bf16_tensor(raw.tobytes()), deserialize_bf16_tensor(serialize_bf16_tensor(x).item()))
+    hipshm.destroy_shared_memory_region(h)
+
+
+@pytest.fixture(scope="module")
+def gpu_server():
+    from triton_client_amd.perf.harness import ServerProcess
+
+    log = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "pytest_gpu_server.log")
+    os.makedirs(os.path.dirname(log), exist_ok=True)
+    srv = ServerProcess(device=0, models="simple,densenet_onnx", log_path=log,
+                        extra_args=["--instance-count", "1"])
+    try:
+        srv.wait_ready(timeout=900, model="densenet_onnx")
+        yield srv
+    finally:
+        srv.stop()
+
+
+def test_simple_cudashm_grpc(gpu_server, hipshm):
+    """Port of simple_grpc_cudashm_client.py: INT32 add/sub via device shm."""
+    import tritonclient.grpc as grpcclient
+
+    c = grpcclient.InferenceServerClient(gpu_server.grpc_url)
+    c.unregister_cuda_shared_memory()
+    a = np.arange(16, dtype=np.int32).reshape(1, 16)
+    b = np.ones((1, 16), dtype=np.int32)
+    hin = hipshm.create_shared_memory_region("in_data", 128, 0)
+    hout = hipshm.create_shared_memory_region("out_data", 128, 0)
+    hipshm.set_shared_memory_region(hin, [a, b])
+    c.register_cuda_shared_memory("in_data", hipshm.get_raw_handle(hin), 0, 128)
+    c.register_cuda_shared_memory("out_data", hipshm.get_raw_handle(hout), 0, 128)
+    st = c.get_cuda_shared_memory_status(as_json=True)
+    assert set(st["regions"]) == {"in_data", "out_data"}
+    ins = [grpcclient.InferInput("INPUT0", [1, 16], "INT32"), grpcclient.InferInput("INPUT1", [1, 16], "INT32")]
+    ins[0].set_shared_memory("in_data", 64)
+    ins[1].set_shared_memory("in_data", 64, offset=64)
+    outs = [grpcclient.InferRequestedOutput("OUTPUT0"), grpcclient.InferRequestedOutput("OUTPUT1")]
+    outs[0].set_shared_memory("out_data", 64)
+    outs[1].set_shared_memory("out_data", 64, offset=64)
+    c.infer("simple", ins, outputs=outs)
+    np.testing.assert_array_equal(hipshm.get_contents_as_numpy(hout, np.int32, [1, 16]), a + b)
+    np.testing.assert_array_equal(hipshm.get_contents_as_numpy(hout, np.int32, [1, 16], offset=64), a - b)
+    c.unregister_cuda_shared_memory()
+    hipshm.destroy_shared_memory_region(hin)
+    hipshm.destroy_shared_memory_region(hout)
+    c.close()
+
+
+def _reference_logits(x):
+    import torch
+
+    from triton_client_amd.models import densenet
+
+    m = densenet.build(device="cuda", dtype=torch.float32)
+    with torch.no_grad():
+        return m(torch.from_numpy(x).cuda()).cpu().numpy()
+
+
+def test_densenet_zero_copy_matches_fp32_reference(gpu_server, hipshm):
+    """densenet_onnx bs=2 through HIP shm (K6 gather in, K7 scatter out)
+    against an fp32 torch reference of the same random-init weights."""
+    import tritonclient.grpc as grpcclient
+    import tritonclient.http as httpclient
+
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((2, 3, 224, 224)).astype(np.float32)
+    ref = _reference_logits(x)
+    hin = hipshm.create_shared_memory_region("d_in", x.nbytes, 0)
+    hout = hipshm.create_shared_memory_region("d_out", 2 * 1000 * 4, 0)
+    hipshm.set_shared_memory_region(hin, [x])
+    g = grpcclient.InferenceServerClient(gpu_server.grpc_url)
+    g.register_cuda_shared_memory("d_in", hipshm.get_raw_handle(hin), 0, x.nbytes)
+    g.register_cuda_shared_memory("d_out", hipshm.get_raw_handle(hout), 0, 8000)
+    inp = grpcclient.InferInput("data_0", [2, 3, 224, 224], "FP32")
+    inp.set_shared_memory("d_in", x.nbytes)
+    out = grpcclient.InferRequestedOutput("fc6_1")
+    out.set_shared_memory("d_out", 8000)
+    r = g.infer("densenet_onnx", [inp], outputs=[out])
+    assert r.get_output("fc6_1").parameters["shared_memory_region"].string_param == "d_out"
+    got = hipshm.get_contents_as_numpy(hout, np.float32, [2, 1000])
+    err = np.abs(got - ref).max() / (np.abs(ref).max() + 1e-6)
+    assert err < 0.05, err
+    assert (got.argmax(1) == ref.argmax(1)).all() or err < 0.02
+    # same request over HTTP with host (binary) input and output
+    h = httpclient.InferenceServerClient(gpu_server.http_url)
+    hi = httpclient.InferInput("data_0", [2, 3, 224, 224], "FP32")
+    hi.set_data_from_numpy(x)
+    res = h.infer("densenet_onnx", [hi], outputs=[httpclient.InferRequestedOutput("fc6_1")])
+    np.testing.assert_allclose(res.as_numpy("fc6_1"), got, rtol=0, atol=1e-5)
+    # classification extension
+    res = h.infer("densenet_onnx", [hi], outputs=[httpclient.InferRequestedOutput("fc6_1", class_count=3)])
+    top = res.as_numpy("fc6_1")
+    assert top.shape == (2, 3)
+    assert int(top[0, 0].decode().split(":")[1]) == int(got[0].argmax())
+    g.unregister_cuda_shared_memory()
+    hipshm.destroy_shared_memory_region(hin)
+    hipshm.destroy_shared_memory_region(hout)
+    g.close()
+    h.close()

@@ -1,0 +1,240 @@
+"""Numerics of the CDNA4 kernels (csrc/kernels/*.hip) against numpy / fp32
+torch references of the same op.  All tests run through libtcamd_hip.so."""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from tests.philox_ref import raw_u32, uniform_f32  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+
+    from triton_client_amd.ops import hip
+
+    torch.cuda.set_device(0)
+    return torch, hip
+
+
+def _stream(torch):
+    return torch.cuda.current_stream().cuda_stream
+
+
+def test_native_library_is_loaded(env):
+    torch, hip = env
+    import os
+
+    assert os.path.exists(hip.loaded_path())
+    assert hip.device_count() >= 1
+    assert hip.device_arch(0).startswith("gfx950")
+
+
+@pytest.mark.parametrize("n", [1, 15, 4096, 1000003])
+def test_synth_uniform_fp32_matches_philox_reference(env, n):
+    torch, hip = env
+    t = torch.empty(n + 16, device="cuda", dtype=torch.float32)
+    hip.synth_fill(t.data_ptr(), n, "FP32", hip.SYNTH_UNIFORM, -2.0, 3.0, seed=99, stream_id=5,
+                   stream=_stream(torch))
+    got = t[:n].cpu().numpy()
+    ref = uniform_f32(n, -2.0, 3.0, seed=99, stream_id=5)
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_synth_int32_range_and_determinism(env):
+    torch, hip = env
+    n = 100000
+    a = torch.empty(n, device="cuda", dtype=torch.int32)
+    b = torch.empty(n, device="cuda", dtype=torch.int32)
+    for t in (a, b):
+        hip.synth_fill(t.data_ptr(), n, "INT32", hip.SYNTH_UNIFORM, 0, 30521, seed=3, stream=_stream(torch))
+    assert torch.equal(a, b)
+    x = a.cpu().numpy()
+    assert x.min() >= 0 and x.max() <= 30521
+    ref = (raw_u32(n, 4, seed=3).astype(np.int64) % 30522).astype(np.int32)
+    np.testing.assert_array_equal(x, ref)
+
+
+@pytest.mark.parametrize("dt,tdt", [("BF16", "bfloat16"), ("FP16", "float16"), ("INT8", "int8"),
+                                    ("UINT8", "uint8"), ("INT64", "int64"), ("BOOL", "bool")])
+def test_synth_other_dtypes(env, dt, tdt):
+    torch, hip = env
+    n = 4099
+    t = torch.zeros(n + 64, device="cuda", dtype=getattr(torch, tdt))
+    lo, hi = (0, 1) if dt == "BOOL" else (-5, 5) if dt in ("INT8", "INT64") else (0, 200) if dt == "UINT8" else (-1.0, 1.0)
+    hip.synth_fill(t.data_ptr(), n, dt, hip.SYNTH_UNIFORM, lo, hi, seed=11, stream=_stream(torch))
+    x = t[:n].float().cpu().numpy()
+    assert x.min() >= lo and x.max() <= hi
+    assert np.unique(x).size > 1
+    assert (t[n:].float() == 0).all()  # no overrun past n elements
+
+
+def test_synth_zero_const_normal(env):
+    torch, hip = env
+    n = 1 << 20
+    t = torch.ones(n, device="cuda")
+    hip.synth_fill(t.data_ptr(), n, "FP32", hip.SYNTH_ZERO, stream=_stream(torch))
+    assert float(t.abs().sum()) == 0.0
+    hip.synth_fill(t.data_ptr(), n, "FP32", hip.SYNTH_CONST, 2.5, stream=_stream(torch))
+    assert bool((t == 2.5).all())
+    hip.synth_fill(t.data_ptr(), n, "FP32", hip.SYNTH_NORMAL, 1.0, 2.0, seed=4, stream=_stream(torch))
+    assert abs(float(t.mean()) - 1.0) < 0.02 and abs(float(t.std()) - 2.0) < 0.02
+
+
+@pytest.mark.parametrize("n", [7, 8, 1023, 262147])
+def test_convert_bf16_trunc_is_wire_compatible(env, n):
+    torch, hip = env
+    from tritonclient.utils import serialize_bf16_tensor
+
+    x = torch.randn(n, device="cuda") * 100
+    y = torch.empty(n, device="cuda", dtype=torch.int16)
+    hip.convert(x.data_ptr(), "FP32", y.data_ptr(), "BF16", n, "trunc", _stream(torch))
+    got = y.cpu().numpy().tobytes()
+    assert got == serialize_bf16_tensor(x.cpu().numpy()).item()
+
+
+def test_convert_bf16_rne_matches_torch(env):
+    torch, hip = env
+    n = 100003
+    x = torch.randn(n, device="cuda") * 10
+    y = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    hip.convert(x.data_ptr(), "FP32", y.data_ptr(), "BF16", n, "rne", _stream(torch))
+    assert torch.equal(y, x.to(torch.bfloat16))
+    back = torch.empty(n, device="cuda")
+    hip.convert(y.data_ptr(), "BF16", back.data_ptr(), "FP32", n, stream=_stream(torch))
+    assert torch.equal(back, y.float())
+
+
+def test_convert_fp16_roundtrip(env):
+    torch, hip = env
+    n = 65541
+    x = torch.randn(n, device="cuda") * 50
+    y = torch.empty(n, device="cuda", dtype=torch.float16)
+    hip.convert(x.data_ptr(), "FP32", y.data_ptr(), "FP16", n, stream=_stream(torch))
+    assert torch.equal(y, x.half())
+    z = torch.empty(n, device="cuda")
+    hip.convert(y.data_ptr(), "FP16", z.data_ptr(), "FP32", n, stream=_stream(torch))
+    assert torch.equal(z, y.float())
+
+
+@pytest.mark.parametrize("fmt,tfmt", [("FP8_E4M3", "float8_e4m3fn"), ("FP8_E5M2", "float8_e5m2")])
+def test_convert_fp8_matches_reference(env, fmt, tfmt):
+    torch, hip = env
+    from tritonclient.utils import deserialize_fp8_tensor, serialize_fp8_tensor
+
+    n = 40961
+    x = torch.randn(n, device="cuda") * (100 if fmt == "FP8_E4M3" else 10000)
+    y = torch.empty(n, device="cuda", dtype=torch.uint8)
+    hip.convert(x.data_ptr(), "FP32", y.data_ptr(), fmt, n, stream=_stream(torch))
+    got = y.cpu().numpy()
+    ref = np.frombuffer(serialize_fp8_tensor(x.cpu().numpy(), fmt).item(), dtype=np.uint8)
+    np.testing.assert_array_equal(got, ref)
+    # in-range values also match torch's (non-saturating) float8 cast
+    maxv = 448.0 if fmt == "FP8_E4M3" else 57344.0
+    inr = x.abs() < maxv
+    tref = x.to(getattr(torch, tfmt)).view(torch.uint8)
+    assert torch.equal(y[inr], tref[inr])
+    z = torch.empty(n, device="cuda")
+    hip.convert(y.data_ptr(), fmt, z.data_ptr(), "FP32", n, stream=_stream(torch))
+    np.testing.assert_array_equal(z.cpu().numpy(), deserialize_fp8_tensor(got.tobytes(), fmt))
+
+
+def test_layout_pack_nchw_to_nhwc_bf16_gather(env):
+    torch, hip = env
+    imgs = [torch.randn(3, 224, 224, device="cuda") for _ in range(5)]
+    out = torch.empty(5, 224, 224, 3, device="cuda", dtype=torch.bfloat16)
+    hip.layout_pack([t.data_ptr() for t in imgs], "FP32", "NCHW", out.data_ptr(), "BF16", "NHWC", 3, 224, 224,
+                    stream=_stream(torch))
+    ref = torch.stack(imgs).permute(0, 2, 3, 1).to(torch.bfloat16)
+    assert torch.equal(out, ref)
+
+
+def test_layout_pack_affine_u8_nhwc_to_nchw(env):
+    torch, hip = env
+    img = torch.randint(0, 256, (2, 64, 48, 3), device="cuda", dtype=torch.uint8)
+    out = torch.empty(2, 3, 64, 48, device="cuda")
+    scale = [1 / 127.5] * 3
+    bias = [-1.0] * 3
+    hip.layout_pack([img[0].data_ptr(), img[1].data_ptr()], "UINT8", "NHWC", out.data_ptr(), "FP32", "NCHW",
+                    3, 64, 48, scale=scale, bias=bias, stream=_stream(torch))
+    ref = img.permute(0, 3, 1, 2).float() * (1 / 127.5) - 1.0
+    assert torch.allclose(out, ref, atol=1e-6)
+
+
+@pytest.mark.parametrize("C,H,W", [(37, 9, 13), (64, 14, 14), (5, 7, 7)])
+def test_layout_pack_general_c_tiled_path(env, C, H, W):
+    torch, hip = env
+    x = torch.randn(3, C, H, W, device="cuda")
+    out = torch.empty(3, H, W, C, device="cuda", dtype=torch.float16)
+    hip.layout_pack([x[i].data_ptr() for i in range(3)], "FP32", "NCHW", out.data_ptr(), "FP16", "NHWC",
+                    C, H, W, stream=_stream(torch))
+    assert torch.equal(out, x.permute(0, 2, 3, 1).half())
+    back = torch.empty(3, C, H, W, device="cuda")
+    hip.layout_pack([out[i].data_ptr() for i in range(3)], "FP16", "NHWC", back.data_ptr(), "FP32", "NCHW",
+                    C, H, W, stream=_stream(torch))
+    assert torch.equal(back, x.half().float())
+
+
+def test_batched_copy_mixed_alignment(env):
+    torch, hip = env
+    src = torch.randint(0, 255, (1 << 20,), device="cuda", dtype=torch.uint8)
+    dst = torch.zeros_like(src)
+    rng = np.random.default_rng(0)
+    srcs, dsts, sizes = [], [], []
+    off = 0
+    for i in range(40):
+        n = int(rng.integers(1, 20000))
+        so = int(rng.integers(0, 4)) if i % 3 == 0 else 0
+        srcs.append(src.data_ptr() + off + so)
+        dsts.append(dst.data_ptr() + off)
+        sizes.append(n)
+        off += ((n + so + 15) // 16) * 16 + 16
+    hip.batched_copy(srcs, dsts, sizes, _stream(torch))
+    torch.cuda.synchronize()
+    s = src.cpu().numpy()
+    d = dst.cpu().numpy()
+    for sp, dp, n in zip(srcs, dsts, sizes):
+        a = sp - src.data_ptr()
+        b = dp - dst.data_ptr()
+        assert (s[a : a + n] == d[b : b + n]).all()
+
+
+def test_pack_and_index_bytes_match_wire_format(env):
+    torch, hip = env
+    from tritonclient.utils import serialize_byte_tensor
+
+    rng = np.random.default_rng(1)
+    elems = [bytes(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8)) for _ in range(5000)]
+    lens = np.array([len(e) for e in elems], dtype=np.uint32)
+    payload = np.frombuffer(b"".join(elems), dtype=np.uint8)
+    d_payload = torch.from_numpy(payload.copy()).cuda()
+    d_lens = torch.from_numpy(lens.view(np.int32).copy()).cuda()
+    total = int(lens.sum()) + 4 * len(elems)
+    out = torch.zeros(total, device="cuda", dtype=torch.uint8)
+    ws = torch.empty(hip.pack_bytes_workspace(len(elems)), device="cuda", dtype=torch.uint8)
+    hip.pack_bytes(d_payload.data_ptr(), d_lens.data_ptr(), len(elems), out.data_ptr(), ws.data_ptr(),
+                   _stream(torch))
+    ref = serialize_byte_tensor(np.array(elems, dtype=np.object_)).item()
+    assert out.cpu().numpy().tobytes() == ref
+    offs = torch.empty(len(elems), device="cuda", dtype=torch.int64)
+    lns = torch.empty(len(elems), device="cuda", dtype=torch.int32)
+    status = torch.zeros(4, device="cuda", dtype=torch.int32)
+    hip.index_bytes(out.data_ptr(), total, len(elems), offs.data_ptr(), lns.data_ptr(), status.data_ptr(),
+                    _stream(torch))
+    st = status.cpu().numpy()
+    assert st[0] == 0
+    np.testing.assert_array_equal(lns.cpu().numpy().view(np.uint32), lens)
+    exp_offs = np.cumsum(np.concatenate([[0], lens[:-1].astype(np.int64) + 4])) + 4
+    np.testing.assert_array_equal(offs.cpu().numpy(), exp_offs)
+
+
+def test_index_bytes_detects_malformed(env):
+    torch, hip = env
+    buf = torch.tensor([5, 0, 0, 0, 1, 2], device="cuda", dtype=torch.uint8)
+    offs = torch.empty(4, device="cuda", dtype=torch.int64)
+    lns = torch.empty(4, device="cuda", dtype=torch.int32)
+    status = torch.zeros(4, device="cuda", dtype=torch.int32)
+    hip.index_bytes(buf.data_ptr(), 6, 1, offs.data_ptr(), lns.data_ptr(), status.data_ptr(), _stream(torch))
+    assert int(status[0]) == -1

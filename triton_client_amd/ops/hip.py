@@ -1,0 +1,444 @@
+"""ctypes binding of libtcamd_hip.so: HIP runtime glue and CDNA4 kernels.
+
+Runtime: device memory, pinned host memory, IPC handles, copies, streams,
+events, peer access.  Kernels (csrc/kernels/*.hip, gfx950):
+
+* :func:`synth_fill`      K1 Philox synthetic data (random/zero/constant/normal)
+* :func:`convert`         K4/K5 FP32 <-> BF16 (trunc|RNE) / FP16 / FP8 e4m3,e5m2
+* :func:`layout_pack`     K6 fused gather + NCHW<->NHWC + convert + scale/bias
+* :func:`batched_copy`    K7 one-launch gather/concat/scatter of byte ranges
+* :func:`pack_bytes`      K2 BYTES serialisation (LDS block scan + scatter)
+* :func:`index_bytes`     K3 BYTES index walk through an LDS window
+
+Pointers are plain ints (device addresses).  ``stream`` is a hipStream_t as an
+int (``torch.cuda.current_stream().cuda_stream`` works) or None for the
+library's per-device copy stream / the null stream.
+"""
+
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+from . import dtypes
+
+_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libtcamd_hip.so")
+IPC_HANDLE_SIZE = 64
+
+MEMORY_UNREGISTERED = 0
+MEMORY_HOST = 1
+MEMORY_DEVICE = 2
+MEMORY_MANAGED = 3
+
+
+class HipError(RuntimeError):
+    def __init__(self, code, what):
+        self.code = code
+        msg = _lib.tcamd_error_string(code).decode() if _lib is not None else str(code)
+        super().__init__("%s failed: %s (hipError %d)" % (what, msg, code))
+
+
+_lib = None
+
+_SIGS = {
+    "tcamd_error_string": ([ctypes.c_int], ctypes.c_char_p),
+    "tcamd_ipc_handle_size": ([], ctypes.c_int),
+    "tcamd_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "tcamd_set_device": ([ctypes.c_int], ctypes.c_int),
+    "tcamd_get_device": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "tcamd_device_synchronize": ([ctypes.c_int], ctypes.c_int),
+    "tcamd_device_uva": ([ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "tcamd_device_name": ([ctypes.c_int, ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
+    "tcamd_malloc": ([ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "tcamd_free": ([ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
+    "tcamd_host_alloc": ([ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "tcamd_host_free": ([ctypes.c_void_p], ctypes.c_int),
+    "tcamd_host_register": ([ctypes.c_void_p, ctypes.c_size_t], ctypes.c_int),
+    "tcamd_host_unregister": ([ctypes.c_void_p], ctypes.c_int),
+    "tcamd_ipc_get_handle": ([ctypes.c_void_p, ctypes.c_char_p], ctypes.c_int),
+    "tcamd_ipc_open": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "tcamd_ipc_close": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
+    "tcamd_pointer_info": (
+        [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
+        ctypes.c_int,
+    ),
+    "tcamd_memcpy": ([ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t], ctypes.c_int),
+    "tcamd_memcpy_async": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
+    "tcamd_memset_async": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p], ctypes.c_int),
+    "tcamd_memcpy_peer_async": (
+        [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "tcamd_enable_peer": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "tcamd_stream_create": ([ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "tcamd_stream_destroy": ([ctypes.c_void_p], ctypes.c_int),
+    "tcamd_stream_synchronize": ([ctypes.c_void_p], ctypes.c_int),
+    "tcamd_event_create": ([ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "tcamd_event_destroy": ([ctypes.c_void_p], ctypes.c_int),
+    "tcamd_event_record": ([ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "tcamd_event_synchronize": ([ctypes.c_void_p], ctypes.c_int),
+    "tcamd_event_elapsed_ms": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+    "tcamd_stream_wait_event": ([ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "tcamd_last_error": ([], ctypes.c_int),
+    # kernels
+    "tcamd_synth_fill": (
+        [
+            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+            ctypes.c_double, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
+    "tcamd_convert": (
+        [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "tcamd_layout_pack": (
+        [
+            ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+            ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
+    "tcamd_batched_copy": (
+        [
+            ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64),
+            ctypes.c_int, ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
+    "tcamd_pack_bytes_workspace": ([ctypes.c_uint64], ctypes.c_uint64),
+    "tcamd_pack_bytes": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "tcamd_index_bytes": (
+        [
+            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
+}
+
+
+def _load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_PATH):
+        raise ImportError(
+            "libtcamd_hip.so is not built (expected at %s); run `python __graft_entry__.py build`" % _PATH
+        )
+    # One HIP runtime per process: torch bundles libamdhip64.so.7 with the same
+    # SONAME, so whichever copy is loaded first is shared by both.
+    lib = ctypes.CDLL(_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (argtypes, restype) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    _lib = lib
+    return lib
+
+
+def lib():
+    return _load()
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise HipError(rc, what)
+
+
+def _vp(x):
+    return None if x is None or x == 0 else ctypes.c_void_p(int(x))
+
+
+def loaded_path():
+    return _PATH
+
+
+# ---------------------------------------------------------------------------
+# runtime
+# ---------------------------------------------------------------------------
+def device_count():
+    n = ctypes.c_int(0)
+    rc = _load().tcamd_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def set_device(dev):
+    _check(_load().tcamd_set_device(dev), "hipSetDevice")
+
+
+def get_device():
+    d = ctypes.c_int(0)
+    _check(_load().tcamd_get_device(ctypes.byref(d)), "hipGetDevice")
+    return d.value
+
+
+def synchronize(dev=0):
+    _check(_load().tcamd_device_synchronize(dev), "hipDeviceSynchronize")
+
+
+def device_uva(dev):
+    v = ctypes.c_int(0)
+    _check(_load().tcamd_device_uva(dev, ctypes.byref(v)), "hipGetDeviceProperties")
+    return bool(v.value)
+
+
+def device_arch(dev=0):
+    buf = ctypes.create_string_buffer(128)
+    _check(_load().tcamd_device_name(dev, buf, 128), "hipGetDeviceProperties")
+    return buf.value.decode()
+
+
+def malloc(dev, nbytes):
+    p = ctypes.c_void_p()
+    _check(_load().tcamd_malloc(dev, nbytes, ctypes.byref(p)), "hipMalloc(%d B)" % nbytes)
+    return p.value
+
+
+def free(dev, ptr):
+    _check(_load().tcamd_free(dev, _vp(ptr)), "hipFree")
+
+
+def host_alloc(nbytes):
+    p = ctypes.c_void_p()
+    _check(_load().tcamd_host_alloc(nbytes, ctypes.byref(p)), "hipHostMalloc")
+    return p.value
+
+
+def host_free(ptr):
+    _check(_load().tcamd_host_free(_vp(ptr)), "hipHostFree")
+
+
+def host_register(ptr, nbytes):
+    _check(_load().tcamd_host_register(_vp(ptr), nbytes), "hipHostRegister")
+
+
+def host_unregister(ptr):
+    _check(_load().tcamd_host_unregister(_vp(ptr)), "hipHostUnregister")
+
+
+def ipc_get_handle(ptr):
+    buf = ctypes.create_string_buffer(IPC_HANDLE_SIZE)
+    _check(_load().tcamd_ipc_get_handle(_vp(ptr), buf), "hipIpcGetMemHandle")
+    return buf.raw
+
+
+def ipc_open(handle, dev):
+    if len(handle) != IPC_HANDLE_SIZE:
+        raise ValueError("IPC handle must be %d bytes" % IPC_HANDLE_SIZE)
+    p = ctypes.c_void_p()
+    _check(_load().tcamd_ipc_open(bytes(handle), dev, ctypes.byref(p)), "hipIpcOpenMemHandle")
+    return p.value
+
+
+def ipc_close(ptr, dev):
+    _check(_load().tcamd_ipc_close(_vp(ptr), dev), "hipIpcCloseMemHandle")
+
+
+def pointer_info(ptr):
+    mt = ctypes.c_int(0)
+    dev = ctypes.c_int(-1)
+    _check(_load().tcamd_pointer_info(_vp(ptr), ctypes.byref(mt), ctypes.byref(dev)), "hipPointerGetAttributes")
+    return mt.value, dev.value
+
+
+def _host_ptr(buf):
+    if isinstance(buf, np.ndarray):
+        if not buf.flags["C_CONTIGUOUS"]:
+            raise ValueError("host buffer must be C-contiguous")
+        return buf.ctypes.data
+    if isinstance(buf, int):
+        return buf
+    return ctypes.addressof(ctypes.c_char.from_buffer(buf))
+
+
+def memcpy(dst, src, nbytes, dev=0):
+    """Synchronous copy (any direction, UVA) on the per-device copy stream."""
+    if nbytes:
+        _check(_load().tcamd_memcpy(dev, _vp(dst), _vp(src), nbytes), "hipMemcpy")
+
+
+def memcpy_h2d(dst_ptr, host, nbytes, dev=0):
+    memcpy(dst_ptr, _host_ptr(host), nbytes, dev)
+
+
+def memcpy_d2h(host, src_ptr, nbytes, dev=0):
+    memcpy(_host_ptr(host), src_ptr, nbytes, dev)
+
+
+def memcpy_d2d(dst_ptr, src_ptr, nbytes, dev=0):
+    memcpy(dst_ptr, src_ptr, nbytes, dev)
+
+
+def memcpy_async(dst, src, nbytes, stream=None):
+    if nbytes:
+        _check(_load().tcamd_memcpy_async(_vp(dst), _vp(src), nbytes, _vp(stream)), "hipMemcpyAsync")
+
+
+def memset_async(dst, value, nbytes, stream=None):
+    _check(_load().tcamd_memset_async(_vp(dst), value, nbytes, _vp(stream)), "hipMemsetAsync")
+
+
+def memcpy_peer_async(dst, dst_dev, src, src_dev, nbytes, stream=None):
+    _check(
+        _load().tcamd_memcpy_peer_async(_vp(dst), dst_dev, _vp(src), src_dev, nbytes, _vp(stream)),
+        "hipMemcpyPeerAsync",
+    )
+
+
+def enable_peer(dev, peer):
+    _check(_load().tcamd_enable_peer(dev, peer), "hipDeviceEnablePeerAccess(%d->%d)" % (dev, peer))
+
+
+class Stream:
+    """A non-blocking HIP stream owned by this library."""
+
+    def __init__(self, dev=0):
+        self.dev = dev
+        s = ctypes.c_void_p()
+        _check(_load().tcamd_stream_create(dev, ctypes.byref(s)), "hipStreamCreate")
+        self.handle = s.value
+
+    def synchronize(self):
+        _check(_load().tcamd_stream_synchronize(_vp(self.handle)), "hipStreamSynchronize")
+
+    def close(self):
+        if self.handle:
+            _load().tcamd_stream_destroy(_vp(self.handle))
+            self.handle = None
+
+    def __int__(self):
+        return self.handle or 0
+
+
+def stream_synchronize(stream):
+    _check(_load().tcamd_stream_synchronize(_vp(stream)), "hipStreamSynchronize")
+
+
+class Event:
+    def __init__(self):
+        e = ctypes.c_void_p()
+        _check(_load().tcamd_event_create(ctypes.byref(e)), "hipEventCreate")
+        self.handle = e.value
+
+    def record(self, stream=None):
+        _check(_load().tcamd_event_record(_vp(self.handle), _vp(stream)), "hipEventRecord")
+
+    def synchronize(self):
+        _check(_load().tcamd_event_synchronize(_vp(self.handle)), "hipEventSynchronize")
+
+    def elapsed_ms(self, end):
+        ms = ctypes.c_float(0)
+        _check(_load().tcamd_event_elapsed_ms(_vp(self.handle), _vp(end.handle), ctypes.byref(ms)), "hipEventElapsedTime")
+        return ms.value
+
+    def close(self):
+        if self.handle:
+            _load().tcamd_event_destroy(_vp(self.handle))
+            self.handle = None
+
+
+# ---------------------------------------------------------------------------
+# kernels
+# ---------------------------------------------------------------------------
+SYNTH_ZERO, SYNTH_CONST, SYNTH_UNIFORM, SYNTH_NORMAL = 0, 1, 2, 3
+
+
+def synth_fill(ptr, n_elems, datatype, mode=SYNTH_UNIFORM, lo=0.0, hi=1.0, seed=0, stream_id=0, stream=None):
+    """K1: fill ``n_elems`` of ``datatype`` at device ``ptr`` (16-B aligned).
+
+    uniform: floats in [lo, hi), integers in [lo, hi]; normal: mean lo, std hi.
+    Deterministic in (seed, stream_id, element offset).
+    """
+    _check(
+        _load().tcamd_synth_fill(
+            _vp(ptr), n_elems, dtypes.code(datatype), mode, float(lo), float(hi),
+            seed & (2**64 - 1), stream_id & (2**64 - 1), _vp(stream),
+        ),
+        "synth_fill",
+    )
+
+
+def convert(src, src_dtype, dst, dst_dtype, n, rounding="trunc", stream=None):
+    """K4/K5 elementwise conversion between FP32 and BF16/FP16/FP8."""
+    r = 0 if rounding == "trunc" else 1
+    _check(
+        _load().tcamd_convert(_vp(src), dtypes.code(src_dtype), _vp(dst), dtypes.code(dst_dtype), n, r, _vp(stream)),
+        "convert %s->%s" % (src_dtype, dst_dtype),
+    )
+
+
+LAYOUTS = {"NCHW": 0, "NHWC": 1}
+
+
+def layout_pack(srcs, src_dtype, src_layout, dst, dst_dtype, dst_layout, C, H, W,
+                scale=None, bias=None, rounding="rne", stream=None):
+    """K6: gather len(srcs) images (each C*H*W) into ``dst`` with layout/dtype
+    conversion and per-channel ``x*scale[c]+bias[c]``."""
+    n = len(srcs)
+    arr = (ctypes.c_void_p * max(n, 1))(*[int(p) for p in srcs])
+    sc = (ctypes.c_float * C)(*scale) if scale is not None else None
+    bi = (ctypes.c_float * C)(*bias) if bias is not None else None
+    _check(
+        _load().tcamd_layout_pack(
+            arr, n, dtypes.code(src_dtype), LAYOUTS[src_layout], _vp(dst), dtypes.code(dst_dtype),
+            LAYOUTS[dst_layout], C, H, W, sc, bi, 0 if rounding == "trunc" else 1, _vp(stream),
+        ),
+        "layout_pack",
+    )
+
+
+def batched_copy(srcs, dsts, sizes, stream=None):
+    """K7: copy sizes[i] bytes srcs[i] -> dsts[i] for all i in one launch."""
+    n = len(srcs)
+    if n == 0:
+        return
+    s = (ctypes.c_void_p * n)(*[int(p) for p in srcs])
+    d = (ctypes.c_void_p * n)(*[int(p) for p in dsts])
+    b = (ctypes.c_uint64 * n)(*[int(x) for x in sizes])
+    _check(_load().tcamd_batched_copy(s, d, b, n, _vp(stream)), "batched_copy")
+
+
+def pack_bytes_workspace(n):
+    return int(_load().tcamd_pack_bytes_workspace(n))
+
+
+def pack_bytes(data_ptr, lens_ptr, n, out_ptr, workspace_ptr, stream=None):
+    """K2: device BYTES serialisation (see csrc/kernels/bytes.hip)."""
+    _check(
+        _load().tcamd_pack_bytes(_vp(data_ptr), _vp(lens_ptr), n, _vp(out_ptr), _vp(workspace_ptr), _vp(stream)),
+        "pack_bytes",
+    )
+
+
+def index_bytes(buf_ptr, nbytes, n_expected, offs_ptr, lens_ptr, status_ptr, stream=None):
+    """K3: device BYTES index (offsets/lengths of each element)."""
+    _check(
+        _load().tcamd_index_bytes(
+            _vp(buf_ptr), nbytes, n_expected, _vp(offs_ptr), _vp(lens_ptr), _vp(status_ptr), _vp(stream)
+        ),
+        "index_bytes",
+    )
+
+
+def available():
+    """True if the library loads and at least one GPU is visible."""
+    try:
+        _load()
+    except Exception:
+        return False
+    return device_count() > 0
+
+
+# eager load so a missing .so fails at import time (loudly) on GPU boxes
+if os.environ.get("TCAMD_LAZY_HIP", "0") != "1":
+    try:
+        _load()
+    except OSError as e:  # pragma: no cover
+        print("warning: libtcamd_hip.so failed to load: %s" % e, file=sys.stderr)
+        raise

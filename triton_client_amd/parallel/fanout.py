@@ -1,0 +1,143 @@
+"""Multi-GPU fan-out of the shared synthetic input batch.
+
+One process per GPU (torch.distributed, backend "nccl" == RCCL on ROCm).
+Rank 0 generates the synthetic batch once on its GPU (K1 synth_fill) and the
+batch is replicated into every rank's HIP shared-memory input region:
+
+* ``rccl``  — X1: ``dist.broadcast`` straight into the region (the region is
+  exposed to torch through a zero-copy kDLROCM DLPack view).
+* ``p2p``   — X2: a one-hop star over xGMI: ranks all-gather their regions'
+  IPC handles, rank 0 opens them and issues one hipMemcpyAsync per peer on
+  its own stream (each copy uses the direct rank0->peer link; no ring hops).
+  Ranks then barrier.
+* ``local`` — every rank generates the identical data itself (K1 is a pure
+  function of (seed, offset)), used when no process group exists.
+
+For a few-MB batch the broadcast is latency-bound (densenet bs=8: 4.8 MB is
+~31 us at ~153 GB/s per link), so the star pays one hop where a ring pays 7.
+"""
+
+import numpy as np
+
+
+def _dist():
+    import torch.distributed as dist
+
+    return dist if dist.is_available() and dist.is_initialized() else None
+
+
+def region_tensor(region, nbytes):
+    """torch uint8 tensor aliasing the first ``nbytes`` of a HIP shm region."""
+    import torch
+
+    from tritonclient.utils import hip_shared_memory as hipshm
+
+    view = hipshm.as_shared_memory_tensor(region, "UINT8", [nbytes])
+    return torch.from_dlpack(view)
+
+
+def fill_and_fanout(region, datatype, n_elems, seed=0, mode="random", lo=0.0, hi=1.0, method="rccl"):
+    """Fill ``region`` on rank 0 and replicate to every rank. Returns method used."""
+    from tritonclient.utils import hip_shared_memory as hipshm
+    from triton_client_amd.ops import dtypes
+
+    dist = _dist()
+    nbytes = n_elems * dtypes.SIZES[datatype]
+    if dist is None or dist.get_world_size() == 1:
+        hipshm.fill_synthetic_data(region, datatype, n_elems, mode, lo, hi, seed)
+        return "local"
+    rank = dist.get_rank()
+    if method == "local":
+        hipshm.fill_synthetic_data(region, datatype, n_elems, mode, lo, hi, seed)
+        dist.barrier()
+        return "local"
+    if rank == 0:
+        hipshm.fill_synthetic_data(region, datatype, n_elems, mode, lo, hi, seed)
+    if method == "rccl":
+        import torch
+
+        t = region_tensor(region, nbytes)
+        dist.broadcast(t, src=0)
+        torch.cuda.synchronize()
+        return "rccl"
+    if method == "p2p":
+        return _p2p_star(region, nbytes, dist)
+    raise ValueError("unknown fan-out method %s" % method)
+
+
+def _p2p_star(region, nbytes, dist):
+    from tritonclient.utils import hip_shared_memory as hipshm  # noqa: F401
+    from triton_client_amd.ops import hip
+
+    rank = dist.get_rank()
+    world = dist.get_world_size()
+    handles = [None] * world
+    dist.all_gather_object(handles, (region._device_id, region._hip_shm_handle))
+    if rank == 0:
+        src_dev = region._device_id
+        streams = []
+        opened = []
+        try:
+            for peer in range(1, world):
+                dev, h = handles[peer]
+                try:
+                    hip.enable_peer(src_dev, dev)
+                except Exception:
+                    pass  # copies still work through the runtime's staging path
+                ptr = hip.ipc_open(h, src_dev)
+                opened.append(ptr)
+                s = hip.Stream(src_dev)
+                streams.append(s)
+                hip.memcpy_async(ptr, region._base_addr, nbytes, s.handle)
+            for s in streams:
+                s.synchronize()
+        finally:
+            for s in streams:
+                s.close()
+            for p in opened:
+                hip.ipc_close(p, src_dev)
+    dist.barrier()
+    return "p2p"
+
+
+def verify_replicas(region, nbytes, sample=4096):
+    """Every rank checks a strided sample of its region against rank 0's."""
+    import torch
+
+    dist = _dist()
+    t = region_tensor(region, nbytes)
+    idx = torch.linspace(0, nbytes - 1, min(sample, nbytes), device=t.device).long()
+    s = t[idx].to(torch.int64)
+    if dist is None:
+        return True
+    ref = s.clone()
+    dist.broadcast(ref, src=0)
+    ok = torch.equal(s, ref)
+    flag = torch.tensor([1 if ok else 0], device=t.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item())
+
+
+def max_over_ranks(value):
+    """MAX of a python float across ranks (identity without a process group)."""
+    dist = _dist()
+    if dist is None:
+        return value
+    import torch
+
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+    if dist.get_backend() == "gloo":
+        dev = "cpu"
+    t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_arrays(arr):
+    """Concatenate a 1-D numpy int64 array from all ranks (on every rank)."""
+    dist = _dist()
+    if dist is None:
+        return arr
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, np.asarray(arr))
+    return np.concatenate(out) if out else arr

@@ -1,0 +1,87 @@
+"""Bench-server lifecycle helpers shared by bench.py, perf tools and GPU tests."""
+
+import os
+import socket
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class ServerProcess:
+    """The KServe-v2 server in a child process (HIP IPC needs a 2nd process)."""
+
+    def __init__(self, device=0, gpu=True, models="", http_port=None, grpc_port=None,
+                 extra_args=(), log_path=None, env=None):
+        self.http_port = http_port or free_port()
+        self.grpc_port = grpc_port or free_port()
+        self.device = device
+        args = [sys.executable, "-m", "triton_client_amd.server",
+                "--http-port", str(self.http_port), "--grpc-port", str(self.grpc_port),
+                "--device", str(device)]
+        if gpu:
+            args.append("--gpu")
+        if models:
+            args += ["--models", models]
+        args += list(extra_args)
+        e = dict(os.environ)
+        e["PYTHONPATH"] = REPO + os.pathsep + e.get("PYTHONPATH", "")
+        if env:
+            e.update(env)
+        self.log_path = log_path
+        self._log = open(log_path, "w") if log_path else subprocess.DEVNULL
+        self.proc = subprocess.Popen(args, cwd=REPO, env=e, stdout=self._log, stderr=subprocess.STDOUT,
+                                     start_new_session=True)
+
+    @property
+    def grpc_url(self):
+        return "127.0.0.1:%d" % self.grpc_port
+
+    @property
+    def http_url(self):
+        return "127.0.0.1:%d" % self.http_port
+
+    def wait_ready(self, timeout=600, model=None):
+        import tritonclient.http as httpclient
+
+        t0 = time.time()
+        last = None
+        while time.time() - t0 < timeout:
+            if self.proc.poll() is not None:
+                raise RuntimeError("server exited with %s (log: %s)" % (self.proc.returncode, self.log_path))
+            try:
+                c = httpclient.InferenceServerClient(self.http_url, connection_timeout=2, network_timeout=5)
+                ok = c.is_server_ready() and (model is None or c.is_model_ready(model))
+                c.close()
+                if ok:
+                    return self
+            except Exception as e:  # noqa: BLE001
+                last = e
+            time.sleep(0.5)
+        raise TimeoutError("server not ready after %ss: %s" % (timeout, last))
+
+    def stop(self):
+        if self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(30)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait(10)
+        if self._log not in (None, subprocess.DEVNULL):
+            self._log.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.stop()

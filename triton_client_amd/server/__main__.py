@@ -1,0 +1,72 @@
+"""``python -m triton_client_amd.server`` — run the KServe-v2 test/bench server.
+
+Example::
+
+    python -m triton_client_amd.server --http-port 8000 --grpc-port 8001 --gpu --device 0
+"""
+import argparse
+import asyncio
+import os
+import signal
+import sys
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--http-port", type=int, default=8000, help="0 disables HTTP")
+    ap.add_argument("--grpc-port", type=int, default=8001, help="0 disables gRPC")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--gpu", action="store_true", help="also load the GPU model zoo")
+    ap.add_argument("--device", type=int, default=0, help="GPU for the GPU models")
+    ap.add_argument("--models", default="", help="comma-separated subset of models to load")
+    ap.add_argument("--instance-count", type=int, default=0, help="override GPU model instance count")
+    ap.add_argument("--max-queue-delay-us", type=int, default=-1)
+    ap.add_argument("--no-graphs", action="store_true", help="disable HIP graph capture")
+    ap.add_argument("--ready-file", default="", help="touch this file once serving")
+    args = ap.parse_args(argv)
+
+    from .app import default_models, serve
+    from .core import InferenceServer
+
+    models = default_models(gpu=args.gpu)
+    if args.models:
+        keep = set(args.models.split(","))
+        models = [m for m in models if m.name in keep]
+    opts = {}
+    for m in models:
+        if getattr(m, "instance_kind", "") == "KIND_GPU":
+            o = {"device": args.device}
+            if args.no_graphs:
+                o["use_graphs"] = False
+            opts[m.name] = o
+            if args.instance_count:
+                m.instance_count = args.instance_count
+            if args.max_queue_delay_us >= 0 and m.dynamic_batching is not None:
+                m.dynamic_batching = dict(m.dynamic_batching, max_queue_delay_us=args.max_queue_delay_us)
+    server = InferenceServer(models, opts, device_id=args.device)
+    server.load_all()
+
+    async def run():
+        stop = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        for sig in (signal.SIGINT, signal.SIGTERM):
+            loop.add_signal_handler(sig, stop.set)
+        ready = asyncio.Event()
+        task = asyncio.ensure_future(
+            serve(server, args.http_port or None, args.grpc_port or None, args.host, ready, stop)
+        )
+        await ready.wait()
+        print("SERVER READY http=%s grpc=%s" % (args.http_port, args.grpc_port), flush=True)
+        if args.ready_file:
+            with open(args.ready_file, "w") as f:
+                f.write(str(os.getpid()))
+        await task
+
+    asyncio.run(run())
+    server.sys_shm.unregister()
+    server.dev_shm.unregister()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -377,6 +377,7 @@ class InferenceServer:
                 opts = {k: val for k, val in entry.options.items() if k not in ("name", "versions", "base_cls")}
                 try:
                     inst = entry.cls(version=v, **opts)
+                    inst._server = self  # lets GPU backends resolve shm targets directly
                     inst.load()
                 except Exception as e:
                     entry.state = "UNAVAILABLE"

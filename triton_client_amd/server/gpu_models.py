@@ -1,0 +1,233 @@
+"""GPU model backends of the bench server (torch-ROCm + in-tree HIP kernels).
+
+``densenet_onnx`` — the BASELINE model (FP32 ``data_0`` [3,224,224] NCHW in,
+FP32 ``fc6_1`` [1000] out; same I/O contract as Triton's densenet_onnx example)
+served with dynamic batching on one MI355X:
+
+  request inputs (device shm views / host tensors)
+    --K6 layout_pack--> one bf16 NHWC batch buffer   (gather+transpose+cvt,
+                                                      one launch per batch)
+    --HIP graph replay--> DenseNet-121 (bf16, channels_last, MIOpen MFMA convs)
+    --K7 batched_copy--> each request's fp32 logits straight into its output
+                         device-shm region (one launch per batch)
+
+Host (non-shm) inputs are staged through pinned memory; host outputs come back
+with one D2H of the whole batch.  Each model instance owns a torch stream, its
+graphs (one per batch bucket) and static buffers, so ``instance_count``
+batches pipeline on separate HIP streams.
+"""
+
+import threading
+
+import numpy as np
+
+from .model_base import Model, TensorSpec
+from .types import DeviceView, OutputTensor, ServerError
+
+BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128)
+
+
+class DensenetOnnx(Model):
+    name = "densenet_onnx"
+    platform = "onnxruntime_onnx"
+    backend = "onnxruntime"
+    max_batch_size = 128
+    inputs = (TensorSpec("data_0", "FP32", [3, 224, 224], fmt="NCHW"),)
+    outputs = (TensorSpec("fc6_1", "FP32", [1000], label_filename="densenet_labels.txt"),)
+    dynamic_batching = {"preferred": [], "max_queue_delay_us": 500}
+    instance_kind = "KIND_GPU"
+    instance_count = 2
+    gpus = (0,)
+    labels = ["class_%d" % i for i in range(1000)]
+
+    C, H, W = 3, 224, 224
+    OUT = 1000
+
+    def __init__(self, version=1, device_id=0, buckets=BUCKETS, use_graphs=True, **kw):
+        super().__init__(version, **kw)
+        self.device_id = int(kw.get("device", device_id))
+        self.buckets = tuple(b for b in buckets if b <= self.max_batch_size)
+        self.use_graphs = use_graphs
+        self._slots = []
+        self._free = []
+        self._cv = threading.Condition()
+
+    # -- load ----------------------------------------------------------------------
+    def load(self):
+        import torch
+
+        from triton_client_amd.models import densenet
+        from triton_client_amd.ops import hip
+
+        if not torch.cuda.is_available():
+            raise ServerError("densenet_onnx requires a GPU")
+        hip.lib()  # fail loudly if the native kernels are missing
+        torch.cuda.set_device(self.device_id)
+        self.torch = torch
+        dev = torch.device("cuda", self.device_id)
+        model = densenet.build(device=dev)
+        self.model = model
+        self.scale = None
+        for _ in range(max(1, self.instance_count)):
+            self._slots.append(self._make_slot(dev))
+        self._free = list(range(len(self._slots)))
+
+    def _make_slot(self, dev):
+        torch = self.torch
+        from triton_client_amd.ops import hip
+
+        slot = {"stream": torch.cuda.Stream(device=dev), "graphs": {}}
+        maxb = max(self.buckets)
+        slot["inp"] = torch.zeros(maxb, self.H, self.W, self.C, device=dev, dtype=torch.bfloat16)
+        slot["out"] = torch.zeros(maxb, self.OUT, device=dev, dtype=torch.float32)
+        slot["stage_host"] = hip.host_alloc(maxb * self.C * self.H * self.W * 4)
+        slot["stage_dev"] = torch.empty(maxb * self.C * self.H * self.W, device=dev, dtype=torch.float32)
+        slot["out_host"] = hip.host_alloc(maxb * self.OUT * 4)
+        with torch.cuda.stream(slot["stream"]), torch.no_grad():
+            for b in self.buckets:
+                x = slot["inp"][:b].permute(0, 3, 1, 2)  # NCHW view of NHWC memory
+                for _ in range(2):  # warm up MIOpen kernel selection
+                    slot["out"][:b].copy_(self.model(x).float())
+                if self.use_graphs:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=slot["stream"]):
+                        y = self.model(x)
+                        slot["out"][:b].copy_(y.float())
+                    slot["graphs"][b] = g
+        slot["stream"].synchronize()
+        return slot
+
+    def unload(self):
+        from triton_client_amd.ops import hip
+
+        for s in self._slots:
+            try:
+                hip.host_free(s["stage_host"])
+                hip.host_free(s["out_host"])
+            except Exception:
+                pass
+        self._slots = []
+
+    # -- execute ----------------------------------------------------------------------
+    def _acquire(self):
+        with self._cv:
+            while not self._free:
+                self._cv.wait()
+            return self._free.pop()
+
+    def _release(self, i):
+        with self._cv:
+            self._free.append(i)
+            self._cv.notify()
+
+    def forward_device(self, slot, srcs, rows):
+        """Assemble ``rows`` images from device pointers and run the model."""
+        torch = self.torch
+        from triton_client_amd.ops import hip
+
+        bucket = next(b for b in self.buckets if b >= rows)
+        stream = slot["stream"]
+        sh = stream.cuda_stream
+        hip.layout_pack(srcs, "FP32", "NCHW", slot["inp"].data_ptr(), "BF16", "NHWC",
+                        self.C, self.H, self.W, rounding="rne", stream=sh)
+        if self.use_graphs:
+            with torch.cuda.stream(stream):
+                slot["graphs"][bucket].replay()
+        else:
+            with torch.cuda.stream(stream), torch.no_grad():
+                x = slot["inp"][:bucket].permute(0, 3, 1, 2)
+                slot["out"][:bucket].copy_(self.model(x).float())
+        return bucket
+
+    def execute(self, requests):
+        torch = self.torch
+        from triton_client_amd.ops import hip
+
+        img_bytes = self.C * self.H * self.W * 4
+        out_row = self.OUT * 4
+        rows = 0
+        plan = []  # (request, first_row, nrows)
+        for r in requests:
+            t = r.input("data_0")
+            n = int(t.shape[0])
+            plan.append((r, rows, n))
+            rows += n
+        if rows > max(self.buckets):
+            return [ServerError("batch of %d rows exceeds the largest bucket" % rows)] * len(requests)
+        i = self._acquire()
+        slot = self._slots[i]
+        try:
+            stream = slot["stream"]
+            sh = stream.cuda_stream
+            srcs = []
+            host_rows = 0
+            for r, first, n in plan:
+                t = r.input("data_0")
+                if isinstance(t.data, DeviceView):
+                    if t.data.nbytes < n * img_bytes:
+                        raise ServerError("input region too small for data_0")
+                    srcs += [t.data.ptr + k * img_bytes for k in range(n)]
+                else:
+                    a = np.ascontiguousarray(t.data, dtype=np.float32)
+                    dst = slot["stage_host"] + host_rows * img_bytes
+                    np.copyto(np.ctypeslib.as_array((np.ctypeslib.ctypes.c_float * a.size).from_address(dst)),
+                              a.reshape(-1))
+                    srcs += [slot["stage_dev"].data_ptr() + (host_rows + k) * img_bytes for k in range(n)]
+                    host_rows += n
+            if host_rows:
+                hip.memcpy_async(slot["stage_dev"].data_ptr(), slot["stage_host"], host_rows * img_bytes, sh)
+            self.forward_device(slot, srcs, rows)
+            # outputs: device-shm targets get a K7 scatter, the rest one D2H
+            out_base = slot["out"].data_ptr()
+            c_src, c_dst, c_n = [], [], []
+            need_host = False
+            results = []
+            for r, first, n in plan:
+                ro = next((o for o in r.outputs if o.name == "fc6_1"), None)
+                target = None
+                if ro is not None and ro.shm is not None and ro.class_count == 0:
+                    target = self._server_target(r, ro)
+                if isinstance(target, DeviceView):
+                    if target.nbytes < n * out_row:
+                        raise ServerError(
+                            "shared memory size specified with the request for output 'fc6_1' "
+                            "(%d bytes) should be at least %d bytes" % (target.nbytes, n * out_row)
+                        )
+                    c_src.append(out_base + first * out_row)
+                    c_dst.append(target.ptr)
+                    c_n.append(n * out_row)
+                    results.append(("shm", ro))
+                else:
+                    need_host = True
+                    results.append(("host", None))
+            if c_src:
+                hip.batched_copy(c_src, c_dst, c_n, sh)
+            if need_host:
+                hip.memcpy_async(slot["out_host"], out_base, rows * out_row, sh)
+            stream.synchronize()
+            host_all = None
+            if need_host:
+                host_all = np.ctypeslib.as_array(
+                    (np.ctypeslib.ctypes.c_float * (rows * self.OUT)).from_address(slot["out_host"])
+                ).reshape(rows, self.OUT).copy()
+            out = []
+            for (r, first, n), (kind, ro) in zip(plan, results):
+                if kind == "shm":
+                    o = OutputTensor("fc6_1", "FP32", [n, self.OUT], None, shm=ro.shm)
+                else:
+                    o = OutputTensor("fc6_1", "FP32", [n, self.OUT], host_all[first : first + n])
+                out.append([o])
+            return out
+        except ServerError as e:
+            return [e] * len(requests)
+        finally:
+            self._release(i)
+
+    _server = None
+
+    def _server_target(self, r, ro):
+        region, nbytes, offset = ro.shm
+        return self._server.shm_target(region, nbytes, offset)
+
+
+GPU_MODELS = [DensenetOnnx]

@@ -63,6 +63,8 @@ class InferResult:
                             arr[:] = list(values)
                         else:
                             arr = np.array(values, dtype=triton_to_np_dtype(datatype))
+                    elif "shared_memory_region" in output.parameters:
+                        return None  # delivered through shared memory
                     else:
                         arr = np.empty(0)
                 return arr.reshape(shape)

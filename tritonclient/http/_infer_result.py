@@ -108,8 +108,10 @@ class InferResult:
                         arr = deserialize_fp8_tensor(chunk, datatype)
                     else:
                         arr = np.frombuffer(chunk, dtype=triton_to_np_dtype(datatype))
-            else:
+            elif "data" in output:
                 arr = np.array(output["data"], dtype=triton_to_np_dtype(datatype))
+            else:
+                return None  # delivered through shared memory: no payload in the body
             return arr.reshape(output["shape"])
         return None
 
