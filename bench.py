@@ -49,6 +49,20 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
+    from triton_client_amd.perf.harness import ServerProcess
+
+    bs, conc = args.batch, args.concurrency
+    log_path = args.server_log or os.path.join(REPO, "gpurun_out", "bench_server_r%d.log" % rank)
+    os.makedirs(os.path.dirname(log_path), exist_ok=True)
+    # spawn the server before this process touches the GPU
+    srv = ServerProcess(
+        device=local_rank,
+        models="densenet_onnx",
+        extra_args=["--instance-count", str(args.instance_count),
+                    "--max-queue-delay-us", str(args.max_queue_delay_us)],
+        log_path=log_path,
+    )
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -60,19 +74,7 @@ def main():
     import tritonclient.grpc as grpcclient
     from tritonclient.utils import hip_shared_memory as hipshm
     from triton_client_amd.parallel import fanout
-    from triton_client_amd.perf.harness import ServerProcess
     from triton_client_amd.perf.loadgen import ConcurrencyRun, percentile_us
-
-    bs, conc = args.batch, args.concurrency
-    log_path = args.server_log or os.path.join(REPO, "gpurun_out", "bench_server_r%d.log" % rank)
-    os.makedirs(os.path.dirname(log_path), exist_ok=True)
-    srv = ServerProcess(
-        device=local_rank,
-        models="densenet_onnx",
-        extra_args=["--instance-count", str(args.instance_count),
-                    "--max-queue-delay-us", str(args.max_queue_delay_us)],
-        log_path=log_path,
-    )
     regions = []
     client = None
     try:
@@ -133,6 +135,12 @@ def main():
             ms = stats["model_stats"][0]
             execs = int(ms.get("execution_count", 0))
             infers = int(ms.get("inference_count", 0))
+            bst = ms.get("batch_stats", [])
+            nb = sum(int(b["compute_infer"].get("count", 0)) for b in bst) or 1
+            gpu_ms = {k: sum(int(b[k].get("ns", 0)) for b in bst) / nb / 1e6
+                      for k in ("compute_input", "compute_infer", "compute_output")}
+            log("server per-batch device ms: %s  avg rows %.1f" % (
+                {k: round(v, 3) for k, v in gpu_ms.items()}, infers / max(execs, 1)))
             res = {
                 "metric": "perf_analyzer inferences/sec (densenet_onnx, HIP shm)",
                 "value": round(value, 2),
@@ -161,6 +169,7 @@ def main():
                 "p99_latency_us": round(percentile_us(all_lat, 99), 1),
                 "requests_per_sec": round(value / bs, 2),
                 "server_avg_batch_rows_rank0": round(infers / max(execs, 1), 2),
+                "server_device_ms_per_batch_rank0": {k: round(v, 3) for k, v in gpu_ms.items()},
             }
             print(json.dumps(res), flush=True)
         return 0

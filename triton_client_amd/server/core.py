@@ -789,6 +789,10 @@ class DirectScheduler:
         self.stats = stats
         self.sem = threading.Semaphore(max(1, inst.instance_count))
         self.serial = threading.Lock() if inst.sequence_batching else None
+        # GPU backends time their phases with device events and report them
+        self.model_reports = bool(getattr(inst, "reports_batch_stats", False))
+        if self.model_reports:
+            inst._batch_stats = stats.record_batch
 
     def _run(self, requests, t_enq):
         t_start = _now_ns()
@@ -803,8 +807,9 @@ class DirectScheduler:
             self.sem.release()
             if self.serial is not None:
                 self.serial.release()
-        bs = sum(_batch_size(self.inst, r) for r in requests)
-        self.stats.record_batch(bs, len(requests), 0, t1 - t0, 0)
+        if not self.model_reports:
+            bs = sum(_batch_size(self.inst, r) for r in requests)
+            self.stats.record_batch(bs, len(requests), 0, t1 - t0, 0)
         return results, t_start - t_enq
 
     async def submit(self, request):

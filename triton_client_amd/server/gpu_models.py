@@ -76,7 +76,8 @@ class DensenetOnnx(Model):
         torch = self.torch
         from triton_client_amd.ops import hip
 
-        slot = {"stream": torch.cuda.Stream(device=dev), "graphs": {}}
+        slot = {"stream": torch.cuda.Stream(device=dev), "graphs": {},
+                "ev": [torch.cuda.Event(enable_timing=True) for _ in range(4)]}
         maxb = max(self.buckets)
         slot["inp"] = torch.zeros(maxb, self.H, self.W, self.C, device=dev, dtype=torch.bfloat16)
         slot["out"] = torch.zeros(maxb, self.OUT, device=dev, dtype=torch.float32)
@@ -128,8 +129,10 @@ class DensenetOnnx(Model):
         bucket = next(b for b in self.buckets if b >= rows)
         stream = slot["stream"]
         sh = stream.cuda_stream
+        slot["ev"][0].record(stream)
         hip.layout_pack(srcs, "FP32", "NCHW", slot["inp"].data_ptr(), "BF16", "NHWC",
                         self.C, self.H, self.W, rounding="rne", stream=sh)
+        slot["ev"][1].record(stream)
         if self.use_graphs:
             with torch.cuda.stream(stream):
                 slot["graphs"][bucket].replay()
@@ -137,6 +140,7 @@ class DensenetOnnx(Model):
             with torch.cuda.stream(stream), torch.no_grad():
                 x = slot["inp"][:bucket].permute(0, 3, 1, 2)
                 slot["out"][:bucket].copy_(self.model(x).float())
+        slot["ev"][2].record(stream)
         return bucket
 
     def execute(self, requests):
@@ -204,7 +208,13 @@ class DensenetOnnx(Model):
                 hip.batched_copy(c_src, c_dst, c_n, sh)
             if need_host:
                 hip.memcpy_async(slot["out_host"], out_base, rows * out_row, sh)
+            slot["ev"][3].record(stream)
             stream.synchronize()
+            if self._batch_stats is not None:
+                ev = slot["ev"]
+                ms_in, ms_inf, ms_out = (ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]),
+                                         ev[2].elapsed_time(ev[3]))
+                self._batch_stats(rows, len(requests), int(ms_in * 1e6), int(ms_inf * 1e6), int(ms_out * 1e6))
             host_all = None
             if need_host:
                 host_all = np.ctypeslib.as_array(
@@ -224,6 +234,9 @@ class DensenetOnnx(Model):
             self._release(i)
 
     _server = None
+    # set by the scheduler: (rows, n_requests, compute_input_ns, compute_infer_ns, compute_output_ns)
+    _batch_stats = None
+    reports_batch_stats = True
 
     def _server_target(self, r, ro):
         region, nbytes, offset = ro.shm

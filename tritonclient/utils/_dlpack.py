@@ -193,8 +193,11 @@ class ConsumedTensor:
 def consume(obj, stream=None):
     """Consume ``obj`` (``__dlpack__`` provider or raw capsule)."""
     if hasattr(obj, "__dlpack__"):
+        dev = get_dlpack_device(obj)
+        on_device = dev is not None and dev[0] in (kDLROCM, kDLCUDA)
         try:
-            capsule = obj.__dlpack__(stream=stream) if stream is not None else obj.__dlpack__()
+            # producers reject a stream argument for host tensors
+            capsule = obj.__dlpack__(stream=stream) if (stream is not None and on_device) else obj.__dlpack__()
         except TypeError:
             capsule = obj.__dlpack__()
     else:
