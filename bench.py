@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--instance-count", type=int, default=2)
     ap.add_argument("--max-queue-delay-us", type=int, default=500)
     ap.add_argument("--server-log", default="")
+    ap.add_argument("--server-url", default="", help="use an already running server (gRPC host:port, HTTP port = +1 unless --http-url)")
+    ap.add_argument("--http-url", default="")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -49,19 +51,22 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
-    from triton_client_amd.perf.harness import ServerProcess
+    from triton_client_amd.perf.harness import ExternalServer, ServerProcess
 
     bs, conc = args.batch, args.concurrency
     log_path = args.server_log or os.path.join(REPO, "gpurun_out", "bench_server_r%d.log" % rank)
     os.makedirs(os.path.dirname(log_path), exist_ok=True)
     # spawn the server before this process touches the GPU
-    srv = ServerProcess(
-        device=local_rank,
-        models="densenet_onnx",
-        extra_args=["--instance-count", str(args.instance_count),
-                    "--max-queue-delay-us", str(args.max_queue_delay_us)],
-        log_path=log_path,
-    )
+    if args.server_url:
+        srv = ExternalServer(args.server_url, args.http_url)
+    else:
+        srv = ServerProcess(
+            device=local_rank,
+            models="densenet_onnx",
+            extra_args=["--instance-count", str(args.instance_count),
+                        "--max-queue-delay-us", str(args.max_queue_delay_us)],
+            log_path=log_path,
+        )
 
     import numpy as np
     import torch

@@ -192,7 +192,12 @@ __global__ void __launch_bounds__(kBlock) tiled_transpose(LayoutParams p, void* 
 template <int SRC, int DST>
 int dispatch_dst(const LayoutParams& p, int src_layout, int dst_layout, void* dst, hipStream_t s) {
   const int C = p.C, HW = p.HW;
-  const bool small = C <= 4 && (HW % 4) == 0;
+  // the register path does 4-element vector accesses: every source and the
+  // destination must be aligned to 4 elements of their dtype
+  bool aligned = (((uintptr_t)dst) % (4 * sizeof(uint32_t) / (DST == kFP32 ? 1 : 2))) == 0;
+  for (int i = 0; i < p.n_imgs; ++i)
+    aligned = aligned && (((uintptr_t)p.src[i]) % (4 * (SRC == kFP32 ? 4 : SRC == kUInt8 ? 1 : 2))) == 0;
+  const bool small = C <= 4 && (HW % 4) == 0 && aligned;
   const uint64_t quads = (uint64_t)(HW / 4) * p.n_imgs;
   if (src_layout == 0 && dst_layout == 1) {  // NCHW -> NHWC
     if (small) {
@@ -254,10 +259,7 @@ extern "C" int tcamd_layout_pack(const void* const* srcs, int n_imgs, int src_dt
   for (int base = 0; base < n_imgs; base += kMaxImgs) {
     LayoutParams p;
     int cnt = n_imgs - base < kMaxImgs ? n_imgs - base : kMaxImgs;
-    for (int i = 0; i < cnt; ++i) {
-      p.src[i] = srcs[base + i];
-      if (((uintptr_t)p.src[i]) & 15) return hipErrorInvalidValue;
-    }
+    for (int i = 0; i < cnt; ++i) p.src[i] = srcs[base + i];
     p.n_imgs = cnt;
     p.C = C;
     p.HW = H * W;

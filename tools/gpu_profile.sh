@@ -1,9 +1,24 @@
 #!/bin/bash
-# Profile the flagship bench on the GPU box: per-kernel stats for the server
-# (child process inherits the rocprofv3 preload).  Usage: tools/gpu_profile.sh [bench args]
+# Profile the bench SERVER (where the model kernels run) with rocprofv3:
+# the server runs under the profiler, bench.py drives it from outside, then the
+# server is stopped with SIGTERM so the profiler flushes its CSVs.
+# Usage: tools/gpu_profile.sh [bench args]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- \
-  python3 bench.py "$@" > gpurun_out/prof_bench.log 2>&1
+rm -f gpurun_out/prof/*.csv
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o server -- \
+  python3 -m triton_client_amd.server --http-port 18000 --grpc-port 18001 --gpu --models densenet_onnx \
+  --instance-count 2 > gpurun_out/prof_server.log 2>&1 &
+PROF_PID=$!
+timeout -k 10 600 python3 bench.py --server-url 127.0.0.1:18001 --http-url 127.0.0.1:18000 "$@" \
+  > gpurun_out/prof_bench.log 2>&1
+RC=$?
+# stop the python server (child of rocprofv3) gracefully
+# rocprofv3 may exec the program itself (then PROF_PID is the server)
+SRV_PID=$(pgrep -P $PROF_PID -n python3 || true)
+kill -TERM "${SRV_PID:-$PROF_PID}"
+wait $PROF_PID
+echo "bench rc=$RC profiler rc=$?"
+exit $RC

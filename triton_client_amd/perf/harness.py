@@ -85,3 +85,36 @@ class ServerProcess:
 
     def __exit__(self, *a):
         self.stop()
+
+
+class ExternalServer:
+    """A server started elsewhere (e.g. under rocprofv3); same interface."""
+
+    def __init__(self, grpc_url, http_url=""):
+        self.grpc_url = grpc_url
+        if not http_url:
+            host, port = grpc_url.rsplit(":", 1)
+            http_url = "%s:%d" % (host, int(port) - 1)
+        self.http_url = http_url
+        self.log_path = None
+        self.proc = None
+
+    def wait_ready(self, timeout=600, model=None):
+        import tritonclient.http as httpclient
+
+        t0 = time.time()
+        last = None
+        while time.time() - t0 < timeout:
+            try:
+                c = httpclient.InferenceServerClient(self.http_url, connection_timeout=2, network_timeout=5)
+                ok = c.is_server_ready() and (model is None or c.is_model_ready(model))
+                c.close()
+                if ok:
+                    return self
+            except Exception as e:  # noqa: BLE001
+                last = e
+            time.sleep(0.5)
+        raise TimeoutError("external server not ready after %ss: %s" % (timeout, last))
+
+    def stop(self):
+        pass
