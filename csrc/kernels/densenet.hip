@@ -1,0 +1,515 @@
+// K8/K9/K10 — fused DenseNet-121 inference kernels for CDNA4 (gfx950).
+//
+// The reference serves `densenet_onnx` through onnxruntime in the server
+// (reference src/python/examples/image_client.py:86-152 and
+// src/c++/perf_analyzer docs name it as the headline model); here the model
+// runs on hand-written MFMA kernels whose layout is chosen for the hardware
+// instead of per-op library calls:
+//
+//  * every dense block owns ONE NHWC bf16 feature buffer [pixels][C_block];
+//    each layer's 3x3 conv writes its 32 new channels straight into its slice
+//    (no torch.cat: the concat is free), and the next layer's 1x1 conv reads
+//    the first K channels of the same rows;
+//  * K8 conv1x1: Y = epi( relu(X*s+b) @ W^T ) — the pre-activation BN+ReLU
+//    of DenseNet (different per consumer layer, so it cannot be folded into
+//    a producer) is applied while staging the X tile global->LDS, the
+//    following BN (norm2) is folded into W/bias and applied with ReLU in the
+//    epilogue.  POOL=true is the transition layer: BN+ReLU+2x2 avg-pool in
+//    the prologue, 4x fewer GEMM rows;
+//  * K9 conv3x3 (128->32, pad 1): implicit GEMM, the whole 73 KB weight
+//    tensor resident in LDS for a persistent block, activations fetched
+//    with bounds-checked buffer loads (out-of-image taps read as 0);
+//  * K10 stem epilogue (bias+ReLU+3x3/2 max-pool) and head (BN+ReLU+global
+//    avg-pool).
+//
+// MFMA: v_mfma_f32_16x16x32_bf16 with the WEIGHT tile as operand A (rows =
+// output channels) and the activation tile as operand B (cols = pixels), so
+// each lane's 4 accumulators are 4 consecutive output channels of one pixel
+// and the epilogue stores 8 contiguous bytes per lane with no LDS transpose.
+
+#include "kernels/common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
+constexpr int kLdsK = 40;        // 32-wide K tile + 8 pad: 80-B rows, conflict-free b128 reads
+constexpr int kMaxK = 1024;      // prologue scale/bias table
+constexpr int kC3 = 128;         // 3x3 conv input channels (bn_size * growth)
+constexpr int kN3 = 32;          // 3x3 conv output channels (growth)
+constexpr int kK3 = 9 * kC3;     // 1152
+constexpr int kWsK = kK3 + 8;    // LDS row stride of the resident 3x3 weights
+
+__device__ __forceinline__ v4u ldg16(const uint16_t* p) { return *reinterpret_cast<const v4u*>(p); }
+
+__device__ __forceinline__ void unpack8(v4u v, float* f) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f[2 * q] = __uint_as_float(v[q] << 16);
+    f[2 * q + 1] = __uint_as_float(v[q] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)tcamd::f32_to_bf16_rne(a) | ((uint32_t)tcamd::f32_to_bf16_rne(b) << 16);
+}
+
+__device__ __forceinline__ v4u pack8(const float* f) {
+  v4u v;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = pack2(f[2 * q], f[2 * q + 1]);
+  return v;
+}
+
+__device__ __forceinline__ bf16x8 as_frag(v4u v) { return __builtin_bit_cast(bf16x8, v); }
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ============================================================================
+// K8: 1x1 conv as GEMM with fused pre-activation (and optional 2x2 avg-pool)
+// ============================================================================
+struct Conv1x1Params {
+  const uint16_t* x;        // [rows][ldx] bf16 (rows = M, or the pre-pool pixels)
+  const float* in_scale;    // [K] prologue BN scale (PRO)
+  const float* in_bias;     // [K]
+  const uint16_t* w;        // [N][K] bf16
+  const float* out_bias;    // [N] or null
+  uint16_t* y;              // [M][ldy] bf16, already offset to the first output channel
+  int ldx, M, K, N, ldy;
+  int relu_out;
+  int H, W;                 // POOL: pre-pool spatial dims (M = imgs * H/2 * W/2)
+};
+
+// Block = 4 waves as 2 (pixels) x 2 (channels); block tile (32*TM) x 128,
+// wave tile (16*TM pixels) x 64 channels, BK = 32, LDS double-buffered with
+// register prefetch (global loads of tile k+1 are in flight during MFMAs on k).
+template <int TM, bool PRO, bool POOL>
+__global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
+  constexpr int BM = 32 * TM, BN = 128;
+  constexpr int A_CHUNKS = BM * 4, AI = (A_CHUNKS + 255) / 256;
+  constexpr int NS = POOL ? 4 : 1;
+  __shared__ __attribute__((aligned(16))) uint16_t sA[2][BM * kLdsK];
+  __shared__ __attribute__((aligned(16))) uint16_t sB[2][BN * kLdsK];
+  __shared__ float sS[PRO ? kMaxK : 1], sT[PRO ? kMaxK : 1];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  if constexpr (PRO) {
+    for (int k = tid; k < p.K; k += 256) {
+      sS[k] = p.in_scale[k];
+      sT[k] = p.in_bias[k];
+    }
+  }
+
+  // per-thread A chunk sources (row pointers; POOL: the 2x2 window's 4 rows)
+  const uint16_t* a_src[AI][NS];
+  bool a_ok[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int c = tid + i * 256;
+    const int m = m0 + (c >> 2);
+    a_ok[i] = (c < A_CHUNKS) && (m < p.M);
+    const int mm = a_ok[i] ? m : 0;
+    const int kc = (c & 3) * 8;
+    if constexpr (POOL) {
+      const int wo = p.W >> 1, ho = p.H >> 1;
+      const int img = mm / (ho * wo), r = mm - img * ho * wo;
+      const int oh = r / wo, ow = r - oh * wo;
+      const size_t base = ((size_t)img * p.H + 2 * oh) * p.W + 2 * ow;
+      a_src[i][0] = p.x + base * p.ldx + kc;
+      a_src[i][1] = p.x + (base + 1) * p.ldx + kc;
+      a_src[i][2] = p.x + (base + p.W) * p.ldx + kc;
+      a_src[i][3] = p.x + (base + p.W + 1) * p.ldx + kc;
+    } else {
+      a_src[i][0] = p.x + (size_t)mm * p.ldx + kc;
+    }
+  }
+  const uint16_t* b_src[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + i * 256;
+    b_src[i] = p.w + (size_t)(n0 + (c >> 2)) * p.K + (c & 3) * 8;
+  }
+
+  v4u ra[AI][NS], rb[2];
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * 32;
+#pragma unroll
+    for (int i = 0; i < AI; ++i)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) ra[i][s] = ldg16(a_src[i][s] + k0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) rb[i] = ldg16(b_src[i] + k0);
+  };
+  auto store_tile = [&](int kt, int buf) {
+    const int k0 = kt * 32;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int c = tid + i * 256;
+      if (c < A_CHUNKS) {
+        const int kc = (c & 3) * 8;
+        v4u v;
+        if constexpr (PRO) {
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = 0.f;
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            float f[8];
+            unpack8(ra[i][s], f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float t = fmaxf(f[e] * sS[k0 + kc + e] + sT[k0 + kc + e], 0.f);
+              o[e] += POOL ? 0.25f * t : t;
+            }
+          }
+          v = pack8(o);
+        } else {
+          v = ra[i][0];
+        }
+        if (!a_ok[i]) v = v4u{0, 0, 0, 0};
+        *reinterpret_cast<v4u*>(&sA[buf][(c >> 2) * kLdsK + kc]) = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + i * 256;
+      *reinterpret_cast<v4u*>(&sB[buf][(c >> 2) * kLdsK + (c & 3) * 8]) = rb[i];
+    }
+  };
+
+  f32x4 acc[4][TM];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = p.K / 32;
+  load_tile(0);
+  __syncthreads();  // prologue tables
+  store_tile(0, 0);
+  __syncthreads();
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < KT) load_tile(kt + 1);
+    bf16x8 fa[4], fb[TM];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      fa[j] = *reinterpret_cast<const bf16x8*>(&sB[buf][(wn * 64 + j * 16 + fr) * kLdsK + fk]);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+      fb[i] = *reinterpret_cast<const bf16x8*>(&sA[buf][(wm * 16 * TM + i * 16 + fr) * kLdsK + fk]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = mfma16(fa[j], fb[i], acc[j][i]);
+    if (kt + 1 < KT) store_tile(kt + 1, buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds out channels nb..nb+3 of pixel m
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int nb = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.out_bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias[r] = p.out_bias[nb + r];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm * 16 * TM + i * 16 + fr;
+      if (m < p.M) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[j][i][r] + bias[r];
+          if (p.relu_out) v[r] = fmaxf(v[r], 0.f);
+        }
+        *reinterpret_cast<v2u*>(p.y + (size_t)m * p.ldy + nb) = v2u{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      }
+    }
+  }
+}
+
+// ============================================================================
+// K9: 3x3 conv, 128 -> 32 channels, stride 1, pad 1 (implicit GEMM)
+// ============================================================================
+struct Conv3x3Params {
+  const uint16_t* z;   // [M][128] bf16 NHWC (contiguous rows)
+  const uint16_t* w;   // [32][3][3][128] bf16
+  uint16_t* y;         // [M][ldy], already offset to the first output channel
+  int M, H, W, ldy;
+  int tiles;           // ceil(M / (64*TM))
+};
+
+// Persistent blocks: weights loaded to LDS once, then the block walks pixel
+// tiles of 4 waves x 16*TM pixels.  Each tap's 16 B activation fragments are
+// prefetched one tap ahead (register double-buffer across the unrolled taps).
+template <int TM>
+__global__ void __launch_bounds__(256) conv3x3_kernel(Conv3x3Params p) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t Ws[];  // [32][kWsK]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int c = tid; c < kN3 * (kK3 / 8); c += 256) {
+    const int n = c / (kK3 / 8), kc = (c - n * (kK3 / 8)) * 8;
+    *reinterpret_cast<v4u*>(&Ws[n * kWsK + kc]) = ldg16(p.w + (size_t)n * kK3 + kc);
+  }
+  __syncthreads();
+
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.z, (short)0,
+                                                      (int)((size_t)p.M * kC3 * 2), 0x00020000);
+  const int HW = p.H * p.W;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  for (int tile = blockIdx.x; tile < p.tiles; tile += gridDim.x) {
+    const int mb = tile * (64 * TM) + wave * 16 * TM;
+    int pm[TM], ph[TM], pw[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = mb + i * 16 + fr;
+      pm[i] = m < p.M ? m : -1;
+      const int mm = m < p.M ? m : 0;
+      const int img = mm / HW, r = mm - img * HW;
+      ph[i] = r / p.W;
+      pw[i] = r - ph[i] * p.W;
+    }
+    f32x4 acc[2][TM];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto load_tap = [&](int tap, v4u (&dst)[TM][4]) {
+      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int hh = ph[i] + dy, ww = pw[i] + dx;
+        const bool ok = pm[i] >= 0 && hh >= 0 && hh < p.H && ww >= 0 && ww < p.W;
+        // out-of-image taps: an offset past num_records makes the buffer load return 0
+        const int off = ok ? ((pm[i] + dy * p.W + dx) * kC3 + fk) * 2 : 0x40000000;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) dst[i][c] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + c * 64, 0, 0);
+      }
+    };
+    auto mma_tap = [&](int tap, const v4u (&src)[TM][4]) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        bf16x8 fa[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          fa[j] = *reinterpret_cast<const bf16x8*>(&Ws[(j * 16 + fr) * kWsK + tap * kC3 + c * 32 + fk]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) acc[j][i] = mfma16(fa[j], as_frag(src[i][c]), acc[j][i]);
+      }
+    };
+    // taps in ping-pong pairs: tap t+1's fragments load while tap t multiplies
+    v4u xa[TM][4], xb[TM][4];
+    load_tap(0, xa);
+#pragma unroll 1
+    for (int tap = 0; tap < 8; tap += 2) {
+      load_tap(tap + 1, xb);
+      mma_tap(tap, xa);
+      load_tap(tap + 2, xa);
+      mma_tap(tap + 1, xb);
+    }
+    mma_tap(8, xa);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int nb = j * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if (pm[i] >= 0) {
+          const f32x4 v = acc[j][i];
+          *reinterpret_cast<v2u*>(p.y + (size_t)pm[i] * p.ldy + nb) = v2u{pack2(v[0], v[1]), pack2(v[2], v[3])};
+        }
+      }
+    }
+  }
+}
+
+// ============================================================================
+// K10a: stem epilogue  y = relu(maxpool3x3/2(x) + b)  (bias+ReLU commute with max)
+// ============================================================================
+// x: [imgs][H][W][C] bf16 (conv0 output without bias), y: [imgs][Ho][Wo] rows of ldy.
+// One thread per (output pixel, 8-channel chunk).
+__global__ void __launch_bounds__(256) stem_pool_kernel(const uint16_t* __restrict__ x, const float* __restrict__ bias,
+                                                        uint16_t* __restrict__ y, int imgs, int H, int W, int C,
+                                                        int ldy) {
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2, CC = C / 8;
+  const size_t total = (size_t)imgs * Ho * Wo * CC;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(t % CC);
+    const size_t pix = t / CC;
+    const int ow = (int)(pix % Wo);
+    const int oh = (int)((pix / Wo) % Ho);
+    const int img = (int)(pix / ((size_t)Wo * Ho));
+    float mx[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mx[e] = -3.0e38f;
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int h = 2 * oh + dy;
+      if (h < 0 || h >= H) continue;
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int w = 2 * ow + dx;
+        if (w < 0 || w >= W) continue;
+        float f[8];
+        unpack8(ldg16(x + (((size_t)img * H + h) * W + w) * C + cc * 8), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], f[e]);
+      }
+    }
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = fmaxf(mx[e] + bias[cc * 8 + e], 0.f);
+    *reinterpret_cast<v4u*>(y + pix * ldy + cc * 8) = pack8(o);
+  }
+}
+
+// ============================================================================
+// K10b: head  out[img][c] = mean_p relu(x[img][p][c]*s[c] + b[c])   (bf16 out)
+// ============================================================================
+// One block per image; each thread owns 8-channel chunks and walks the pixels.
+__global__ void __launch_bounds__(256) head_pool_kernel(const uint16_t* __restrict__ x, const float* __restrict__ s,
+                                                        const float* __restrict__ b, uint16_t* __restrict__ out,
+                                                        int HW, int C) {
+  const int img = blockIdx.x;
+  for (int cc = threadIdx.x; cc < C / 8; cc += blockDim.x) {
+    float sc[8], bi[8], acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sc[e] = s[cc * 8 + e];
+      bi[e] = b[cc * 8 + e];
+      acc[e] = 0.f;
+    }
+    for (int p = 0; p < HW; ++p) {
+      float f[8];
+      unpack8(ldg16(x + ((size_t)img * HW + p) * C + cc * 8), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += fmaxf(f[e] * sc[e] + bi[e], 0.f);
+    }
+    const float inv = 1.0f / (float)HW;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    *reinterpret_cast<v4u*>(out + (size_t)img * C + cc * 8) = pack8(acc);
+  }
+}
+
+template <int TM, bool PRO, bool POOL>
+int launch_1x1(const Conv1x1Params& p, hipStream_t s) {
+  dim3 g((p.M + 32 * TM - 1) / (32 * TM), p.N / 128);
+  hipLaunchKernelGGL((conv1x1_kernel<TM, PRO, POOL>), g, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+template <bool PRO, bool POOL>
+int pick_tm(const Conv1x1Params& p, hipStream_t s) {
+  // largest tile that still yields >= 512 blocks (2 per CU); small problems
+  // take 32-row tiles to spread over the CUs
+  const long nb = p.N / 128;
+  if ((long)((p.M + 127) / 128) * nb >= 512) return launch_1x1<4, PRO, POOL>(p, s);
+  if ((long)((p.M + 63) / 64) * nb >= 512) return launch_1x1<2, PRO, POOL>(p, s);
+  return launch_1x1<1, PRO, POOL>(p, s);
+}
+
+template <int TM>
+int launch_3x3(Conv3x3Params p, hipStream_t s) {
+  static bool attr = false;
+  const int lds = kN3 * kWsK * 2;
+  if (!attr) {
+    int rc = hipFuncSetAttribute((const void*)conv3x3_kernel<TM>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (rc != hipSuccess) return rc;
+    attr = true;
+  }
+  p.tiles = (p.M + 64 * TM - 1) / (64 * TM);
+  const int grid = p.tiles < 512 ? p.tiles : 512;  // 2 resident blocks per CU (LDS-limited)
+  hipLaunchKernelGGL((conv3x3_kernel<TM>), dim3(grid), dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+// 1x1 conv (GEMM) with optional fused pre-activation BN+ReLU (in_scale/in_bias
+// non-null) and 2x2 average pool (pool != 0; H, W = pre-pool dims, M = pooled
+// rows).  Requires K % 32 == 0, K <= 1024 when fused, N % 128 == 0,
+// ldx/ldy/y offsets multiples of 8 elements and 16-B aligned x/w.
+int tcamd_dn_conv1x1(const void* x, int ldx, int M, int K, const float* in_scale, const float* in_bias,
+                     const void* w, int N, const float* out_bias, int relu_out, void* y, int ldy, int pool, int H,
+                     int W, void* stream) {
+  if (M <= 0) return hipSuccess;
+  if (K % 32 || N % 128 || ldx % 8 || ldy % 4 || K > ldx) return hipErrorInvalidValue;
+  const bool pro = in_scale != nullptr && in_bias != nullptr;
+  if (pro && K > kMaxK) return hipErrorInvalidValue;
+  if (pool && (!pro || H % 2 || W % 2)) return hipErrorInvalidValue;
+  if (((uintptr_t)x | (uintptr_t)w) % 16 || ((uintptr_t)y) % 8) return hipErrorInvalidValue;
+  Conv1x1Params p;
+  p.x = (const uint16_t*)x;
+  p.in_scale = in_scale;
+  p.in_bias = in_bias;
+  p.w = (const uint16_t*)w;
+  p.out_bias = out_bias;
+  p.y = (uint16_t*)y;
+  p.ldx = ldx;
+  p.M = M;
+  p.K = K;
+  p.N = N;
+  p.ldy = ldy;
+  p.relu_out = relu_out;
+  p.H = H;
+  p.W = W;
+  hipStream_t s = (hipStream_t)stream;
+  if (pool) return pick_tm<true, true>(p, s);
+  if (pro) return pick_tm<true, false>(p, s);
+  return pick_tm<false, false>(p, s);
+}
+
+// 3x3 conv 128->32, pad 1, over z [imgs*H*W][128]; w [32][3][3][128];
+// writes 32 channels per pixel at y + pixel*ldy.
+int tcamd_dn_conv3x3(const void* z, int imgs, int H, int W, const void* w, void* y, int ldy, void* stream) {
+  const long M = (long)imgs * H * W;
+  if (M <= 0) return hipSuccess;
+  if (M * kC3 * 2 >= 0x3ffff000L || ldy % 4) return hipErrorInvalidValue;
+  if (((uintptr_t)z | (uintptr_t)w) % 16 || ((uintptr_t)y) % 8) return hipErrorInvalidValue;
+  Conv3x3Params p;
+  p.z = (const uint16_t*)z;
+  p.w = (const uint16_t*)w;
+  p.y = (uint16_t*)y;
+  p.M = (int)M;
+  p.H = H;
+  p.W = W;
+  p.ldy = ldy;
+  hipStream_t s = (hipStream_t)stream;
+  if ((M + 255) / 256 >= 512) return launch_3x3<4>(p, s);
+  if ((M + 127) / 128 >= 256) return launch_3x3<2>(p, s);
+  return launch_3x3<1>(p, s);
+}
+
+int tcamd_dn_stem_pool(const void* x, const float* bias, void* y, int imgs, int H, int W, int C, int ldy,
+                       void* stream) {
+  if (imgs <= 0) return hipSuccess;
+  if (C % 8 || ldy % 8) return hipErrorInvalidValue;
+  const size_t total = (size_t)imgs * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+  hipLaunchKernelGGL(stem_pool_kernel, dim3(tcamd::grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                     (const uint16_t*)x, bias, (uint16_t*)y, imgs, H, W, C, ldy);
+  return hipGetLastError();
+}
+
+int tcamd_dn_head_pool(const void* x, const float* s, const float* b, void* out, int imgs, int HW, int C,
+                       void* stream) {
+  if (imgs <= 0) return hipSuccess;
+  if (C % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_pool_kernel, dim3(imgs), dim3(128), 0, (hipStream_t)stream, (const uint16_t*)x, s, b,
+                     (uint16_t*)out, HW, C);
+  return hipGetLastError();
+}
+
+}  // extern "C"

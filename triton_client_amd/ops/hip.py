@@ -108,6 +108,30 @@ _SIGS = {
         ],
         ctypes.c_int,
     ),
+    # fused DenseNet kernels (csrc/kernels/densenet.hip)
+    "tcamd_dn_conv1x1": (
+        [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
+    "tcamd_dn_conv3x3": (
+        [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+         ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "tcamd_dn_stem_pool": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+         ctypes.c_int, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "tcamd_dn_head_pool": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+         ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_pack_bytes_workspace": ([ctypes.c_uint64], ctypes.c_uint64),
     "tcamd_pack_bytes": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
@@ -402,6 +426,27 @@ def batched_copy(srcs, dsts, sizes, stream=None):
     d = (ctypes.c_void_p * n)(*[int(p) for p in dsts])
     b = (ctypes.c_uint64 * n)(*[int(x) for x in sizes])
     _check(_load().tcamd_batched_copy(s, d, b, n, _vp(stream)), "batched_copy")
+
+
+def dn_conv1x1(x, ldx, M, K, in_scale, in_bias, w, N, out_bias, relu_out, y, ldy, pool=0, H=0, W=0, stream=None):
+    """K8: y[m, :N] = epi(relu(x[m, :K]*s + b) @ w[N, K]^T); pool=1 fuses a 2x2 avg-pool (transition)."""
+    _check(_load().tcamd_dn_conv1x1(x, ldx, M, K, in_scale, in_bias, w, N, out_bias, int(relu_out), y, ldy,
+                                    int(pool), H, W, _vp(stream)), "dn_conv1x1")
+
+
+def dn_conv3x3(z, imgs, H, W, w, y, ldy, stream=None):
+    """K9: 3x3/pad-1 conv 128->32 over NHWC rows z; 32 channels per pixel written at y + pixel*ldy."""
+    _check(_load().tcamd_dn_conv3x3(z, imgs, H, W, w, y, ldy, _vp(stream)), "dn_conv3x3")
+
+
+def dn_stem_pool(x, bias, y, imgs, H, W, C, ldy, stream=None):
+    """K10a: y = relu(maxpool3x3/2(x) + bias) into rows of ldy elements."""
+    _check(_load().tcamd_dn_stem_pool(x, bias, y, imgs, H, W, C, ldy, _vp(stream)), "dn_stem_pool")
+
+
+def dn_head_pool(x, scale, bias, out, imgs, HW, C, stream=None):
+    """K10b: out[i, c] = mean_p relu(x[i, p, c]*scale[c] + bias[c])."""
+    _check(_load().tcamd_dn_head_pool(x, scale, bias, out, imgs, HW, C, _vp(stream)), "dn_head_pool")
 
 
 def pack_bytes_workspace(n):
