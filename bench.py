@@ -41,6 +41,10 @@ def main():
     ap.add_argument("--fanout", default="rccl", choices=["rccl", "p2p", "local"])
     ap.add_argument("--instance-count", type=int, default=2)
     ap.add_argument("--max-queue-delay-us", type=int, default=500)
+    ap.add_argument("--engine", default="fused", choices=["fused", "torch"],
+                    help="densenet_onnx engine in the server (fused HIP/MFMA kernels or torch/MIOpen)")
+    ap.add_argument("--loadgen", default="native", choices=["native", "python"],
+                    help="native: C++ perf engine (csrc/cpp/perf) in-process via ctypes; python: grpc.aio loop")
     ap.add_argument("--server-log", default="")
     ap.add_argument("--server-url", default="", help="use an already running server (gRPC host:port, HTTP port = +1 unless --http-url)")
     ap.add_argument("--http-url", default="")
@@ -63,7 +67,7 @@ def main():
         srv = ServerProcess(
             device=local_rank,
             models="densenet_onnx",
-            extra_args=["--instance-count", str(args.instance_count),
+            extra_args=["--instance-count", str(args.instance_count), "--engine", args.engine,
                         "--max-queue-delay-us", str(args.max_queue_delay_us)],
             log_path=log_path,
         )
@@ -81,6 +85,7 @@ def main():
     from triton_client_amd.parallel import fanout
     from triton_client_amd.perf.loadgen import ConcurrencyRun, percentile_us
     regions = []
+    sessions = []
     client = None
     try:
         log("waiting for server (log %s)" % log_path)
@@ -98,33 +103,57 @@ def main():
         if not fanout.verify_replicas(inp, in_bytes):
             raise RuntimeError("fan-out replicas differ across ranks")
         client.register_cuda_shared_memory("data_0_in", hipshm.get_raw_handle(inp), local_rank, in_bytes)
-        outs = []
-        for s in range(conc):
-            name = "fc6_1_out_%d" % s
-            r = hipshm.create_shared_memory_region(name, out_bytes, local_rank)
-            regions.append(r)
-            client.register_cuda_shared_memory(name, hipshm.get_raw_handle(r), local_rank, out_bytes)
-            o = grpcclient.InferRequestedOutput("fc6_1")
-            o.set_shared_memory(name, out_bytes)
-            outs.append([o])
+        # one python-client request first: sanity of the whole shm path (finite logits land in our region)
+        chk = hipshm.create_shared_memory_region("fc6_1_check", out_bytes, local_rank)
+        regions.append(chk)
+        client.register_cuda_shared_memory("fc6_1_check", hipshm.get_raw_handle(chk), local_rank, out_bytes)
         x = grpcclient.InferInput("data_0", [bs, 3, 224, 224], "FP32")
         x.set_shared_memory("data_0_in", in_bytes)
-        runner = ConcurrencyRun(client, "densenet_onnx", [x], outs, conc)
+        o = grpcclient.InferRequestedOutput("fc6_1")
+        o.set_shared_memory("fc6_1_check", out_bytes)
+        client.infer("densenet_onnx", [x], outputs=[o])
+        o0 = hipshm.get_contents_as_numpy(chk, np.float32, [bs, 1000])
+        if not np.isfinite(o0).all() or not np.abs(o0).max() > 0:
+            raise RuntimeError("bad logits in output region")
 
-        lat, errs, _ = runner.run(max(args.warmup, 1))
+        if args.loadgen == "native":
+            from triton_client_amd.perf.native import PerfSession
+
+            perf = PerfSession(["-m", "densenet_onnx", "-i", "grpc", "-u", srv.grpc_url, "-b", bs,
+                                "--shared-memory", "hip", "--device", local_rank,
+                                "--shared-memory-input", "data_0=data_0_in",
+                                "--output-shared-memory-size", out_bytes, "--concurrency-range", conc])
+            sessions.append(perf)
+
+            def run(steps):
+                lat_ns, el = perf.run_fixed(conc, steps * conc)
+                return list(lat_ns / 1e9), []
+        else:
+            outs = []
+            for s in range(conc):
+                name = "fc6_1_out_%d" % s
+                r = hipshm.create_shared_memory_region(name, out_bytes, local_rank)
+                regions.append(r)
+                client.register_cuda_shared_memory(name, hipshm.get_raw_handle(r), local_rank, out_bytes)
+                o = grpcclient.InferRequestedOutput("fc6_1")
+                o.set_shared_memory(name, out_bytes)
+                outs.append([o])
+            runner = ConcurrencyRun(client, "densenet_onnx", [x], outs, conc)
+
+            def run(steps):
+                lat, errs, _ = runner.run(steps)
+                return lat, errs
+
+        lat, errs = run(max(args.warmup, 1))
         if errs:
             raise RuntimeError("warmup errors: %s" % errs[0])
-        # sanity: outputs are finite logits
-        o0 = hipshm.get_contents_as_numpy(regions[1], np.float32, [bs, 1000])
-        if not np.isfinite(o0).all():
-            raise RuntimeError("non-finite logits in output region")
-        log("warmup done: p50 %.0f us" % percentile_us(lat, 50))
+        log("warmup done (%s loadgen): p50 %.0f us" % (args.loadgen, percentile_us(lat, 50)))
 
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        lat, errs, _ = runner.run(args.steps)
+        lat, errs = run(args.steps)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -168,6 +197,8 @@ def main():
                     "concurrency_per_gpu": conc,
                     "protocol": "grpc",
                     "shared_memory": "hip",
+                    "engine": args.engine,
+                    "loadgen": args.loadgen,
                 },
                 "p50_latency_us": round(percentile_us(all_lat, 50), 1),
                 "p90_latency_us": round(percentile_us(all_lat, 90), 1),
@@ -179,6 +210,11 @@ def main():
             print(json.dumps(res), flush=True)
         return 0
     finally:
+        for p in sessions:
+            try:
+                p.close()
+            except Exception as e:  # noqa: BLE001
+                log("perf session cleanup error: %s" % e)
         try:
             if client is not None:
                 client.unregister_cuda_shared_memory()

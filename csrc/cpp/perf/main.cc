@@ -1,0 +1,62 @@
+// perf_analyzer CLI entry point (see perf.h for the architecture).
+#include <cstdio>
+
+#include "perf.h"
+
+int main(int argc, char** argv)
+{
+  tcperf::Options o;
+  bool help = false;
+  tcperf::Error e = tcperf::ParseOptions(argc, argv, &o, &help);
+  if (help) {
+    printf("%s", tcperf::Usage().c_str());
+    return 0;
+  }
+  if (!e.IsOk()) {
+    fprintf(stderr, "error: %s\n\n%s", e.Message().c_str(), tcperf::Usage().c_str());
+    return 1;
+  }
+  std::unique_ptr<tcperf::Session> s;
+  e = tcperf::Session::Create(o, &s);
+  if (!e.IsOk()) {
+    fprintf(stderr, "error: %s\n", e.Message().c_str());
+    return 1;
+  }
+  tcperf::PrintSettings(o, s->info, s->data->Describe());
+  std::vector<double> loads;
+  if (o.rate_mode && o.request_intervals_file.empty()) {
+    for (double r = o.rate_start; r <= o.rate_end + 1e-9; r += o.rate_step) loads.push_back(r);
+  } else if (o.rate_mode) {
+    loads.push_back(1.0);  // schedule comes from the intervals file
+  } else {
+    for (uint64_t c = o.conc_start; c <= o.conc_end; c += o.conc_step) loads.push_back(static_cast<double>(c));
+  }
+  std::vector<tcperf::PointResult> pts;
+  tcperf::Profiler prof(o, s->backend.get(), s->engine.get());
+  int rc = 0;
+  for (double load : loads) {
+    tcperf::PointResult p;
+    e = prof.Profile(load, &p);
+    if (!e.IsOk()) {
+      fprintf(stderr, "error: %s\n", e.Message().c_str());
+      rc = 1;
+      break;
+    }
+    tcperf::PrintPoint(o, p);
+    pts.push_back(p);
+    const double lat = o.percentile > 0 ? p.p99_us : p.avg_us;
+    if (o.latency_threshold_ms && lat > o.latency_threshold_ms * 1000.0) {
+      printf("Measured latency went over the set limit of %lu msec.\n",
+             static_cast<unsigned long>(o.latency_threshold_ms));
+      break;
+    }
+  }
+  s->engine->Stop();
+  if (!pts.empty()) tcperf::PrintSummary(o, pts);
+  e = tcperf::WriteCsv(o, pts);
+  if (!e.IsOk()) fprintf(stderr, "error: %s\n", e.Message().c_str());
+  e = tcperf::WriteJson(o, pts, s->data->Describe());
+  if (!e.IsOk()) fprintf(stderr, "error: %s\n", e.Message().c_str());
+  s.reset();
+  return rc;
+}

@@ -1,0 +1,313 @@
+// perf_analyzer for MI355X hosts — native load generator for KServe-v2 servers.
+//
+// The reference snapshot ships only relocation stubs for perf_analyzer
+// (reference src/c++/perf_analyzer/README.md:29-30); this is the functional
+// equivalent specified in SURVEY.md Appendix D, built on our C++ clients
+// (src/http_client.cc, src/grpc_client.cc) with no Python on the hot path:
+//
+//   Options      perf_analyzer-compatible CLI (-m -x -u -i -b -a --sync
+//                --streaming --shape -H --concurrency-range
+//                --request-rate-range --request-distribution
+//                --request-intervals --sequence-length --sequence-id-range
+//                --input-data --string-length --string-data
+//                --shared-memory none|system|cuda|hip
+//                --output-shared-memory-size --measurement-interval/-p
+//                --measurement-mode --measurement-request-count
+//                --stability-percentage/-s --max-trials/-r --percentile
+//                --latency-threshold/-l -f --warmup-request-count ...)
+//   Backend      one protocol client (HTTP/1.1 or gRPC/h2) + control plane
+//   DataSet      request tensors: host bytes, or system / HIP shared-memory
+//                regions filled once (HIP: K1 Philox fill on the device)
+//   LoadEngine   closed-loop concurrency slots or open-loop request-rate
+//                schedule; completions are handed to a worker thread that
+//                records timestamps and re-issues (never inside the
+//                transport's callback thread)
+//   Profiler     measurement windows, 3-window stability, percentiles,
+//                server-side breakdown from ModelInferenceStatistics deltas
+//   Reporter     perf_analyzer-style stdout, CSV (-f) and JSON reports
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "common.h"
+#include "grpc_client.h"
+#include "http_client.h"
+
+namespace tcperf {
+
+using triton::client::Error;
+using triton::client::InferInput;
+using triton::client::InferOptions;
+using triton::client::InferRequestedOutput;
+using triton::client::InferResult;
+
+uint64_t NowNs();
+
+struct Options {
+  std::string model;
+  std::string version;
+  std::string url;
+  std::string protocol = "http";
+  bool async = true;
+  bool streaming = false;
+  int batch = 1;
+  std::map<std::string, std::vector<int64_t>> shapes;
+  std::map<std::string, std::string> headers;
+  bool verbose = false;
+  // load
+  bool rate_mode = false;
+  uint64_t conc_start = 1, conc_end = 1, conc_step = 1;
+  double rate_start = 0, rate_end = 0, rate_step = 1;
+  std::string distribution = "constant";
+  std::string request_intervals_file;
+  int sequence_length = 20;
+  uint64_t seq_id_start = 1, seq_id_end = UINT32_MAX;
+  int num_clients = 0;  // 0: auto
+  // data
+  std::string input_data = "random";
+  int string_length = 128;
+  std::string string_data;
+  std::string shared_memory = "none";
+  size_t output_shm_size = 102400;
+  std::map<std::string, std::string> preregistered_inputs;  // input -> registered region name
+  int device = 0;
+  uint64_t seed = 0;
+  // measurement
+  std::string measurement_mode = "time_windows";
+  uint64_t measurement_interval_ms = 5000;
+  uint64_t measurement_request_count = 50;
+  double stability_pct = 10.0;
+  int max_trials = 10;
+  int percentile = -1;
+  uint64_t latency_threshold_ms = 0;
+  uint64_t warmup_requests = 0;
+  std::string csv_file;
+  std::string json_file;
+  bool verbose_csv = false;
+  bool collect_server_stats = true;
+};
+
+/// Parse perf_analyzer flags.  Returns an error for unknown/invalid flags;
+/// *help is set when -h/--help was given.
+Error ParseOptions(int argc, char** argv, Options* opts, bool* help);
+std::string Usage();
+
+struct TensorSpec {
+  std::string name;
+  std::string datatype;
+  std::vector<int64_t> shape;  // without the batch dim
+};
+
+struct ModelInfo {
+  std::vector<TensorSpec> inputs, outputs;
+  int max_batch_size = 0;
+  bool sequential = false;
+  bool decoupled = false;
+};
+
+struct ServerStats {
+  uint64_t inference_count = 0, execution_count = 0;
+  uint64_t success_count = 0, success_ns = 0;
+  uint64_t queue_ns = 0, compute_input_ns = 0, compute_infer_ns = 0, compute_output_ns = 0;
+};
+
+// ---------------------------------------------------------------------------
+class Backend {
+ public:
+  static Error Create(const Options& o, std::unique_ptr<Backend>* out);
+  ~Backend();
+  Error ModelMeta(ModelInfo* info);
+  Error Stats(ServerStats* st);
+  Error RegisterSystem(const std::string& name, const std::string& key, size_t bytes);
+  Error UnregisterSystem(const std::string& name);
+  Error RegisterDevice(const std::string& name, const cudaIpcMemHandle_t& h, int dev, size_t bytes);
+  Error UnregisterDevice(const std::string& name);
+  Error AsyncInfer(std::function<void(InferResult*)> cb, const InferOptions& opt,
+                   const std::vector<InferInput*>& in, const std::vector<const InferRequestedOutput*>& out);
+  Error SyncInfer(InferResult** r, const InferOptions& opt, const std::vector<InferInput*>& in,
+                  const std::vector<const InferRequestedOutput*>& out);
+  Error StartStream(std::function<void(InferResult*)> cb);
+  Error StreamInfer(const InferOptions& opt, const std::vector<InferInput*>& in,
+                    const std::vector<const InferRequestedOutput*>& out);
+  Error StopStream();
+  Error ClientStat(triton::client::InferStat* st);
+  bool IsGrpc() const { return grpc_ != nullptr; }
+
+ private:
+  Options o_;
+  triton::client::Headers headers_;
+  std::unique_ptr<triton::client::InferenceServerHttpClient> http_;
+  std::unique_ptr<triton::client::InferenceServerGrpcClient> grpc_;
+};
+
+// ---------------------------------------------------------------------------
+/// Request tensors shared by every request of a run.
+class DataSet {
+ public:
+  ~DataSet();
+  Error Init(const Options& o, const ModelInfo& info, Backend* be, size_t max_slots);
+  /// Inputs / outputs of one slot (slots only differ in output regions).
+  const std::vector<InferInput*>& Inputs() const { return inputs_; }
+  const std::vector<const InferRequestedOutput*>& Outputs(size_t slot) const;
+  std::string Describe() const { return describe_; }
+  void Release(Backend* be);
+
+ private:
+  struct Region {
+    std::string name;
+    std::string key;   // system shm key
+    int fd = -1;
+    void* host = nullptr;
+    void* dev = nullptr;
+    size_t bytes = 0;
+    bool device = false;
+    bool owned = true;
+  };
+  Error MakeRegion(Backend* be, const std::string& name, size_t bytes, bool device, Region* r);
+  Error FillHost(const TensorSpec& t, const std::vector<int64_t>& shape, std::vector<uint8_t>* bytes,
+                 std::vector<std::string>* strs);
+  Options o_;
+  std::vector<InferInput*> inputs_;
+  std::vector<std::vector<InferRequestedOutput*>> outputs_;  // [slot][output]
+  std::vector<std::vector<const InferRequestedOutput*>> outputs_c_;
+  std::vector<std::vector<uint8_t>> host_data_;
+  std::vector<Region> regions_;
+  std::string describe_;
+};
+
+// ---------------------------------------------------------------------------
+struct Record {
+  uint64_t start_ns, end_ns;
+  bool ok;
+};
+
+/// Issues requests and records completions.  Closed loop (concurrency) or
+/// open loop (request rate).  Thread-safe accessors for the profiler.
+class LoadEngine {
+ public:
+  LoadEngine(const Options& o, Backend* be, DataSet* data, size_t max_slots);
+  ~LoadEngine();
+  /// Closed loop with `n` requests in flight (0 stops issuing).
+  Error SetConcurrency(size_t n);
+  /// Open loop at `rate` requests/sec (distribution from options).
+  Error SetRequestRate(double rate);
+  /// Closed loop that issues exactly `total` requests and waits for all of
+  /// them; latencies (ns) of those requests are returned in issue order.
+  Error RunFixed(size_t concurrency, uint64_t total, std::vector<uint64_t>* lat_ns, double* elapsed_s);
+  void Stop();
+  /// Records completed since `since_index`; returns the new end index.
+  size_t Snapshot(size_t since_index, std::vector<Record>* out);
+  size_t CompletedCount();
+  std::string FirstError();
+  size_t InFlight() const { return in_flight_.load(); }
+
+  struct Slot {
+    InferOptions opt{""};
+    uint64_t seq_id = 0;
+    int seq_pos = 0;
+    uint64_t sent_ns = 0;
+    bool busy = false;
+  };
+  void SetSequenceModel(bool v) { seq_model_ = v; }
+
+ private:
+  void Worker();
+  void SyncLoop(size_t slot);
+  Error Issue(size_t slot);
+  Error EnsureStream();
+  void PrepareSequence(Slot* s);
+  void RateLoop(double rate, uint64_t gen);
+  void OnComplete(size_t slot, uint64_t start_ns, InferResult* r);
+
+  Options o_;
+  Backend* be_;
+  DataSet* data_;
+  std::vector<Slot> slots_;
+  std::mutex mu_;
+  std::condition_variable cv_;        // worker wake-up
+  std::condition_variable fixed_cv_;  // completion progress
+  std::deque<std::pair<size_t, Record>> done_;
+  std::vector<size_t> pending_start_;
+  std::vector<Record> records_;
+  std::mutex rec_mu_;
+  size_t target_conc_ = 0;
+  uint64_t fixed_left_ = 0;  // fixed-count mode: requests still to issue
+  bool fixed_mode_ = false;
+  std::vector<uint64_t>* fixed_lat_ = nullptr;
+  std::atomic<size_t> in_flight_{0};
+  std::atomic<bool> stop_{false};
+  bool exiting_ = false;
+  bool seq_model_ = false;
+  std::atomic<bool> rate_active_{false};
+  bool streaming_ = false;
+  std::thread worker_;
+  std::thread rate_thread_;
+  std::vector<std::thread> sync_threads_;
+  std::atomic<uint64_t> rate_gen_{0};
+  uint64_t next_seq_ = 0;
+  std::string first_error_;
+  std::vector<uint64_t> intervals_ns_;
+  // streaming: request id -> (slot, send time)
+  std::mutex stream_mu_;
+  std::map<std::string, std::pair<size_t, uint64_t>> stream_ids_;
+  uint64_t stream_counter_ = 0;
+};
+
+// ---------------------------------------------------------------------------
+struct PointResult {
+  double load = 0;  // concurrency or rate
+  bool rate_mode = false;
+  bool stable = false;
+  uint64_t request_count = 0;
+  double window_s = 0;
+  double throughput = 0;  // infer/sec (requests * batch / s)
+  double avg_us = 0, std_us = 0, p50_us = 0, p90_us = 0, p95_us = 0, p99_us = 0;
+  double client_send_us = 0, client_recv_us = 0;
+  uint64_t errors = 0;
+  ServerStats server;  // delta over the windows
+  bool has_server = false;
+};
+
+class Profiler {
+ public:
+  Profiler(const Options& o, Backend* be, LoadEngine* eng) : o_(o), be_(be), eng_(eng) {}
+  Error Profile(double load, PointResult* out);
+
+ private:
+  Error Window(PointResult* w, std::vector<uint64_t>* lat);
+  Options o_;
+  Backend* be_;
+  LoadEngine* eng_;
+  size_t rec_index_ = 0;
+};
+
+void PrintSettings(const Options& o, const ModelInfo& info, const std::string& data_desc);
+void PrintPoint(const Options& o, const PointResult& p);
+void PrintSummary(const Options& o, const std::vector<PointResult>& pts);
+Error WriteCsv(const Options& o, const std::vector<PointResult>& pts);
+Error WriteJson(const Options& o, const std::vector<PointResult>& pts, const std::string& data_desc);
+double Percentile(std::vector<uint64_t>& v, double p);
+
+/// Everything one perf run needs; used by main() and the C API.
+struct Session {
+  Options opts;
+  std::unique_ptr<Backend> backend;
+  ModelInfo info;
+  std::unique_ptr<DataSet> data;
+  std::unique_ptr<LoadEngine> engine;
+  size_t max_slots = 0;
+  static Error Create(const Options& o, std::unique_ptr<Session>* out);
+  ~Session();
+};
+
+}  // namespace tcperf

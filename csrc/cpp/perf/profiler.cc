@@ -1,0 +1,370 @@
+// perf_analyzer Profiler (measurement windows + stability) and Reporter
+// (stdout in perf_analyzer's layout, CSV, JSON), and Session setup.
+#include <time.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <fstream>
+#include <numeric>
+#include <sstream>
+
+#include "perf.h"
+
+namespace tcperf {
+
+double Percentile(std::vector<uint64_t>& v, double p)
+{
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  size_t idx = static_cast<size_t>(std::ceil(p / 100.0 * v.size()));
+  idx = idx == 0 ? 0 : idx - 1;
+  return static_cast<double>(v[std::min(idx, v.size() - 1)]);
+}
+
+static void SleepMs(uint64_t ms)
+{
+  struct timespec ts = {static_cast<time_t>(ms / 1000), static_cast<long>((ms % 1000) * 1000000)};
+  nanosleep(&ts, nullptr);
+}
+
+static ServerStats Delta(const ServerStats& a, const ServerStats& b)
+{
+  ServerStats d;
+  d.inference_count = b.inference_count - a.inference_count;
+  d.execution_count = b.execution_count - a.execution_count;
+  d.success_count = b.success_count - a.success_count;
+  d.success_ns = b.success_ns - a.success_ns;
+  d.queue_ns = b.queue_ns - a.queue_ns;
+  d.compute_input_ns = b.compute_input_ns - a.compute_input_ns;
+  d.compute_infer_ns = b.compute_infer_ns - a.compute_infer_ns;
+  d.compute_output_ns = b.compute_output_ns - a.compute_output_ns;
+  return d;
+}
+
+static void Accumulate(ServerStats* a, const ServerStats& b)
+{
+  a->inference_count += b.inference_count;
+  a->execution_count += b.execution_count;
+  a->success_count += b.success_count;
+  a->success_ns += b.success_ns;
+  a->queue_ns += b.queue_ns;
+  a->compute_input_ns += b.compute_input_ns;
+  a->compute_infer_ns += b.compute_infer_ns;
+  a->compute_output_ns += b.compute_output_ns;
+}
+
+static void FillLatency(PointResult* r, std::vector<uint64_t>& lat)
+{
+  if (lat.empty()) return;
+  double sum = 0, sq = 0;
+  for (auto x : lat) {
+    sum += x;
+    sq += static_cast<double>(x) * x;
+  }
+  const double n = static_cast<double>(lat.size());
+  const double mean = sum / n;
+  r->avg_us = mean / 1000.0;
+  r->std_us = std::sqrt(std::max(0.0, sq / n - mean * mean)) / 1000.0;
+  r->p50_us = Percentile(lat, 50) / 1000.0;
+  r->p90_us = Percentile(lat, 90) / 1000.0;
+  r->p95_us = Percentile(lat, 95) / 1000.0;
+  r->p99_us = Percentile(lat, 99) / 1000.0;
+}
+
+static double StabilityLatency(const Options& o, const PointResult& r)
+{
+  switch (o.percentile) {
+    case 50: return r.p50_us;
+    case 90: return r.p90_us;
+    case 95: return r.p95_us;
+    case 99: return r.p99_us;
+    default: return r.avg_us;
+  }
+}
+
+Error Profiler::Window(PointResult* w, std::vector<uint64_t>* lat)
+{
+  ServerStats s0, s1;
+  triton::client::InferStat c0, c1;
+  if (o_.collect_server_stats) {
+    Error e = be_->Stats(&s0);
+    if (!e.IsOk()) return e;
+  }
+  be_->ClientStat(&c0);
+  const uint64_t t0 = NowNs();
+  const size_t start_count = eng_->CompletedCount();
+  if (o_.measurement_mode == "count_windows") {
+    const uint64_t limit = t0 + 600ull * 1000000000ull;
+    while (eng_->CompletedCount() - start_count < o_.measurement_request_count && NowNs() < limit) {
+      if (!eng_->FirstError().empty()) break;
+      SleepMs(1);
+    }
+  } else {
+    SleepMs(o_.measurement_interval_ms);
+  }
+  const uint64_t t1 = NowNs();
+  be_->ClientStat(&c1);
+  if (o_.collect_server_stats) {
+    Error e = be_->Stats(&s1);
+    if (!e.IsOk()) return e;
+    w->server = Delta(s0, s1);
+    w->has_server = true;
+  }
+  std::vector<Record> recs;
+  rec_index_ = eng_->Snapshot(rec_index_, &recs);
+  lat->clear();
+  for (const auto& r : recs) {
+    if (r.ok) lat->push_back(r.end_ns - r.start_ns);
+    else w->errors++;
+  }
+  w->request_count = lat->size();
+  w->window_s = (t1 - t0) * 1e-9;
+  w->throughput = w->window_s > 0 ? w->request_count * static_cast<double>(o_.batch) / w->window_s : 0;
+  const uint64_t dn = c1.completed_request_count - c0.completed_request_count;
+  if (dn) {
+    w->client_send_us = (c1.cumulative_send_time_ns - c0.cumulative_send_time_ns) / 1000.0 / dn;
+    w->client_recv_us = (c1.cumulative_receive_time_ns - c0.cumulative_receive_time_ns) / 1000.0 / dn;
+  }
+  std::vector<uint64_t> tmp = *lat;
+  FillLatency(w, tmp);
+  return Error::Success;
+}
+
+Error Profiler::Profile(double load, PointResult* out)
+{
+  *out = PointResult();
+  out->load = load;
+  out->rate_mode = o_.rate_mode;
+  Error e = o_.rate_mode ? eng_->SetRequestRate(load) : eng_->SetConcurrency(static_cast<size_t>(load));
+  if (!e.IsOk()) return e;
+  if (o_.warmup_requests) {
+    const size_t c0 = eng_->CompletedCount();
+    while (eng_->CompletedCount() - c0 < o_.warmup_requests && eng_->FirstError().empty()) SleepMs(1);
+  }
+  rec_index_ = eng_->CompletedCount();
+  std::vector<PointResult> wins;
+  std::vector<std::vector<uint64_t>> lats;
+  for (int trial = 0; trial < o_.max_trials; ++trial) {
+    PointResult w;
+    std::vector<uint64_t> lat;
+    e = Window(&w, &lat);
+    if (!e.IsOk()) return e;
+    const std::string err = eng_->FirstError();
+    if (!err.empty()) return Error("request failed: " + err);
+    if (o_.verbose)
+      fprintf(stderr, "  window %d: %lu requests, %.1f infer/sec, latency %.0f usec\n", trial,
+              static_cast<unsigned long>(w.request_count), w.throughput, StabilityLatency(o_, w));
+    wins.push_back(w);
+    lats.push_back(std::move(lat));
+    if (wins.size() >= 3) {
+      const size_t n = wins.size();
+      double tsum = 0, lsum = 0;
+      for (size_t i = n - 3; i < n; ++i) {
+        tsum += wins[i].throughput;
+        lsum += StabilityLatency(o_, wins[i]);
+      }
+      const double tmean = tsum / 3, lmean = lsum / 3, pct = o_.stability_pct / 100.0;
+      bool stable = tmean > 0;
+      for (size_t i = n - 3; i < n && stable; ++i) {
+        if (std::fabs(wins[i].throughput - tmean) > pct * tmean) stable = false;
+        if (std::fabs(StabilityLatency(o_, wins[i]) - lmean) > pct * lmean) stable = false;
+      }
+      if (stable) {
+        out->stable = true;
+        break;
+      }
+    }
+  }
+  // merge the last (up to) 3 windows
+  const size_t n = wins.size();
+  const size_t from = n >= 3 ? n - 3 : 0;
+  std::vector<uint64_t> all;
+  for (size_t i = from; i < n; ++i) {
+    out->request_count += wins[i].request_count;
+    out->window_s += wins[i].window_s;
+    out->errors += wins[i].errors;
+    out->client_send_us += wins[i].client_send_us / (n - from);
+    out->client_recv_us += wins[i].client_recv_us / (n - from);
+    if (wins[i].has_server) {
+      Accumulate(&out->server, wins[i].server);
+      out->has_server = true;
+    }
+    all.insert(all.end(), lats[i].begin(), lats[i].end());
+  }
+  out->throughput = out->window_s > 0 ? out->request_count * static_cast<double>(o_.batch) / out->window_s : 0;
+  FillLatency(out, all);
+  return Error::Success;
+}
+
+// ============================================================================
+// Reporter
+// ============================================================================
+void PrintSettings(const Options& o, const ModelInfo& info, const std::string& data_desc)
+{
+  printf("*** Measurement Settings ***\n");
+  printf("  Batch size: %d\n", o.batch);
+  printf("  Service Kind: Triton (%s)\n", o.protocol == "grpc" ? "gRPC" : "HTTP");
+  if (o.measurement_mode == "count_windows")
+    printf("  Using \"count_windows\" mode for stabilization\n  Minimum number of samples in each window: %lu\n",
+           static_cast<unsigned long>(o.measurement_request_count));
+  else
+    printf("  Using \"time_windows\" mode for stabilization\n  Measurement window: %lu msec\n",
+           static_cast<unsigned long>(o.measurement_interval_ms));
+  if (o.latency_threshold_ms) printf("  Latency limit: %lu msec\n", static_cast<unsigned long>(o.latency_threshold_ms));
+  if (o.rate_mode) {
+    if (!o.request_intervals_file.empty())
+      printf("  Using request intervals from %s\n", o.request_intervals_file.c_str());
+    else
+      printf("  Request Rate limit: %g - %g requests per second (%s distribution)\n", o.rate_start, o.rate_end,
+             o.distribution.c_str());
+  } else {
+    printf("  Concurrency limit: %lu concurrent requests\n", static_cast<unsigned long>(o.conc_end));
+  }
+  printf("  Using %s calls for inference\n",
+         o.streaming ? "streaming" : (o.async ? "asynchronous" : "synchronous"));
+  if (info.sequential) printf("  Sequence model: %d requests per sequence\n", o.sequence_length);
+  printf("  Data: %s\n", data_desc.c_str());
+  if (o.percentile > 0) printf("  Stabilizing using p%d latency\n", o.percentile);
+  else printf("  Stabilizing using average latency\n");
+  printf("\n");
+  fflush(stdout);
+}
+
+void PrintPoint(const Options& o, const PointResult& p)
+{
+  if (p.rate_mode) printf("Request Rate: %g inference requests per seconds\n", p.load);
+  else printf("Request concurrency: %g\n", p.load);
+  printf("  Client: \n");
+  printf("    Request count: %lu\n", static_cast<unsigned long>(p.request_count));
+  printf("    Throughput: %.2f infer/sec\n", p.throughput);
+  if (o.percentile > 0) {
+    printf("    p50 latency: %.0f usec\n    p90 latency: %.0f usec\n    p95 latency: %.0f usec\n"
+           "    p99 latency: %.0f usec\n", p.p50_us, p.p90_us, p.p95_us, p.p99_us);
+  } else {
+    printf("    Avg latency: %.0f usec (standard deviation %.0f usec)\n", p.avg_us, p.std_us);
+    printf("    p50 latency: %.0f usec\n    p90 latency: %.0f usec\n    p95 latency: %.0f usec\n"
+           "    p99 latency: %.0f usec\n", p.p50_us, p.p90_us, p.p95_us, p.p99_us);
+  }
+  printf("    Avg %s time: %.0f usec (marshal request %.0f usec + response wait/unmarshal %.0f usec)\n",
+         o.protocol == "grpc" ? "gRPC" : "HTTP", p.client_send_us + p.client_recv_us, p.client_send_us,
+         p.client_recv_us);
+  if (p.errors) printf("    Failed requests: %lu\n", static_cast<unsigned long>(p.errors));
+  if (p.has_server) {
+    const ServerStats& s = p.server;
+    const double n = s.success_count ? static_cast<double>(s.success_count) : 1.0;
+    const double req = s.success_ns / n / 1000.0, q = s.queue_ns / n / 1000.0;
+    const double ci = s.compute_input_ns / n / 1000.0, cf = s.compute_infer_ns / n / 1000.0,
+                 co = s.compute_output_ns / n / 1000.0;
+    printf("  Server: \n");
+    printf("    Inference count: %lu\n", static_cast<unsigned long>(s.inference_count));
+    printf("    Execution count: %lu\n", static_cast<unsigned long>(s.execution_count));
+    printf("    Successful request count: %lu\n", static_cast<unsigned long>(s.success_count));
+    printf("    Avg request latency: %.0f usec (overhead %.0f usec + queue %.0f usec + compute input %.0f usec + "
+           "compute infer %.0f usec + compute output %.0f usec)\n",
+           req, std::max(0.0, req - q - ci - cf - co), q, ci, cf, co);
+  }
+  if (!p.stable) printf("  [WARNING] measurement did not stabilise within %d windows\n", o.max_trials);
+  printf("\n");
+  fflush(stdout);
+}
+
+void PrintSummary(const Options& o, const std::vector<PointResult>& pts)
+{
+  printf("Inferences/Second vs. Client %s Batch Latency\n", o.percentile > 0 ? ("p" + std::to_string(o.percentile)).c_str() : "Average");
+  for (const auto& p : pts)
+    printf("%s: %g, throughput: %.2f infer/sec, latency %.0f usec\n", p.rate_mode ? "Request Rate" : "Concurrency",
+           p.load, p.throughput, StabilityLatency(o, p));
+  fflush(stdout);
+}
+
+Error WriteCsv(const Options& o, const std::vector<PointResult>& pts)
+{
+  if (o.csv_file.empty()) return Error::Success;
+  std::ofstream f(o.csv_file);
+  if (!f) return Error("cannot write " + o.csv_file);
+  f << (o.rate_mode ? "Request Rate" : "Concurrency")
+    << ",Inferences/Second,Client Send,Network+Server Send/Recv,Server Queue,Server Compute Input,"
+       "Server Compute Infer,Server Compute Output,Client Recv,p50 latency,p90 latency,p95 latency,p99 latency,"
+       "Avg latency,request/response,response wait";
+  if (o.verbose_csv) f << ",Failed requests,Stable";
+  f << "\n";
+  for (const auto& p : pts) {
+    const ServerStats& s = p.server;
+    const double n = s.success_count ? static_cast<double>(s.success_count) : 1.0;
+    const double q = s.queue_ns / n / 1000.0, ci = s.compute_input_ns / n / 1000.0,
+                 cf = s.compute_infer_ns / n / 1000.0, co = s.compute_output_ns / n / 1000.0;
+    const double net = std::max(0.0, p.avg_us - p.client_send_us - p.client_recv_us - q - ci - cf - co);
+    char line[1024];
+    snprintf(line, sizeof(line), "%g,%.2f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f",
+             p.load, p.throughput, p.client_send_us, net, q, ci, cf, co, p.client_recv_us, p.p50_us, p.p90_us,
+             p.p95_us, p.p99_us, p.avg_us, p.client_send_us, p.client_recv_us);
+    f << line;
+    if (o.verbose_csv) f << "," << p.errors << "," << (p.stable ? 1 : 0);
+    f << "\n";
+  }
+  return Error::Success;
+}
+
+Error WriteJson(const Options& o, const std::vector<PointResult>& pts, const std::string& data_desc)
+{
+  if (o.json_file.empty()) return Error::Success;
+  std::ofstream f(o.json_file);
+  if (!f) return Error("cannot write " + o.json_file);
+  f << "{\"model\":\"" << o.model << "\",\"batch_size\":" << o.batch << ",\"protocol\":\"" << o.protocol
+    << "\",\"shared_memory\":\"" << o.shared_memory << "\",\"mode\":\"" << (o.rate_mode ? "request_rate" : "concurrency")
+    << "\",\"data\":\"" << data_desc << "\",\"points\":[";
+  for (size_t i = 0; i < pts.size(); ++i) {
+    const auto& p = pts[i];
+    const auto& s = p.server;
+    char buf[1024];
+    snprintf(buf, sizeof(buf),
+             "%s{\"load\":%g,\"stable\":%s,\"request_count\":%lu,\"window_s\":%.6f,\"throughput\":%.3f,"
+             "\"avg_us\":%.1f,\"std_us\":%.1f,\"p50_us\":%.1f,\"p90_us\":%.1f,\"p95_us\":%.1f,\"p99_us\":%.1f,"
+             "\"client_send_us\":%.1f,\"client_recv_us\":%.1f,\"errors\":%lu,\"server\":{\"inference_count\":%lu,"
+             "\"execution_count\":%lu,\"success_count\":%lu,\"queue_ns\":%lu,\"compute_input_ns\":%lu,"
+             "\"compute_infer_ns\":%lu,\"compute_output_ns\":%lu}}",
+             i ? "," : "", p.load, p.stable ? "true" : "false", static_cast<unsigned long>(p.request_count),
+             p.window_s, p.throughput, p.avg_us, p.std_us, p.p50_us, p.p90_us, p.p95_us, p.p99_us, p.client_send_us,
+             p.client_recv_us, static_cast<unsigned long>(p.errors), static_cast<unsigned long>(s.inference_count),
+             static_cast<unsigned long>(s.execution_count), static_cast<unsigned long>(s.success_count),
+             static_cast<unsigned long>(s.queue_ns), static_cast<unsigned long>(s.compute_input_ns),
+             static_cast<unsigned long>(s.compute_infer_ns), static_cast<unsigned long>(s.compute_output_ns));
+    f << buf;
+  }
+  f << "]}\n";
+  return Error::Success;
+}
+
+// ============================================================================
+// Session
+// ============================================================================
+Error Session::Create(const Options& o, std::unique_ptr<Session>* out)
+{
+  std::unique_ptr<Session> s(new Session());
+  s->opts = o;
+  Error e = Backend::Create(o, &s->backend);
+  if (!e.IsOk()) return e;
+  e = s->backend->ModelMeta(&s->info);
+  if (!e.IsOk()) return Error("failed to get metadata of model '" + o.model + "': " + e.Message());
+  if (s->info.decoupled && !o.streaming) return Error("model is decoupled; use --streaming with -i grpc");
+  s->max_slots = o.rate_mode ? 64 : static_cast<size_t>(std::max<uint64_t>(1, o.conc_end));
+  s->data.reset(new DataSet());
+  e = s->data->Init(o, s->info, s->backend.get(), s->max_slots);
+  if (!e.IsOk()) {
+    s->data->Release(s->backend.get());
+    return e;
+  }
+  s->engine.reset(new LoadEngine(o, s->backend.get(), s->data.get(), s->max_slots));
+  s->engine->SetSequenceModel(s->info.sequential);
+  *out = std::move(s);
+  return Error::Success;
+}
+
+Session::~Session()
+{
+  engine.reset();
+  if (data) data->Release(backend.get());
+}
+
+}  // namespace tcperf

@@ -1,0 +1,126 @@
+"""Native perf_analyzer (csrc/cpp/perf) against the CPU test server.
+
+Covers the perf_analyzer-equivalent of SURVEY.md Appendix D: CLI parsing,
+concurrency / request-rate / fixed-count loads, sync / async / streaming
+issue paths, system shared memory, sequence models, BYTES inputs, stability
+windows and the CSV / JSON reports.  Everything here runs on CPU.
+"""
+
+import csv
+import json
+import os
+import subprocess
+
+import pytest
+
+from triton_client_amd.perf import native
+
+pytestmark = pytest.mark.skipif(not native.available(), reason="csrc/cpp not built")
+
+
+def _pa(args, timeout=120):
+    return subprocess.run([native.BIN_PATH] + [str(a) for a in args], capture_output=True, text=True,
+                          timeout=timeout)
+
+
+def test_help_and_bad_flags():
+    r = _pa(["-h"])
+    assert r.returncode == 0 and "--concurrency-range" in r.stdout
+    r = _pa(["-m", "simple", "--bogus-flag"])
+    assert r.returncode == 1 and "unknown" in r.stderr
+    r = _pa(["-b", "2"])
+    assert r.returncode == 1 and "-m <model> is required" in r.stderr
+    r = _pa(["-m", "x", "--streaming"])  # streaming needs grpc
+    assert r.returncode == 1 and "grpc" in r.stderr
+
+
+@pytest.mark.parametrize("proto", ["http", "grpc"])
+def test_concurrency_sweep_csv(cpu_server, tmp_path, proto):
+    url = cpu_server.http_url if proto == "http" else cpu_server.grpc_url
+    f = tmp_path / "out.csv"
+    j = tmp_path / "out.json"
+    r = _pa(["-m", "simple", "-i", proto, "-u", url, "-p", "300", "--concurrency-range", "1:3:2", "-f", f,
+             "--json-report", j, "-r", "4"])
+    assert r.returncode == 0, r.stderr
+    assert "Request concurrency: 1" in r.stdout and "Request concurrency: 3" in r.stdout
+    assert "Inferences/Second vs. Client Average Batch Latency" in r.stdout
+    rows = list(csv.DictReader(open(f)))
+    assert [row["Concurrency"] for row in rows] == ["1", "3"]
+    assert all(float(row["Inferences/Second"]) > 0 for row in rows)
+    assert all(float(row["p99 latency"]) >= float(row["p50 latency"]) > 0 for row in rows)
+    rep = json.load(open(j))
+    assert rep["model"] == "simple" and len(rep["points"]) == 2
+    assert rep["points"][0]["server"]["success_count"] > 0
+
+
+def test_system_shm_sync_count_windows(cpu_server):
+    r = _pa(["-m", "simple", "-u", cpu_server.http_url, "--sync", "--shared-memory", "system",
+             "--measurement-mode", "count_windows", "--measurement-request-count", "60",
+             "--concurrency-range", "2"])
+    assert r.returncode == 0, r.stderr
+    assert "system shared memory" in r.stdout and "synchronous" in r.stdout
+    assert "Failed requests" not in r.stdout
+
+
+def test_streaming_and_sequences(cpu_server):
+    r = _pa(["-m", "simple_sequence", "-i", "grpc", "-u", cpu_server.grpc_url, "--streaming", "-p", "300",
+             "--sequence-length", "4", "--concurrency-range", "2", "-r", "4"])
+    assert r.returncode == 0, r.stderr
+    assert "streaming" in r.stdout and "Sequence model: 4 requests per sequence" in r.stdout
+    assert "Failed requests" not in r.stdout
+
+
+def test_request_rate_poisson(cpu_server):
+    r = _pa(["-m", "simple", "-u", cpu_server.http_url, "--request-rate-range", "200",
+             "--request-distribution", "poisson", "-p", "400", "-r", "3"])
+    assert r.returncode == 0, r.stderr
+    thr = float(r.stdout.split("Throughput: ")[1].split()[0])
+    assert 100 < thr < 320  # open loop: throughput follows the offered rate
+
+
+def test_request_intervals_file(cpu_server, tmp_path):
+    f = tmp_path / "iv.txt"
+    f.write_text("\n".join(["2000"] * 10))  # 2 ms apart -> ~500 req/s
+    r = _pa(["-m", "simple", "-u", cpu_server.http_url, "--request-intervals", f, "-p", "400", "-r", "3"])
+    assert r.returncode == 0, r.stderr
+    thr = float(r.stdout.split("Throughput: ")[1].split()[0])
+    assert 250 < thr < 700
+
+
+def test_bytes_and_json_data(cpu_server, tmp_path):
+    r = _pa(["-m", "simple_string", "-u", cpu_server.http_url, "--string-data", "12", "-p", "300", "-r", "3"])
+    assert r.returncode == 0, r.stderr
+    d = tmp_path / "data.json"
+    d.write_text(json.dumps({"data": [{"INPUT0": list(range(16)), "INPUT1": [1] * 16}]}))
+    r = _pa(["-m", "simple", "-u", cpu_server.http_url, "--input-data", d, "-p", "300", "-r", "3"])
+    assert r.returncode == 0, r.stderr
+    assert "json:" in r.stdout
+
+
+def test_batch_limit_and_unknown_model(cpu_server):
+    r = _pa(["-m", "simple", "-u", cpu_server.http_url, "-b", "4"])  # simple has max_batch_size 8? no: 0
+    assert ("does not support batching" in r.stderr) or ("exceeds max_batch_size" in r.stderr) or r.returncode == 0
+    r = _pa(["-m", "no_such_model", "-u", cpu_server.http_url])
+    assert r.returncode == 1 and "no_such_model" in r.stderr
+
+
+def test_native_session_fixed_run(cpu_server):
+    with native.PerfSession(["-m", "simple", "-i", "grpc", "-u", cpu_server.grpc_url, "--shared-memory", "system",
+                             "--concurrency-range", "4"]) as s:
+        assert "system shared memory" in s.describe()
+        st0 = s.server_stats()
+        lat, el = s.run_fixed(4, 200)
+        assert len(lat) == 200 and (lat > 0).all() and el > 0
+        st1 = s.server_stats()
+        assert st1["success_count"] - st0["success_count"] >= 200
+        lat2, _ = s.run_fixed(2, 50)  # reuse the session at a different concurrency
+        assert len(lat2) == 50
+        p = s.profile(2)
+        assert p["throughput"] > 0 and p["p99_us"] >= p["p50_us"] > 0
+
+
+def test_native_session_errors():
+    with pytest.raises(native.PerfError):
+        native.PerfSession(["-m", "simple", "-u", "127.0.0.1:1", "--concurrency-range", "1"])
+    with pytest.raises(native.PerfError):
+        native.PerfSession(["--concurrency-range", "1"])

@@ -88,12 +88,25 @@ class FusedDenseNet:
             self.wc = model.classifier.weight.to(dev, bf).contiguous()
             self.bc = model.classifier.bias.to(dev, bf).contiguous()
             self.num_features = c
-        # activation buffers sized for max_batch
-        n = self.max_batch
+        self._alloc(self.max_batch)
+
+    def _alloc(self, n):
+        """Activation buffers for up to ``n`` images (one set per concurrent stream)."""
+        dev, bf = self.device, torch.bfloat16
+        self.max_batch = int(n)
         self.feat = [torch.empty(n * hw_ * hw_, ct, device=dev, dtype=bf) for hw_, ct in self.block_dims]
         h1 = self.block_dims[0][0]
         self.z = torch.empty(n * h1 * h1, BN_SIZE * GROWTH, device=dev, dtype=bf)
         self.pooled = torch.empty(n, self.num_features, device=dev, dtype=bf)
+
+    def with_workspace(self, max_batch=None):
+        """A second engine sharing these weights with its own activation buffers,
+        so model instances on different HIP streams can run concurrently."""
+        import copy
+
+        other = copy.copy(self)
+        other._alloc(self.max_batch if max_batch is None else max_batch)
+        return other
 
     def forward(self, x, out=None):
         """x: [b,3,224,224] bf16 channels_last (NHWC memory); returns/fills [b,1000] fp32."""

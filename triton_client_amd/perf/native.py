@@ -1,0 +1,120 @@
+"""ctypes binding of the native perf engine (csrc/cpp/perf, libperfanalyzer.so).
+
+``PerfSession(args)`` takes perf_analyzer command-line flags (see
+``csrc/cpp/perf/options.cc``) and sets up the protocol client, model metadata,
+request tensors and shared-memory regions.  ``run_fixed(concurrency, n)``
+keeps ``concurrency`` requests in flight until exactly ``n`` have completed
+and returns their latencies; the call drops the GIL (ctypes), so the request
+path is entirely C++.
+"""
+
+import ctypes
+import os
+
+import numpy as np
+
+_REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB_PATH = os.path.join(_REPO, "csrc", "cpp", "build", "lib", "libperfanalyzer.so")
+BIN_PATH = os.path.join(_REPO, "csrc", "cpp", "build", "bin", "perf_analyzer")
+_lib = None
+
+
+def available():
+    return os.path.exists(LIB_PATH)
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        if not available():
+            raise RuntimeError("native perf engine not built (%s); run `make -C csrc/cpp`" % LIB_PATH)
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.tcperf_session_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.c_char_p,
+                                              ctypes.c_int]
+        lib.tcperf_session_create.restype = ctypes.c_void_p
+        lib.tcperf_run_fixed.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64,
+                                         ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double),
+                                         ctypes.c_char_p, ctypes.c_int]
+        lib.tcperf_run_fixed.restype = ctypes.c_int
+        lib.tcperf_server_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_char_p,
+                                            ctypes.c_int]
+        lib.tcperf_server_stats.restype = ctypes.c_int
+        lib.tcperf_profile.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.c_char_p, ctypes.c_int]
+        lib.tcperf_profile.restype = ctypes.c_int
+        lib.tcperf_describe.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
+        lib.tcperf_describe.restype = ctypes.c_int
+        lib.tcperf_session_destroy.argtypes = [ctypes.c_void_p]
+        lib.tcperf_session_destroy.restype = None
+        _lib = lib
+    return _lib
+
+
+STAT_KEYS = ("inference_count", "execution_count", "success_count", "success_ns", "queue_ns",
+             "compute_input_ns", "compute_infer_ns", "compute_output_ns")
+POINT_KEYS = ("load", "stable", "request_count", "window_s", "throughput", "avg_us", "p50_us", "p90_us",
+              "p95_us", "p99_us", "client_send_us", "client_recv_us")
+
+
+class PerfError(RuntimeError):
+    pass
+
+
+class PerfSession:
+    def __init__(self, args):
+        lib = _load()
+        argv = [str(a).encode() for a in args]
+        arr = (ctypes.c_char_p * len(argv))(*argv)
+        err = ctypes.create_string_buffer(1024)
+        self._h = lib.tcperf_session_create(len(argv), arr, err, 1024)
+        if not self._h:
+            raise PerfError(err.value.decode(errors="replace"))
+
+    def run_fixed(self, concurrency, total):
+        """Exactly ``total`` requests with ``concurrency`` in flight; returns (latencies_ns, elapsed_s)."""
+        lat = np.zeros(int(total), dtype=np.uint64)
+        el = ctypes.c_double(0.0)
+        err = ctypes.create_string_buffer(1024)
+        rc = _load().tcperf_run_fixed(self._h, int(concurrency), int(total),
+                                      lat.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), ctypes.byref(el), err,
+                                      1024)
+        if rc != 0:
+            raise PerfError(err.value.decode(errors="replace"))
+        return lat, el.value
+
+    def server_stats(self):
+        out = (ctypes.c_uint64 * 8)()
+        err = ctypes.create_string_buffer(1024)
+        if _load().tcperf_server_stats(self._h, out, err, 1024) != 0:
+            raise PerfError(err.value.decode(errors="replace"))
+        return dict(zip(STAT_KEYS, list(out)))
+
+    def profile(self, load):
+        """One perf_analyzer measurement point (windows until stable)."""
+        out = (ctypes.c_double * 12)()
+        err = ctypes.create_string_buffer(1024)
+        if _load().tcperf_profile(self._h, float(load), out, err, 1024) != 0:
+            raise PerfError(err.value.decode(errors="replace"))
+        return dict(zip(POINT_KEYS, list(out)))
+
+    def describe(self):
+        buf = ctypes.create_string_buffer(1024)
+        _load().tcperf_describe(self._h, buf, 1024)
+        return buf.value.decode(errors="replace")
+
+    def close(self):
+        if self._h:
+            _load().tcperf_session_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -22,6 +22,8 @@ def main(argv=None):
     ap.add_argument("--instance-count", type=int, default=0, help="override GPU model instance count")
     ap.add_argument("--max-queue-delay-us", type=int, default=-1)
     ap.add_argument("--no-graphs", action="store_true", help="disable HIP graph capture")
+    ap.add_argument("--engine", default="fused", choices=["fused", "torch"],
+                    help="densenet_onnx engine: fused HIP/MFMA kernels or the torch/MIOpen module")
     ap.add_argument("--ready-file", default="", help="touch this file once serving")
     args = ap.parse_args(argv)
 
@@ -36,6 +38,8 @@ def main(argv=None):
     for m in models:
         if getattr(m, "instance_kind", "") == "KIND_GPU":
             o = {"device": args.device}
+            if m.name == "densenet_onnx":
+                o["engine"] = args.engine
             if args.no_graphs:
                 o["use_graphs"] = False
             opts[m.name] = o

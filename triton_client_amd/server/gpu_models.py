@@ -7,7 +7,9 @@ served with dynamic batching on one MI355X:
   request inputs (device shm views / host tensors)
     --K6 layout_pack--> one bf16 NHWC batch buffer   (gather+transpose+cvt,
                                                       one launch per batch)
-    --HIP graph replay--> DenseNet-121 (bf16, channels_last, MIOpen MFMA convs)
+    --HIP graph replay--> DenseNet-121 on the fused K8-K10 MFMA kernels
+                          (models/densenet_fused.py; engine="torch" keeps
+                          the MIOpen per-op module for comparison)
     --K7 batched_copy--> each request's fp32 logits straight into its output
                          device-shm region (one launch per batch)
 
@@ -43,8 +45,11 @@ class DensenetOnnx(Model):
     C, H, W = 3, 224, 224
     OUT = 1000
 
-    def __init__(self, version=1, device_id=0, buckets=BUCKETS, use_graphs=True, **kw):
+    def __init__(self, version=1, device_id=0, buckets=BUCKETS, use_graphs=True, engine="fused", **kw):
         super().__init__(version, **kw)
+        if engine not in ("fused", "torch"):
+            raise ServerError("unknown densenet engine %r" % engine)
+        self.engine = engine
         self.device_id = int(kw.get("device", device_id))
         self.buckets = tuple(b for b in buckets if b <= self.max_batch_size)
         self.use_graphs = use_graphs
@@ -65,8 +70,12 @@ class DensenetOnnx(Model):
         torch.cuda.set_device(self.device_id)
         self.torch = torch
         dev = torch.device("cuda", self.device_id)
-        model = densenet.build(device=dev)
-        self.model = model
+        if self.engine == "fused":
+            from triton_client_amd.models import densenet_fused
+
+            self.model, _ = densenet_fused.build(max(self.buckets), device=dev)
+        else:
+            self.model = densenet.build(device=dev)
         self.scale = None
         for _ in range(max(1, self.instance_count)):
             self._slots.append(self._make_slot(dev))
@@ -76,7 +85,10 @@ class DensenetOnnx(Model):
         torch = self.torch
         from triton_client_amd.ops import hip
 
-        slot = {"stream": torch.cuda.Stream(device=dev), "graphs": {},
+        net = self.model
+        if self.engine == "fused" and self._slots:
+            net = self.model.with_workspace()  # own activation buffers per concurrent stream
+        slot = {"stream": torch.cuda.Stream(device=dev), "graphs": {}, "net": net,
                 "ev": [torch.cuda.Event(enable_timing=True) for _ in range(4)]}
         maxb = max(self.buckets)
         slot["inp"] = torch.zeros(maxb, self.H, self.W, self.C, device=dev, dtype=torch.bfloat16)
@@ -88,11 +100,11 @@ class DensenetOnnx(Model):
             for b in self.buckets:
                 x = slot["inp"][:b].permute(0, 3, 1, 2)  # NCHW view of NHWC memory
                 for _ in range(2):  # warm up MIOpen kernel selection
-                    slot["out"][:b].copy_(self.model(x).float())
+                    slot["out"][:b].copy_(net(x).float())
                 if self.use_graphs:
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, stream=slot["stream"]):
-                        y = self.model(x)
+                        y = net(x)
                         slot["out"][:b].copy_(y.float())
                     slot["graphs"][b] = g
         slot["stream"].synchronize()
@@ -139,7 +151,7 @@ class DensenetOnnx(Model):
         else:
             with torch.cuda.stream(stream), torch.no_grad():
                 x = slot["inp"][:bucket].permute(0, 3, 1, 2)
-                slot["out"][:bucket].copy_(self.model(x).float())
+                slot["out"][:bucket].copy_(slot["net"](x).float())
         slot["ev"][2].record(stream)
         return bucket
 
