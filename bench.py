@@ -127,7 +127,7 @@ def main():
 
             def run(steps):
                 lat_ns, el = perf.run_fixed(conc, steps * conc)
-                return list(lat_ns / 1e9), []
+                return lat_ns.astype(np.float64), []
         else:
             outs = []
             for s in range(conc):

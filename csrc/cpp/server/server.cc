@@ -1,0 +1,1332 @@
+// tcserve implementation: HTTP/2 server transport, proxy to the Python
+// grpc.aio server, native ModelInfer fast path with a dynamic batcher.
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <nghttp2/nghttp2.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "grpc_service.pb.h"
+#include "h2.h"
+#include "net.h"
+#include "tcserve.h"
+
+namespace tcserve {
+
+namespace tc = triton::client;
+
+static uint64_t NowNs()
+{
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+static const char kInferPath[] = "/inference.GRPCInferenceService/ModelInfer";
+
+// gRPC status codes used here
+enum { kOk = 0, kInvalidArgument = 3, kNotFound = 5, kInternal = 13, kUnavailable = 14 };
+
+class Server;
+class Loop;
+
+// ---------------------------------------------------------------------------
+struct Stream {
+  int32_t id = 0;
+  std::string path;
+  std::vector<std::pair<std::string, std::string>> meta;
+  std::string inbuf;
+  bool end_stream = false;
+  bool started = false;        // dispatched (unary) / upstream opened (streaming)
+  bool streaming_rpc = false;
+  // response
+  bool response_submitted = false;
+  std::deque<std::string> out;  // framed messages
+  size_t out_pos = 0;
+  bool finish = false;          // send trailers once `out` drains
+  int status = 0;
+  std::string message;
+  bool trailers_sent = false;
+  bool deferred = false;
+  std::shared_ptr<tc::H2Call> upstream;
+};
+
+struct Conn {
+  uint64_t id = 0;
+  int fd = -1;
+  Loop* loop = nullptr;
+  nghttp2_session* s = nullptr;
+  std::unordered_map<int32_t, std::unique_ptr<Stream>> streams;
+  std::string sendbuf;
+  size_t sendpos = 0;
+  bool closing = false;
+  bool want_write = false;
+};
+
+// ---------------------------------------------------------------------------
+// Native models
+// ---------------------------------------------------------------------------
+struct TensorDef {
+  std::string name, dtype;
+  std::vector<int64_t> dims;
+  size_t sample_bytes = 0;
+};
+
+struct PendingReq {
+  uint64_t conn_id;
+  Loop* loop;
+  int32_t stream_id;
+  std::string id;
+  int32_t rows;
+  std::vector<tcserve_ref> in;    // [n_inputs]
+  std::vector<tcserve_ref> out;   // [n_outputs] (ptr 0: not requested / host)
+  std::vector<bool> out_requested;
+  std::vector<bool> out_shm;
+  std::vector<std::string> out_region;
+  std::vector<int64_t> out_region_bytes, out_region_offset;
+  std::vector<std::string> host_out;  // host output buffers (non-shm)
+  std::vector<std::string> host_in;   // raw_input_contents kept alive
+  uint64_t t_arrive = 0;
+};
+
+struct Stat {
+  uint64_t count = 0, ns = 0;
+};
+
+struct BatchStat {
+  uint64_t count = 0, in_ns = 0, infer_ns = 0, out_ns = 0;
+};
+
+struct NativeModel {
+  std::string name, version;
+  int max_batch = 0;
+  uint64_t delay_ns = 0;
+  int instances = 1;
+  std::vector<TensorDef> inputs, outputs;
+  tcserve_exec_fn fn = nullptr;
+  void* user = nullptr;
+  // batcher
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::unique_ptr<PendingReq>> q;
+  int q_rows = 0;
+  bool stopping = false;
+  std::vector<std::thread> workers;
+  // stats
+  std::mutex smu;
+  uint64_t inference_count = 0, execution_count = 0, last_inference_ms = 0;
+  Stat success, fail, queue, cin, cinf, cout;
+  std::map<int, BatchStat> batch;
+};
+
+static size_t DtypeSize(const std::string& dt)
+{
+  if (dt == "BOOL" || dt == "INT8" || dt == "UINT8") return 1;
+  if (dt == "INT16" || dt == "UINT16" || dt == "FP16" || dt == "BF16") return 2;
+  if (dt == "INT32" || dt == "UINT32" || dt == "FP32") return 4;
+  if (dt == "INT64" || dt == "UINT64" || dt == "FP64") return 8;
+  return 0;
+}
+
+struct ShmEntry {
+  uint64_t ptr = 0, bytes = 0;
+  int device = 0;
+};
+
+// ---------------------------------------------------------------------------
+class Loop {
+ public:
+  Loop(Server* srv, int idx) : srv_(srv), idx_(idx) {}
+  bool Start(std::string* err);
+  void Stop();
+  void Post(std::function<void()> fn);
+  void AddConn(int fd);
+  Conn* Find(uint64_t id)
+  {
+    auto it = conns_.find(id);
+    return it == conns_.end() ? nullptr : it->second.get();
+  }
+  void Flush(Conn* c);
+  void Close(Conn* c);
+  int idx() const { return idx_; }
+  Server* srv() { return srv_; }
+  int listen_fd = -1;  // only loop 0 accepts
+
+ private:
+  void Run();
+  void OnReadable(Conn* c);
+  void DoAccept();
+  Server* srv_;
+  int idx_;
+  int ep_ = -1, ev_ = -1;
+  std::thread th_;
+  std::atomic<bool> stop_{false};
+  std::mutex mu_;
+  std::deque<std::function<void()>> tasks_;
+  std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns_;
+};
+
+class Server {
+ public:
+  ~Server();
+  bool Start(const std::string& host, int port, const std::string& up_host, int up_port, int io_threads,
+             std::string* err);
+  int port() const { return port_; }
+
+  // transport hooks (loop thread)
+  void OnRequestComplete(Conn* c, Stream* st);
+  void OnStreamMessage(Conn* c, Stream* st, std::string&& msg);
+  void OnStreamEnd(Conn* c, Stream* st);
+  void OnStreamClosed(Conn* c, Stream* st);
+
+  // response helpers (loop thread)
+  void Reply(Conn* c, Stream* st, std::string* msg, int status, const std::string& message);
+  void PostReply(Loop* loop, uint64_t conn_id, int32_t stream_id, std::string&& msg, int status,
+                 const std::string& message);
+
+  // native models / shm mirror
+  int AddModel(std::unique_ptr<NativeModel> m, std::string* err);
+  int RemoveModel(const std::string& name);
+  void ShmAdd(int kind, const std::string& name, const ShmEntry& e);
+  void ShmRemove(int kind, const std::string& name);
+  NativeModel* FindModel(const std::string& name);
+  std::mutex models_mu;
+  std::map<std::string, std::shared_ptr<NativeModel>> models;
+  std::atomic<uint64_t> n_native{0}, n_proxied{0}, n_conns{0};
+
+  std::vector<std::unique_ptr<Loop>> loops;
+  std::atomic<uint64_t> next_conn_id{1};
+  std::atomic<int> next_loop{0};
+
+ private:
+  bool TryNative(Conn* c, Stream* st, const std::string& raw);
+  void Proxy(Conn* c, Stream* st, bool streaming);
+  std::shared_ptr<tc::H2Channel> Upstream();
+  void Worker(std::shared_ptr<NativeModel> m, int instance);
+  void Execute(NativeModel* m, int instance, std::vector<std::unique_ptr<PendingReq>>& batch);
+
+  int port_ = 0;
+  std::string up_host_;
+  int up_port_ = 0;
+  std::mutex up_mu_;
+  std::vector<std::shared_ptr<tc::H2Channel>> up_;
+  std::atomic<uint32_t> up_rr_{0};
+  std::mutex shm_mu_;
+  std::map<std::string, ShmEntry> shm_[2];
+};
+
+// ---------------------------------------------------------------------------
+// nghttp2 server callbacks
+// ---------------------------------------------------------------------------
+static ssize_t ReadCb(nghttp2_session* session, int32_t stream_id, uint8_t* buf, size_t length, uint32_t* flags,
+                      nghttp2_data_source* source, void* user)
+{
+  Conn* c = static_cast<Conn*>(user);
+  auto it = c->streams.find(stream_id);
+  if (it == c->streams.end()) {
+    *flags |= NGHTTP2_DATA_FLAG_EOF;
+    return 0;
+  }
+  Stream* st = it->second.get();
+  size_t n = 0;
+  while (n < length && !st->out.empty()) {
+    std::string& f = st->out.front();
+    size_t take = std::min(length - n, f.size() - st->out_pos);
+    memcpy(buf + n, f.data() + st->out_pos, take);
+    n += take;
+    st->out_pos += take;
+    if (st->out_pos == f.size()) {
+      st->out.pop_front();
+      st->out_pos = 0;
+    }
+  }
+  if (st->out.empty() && st->finish) {
+    *flags |= NGHTTP2_DATA_FLAG_EOF;
+    if (!st->trailers_sent) {
+      *flags |= NGHTTP2_DATA_FLAG_NO_END_STREAM;
+      std::string code = std::to_string(st->status);
+      std::vector<nghttp2_nv> nv;
+      auto mk = [](const std::string& k, const std::string& v) {
+        nghttp2_nv x;
+        x.name = (uint8_t*)k.data();
+        x.value = (uint8_t*)v.data();
+        x.namelen = k.size();
+        x.valuelen = v.size();
+        x.flags = NGHTTP2_NV_FLAG_NONE;
+        return x;
+      };
+      static const std::string kStatus = "grpc-status", kMsg = "grpc-message";
+      std::string msg = tc::UrlEncode(st->message);
+      nv.push_back(mk(kStatus, code));
+      if (!st->message.empty()) nv.push_back(mk(kMsg, msg));
+      nghttp2_submit_trailer(session, stream_id, nv.data(), nv.size());  // copies nv
+      st->trailers_sent = true;
+    }
+    return static_cast<ssize_t>(n);
+  }
+  if (n == 0) {
+    st->deferred = true;
+    return NGHTTP2_ERR_DEFERRED;
+  }
+  return static_cast<ssize_t>(n);
+}
+
+static int OnBeginHeaders(nghttp2_session*, const nghttp2_frame* frame, void* user)
+{
+  Conn* c = static_cast<Conn*>(user);
+  if (frame->hd.type == NGHTTP2_HEADERS && frame->headers.cat == NGHTTP2_HCAT_REQUEST) {
+    std::unique_ptr<Stream> st(new Stream());
+    st->id = frame->hd.stream_id;
+    c->streams[st->id] = std::move(st);
+  }
+  return 0;
+}
+
+static int OnHeader(nghttp2_session*, const nghttp2_frame* frame, const uint8_t* name, size_t namelen,
+                    const uint8_t* value, size_t valuelen, uint8_t, void* user)
+{
+  Conn* c = static_cast<Conn*>(user);
+  auto it = c->streams.find(frame->hd.stream_id);
+  if (it == c->streams.end()) return 0;
+  std::string k(reinterpret_cast<const char*>(name), namelen), v(reinterpret_cast<const char*>(value), valuelen);
+  if (k == ":path") {
+    it->second->path = v;
+    it->second->streaming_rpc = v == "/inference.GRPCInferenceService/ModelStreamInfer";
+  } else if (!k.empty() && k[0] != ':' && k != "content-type" && k != "te" && k != "grpc-accept-encoding" &&
+             k != "user-agent" && k != "grpc-timeout" && k != "content-length") {
+    it->second->meta.emplace_back(k, v);
+  }
+  return 0;
+}
+
+// Pop complete gRPC messages off the stream's input buffer.
+static bool PopMessages(Stream* st, std::vector<std::string>* msgs, std::string* err)
+{
+  size_t pos = 0;
+  bool gz = false;
+  for (const auto& kv : st->meta)
+    if (kv.first == "grpc-encoding" && kv.second != "identity") gz = true;
+  while (st->inbuf.size() - pos >= 5) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(st->inbuf.data() + pos);
+    const uint32_t n = (uint32_t(p[1]) << 24) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 8) | p[4];
+    if (st->inbuf.size() - pos - 5 < n) break;
+    if (p[0] && gz) {
+      std::string dec;
+      if (!tc::Decompress(st->inbuf.substr(pos + 5, n), &dec)) {
+        *err = "failed to decompress request message";
+        return false;
+      }
+      msgs->push_back(std::move(dec));
+    } else {
+      msgs->emplace_back(st->inbuf.data() + pos + 5, n);
+    }
+    pos += 5 + n;
+  }
+  st->inbuf.erase(0, pos);
+  return true;
+}
+
+static int OnDataChunk(nghttp2_session*, uint8_t, int32_t stream_id, const uint8_t* data, size_t len, void* user)
+{
+  Conn* c = static_cast<Conn*>(user);
+  auto it = c->streams.find(stream_id);
+  if (it == c->streams.end()) return 0;
+  Stream* st = it->second.get();
+  st->inbuf.append(reinterpret_cast<const char*>(data), len);
+  if (st->streaming_rpc) {
+    std::vector<std::string> msgs;
+    std::string err;
+    if (!PopMessages(st, &msgs, &err)) return 0;
+    for (auto& m : msgs) c->loop->srv()->OnStreamMessage(c, st, std::move(m));
+  }
+  return 0;
+}
+
+static int OnFrameRecv(nghttp2_session*, const nghttp2_frame* frame, void* user)
+{
+  Conn* c = static_cast<Conn*>(user);
+  if (frame->hd.type != NGHTTP2_HEADERS && frame->hd.type != NGHTTP2_DATA) return 0;
+  auto it = c->streams.find(frame->hd.stream_id);
+  if (it == c->streams.end()) return 0;
+  Stream* st = it->second.get();
+  if (frame->hd.type == NGHTTP2_HEADERS && st->streaming_rpc && !st->started) {
+    c->loop->srv()->OnStreamMessage(c, st, std::string());  // opens the upstream call (empty = open only)
+  }
+  if (frame->hd.flags & NGHTTP2_FLAG_END_STREAM) {
+    st->end_stream = true;
+    if (st->streaming_rpc) c->loop->srv()->OnStreamEnd(c, st);
+    else c->loop->srv()->OnRequestComplete(c, st);
+  }
+  return 0;
+}
+
+static int OnStreamClose(nghttp2_session*, int32_t stream_id, uint32_t, void* user)
+{
+  Conn* c = static_cast<Conn*>(user);
+  auto it = c->streams.find(stream_id);
+  if (it == c->streams.end()) return 0;
+  c->loop->srv()->OnStreamClosed(c, it->second.get());
+  c->streams.erase(it);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Loop
+// ---------------------------------------------------------------------------
+bool Loop::Start(std::string* err)
+{
+  ep_ = epoll_create1(EPOLL_CLOEXEC);
+  ev_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  if (ep_ < 0 || ev_ < 0) {
+    *err = "epoll/eventfd failed";
+    return false;
+  }
+  epoll_event e{};
+  e.events = EPOLLIN;
+  e.data.u64 = 0;  // 0 = eventfd
+  epoll_ctl(ep_, EPOLL_CTL_ADD, ev_, &e);
+  if (listen_fd >= 0) {
+    e.events = EPOLLIN;
+    e.data.u64 = 1;  // 1 = listen socket
+    epoll_ctl(ep_, EPOLL_CTL_ADD, listen_fd, &e);
+  }
+  th_ = std::thread(&Loop::Run, this);
+  return true;
+}
+
+void Loop::Stop()
+{
+  stop_ = true;
+  uint64_t one = 1;
+  if (ev_ >= 0) (void)!write(ev_, &one, 8);
+  if (th_.joinable()) th_.join();
+  for (auto& kv : conns_) {
+    if (kv.second->s) nghttp2_session_del(kv.second->s);
+    close(kv.second->fd);
+  }
+  conns_.clear();
+  if (ep_ >= 0) close(ep_);
+  if (ev_ >= 0) close(ev_);
+}
+
+void Loop::Post(std::function<void()> fn)
+{
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    tasks_.push_back(std::move(fn));
+  }
+  uint64_t one = 1;
+  (void)!write(ev_, &one, 8);
+}
+
+void Loop::AddConn(int fd)
+{
+  std::unique_ptr<Conn> c(new Conn());
+  c->id = srv_->next_conn_id++;
+  c->fd = fd;
+  c->loop = this;
+  nghttp2_session_callbacks* cbs;
+  nghttp2_session_callbacks_new(&cbs);
+  nghttp2_session_callbacks_set_on_begin_headers_callback(cbs, OnBeginHeaders);
+  nghttp2_session_callbacks_set_on_header_callback(cbs, OnHeader);
+  nghttp2_session_callbacks_set_on_data_chunk_recv_callback(cbs, OnDataChunk);
+  nghttp2_session_callbacks_set_on_frame_recv_callback(cbs, OnFrameRecv);
+  nghttp2_session_callbacks_set_on_stream_close_callback(cbs, OnStreamClose);
+  nghttp2_session_server_new(&c->s, cbs, c.get());
+  nghttp2_session_callbacks_del(cbs);
+  nghttp2_settings_entry iv[3] = {{NGHTTP2_SETTINGS_MAX_CONCURRENT_STREAMS, 4096},
+                                  {NGHTTP2_SETTINGS_INITIAL_WINDOW_SIZE, (1u << 31) - 1},
+                                  {NGHTTP2_SETTINGS_MAX_FRAME_SIZE, 1u << 20}};
+  nghttp2_submit_settings(c->s, NGHTTP2_FLAG_NONE, iv, 3);
+  nghttp2_session_set_local_window_size(c->s, NGHTTP2_FLAG_NONE, 0, (1 << 30));
+  epoll_event e{};
+  e.events = EPOLLIN;
+  e.data.u64 = c->id + 16;  // ids below 16 are reserved
+  epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &e);
+  Conn* raw = c.get();
+  conns_[c->id] = std::move(c);
+  srv_->n_conns++;
+  Flush(raw);
+}
+
+void Loop::Close(Conn* c)
+{
+  epoll_ctl(ep_, EPOLL_CTL_DEL, c->fd, nullptr);
+  for (auto& kv : c->streams) srv_->OnStreamClosed(c, kv.second.get());
+  c->streams.clear();
+  nghttp2_session_del(c->s);
+  close(c->fd);
+  conns_.erase(c->id);
+}
+
+void Loop::Flush(Conn* c)
+{
+  while (true) {
+    if (c->sendpos == c->sendbuf.size()) {
+      c->sendbuf.clear();
+      c->sendpos = 0;
+      const uint8_t* data;
+      ssize_t n;
+      while ((n = nghttp2_session_mem_send(c->s, &data)) > 0) {
+        c->sendbuf.append(reinterpret_cast<const char*>(data), n);
+        if (c->sendbuf.size() > (1 << 20)) break;
+      }
+      if (n < 0) {
+        c->closing = true;
+        break;
+      }
+      if (c->sendbuf.empty()) break;
+    }
+    ssize_t w = send(c->fd, c->sendbuf.data() + c->sendpos, c->sendbuf.size() - c->sendpos, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+      if (errno == EINTR) continue;
+      c->closing = true;
+      break;
+    }
+    c->sendpos += w;
+  }
+  const bool pending = c->sendpos < c->sendbuf.size();
+  if (pending != c->want_write && !c->closing) {
+    epoll_event e{};
+    e.events = EPOLLIN | (pending ? EPOLLOUT : 0);
+    e.data.u64 = c->id + 16;
+    epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &e);
+    c->want_write = pending;
+  }
+  if (c->closing ||
+      (!nghttp2_session_want_read(c->s) && !nghttp2_session_want_write(c->s) && !pending)) {
+    Close(c);
+  }
+}
+
+void Loop::OnReadable(Conn* c)
+{
+  uint8_t buf[65536];
+  while (true) {
+    ssize_t n = recv(c->fd, buf, sizeof(buf), 0);
+    if (n > 0) {
+      ssize_t r = nghttp2_session_mem_recv(c->s, buf, n);
+      if (r < 0) {
+        c->closing = true;
+        break;
+      }
+      continue;
+    }
+    if (n == 0) {
+      c->closing = true;
+      break;
+    }
+    if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+    if (errno == EINTR) continue;
+    c->closing = true;
+    break;
+  }
+  if (c->closing) {
+    Close(c);
+    return;
+  }
+  Flush(c);
+}
+
+void Loop::DoAccept()
+{
+  while (true) {
+    int fd = accept4(listen_fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+    if (fd < 0) break;
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    const int li = srv_->next_loop++ % static_cast<int>(srv_->loops.size());
+    Loop* l = srv_->loops[li].get();
+    if (l == this) AddConn(fd);
+    else l->Post([l, fd] { l->AddConn(fd); });
+  }
+}
+
+void Loop::Run()
+{
+  epoll_event evs[64];
+  while (!stop_) {
+    int n = epoll_wait(ep_, evs, 64, 200);
+    for (int i = 0; i < n; ++i) {
+      const uint64_t tag = evs[i].data.u64;
+      if (tag == 0) {
+        uint64_t v;
+        (void)!read(ev_, &v, 8);
+        std::deque<std::function<void()>> tasks;
+        {
+          std::lock_guard<std::mutex> lk(mu_);
+          tasks.swap(tasks_);
+        }
+        for (auto& t : tasks) t();
+      } else if (tag == 1) {
+        DoAccept();
+      } else {
+        Conn* c = Find(tag - 16);
+        if (!c) continue;
+        if (evs[i].events & (EPOLLERR | EPOLLHUP)) {
+          Close(c);
+          continue;
+        }
+        if (evs[i].events & EPOLLIN) {
+          OnReadable(c);
+          c = Find(tag - 16);
+        }
+        if (c && (evs[i].events & EPOLLOUT)) Flush(c);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Server
+// ---------------------------------------------------------------------------
+bool Server::Start(const std::string& host, int port, const std::string& up_host, int up_port, int io_threads,
+                   std::string* err)
+{
+  up_host_ = up_host;
+  up_port_ = up_port;
+  int fd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  int one = 1;
+  setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(port));
+  if (inet_pton(AF_INET, host.c_str(), &a.sin_addr) != 1) a.sin_addr.s_addr = htonl(INADDR_ANY);
+  if (bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 || listen(fd, 1024) != 0) {
+    *err = "cannot bind/listen on port " + std::to_string(port) + ": " + strerror(errno);
+    close(fd);
+    return false;
+  }
+  socklen_t al = sizeof(a);
+  getsockname(fd, reinterpret_cast<sockaddr*>(&a), &al);
+  port_ = ntohs(a.sin_port);
+  const int n = std::max(1, io_threads);
+  for (int i = 0; i < n; ++i) loops.emplace_back(new Loop(this, i));
+  loops[0]->listen_fd = fd;
+  for (auto& l : loops)
+    if (!l->Start(err)) return false;
+  return true;
+}
+
+Server::~Server()
+{
+  std::vector<std::shared_ptr<NativeModel>> ms;
+  {
+    std::lock_guard<std::mutex> lk(models_mu);
+    for (auto& kv : models) ms.push_back(kv.second);
+    models.clear();
+  }
+  for (auto& m : ms) {
+    {
+      std::lock_guard<std::mutex> lk(m->mu);
+      m->stopping = true;
+    }
+    m->cv.notify_all();
+    for (auto& t : m->workers)
+      if (t.joinable()) t.join();
+  }
+  for (auto& l : loops) l->Stop();
+  if (!loops.empty() && loops[0]->listen_fd >= 0) close(loops[0]->listen_fd);
+  loops.clear();
+  std::lock_guard<std::mutex> lk(up_mu_);
+  up_.clear();
+}
+
+std::shared_ptr<tc::H2Channel> Server::Upstream()
+{
+  std::lock_guard<std::mutex> lk(up_mu_);
+  if (up_.empty()) up_.resize(4);
+  const size_t i = up_rr_++ % up_.size();
+  if (!up_[i] || !up_[i]->Healthy()) {
+    std::string err;
+    tc::H2ChannelOptions o;
+    up_[i] = tc::H2Channel::Create(up_host_, up_port_, o, &err);
+  }
+  return up_[i];
+}
+
+void Server::Reply(Conn* c, Stream* st, std::string* msg, int status, const std::string& message)
+{
+  if (msg) {
+    std::string framed;
+    tc::GrpcFrame(*msg, tc::GrpcCompression::NONE, &framed);
+    st->out.push_back(std::move(framed));
+  }
+  if (status >= 0) {
+    st->finish = true;
+    st->status = status;
+    st->message = message;
+  }
+  if (!st->response_submitted) {
+    nghttp2_nv hdrs[2];
+    static const char s200[] = "200", ctype[] = "application/grpc";
+    hdrs[0] = {(uint8_t*)":status", (uint8_t*)s200, 7, 3, NGHTTP2_NV_FLAG_NONE};
+    hdrs[1] = {(uint8_t*)"content-type", (uint8_t*)ctype, 12, sizeof(ctype) - 1, NGHTTP2_NV_FLAG_NONE};
+    nghttp2_data_provider prd;
+    prd.source.ptr = nullptr;
+    prd.read_callback = ReadCb;
+    nghttp2_submit_response(c->s, st->id, hdrs, 2, &prd);
+    st->response_submitted = true;
+  } else if (st->deferred) {
+    st->deferred = false;
+    nghttp2_session_resume_data(c->s, st->id);
+  }
+}
+
+void Server::PostReply(Loop* loop, uint64_t conn_id, int32_t stream_id, std::string&& msg, int status,
+                       const std::string& message)
+{
+  auto m = std::make_shared<std::string>(std::move(msg));
+  loop->Post([this, loop, conn_id, stream_id, m, status, message] {
+    Conn* c = loop->Find(conn_id);
+    if (!c) return;
+    auto it = c->streams.find(stream_id);
+    if (it == c->streams.end()) return;
+    Reply(c, it->second.get(), status == kOk ? m.get() : nullptr, status, message);
+    loop->Flush(c);
+  });
+}
+
+void Server::OnRequestComplete(Conn* c, Stream* st)
+{
+  if (st->started) return;
+  st->started = true;
+  if (st->path == kInferPath) {
+    std::vector<std::string> msgs;
+    std::string err;
+    if (!PopMessages(st, &msgs, &err) || msgs.size() != 1) {
+      Reply(c, st, nullptr, kInternal, err.empty() ? "expected one request message" : err);
+      return;
+    }
+    if (TryNative(c, st, msgs[0])) return;
+    // not native: forward the message we already popped
+    st->inbuf.clear();
+    tc::GrpcFrame(msgs[0], tc::GrpcCompression::NONE, &st->inbuf);
+  }
+  Proxy(c, st, false);
+}
+
+void Server::Proxy(Conn* c, Stream* st, bool streaming)
+{
+  n_proxied++;
+  auto ch = Upstream();
+  if (!ch) {
+    Reply(c, st, nullptr, kUnavailable, "upstream server unavailable");
+    return;
+  }
+  Loop* loop = c->loop;
+  const uint64_t cid = c->id;
+  const int32_t sid = st->id;
+  tc::H2CallHandlers h;
+  h.on_message = [this, loop, cid, sid](std::string&& m) {
+    auto mm = std::make_shared<std::string>(std::move(m));
+    loop->Post([this, loop, cid, sid, mm] {
+      Conn* c2 = loop->Find(cid);
+      if (!c2) return;
+      auto it = c2->streams.find(sid);
+      if (it == c2->streams.end()) return;
+      Reply(c2, it->second.get(), mm.get(), -1, "");
+      loop->Flush(c2);
+    });
+  };
+  h.on_close = [this, loop, cid, sid](const tc::GrpcStatus& s) {
+    loop->Post([this, loop, cid, sid, s] {
+      Conn* c2 = loop->Find(cid);
+      if (!c2) return;
+      auto it = c2->streams.find(sid);
+      if (it == c2->streams.end()) return;
+      it->second->upstream.reset();
+      Reply(c2, it->second.get(), nullptr, s.code, s.message);
+      loop->Flush(c2);
+    });
+  };
+  st->upstream = ch->StartCall(st->path, st->meta, 0, tc::GrpcCompression::NONE, h);
+  if (!st->upstream) {
+    Reply(c, st, nullptr, kUnavailable, "upstream call failed");
+    return;
+  }
+  if (!streaming) {
+    std::vector<std::string> msgs;
+    std::string err;
+    if (!PopMessages(st, &msgs, &err)) {
+      st->upstream->Cancel();
+      return;
+    }
+    for (auto& m : msgs) st->upstream->Write(std::move(m));
+    st->upstream->WritesDone();
+  }
+}
+
+void Server::OnStreamMessage(Conn* c, Stream* st, std::string&& msg)
+{
+  if (!st->started) {
+    st->started = true;
+    Proxy(c, st, true);
+  }
+  if (!msg.empty() && st->upstream) st->upstream->Write(std::move(msg));
+}
+
+void Server::OnStreamEnd(Conn* c, Stream* st)
+{
+  if (!st->started) {
+    st->started = true;
+    Proxy(c, st, true);
+  }
+  if (st->upstream) st->upstream->WritesDone();
+}
+
+void Server::OnStreamClosed(Conn*, Stream* st)
+{
+  if (st->upstream) {
+    st->upstream->Cancel();
+    st->upstream.reset();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Native fast path
+// ---------------------------------------------------------------------------
+NativeModel* Server::FindModel(const std::string& name)
+{
+  std::lock_guard<std::mutex> lk(models_mu);
+  auto it = models.find(name);
+  return it == models.end() ? nullptr : it->second.get();
+}
+
+bool Server::TryNative(Conn* c, Stream* st, const std::string& raw)
+{
+  inference::ModelInferRequest req;
+  if (!req.ParseFromString(raw)) return false;
+  std::shared_ptr<NativeModel> m;
+  {
+    std::lock_guard<std::mutex> lk(models_mu);
+    auto it = models.find(req.model_name());
+    if (it == models.end()) return false;
+    m = it->second;
+  }
+  if (!req.model_version().empty() && req.model_version() != m->version) return false;
+  // features the fast path leaves to the Python server
+  for (const auto& kv : req.parameters())
+    if (kv.first != "triton_enable_empty_final_response" && kv.first != "priority" && kv.first != "timeout")
+      return false;
+  if (req.inputs_size() != static_cast<int>(m->inputs.size())) return false;
+  std::unique_ptr<PendingReq> pr(new PendingReq());
+  pr->conn_id = c->id;
+  pr->loop = c->loop;
+  pr->stream_id = st->id;
+  pr->id = req.id();
+  pr->t_arrive = NowNs();
+  pr->in.resize(m->inputs.size());
+  pr->rows = -1;
+  int raw_idx = 0;
+  auto fail = [&](const std::string& msg) {
+    Reply(c, st, nullptr, kInvalidArgument, msg);
+    std::lock_guard<std::mutex> lk(m->smu);
+    m->fail.count++;
+    m->fail.ns += NowNs() - pr->t_arrive;
+    return true;
+  };
+  for (int i = 0; i < req.inputs_size(); ++i) {
+    const auto& t = req.inputs(i);
+    int idx = -1;
+    for (size_t k = 0; k < m->inputs.size(); ++k)
+      if (m->inputs[k].name == t.name()) idx = static_cast<int>(k);
+    if (idx < 0) return false;
+    const TensorDef& d = m->inputs[idx];
+    if (t.datatype() != d.dtype || t.has_contents()) return false;
+    const auto& shape = t.shape();
+    if (shape.size() != d.dims.size() + (m->max_batch > 0 ? 1 : 0)) return false;
+    int rows = 1;
+    size_t off = 0;
+    if (m->max_batch > 0) {
+      rows = static_cast<int>(shape[0]);
+      off = 1;
+    }
+    for (size_t k = 0; k < d.dims.size(); ++k)
+      if (shape[k + off] != d.dims[k]) return false;
+    if (rows < 1 || (m->max_batch > 0 && rows > m->max_batch)) return false;
+    if (pr->rows >= 0 && pr->rows != rows) return false;
+    pr->rows = rows;
+    const uint64_t need = static_cast<uint64_t>(rows) * d.sample_bytes;
+    std::string region;
+    int64_t rbytes = 0, roff = 0;
+    bool has_shm = false;
+    for (const auto& kv : t.parameters()) {
+      if (kv.first == "shared_memory_region") {
+        region = kv.second.string_param();
+        has_shm = true;
+      } else if (kv.first == "shared_memory_byte_size") {
+        rbytes = kv.second.int64_param();
+      } else if (kv.first == "shared_memory_offset") {
+        roff = kv.second.int64_param();
+      } else {
+        return false;
+      }
+    }
+    tcserve_ref& ref = pr->in[idx];
+    if (has_shm) {
+      ShmEntry e;
+      int kind = -1;
+      {
+        std::lock_guard<std::mutex> lk(shm_mu_);
+        for (int kk = 0; kk < 2 && kind < 0; ++kk) {
+          auto it = shm_[kk].find(region);
+          if (it != shm_[kk].end()) {
+            e = it->second;
+            kind = kk;
+          }
+        }
+      }
+      if (kind < 0) return fail("Unable to find shared memory region: '" + region + "'");
+      if (roff < 0 || static_cast<uint64_t>(roff + rbytes) > e.bytes)
+        return fail("Invalid offset + byte size for shared memory region: '" + region + "'");
+      if (static_cast<uint64_t>(rbytes) < need)
+        return fail("input '" + d.name + "' shared memory region is smaller than the tensor");
+      ref.kind = kind;
+      ref.device = e.device;
+      ref.ptr = e.ptr + roff;
+      ref.bytes = need;
+    } else {
+      if (raw_idx >= req.raw_input_contents_size()) return fail("input '" + d.name + "' has no data");
+      pr->host_in.push_back(req.raw_input_contents(raw_idx++));
+      if (pr->host_in.back().size() != need)
+        return fail("unexpected byte size for input '" + d.name + "'");
+      ref.kind = 0;
+      ref.device = 0;
+      ref.ptr = reinterpret_cast<uint64_t>(pr->host_in.back().data());
+      ref.bytes = need;
+    }
+  }
+  // outputs
+  const size_t no = m->outputs.size();
+  pr->out.assign(no, tcserve_ref{0, 0, 0, 0});
+  pr->out_requested.assign(no, req.outputs_size() == 0);
+  pr->out_shm.assign(no, false);
+  pr->out_region.assign(no, "");
+  pr->out_region_bytes.assign(no, 0);
+  pr->out_region_offset.assign(no, 0);
+  pr->host_out.resize(no);
+  for (int i = 0; i < req.outputs_size(); ++i) {
+    const auto& o = req.outputs(i);
+    int idx = -1;
+    for (size_t k = 0; k < no; ++k)
+      if (m->outputs[k].name == o.name()) idx = static_cast<int>(k);
+    if (idx < 0) return false;
+    pr->out_requested[idx] = true;
+    std::string region;
+    int64_t rbytes = 0, roff = 0;
+    bool has_shm = false;
+    for (const auto& kv : o.parameters()) {
+      if (kv.first == "shared_memory_region") {
+        region = kv.second.string_param();
+        has_shm = true;
+      } else if (kv.first == "shared_memory_byte_size") {
+        rbytes = kv.second.int64_param();
+      } else if (kv.first == "shared_memory_offset") {
+        roff = kv.second.int64_param();
+      } else if (kv.first == "binary_data") {
+      } else {
+        return false;  // classification etc.
+      }
+    }
+    const uint64_t need = static_cast<uint64_t>(pr->rows) * m->outputs[idx].sample_bytes;
+    if (has_shm) {
+      ShmEntry e;
+      int kind = -1;
+      {
+        std::lock_guard<std::mutex> lk(shm_mu_);
+        for (int kk = 0; kk < 2 && kind < 0; ++kk) {
+          auto it = shm_[kk].find(region);
+          if (it != shm_[kk].end()) {
+            e = it->second;
+            kind = kk;
+          }
+        }
+      }
+      if (kind < 0) return fail("Unable to find shared memory region: '" + region + "'");
+      if (roff < 0 || static_cast<uint64_t>(roff + rbytes) > e.bytes)
+        return fail("Invalid offset + byte size for shared memory region: '" + region + "'");
+      if (static_cast<uint64_t>(rbytes) < need)
+        return fail("shared memory size specified with the request for output '" + m->outputs[idx].name + "' (" +
+                    std::to_string(rbytes) + " bytes) should be at least " + std::to_string(need) + " bytes");
+      pr->out[idx] = tcserve_ref{kind, e.device, e.ptr + roff, need};
+      pr->out_shm[idx] = true;
+      pr->out_region[idx] = region;
+      pr->out_region_bytes[idx] = rbytes;
+      pr->out_region_offset[idx] = roff;
+    }
+  }
+  for (size_t k = 0; k < no; ++k) {
+    if (pr->out_requested[k] && !pr->out_shm[k]) {
+      const uint64_t need = static_cast<uint64_t>(pr->rows) * m->outputs[k].sample_bytes;
+      pr->host_out[k].resize(need);
+      pr->out[k] = tcserve_ref{0, 0, reinterpret_cast<uint64_t>(&pr->host_out[k][0]), need};
+    }
+  }
+  n_native++;
+  {
+    std::lock_guard<std::mutex> lk(m->mu);
+    m->q_rows += pr->rows;
+    m->q.push_back(std::move(pr));
+  }
+  m->cv.notify_one();
+  return true;
+}
+
+void Server::Worker(std::shared_ptr<NativeModel> m, int instance)
+{
+  while (true) {
+    std::vector<std::unique_ptr<PendingReq>> batch;
+    {
+      std::unique_lock<std::mutex> lk(m->mu);
+      m->cv.wait(lk, [&] { return m->stopping || !m->q.empty(); });
+      if (m->stopping) return;
+      const int cap = m->max_batch > 0 ? m->max_batch : 1;
+      if (m->max_batch > 0 && m->delay_ns > 0) {
+        const uint64_t deadline = m->q.front()->t_arrive + m->delay_ns;
+        while (!m->stopping && m->q_rows < cap) {
+          const uint64_t now = NowNs();
+          if (now >= deadline) break;
+          m->cv.wait_for(lk, std::chrono::nanoseconds(deadline - now));
+          if (m->q.empty()) break;
+        }
+        if (m->stopping) return;
+        if (m->q.empty()) continue;
+      }
+      int rows = 0;
+      while (!m->q.empty() && (rows == 0 || rows + m->q.front()->rows <= cap)) {
+        rows += m->q.front()->rows;
+        m->q_rows -= m->q.front()->rows;
+        batch.push_back(std::move(m->q.front()));
+        m->q.pop_front();
+      }
+      if (!m->q.empty()) m->cv.notify_one();
+    }
+    Execute(m.get(), instance, batch);
+  }
+}
+
+void Server::Execute(NativeModel* m, int instance, std::vector<std::unique_ptr<PendingReq>>& batch)
+{
+  const int n = static_cast<int>(batch.size());
+  const size_t ni = m->inputs.size(), no = m->outputs.size();
+  std::vector<int32_t> rows(n);
+  std::vector<tcserve_ref> ins(n * ni), outs(n * no);
+  int total = 0;
+  for (int r = 0; r < n; ++r) {
+    rows[r] = batch[r]->rows;
+    total += rows[r];
+    for (size_t k = 0; k < ni; ++k) ins[r * ni + k] = batch[r]->in[k];
+    for (size_t k = 0; k < no; ++k) outs[r * no + k] = batch[r]->out[k];
+  }
+  uint64_t timing[3] = {0, 0, 0};
+  tcserve_batch b;
+  b.n_requests = n;
+  b.total_rows = total;
+  b.rows = rows.data();
+  b.n_inputs = static_cast<int32_t>(ni);
+  b.inputs = ins.data();
+  b.n_outputs = static_cast<int32_t>(no);
+  b.outputs = outs.data();
+  b.timing_ns = timing;
+  char err[1024] = {0};
+  const uint64_t t_exec = NowNs();
+  const int rc = m->fn(m->user, instance, &b, err, sizeof(err));
+  const uint64_t t_done = NowNs();
+  {
+    std::lock_guard<std::mutex> lk(m->smu);
+    if (rc == 0) {
+      m->execution_count++;
+      m->inference_count += total;
+      BatchStat& bs = m->batch[total];
+      bs.count++;
+      bs.in_ns += timing[0];
+      bs.infer_ns += timing[1];
+      bs.out_ns += timing[2];
+      m->cin.count += n;
+      m->cin.ns += timing[0];
+      m->cinf.count += n;
+      m->cinf.ns += timing[1];
+      m->cout.count += n;
+      m->cout.ns += timing[2];
+    }
+    m->last_inference_ms =
+        std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch())
+            .count();
+    for (auto& pr : batch) {
+      Stat& s = rc == 0 ? m->success : m->fail;
+      s.count++;
+      s.ns += t_done - pr->t_arrive;
+      if (rc == 0) {
+        m->queue.count++;
+        m->queue.ns += t_exec - pr->t_arrive;
+      }
+    }
+  }
+  for (auto& pr : batch) {
+    if (rc != 0) {
+      PostReply(pr->loop, pr->conn_id, pr->stream_id, std::string(), kInternal, err);
+      continue;
+    }
+    inference::ModelInferResponse resp;
+    resp.set_model_name(m->name);
+    resp.set_model_version(m->version);
+    resp.set_id(pr->id);
+    int last_raw = -1;
+    std::vector<int> order;
+    for (size_t k = 0; k < no; ++k)
+      if (pr->out_requested[k]) order.push_back(static_cast<int>(k));
+    for (size_t j = 0; j < order.size(); ++j) {
+      const int k = order[j];
+      auto* o = resp.add_outputs();
+      o->set_name(m->outputs[k].name);
+      o->set_datatype(m->outputs[k].dtype);
+      if (m->max_batch > 0) o->add_shape(pr->rows);
+      for (auto d : m->outputs[k].dims) o->add_shape(d);
+      if (pr->out_shm[k]) {
+        (*o->mutable_parameters())["shared_memory_region"].set_string_param(pr->out_region[k]);
+        (*o->mutable_parameters())["shared_memory_byte_size"].set_int64_param(pr->out_region_bytes[k]);
+        if (pr->out_region_offset[k])
+          (*o->mutable_parameters())["shared_memory_offset"].set_int64_param(pr->out_region_offset[k]);
+      } else {
+        last_raw = static_cast<int>(j);
+      }
+    }
+    // raw_output_contents stays position-aligned with outputs (empty for shm outputs)
+    for (int j = 0; j <= last_raw; ++j) {
+      const int k = order[j];
+      std::string* dst = resp.add_raw_output_contents();
+      if (!pr->out_shm[k]) *dst = std::move(pr->host_out[k]);
+    }
+    std::string enc;
+    resp.Encode(&enc);
+    PostReply(pr->loop, pr->conn_id, pr->stream_id, std::move(enc), kOk, "");
+  }
+}
+
+int Server::AddModel(std::unique_ptr<NativeModel> m, std::string* err)
+{
+  std::shared_ptr<NativeModel> sm(m.release());
+  std::lock_guard<std::mutex> lk(models_mu);
+  if (models.count(sm->name)) {
+    *err = "model '" + sm->name + "' already registered";
+    return 1;
+  }
+  for (int i = 0; i < std::max(1, sm->instances); ++i)
+    sm->workers.emplace_back(&Server::Worker, this, sm, i);
+  models[sm->name] = sm;
+  return 0;
+}
+
+int Server::RemoveModel(const std::string& name)
+{
+  std::shared_ptr<NativeModel> m;
+  {
+    std::lock_guard<std::mutex> lk(models_mu);
+    auto it = models.find(name);
+    if (it == models.end()) return 1;
+    m = it->second;
+    models.erase(it);
+  }
+  {
+    std::lock_guard<std::mutex> lk(m->mu);
+    m->stopping = true;
+  }
+  m->cv.notify_all();
+  for (auto& t : m->workers)
+    if (t.joinable()) t.join();
+  // fail what was still queued
+  for (auto& pr : m->q) PostReply(pr->loop, pr->conn_id, pr->stream_id, std::string(), kUnavailable, "model unloaded");
+  m->q.clear();
+  return 0;
+}
+
+void Server::ShmAdd(int kind, const std::string& name, const ShmEntry& e)
+{
+  std::lock_guard<std::mutex> lk(shm_mu_);
+  shm_[kind][name] = e;
+}
+
+void Server::ShmRemove(int kind, const std::string& name)
+{
+  std::lock_guard<std::mutex> lk(shm_mu_);
+  if (name.empty()) shm_[kind].clear();
+  else shm_[kind].erase(name);
+}
+
+}  // namespace tcserve
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+using tcserve::NativeModel;
+using tcserve::Server;
+
+static void SetErr(char* err, int32_t errlen, const std::string& m)
+{
+  if (err && errlen > 0) {
+    strncpy(err, m.c_str(), errlen - 1);
+    err[errlen - 1] = 0;
+  }
+}
+
+extern "C" {
+
+void* tcserve_create(const char* host, int32_t port, const char* upstream_host, int32_t upstream_port,
+                     int32_t io_threads, char* err, int32_t errlen)
+{
+  std::unique_ptr<Server> s(new Server());
+  std::string e;
+  if (!s->Start(host ? host : "0.0.0.0", port, upstream_host ? upstream_host : "127.0.0.1", upstream_port,
+                io_threads, &e)) {
+    SetErr(err, errlen, e);
+    return nullptr;
+  }
+  return s.release();
+}
+
+int32_t tcserve_port(void* server) { return static_cast<Server*>(server)->port(); }
+
+int32_t tcserve_add_model(void* server, const char* name, const char* version, int32_t max_batch,
+                          int32_t max_queue_delay_us, int32_t instances, int32_t n_inputs, const char** in_names,
+                          const char** in_dtypes, const int32_t* in_ndims, const int64_t* in_dims, int32_t n_outputs,
+                          const char** out_names, const char** out_dtypes, const int32_t* out_ndims,
+                          const int64_t* out_dims, tcserve_exec_fn fn, void* user, char* err, int32_t errlen)
+{
+  std::unique_ptr<NativeModel> m(new NativeModel());
+  m->name = name;
+  m->version = version;
+  m->max_batch = max_batch;
+  m->delay_ns = static_cast<uint64_t>(std::max(0, max_queue_delay_us)) * 1000ull;
+  m->instances = instances;
+  m->fn = fn;
+  m->user = user;
+  auto fill = [&](int32_t n, const char** names, const char** dts, const int32_t* nd, const int64_t* dims,
+                  std::vector<tcserve::TensorDef>* out) -> bool {
+    size_t p = 0;
+    for (int i = 0; i < n; ++i) {
+      tcserve::TensorDef d;
+      d.name = names[i];
+      d.dtype = dts[i];
+      size_t elems = 1;
+      for (int k = 0; k < nd[i]; ++k) {
+        d.dims.push_back(dims[p]);
+        if (dims[p] < 0) return false;
+        elems *= static_cast<size_t>(dims[p]);
+        ++p;
+      }
+      const size_t es = tcserve::DtypeSize(d.dtype);
+      if (es == 0) return false;
+      d.sample_bytes = elems * es;
+      out->push_back(d);
+    }
+    return true;
+  };
+  if (!fill(n_inputs, in_names, in_dtypes, in_ndims, in_dims, &m->inputs) ||
+      !fill(n_outputs, out_names, out_dtypes, out_ndims, out_dims, &m->outputs)) {
+    SetErr(err, errlen, "native models need fixed-size, fixed-width tensors");
+    return 1;
+  }
+  std::string e;
+  if (static_cast<Server*>(server)->AddModel(std::move(m), &e) != 0) {
+    SetErr(err, errlen, e);
+    return 1;
+  }
+  return 0;
+}
+
+int32_t tcserve_remove_model(void* server, const char* name) { return static_cast<Server*>(server)->RemoveModel(name); }
+
+int32_t tcserve_shm_add(void* server, const char* name, int32_t kind, uint64_t ptr, uint64_t bytes, int32_t device)
+{
+  if (kind != 0 && kind != 1) return 1;
+  tcserve::ShmEntry e;
+  e.ptr = ptr;
+  e.bytes = bytes;
+  e.device = device;
+  static_cast<Server*>(server)->ShmAdd(kind, name, e);
+  return 0;
+}
+
+int32_t tcserve_shm_remove(void* server, int32_t kind, const char* name)
+{
+  if (kind != 0 && kind != 1) return 1;
+  static_cast<Server*>(server)->ShmRemove(kind, name ? name : "");
+  return 0;
+}
+
+int32_t tcserve_model_stats(void* server, const char* name, uint64_t* out)
+{
+  Server* s = static_cast<Server*>(server);
+  std::shared_ptr<NativeModel> m;
+  {
+    std::lock_guard<std::mutex> lk(s->models_mu);
+    auto it = s->models.find(name);
+    if (it == s->models.end()) return 1;
+    m = it->second;
+  }
+  std::lock_guard<std::mutex> lk(m->smu);
+  const uint64_t v[11] = {m->inference_count, m->execution_count, m->success.count, m->success.ns, m->fail.count,
+                          m->fail.ns, m->queue.ns, m->cin.ns, m->cinf.ns, m->cout.ns, m->last_inference_ms};
+  memcpy(out, v, sizeof(v));
+  return 0;
+}
+
+int32_t tcserve_batch_stats(void* server, const char* name, uint64_t* out, int32_t max_rows)
+{
+  Server* s = static_cast<Server*>(server);
+  std::shared_ptr<NativeModel> m;
+  {
+    std::lock_guard<std::mutex> lk(s->models_mu);
+    auto it = s->models.find(name);
+    if (it == s->models.end()) return -1;
+    m = it->second;
+  }
+  std::lock_guard<std::mutex> lk(m->smu);
+  int32_t r = 0;
+  for (const auto& kv : m->batch) {
+    if (r >= max_rows) break;
+    uint64_t* row = out + 7 * r;
+    row[0] = kv.first;
+    row[1] = kv.second.count;
+    row[2] = kv.second.in_ns;
+    row[3] = kv.second.infer_ns;
+    row[4] = kv.second.out_ns;
+    row[5] = row[6] = 0;
+    ++r;
+  }
+  return r;
+}
+
+int32_t tcserve_counters(void* server, uint64_t* out)
+{
+  Server* s = static_cast<Server*>(server);
+  out[0] = s->n_native.load();
+  out[1] = s->n_proxied.load();
+  out[2] = s->n_conns.load();
+  return 0;
+}
+
+void tcserve_destroy(void* server) { delete static_cast<Server*>(server); }
+
+}  // extern "C"

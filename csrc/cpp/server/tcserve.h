@@ -1,0 +1,71 @@
+// tcserve — native gRPC front end of the bench/test server.
+//
+// The Python server (triton_client_amd/server) implements every KServe-v2
+// endpoint; its grpc.aio front end tops out at a few thousand requests/s on
+// one core, which caps perf_analyzer at small batch sizes.  tcserve puts a
+// C++ HTTP/2 server on the public gRPC port:
+//
+//   * ModelInfer for models registered as *native* is handled entirely here:
+//     protobuf decode (generated classes, csrc/cpp/proto), shared-memory
+//     resolution against a mirror of the Python registries, a C++ dynamic
+//     batcher with one worker per model instance, and ONE call per batch into
+//     the model's executor (a Python callback that launches HIP work and
+//     drops the GIL while the GPU runs), then response encode and send;
+//   * every other RPC (control plane, streaming, non-native models, requests
+//     using features the fast path does not cover) is proxied verbatim over
+//     HTTP/2 to the Python grpc.aio server on an internal loopback port.
+//
+// Threading: N event loops (epoll + nghttp2 server sessions, one connection
+// belongs to one loop); other threads post closures to a loop via eventfd.
+#pragma once
+
+#include <cstdint>
+
+extern "C" {
+
+/// One tensor reference of a batch: kind 0 = host memory, 1 = device memory.
+struct tcserve_ref {
+  int32_t kind;
+  int32_t device;
+  uint64_t ptr;
+  uint64_t bytes;
+};
+
+/// A batch handed to a native model's executor.
+struct tcserve_batch {
+  int32_t n_requests;
+  int32_t total_rows;
+  const int32_t* rows;              // [n_requests]
+  int32_t n_inputs;
+  const tcserve_ref* inputs;        // [n_requests][n_inputs]
+  int32_t n_outputs;
+  const tcserve_ref* outputs;       // [n_requests][n_outputs]; ptr 0 = output not requested
+  uint64_t* timing_ns;              // out: compute_input, compute_infer, compute_output
+};
+
+/// Executor: return 0 on success, else write a message into err.
+typedef int (*tcserve_exec_fn)(void* user, int32_t instance, const tcserve_batch* batch, char* err, int32_t errlen);
+
+void* tcserve_create(const char* host, int32_t port, const char* upstream_host, int32_t upstream_port,
+                     int32_t io_threads, char* err, int32_t errlen);
+int32_t tcserve_port(void* server);
+/// dims are per-sample (without the batch dimension), flattened; ndims[i] gives each tensor's rank.
+int32_t tcserve_add_model(void* server, const char* name, const char* version, int32_t max_batch,
+                          int32_t max_queue_delay_us, int32_t instances, int32_t n_inputs, const char** in_names,
+                          const char** in_dtypes, const int32_t* in_ndims, const int64_t* in_dims, int32_t n_outputs,
+                          const char** out_names, const char** out_dtypes, const int32_t* out_ndims,
+                          const int64_t* out_dims, tcserve_exec_fn fn, void* user, char* err, int32_t errlen);
+int32_t tcserve_remove_model(void* server, const char* name);
+/// Mirror of the Python shared-memory registries; kind 0 = system (ptr = host mapping), 1 = device.
+int32_t tcserve_shm_add(void* server, const char* name, int32_t kind, uint64_t ptr, uint64_t bytes, int32_t device);
+int32_t tcserve_shm_remove(void* server, int32_t kind, const char* name);  // name "" = all of kind
+/// out[0..9]: inference_count, execution_count, success_count, success_ns, fail_count, fail_ns,
+/// queue_ns, compute_input_ns, compute_infer_ns, compute_output_ns; last_inference_ms at out[10].
+int32_t tcserve_model_stats(void* server, const char* name, uint64_t* out);
+/// Per batch size rows of 7: batch_size, count, in_ns, infer_ns, out_ns, (reserved x2). Returns row count.
+int32_t tcserve_batch_stats(void* server, const char* name, uint64_t* out, int32_t max_rows);
+/// Counters: [0] native requests, [1] proxied calls, [2] connections accepted.
+int32_t tcserve_counters(void* server, uint64_t* out);
+void tcserve_destroy(void* server);
+
+}  // extern "C"

@@ -137,6 +137,17 @@ def _reference_logits(x, dtype_name="float32"):
         return m(xt).float().cpu().numpy()
 
 
+def _fused_logits(x):
+    import torch
+
+    from triton_client_amd.models import densenet_fused
+
+    eng, _ = densenet_fused.build(max_batch=x.shape[0], device="cuda")
+    xt = torch.from_numpy(x).cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        return eng(xt).float().cpu().numpy()
+
+
 def test_densenet_zero_copy_matches_fp32_reference(gpu_server, hipshm):
     """densenet_onnx bs=2 through HIP shm (K6 gather in, K7 scatter out)
     against an fp32 torch reference of the same random-init weights."""
@@ -159,9 +170,9 @@ def test_densenet_zero_copy_matches_fp32_reference(gpu_server, hipshm):
     r = g.infer("densenet_onnx", [inp], outputs=[out])
     assert r.get_output("fc6_1").parameters["shared_memory_region"].string_param == "d_out"
     got = hipshm.get_contents_as_numpy(hout, np.float32, [2, 1000])
-    # (1) same bf16 model run eagerly: the served path (K6 gather, HIP graph,
-    #     K7 scatter) must not add error beyond kernel-selection noise
-    ref_bf16 = _reference_logits(x, "bfloat16")
+    # (1) the same fused engine run eagerly: the served path (K6 gather, HIP
+    #     graph, K7 scatter, native front end) must not add error
+    ref_bf16 = _fused_logits(x)
     rel_bf16 = np.linalg.norm(got - ref_bf16) / np.linalg.norm(ref_bf16)
     assert rel_bf16 < 0.02, rel_bf16
     # (2) fp32 reference of the same weights: bf16 error over 121 layers

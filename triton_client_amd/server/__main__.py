@@ -25,6 +25,8 @@ def main(argv=None):
     ap.add_argument("--engine", default="fused", choices=["fused", "torch"],
                     help="densenet_onnx engine: fused HIP/MFMA kernels or the torch/MIOpen module")
     ap.add_argument("--ready-file", default="", help="touch this file once serving")
+    ap.add_argument("--native-grpc", default="auto", choices=["auto", "on", "off"],
+                    help="serve the gRPC port with tcserve (C++ front end, csrc/cpp/server)")
     args = ap.parse_args(argv)
 
     from .app import default_models, serve
@@ -57,7 +59,8 @@ def main(argv=None):
             loop.add_signal_handler(sig, stop.set)
         ready = asyncio.Event()
         task = asyncio.ensure_future(
-            serve(server, args.http_port or None, args.grpc_port or None, args.host, ready, stop)
+            serve(server, args.http_port or None, args.grpc_port or None, args.host, ready, stop,
+                  native_grpc={"auto": None, "on": True, "off": False}[args.native_grpc])
         )
         await ready.wait()
         print("SERVER READY http=%s grpc=%s" % (args.http_port, args.grpc_port), flush=True)

@@ -40,8 +40,19 @@ GRPC_OPTIONS = [
 ]
 
 
-async def serve(server, http_port, grpc_port, host="127.0.0.1", ready_evt=None, stop_evt=None):
+def native_grpc_available():
+    from . import native_frontend
+
+    return native_frontend.available()
+
+
+async def serve(server, http_port, grpc_port, host="127.0.0.1", ready_evt=None, stop_evt=None, native_grpc=None):
+    """Serve HTTP (aiohttp) and gRPC.  With ``native_grpc`` (default: when
+    libtcserve.so is built) the public gRPC port is tcserve, the C++ front
+    end, and grpc.aio listens on a loopback port behind it."""
     server.loop = asyncio.get_running_loop()
+    if native_grpc is None:
+        native_grpc = native_grpc_available()
     runner = None
     if http_port is not None:
         runner = web.AppRunner(HttpFrontend(server).app, access_log=None)
@@ -49,17 +60,30 @@ async def serve(server, http_port, grpc_port, host="127.0.0.1", ready_evt=None, 
         site = web.TCPSite(runner, host, http_port, reuse_address=True)
         await site.start()
     gserver = None
+    nf = None
     if grpc_port is not None:
         gserver = grpc.aio.server(options=GRPC_OPTIONS)
         service_pb2_grpc.add_GRPCInferenceServiceServicer_to_server(GrpcFrontend(server), gserver)
-        gserver.add_insecure_port("%s:%d" % (host, grpc_port))
+        if native_grpc:
+            inner = gserver.add_insecure_port("127.0.0.1:0")
+        else:
+            gserver.add_insecure_port("%s:%d" % (host, grpc_port))
         await gserver.start()
+        if native_grpc:
+            from .native_frontend import NativeFrontend
+
+            nf = NativeFrontend(server, host, grpc_port, inner)
+            nf.register_all()
+            server.native_frontend = nf
     if ready_evt is not None:
         ready_evt.set()
     stop = stop_evt or asyncio.Event()
     try:
         await stop.wait()
     finally:
+        if nf is not None:
+            nf.close()
+            server.native_frontend = None
         if gserver is not None:
             await gserver.stop(0.5)
         if runner is not None:
@@ -69,7 +93,8 @@ async def serve(server, http_port, grpc_port, host="127.0.0.1", ready_evt=None, 
 class ServerHandle:
     """Runs an InferenceServer on a background thread (tests, benches)."""
 
-    def __init__(self, models=None, http_port=None, grpc_port=None, model_options=None, load=True):
+    def __init__(self, models=None, http_port=None, grpc_port=None, model_options=None, load=True, native_grpc=None):
+        self.native_grpc = native_grpc
         self.http_port = http_port or _free_port()
         self.grpc_port = grpc_port or _free_port()
         self.server = InferenceServer(models if models is not None else default_models(), model_options)
@@ -95,7 +120,8 @@ class ServerHandle:
 
         async def main():
             self._stop = asyncio.Event()
-            await serve(self.server, self.http_port, self.grpc_port, ready_evt=self._ready, stop_evt=self._stop)
+            await serve(self.server, self.http_port, self.grpc_port, ready_evt=self._ready, stop_evt=self._stop,
+                        native_grpc=self.native_grpc)
 
         loop.run_until_complete(main())
         loop.close()

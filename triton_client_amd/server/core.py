@@ -134,10 +134,42 @@ class ModelStats:
 # ---------------------------------------------------------------------------
 # Shared memory registries
 # ---------------------------------------------------------------------------
+def _merge_native_stats(d, ns):
+    """Fold counters of natively served requests (tcserve) into a stats dict."""
+    d["inference_count"] += ns["inference_count"]
+    d["execution_count"] += ns["execution_count"]
+    d["last_inference"] = max(d["last_inference"], ns["last_inference"])
+    st = d["inference_stats"]
+    n = ns["success_count"]
+    st["success"]["count"] += n
+    st["success"]["ns"] += ns["success_ns"]
+    st["fail"]["count"] += ns["fail_count"]
+    st["fail"]["ns"] += ns["fail_ns"]
+    st["queue"]["count"] += n
+    st["queue"]["ns"] += ns["queue_ns"]
+    for k in ("compute_input", "compute_infer", "compute_output"):
+        st[k]["count"] += n
+        st[k]["ns"] += ns[k + "_ns"]
+    by_bs = {b["batch_size"]: b for b in d["batch_stats"]}
+    for bs, (cnt, t_in, t_inf, t_out) in ns["batches"].items():
+        b = by_bs.get(bs)
+        if b is None:
+            b = {"batch_size": bs}
+            for k in ("compute_input", "compute_infer", "compute_output"):
+                b[k] = {"count": 0, "ns": 0}
+            d["batch_stats"].append(b)
+            by_bs[bs] = b
+        for k, t in (("compute_input", t_in), ("compute_infer", t_inf), ("compute_output", t_out)):
+            b[k]["count"] += cnt
+            b[k]["ns"] += t
+    d["batch_stats"].sort(key=lambda b: b["batch_size"])
+
+
 class SystemShmRegistry:
-    def __init__(self):
+    def __init__(self, listeners=None):
         self.regions = {}
         self.lock = threading.Lock()
+        self.listeners = listeners if listeners is not None else []
 
     def register(self, name, key, offset, byte_size):
         from tritonclient.utils import shared_memory as shm
@@ -154,6 +186,8 @@ class SystemShmRegistry:
                     "Unable to open shared memory region: '%s' (%s)" % (key, e), 400, "INVALID_ARGUMENT"
                 )
             self.regions[name] = (region, key, offset, byte_size)
+            for fn in self.listeners:
+                fn("system", "add", name, region.address(0), byte_size, 0)
 
     def unregister(self, name=""):
         with self.lock:
@@ -161,6 +195,8 @@ class SystemShmRegistry:
             for n in names:
                 entry = self.regions.pop(n, None)
                 if entry is not None:
+                    for fn in self.listeners:
+                        fn("system", "remove", n)
                     entry[0].close()
 
     def status(self, name=""):
@@ -190,9 +226,10 @@ class SystemShmRegistry:
 class DeviceShmRegistry:
     """HIP IPC regions (wire name: cudasharedmemory)."""
 
-    def __init__(self):
+    def __init__(self, listeners=None):
         self.regions = {}
         self.lock = threading.Lock()
+        self.listeners = listeners if listeners is not None else []
 
     def register(self, name, raw_handle, device_id, byte_size):
         from triton_client_amd.ops import hip
@@ -211,6 +248,8 @@ class DeviceShmRegistry:
             except Exception as e:
                 raise ServerError("failed to open HIP IPC handle for '%s': %s" % (name, e))
             self.regions[name] = (ptr, device_id, byte_size)
+            for fn in self.listeners:
+                fn("device", "add", name, ptr, byte_size, device_id)
 
     def unregister(self, name=""):
         from triton_client_amd.ops import hip
@@ -220,6 +259,8 @@ class DeviceShmRegistry:
             for n in names:
                 e = self.regions.pop(n, None)
                 if e is not None:
+                    for fn in self.listeners:
+                        fn("device", "remove", n)
                     try:
                         hip.ipc_close(e[0], e[1])
                     except Exception:
@@ -297,8 +338,12 @@ class InferenceServer:
         self.model_options = model_options or {}
         for cls in model_classes:
             self.add_model(cls, self.model_options.get(cls.name))
-        self.sys_shm = SystemShmRegistry()
-        self.dev_shm = DeviceShmRegistry()
+        # native front end hooks (server/native_frontend.py)
+        self.shm_listeners = []
+        self.model_listeners = []
+        self.native_stats = None
+        self.sys_shm = SystemShmRegistry(self.shm_listeners)
+        self.dev_shm = DeviceShmRegistry(self.shm_listeners)
         self.executor = ThreadPoolExecutor(max_workers=executor_workers, thread_name_prefix="tcamd-exec")
         self.trace_settings = {
             "trace_level": ["OFF"],
@@ -319,6 +364,7 @@ class InferenceServer:
         }
         self.ready = True
         self.loop = None
+        self.native_frontend = None
 
     # -- repository ------------------------------------------------------------
     def add_model(self, cls, options=None):
@@ -389,6 +435,8 @@ class InferenceServer:
             entry.state = "READY"
             entry.reason = ""
         self.repo[entry.name] = entry
+        for fn in list(self.model_listeners):
+            fn("load", entry)
 
     def _override_entry(self, name, cfg, files, base=None):
         versions = set()
@@ -420,6 +468,8 @@ class InferenceServer:
         return entry
 
     def _unload_version(self, entry, v):
+        for fn in list(self.model_listeners):
+            fn("unload", entry, v)
         sch = entry.schedulers.pop(v, None)
         if sch is not None:
             sch.close()
@@ -521,7 +571,11 @@ class InferenceServer:
             for v, st in sorted(e.stats.items()):
                 if version not in ("", None) and str(v) != str(version):
                     continue
-                out.append(st.json(n, v))
+                d = st.json(n, v)
+                ns = self.native_stats(n) if self.native_stats is not None else None
+                if ns and str(ns.get("version")) == str(v):
+                    _merge_native_stats(d, ns)
+                out.append(d)
             if name and version not in ("", None) and not out:
                 raise unavailable("requested model version is not available for model '%s'" % n)
         return {"model_stats": out}

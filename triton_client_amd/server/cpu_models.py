@@ -241,6 +241,60 @@ class PreprocessInception(Model):
         return res
 
 
+class AddSubBatched(Model):
+    """INT32 add/sub with dynamic batching; also served on the native fast path.
+
+    ``execute_native`` receives one batch from tcserve (csrc/cpp/server) with
+    host pointers (in-band tensors or system shared memory) and writes the
+    outputs in place.
+    """
+
+    name = "add_sub_batched"
+    max_batch_size = 8
+    inputs = (TensorSpec("INPUT0", "INT32", [16]), TensorSpec("INPUT1", "INT32", [16]))
+    outputs = (TensorSpec("OUTPUT0", "INT32", [16]), TensorSpec("OUTPUT1", "INT32", [16]))
+    dynamic_batching = {"preferred": [], "max_queue_delay_us": 200}
+    instance_count = 2
+    supports_native = True
+
+    def execute(self, requests):
+        out = []
+        for r in requests:
+            try:
+                a = r.input("INPUT0").numpy()
+                b = r.input("INPUT1").numpy()
+                out.append([self.out("OUTPUT0", a + b), self.out("OUTPUT1", a - b)])
+            except Exception as e:  # per-request failure
+                out.append(e)
+        return out
+
+    def execute_native(self, instance, b):
+        import ctypes
+        import time
+
+        t0 = time.monotonic_ns()
+        ni, no = b.n_inputs, b.n_outputs
+        for r in range(b.n_requests):
+            rows = b.rows[r]
+            arrs = []
+            for k in range(ni):
+                ref = b.inputs[r * ni + k]
+                if ref.kind != 0:
+                    raise ServerError("add_sub_batched runs on host memory only")
+                arrs.append(np.ctypeslib.as_array((ctypes.c_int32 * (rows * 16)).from_address(ref.ptr)))
+            res = (arrs[0] + arrs[1], arrs[0] - arrs[1])
+            for k in range(no):
+                ref = b.outputs[r * no + k]
+                if ref.ptr:
+                    if ref.kind != 0:
+                        raise ServerError("add_sub_batched runs on host memory only")
+                    np.ctypeslib.as_array((ctypes.c_int32 * (rows * 16)).from_address(ref.ptr))[:] = res[k]
+        t1 = time.monotonic_ns()
+        b.timing_ns[0] = 0
+        b.timing_ns[1] = t1 - t0
+        b.timing_ns[2] = 0
+
+
 CPU_MODELS = [
     SimpleAddSub,
     OnnxInt32,
@@ -254,4 +308,5 @@ CPU_MODELS = [
     SimpleStringDynaSequence,
     RepeatInt32,
     PreprocessInception,
+    AddSubBatched,
 ]
