@@ -36,7 +36,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
-constexpr int kLdsK = 40;        // 32-wide K tile + 8 pad: 80-B rows, conflict-free b128 reads
 constexpr int kMaxK = 1024;      // prologue scale/bias table
 constexpr int kC3 = 128;         // 3x3 conv input channels (bn_size * growth)
 constexpr int kN3 = 32;          // 3x3 conv output channels (growth)
@@ -83,18 +82,25 @@ struct Conv1x1Params {
   int ldx, M, K, N, ldy;
   int relu_out;
   int H, W;                 // POOL: pre-pool spatial dims (M = imgs * H/2 * W/2)
+  float* ws;                // split-K: fp32 partials [splits][M][N] (null = no split)
+  int k_per_split;          // K range per blockIdx.z (multiple of BK)
 };
 
 // Block = 4 waves as 2 (pixels) x 2 (channels); block tile (32*TM) x 128,
-// wave tile (16*TM pixels) x 64 channels, BK = 32, LDS double-buffered with
-// register prefetch (global loads of tile k+1 are in flight during MFMAs on k).
-template <int TM, bool PRO, bool POOL>
+// wave tile (16*TM pixels) x 64 channels, K tile BK (32 or 64), LDS
+// double-buffered with register prefetch (global loads of tile k+1 are in
+// flight during the MFMAs on tile k).  K need not be a multiple of BK: the
+// tail chunk is zero-filled (K % 32 == 0 always holds).
+template <int TM, int BK, bool PRO, bool POOL>
 __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
   constexpr int BM = 32 * TM, BN = 128;
-  constexpr int A_CHUNKS = BM * 4, AI = (A_CHUNKS + 255) / 256;
+  constexpr int CPR = BK / 8;                 // 16-B chunks per row of a K tile
+  constexpr int LDK = BK + 8;                 // LDS row stride (elements): conflict-free b128 reads
+  constexpr int A_CHUNKS = BM * CPR, AI = (A_CHUNKS + 255) / 256;
+  constexpr int BI = BN * CPR / 256;
   constexpr int NS = POOL ? 4 : 1;
-  __shared__ __attribute__((aligned(16))) uint16_t sA[2][BM * kLdsK];
-  __shared__ __attribute__((aligned(16))) uint16_t sB[2][BN * kLdsK];
+  __shared__ __attribute__((aligned(16))) uint16_t sA[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) uint16_t sB[2][BN * LDK];
   __shared__ float sS[PRO ? kMaxK : 1], sT[PRO ? kMaxK : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -113,10 +119,10 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
     const int c = tid + i * 256;
-    const int m = m0 + (c >> 2);
+    const int m = m0 + c / CPR;
     a_ok[i] = (c < A_CHUNKS) && (m < p.M);
     const int mm = a_ok[i] ? m : 0;
-    const int kc = (c & 3) * 8;
+    const int kc = (c % CPR) * 8;
     if constexpr (POOL) {
       const int wo = p.W >> 1, ho = p.H >> 1;
       const int img = mm / (ho * wo), r = mm - img * ho * wo;
@@ -130,57 +136,66 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
       a_src[i][0] = p.x + (size_t)mm * p.ldx + kc;
     }
   }
-  const uint16_t* b_src[2];
+  const uint16_t* b_src[BI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < BI; ++i) {
     const int c = tid + i * 256;
-    b_src[i] = p.w + (size_t)(n0 + (c >> 2)) * p.K + (c & 3) * 8;
+    b_src[i] = p.w + (size_t)(n0 + c / CPR) * p.K + (c % CPR) * 8;
   }
 
-  v4u ra[AI][NS], rb[2];
+  v4u ra[AI][NS], rb[BI];
   auto load_tile = [&](int kt) {
-    const int k0 = kt * 32;
+    const int k0 = kt * BK;
 #pragma unroll
-    for (int i = 0; i < AI; ++i)
+    for (int i = 0; i < AI; ++i) {
+      const int kc = ((tid + i * 256) % CPR) * 8;
+      const bool kin = BK == 32 || k0 + kc < p.K;
 #pragma unroll
-      for (int s = 0; s < NS; ++s) ra[i][s] = ldg16(a_src[i][s] + k0);
+      for (int s = 0; s < NS; ++s) ra[i][s] = kin ? ldg16(a_src[i][s] + k0) : v4u{0, 0, 0, 0};
+    }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) rb[i] = ldg16(b_src[i] + k0);
+    for (int i = 0; i < BI; ++i) {
+      const int kc = ((tid + i * 256) % CPR) * 8;
+      rb[i] = (BK == 32 || k0 + kc < p.K) ? ldg16(b_src[i] + k0) : v4u{0, 0, 0, 0};
+    }
   };
   auto store_tile = [&](int kt, int buf) {
-    const int k0 = kt * 32;
+    const int k0 = kt * BK;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int c = tid + i * 256;
       if (c < A_CHUNKS) {
-        const int kc = (c & 3) * 8;
+        const int kc = (c % CPR) * 8;
+        const bool kin = BK == 32 || k0 + kc < p.K;
         v4u v;
         if constexpr (PRO) {
           float o[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = 0.f;
+          if (kin) {
 #pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            float f[8];
-            unpack8(ra[i][s], f);
+            for (int s = 0; s < NS; ++s) {
+              float f[8];
+              unpack8(ra[i][s], f);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float t = fmaxf(f[e] * sS[k0 + kc + e] + sT[k0 + kc + e], 0.f);
-              o[e] += POOL ? 0.25f * t : t;
+              for (int e = 0; e < 8; ++e) {
+                const float t = fmaxf(f[e] * sS[k0 + kc + e] + sT[k0 + kc + e], 0.f);
+                o[e] += POOL ? 0.25f * t : t;
+              }
             }
           }
           v = pack8(o);
         } else {
           v = ra[i][0];
         }
-        if (!a_ok[i]) v = v4u{0, 0, 0, 0};
-        *reinterpret_cast<v4u*>(&sA[buf][(c >> 2) * kLdsK + kc]) = v;
+        if (!a_ok[i] || !kin) v = v4u{0, 0, 0, 0};
+        *reinterpret_cast<v4u*>(&sA[buf][(c / CPR) * LDK + kc]) = v;
       }
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < BI; ++i) {
       const int c = tid + i * 256;
-      *reinterpret_cast<v4u*>(&sB[buf][(c >> 2) * kLdsK + (c & 3) * 8]) = rb[i];
+      *reinterpret_cast<v4u*>(&sB[buf][(c / CPR) * LDK + (c % CPR) * 8]) = rb[i];
     }
   };
 
@@ -190,30 +205,48 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int KT = p.K / 32;
-  load_tile(0);
+  // K tiles of this block: all of K, or one split's range
+  const int kt0 = p.ws ? (int)blockIdx.z * (p.k_per_split / BK) : 0;
+  const int KT = p.ws ? min((p.K + BK - 1) / BK, kt0 + p.k_per_split / BK) : (p.K + BK - 1) / BK;
+  load_tile(kt0);
   __syncthreads();  // prologue tables
-  store_tile(0, 0);
+  store_tile(kt0, 0);
   __syncthreads();
   const int fr = lane & 15, fk = 8 * (lane >> 4);
-  for (int kt = 0; kt < KT; ++kt) {
-    const int buf = kt & 1;
+  for (int kt = kt0; kt < KT; ++kt) {
+    const int buf = (kt - kt0) & 1;
     if (kt + 1 < KT) load_tile(kt + 1);
-    bf16x8 fa[4], fb[TM];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      fa[j] = *reinterpret_cast<const bf16x8*>(&sB[buf][(wn * 64 + j * 16 + fr) * kLdsK + fk]);
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 fa[4], fb[TM];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-      fb[i] = *reinterpret_cast<const bf16x8*>(&sA[buf][(wm * 16 * TM + i * 16 + fr) * kLdsK + fk]);
+      for (int j = 0; j < 4; ++j)
+        fa[j] = *reinterpret_cast<const bf16x8*>(&sB[buf][(wn * 64 + j * 16 + fr) * LDK + ks * 32 + fk]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+      for (int i = 0; i < TM; ++i)
+        fb[i] = *reinterpret_cast<const bf16x8*>(&sA[buf][(wm * 16 * TM + i * 16 + fr) * LDK + ks * 32 + fk]);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) acc[j][i] = mfma16(fa[j], fb[i], acc[j][i]);
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = mfma16(fa[j], fb[i], acc[j][i]);
+    }
     if (kt + 1 < KT) store_tile(kt + 1, buf ^ 1);
     __syncthreads();
   }
 
+  if (p.ws) {  // split-K: raw fp32 partials, epilogue in dn_splitk_reduce
+    float* ws = p.ws + (size_t)blockIdx.z * p.M * p.N;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nb = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * 16 * TM + i * 16 + fr;
+        if (m < p.M) *reinterpret_cast<f32x4*>(ws + (size_t)m * p.N + nb) = acc[j][i];
+      }
+    }
+    return;
+  }
   // epilogue: lane holds out channels nb..nb+3 of pixel m
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -239,6 +272,26 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
   }
 }
 
+// split-K combine: y[m][n..n+3] = epi(sum_z ws[z][m][n..n+3] + bias)
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N,
+                                                            const float* __restrict__ bias, int relu,
+                                                            uint16_t* __restrict__ y, int ldy) {
+  const int q = N / 4;
+  const size_t total = (size_t)M * q;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(t / q), n = (int)(t - (size_t)m * q) * 4;
+    f32x4 a = *reinterpret_cast<const f32x4*>(ws + (size_t)m * N + n);
+    for (int z = 1; z < splits; ++z) a += *reinterpret_cast<const f32x4*>(ws + ((size_t)z * M + m) * N + n);
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r] = a[r] + (bias ? bias[n + r] : 0.f);
+      if (relu) v[r] = fmaxf(v[r], 0.f);
+    }
+    *reinterpret_cast<v2u*>(y + (size_t)m * ldy + n) = v2u{pack2(v[0], v[1]), pack2(v[2], v[3])};
+  }
+}
+
 // ============================================================================
 // K9: 3x3 conv, 128 -> 32 channels, stride 1, pad 1 (implicit GEMM)
 // ============================================================================
@@ -253,7 +306,7 @@ struct Conv3x3Params {
 // Persistent blocks: weights loaded to LDS once, then the block walks pixel
 // tiles of 4 waves x 16*TM pixels.  Each tap's 16 B activation fragments are
 // prefetched one tap ahead (register double-buffer across the unrolled taps).
-template <int TM>
+template <int TM, int G>
 __global__ void __launch_bounds__(256) conv3x3_kernel(Conv3x3Params p) {
   extern __shared__ __attribute__((aligned(16))) uint16_t Ws[];  // [32][kWsK]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -310,17 +363,34 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(Conv3x3Params p) {
           for (int i = 0; i < TM; ++i) acc[j][i] = mfma16(fa[j], as_frag(src[i][c]), acc[j][i]);
       }
     };
-    // taps in ping-pong pairs: tap t+1's fragments load while tap t multiplies
-    v4u xa[TM][4], xb[TM][4];
-    load_tap(0, xa);
+    if constexpr (G == 1) {
+      // taps in ping-pong pairs: tap t+1's fragments load while tap t multiplies
+      v4u xa[TM][4], xb[TM][4];
+      load_tap(0, xa);
 #pragma unroll 1
-    for (int tap = 0; tap < 8; tap += 2) {
-      load_tap(tap + 1, xb);
-      mma_tap(tap, xa);
-      load_tap(tap + 2, xa);
-      mma_tap(tap + 1, xb);
+      for (int tap = 0; tap < 8; tap += 2) {
+        load_tap(tap + 1, xb);
+        mma_tap(tap, xa);
+        load_tap(tap + 2, xa);
+        mma_tap(tap + 1, xb);
+      }
+      mma_tap(8, xa);
+    } else {
+      // groups of 3 taps (one filter row): 12*TM loads in flight per lane
+      v4u ga[3][TM][4], gb[3][TM][4];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) load_tap(t, ga[t]);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) load_tap(3 + t, gb[t]);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) mma_tap(t, ga[t]);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) load_tap(6 + t, ga[t]);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) mma_tap(3 + t, gb[t]);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) mma_tap(6 + t, ga[t]);
     }
-    mma_tap(8, xa);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int nb = j * 16 + (lane >> 4) * 4;
@@ -402,35 +472,71 @@ __global__ void __launch_bounds__(256) head_pool_kernel(const uint16_t* __restri
   }
 }
 
-template <int TM, bool PRO, bool POOL>
-int launch_1x1(const Conv1x1Params& p, hipStream_t s) {
-  dim3 g((p.M + 32 * TM - 1) / (32 * TM), p.N / 128);
-  hipLaunchKernelGGL((conv1x1_kernel<TM, PRO, POOL>), g, dim3(256), 0, s, p);
+template <int TM, int BK, bool PRO, bool POOL>
+int launch_1x1(Conv1x1Params p, int splits, hipStream_t s) {
+  const int mb = (p.M + 32 * TM - 1) / (32 * TM), nb = p.N / 128;
+  if (splits > 1) {
+    const int kts = (p.K + BK - 1) / BK;
+    const int per = (kts + splits - 1) / splits;
+    splits = (kts + per - 1) / per;
+    p.k_per_split = per * BK;
+  } else {
+    p.ws = nullptr;
+  }
+  dim3 g(mb, nb, splits > 1 ? splits : 1);
+  hipLaunchKernelGGL((conv1x1_kernel<TM, BK, PRO, POOL>), g, dim3(256), 0, s, p);
+  if (splits > 1) {
+    const size_t total = (size_t)p.M * (p.N / 4);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(tcamd::grid_for(total)), dim3(256), 0, s, p.ws, splits, p.M, p.N,
+                       p.out_bias, p.relu_out, p.y, p.ldy);
+  }
   return hipGetLastError();
 }
 
+// variant: 0 = heuristic, else 10*TM + BK/32 (e.g. 42 = TM 4, BK 64)
+// variant: 0 = heuristic, else 10*TM + BK/32.  splits: 0 = heuristic (needs a
+// workspace), 1 = no split-K.  Heuristic from tools/kbench_densenet.py on
+// MI355X: TM 2 / BK 32 once M >= 32K rows, TM 1 below; BK 64 for small M,
+// where the launch is latency-bound over K; small grids split K until ~256
+// blocks run (the reduce launch costs ~2 us, so only when it pays).
 template <bool PRO, bool POOL>
-int pick_tm(const Conv1x1Params& p, hipStream_t s) {
-  // largest tile that still yields >= 512 blocks (2 per CU); small problems
-  // take 32-row tiles to spread over the CUs
-  const long nb = p.N / 128;
-  if ((long)((p.M + 127) / 128) * nb >= 512) return launch_1x1<4, PRO, POOL>(p, s);
-  if ((long)((p.M + 63) / 64) * nb >= 512) return launch_1x1<2, PRO, POOL>(p, s);
-  return launch_1x1<1, PRO, POOL>(p, s);
+int pick_1x1(const Conv1x1Params& p, int variant, int splits, size_t ws_bytes, hipStream_t s) {
+  if (variant == 0) variant = p.M >= 32768 ? 21 : p.M >= 8192 ? 11 : 12;
+  const int tm = variant / 10, bk = (variant % 10) * 32;
+  const long blocks = (long)((p.M + 32 * tm - 1) / (32 * tm)) * (p.N / 128);
+  const int kts = (p.K + bk - 1) / bk;
+  if (splits == 0) {
+    splits = 1;
+    if (p.ws && blocks < 128 && kts >= 4) {
+      splits = (int)((256 + blocks - 1) / blocks);
+      if (splits > kts / 2) splits = kts / 2;
+      if (splits > 16) splits = 16;
+    }
+  }
+  if (splits > 1 && (!p.ws || ws_bytes < (size_t)splits * p.M * p.N * sizeof(float))) splits = 1;
+  switch (variant) {
+    case 11: return launch_1x1<1, 32, PRO, POOL>(p, splits, s);
+    case 12: return launch_1x1<1, 64, PRO, POOL>(p, splits, s);
+    case 21: return launch_1x1<2, 32, PRO, POOL>(p, splits, s);
+    case 22: return launch_1x1<2, 64, PRO, POOL>(p, splits, s);
+    case 41: return launch_1x1<4, 32, PRO, POOL>(p, splits, s);
+    case 42: return launch_1x1<4, 64, PRO, POOL>(p, splits, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
-template <int TM>
+template <int TM, int G>
 int launch_3x3(Conv3x3Params p, hipStream_t s) {
   static bool attr = false;
   const int lds = kN3 * kWsK * 2;
   if (!attr) {
-    int rc = hipFuncSetAttribute((const void*)conv3x3_kernel<TM>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    int rc = hipFuncSetAttribute((const void*)conv3x3_kernel<TM, G>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (rc != hipSuccess) return rc;
     attr = true;
   }
   p.tiles = (p.M + 64 * TM - 1) / (64 * TM);
   const int grid = p.tiles < 512 ? p.tiles : 512;  // 2 resident blocks per CU (LDS-limited)
-  hipLaunchKernelGGL((conv3x3_kernel<TM>), dim3(grid), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((conv3x3_kernel<TM, G>), dim3(grid), dim3(256), lds, s, p);
   return hipGetLastError();
 }
 
@@ -442,9 +548,9 @@ extern "C" {
 // non-null) and 2x2 average pool (pool != 0; H, W = pre-pool dims, M = pooled
 // rows).  Requires K % 32 == 0, K <= 1024 when fused, N % 128 == 0,
 // ldx/ldy/y offsets multiples of 8 elements and 16-B aligned x/w.
-int tcamd_dn_conv1x1(const void* x, int ldx, int M, int K, const float* in_scale, const float* in_bias,
-                     const void* w, int N, const float* out_bias, int relu_out, void* y, int ldy, int pool, int H,
-                     int W, void* stream) {
+int tcamd_dn_conv1x1_ex(const void* x, int ldx, int M, int K, const float* in_scale, const float* in_bias,
+                        const void* w, int N, const float* out_bias, int relu_out, void* y, int ldy, int pool, int H,
+                        int W, int variant, int splits, void* ws, size_t ws_bytes, void* stream) {
   if (M <= 0) return hipSuccess;
   if (K % 32 || N % 128 || ldx % 8 || ldy % 4 || K > ldx) return hipErrorInvalidValue;
   const bool pro = in_scale != nullptr && in_bias != nullptr;
@@ -466,15 +572,32 @@ int tcamd_dn_conv1x1(const void* x, int ldx, int M, int K, const float* in_scale
   p.relu_out = relu_out;
   p.H = H;
   p.W = W;
+  p.ws = (float*)ws;
+  p.k_per_split = 0;
+  if (ws && ((uintptr_t)ws) % 16) return hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  if (pool) return pick_tm<true, true>(p, s);
-  if (pro) return pick_tm<true, false>(p, s);
-  return pick_tm<false, false>(p, s);
+  if (pool) return pick_1x1<true, true>(p, variant, splits, ws_bytes, s);
+  if (pro) return pick_1x1<true, false>(p, variant, splits, ws_bytes, s);
+  return pick_1x1<false, false>(p, variant, splits, ws_bytes, s);
+}
+
+int tcamd_dn_conv1x1_v(const void* x, int ldx, int M, int K, const float* in_scale, const float* in_bias,
+                       const void* w, int N, const float* out_bias, int relu_out, void* y, int ldy, int pool, int H,
+                       int W, int variant, void* stream) {
+  return tcamd_dn_conv1x1_ex(x, ldx, M, K, in_scale, in_bias, w, N, out_bias, relu_out, y, ldy, pool, H, W,
+                             variant, 1, nullptr, 0, stream);
+}
+
+int tcamd_dn_conv1x1(const void* x, int ldx, int M, int K, const float* in_scale, const float* in_bias,
+                     const void* w, int N, const float* out_bias, int relu_out, void* y, int ldy, int pool, int H,
+                     int W, void* stream) {
+  return tcamd_dn_conv1x1_v(x, ldx, M, K, in_scale, in_bias, w, N, out_bias, relu_out, y, ldy, pool, H, W, 0, stream);
 }
 
 // 3x3 conv 128->32, pad 1, over z [imgs*H*W][128]; w [32][3][3][128];
 // writes 32 channels per pixel at y + pixel*ldy.
-int tcamd_dn_conv3x3(const void* z, int imgs, int H, int W, const void* w, void* y, int ldy, void* stream) {
+int tcamd_dn_conv3x3_v(const void* z, int imgs, int H, int W, const void* w, void* y, int ldy, int variant,
+                       void* stream) {
   const long M = (long)imgs * H * W;
   if (M <= 0) return hipSuccess;
   if (M * kC3 * 2 >= 0x3ffff000L || ldy % 4) return hipErrorInvalidValue;
@@ -488,9 +611,19 @@ int tcamd_dn_conv3x3(const void* z, int imgs, int H, int W, const void* w, void*
   p.W = W;
   p.ldy = ldy;
   hipStream_t s = (hipStream_t)stream;
-  if ((M + 255) / 256 >= 512) return launch_3x3<4>(p, s);
-  if ((M + 127) / 128 >= 256) return launch_3x3<2>(p, s);
-  return launch_3x3<1>(p, s);
+  if (variant == 0) variant = 11;  // TM 1 measured fastest at every DenseNet shape (tools/kbench_densenet.py)
+  switch (variant) {
+    case 11: return launch_3x3<1, 1>(p, s);
+    case 13: return launch_3x3<1, 3>(p, s);
+    case 21: return launch_3x3<2, 1>(p, s);
+    case 23: return launch_3x3<2, 3>(p, s);
+    case 41: return launch_3x3<4, 1>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+int tcamd_dn_conv3x3(const void* z, int imgs, int H, int W, const void* w, void* y, int ldy, void* stream) {
+  return tcamd_dn_conv3x3_v(z, imgs, H, W, w, y, ldy, 0, stream);
 }
 
 int tcamd_dn_stem_pool(const void* x, const float* bias, void* y, int imgs, int H, int W, int C, int ldy,

@@ -58,6 +58,40 @@ def test_conv1x1_prologue_epilogue(M, K, ldx, N, off):
     assert (y[:, :off] == 7.0).all() and (y[:, off + N:] == 7.0).all()
 
 
+@pytest.mark.parametrize("M,K,N,pool,splits", [(49, 992, 128, 0, 0), (196, 640, 128, 0, 4), (49, 1024, 512, 1, 0),
+                                               (300, 96, 128, 0, 3), (1000, 512, 256, 0, 16)])
+@pytest.mark.parametrize("variant", [0, 11, 12, 21, 42])
+def test_conv1x1_split_k(M, K, N, pool, splits, variant):
+    """Split-K partials + reduce must equal the single-pass kernel's math."""
+    _need_gpu()
+    hip = _hip()
+    g = torch.Generator(device=DEV).manual_seed(K + N)
+    H = 14 if pool else 0
+    rows = M * 4 if pool else M
+    if pool:
+        M = 49
+        rows = 196
+    x = torch.randn(rows, K, device=DEV, generator=g).bfloat16()
+    s = torch.rand(K, device=DEV, generator=g) + 0.5
+    b = torch.randn(K, device=DEV, generator=g) * 0.2
+    w = (torch.randn(N, K, device=DEV, generator=g) / K ** 0.5).bfloat16()
+    ob = None if pool else torch.randn(N, device=DEV, generator=g)
+    ws = torch.empty(16 * M * N * 4, device=DEV, dtype=torch.uint8)
+    y = torch.zeros(M, N, device=DEV).bfloat16()
+    hip.dn_conv1x1(x.data_ptr(), K, M, K, s.data_ptr(), b.data_ptr(), w.data_ptr(), N,
+                   ob.data_ptr() if ob is not None else None, 0 if pool else 1, y.data_ptr(), N, pool=pool, H=H, W=H,
+                   variant=variant, splits=splits, ws=ws.data_ptr(), ws_bytes=ws.numel())
+    torch.cuda.synchronize()
+    a = torch.relu(x.float() * s + b)
+    if pool:
+        a = F.avg_pool2d(a.view(1, 14, 14, K).permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1).reshape(M, K)
+    a = a.bfloat16().float()
+    ref = a @ w.float().t()
+    if ob is not None:
+        ref = torch.relu(ref + ob)
+    _close(y, ref)
+
+
 def test_conv1x1_plain_gemm():
     _need_gpu()
     hip = _hip()

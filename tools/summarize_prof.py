@@ -9,8 +9,12 @@ import re
 
 
 def short(name, n=90):
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "", 1)
     name = re.sub(r"\(.*", "", name)
-    name = re.sub(r"<.*", "<...>", name)
+    if not name.startswith("at::"):  # keep our template args (tile variants), elide torch's
+        name = name if len(name) <= n else name[: n - 3] + "..."
+    else:
+        name = re.sub(r"<.*", "<...>", name)
     return name if len(name) <= n else name[: n - 3] + "..."
 
 

@@ -23,8 +23,11 @@ def main():
     rows = rows[cut + 1:]
     agg = collections.defaultdict(lambda: [0, 0])
     for r in rows:
-        n = re.sub(r"\(.*", "", r["Kernel_Name"])
-        n = re.sub(r"<.*", "<...>", n)[:90]
+        n = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "", 1)
+        n = re.sub(r"\(.*", "", n)
+        if n.startswith("at::"):
+            n = re.sub(r"<.*", "<...>", n)
+        n = n[:90]
         d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         agg[n][0] += 1
         agg[n][1] += d

@@ -98,6 +98,9 @@ class FusedDenseNet:
         h1 = self.block_dims[0][0]
         self.z = torch.empty(n * h1 * h1, BN_SIZE * GROWTH, device=dev, dtype=bf)
         self.pooled = torch.empty(n, self.num_features, device=dev, dtype=bf)
+        # split-K fp32 partials for the small-M 1x1 convs (K8 splits only while
+        # its grid is < 128 blocks, so splits * M * N <= 16 * 128 * 32 * 128)
+        self.ws = torch.empty(16 * 128 * 32 * 128 * 4, device=dev, dtype=torch.uint8)
 
     def with_workspace(self, max_batch=None):
         """A second engine sharing these weights with its own activation buffers,
@@ -129,14 +132,14 @@ class FusedDenseNet:
             for L in layers:
                 hip.dn_conv1x1(fp, ctot, M, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(), L["w1"].data_ptr(),
                                BN_SIZE * GROWTH, L["b1"].data_ptr(), 1, self.z.data_ptr(), BN_SIZE * GROWTH,
-                               stream=st)
+                               stream=st, ws=self.ws.data_ptr(), ws_bytes=self.ws.numel())
                 hip.dn_conv3x3(self.z.data_ptr(), b, hw, hw, L["w2"].data_ptr(), fp + 2 * L["cin"], ctot, stream=st)
             if bi < len(self.trans):
                 T = self.trans[bi]
                 nhw, nct = self.block_dims[bi + 1]
                 hip.dn_conv1x1(fp, ctot, b * nhw * nhw, ctot, T["s"].data_ptr(), T["t"].data_ptr(),
                                T["w"].data_ptr(), ctot // 2, None, 0, self.feat[bi + 1].data_ptr(), nct,
-                               pool=1, H=hw, W=hw, stream=st)
+                               pool=1, H=hw, W=hw, stream=st, ws=self.ws.data_ptr(), ws_bytes=self.ws.numel())
         hw4, c4 = self.block_dims[-1]
         hip.dn_head_pool(self.feat[-1].data_ptr(), self.s5.data_ptr(), self.t5.data_ptr(), self.pooled.data_ptr(),
                          b, hw4 * hw4, c4, stream=st)

@@ -117,6 +117,28 @@ _SIGS = {
         ],
         ctypes.c_int,
     ),
+    "tcamd_dn_conv1x1_ex": (
+        [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+            ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
+    "tcamd_dn_conv1x1_v": (
+        [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
+    "tcamd_dn_conv3x3_v": (
+        [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+         ctypes.c_int, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_dn_conv3x3": (
         [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
          ctypes.c_void_p],
@@ -428,15 +450,20 @@ def batched_copy(srcs, dsts, sizes, stream=None):
     _check(_load().tcamd_batched_copy(s, d, b, n, _vp(stream)), "batched_copy")
 
 
-def dn_conv1x1(x, ldx, M, K, in_scale, in_bias, w, N, out_bias, relu_out, y, ldy, pool=0, H=0, W=0, stream=None):
-    """K8: y[m, :N] = epi(relu(x[m, :K]*s + b) @ w[N, K]^T); pool=1 fuses a 2x2 avg-pool (transition)."""
-    _check(_load().tcamd_dn_conv1x1(x, ldx, M, K, in_scale, in_bias, w, N, out_bias, int(relu_out), y, ldy,
-                                    int(pool), H, W, _vp(stream)), "dn_conv1x1")
+def dn_conv1x1(x, ldx, M, K, in_scale, in_bias, w, N, out_bias, relu_out, y, ldy, pool=0, H=0, W=0, stream=None,
+               variant=0, splits=0, ws=None, ws_bytes=0):
+    """K8: y[m, :N] = epi(relu(x[m, :K]*s + b) @ w[N, K]^T); pool=1 fuses a 2x2 avg-pool (transition).
+    variant: 0 = heuristic, else 10*TM + BK/32 (tile-size override for benchmarking).
+    splits: split-K factor (0 = heuristic when a fp32 workspace ``ws`` of ``ws_bytes`` is given)."""
+    _check(_load().tcamd_dn_conv1x1_ex(x, ldx, M, K, in_scale, in_bias, w, N, out_bias, int(relu_out), y, ldy,
+                                       int(pool), H, W, int(variant), int(splits), ws, int(ws_bytes), _vp(stream)),
+           "dn_conv1x1")
 
 
-def dn_conv3x3(z, imgs, H, W, w, y, ldy, stream=None):
-    """K9: 3x3/pad-1 conv 128->32 over NHWC rows z; 32 channels per pixel written at y + pixel*ldy."""
-    _check(_load().tcamd_dn_conv3x3(z, imgs, H, W, w, y, ldy, _vp(stream)), "dn_conv3x3")
+def dn_conv3x3(z, imgs, H, W, w, y, ldy, stream=None, variant=0):
+    """K9: 3x3/pad-1 conv 128->32 over NHWC rows z; 32 channels per pixel written at y + pixel*ldy.
+    variant: 0 = heuristic, else 10*TM + taps-per-load-group."""
+    _check(_load().tcamd_dn_conv3x3_v(z, imgs, H, W, w, y, ldy, int(variant), _vp(stream)), "dn_conv3x3")
 
 
 def dn_stem_pool(x, bias, y, imgs, H, W, C, ldy, stream=None):
