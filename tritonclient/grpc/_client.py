@@ -82,6 +82,51 @@ def _to_json(msg):
     return json.loads(MessageToJson(msg, preserving_proto_field_name=True))
 
 
+# -- request builders shared with tritonclient.grpc.aio ------------------------------
+def _load_request(model_name, config=None, files=None):
+    req = service_pb2.RepositoryModelLoadRequest(model_name=model_name)
+    if config is not None:
+        req.parameters["config"].string_param = config
+    if files is not None:
+        for path, content in files.items():
+            req.parameters[path].bytes_param = content
+    return req
+
+
+def _unload_request(model_name, unload_dependents=False):
+    req = service_pb2.RepositoryModelUnloadRequest(model_name=model_name)
+    req.parameters["unload_dependents"].bool_param = unload_dependents
+    return req
+
+
+def _trace_request(model_name=None, settings=None):
+    req = service_pb2.TraceSettingRequest()
+    if model_name:
+        req.model_name = model_name
+    for key, value in (settings or {}).items():
+        if value is None:
+            req.settings[key]  # present-but-empty => clear
+        elif isinstance(value, (list, tuple)):
+            req.settings[key].value.extend([str(v) for v in value])
+        else:
+            req.settings[key].value.append(str(value))
+    return req
+
+
+def _log_request(settings=None):
+    req = service_pb2.LogSettingsRequest()
+    for key, value in (settings or {}).items():
+        if value is None:
+            req.settings[key]
+        elif key in ("log_file", "log_format"):
+            req.settings[key].string_param = value
+        elif key == "log_verbose_level":
+            req.settings[key].uint32_param = value
+        else:
+            req.settings[key].bool_param = value
+    return req
+
+
 class InferenceServerClient(InferenceServerClientBase):
     """gRPC client for a KServe-v2 / Triton server (``host:port``)."""
 
@@ -231,9 +276,8 @@ class InferenceServerClient(InferenceServerClientBase):
 
     def unload_model(self, model_name, headers=None, unload_dependents=False, client_timeout=None):
         """Unload a model (and optionally its dependents)."""
-        req = service_pb2.RepositoryModelUnloadRequest(model_name=model_name)
-        req.parameters["unload_dependents"].bool_param = unload_dependents
-        self._unary("RepositoryModelUnload", req, headers, client_timeout, verbose_tag="unload_model")
+        self._unary("RepositoryModelUnload", _unload_request(model_name, unload_dependents), headers,
+                    client_timeout, verbose_tag="unload_model")
         if self._verbose:
             print("Unloaded model '{}'".format(model_name))
 
@@ -251,17 +295,7 @@ class InferenceServerClient(InferenceServerClientBase):
         self, model_name=None, settings={}, headers=None, as_json=False, client_timeout=None
     ):
         """Update trace settings; a None value clears the setting."""
-        req = service_pb2.TraceSettingRequest()
-        if model_name:
-            req.model_name = model_name
-        for key, value in settings.items():
-            if value is None:
-                req.settings[key]  # present-but-empty => clear
-            elif isinstance(value, (list, tuple)):
-                req.settings[key].value.extend([str(v) for v in value])
-            else:
-                req.settings[key].value.append(str(value))
-        return self._unary("TraceSetting", req, headers, client_timeout, as_json)
+        return self._unary("TraceSetting", _trace_request(model_name, settings), headers, client_timeout, as_json)
 
     def get_trace_settings(self, model_name=None, headers=None, as_json=False, client_timeout=None):
         """Current trace settings."""
@@ -272,17 +306,7 @@ class InferenceServerClient(InferenceServerClientBase):
 
     def update_log_settings(self, settings, headers=None, as_json=False, client_timeout=None):
         """Update global log settings (typed per key as in the reference)."""
-        req = service_pb2.LogSettingsRequest()
-        for key, value in settings.items():
-            if value is None:
-                req.settings[key]
-            elif key in ("log_file", "log_format"):
-                req.settings[key].string_param = value
-            elif key == "log_verbose_level":
-                req.settings[key].uint32_param = value
-            else:
-                req.settings[key].bool_param = value
-        return self._unary("LogSettings", req, headers, client_timeout, as_json)
+        return self._unary("LogSettings", _log_request(settings), headers, client_timeout, as_json)
 
     def get_log_settings(self, headers=None, as_json=False, client_timeout=None):
         """Current global log settings."""

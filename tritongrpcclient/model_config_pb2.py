@@ -1,0 +1,10 @@
+"""Deprecated alias of ``tritonclient.grpc.model_config_pb2`` (reference package ``tritongrpcclient.model_config_pb2``)."""
+import warnings
+
+warnings.warn(
+    "The package `tritongrpcclient.model_config_pb2` is deprecated and will be removed in a future version. Please use instead `tritonclient.grpc.model_config_pb2`",
+    DeprecationWarning,
+    stacklevel=2,
+)
+
+from tritonclient.grpc.model_config_pb2 import *  # noqa: E402,F401,F403
