@@ -40,3 +40,19 @@ def cpu_server():
     h = ServerHandle().start()
     yield h
     h.stop()
+
+
+@pytest.fixture(scope="session")
+def gpu_server():
+    """The bench server as a child process on GPU 0 (GPU model zoo + a few CPU models)."""
+    from triton_client_amd.perf.harness import ServerProcess
+
+    log = os.path.join(os.environ.get("GRAFT_REPO_ROOT", REPO), "gpurun_out", "pytest_gpu_server.log")
+    os.makedirs(os.path.dirname(log), exist_ok=True)
+    srv = ServerProcess(device=0, models="simple,densenet_onnx,preprocess_inception,preprocess_inception_ensemble",
+                        log_path=log, extra_args=["--instance-count", "1"])
+    try:
+        srv.wait_ready(timeout=900, model="densenet_onnx")
+        yield srv
+    finally:
+        srv.stop()

@@ -1,0 +1,56 @@
+"""GPU examples: HIP (cuda-named) shared memory and DenseNet image
+classification (image_client / grpc_image_client / ensemble_image_client)
+against the GPU server."""
+
+import os
+
+import numpy as np
+import pytest
+
+from tests.test_examples import run_example
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def image_dir(tmp_path_factory):
+    from triton_client_amd.utils.image import encode_ppm
+
+    d = tmp_path_factory.mktemp("imgs")
+    rng = np.random.default_rng(3)
+    for i in range(3):
+        img = rng.integers(0, 255, size=(240 + 16 * i, 320, 3), dtype=np.uint8)
+        with open(os.path.join(d, "img%d.ppm" % i), "wb") as f:
+            f.write(encode_ppm(img))
+    return str(d)
+
+
+@pytest.mark.parametrize("script,proto", [("simple_http_cudashm_client.py", "http"),
+                                          ("simple_grpc_cudashm_client.py", "grpc")])
+def test_cudashm_examples(gpu_server, script, proto):
+    url = gpu_server.http_url if proto == "http" else gpu_server.grpc_url
+    r = run_example(script, url, [])
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]
+
+
+@pytest.mark.parametrize("proto,extra", [("http", []), ("grpc", ["-a"]), ("grpc", ["--streaming"]),
+                                         ("http", ["-a", "-b", "2"])])
+def test_image_client(gpu_server, image_dir, proto, extra):
+    url = gpu_server.http_url if proto == "http" else gpu_server.grpc_url
+    r = run_example("image_client.py", url, ["-m", "densenet_onnx", "-s", "INCEPTION", "-c", "3", "-i", proto]
+                    + extra + [image_dir], timeout=300)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]
+    assert r.stdout.count("class_") >= 3
+
+
+def test_grpc_image_client(gpu_server, image_dir):
+    r = run_example("grpc_image_client.py", gpu_server.grpc_url,
+                    ["-m", "densenet_onnx", "-c", "2", "-b", "2", os.path.join(image_dir, "img0.ppm")], timeout=300)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]
+
+
+@pytest.mark.parametrize("proto", ["http", "grpc"])
+def test_ensemble_image_client(gpu_server, image_dir, proto):
+    url = gpu_server.http_url if proto == "http" else gpu_server.grpc_url
+    r = run_example("ensemble_image_client.py", url, ["-c", "2", "-i", proto, image_dir], timeout=300)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]

@@ -80,19 +80,6 @@ def test_device_side_synthetic_and_bf16(hipshm):
     hipshm.destroy_shared_memory_region(h)
 
 
-@pytest.fixture(scope="module")
-def gpu_server():
-    from triton_client_amd.perf.harness import ServerProcess
-
-    log = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "pytest_gpu_server.log")
-    os.makedirs(os.path.dirname(log), exist_ok=True)
-    srv = ServerProcess(device=0, models="simple,densenet_onnx", log_path=log,
-                        extra_args=["--instance-count", "1"])
-    try:
-        srv.wait_ready(timeout=900, model="densenet_onnx")
-        yield srv
-    finally:
-        srv.stop()
 
 
 def test_simple_cudashm_grpc(gpu_server, hipshm):

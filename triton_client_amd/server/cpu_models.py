@@ -113,6 +113,11 @@ class IdentityFP32(Identity):
     max_batch_size = 0
 
 
+class IdentityInt8(Identity):
+    name = "identity_int8"
+    datatype = "INT8"
+
+
 class IdentityBF16(Identity):
     name = "identity_bf16"
     datatype = "BF16"
@@ -303,6 +308,7 @@ CPU_MODELS = [
     CustomIdentityInt32,
     IdentityFP32,
     IdentityBF16,
+    IdentityInt8,
     SimpleSequence,
     SimpleDynaSequence,
     SimpleStringDynaSequence,

@@ -319,4 +319,28 @@ class DensenetOnnx(Model):
         return self._server.shm_target(region, nbytes, offset)
 
 
-GPU_MODELS = [DensenetOnnx]
+class PreprocessInceptionEnsemble(Model):
+    """Ensemble: raw image bytes -> preprocess_inception -> densenet_onnx
+    (the model the reference's ensemble_image_client drives,
+    src/python/examples/ensemble_image_client.py)."""
+
+    name = "preprocess_inception_ensemble"
+    platform = "ensemble"
+    backend = ""
+    max_batch_size = 8
+    inputs = (TensorSpec("INPUT", "BYTES", [1]),)
+    outputs = (TensorSpec("OUTPUT", "FP32", [1000], label_filename="densenet_labels.txt"),)
+    ensemble_steps = [
+        ("preprocess_inception", {"INPUT": "INPUT"}, {"OUTPUT": "preprocessed_image"}),
+        ("densenet_onnx", {"data_0": "preprocessed_image"}, {"fc6_1": "OUTPUT"}),
+    ]
+    labels = DensenetOnnx.labels
+
+    def load(self):
+        pass
+
+    def execute(self, requests):  # pragma: no cover - the server runs ensembles step by step
+        raise ServerError("ensemble models are scheduled by the server")
+
+
+GPU_MODELS = [DensenetOnnx, PreprocessInceptionEnsemble]
