@@ -33,6 +33,11 @@ def load_image(path):
             return decode_image(f.read())
 
 
+def completion_callback(user_data, result, error):
+    """async_infer / stream callback: the client calls it as callback(result=..., error=...)."""
+    user_data.put(error if error else result)
+
+
 def parse_model(metadata, config, protocol):
     """-> (max_batch_size, input_name, output_name, c, h, w, format, dtype)."""
     if protocol == "grpc":
@@ -147,7 +152,7 @@ def main():
     responses = []
     if a.streaming:
         q = queue.Queue()
-        client.start_stream(partial(lambda qq, r, e: qq.put(e if e else r), q))
+        client.start_stream(partial(completion_callback, q))
         for i, (inp, out) in enumerate(requests):
             client.async_stream_infer(a.model_name, inp, request_id=str(i), model_version=a.model_version,
                                       outputs=out)
@@ -162,7 +167,7 @@ def main():
         if protocol == "grpc":
             q = queue.Queue()
             for i, (inp, out) in enumerate(requests):
-                client.async_infer(a.model_name, inp, partial(lambda qq, r, e: qq.put(e if e else r), q),
+                client.async_infer(a.model_name, inp, partial(completion_callback, q),
                                    request_id=str(i), model_version=a.model_version, outputs=out)
             for _ in requests:
                 r = q.get(timeout=120)

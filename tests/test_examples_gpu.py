@@ -54,3 +54,34 @@ def test_ensemble_image_client(gpu_server, image_dir, proto):
     url = gpu_server.http_url if proto == "http" else gpu_server.grpc_url
     r = run_example("ensemble_image_client.py", url, ["-c", "2", "-i", proto, image_dir], timeout=300)
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]
+
+
+# -- C++ examples ------------------------------------------------------------------
+@pytest.mark.parametrize("name,proto", [("simple_http_cudashm_client", "http"),
+                                        ("simple_grpc_cudashm_client", "grpc")])
+def test_cpp_cudashm_examples(gpu_server, name, proto):
+    from tests.test_cpp_examples import run_bin
+
+    url = gpu_server.http_url if proto == "http" else gpu_server.grpc_url
+    r = run_bin(name, url, [])
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]
+
+
+@pytest.mark.parametrize("proto,extra", [("http", []), ("grpc", ["-a"]), ("grpc", ["--streaming", "-b", "2"])])
+def test_cpp_image_client(gpu_server, image_dir, proto, extra):
+    from tests.test_cpp_examples import run_bin
+
+    url = gpu_server.http_url if proto == "http" else gpu_server.grpc_url
+    r = run_bin("image_client", url, ["-m", "densenet_onnx", "-s", "INCEPTION", "-c", "3", "-i", proto] + extra
+                + [image_dir], timeout=300)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]
+
+
+@pytest.mark.parametrize("proto", ["http", "grpc"])
+def test_cpp_ensemble_image_client(gpu_server, image_dir, proto):
+    from tests.test_cpp_examples import run_bin
+
+    url = gpu_server.http_url if proto == "http" else gpu_server.grpc_url
+    r = run_bin("ensemble_image_client", url, ["-c", "2", "-i", proto, os.path.join(image_dir, "img1.ppm")],
+                timeout=300)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]
