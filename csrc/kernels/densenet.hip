@@ -301,6 +301,7 @@ struct Conv3x3Params {
   uint16_t* y;         // [M][ldy], already offset to the first output channel
   int M, H, W, ldy;
   int tiles;           // ceil(M / (64*TM))
+  int ablate;          // diagnostics only (tools/kbench_densenet.py): bit0 drop activation loads, bit1 drop stores
 };
 
 // Persistent blocks: weights loaded to LDS once, then the block walks pixel
@@ -317,7 +318,8 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(Conv3x3Params p) {
   __syncthreads();
 
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.z, (short)0,
-                                                      (int)((size_t)p.M * kC3 * 2), 0x00020000);
+                                                      (p.ablate & 1) ? 0 : (int)((size_t)p.M * kC3 * 2),
+                                                      0x00020000);
   const int HW = p.H * p.W;
   const int fr = lane & 15, fk = 8 * (lane >> 4);
   for (int tile = blockIdx.x; tile < p.tiles; tile += gridDim.x) {
@@ -363,7 +365,76 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(Conv3x3Params p) {
           for (int i = 0; i < TM; ++i) acc[j][i] = mfma16(fa[j], as_frag(src[i][c]), acc[j][i]);
       }
     };
-    if constexpr (G == 1) {
+    if constexpr (G >= 4) {
+      // tap-major steps of 32 channels with a G-deep load ring: G * TM 16-B
+      // loads in flight per lane to cover L2 latency at 2 waves / SIMD
+      auto load_step = [&](int st, v4u (&dst)[TM]) {
+        const int tap = st >> 2, c = st & 3;
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int hh = ph[i] + dy, ww = pw[i] + dx;
+          const bool ok = pm[i] >= 0 && hh >= 0 && hh < p.H && ww >= 0 && ww < p.W;
+          const int off = ok ? ((pm[i] + dy * p.W + dx) * kC3 + fk) * 2 : 0x40000000;
+          dst[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + c * 64, 0, 0);
+        }
+      };
+      v4u ring[G][TM];
+#pragma unroll
+      for (int st = 0; st < G; ++st) load_step(st, ring[st]);
+#pragma unroll 1
+      for (int s0 = 0; s0 < 36; s0 += G) {
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+          const int st = s0 + u;
+          const int tap = st >> 2, c = st & 3;
+          bf16x8 fa[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            fa[j] = *reinterpret_cast<const bf16x8*>(&Ws[(j * 16 + fr) * kWsK + tap * kC3 + c * 32 + fk]);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < TM; ++i) acc[j][i] = mfma16(fa[j], as_frag(ring[u][i]), acc[j][i]);
+          if (st + G < 36) load_step(st + G, ring[u]);
+        }
+      }
+    } else if constexpr (G == 0) {
+      // channel-major order: for each 32-channel chunk walk all 9 taps, so the
+      // 3 input rows touched by a tile stay L1-resident across the taps
+      // (working set (64 + 2W + 2) x 64 B instead of x 256 B); 4 steps in flight.
+      auto load_step = [&](int st, v4u (&dst)[TM]) {
+        const int c = st / 9, tap = st - c * 9;
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int hh = ph[i] + dy, ww = pw[i] + dx;
+          const bool ok = pm[i] >= 0 && hh >= 0 && hh < p.H && ww >= 0 && ww < p.W;
+          const int off = ok ? ((pm[i] + dy * p.W + dx) * kC3 + fk) * 2 : 0x40000000;
+          dst[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + c * 64, 0, 0);
+        }
+      };
+      v4u ring[4][TM];
+#pragma unroll
+      for (int st = 0; st < 4; ++st) load_step(st, ring[st]);
+#pragma unroll 1
+      for (int s0 = 0; s0 < 36; s0 += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int st = s0 + u;
+          const int c = st / 9, tap = st - c * 9;
+          bf16x8 fa[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            fa[j] = *reinterpret_cast<const bf16x8*>(&Ws[(j * 16 + fr) * kWsK + tap * kC3 + c * 32 + fk]);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < TM; ++i) acc[j][i] = mfma16(fa[j], as_frag(ring[u][i]), acc[j][i]);
+          if (st + 4 < 36) load_step(st + 4, ring[u]);
+        }
+      }
+    } else if constexpr (G == 1) {
       // taps in ping-pong pairs: tap t+1's fragments load while tap t multiplies
       v4u xa[TM][4], xb[TM][4];
       load_tap(0, xa);
@@ -391,6 +462,13 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(Conv3x3Params p) {
 #pragma unroll
       for (int t = 0; t < 3; ++t) mma_tap(6 + t, ga[t]);
     }
+    if (p.ablate & 2) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(acc[j][i]));
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int nb = j * 16 + (lane >> 4) * 4;
@@ -401,6 +479,177 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(Conv3x3Params p) {
           *reinterpret_cast<v2u*>(p.y + (size_t)pm[i] * p.ldy + nb) = v2u{pack2(v[0], v[1]), pack2(v[2], v[3])};
         }
       }
+    }
+  }
+}
+
+// K9b: the same conv on v_mfma_f32_32x32x16_bf16 with the weights as operand A.
+// One 32x16 weight slab (all 32 output channels) is ONE ds_read_b128 per
+// lane and is reused by the wave's TM 32-pixel subtiles, so LDS traffic per
+// MFMA drops 4-8x against the 16x16x32 form (which needs 2 weight fragments
+// per 2 MFMAs).  Wave tile: 32*TM pixels x 32 channels; block: 4 waves.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int TM>
+__global__ void __launch_bounds__(256) conv3x3_m32_kernel(Conv3x3Params p) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t Ws[];  // [32][kWsK]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int c = tid; c < kN3 * (kK3 / 8); c += 256) {
+    const int n = c / (kK3 / 8), kc = (c - n * (kK3 / 8)) * 8;
+    *reinterpret_cast<v4u*>(&Ws[n * kWsK + kc]) = ldg16(p.w + (size_t)n * kK3 + kc);
+  }
+  __syncthreads();
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.z, (short)0,
+                                                      (int)((size_t)p.M * kC3 * 2), 0x00020000);
+  const int HW = p.H * p.W;
+  const int col = lane & 31, kh = 8 * (lane >> 5);
+  for (int tile = blockIdx.x; tile < p.tiles; tile += gridDim.x) {
+    const int mb = tile * (128 * TM) + wave * 32 * TM;
+    int pm[TM], ph[TM], pw[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = mb + i * 32 + col;
+      pm[i] = m < p.M ? m : -1;
+      const int mm = m < p.M ? m : 0;
+      const int img = mm / HW, r = mm - img * HW;
+      ph[i] = r / p.W;
+      pw[i] = r - ph[i] * p.W;
+    }
+    f32x16 acc[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+
+    // per tap: 8 k-steps of 16 channels; lane fetches 16 B = 8 channels of its pixel
+    auto load_tap = [&](int tap, v4u (&dst)[TM][8]) {
+      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int hh = ph[i] + dy, ww = pw[i] + dx;
+        const bool ok = pm[i] >= 0 && hh >= 0 && hh < p.H && ww >= 0 && ww < p.W;
+        const int off = ok ? ((pm[i] + dy * p.W + dx) * kC3 + kh) * 2 : 0x40000000;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) dst[i][c] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + c * 32, 0, 0);
+      }
+    };
+    auto mma_tap = [&](int tap, const v4u (&src)[TM][8]) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ws[col * kWsK + tap * kC3 + c * 16 + kh]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i] = mfma32(a, as_frag(src[i][c]), acc[i]);
+      }
+    };
+    v4u xa[TM][8], xb[TM][8];
+    load_tap(0, xa);
+#pragma unroll 1
+    for (int tap = 0; tap < 8; tap += 2) {
+      load_tap(tap + 1, xb);
+      mma_tap(tap, xa);
+      load_tap(tap + 2, xa);
+      mma_tap(tap + 1, xb);
+    }
+    mma_tap(8, xa);
+    // C/D: col = pixel (lane & 31); reg r -> channel (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if (pm[i] < 0) continue;
+      uint16_t* yp = p.y + (size_t)pm[i] * p.ldy + 4 * (lane >> 5);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<v2u*>(yp + 8 * g) =
+            v2u{pack2(acc[i][4 * g], acc[i][4 * g + 1]), pack2(acc[i][4 * g + 2], acc[i][4 * g + 3])};
+    }
+  }
+}
+
+// K9c: LDS-staged activations.  Profiling (ablation in tools/kbench_densenet.py)
+// showed K9's time is 60% fragment-shaped activation fetches: every input
+// pixel is pulled through L1 9x (once per tap) in 64-B pieces.  Here a block
+// stages the contiguous pixel band its 128 output pixels need ([m0-W-1,
+// m0+128+W+1), 272-B padded rows: conflict-free b128 reads) into LDS once,
+// with full-row coalesced loads that are issued for the NEXT tile while the
+// current one computes; all 9 taps then read LDS.  Weights stay LDS-resident
+// (74 KB) and feed v_mfma_f32_32x32x16_bf16 as operand A; one 32-pixel
+// subtile per wave.  Out-of-image taps are zeroed by a per-tap mask.
+constexpr int kActStride = kC3 + 8;  // 272-B rows
+constexpr int kTileP = 128;          // output pixels per tile (4 waves x 32)
+
+__global__ void __launch_bounds__(256) conv3x3_lds_kernel(Conv3x3Params p) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Ws = smem;                   // [32][kWsK]
+  uint16_t* As = smem + kN3 * kWsK;      // [rows][kActStride]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int c = tid; c < kN3 * (kK3 / 8); c += 256) {
+    const int n = c / (kK3 / 8), kc = (c - n * (kK3 / 8)) * 8;
+    *reinterpret_cast<v4u*>(&Ws[n * kWsK + kc]) = ldg16(p.w + (size_t)n * kK3 + kc);
+  }
+  const int W = p.W, HW = p.H * p.W;
+  const int halo = W + 1, rows = kTileP + 2 * halo, chunks = rows * 16;
+  constexpr int kMaxChunks = (kTileP + 2 * 57) * 16;       // W <= 56
+  constexpr int CPT = (kMaxChunks + 255) / 256;           // 16-B chunks per thread
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.z, (short)0,
+                                                      (int)((size_t)p.M * kC3 * 2), 0x00020000);
+  v4u st[CPT];
+  auto load_tile = [&](int tile) {
+    const int base = tile * kTileP - halo;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + i * 256;
+      const int r = c >> 4, q = c & 15;
+      const int pix = base + r;
+      const bool ok = c < chunks && pix >= 0 && pix < p.M;
+      st[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? (pix * kC3 + q * 8) * 2 : 0x40000000, 0, 0);
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + i * 256;
+      if (c < chunks) *reinterpret_cast<v4u*>(&As[(c >> 4) * kActStride + (c & 15) * 8]) = st[i];
+    }
+  };
+  const int col = lane & 31, kh = 8 * (lane >> 5);
+  int tile = blockIdx.x;
+  if (tile < p.tiles) load_tile(tile);
+  for (; tile < p.tiles; tile += gridDim.x) {
+    __syncthreads();  // previous tile's LDS reads done (and, first time, weights staged)
+    store_tile();
+    __syncthreads();
+    if (tile + (int)gridDim.x < p.tiles) load_tile(tile + gridDim.x);
+    const int tp = wave * 32 + col;  // tile-relative output pixel of this lane
+    const int m = tile * kTileP + tp;
+    const int mm = m < p.M ? m : 0;
+    const int img = mm / HW, rr = mm - img * HW;
+    const int h = rr / W, w = rr - h * W;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+      const bool ok = m < p.M && h + dy >= 0 && h + dy < p.H && w + dx >= 0 && w + dx < W;
+      const uint16_t* arow = &As[(tp + halo + dy * W + dx) * kActStride + kh];
+      const uint16_t* wrow = &Ws[col * kWsK + tap * kC3 + kh];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        v4u b = *reinterpret_cast<const v4u*>(arow + c * 16);
+        if (!ok) b = v4u{0, 0, 0, 0};
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(wrow + c * 16);
+        acc = mfma32(a, as_frag(b), acc);
+      }
+    }
+    if (m < p.M) {
+      uint16_t* yp = p.y + (size_t)m * p.ldy + 4 * (lane >> 5);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<v2u*>(yp + 8 * g) =
+            v2u{pack2(acc[4 * g], acc[4 * g + 1]), pack2(acc[4 * g + 2], acc[4 * g + 3])};
     }
   }
 }
@@ -540,6 +789,37 @@ int launch_3x3(Conv3x3Params p, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int TM>
+int launch_3x3_m32(Conv3x3Params p, hipStream_t s) {
+  static bool attr = false;
+  const int lds = kN3 * kWsK * 2;
+  if (!attr) {
+    int rc = hipFuncSetAttribute((const void*)conv3x3_m32_kernel<TM>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (rc != hipSuccess) return rc;
+    attr = true;
+  }
+  p.tiles = (p.M + 128 * TM - 1) / (128 * TM);
+  const int grid = p.tiles < 512 ? p.tiles : 512;
+  hipLaunchKernelGGL((conv3x3_m32_kernel<TM>), dim3(grid), dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
+int launch_3x3_lds(Conv3x3Params p, hipStream_t s) {
+  if (p.W > 56) return hipErrorInvalidValue;
+  const int lds = (kN3 * kWsK + (kTileP + 2 * (p.W + 1)) * kActStride) * 2;
+  static int attr = 0;
+  if (attr < lds) {
+    int rc = hipFuncSetAttribute((const void*)conv3x3_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (kN3 * kWsK + (kTileP + 2 * 57) * kActStride) * 2);
+    if (rc != hipSuccess) return rc;
+    attr = (kN3 * kWsK + (kTileP + 2 * 57) * kActStride) * 2;
+  }
+  p.tiles = (p.M + kTileP - 1) / kTileP;
+  const int grid = p.tiles < 256 ? p.tiles : 256;  // one resident block per CU (LDS-limited)
+  hipLaunchKernelGGL(conv3x3_lds_kernel, dim3(grid), dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
@@ -603,6 +883,8 @@ int tcamd_dn_conv3x3_v(const void* z, int imgs, int H, int W, const void* w, voi
   if (M * kC3 * 2 >= 0x3ffff000L || ldy % 4) return hipErrorInvalidValue;
   if (((uintptr_t)z | (uintptr_t)w) % 16 || ((uintptr_t)y) % 8) return hipErrorInvalidValue;
   Conv3x3Params p;
+  p.ablate = variant / 1000;
+  variant %= 1000;
   p.z = (const uint16_t*)z;
   p.w = (const uint16_t*)w;
   p.y = (uint16_t*)y;
@@ -611,13 +893,25 @@ int tcamd_dn_conv3x3_v(const void* z, int imgs, int H, int W, const void* w, voi
   p.W = W;
   p.ldy = ldy;
   hipStream_t s = (hipStream_t)stream;
-  if (variant == 0) variant = 11;  // TM 1 measured fastest at every DenseNet shape (tools/kbench_densenet.py)
+  // heuristic from tools/kbench_densenet.py on MI355X: the LDS-staged kernel
+  // wins once there are enough 128-pixel tiles to fill the CUs; tiny problems
+  // keep the 64-pixel-tile direct-load kernel
+  if (variant == 0) variant = (W <= 56 && (M + 127) / 128 >= 96) ? 60 : 11;
   switch (variant) {
+    case 10: return launch_3x3<1, 0>(p, s);  // channel-major tap walk
+    case 16: return launch_3x3<1, 6>(p, s);   // 6-deep load ring
+    case 19: return launch_3x3<1, 12>(p, s);  // 12-deep load ring
+    case 29: return launch_3x3<2, 12>(p, s);
+    case 26: return launch_3x3<2, 6>(p, s);
+    case 20: return launch_3x3<2, 0>(p, s);
     case 11: return launch_3x3<1, 1>(p, s);
     case 13: return launch_3x3<1, 3>(p, s);
     case 21: return launch_3x3<2, 1>(p, s);
     case 23: return launch_3x3<2, 3>(p, s);
     case 41: return launch_3x3<4, 1>(p, s);
+    case 60: return launch_3x3_lds(p, s);     // LDS-staged activations, 32x32x16 MFMA
+    case 51: return launch_3x3_m32<1>(p, s);  // 32x32x16 MFMA, 32 px / wave
+    case 52: return launch_3x3_m32<2>(p, s);  // 32x32x16 MFMA, 64 px / wave
     default: return hipErrorInvalidValue;
   }
 }

@@ -125,8 +125,9 @@ def test_conv1x1_transition_pool(imgs, H, C, N):
     assert (y[:, N:] == 0).all()
 
 
+@pytest.mark.parametrize("variant", [0, 10, 11, 13, 16, 19, 21, 41, 51, 52, 60])
 @pytest.mark.parametrize("imgs,H", [(1, 7), (3, 14), (8, 56), (48, 56), (5, 28)])
-def test_conv3x3(imgs, H):
+def test_conv3x3(imgs, H, variant):
     _need_gpu()
     hip = _hip()
     g = torch.Generator(device=DEV).manual_seed(imgs * 100 + H)
@@ -135,7 +136,7 @@ def test_conv3x3(imgs, H):
     wt = w.permute(0, 2, 3, 1).contiguous()
     ldy = 96
     y = torch.full((imgs * H * H, ldy), -3.0, device=DEV).bfloat16()
-    hip.dn_conv3x3(z.data_ptr(), imgs, H, H, wt.data_ptr(), y.data_ptr() + 2 * 32, ldy)
+    hip.dn_conv3x3(z.data_ptr(), imgs, H, H, wt.data_ptr(), y.data_ptr() + 2 * 32, ldy, variant=variant)
     torch.cuda.synchronize()
     ref = F.conv2d(z.float().permute(0, 3, 1, 2), w.float(), padding=1).permute(0, 2, 3, 1).reshape(-1, 32)
     _close(y[:, 32:64], ref)

@@ -15,7 +15,7 @@ import torch
 from triton_client_amd.ops import hip
 
 V1 = (11, 12, 21, 22, 41, 42)
-V3 = (11, 13, 21, 23, 41)
+V3 = (0, 11, 60)
 
 
 def cs():
