@@ -100,6 +100,45 @@ def _p2p_star(region, nbytes, dist):
     return "p2p"
 
 
+def fanout_host(buf, src=0):
+    """Replicate a host buffer (e.g. a system shared-memory region's numpy
+    view) from rank ``src`` to every rank with one collective broadcast
+    (gloo on CPU hosts, or RCCL when the process group is nccl — the tensor is
+    then staged through the GPU)."""
+    import torch
+
+    dist = _dist()
+    if dist is None or dist.get_world_size() == 1:
+        return "local"
+    t = torch.from_numpy(np.asarray(buf).view(np.uint8).reshape(-1))
+    if dist.get_backend() == "gloo":
+        dist.broadcast(t, src=src)
+    else:
+        d = t.cuda()
+        dist.broadcast(d, src=src)
+        t.copy_(d.cpu())
+    return dist.get_backend()
+
+
+def verify_host_replicas(buf, sample=4096):
+    """Every rank checks a strided sample of a host buffer against rank 0's."""
+    import torch
+
+    dist = _dist()
+    if dist is None:
+        return True
+    a = np.asarray(buf).view(np.uint8).reshape(-1)
+    idx = np.linspace(0, a.size - 1, min(sample, a.size)).astype(np.int64)
+    s = torch.from_numpy(a[idx].astype(np.int64))
+    ref = s.clone()
+    dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+    ref = ref.to(dev)
+    dist.broadcast(ref, src=0)
+    flag = torch.tensor([1 if torch.equal(s, ref.cpu()) else 0], device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item())
+
+
 def verify_replicas(region, nbytes, sample=4096):
     """Every rank checks a strided sample of its region against rank 0's."""
     import torch
