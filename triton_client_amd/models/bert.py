@@ -1,0 +1,98 @@
+"""BERT-large (SQuAD head) for the ``bert_large`` bench model (random-init).
+
+Public BERT-large architecture: vocab 30522, hidden 1024, 24 layers, 16
+heads, FFN 4096, GELU, post-LN, max 512 positions, 2 token types; the
+question-answering head maps every token to (start, end) logits.  Weights are
+random (seeded, std 0.02 as in BERT's initializer) — there is no checkpoint
+on the box.
+
+Compute layout for MI355X: bf16 everywhere, fused QKV projection (one
+[3H, H] GEMM per layer instead of three), attention through
+``F.scaled_dot_product_attention`` with an additive key-padding mask (the
+fused attention kernels of torch-ROCm), plain GEMMs on hipBLASLt.  The
+serving wrapper captures one HIP graph per batch bucket.
+"""
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+VOCAB = 30522
+HIDDEN = 1024
+LAYERS = 24
+HEADS = 16
+FFN = 4096
+MAX_POS = 512
+TYPES = 2
+
+
+class _Layer(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.qkv = nn.Linear(HIDDEN, 3 * HIDDEN)
+        self.out = nn.Linear(HIDDEN, HIDDEN)
+        self.ln1 = nn.LayerNorm(HIDDEN, eps=1e-12)
+        self.ffn1 = nn.Linear(HIDDEN, FFN)
+        self.ffn2 = nn.Linear(FFN, HIDDEN)
+        self.ln2 = nn.LayerNorm(HIDDEN, eps=1e-12)
+
+    def forward(self, x, bias):
+        b, s, _ = x.shape
+        q, k, v = self.qkv(x).view(b, s, 3, HEADS, HIDDEN // HEADS).permute(2, 0, 3, 1, 4)
+        a = F.scaled_dot_product_attention(q, k, v, attn_mask=bias)
+        x = self.ln1(x + self.out(a.transpose(1, 2).reshape(b, s, HIDDEN)))
+        return self.ln2(x + self.ffn2(F.gelu(self.ffn1(x))))
+
+
+class BertLargeQA(nn.Module):
+    def __init__(self, layers=LAYERS):
+        super().__init__()
+        self.word = nn.Embedding(VOCAB, HIDDEN)
+        self.pos = nn.Embedding(MAX_POS, HIDDEN)
+        self.type = nn.Embedding(TYPES, HIDDEN)
+        self.ln = nn.LayerNorm(HIDDEN, eps=1e-12)
+        self.layers = nn.ModuleList(_Layer() for _ in range(layers))
+        self.qa = nn.Linear(HIDDEN, 2)
+
+    def forward(self, input_ids, attention_mask, token_type_ids):
+        b, s = input_ids.shape
+        pos = torch.arange(s, device=input_ids.device)
+        x = self.ln(self.word(input_ids) + self.pos(pos)[None] + self.type(token_type_ids))
+        # additive key-padding mask [b, 1, 1, s] in the compute dtype
+        bias = ((1.0 - attention_mask[:, None, None, :].to(x.dtype)) * -10000.0).to(x.dtype)
+        for layer in self.layers:
+            x = layer(x, bias)
+        logits = self.qa(x).float()
+        return logits[..., 0], logits[..., 1]
+
+
+def init_weights(model, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, (nn.Linear, nn.Embedding)):
+                m.weight.copy_(torch.randn(m.weight.shape, generator=g) * 0.02)
+                if isinstance(m, nn.Linear) and m.bias is not None:
+                    m.bias.zero_()
+            elif isinstance(m, nn.LayerNorm):
+                m.weight.fill_(1.0)
+                m.bias.zero_()
+
+
+def build(device="cuda", dtype=torch.bfloat16, seed=0, layers=LAYERS):
+    model = BertLargeQA(layers)
+    init_weights(model, seed)
+    return model.eval().to(device=device, dtype=dtype)
+
+
+def flops_per_sequence(seq=384, layers=LAYERS):
+    """Forward FLOPs of one sequence (GEMMs + attention), for reporting."""
+    gemm = 2 * seq * (HIDDEN * 3 * HIDDEN + HIDDEN * HIDDEN + 2 * HIDDEN * FFN)
+    attn = 2 * 2 * seq * seq * HIDDEN
+    return layers * (gemm + attn) + 2 * seq * HIDDEN * 2
+
+
+def _check_head_dim():
+    assert HIDDEN % HEADS == 0 and math.log2(HIDDEN // HEADS).is_integer()

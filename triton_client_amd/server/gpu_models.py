@@ -343,4 +343,239 @@ class PreprocessInceptionEnsemble(Model):
         raise ServerError("ensemble models are scheduled by the server")
 
 
-GPU_MODELS = [DensenetOnnx, PreprocessInceptionEnsemble]
+class BertLarge(Model):
+    """``bert_large`` — BERT-large SQuAD-style QA (models/bert.py), the model of
+    BASELINE.json's concurrency-sweep config.  INT32 [384] input_ids /
+    attention_mask / token_type_ids in, FP32 [384] start/end logits out;
+    dynamic batching into HIP-graph buckets.  Inputs from device shm are
+    gathered with K7 batched_copy (one launch per input tensor), outputs are
+    scattered the same way; both the Python scheduler and the native front end
+    (execute_native) use it."""
+
+    name = "bert_large"
+    platform = "pytorch_libtorch"
+    backend = "pytorch"
+    max_batch_size = 64
+    SEQ = 384
+    inputs = (TensorSpec("input_ids", "INT32", [384]), TensorSpec("attention_mask", "INT32", [384]),
+              TensorSpec("token_type_ids", "INT32", [384]))
+    outputs = (TensorSpec("start_logits", "FP32", [384]), TensorSpec("end_logits", "FP32", [384]))
+    dynamic_batching = {"preferred": [], "max_queue_delay_us": 1000}
+    instance_kind = "KIND_GPU"
+    instance_count = 1
+    supports_native = True
+    BUCKETS = (1, 2, 4, 8, 16, 32, 64)
+
+    def __init__(self, version=1, device_id=0, use_graphs=True, layers=24, **kw):
+        super().__init__(version, **kw)
+        self.device_id = int(kw.get("device", device_id))
+        self.use_graphs = use_graphs
+        self.layers = int(layers)
+        self._slots = []
+        self._free = []
+        self._cv = threading.Condition()
+
+    def load(self):
+        import torch
+
+        from triton_client_amd.models import bert
+        from triton_client_amd.ops import hip
+
+        if not torch.cuda.is_available():
+            raise ServerError("bert_large requires a GPU")
+        hip.lib()
+        torch.cuda.set_device(self.device_id)
+        self.torch = torch
+        dev = torch.device("cuda", self.device_id)
+        self.model = bert.build(device=dev, layers=self.layers)
+        for _ in range(max(1, self.instance_count)):
+            self._slots.append(self._make_slot(dev))
+        self._free = list(range(len(self._slots)))
+
+    def _make_slot(self, dev):
+        torch = self.torch
+        from triton_client_amd.ops import hip
+
+        n, s = self.max_batch_size, self.SEQ
+        slot = {"stream": torch.cuda.Stream(device=dev), "graphs": {},
+                "ins": [torch.zeros(n, s, device=dev, dtype=torch.int32) for _ in range(3)],
+                "outs": [torch.zeros(n, s, device=dev, dtype=torch.float32) for _ in range(2)],
+                "ev": [torch.cuda.Event(enable_timing=True) for _ in range(4)]}
+        slot["ins"][1].fill_(1)
+        slot["stage_host"] = hip.host_alloc(3 * n * s * 4)
+        slot["out_host"] = hip.host_alloc(2 * n * s * 4)
+
+        def run(b):
+            ids, mask, tt = (t[:b] for t in slot["ins"])
+            # synthetic load generators send arbitrary INT32: keep indices in range
+            # (an out-of-range embedding index is a device fault, not an error)
+            st, en = self.model(ids.long().remainder(30522), mask.clamp(0, 1), tt.long().clamp(0, 1))
+            slot["outs"][0][:b].copy_(st)
+            slot["outs"][1][:b].copy_(en)
+
+        slot["run"] = run
+        with torch.cuda.stream(slot["stream"]), torch.no_grad():
+            for b in self.BUCKETS:
+                run(b)
+                if self.use_graphs:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=slot["stream"]):
+                        run(b)
+                    slot["graphs"][b] = g
+        slot["stream"].synchronize()
+        return slot
+
+    def unload(self):
+        from triton_client_amd.ops import hip
+
+        for sl in self._slots:
+            for k in ("stage_host", "out_host"):
+                try:
+                    hip.host_free(sl[k])
+                except Exception:
+                    pass
+        self._slots = []
+
+    def _acquire(self):
+        with self._cv:
+            while not self._free:
+                self._cv.wait()
+            return self._free.pop()
+
+    def _release(self, i):
+        with self._cv:
+            self._free.append(i)
+            self._cv.notify()
+
+    def _run_batch(self, slot, srcs, outs, total):
+        """srcs: per input a list of (kind, ptr, rows) in row order; outs: per
+        output a list of (kind, ptr, first_row, rows).  Returns timings (ns)."""
+        import ctypes
+
+        from triton_client_amd.ops import hip
+
+        row = self.SEQ * 4
+        bucket = next(b for b in self.BUCKETS if b >= total)
+        stream = slot["stream"]
+        sh = stream.cuda_stream
+        ev = slot["ev"]
+        ev[0].record(stream)
+        for k, parts in enumerate(srcs):
+            base = slot["ins"][k].data_ptr()
+            c_src, c_dst, c_n = [], [], []
+            host_off = 0
+            first = 0
+            stage = slot["stage_host"] + k * self.max_batch_size * row
+            for kind, ptr, rows in parts:
+                if kind == 1:
+                    c_src.append(ptr)
+                    c_dst.append(base + first * row)
+                    c_n.append(rows * row)
+                else:
+                    ctypes.memmove(stage + host_off, ptr, rows * row)
+                    hip.memcpy_async(base + first * row, stage + host_off, rows * row, sh)
+                    host_off += rows * row
+                first += rows
+            if c_src:
+                hip.batched_copy(c_src, c_dst, c_n, sh)
+            if bucket > total:  # padding rows: keep them deterministic (mask 1, ids 0)
+                hip.memset_async(base + total * row, 0, (bucket - total) * row, sh)
+        ev[1].record(stream)
+        with self.torch.cuda.stream(stream), self.torch.no_grad():
+            if self.use_graphs:
+                slot["graphs"][bucket].replay()
+            else:
+                slot["run"](bucket)
+        ev[2].record(stream)
+        host_outs = []
+        for k, parts in enumerate(outs):
+            base = slot["outs"][k].data_ptr()
+            c_src, c_dst, c_n = [], [], []
+            for kind, ptr, first, rows in parts:
+                if not ptr:
+                    continue
+                if kind == 1:
+                    c_src.append(base + first * row)
+                    c_dst.append(ptr)
+                    c_n.append(rows * row)
+                else:
+                    host_outs.append((k, ptr, first, rows))
+            if c_src:
+                hip.batched_copy(c_src, c_dst, c_n, sh)
+        if host_outs:
+            for k in range(2):
+                hip.memcpy_async(slot["out_host"] + k * self.max_batch_size * row, slot["outs"][k].data_ptr(),
+                                 total * row, sh)
+        ev[3].record(stream)
+        hip.stream_synchronize(sh)
+        for k, ptr, first, rows in host_outs:
+            ctypes.memmove(ptr, slot["out_host"] + k * self.max_batch_size * row + first * row, rows * row)
+        return [int(ev[0].elapsed_time(ev[1]) * 1e6), int(ev[1].elapsed_time(ev[2]) * 1e6),
+                int(ev[2].elapsed_time(ev[3]) * 1e6)]
+
+    def execute_native(self, instance, b):
+        total = int(b.total_rows)
+        if total > self.max_batch_size:
+            raise ServerError("batch of %d rows exceeds max_batch_size" % total)
+        srcs = [[] for _ in range(3)]
+        outs = [[] for _ in range(2)]
+        first = 0
+        for r in range(b.n_requests):
+            rows = int(b.rows[r])
+            for k in range(3):
+                ref = b.inputs[r * b.n_inputs + k]
+                srcs[k].append((ref.kind, ref.ptr, rows))
+            for k in range(2):
+                ref = b.outputs[r * b.n_outputs + k]
+                outs[k].append((ref.kind, ref.ptr, first, rows))
+            first += rows
+        i = self._acquire()
+        try:
+            t = self._run_batch(self._slots[i], srcs, outs, total)
+        finally:
+            self._release(i)
+        for k in range(3):
+            b.timing_ns[k] = t[k]
+
+    def execute(self, requests):
+        import ctypes
+
+        total = 0
+        plan = []
+        for r in requests:
+            n = int(r.input("input_ids").shape[0])
+            plan.append((r, total, n))
+            total += n
+        if total > self.max_batch_size:
+            return [ServerError("batch of %d rows exceeds max_batch_size" % total)] * len(requests)
+        names = [s.name for s in self.inputs]
+        srcs = [[] for _ in range(3)]
+        keep = []
+        for r, first, n in plan:
+            for k, nm in enumerate(names):
+                t = r.input(nm)
+                if isinstance(t.data, DeviceView):
+                    srcs[k].append((1, t.data.ptr, n))
+                else:
+                    a = np.ascontiguousarray(t.data, dtype=np.int32)
+                    keep.append(a)
+                    srcs[k].append((0, a.ctypes.data, n))
+        # outputs come back to host; shm targets are filled by the server (deliver_to_shm)
+        res = np.empty((2, total, self.SEQ), dtype=np.float32)
+        outs = [[(0, res[k].ctypes.data, 0, total)] for k in range(2)]
+        i = self._acquire()
+        try:
+            t = self._run_batch(self._slots[i], srcs, outs, total)
+        finally:
+            self._release(i)
+        if self._batch_stats is not None:
+            self._batch_stats(total, len(requests), *t)
+        del ctypes
+        return [[OutputTensor("start_logits", "FP32", [n, self.SEQ], res[0, f:f + n]),
+                 OutputTensor("end_logits", "FP32", [n, self.SEQ], res[1, f:f + n])] for _, f, n in plan]
+
+    _batch_stats = None
+    reports_batch_stats = True
+
+
+GPU_MODELS = [DensenetOnnx, PreprocessInceptionEnsemble, BertLarge]
