@@ -51,7 +51,7 @@ class BertLargeQA(nn.Module):
         super().__init__()
         self.word = nn.Embedding(VOCAB, HIDDEN)
         self.pos = nn.Embedding(MAX_POS, HIDDEN)
-        self.type = nn.Embedding(TYPES, HIDDEN)
+        self.tok_type = nn.Embedding(TYPES, HIDDEN)
         self.ln = nn.LayerNorm(HIDDEN, eps=1e-12)
         self.layers = nn.ModuleList(_Layer() for _ in range(layers))
         self.qa = nn.Linear(HIDDEN, 2)
@@ -59,7 +59,7 @@ class BertLargeQA(nn.Module):
     def forward(self, input_ids, attention_mask, token_type_ids):
         b, s = input_ids.shape
         pos = torch.arange(s, device=input_ids.device)
-        x = self.ln(self.word(input_ids) + self.pos(pos)[None] + self.type(token_type_ids))
+        x = self.ln(self.word(input_ids) + self.pos(pos)[None] + self.tok_type(token_type_ids))
         # additive key-padding mask [b, 1, 1, s] in the compute dtype
         bias = ((1.0 - attention_mask[:, None, None, :].to(x.dtype)) * -10000.0).to(x.dtype)
         for layer in self.layers:
