@@ -77,8 +77,9 @@ def main():
             print(json.dumps({k: p.get(k) for k in ("model", "conc", "throughput", "p99_us", "error")}), flush=True)
     finally:
         srv.stop()
-    sha = subprocess.run(["git", "rev-parse", "--short", "HEAD"], cwd=REPO, capture_output=True,
-                         text=True).stdout.strip() or "unknown"
+    # the GPU box gets a snapshot without .git: pass the SHA in (TC_GIT_SHA=$(git rev-parse --short HEAD))
+    sha = os.environ.get("TC_GIT_SHA") or subprocess.run(
+        ["git", "rev-parse", "--short", "HEAD"], cwd=REPO, capture_output=True, text=True).stdout.strip() or "unknown"
     with open(a.out, "w") as f:
         f.write("# perf_analyzer sweep on 1x MI355X (measured)\n\n")
         f.write("git %s; server: `python -m triton_client_amd.server --gpu --models densenet_onnx,bert_large "
