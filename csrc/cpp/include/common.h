@@ -22,6 +22,17 @@
 #include <unordered_map>
 #include <vector>
 
+
+/// Friend hook (reference src/c++/library/common.h:42-47,358-361,462-464): a
+/// translation unit that defines TRITON_INFERENCE_SERVER_CLIENT_CLASS before
+/// including this header (an in-process backend, a white-box test) is granted
+/// access to the private state of the request/tensor classes.
+#ifdef TRITON_INFERENCE_SERVER_CLIENT_CLASS
+#define TC_CLIENT_FRIEND friend class TRITON_INFERENCE_SERVER_CLIENT_CLASS;
+#else
+#define TC_CLIENT_FRIEND
+#endif
+
 namespace triton { namespace client {
 
 constexpr char kInferHeaderContentLengthHTTPHeader[] = "Inference-Header-Content-Length";
@@ -150,6 +161,7 @@ class InferInput {
   Error GetNext(const uint8_t** buf, size_t* input_bytes, bool* end_of_input);
 
  private:
+  TC_CLIENT_FRIEND
   InferInput(const std::string& name, const std::vector<int64_t>& dims, const std::string& datatype);
 
   std::string name_;
@@ -184,6 +196,7 @@ class InferRequestedOutput {
   Error SetBinaryData(const bool binary_data);
 
  private:
+  TC_CLIENT_FRIEND
   explicit InferRequestedOutput(const std::string& name, const std::string& datatype, const size_t class_count = 0);
   std::string name_;
   std::string datatype_;

@@ -9,6 +9,9 @@
 // typed gtest suite).  No gtest on the box: a tiny CHECK harness instead.
 #include <unistd.h>
 
+// white-box access through the C10 friend hook (see include/common.h)
+#define TRITON_INFERENCE_SERVER_CLIENT_CLASS InternalsProbe
+
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -23,6 +26,18 @@
 #include "shm_utils.h"
 
 namespace tc = triton::client;
+
+namespace triton { namespace client {
+// Granted friendship by TRITON_INFERENCE_SERVER_CLIENT_CLASS.
+class InternalsProbe {
+ public:
+  static size_t BufferCount(const InferInput* in) { return in->bufs_.size(); }
+  static size_t StringBufferCount(const InferInput* in) { return in->str_bufs_.size(); }
+  static bool IsShm(const InferInput* in) { return in->io_type_ == InferInput::SHARED_MEMORY; }
+  static size_t ByteSize(const InferInput* in) { return in->byte_size_; }
+  static size_t ShmOffset(const InferRequestedOutput* out) { return out->shm_offset_; }
+};
+}}  // namespace triton::client
 
 static int g_failures = 0;
 static int g_checks = 0;
@@ -474,6 +489,35 @@ TestHttpSpecific(tc::InferenceServerHttpClient* c)
   CHECK(logs.find("\"log_verbose_level\":1") != std::string::npos, "log settings " << logs);
 }
 
+// InferInput buffer chain state, through the friend hook (reference
+// src/c++/tests/cc_client_test.cc:29-33 uses the same mechanism).
+static void
+TestFriendHook()
+{
+  using P = tc::InternalsProbe;
+  tc::InferInput* in;
+  CHECK_OK(tc::InferInput::Create(&in, "X", {1, 4}, "INT32"), "create");
+  std::unique_ptr<tc::InferInput> own(in);
+  std::vector<uint8_t> a(8), b(8);
+  CHECK_OK(in->AppendRaw(a), "append a");
+  CHECK_OK(in->AppendRaw(b), "append b");
+  CHECK(P::BufferCount(in) == 2 && P::ByteSize(in) == 16, "two buffers, 16 bytes");
+  CHECK_OK(in->Reset(), "reset");
+  CHECK(P::BufferCount(in) == 0 && P::ByteSize(in) == 0, "reset clears the chain");
+  CHECK_OK(in->SetSharedMemory("r", 16, 0), "shm");
+  CHECK(P::IsShm(in) && P::BufferCount(in) == 0, "shm input has no buffers");
+  tc::InferInput* s;
+  CHECK_OK(tc::InferInput::Create(&s, "S", {2}, "BYTES"), "create bytes");
+  std::unique_ptr<tc::InferInput> own_s(s);
+  CHECK_OK(s->AppendFromString({"ab", "cde"}), "append strings");
+  CHECK(P::StringBufferCount(s) == 1 && P::ByteSize(s) == 4 + 2 + 4 + 3, "strings owned by the input");
+  tc::InferRequestedOutput* o;
+  CHECK_OK(tc::InferRequestedOutput::Create(&o, "Y"), "output");
+  std::unique_ptr<tc::InferRequestedOutput> own_o(o);
+  CHECK_OK(o->SetSharedMemory("r", 64, 32), "output shm");
+  CHECK(P::ShmOffset(o) == 32, "output shm offset");
+}
+
 int
 main(int argc, char** argv)
 {
@@ -489,6 +533,7 @@ main(int argc, char** argv)
     std::function<void()> fn;
   };
   std::vector<T> tests = {
+      {"friend hook", [&] { TestFriendHook(); }},
       {"health/metadata", [&] { TestHealthAndMetadata(http.get(), "http"); TestHealthAndMetadata(grpc.get(), "grpc"); }},
       {"infer", [&] { TestInfer(http.get(), "http"); TestInfer(grpc.get(), "grpc"); }},
       {"async/multi", [&] { TestAsyncAndMulti(http.get(), "http"); TestAsyncAndMulti(grpc.get(), "grpc"); }},

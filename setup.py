@@ -55,6 +55,19 @@ def _native_payload():
     return files
 
 
+def _packages():
+    """All packages, minus the protocols disabled by the CMake options
+    TRITON_ENABLE_PYTHON_{HTTP,GRPC} (passed through the environment)."""
+    pk = find_packages(include=["tritonclient*", "triton_client_amd*", "tritonclientutils",
+                                "tritonhttpclient", "tritongrpcclient", "tritonshmutils"])
+    off = lambda k: os.environ.get(k, "ON").upper() in ("OFF", "0", "FALSE", "NO")
+    if off("TRITON_ENABLE_PYTHON_HTTP"):
+        pk = [p for p in pk if not (p.startswith("tritonclient.http") or p == "tritonhttpclient")]
+    if off("TRITON_ENABLE_PYTHON_GRPC"):
+        pk = [p for p in pk if not (p.startswith("tritonclient.grpc") or p == "tritongrpcclient")]
+    return pk
+
+
 if __name__ == "__main__":
     setup(
         name="tritonclient",
@@ -71,8 +84,7 @@ if __name__ == "__main__":
             "Programming Language :: Python :: 3",
             "Operating System :: POSIX :: Linux",
         ],
-        packages=find_packages(include=["tritonclient*", "triton_client_amd*", "tritonclientutils",
-                                        "tritonhttpclient", "tritongrpcclient", "tritonshmutils"]),
+        packages=_packages(),
         install_requires=install_requires,
         extras_require=extras_require,
         package_data={

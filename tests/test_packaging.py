@@ -37,3 +37,16 @@ def test_deprecated_shims_warn_and_reexport():
             m = importlib.import_module(mod)
         assert hasattr(m, attr), (mod, attr)
         assert any(issubclass(x.category, DeprecationWarning) for x in w), mod
+
+
+def test_protocol_options_trim_packages():
+    code = "import setup; print(','.join(setup._packages()))"
+    env = dict(os.environ, TRITON_ENABLE_PYTHON_GRPC="OFF")
+    out = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True, env=env,
+                         check=True).stdout
+    pk = out.strip().split(",")
+    assert "tritonclient.http" in pk and "tritonclient.grpc" not in pk and "tritongrpcclient" not in pk
+    env = dict(os.environ, TRITON_ENABLE_PYTHON_HTTP="OFF")
+    pk = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True, env=env,
+                        check=True).stdout.strip().split(",")
+    assert "tritonclient.grpc" in pk and "tritonclient.http.aio" not in pk
