@@ -23,6 +23,20 @@ LoadEngine::LoadEngine(const Options& o, Backend* be, DataSet* data, size_t max_
     uint64_t us;
     while (f >> us) intervals_ns_.push_back(us * 1000);
   }
+  // async requests spread over several protocol clients (one connection and
+  // one I/O thread each), so neither side funnels every tensor through one
+  // socket: slot i uses client i % n (--num-clients; auto = min(slots, 4))
+  if (o.async && !o.streaming) {
+    size_t n = o.num_clients > 0 ? static_cast<size_t>(o.num_clients) : std::min<size_t>(slots_.size(), 4);
+    n = std::max<size_t>(1, std::min(n, slots_.size()));
+    clients_.push_back(be_);
+    for (size_t i = 1; i < n; ++i) {
+      std::unique_ptr<Backend> b;
+      if (!Backend::Create(o_, &b).IsOk()) break;
+      clients_.push_back(b.get());
+      owned_.push_back(std::move(b));
+    }
+  }
   if (o.async || o.streaming) worker_ = std::thread(&LoadEngine::Worker, this);
 }
 
@@ -35,6 +49,8 @@ LoadEngine::~LoadEngine()
   }
   cv_.notify_all();
   if (worker_.joinable()) worker_.join();
+  clients_.clear();
+  owned_.clear();  // after the worker: completions may still reference them
 }
 
 void LoadEngine::Stop()
@@ -119,8 +135,9 @@ Error LoadEngine::Issue(size_t slot)
       stream_ids_.erase(id);
     }
   } else {
-    e = be_->AsyncInfer([this, slot, t](InferResult* r) { OnComplete(slot, t, r); }, s.opt, data_->Inputs(),
-                        data_->Outputs(slot));
+    Backend* be = clients_.empty() ? be_ : clients_[slot % clients_.size()];
+    e = be->AsyncInfer([this, slot, t](InferResult* r) { OnComplete(slot, t, r); }, s.opt, data_->Inputs(),
+                       data_->Outputs(slot));
   }
   if (!e.IsOk()) {
     {

@@ -231,6 +231,8 @@ class LoadEngine {
 
   Options o_;
   Backend* be_;
+  std::vector<Backend*> clients_;                // async issue targets (clients_[0] == be_)
+  std::vector<std::unique_ptr<Backend>> owned_;  // clients_[1..]
   DataSet* data_;
   std::vector<Slot> slots_;
   std::mutex mu_;

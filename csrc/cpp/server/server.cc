@@ -5,6 +5,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <nghttp2/nghttp2.h>
+#include <pthread.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
@@ -104,7 +105,8 @@ struct PendingReq {
   std::vector<std::string> out_region;
   std::vector<int64_t> out_region_bytes, out_region_offset;
   std::vector<std::string> host_out;  // host output buffers (non-shm)
-  std::vector<std::string> host_in;   // raw_input_contents kept alive
+  std::string body;                   // request message; raw inputs point into it
+  std::vector<std::pair<int, size_t>> host_in_off;  // (input index, offset of its bytes in body)
   uint64_t t_arrive = 0;
 };
 
@@ -218,7 +220,7 @@ class Server {
   std::atomic<int> next_loop{0};
 
  private:
-  bool TryNative(Conn* c, Stream* st, const std::string& raw);
+  bool TryNative(Conn* c, Stream* st, const char* msg, size_t len, std::string* owner);
   void Proxy(Conn* c, Stream* st, bool streaming);
   std::shared_ptr<tc::H2Channel> Upstream();
   void Worker(std::shared_ptr<NativeModel> m, int instance);
@@ -351,7 +353,14 @@ static int OnDataChunk(nghttp2_session*, uint8_t, int32_t stream_id, const uint8
   auto it = c->streams.find(stream_id);
   if (it == c->streams.end()) return 0;
   Stream* st = it->second.get();
+  const bool was_short = st->inbuf.size() < 5;
   st->inbuf.append(reinterpret_cast<const char*>(data), len);
+  if (was_short && !st->streaming_rpc && st->inbuf.size() >= 5) {
+    // unary: size the buffer for the whole message now (no regrowth copies)
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(st->inbuf.data());
+    const size_t n = (size_t(p[1]) << 24) | (size_t(p[2]) << 16) | (size_t(p[3]) << 8) | p[4];
+    if (n < (size_t(1) << 31)) st->inbuf.reserve(5 + n);
+  }
   if (st->streaming_rpc) {
     std::vector<std::string> msgs;
     std::string err;
@@ -564,6 +573,7 @@ void Loop::DoAccept()
 
 void Loop::Run()
 {
+  pthread_setname_np(pthread_self(), ("tcs-loop" + std::to_string(idx_)).c_str());
   epoll_event evs[64];
   while (!stop_) {
     int n = epoll_wait(ep_, evs, 64, 200);
@@ -712,14 +722,25 @@ void Server::OnRequestComplete(Conn* c, Stream* st)
   if (st->started) return;
   st->started = true;
   if (st->path == kInferPath) {
+    const std::string& in = st->inbuf;
+    if (in.size() >= 5 && in[0] == 0) {
+      // one uncompressed message: parse it in place (raw tensors are not copied)
+      const uint8_t* p = reinterpret_cast<const uint8_t*>(in.data());
+      const uint32_t n = (uint32_t(p[1]) << 24) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 8) | p[4];
+      if (in.size() == 5 + static_cast<size_t>(n)) {
+        if (TryNative(c, st, in.data() + 5, n, &st->inbuf)) return;
+        Proxy(c, st, false);  // forward the frame as received
+        return;
+      }
+    }
     std::vector<std::string> msgs;
     std::string err;
     if (!PopMessages(st, &msgs, &err) || msgs.size() != 1) {
       Reply(c, st, nullptr, kInternal, err.empty() ? "expected one request message" : err);
       return;
     }
-    if (TryNative(c, st, msgs[0])) return;
-    // not native: forward the message we already popped
+    if (TryNative(c, st, msgs[0].data(), msgs[0].size(), &msgs[0])) return;
+    // not native: forward the (decompressed) message we already popped
     st->inbuf.clear();
     tc::GrpcFrame(msgs[0], tc::GrpcCompression::NONE, &st->inbuf);
   }
@@ -813,10 +834,62 @@ NativeModel* Server::FindModel(const std::string& name)
   return it == models.end() ? nullptr : it->second.get();
 }
 
-bool Server::TryNative(Conn* c, Stream* st, const std::string& raw)
+// Splits a serialized ModelInferRequest into its small fields (copied to
+// `small`) and the byte ranges of its raw_input_contents (field 7), so the
+// tensors can be used where they arrived instead of being copied by the parser.
+static bool SplitRawInputs(const char* p, size_t n, std::string* small, std::vector<std::pair<size_t, size_t>>* raws)
+{
+  size_t pos = 0;
+  auto varint = [&](uint64_t* v) {
+    *v = 0;
+    for (int shift = 0; shift < 64; shift += 7) {
+      if (pos >= n) return false;
+      const uint8_t b = static_cast<uint8_t>(p[pos++]);
+      *v |= static_cast<uint64_t>(b & 0x7f) << shift;
+      if (!(b & 0x80)) return true;
+    }
+    return false;
+  };
+  small->reserve(4096);
+  while (pos < n) {
+    const size_t start = pos;
+    uint64_t tag, v;
+    if (!varint(&tag)) return false;
+    switch (tag & 7) {
+      case 0:
+        if (!varint(&v)) return false;
+        break;
+      case 1:
+        pos += 8;
+        break;
+      case 5:
+        pos += 4;
+        break;
+      case 2:
+        if (!varint(&v) || v > n - pos) return false;
+        if ((tag >> 3) == 7) {
+          raws->emplace_back(pos, static_cast<size_t>(v));
+          pos += v;
+          continue;
+        }
+        pos += v;
+        break;
+      default:
+        return false;
+    }
+    if (pos > n) return false;
+    small->append(p + start, pos - start);
+  }
+  return true;
+}
+
+bool Server::TryNative(Conn* c, Stream* st, const char* msg, size_t len, std::string* owner)
 {
   inference::ModelInferRequest req;
-  if (!req.ParseFromString(raw)) return false;
+  std::string small;
+  std::vector<std::pair<size_t, size_t>> raws;  // offsets relative to msg
+  if (!SplitRawInputs(msg, len, &small, &raws) || !req.ParseFromString(small)) return false;
+  const size_t msg_off = static_cast<size_t>(msg - owner->data());
   std::shared_ptr<NativeModel> m;
   {
     std::lock_guard<std::mutex> lk(models_mu);
@@ -907,13 +980,13 @@ bool Server::TryNative(Conn* c, Stream* st, const std::string& raw)
       ref.ptr = e.ptr + roff;
       ref.bytes = need;
     } else {
-      if (raw_idx >= req.raw_input_contents_size()) return fail("input '" + d.name + "' has no data");
-      pr->host_in.push_back(req.raw_input_contents(raw_idx++));
-      if (pr->host_in.back().size() != need)
-        return fail("unexpected byte size for input '" + d.name + "'");
+      if (raw_idx >= static_cast<int>(raws.size())) return fail("input '" + d.name + "' has no data");
+      const auto& rv = raws[raw_idx++];
+      if (rv.second != need) return fail("unexpected byte size for input '" + d.name + "'");
+      pr->host_in_off.emplace_back(idx, msg_off + rv.first);  // pointer fixed up once the body is owned
       ref.kind = 0;
       ref.device = 0;
-      ref.ptr = reinterpret_cast<uint64_t>(pr->host_in.back().data());
+      ref.ptr = 0;
       ref.bytes = need;
     }
   }
@@ -983,6 +1056,11 @@ bool Server::TryNative(Conn* c, Stream* st, const std::string& raw)
       pr->out[k] = tcserve_ref{0, 0, reinterpret_cast<uint64_t>(&pr->host_out[k][0]), need};
     }
   }
+  if (!pr->host_in_off.empty()) {
+    pr->body = std::move(*owner);  // the heap buffer moves with the string: offsets stay valid
+    for (const auto& io : pr->host_in_off)
+      pr->in[io.first].ptr = reinterpret_cast<uint64_t>(pr->body.data() + io.second);
+  }
   n_native++;
   {
     std::lock_guard<std::mutex> lk(m->mu);
@@ -995,6 +1073,7 @@ bool Server::TryNative(Conn* c, Stream* st, const std::string& raw)
 
 void Server::Worker(std::shared_ptr<NativeModel> m, int instance)
 {
+  pthread_setname_np(pthread_self(), ("tcs-w" + std::to_string(instance) + "-" + m->name).substr(0, 15).c_str());
   while (true) {
     std::vector<std::unique_ptr<PendingReq>> batch;
     {

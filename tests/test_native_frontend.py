@@ -148,3 +148,29 @@ def test_unload_reload_reregisters(cpu_server):
     r = c.infer("add_sub_batched", _inputs(a, a))
     np.testing.assert_array_equal(r.as_numpy("OUTPUT0"), a * 2)
     assert nf.counters()["native_requests"] == before + 1
+
+
+def test_fast_path_large_inband_tensor(cpu_server):
+    """frontend_sink: 600 KB/row in-band tensors parsed in place (no copy of
+    raw_input_contents) for several batch sizes and compressed requests."""
+    nf = cpu_server.server.native_frontend
+    c = grpcclient.InferenceServerClient(cpu_server.grpc_url)
+    before = nf.counters()["native_requests"]
+    rng = np.random.default_rng(0)
+    for rows in (1, 3, 8):
+        x = rng.standard_normal((rows, 3, 224, 224)).astype(np.float32)
+        i = grpcclient.InferInput("data_0", list(x.shape), "FP32")
+        i.set_data_from_numpy(x)
+        for comp in (None, "gzip"):
+            r = c.infer("frontend_sink", [i], compression_algorithm=comp)
+            y = r.as_numpy("fc6_1")
+            assert y.shape == (rows, 1000)
+            np.testing.assert_array_equal(y, np.repeat(x.reshape(rows, -1)[:, :1], 1000, axis=1))
+    assert nf.counters()["native_requests"] - before == 6
+    # a wrong byte size is rejected by the fast path with the Python server's message
+    x = np.zeros((1, 3, 224, 224), np.float32)
+    i = grpcclient.InferInput("data_0", [2, 3, 224, 224], "FP32")
+    i.set_data_from_numpy(np.zeros((2, 3, 224, 224), np.float32))
+    i._raw_content = x.tobytes()
+    with pytest.raises(InferenceServerException, match="unexpected byte size"):
+        c.infer("frontend_sink", [i])

@@ -300,7 +300,45 @@ class AddSubBatched(Model):
         b.timing_ns[2] = 0
 
 
+class FrontendSink(Model):
+    """densenet_onnx-shaped model that does no compute: FP32 [3,224,224] in,
+    FP32 [1000] out (first input value broadcast).  Served natively, it
+    measures what the tcserve front end and the transport alone sustain for
+    the headline request shape, with no GPU involved."""
+
+    name = "frontend_sink"
+    max_batch_size = 8
+    inputs = (TensorSpec("data_0", "FP32", [3, 224, 224]),)
+    outputs = (TensorSpec("fc6_1", "FP32", [1000]),)
+    dynamic_batching = {"preferred": [], "max_queue_delay_us": 100}
+    instance_count = 2
+    supports_native = True
+
+    def execute(self, requests):
+        out = []
+        for r in requests:
+            x = r.input("data_0").numpy()
+            out.append([self.out("fc6_1", np.repeat(x.reshape(x.shape[0], -1)[:, :1], 1000, axis=1))])
+        return out
+
+    def execute_native(self, instance, b):
+        import ctypes
+
+        for r in range(b.n_requests):
+            rows = b.rows[r]
+            src, dst = b.inputs[r], b.outputs[r]
+            if src.kind != 0 or (dst.ptr and dst.kind != 0):
+                raise ServerError("frontend_sink runs on host memory only")
+            if not dst.ptr:
+                continue
+            x = np.ctypeslib.as_array((ctypes.c_float * (rows * 3 * 224 * 224)).from_address(src.ptr))
+            y = np.ctypeslib.as_array((ctypes.c_float * (rows * 1000)).from_address(dst.ptr)).reshape(rows, 1000)
+            y[:] = x.reshape(rows, -1)[:, :1]
+        b.timing_ns[0] = b.timing_ns[1] = b.timing_ns[2] = 0
+
+
 CPU_MODELS = [
+    FrontendSink,
     SimpleAddSub,
     OnnxInt32,
     SimpleString,

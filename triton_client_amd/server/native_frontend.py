@@ -85,7 +85,12 @@ def _strs(xs):
 
 
 class NativeFrontend:
-    def __init__(self, server, host, port, upstream_port, io_threads=2):
+    def __init__(self, server, host, port, upstream_port, io_threads=None):
+        if io_threads is None:
+            # one epoll loop per connection group; in-band tensors cost ~1 core
+            # per 2 GB/s, so scale with the CPUs this process may use (2..8)
+            io_threads = int(os.environ.get("TCSERVE_IO_THREADS", "0")) or max(
+                2, min(8, len(os.sched_getaffinity(0)) // 4))
         lib = _load()
         err = ctypes.create_string_buffer(512)
         h = lib.tcserve_create(host.encode(), int(port), b"127.0.0.1", int(upstream_port), int(io_threads), err, 512)
