@@ -292,6 +292,157 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 
+
+// ============================================================================
+// K8s: small-M 1x1 conv.  Block = 32 pixels x 128 output channels; the four
+// waves split K (wave w takes the 32-wide K chunks w, w+4, ...), so the
+// serial load -> MFMA chain per wave is 4x shorter than in K8, where the
+// waves split the tile and each walks all of K.  The partial tiles are summed
+// through LDS in two rounds (waves 2,3 -> 0,1, then 1 -> 0) and wave 0 runs
+// the epilogue.  Operands come straight from global memory (L2-resident
+// weights, one pass over the activations), so no LDS staging is needed.
+// ============================================================================
+template <bool POOL>
+__global__ void __launch_bounds__(256) conv1x1_sk_kernel(Conv1x1Params p) {
+  constexpr int NS = POOL ? 4 : 1;
+  __shared__ __attribute__((aligned(16))) f32x4 red[2][16][64];  // [slot][frag][lane], 32 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 128;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const int KC = p.K / 32;
+
+  // this lane's two activation rows (POOL: the 2x2 windows' 4 rows each)
+  const uint16_t* a_src[2][NS];
+  bool a_ok[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + 16 * i + fr;
+    a_ok[i] = m < p.M;
+    const int mm = a_ok[i] ? m : 0;
+    if constexpr (POOL) {
+      const int wo = p.W >> 1, ho = p.H >> 1;
+      const int img = mm / (ho * wo), r = mm - img * ho * wo;
+      const int oh = r / wo, ow = r - oh * wo;
+      const size_t base = ((size_t)img * p.H + 2 * oh) * p.W + 2 * ow;
+      a_src[i][0] = p.x + base * p.ldx + fk;
+      a_src[i][1] = p.x + (base + 1) * p.ldx + fk;
+      a_src[i][2] = p.x + (base + p.W) * p.ldx + fk;
+      a_src[i][3] = p.x + (base + p.W + 1) * p.ldx + fk;
+    } else {
+      a_src[i][0] = p.x + (size_t)mm * p.ldx + fk;
+    }
+  }
+  const uint16_t* w_src = p.w + (size_t)(n0 + fr) * p.K + fk;
+
+  struct Raw {
+    v4u w[8];
+    v4u a[2][NS];
+    f32x4 s0, s1, t0, t1;
+  };
+  auto load = [&](int c, Raw& r) {
+    const int k0 = 32 * c;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r.w[j] = ldg16(w_src + (size_t)16 * j * p.K + k0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < NS; ++q) r.a[i][q] = a_ok[i] ? ldg16(a_src[i][q] + k0) : v4u{0, 0, 0, 0};
+    r.s0 = *reinterpret_cast<const f32x4*>(p.in_scale + k0 + fk);
+    r.s1 = *reinterpret_cast<const f32x4*>(p.in_scale + k0 + fk + 4);
+    r.t0 = *reinterpret_cast<const f32x4*>(p.in_bias + k0 + fk);
+    r.t1 = *reinterpret_cast<const f32x4*>(p.in_bias + k0 + fk + 4);
+  };
+
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](const Raw& r) {
+    const float sc[8] = {r.s0[0], r.s0[1], r.s0[2], r.s0[3], r.s1[0], r.s1[1], r.s1[2], r.s1[3]};
+    const float sh[8] = {r.t0[0], r.t0[1], r.t0[2], r.t0[3], r.t1[0], r.t1[1], r.t1[2], r.t1[3]};
+    bf16x8 af[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = 0.f;
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        float f[8];
+        unpack8(r.a[i][q], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float t = fmaxf(f[e] * sc[e] + sh[e], 0.f);
+          o[e] += POOL ? 0.25f * t : t;
+        }
+      }
+      af[i] = as_frag(pack8(o));
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[j][i] = mfma16(as_frag(r.w[j]), af[i], acc[j][i]);
+  };
+
+  Raw cur, nxt;
+  int c = wave;
+  if (c < KC) load(c, cur);
+  for (; c < KC; c += 4) {
+    if (c + 4 < KC) load(c + 4, nxt);
+    compute(cur);
+    cur = nxt;
+  }
+
+  // cross-wave reduction: 2,3 -> 0,1 ; 1 -> 0
+  if (wave >= 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) red[wave - 2][j * 2 + i][lane] = acc[j][i];
+  }
+  __syncthreads();
+  if (wave < 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[j][i] += red[wave][j * 2 + i][lane];
+  }
+  __syncthreads();
+  if (wave == 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) red[0][j * 2 + i][lane] = acc[j][i];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int nb = n0 + j * 16 + (lane >> 4) * 4;
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.out_bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias[r] = p.out_bias[nb + r];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 a = acc[j][i] + red[0][j * 2 + i][lane];
+      const int m = m0 + 16 * i + fr;
+      if (m < p.M) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = a[r] + bias[r];
+          if (p.relu_out) v[r] = fmaxf(v[r], 0.f);
+        }
+        *reinterpret_cast<v2u*>(p.y + (size_t)m * p.ldy + nb) = v2u{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      }
+    }
+  }
+}
+
 // ============================================================================
 // K9: 3x3 conv, 128 -> 32 channels, stride 1, pad 1 (implicit GEMM)
 // ============================================================================
@@ -721,6 +872,91 @@ __global__ void __launch_bounds__(256) head_pool_kernel(const uint16_t* __restri
   }
 }
 
+
+// ============================================================================
+// K9s: small-M 3x3 conv.  Block = 32 pixels x 32 output channels; wave w owns
+// input channels [32w, 32w+32) of all 9 taps (9 K chunks), issues all of its
+// activation and weight fragment loads up front (one memory round trip
+// instead of a tap-by-tap chain), and the 4 partial tiles are summed through
+// LDS.  For the 7x7 / 14x14 blocks where K9's persistent 64-pixel tiles leave
+// most CUs idle and every block pays for a 73 KB weight preload.
+// ============================================================================
+__global__ void __launch_bounds__(256) conv3x3_sk_kernel(Conv3x3Params p) {
+  __shared__ __attribute__((aligned(16))) f32x4 red[2][4][64];  // [slot][frag][lane], 8 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.x * 32;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const int ch0 = wave * 32 + fk;
+  const int HW = p.H * p.W;
+  int pm[2], ph[2], pw[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + 16 * i + fr;
+    pm[i] = m < p.M ? m : -1;
+    const int mm = m < p.M ? m : 0;
+    const int r = mm % HW;
+    ph[i] = r / p.W;
+    pw[i] = r - ph[i] * p.W;
+  }
+  v4u act[9][2], wt[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int dh = t / 3 - 1, dw = t % 3 - 1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) wt[t][j] = ldg16(p.w + (size_t)(16 * j + fr) * kK3 + t * kC3 + ch0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int h = ph[i] + dh, w = pw[i] + dw;
+      const bool ok = pm[i] >= 0 && h >= 0 && h < p.H && w >= 0 && w < p.W;
+      act[t][i] = ok ? ldg16(p.z + (size_t)(pm[i] + dh * p.W + dw) * kC3 + ch0) : v4u{0, 0, 0, 0};
+    }
+  }
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[j][i] = mfma16(as_frag(wt[t][j]), as_frag(act[t][i]), acc[j][i]);
+
+  if (wave >= 2) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) red[wave - 2][j * 2 + i][lane] = acc[j][i];
+  }
+  __syncthreads();
+  if (wave < 2) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[j][i] += red[wave][j * 2 + i][lane];
+  }
+  __syncthreads();
+  if (wave == 1) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) red[0][j * 2 + i][lane] = acc[j][i];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int nb = j * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (pm[i] < 0) continue;
+      const f32x4 a = acc[j][i] + red[0][j * 2 + i][lane];
+      *reinterpret_cast<v2u*>(p.y + (size_t)pm[i] * p.ldy + nb) = v2u{pack2(a[0], a[1]), pack2(a[2], a[3])};
+    }
+  }
+}
+
 template <int TM, int BK, bool PRO, bool POOL>
 int launch_1x1(Conv1x1Params p, int splits, hipStream_t s) {
   const int mb = (p.M + 32 * TM - 1) / (32 * TM), nb = p.N / 128;
@@ -751,6 +987,11 @@ int launch_1x1(Conv1x1Params p, int splits, hipStream_t s) {
 template <bool PRO, bool POOL>
 int pick_1x1(const Conv1x1Params& p, int variant, int splits, size_t ws_bytes, hipStream_t s) {
   if (variant == 0) variant = p.M >= 32768 ? 21 : p.M >= 8192 ? 11 : 12;
+  if (variant == 70) {  // K8s: waves split K (needs the BN prologue)
+    if (!PRO || p.K % 32) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((conv1x1_sk_kernel<POOL>), dim3((p.M + 31) / 32, p.N / 128), dim3(256), 0, s, p);
+    return hipGetLastError();
+  }
   const int tm = variant / 10, bk = (variant % 10) * 32;
   const long blocks = (long)((p.M + 32 * tm - 1) / (32 * tm)) * (p.N / 128);
   const int kts = (p.K + bk - 1) / bk;
@@ -896,7 +1137,8 @@ int tcamd_dn_conv3x3_v(const void* z, int imgs, int H, int W, const void* w, voi
   // heuristic from tools/kbench_densenet.py on MI355X: the LDS-staged kernel
   // wins once there are enough 128-pixel tiles to fill the CUs; tiny problems
   // keep the 64-pixel-tile direct-load kernel
-  if (variant == 0) variant = (W <= 56 && (M + 127) / 128 >= 96) ? 60 : 11;
+  // (M <= 8192: the 7x7 / 14x14 layers of small batches) the wave-split K9s
+  if (variant == 0) variant = M <= 8192 ? 70 : (W <= 56 && (M + 127) / 128 >= 96) ? 60 : 11;
   switch (variant) {
     case 10: return launch_3x3<1, 0>(p, s);  // channel-major tap walk
     case 16: return launch_3x3<1, 6>(p, s);   // 6-deep load ring
@@ -910,6 +1152,9 @@ int tcamd_dn_conv3x3_v(const void* z, int imgs, int H, int W, const void* w, voi
     case 23: return launch_3x3<2, 3>(p, s);
     case 41: return launch_3x3<4, 1>(p, s);
     case 60: return launch_3x3_lds(p, s);     // LDS-staged activations, 32x32x16 MFMA
+    case 70:                                  // K9s: waves split the input channels
+      hipLaunchKernelGGL(conv3x3_sk_kernel, dim3((p.M + 31) / 32), dim3(256), 0, s, p);
+      return hipGetLastError();
     case 51: return launch_3x3_m32<1>(p, s);  // 32x32x16 MFMA, 32 px / wave
     case 52: return launch_3x3_m32<2>(p, s);  // 32x32x16 MFMA, 64 px / wave
     default: return hipErrorInvalidValue;

@@ -37,7 +37,8 @@ def _close(got, ref, tol=2e-2):
 
 @pytest.mark.parametrize("M,K,ldx,N,off", [(100, 64, 96, 128, 32), (40000, 224, 256, 128, 0),
                                            (70000, 96, 128, 128, 0), (3000, 512, 512, 256, 0)])
-def test_conv1x1_prologue_epilogue(M, K, ldx, N, off):
+@pytest.mark.parametrize("variant", [0, 70])
+def test_conv1x1_prologue_epilogue(M, K, ldx, N, off, variant):
     _need_gpu()
     hip = _hip()
     g = torch.Generator(device=DEV).manual_seed(M + K)
@@ -49,7 +50,7 @@ def test_conv1x1_prologue_epilogue(M, K, ldx, N, off):
     ldy = N + off + 32
     y = torch.full((M, ldy), 7.0, device=DEV).bfloat16()
     hip.dn_conv1x1(x.data_ptr(), ldx, M, K, s.data_ptr(), b.data_ptr(), w.data_ptr(), N, ob.data_ptr(), 1,
-                   y.data_ptr() + 2 * off, ldy, stream=torch.cuda.current_stream().cuda_stream)
+                   y.data_ptr() + 2 * off, ldy, stream=torch.cuda.current_stream().cuda_stream, variant=variant)
     torch.cuda.synchronize()
     a = torch.relu(x[:, :K].float() * s + b).bfloat16().float()
     ref = torch.relu(a @ w.float().t() + ob)
@@ -60,7 +61,7 @@ def test_conv1x1_prologue_epilogue(M, K, ldx, N, off):
 
 @pytest.mark.parametrize("M,K,N,pool,splits", [(49, 992, 128, 0, 0), (196, 640, 128, 0, 4), (49, 1024, 512, 1, 0),
                                                (300, 96, 128, 0, 3), (1000, 512, 256, 0, 16)])
-@pytest.mark.parametrize("variant", [0, 11, 12, 21, 42])
+@pytest.mark.parametrize("variant", [0, 11, 12, 21, 42, 70])
 def test_conv1x1_split_k(M, K, N, pool, splits, variant):
     """Split-K partials + reduce must equal the single-pass kernel's math."""
     _need_gpu()
@@ -125,7 +126,7 @@ def test_conv1x1_transition_pool(imgs, H, C, N):
     assert (y[:, N:] == 0).all()
 
 
-@pytest.mark.parametrize("variant", [0, 10, 11, 13, 16, 19, 21, 41, 51, 52, 60])
+@pytest.mark.parametrize("variant", [0, 10, 11, 13, 16, 19, 21, 41, 51, 52, 60, 70])
 @pytest.mark.parametrize("imgs,H", [(1, 7), (3, 14), (8, 56), (48, 56), (5, 28)])
 def test_conv3x3(imgs, H, variant):
     _need_gpu()

@@ -14,8 +14,8 @@ import torch
 
 from triton_client_amd.ops import hip
 
-V1 = (11, 12, 21, 22, 41, 42)
-V3 = (0, 11, 60)
+V1 = (11, 12, 21, 22, 41, 42, 70)
+V3 = (0, 11, 60, 70)
 
 
 def cs():
