@@ -37,10 +37,14 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=8, help="images per request (densenet_onnx bs)")
-    ap.add_argument("--concurrency", type=int, default=16, help="requests in flight per GPU")
+    ap.add_argument("--concurrency", type=int, default=48, help="requests in flight per GPU")
     ap.add_argument("--fanout", default="rccl", choices=["rccl", "p2p", "local"])
-    ap.add_argument("--instance-count", type=int, default=2)
-    ap.add_argument("--max-queue-delay-us", type=int, default=500)
+    # operating point from tools/gpu_bench_sweep.sh on MI355X (profiles/r1_operating_points.md):
+    # three model instances (HIP streams) each running full 128-row batches overlap
+    # well on the 256 CUs (1.3x one stream's throughput)
+    ap.add_argument("--instance-count", type=int, default=3)
+    ap.add_argument("--max-queue-delay-us", type=int, default=2000)
+    ap.add_argument("--preferred", default="128", help="server preferred batch sizes (comma-separated rows; '' = none)")
     ap.add_argument("--engine", default="fused", choices=["fused", "torch"],
                     help="densenet_onnx engine in the server (fused HIP/MFMA kernels or torch/MIOpen)")
     ap.add_argument("--loadgen", default="native", choices=["native", "python"],
@@ -68,7 +72,8 @@ def main():
             device=local_rank,
             models="densenet_onnx",
             extra_args=["--instance-count", str(args.instance_count), "--engine", args.engine,
-                        "--max-queue-delay-us", str(args.max_queue_delay_us)],
+                        "--max-queue-delay-us", str(args.max_queue_delay_us)]
+            + (["--preferred-batch-sizes", args.preferred] if args.preferred else []),
             log_path=log_path,
         )
 
@@ -199,6 +204,9 @@ def main():
                     "shared_memory": "hip",
                     "engine": args.engine,
                     "loadgen": args.loadgen,
+                    "server_instances": args.instance_count,
+                    "preferred_batch_rows": args.preferred,
+                    "max_queue_delay_us": args.max_queue_delay_us,
                 },
                 "p50_latency_us": round(percentile_us(all_lat, 50), 1),
                 "p90_latency_us": round(percentile_us(all_lat, 90), 1),

@@ -122,6 +122,7 @@ struct NativeModel {
   std::string name, version;
   int max_batch = 0;
   uint64_t delay_ns = 0;
+  std::vector<int> preferred;  // ascending; dynamic_batching.preferred_batch_size
   int instances = 1;
   std::vector<TensorDef> inputs, outputs;
   tcserve_exec_fn fn = nullptr;
@@ -1081,9 +1082,14 @@ void Server::Worker(std::shared_ptr<NativeModel> m, int instance)
       m->cv.wait(lk, [&] { return m->stopping || !m->q.empty(); });
       if (m->stopping) return;
       const int cap = m->max_batch > 0 ? m->max_batch : 1;
+      // Triton dynamic-batcher semantics: a batch of the largest preferred
+      // size dispatches at once; otherwise wait up to the queue delay for a
+      // full batch.  Whatever is queued then goes out, capped at the largest
+      // preferred size that fits (so pipelined instances keep alternating).
+      const int pref_max = m->preferred.empty() ? cap : std::min(cap, m->preferred.back());
       if (m->max_batch > 0 && m->delay_ns > 0) {
         const uint64_t deadline = m->q.front()->t_arrive + m->delay_ns;
-        while (!m->stopping && m->q_rows < cap) {
+        while (!m->stopping && m->q_rows < pref_max) {
           const uint64_t now = NowNs();
           if (now >= deadline) break;
           m->cv.wait_for(lk, std::chrono::nanoseconds(deadline - now));
@@ -1092,8 +1098,14 @@ void Server::Worker(std::shared_ptr<NativeModel> m, int instance)
         if (m->stopping) return;
         if (m->q.empty()) continue;
       }
+      int limit = cap;
+      for (auto it = m->preferred.rbegin(); it != m->preferred.rend(); ++it)
+        if (*it <= m->q_rows && *it <= cap) {
+          limit = *it;
+          break;
+        }
       int rows = 0;
-      while (!m->q.empty() && (rows == 0 || rows + m->q.front()->rows <= cap)) {
+      while (!m->q.empty() && (rows == 0 || rows + m->q.front()->rows <= limit)) {
         rows += m->q.front()->rows;
         m->q_rows -= m->q.front()->rows;
         batch.push_back(std::move(m->q.front()));
@@ -1335,6 +1347,25 @@ int32_t tcserve_add_model(void* server, const char* name, const char* version, i
 }
 
 int32_t tcserve_remove_model(void* server, const char* name) { return static_cast<Server*>(server)->RemoveModel(name); }
+
+int32_t tcserve_set_preferred(void* server, const char* name, const int32_t* sizes, int32_t n)
+{
+  Server* s = static_cast<Server*>(server);
+  std::shared_ptr<NativeModel> m;
+  {
+    std::lock_guard<std::mutex> lk(s->models_mu);
+    auto it = s->models.find(name);
+    if (it == s->models.end()) return 1;
+    m = it->second;
+  }
+  std::vector<int> v;
+  for (int32_t i = 0; i < n; ++i)
+    if (sizes[i] > 0) v.push_back(sizes[i]);
+  std::sort(v.begin(), v.end());
+  std::lock_guard<std::mutex> lk(m->mu);
+  m->preferred = std::move(v);
+  return 0;
+}
 
 int32_t tcserve_shm_add(void* server, const char* name, int32_t kind, uint64_t ptr, uint64_t bytes, int32_t device)
 {

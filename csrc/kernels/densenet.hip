@@ -844,6 +844,132 @@ __global__ void __launch_bounds__(256) stem_pool_kernel(const uint16_t* __restri
 }
 
 // ============================================================================
+// K10s: fused stem  y = relu(maxpool3x3/2(conv7x7/2(x)) + b), 3 -> 64 channels
+// ============================================================================
+// Replaces four passes of the unfused path (K6 fp32 NCHW -> bf16 NHWC batch
+// assembly, the library 7x7 conv, its bias op, K10a) with one: a block stages
+// the input patch its 4x14 pooled outputs need ([23 rows][72 cols][4 ch] bf16,
+// read straight from each request's fp32 NCHW image through a device pointer
+// table, so the batch is never assembled), runs the conv for the 9x32 conv
+// pixels under the pooling windows as an implicit GEMM on
+// v_mfma_f32_32x32x16_bf16 (weights = operand A, 64 x K=7*8*4 with the 8th kw
+// and 4th channel zero; one conv row = one 32-pixel MFMA column tile), keeps
+// the conv tile in LDS, and max-pools it from there.  For output (r, c) and
+// kernel row kh, the K values (kw, ch) are 8 contiguous bf16 per lane in the
+// staged patch (stride-2 conv: input col = 2*conv col + kw), so each B
+// fragment is one aligned ds_read_b128.  Conv pixels outside the image (row
+// or col -1) are excluded from the max, as in max-pool padding.
+constexpr int kStemPR = 4, kStemPC = 14;   // pooled outputs per block
+constexpr int kStemCR = 2 * kStemPR + 1;   // 9 conv rows
+constexpr int kStemCC = 32;                // conv cols computed (2*PC+1 = 29 used)
+constexpr int kStemIR = 2 * kStemCR + 5;   // 23 input rows
+constexpr int kStemIC = 72;                // input cols (2*31 + 2*3 + 2 = 70 read, padded)
+constexpr int kStemK = 7 * 32;             // (kh, kw[8], ch[4])
+constexpr int kStemOS = 64 + 4;            // conv-tile pixel stride (bf16): 34 dwords, conflict-free, 3 blocks/CU
+constexpr int kStemHin = 224, kStemHo = 56;
+
+struct StemParams {
+  const float* const* srcs;  // F32: per-image fp32 NCHW [3][224][224] (device pointer table)
+  const uint16_t* x;         // !F32: bf16 NHWC [imgs][224][224][3]
+  const uint16_t* w;         // [64][kStemK] packed bf16 (BN0 scale folded)
+  const float* bias;         // [64] BN0 shift
+  uint16_t* y;               // [imgs][56][56] pixels, rows of ldy
+  int ldy;
+};
+
+template <bool F32>
+__global__ void __launch_bounds__(256) stem_fused_kernel(StemParams p) {
+  __shared__ __attribute__((aligned(16))) uint16_t In[kStemIR * kStemIC * 4];        // 13.2 KB
+  __shared__ __attribute__((aligned(16))) uint16_t Cv[kStemCR * kStemCC * kStemOS];  // 39 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int img = blockIdx.z, pr0 = blockIdx.y * kStemPR, pc0 = blockIdx.x * kStemPC;
+  const int ir0 = 4 * pr0 - 5, ic0 = 4 * pc0 - 5;
+  const float* src = F32 ? p.srcs[img] : nullptr;
+  // all loads of the patch in flight at once (7 per thread per channel), then the LDS stores
+  constexpr int kStage = (kStemIR * kStemIC + 255) / 256;
+  float v[kStage][3];
+#pragma unroll
+  for (int i = 0; i < kStage; ++i) {
+    const int e = tid + i * 256;
+    const int r = e / kStemIC, c = e - r * kStemIC;
+    const int ih = ir0 + r, iw = ic0 + c;
+    v[i][0] = v[i][1] = v[i][2] = 0.f;
+    if (e < kStemIR * kStemIC && ih >= 0 && ih < kStemHin && iw >= 0 && iw < kStemHin) {
+      if (F32) {
+        const float* s = src + ih * kStemHin + iw;
+        v[i][0] = __builtin_nontemporal_load(s);
+        v[i][1] = __builtin_nontemporal_load(s + kStemHin * kStemHin);
+        v[i][2] = __builtin_nontemporal_load(s + 2 * kStemHin * kStemHin);
+      } else {
+        const uint16_t* s = p.x + (((size_t)img * kStemHin + ih) * kStemHin + iw) * 3;
+        v[i][0] = tcamd::bf16_to_f32(s[0]);
+        v[i][1] = tcamd::bf16_to_f32(s[1]);
+        v[i][2] = tcamd::bf16_to_f32(s[2]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kStage; ++i) {
+    const int e = tid + i * 256;
+    if (e < kStemIR * kStemIC)
+      *reinterpret_cast<v2u*>(&In[e * 4]) = v2u{pack2(v[i][0], v[i][1]), pack2(v[i][2], 0.f)};
+  }
+  // wave = (channel half nh) x (conv-row group mg: rows 0-4 / 5-8); its 14
+  // weight fragments stay in registers for all of its rows
+  const int nh = wave & 1, mg = wave >> 1;
+  v4u wa[kStemK / 16];
+  const uint16_t* wp = p.w + (size_t)(nh * 32 + (lane & 31)) * kStemK + 8 * (lane >> 5);
+#pragma unroll
+  for (int s = 0; s < kStemK / 16; ++s) wa[s] = ldg16(wp + s * 16);
+  __syncthreads();
+  const int jj = lane & 31;
+  const int r_lo = mg ? 5 : 0, r_hi = mg ? kStemCR : 5;
+  for (int cr = r_lo; cr < r_hi; ++cr) {
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < kStemK / 16; ++s) {
+      const int kh = s >> 1, q = (s & 1) * 2 + (lane >> 5);
+      const v4u b = *reinterpret_cast<const v4u*>(&In[((2 * cr + kh) * kStemIC + 2 * jj + 2 * q) * 4]);
+      acc = mfma32(as_frag(wa[s]), as_frag(b), acc);
+    }
+    uint16_t* cp = &Cv[(cr * kStemCC + jj) * kStemOS + nh * 32 + 4 * (lane >> 5)];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<v2u*>(cp + 8 * g) =
+          v2u{pack2(acc[4 * g], acc[4 * g + 1]), pack2(acc[4 * g + 2], acc[4 * g + 3])};
+  }
+  __syncthreads();
+  for (int t = tid; t < kStemPR * kStemPC * 8; t += 256) {
+    const int cc = t & 7, px = t >> 3;
+    const int a = px / kStemPC, b = px - a * kStemPC;
+    const int pr = pr0 + a, pc = pc0 + b;
+    float mx[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mx[e] = -3.0e38f;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      if (2 * pr - 1 + dy < 0) continue;
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        if (2 * pc - 1 + dx < 0) continue;
+        float f[8];
+        const uint16_t* cp = &Cv[((2 * a + dy) * kStemCC + 2 * b + dx) * kStemOS + cc * 8];  // 8-B aligned
+        const v2u lo = *reinterpret_cast<const v2u*>(cp), hi = *reinterpret_cast<const v2u*>(cp + 4);
+        unpack8(v4u{lo[0], lo[1], hi[0], hi[1]}, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], f[e]);
+      }
+    }
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = fmaxf(mx[e] + p.bias[cc * 8 + e], 0.f);
+    *reinterpret_cast<v4u*>(p.y + (((size_t)img * kStemHo + pr) * kStemHo + pc) * p.ldy + cc * 8) = pack8(o);
+  }
+}
+
+// ============================================================================
 // K10b: head  out[img][c] = mean_p relu(x[img][p][c]*s[c] + b[c])   (bf16 out)
 // ============================================================================
 // One block per image; each thread owns 8-channel chunks and walks the pixels.
@@ -1172,6 +1298,30 @@ int tcamd_dn_stem_pool(const void* x, const float* bias, void* y, int imgs, int 
   const size_t total = (size_t)imgs * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
   hipLaunchKernelGGL(stem_pool_kernel, dim3(tcamd::grid_for(total)), dim3(256), 0, (hipStream_t)stream,
                      (const uint16_t*)x, bias, (uint16_t*)y, imgs, H, W, C, ldy);
+  return hipGetLastError();
+}
+
+// Fused stem over 224x224x3 images -> 56x56x64 (conv 7x7/2 pad 3, bias, ReLU,
+// max-pool 3x3/2 pad 1).  srcs (device array of imgs fp32 NCHW image
+// pointers) if non-null, else x = bf16 NHWC [imgs][224][224][3].
+// w = [64][7][8][4] bf16 (zero at kw 7 / ch 3); y rows of ldy elements.
+int tcamd_dn_stem_fused(const void* srcs, const void* x, const void* w, const float* bias, void* y, int imgs,
+                        int ldy, void* stream) {
+  if (imgs <= 0) return hipSuccess;
+  if (ldy % 8 || ldy < 64 || (!srcs && !x) || !w || !bias || !y) return hipErrorInvalidValue;
+  if (((uintptr_t)w | (uintptr_t)y) % 16 || (srcs && (uintptr_t)srcs % 8)) return hipErrorInvalidValue;
+  StemParams p;
+  p.srcs = (const float* const*)srcs;
+  p.x = (const uint16_t*)x;
+  p.w = (const uint16_t*)w;
+  p.bias = bias;
+  p.y = (uint16_t*)y;
+  p.ldy = ldy;
+  const dim3 g(kStemHo / kStemPC, kStemHo / kStemPR, imgs);
+  if (srcs)
+    hipLaunchKernelGGL(stem_fused_kernel<true>, g, dim3(256), 0, (hipStream_t)stream, p);
+  else
+    hipLaunchKernelGGL(stem_fused_kernel<false>, g, dim3(256), 0, (hipStream_t)stream, p);
   return hipGetLastError();
 }
 

@@ -159,6 +159,46 @@ def test_stem_pool():
     assert (y[:, 64:] == 0).all()
 
 
+def _stem_ref(img_bf16_nchw, w, b):
+    """fp32 conv7x7/2 on bf16-rounded operands, conv output rounded to bf16
+    (the kernel keeps its conv tile in LDS as bf16), then max-pool + bias + ReLU."""
+    c = F.conv2d(img_bf16_nchw.float(), w.bfloat16().float(), stride=2, padding=3).bfloat16().float()
+    return torch.relu(F.max_pool2d(c, 3, 2, 1) + b.view(1, -1, 1, 1)).permute(0, 2, 3, 1).reshape(-1, 64)
+
+
+def _pack_stem_w(w):
+    wp = torch.zeros(64, 7, 8, 4, device=w.device)
+    wp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
+    return wp.reshape(64, -1).bfloat16().contiguous()
+
+
+@pytest.mark.parametrize("imgs", [1, 3])
+@pytest.mark.parametrize("mode", ["ptrs_fp32_nchw", "bf16_nhwc"])
+def test_stem_fused(imgs, mode):
+    """K10s (conv 7x7/2 + bias + ReLU + max-pool 3x3/2 in one kernel) vs torch fp32."""
+    _need_gpu()
+    hip = _hip()
+    g = torch.Generator(device=DEV).manual_seed(11 + imgs)
+    w = torch.randn(64, 3, 7, 7, device=DEV, generator=g) * 0.1
+    b = torch.randn(64, device=DEV, generator=g) * 0.2
+    x = torch.randn(imgs, 3, 224, 224, device=DEV, generator=g)
+    ldy = 256
+    y = torch.full((imgs * 56 * 56, ldy), 5.0, device=DEV).bfloat16()
+    wp = _pack_stem_w(w)
+    if mode == "ptrs_fp32_nchw":
+        # separate allocations, as with one shm region per request
+        imgs_t = [x[i].clone() for i in range(imgs)]
+        tbl = torch.tensor([t.data_ptr() for t in imgs_t], device=DEV, dtype=torch.int64)
+        hip.dn_stem_fused(tbl.data_ptr(), None, wp.data_ptr(), b.data_ptr(), y.data_ptr(), imgs, ldy)
+    else:
+        xn = x.bfloat16().permute(0, 2, 3, 1).contiguous()
+        hip.dn_stem_fused(None, xn.data_ptr(), wp.data_ptr(), b.data_ptr(), y.data_ptr(), imgs, ldy)
+    torch.cuda.synchronize()
+    ref = _stem_ref(x.bfloat16(), w, b)
+    _close(y[:, :64], ref, tol=1e-2)
+    assert (y[:, 64:] == 5.0).all()
+
+
 def test_head_pool():
     _need_gpu()
     hip = _hip()

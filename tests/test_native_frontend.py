@@ -68,6 +68,44 @@ def test_fast_path_async_batches(cpu_server):
     assert int(st["execution_count"]) < int(st["inference_stats"]["success"]["count"])
 
 
+def test_preferred_batch_size_caps_batches(cpu_server):
+    """With preferred_batch_size [2] the native batcher dispatches 2-row batches
+    as soon as they form instead of filling max_batch_size (8)."""
+    import threading
+
+    nf = cpu_server.server.native_frontend
+    c = grpcclient.InferenceServerClient(cpu_server.grpc_url)
+
+    def sizes():
+        st = c.get_inference_statistics("add_sub_batched", as_json=True)["model_stats"][0]
+        return {int(b["batch_size"]): int(b["compute_infer"]["count"]) for b in st.get("batch_stats", [])}
+
+    before = sizes()
+    nf.set_preferred("add_sub_batched", [2])
+    try:
+        done = threading.Event()
+        got = []
+
+        def cb(result, error):
+            got.append(error)
+            if len(got) == 24:
+                done.set()
+
+        for k in range(24):
+            a = np.full((1, 16), k, dtype=np.int32)
+            c.async_infer("add_sub_batched", _inputs(a, a), cb)
+        assert done.wait(30)
+        assert all(e is None for e in got)
+    finally:
+        nf.set_preferred("add_sub_batched", [])
+    after = sizes()
+    new = {bs: after.get(bs, 0) - before.get(bs, 0) for bs in after}
+    assert all(n == 0 for bs, n in new.items() if bs > 2), new
+    assert new.get(2, 0) > 0, new
+    with pytest.raises(KeyError):
+        nf.set_preferred("no_such_model", [2])
+
+
 def test_fast_path_system_shm(cpu_server):
     c = grpcclient.InferenceServerClient(cpu_server.grpc_url)
     nf = cpu_server.server.native_frontend

@@ -3,9 +3,11 @@
 Executes the same network as :class:`densenet.DenseNet121` (after
 ``fold_for_inference``) without per-op library calls:
 
-  x [b,224,224,3] bf16 NHWC
-   -> conv0 7x7/2 (MIOpen, BN0 folded into weight; bias applied below)
-   -> K10a  relu(maxpool(conv0) + b0)            -> block-1 buffer ch[0:64]
+  x [b,224,224,3] bf16 NHWC, or a device table of per-image fp32 NCHW
+  pointers (``forward_ptrs``: the server's requests, never assembled)
+   -> K10s  relu(maxpool(conv0 7x7/2) + b0)      -> block-1 buffer ch[0:64]
+            (one kernel: BN0 folded into the conv weight, conv tile in LDS;
+            ``stem="miopen"`` keeps the library conv + K10a for comparison)
    -> per dense layer:   K8 conv1x1 (BN1+ReLU prologue, BN2-folded bias+ReLU
                          epilogue) -> z [pixels,128]
                          K9 conv3x3 z -> block buffer ch[c_in : c_in+32]
@@ -40,16 +42,23 @@ class FusedDenseNet:
 
     H0 = 224
 
-    def __init__(self, model, max_batch, device):
+    def __init__(self, model, max_batch, device, stem="fused"):
         assert all(layer.folded for blk in model.blocks for layer in blk), "call fold_for_inference first"
         dev = torch.device(device)
         bf = torch.bfloat16
         self.device = dev
         self.max_batch = int(max_batch)
+        if stem not in ("fused", "miopen"):
+            raise ValueError("stem must be 'fused' or 'miopen'")
+        self.stem = stem
         with torch.no_grad():
             s0, b0 = _bn_affine(model.norm0)
             w0 = model.conv0.weight.float() * s0.view(-1, 1, 1, 1)
             self.w0 = w0.to(dev, bf).contiguous(memory_format=torch.channels_last)
+            # K10s layout: [64][kh 7][kw 8][ch 4], zero at kw 7 / ch 3
+            w0p = torch.zeros(w0.shape[0], 7, 8, 4)
+            w0p[:, :, :7, :3] = w0.permute(0, 2, 3, 1).cpu()
+            self.w0p = w0p.reshape(w0.shape[0], -1).to(dev, bf).contiguous()
             self.b0 = b0.to(dev)
             self.blocks = []
             self.trans = []
@@ -98,6 +107,8 @@ class FusedDenseNet:
         h1 = self.block_dims[0][0]
         self.z = torch.empty(n * h1 * h1, BN_SIZE * GROWTH, device=dev, dtype=bf)
         self.pooled = torch.empty(n, self.num_features, device=dev, dtype=bf)
+        # per-image fp32 NCHW input pointers read by K10s (forward_ptrs)
+        self.ptrs = torch.zeros(n, device=dev, dtype=torch.int64)
         # split-K fp32 partials for the small-M 1x1 convs (K8 splits only while
         # its grid is < 128 blocks, so splits * M * N <= 16 * 128 * 32 * 128)
         self.ws = torch.empty(16 * 128 * 32 * 128 * 4, device=dev, dtype=torch.uint8)
@@ -117,13 +128,33 @@ class FusedDenseNet:
         if b > self.max_batch:
             raise ValueError("batch %d exceeds capacity %d" % (b, self.max_batch))
         st = torch.cuda.current_stream(self.device).cuda_stream
+        if self.stem == "fused":
+            if x.dtype != torch.bfloat16 or not x.is_contiguous(memory_format=torch.channels_last):
+                x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            hip.dn_stem_fused(None, x.data_ptr(), self.w0p.data_ptr(), self.b0.data_ptr(), self.feat[0].data_ptr(),
+                              b, self.block_dims[0][1], stream=st)
+        else:
+            self._stem_miopen(x, b, st)
+        return self._trunk(b, st, out)
+
+    def forward_ptrs(self, b, out=None):
+        """Run ``b`` images whose fp32 NCHW [3,224,224] device pointers are in ``self.ptrs[:b]``."""
+        if b > self.max_batch:
+            raise ValueError("batch %d exceeds capacity %d" % (b, self.max_batch))
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        hip.dn_stem_fused(self.ptrs.data_ptr(), None, self.w0p.data_ptr(), self.b0.data_ptr(),
+                          self.feat[0].data_ptr(), b, self.block_dims[0][1], stream=st)
+        return self._trunk(b, st, out)
+
+    def _stem_miopen(self, x, b, st):
         y0 = F.conv2d(x, self.w0, stride=2, padding=3)  # [b,64,112,112] channels_last
         if not y0.is_contiguous(memory_format=torch.channels_last):
             y0 = y0.contiguous(memory_format=torch.channels_last)
         h0 = int(y0.shape[2])
-        hw1, c1 = self.block_dims[0]
         hip.dn_stem_pool(y0.data_ptr(), self.b0.data_ptr(), self.feat[0].data_ptr(), b, h0, h0, INIT_FEATURES,
-                         c1, stream=st)
+                         self.block_dims[0][1], stream=st)
+
+    def _trunk(self, b, st, out):
         for bi, layers in enumerate(self.blocks):
             hw, ctot = self.block_dims[bi]
             feat = self.feat[bi]
@@ -152,7 +183,7 @@ class FusedDenseNet:
     __call__ = forward
 
 
-def build(max_batch, device="cuda", seed=0):
+def build(max_batch, device="cuda", seed=0, stem="fused"):
     """Random-init, BN-calibrated, folded DenseNet-121 as a fused engine."""
     from . import densenet
 
@@ -161,4 +192,4 @@ def build(max_batch, device="cuda", seed=0):
     densenet.calibrate_bn(model, device="cpu")
     densenet.fold_for_inference(model)
     model.eval()
-    return FusedDenseNet(model, max_batch, device), model
+    return FusedDenseNet(model, max_batch, device, stem=stem), model

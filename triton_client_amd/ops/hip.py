@@ -149,6 +149,11 @@ _SIGS = {
          ctypes.c_int, ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "tcamd_dn_stem_fused": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+         ctypes.c_int, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_dn_head_pool": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
          ctypes.c_void_p],
@@ -469,6 +474,13 @@ def dn_conv3x3(z, imgs, H, W, w, y, ldy, stream=None, variant=0):
 def dn_stem_pool(x, bias, y, imgs, H, W, C, ldy, stream=None):
     """K10a: y = relu(maxpool3x3/2(x) + bias) into rows of ldy elements."""
     _check(_load().tcamd_dn_stem_pool(x, bias, y, imgs, H, W, C, ldy, _vp(stream)), "dn_stem_pool")
+
+
+def dn_stem_fused(srcs, x, w, bias, y, imgs, ldy, stream=None):
+    """K10s: y = relu(maxpool3x3/2(conv7x7/2(img)) + bias) for 224x224x3 images -> 56x56x64.
+    ``srcs``: device array of per-image fp32 NCHW pointers (or None with ``x`` = bf16 NHWC batch);
+    ``w``: [64][7][8][4] bf16 packed weights."""
+    _check(_load().tcamd_dn_stem_fused(_vp(srcs), _vp(x), w, bias, y, imgs, ldy, _vp(stream)), "dn_stem_fused")
 
 
 def dn_head_pool(x, scale, bias, out, imgs, HW, C, stream=None):

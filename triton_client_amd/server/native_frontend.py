@@ -61,6 +61,8 @@ def _load():
             ctypes.POINTER(ctypes.c_int64),
             EXEC_FN, ctypes.c_void_p, cp, ctypes.c_int32]
         lib.tcserve_add_model.restype = ctypes.c_int32
+        lib.tcserve_set_preferred.argtypes = [ctypes.c_void_p, cp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]
+        lib.tcserve_set_preferred.restype = ctypes.c_int32
         lib.tcserve_remove_model.argtypes = [ctypes.c_void_p, cp]
         lib.tcserve_remove_model.restype = ctypes.c_int32
         lib.tcserve_shm_add.argtypes = [ctypes.c_void_p, cp, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64,
@@ -175,9 +177,20 @@ class NativeFrontend:
             cb, None, err, 512)
         if rc != 0:
             raise RuntimeError("tcserve: %s" % err.value.decode(errors="replace"))
+        pref = [int(x) for x in (inst.dynamic_batching or {}).get("preferred", [])]
+        if pref:
+            self.set_preferred(name, pref)
         with self._lock:
             self._cbs[name] = cb
             self._versions[name] = str(inst.version)
+
+    def set_preferred(self, name, sizes):
+        """dynamic_batching.preferred_batch_size of a registered model ([] clears)."""
+        sizes = [int(x) for x in sizes]
+        rc = _load().tcserve_set_preferred(self._h, name.encode(), (ctypes.c_int32 * max(1, len(sizes)))(*sizes),
+                                           len(sizes))
+        if rc != 0:
+            raise KeyError(name)
 
     def unregister_model(self, name):
         _load().tcserve_remove_model(self._h, name.encode())
