@@ -19,6 +19,14 @@ RC=$?
 # rocprofv3 may exec the program itself (then PROF_PID is the server)
 SRV_PID=$(pgrep -P $PROF_PID -n python3 || true)
 kill -TERM "${SRV_PID:-$PROF_PID}"
+# the profiler flushes its CSVs on SIGTERM, but the server may not exit after
+# that: give it 30 s, then kill the process group member by PID
+for i in $(seq 30); do
+  kill -0 $PROF_PID 2>/dev/null || break
+  echo "waiting for profiler exit ($i s)"
+  sleep 1
+done
+kill -KILL ${SRV_PID:-} $PROF_PID 2>/dev/null
 wait $PROF_PID
 echo "bench rc=$RC profiler rc=$?"
 exit $RC
