@@ -107,10 +107,10 @@ void LoadEngine::OnComplete(size_t slot, uint64_t start_ns, InferResult* r)
   } else {
     rec.ok = false;
   }
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    done_.emplace_back(slot, rec);
-  }
+  // runs on a client's io thread: notify under the lock, since the engine
+  // (and cv_) may be destroyed as soon as the worker has drained done_
+  std::lock_guard<std::mutex> lk(mu_);
+  done_.emplace_back(slot, rec);
   cv_.notify_one();
 }
 

@@ -806,10 +806,10 @@ InferenceServerGrpcClient::StartStream(
   };
   h.on_close = [this, closed](const GrpcStatus& st) {
     if (!st.ok() && stream_callback_) stream_callback_(new InferResultGrpc(nullptr, StatusToError(st)));
-    {
-      std::lock_guard<std::mutex> lk2(stream_mutex_);
-      closed->store(true);
-    }
+    // notify under the lock: StopStream (and then the destructor) may run as
+    // soon as `closed` is visible, so the cv must not be touched after unlock
+    std::lock_guard<std::mutex> lk2(stream_mutex_);
+    closed->store(true);
     stream_cv_.notify_all();
   };
   stream_ = channel_->StartCall(std::string(kService) + "ModelStreamInfer", Metadata(headers),

@@ -148,7 +148,18 @@ GrpcFrame(const std::string& message, GrpcCompression comp, std::string* out)
 std::shared_ptr<H2Channel>
 H2Channel::Create(const std::string& host, int port, const H2ChannelOptions& opts, std::string* err)
 {
-  std::shared_ptr<H2Channel> ch(new H2Channel());
+  // The last owner may be released ON the io thread (a finished call or a
+  // posted task holding the channel): joining there would be a self-join
+  // (EDEADLK -> std::terminate), so that case only flags the loop, which
+  // exits and deletes the channel itself.
+  std::shared_ptr<H2Channel> ch(new H2Channel(), [](H2Channel* p) {
+    if (p->io_.joinable() && p->io_.get_id() == std::this_thread::get_id()) {
+      p->delete_on_exit_ = true;
+      p->stop_ = true;
+      return;
+    }
+    delete p;
+  });
   ch->opts_ = opts;
   ch->authority_ = host + ":" + std::to_string(port);
   std::string e = ch->sock_.Connect(host, port, 20000000, opts.tls);
@@ -474,6 +485,16 @@ H2Channel::FlushSend()
 
 void
 H2Channel::Loop()
+{
+  LoopBody();
+  if (delete_on_exit_) {  // released by its last owner on this thread (see Create)
+    io_.detach();
+    delete this;
+  }
+}
+
+void
+H2Channel::LoopBody()
 {
   char buf[1 << 17];
   while (!stop_) {

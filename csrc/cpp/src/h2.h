@@ -71,6 +71,7 @@ class H2Channel : public std::enable_shared_from_this<H2Channel> {
   friend class H2Call;
   H2Channel() = default;
   void Loop();
+  void LoopBody();
   void Wake();
   void Post(std::function<void()> fn);
   void FailAll(const std::string& why);
@@ -86,6 +87,7 @@ class H2Channel : public std::enable_shared_from_this<H2Channel> {
   std::deque<std::function<void()>> tasks_;
   std::atomic<bool> stop_{false};
   std::atomic<bool> dead_{false};
+  bool delete_on_exit_ = false;  // io thread only
   std::string dead_reason_;
   std::unordered_map<int32_t, std::shared_ptr<H2Call>> calls_;
   std::string sendbuf_;

@@ -89,8 +89,11 @@ CheckAddSub(tc::InferResult* r, bool swapped, const std::string& ctx)
     CHECK(false, ctx << " wrong output byte size " << n0 << "/" << n1);
     return;
   }
-  const int32_t* o0 = reinterpret_cast<const int32_t*>(b0);
-  const int32_t* o1 = reinterpret_cast<const int32_t*>(b1);
+  // HTTP outputs sit right after the JSON header, at any byte offset: copy
+  // out instead of reading int32 through a misaligned pointer (UBSan)
+  int32_t o0[16], o1[16];
+  std::memcpy(o0, b0, sizeof(o0));
+  std::memcpy(o1, b1, sizeof(o1));
   for (int i = 0; i < 16; ++i) {
     int sum = i + 1, diff = i - 1;
     CHECK(o0[i] == (swapped ? diff : sum), ctx << " OUTPUT0[" << i << "]=" << o0[i]);

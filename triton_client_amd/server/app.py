@@ -10,7 +10,7 @@ from aiohttp import web
 from tritonclient.grpc import service_pb2_grpc
 
 from .core import InferenceServer
-from .grpc_frontend import GrpcFrontend
+from .grpc_frontend import FaultInjector, GrpcFrontend
 from .http_frontend import HttpFrontend
 
 
@@ -62,7 +62,7 @@ async def serve(server, http_port, grpc_port, host="127.0.0.1", ready_evt=None, 
     gserver = None
     nf = None
     if grpc_port is not None:
-        gserver = grpc.aio.server(options=GRPC_OPTIONS)
+        gserver = grpc.aio.server(options=GRPC_OPTIONS, interceptors=[FaultInjector()])
         service_pb2_grpc.add_GRPCInferenceServiceServicer_to_server(GrpcFrontend(server), gserver)
         if native_grpc:
             inner = gserver.add_insecure_port("127.0.0.1:0")

@@ -107,6 +107,13 @@ class CustomIdentityInt32(Identity):
         super().__init__(version, **kw)
 
 
+class IdentityInt32(Identity):
+    """custom_identity_int32 without the delay (soak tests)."""
+
+    name = "identity_int32"
+    datatype = "INT32"
+
+
 class IdentityFP32(Identity):
     name = "identity_fp32"
     datatype = "FP32"
@@ -344,6 +351,7 @@ CPU_MODELS = [
     SimpleString,
     Identity,
     CustomIdentityInt32,
+    IdentityInt32,
     IdentityFP32,
     IdentityBF16,
     IdentityInt8,

@@ -56,6 +56,25 @@ def _code(e):
     return grpc.StatusCode.INTERNAL, str(e)
 
 
+FAULT_DELAY_KEY = "tc-fault-delay-ms"
+
+
+class FaultInjector(grpc.aio.ServerInterceptor):
+    """Test-server fault knob: a ``tc-fault-delay-ms`` request header delays the
+    RPC before it is handled, so client deadlines on control-plane calls can be
+    exercised (reference src/c++/tests/client_timeout_test.cc drives every
+    API with a timeout against a slow server)."""
+
+    async def intercept_service(self, continuation, handler_call_details):
+        for k, v in handler_call_details.invocation_metadata or ():
+            if k == FAULT_DELAY_KEY:
+                try:
+                    await asyncio.sleep(max(0.0, float(v)) / 1000.0)
+                except ValueError:
+                    pass
+        return await continuation(handler_call_details)
+
+
 class GrpcFrontend(service_pb2_grpc.GRPCInferenceServiceServicer):
     def __init__(self, server):
         self.s = server

@@ -7,6 +7,7 @@ gzip/deflate in both directions, system/device shared memory and the
 ``hipsharedmemory`` alias routes.
 """
 
+import asyncio
 import gzip
 import json
 import zlib
@@ -110,10 +111,23 @@ def _raw_output(arr, datatype):
     return memoryview(np.ascontiguousarray(arr)).cast("B")
 
 
+@web.middleware
+async def fault_delay(request, handler):
+    """Test-server fault knob (see grpc_frontend.FaultInjector): a
+    ``tc-fault-delay-ms`` header delays the response."""
+    d = request.headers.get("tc-fault-delay-ms")
+    if d:
+        try:
+            await asyncio.sleep(max(0.0, float(d)) / 1000.0)
+        except ValueError:
+            pass
+    return await handler(request)
+
+
 class HttpFrontend:
     def __init__(self, server):
         self.s = server
-        app = web.Application(client_max_size=2**31 - 1)
+        app = web.Application(client_max_size=2**31 - 1, middlewares=[fault_delay])
         r = app.router
         r.add_get("/v2/health/live", self.live)
         r.add_get("/v2/health/ready", self.ready)
