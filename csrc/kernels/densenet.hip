@@ -27,6 +27,8 @@
 // each lane's 4 accumulators are 4 consecutive output channels of one pixel
 // and the epilogue stores 8 contiguous bytes per lane with no LDS transpose.
 
+#include <algorithm>
+
 #include "kernels/common.h"
 
 namespace {
@@ -267,6 +269,162 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
           if (p.relu_out) v[r] = fmaxf(v[r], 0.f);
         }
         *reinterpret_cast<v2u*>(p.y + (size_t)m * p.ldy + nb) = v2u{pack2(v[0], v[1]), pack2(v[2], v[3])};
+      }
+    }
+  }
+}
+
+// ============================================================================
+// K8p: persistent, software-pipelined 1x1 conv.  Profiling K8 showed every
+// dense-layer 1x1 latency-bound: each block walks K in 32-wide steps with one
+// tile of loads in flight, so a 14x14 layer (K up to 992) waits ~31 global
+// round trips, and the 56x56 layers (2-7 steps per tile) pay the pipeline
+// fill per 64-pixel tile.  Here a block (grid = resident capacity) owns tiles
+// t = blockIdx.x + j * gridDim.x and walks ONE flattened stream of (tile,
+// k-step) steps with D steps of loads in flight in registers — across tile
+// boundaries too — while the MFMAs consume the LDS double buffer; the
+// epilogue of a tile is just a step with a store.  Same block tile, BN
+// prologue and epilogue as K8 (BK = 32, 4 waves as 2 x 2, 16x16x32 MFMA).
+// ============================================================================
+template <int TM, int D, bool PRO>
+__global__ void __launch_bounds__(256) conv1x1_pipe_kernel(Conv1x1Params p) {
+  constexpr int BK = 32, BM = 32 * TM, BN = 128;
+  constexpr int CPR = BK / 8, LDK = BK + 8;
+  constexpr int A_CHUNKS = BM * CPR, AI = (A_CHUNKS + 255) / 256;
+  constexpr int BI = BN * CPR / 256;
+  __shared__ __attribute__((aligned(16))) uint16_t sA[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) uint16_t sB[2][BN * LDK];
+  __shared__ float sS[PRO ? kMaxK : 1], sT[PRO ? kMaxK : 1], sBias[kMaxK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  if constexpr (PRO) {
+    for (int k = tid; k < p.K; k += 256) {
+      sS[k] = p.in_scale[k];
+      sT[k] = p.in_bias[k];
+    }
+  }
+  // epilogue bias from LDS: a global load in the epilogue would make the
+  // in-order vmcnt wait drain every prefetched tile behind it
+  for (int n = tid; n < p.N; n += 256) sBias[n] = p.out_bias ? p.out_bias[n] : 0.f;
+  const int nt = p.N / BN, tiles = ((p.M + BM - 1) / BM) * nt;
+  const int KT = p.K / BK;
+  const int mine = (int)blockIdx.x < tiles ? (tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int G = mine * KT;
+  if (G == 0) return;  // whole block
+
+  // step g -> tile origin (m0, n0) and k offset
+  auto decode = [&](int g, int& m0, int& n0, int& k0) {
+    const int j = g / KT, kt = g - j * KT;
+    const int t = (int)blockIdx.x + j * (int)gridDim.x;
+    const int tm = t / nt;
+    m0 = tm * BM;
+    n0 = (t - tm * nt) * BN;
+    k0 = kt * BK;
+  };
+  v4u ra[D][AI], rb[D][BI];
+  auto load = [&](int g, v4u(&a)[AI], v4u(&b)[BI]) {
+    int m0, n0, k0;
+    decode(g, m0, n0, k0);
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int c = tid + i * 256;
+      const int m = m0 + c / CPR;
+      a[i] = (c < A_CHUNKS && m < p.M) ? ldg16(p.x + (size_t)m * p.ldx + k0 + (c % CPR) * 8) : v4u{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int c = tid + i * 256;
+      b[i] = ldg16(p.w + (size_t)(n0 + c / CPR) * p.K + k0 + (c % CPR) * 8);
+    }
+  };
+  auto store = [&](int g, int buf, const v4u(&a)[AI], const v4u(&b)[BI]) {
+    int m0, n0, k0;
+    decode(g, m0, n0, k0);
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int c = tid + i * 256;
+      if (c < A_CHUNKS) {
+        const int kc = (c % CPR) * 8;
+        v4u v = a[i];
+        if constexpr (PRO) {
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e] * sS[k0 + kc + e] + sT[k0 + kc + e], 0.f);
+          v = pack8(f);
+        }
+        if (m0 + c / CPR >= p.M) v = v4u{0, 0, 0, 0};
+        *reinterpret_cast<v4u*>(&sA[buf][(c / CPR) * LDK + kc]) = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int c = tid + i * 256;
+      *reinterpret_cast<v4u*>(&sB[buf][(c / CPR) * LDK + (c % CPR) * 8]) = b[i];
+    }
+  };
+
+  // loads are issued unconditionally (past the end: the last step again), so
+  // the waitcnt pass sees a straight-line stream of D in-flight steps
+#pragma unroll
+  for (int s = 0; s < D; ++s) load(min(s, G - 1), ra[s], rb[s]);
+  __syncthreads();  // prologue tables
+  store(0, 0, ra[0], rb[0]);
+  __syncthreads();
+
+  f32x4 acc[4][TM];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  for (int g0 = 0; g0 < G; g0 += D) {
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+      const int g = g0 + s;
+      if (g < G) {  // block-uniform
+        const int buf = g & 1;
+        // stage s held step g (already in LDS): refill it with step g + D
+        load(min(g + D, G - 1), ra[s], rb[s]);
+        bf16x8 fa[4], fb[TM];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          fa[j] = *reinterpret_cast<const bf16x8*>(&sB[buf][(wn * 64 + j * 16 + fr) * LDK + fk]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          fb[i] = *reinterpret_cast<const bf16x8*>(&sA[buf][(wm * 16 * TM + i * 16 + fr) * LDK + fk]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) acc[j][i] = mfma16(fa[j], fb[i], acc[j][i]);
+        if (g % KT == KT - 1) {  // tile done: epilogue, restart the accumulators
+          int m0, n0, k0;
+          decode(g, m0, n0, k0);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int nb = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
+            float bias[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bias[r] = sBias[nb + r];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              const int m = m0 + wm * 16 * TM + i * 16 + fr;
+              if (m < p.M) {
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  v[r] = acc[j][i][r] + bias[r];
+                  if (p.relu_out) v[r] = fmaxf(v[r], 0.f);
+                }
+                *reinterpret_cast<v2u*>(p.y + (size_t)m * p.ldy + nb) = v2u{pack2(v[0], v[1]), pack2(v[2], v[3])};
+              }
+              acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+          }
+        }
+        if (g + 1 < G) store(g + 1, buf ^ 1, ra[(s + 1) % D], rb[(s + 1) % D]);
+        __syncthreads();
       }
     }
   }
@@ -728,6 +886,23 @@ __global__ void __launch_bounds__(256) conv3x3_m32_kernel(Conv3x3Params p) {
 // current one computes; all 9 taps then read LDS.  Weights stay LDS-resident
 // (74 KB) and feed v_mfma_f32_32x32x16_bf16 as operand A; one 32-pixel
 // subtile per wave.  Out-of-image taps are zeroed by a per-tap mask.
+// 74 KB of weights global -> LDS with all 18 loads per thread in flight at
+// once (a rolled load->store loop serialises 18 L2 round trips: ~10 us per
+// launch, most of a 14x14 layer's time when each block walks one tile)
+__device__ __forceinline__ void stage_weights(const uint16_t* __restrict__ w, uint16_t* Ws, int tid) {
+  constexpr int kChunks = kN3 * (kK3 / 8), kPer = kChunks / 256;  // 4608 / 256 = 18
+  static_assert(kChunks % 256 == 0, "weight chunks per thread");
+  v4u r[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) r[i] = ldg16(w + (size_t)(tid + i * 256) * 8);
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int c = tid + i * 256;
+    const int n = c / (kK3 / 8), kc = (c - n * (kK3 / 8)) * 8;
+    *reinterpret_cast<v4u*>(&Ws[n * kWsK + kc]) = r[i];
+  }
+}
+
 constexpr int kActStride = kC3 + 8;  // 272-B rows
 constexpr int kTileP = 128;          // output pixels per tile (4 waves x 32)
 
@@ -736,10 +911,7 @@ __global__ void __launch_bounds__(256) conv3x3_lds_kernel(Conv3x3Params p) {
   uint16_t* Ws = smem;                   // [32][kWsK]
   uint16_t* As = smem + kN3 * kWsK;      // [rows][kActStride]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int c = tid; c < kN3 * (kK3 / 8); c += 256) {
-    const int n = c / (kK3 / 8), kc = (c - n * (kK3 / 8)) * 8;
-    *reinterpret_cast<v4u*>(&Ws[n * kWsK + kc]) = ldg16(p.w + (size_t)n * kK3 + kc);
-  }
+  stage_weights(p.w, Ws, tid);
   const int W = p.W, HW = p.H * p.W;
   const int halo = W + 1, rows = kTileP + 2 * halo, chunks = rows * 16;
   constexpr int kMaxChunks = (kTileP + 2 * 57) * 16;       // W <= 56
@@ -801,6 +973,122 @@ __global__ void __launch_bounds__(256) conv3x3_lds_kernel(Conv3x3Params p) {
       for (int g = 0; g < 4; ++g)
         *reinterpret_cast<v2u*>(yp + 8 * g) =
             v2u{pack2(acc[4 * g], acc[4 * g + 1]), pack2(acc[4 * g + 2], acc[4 * g + 3])};
+    }
+  }
+}
+
+// K9r: the K9c tile walk with the weights in REGISTERS instead of LDS.  K9c
+// keeps 74 KB of weights + a 66 KB activation band in LDS, so one block (4
+// waves, one per SIMD) fills a CU and nothing else co-resides.  Here wave w
+// owns input channels [32w, 32w+32) of all 9 taps: its 18 weight fragments
+// (32 out-ch x 16 k each) live in 72 VGPRs for the whole kernel, it runs all
+// four 32-pixel subtiles of the tile over its K quarter, and the four partial
+// tiles are summed through LDS (aliasing the activation band once the taps
+// are done).  LDS per block = the activation band -> two blocks per CU, and
+// per MFMA only the activation fragment is read from LDS.
+constexpr int kRedFloats = 4 * 3 * 64 * 16;  // [subtile][3 other waves][lane][16]
+
+__global__ void __launch_bounds__(256, 2) conv3x3_kr_kernel(Conv3x3Params p) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* As = smem;                                  // [rows][kActStride] bf16
+  float* red = reinterpret_cast<float*>(smem);          // aliases As after the taps
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, kh = 8 * (lane >> 5);
+  v4u wr[18];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) wr[t * 2 + h] = ldg16(p.w + (size_t)col * kK3 + t * kC3 + 32 * wave + 16 * h + kh);
+  const int W = p.W, HW = p.H * p.W;
+  const int halo = W + 1, rows = kTileP + 2 * halo, chunks = rows * 16;
+  constexpr int kMaxChunks = (kTileP + 2 * 57) * 16;
+  constexpr int CPT = (kMaxChunks + 255) / 256;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.z, (short)0,
+                                                      (int)((size_t)p.M * kC3 * 2), 0x00020000);
+  v4u st[CPT];
+  auto load_tile = [&](int tile) {
+    const int base = tile * kTileP - halo;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + i * 256;
+      const int r = c >> 4, q = c & 15;
+      const int pix = base + r;
+      const bool ok = c < chunks && pix >= 0 && pix < p.M;
+      st[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? (pix * kC3 + q * 8) * 2 : 0x40000000, 0, 0);
+    }
+  };
+  // no cross-tile register prefetch (it would not fit next to the resident
+  // weights): the other block on the CU computes while this one loads
+  for (int tile = blockIdx.x; tile < p.tiles; tile += gridDim.x) {
+    load_tile(tile);
+    __syncthreads();  // previous tile's reduction reads done
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + i * 256;
+      if (c < chunks) *reinterpret_cast<v4u*>(&As[(c >> 4) * kActStride + (c & 15) * 8]) = st[i];
+    }
+    __syncthreads();
+    int ph[4], pw[4];
+    bool pv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = tile * kTileP + i * 32 + col;
+      pv[i] = m < p.M;
+      const int r = (pv[i] ? m : 0) % HW;
+      ph[i] = r / W;
+      pw[i] = r - ph[i] * W;
+    }
+    f32x16 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dy = t / 3 - 1, dx = t % 3 - 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = pv[i] && ph[i] + dy >= 0 && ph[i] + dy < p.H && pw[i] + dx >= 0 && pw[i] + dx < W;
+        const uint16_t* arow = &As[(i * 32 + col + halo + dy * W + dx) * kActStride + 32 * wave + kh];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          v4u b = *reinterpret_cast<const v4u*>(arow + 16 * h);
+          if (!ok) b = v4u{0, 0, 0, 0};
+          acc[i] = mfma32(as_frag(wr[t * 2 + h]), as_frag(b), acc[i]);
+        }
+      }
+    }
+    __syncthreads();  // every wave is done reading the activation band
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i == wave) continue;
+      const int slot = wave < i ? wave : wave - 1;
+      f32x4* dst = reinterpret_cast<f32x4*>(red + ((i * 3 + slot) * 64 + lane) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dst[q] = f32x4{acc[i][4 * q], acc[i][4 * q + 1], acc[i][4 * q + 2], acc[i][4 * q + 3]};
+    }
+    __syncthreads();
+    f32x16 sum = acc[0];
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+      if (i == wave) sum = acc[i];  // static register selection (no dynamic indexing)
+#pragma unroll
+    for (int sl = 0; sl < 3; ++sl) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(red + ((wave * 3 + sl) * 64 + lane) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v = src[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sum[4 * q + e] += v[e];
+      }
+    }
+    const int m = tile * kTileP + wave * 32 + col;
+    if (m < p.M) {
+      uint16_t* yp = p.y + (size_t)m * p.ldy + 4 * (lane >> 5);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<v2u*>(yp + 8 * g) =
+            v2u{pack2(sum[4 * g], sum[4 * g + 1]), pack2(sum[4 * g + 2], sum[4 * g + 3])};
     }
   }
 }
@@ -1104,6 +1392,24 @@ int launch_1x1(Conv1x1Params p, int splits, hipStream_t s) {
   return hipGetLastError();
 }
 
+// K8p launch: one persistent block per resident slot (occupancy x CUs), or
+// one per tile when there are fewer tiles.
+template <int TM, int D, bool PRO>
+int launch_1x1_pipe(const Conv1x1Params& p, hipStream_t s) {
+  static int slots = 0;
+  if (!slots) {
+    int dev = 0, cus = 0, occ = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv1x1_pipe_kernel<TM, D, PRO>, 256, 0) != hipSuccess)
+      return hipErrorInvalidValue;
+    slots = std::max(1, cus * occ);
+  }
+  const int tiles = ((p.M + 32 * TM - 1) / (32 * TM)) * (p.N / 128);
+  hipLaunchKernelGGL((conv1x1_pipe_kernel<TM, D, PRO>), dim3(std::min(tiles, slots)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
 // variant: 0 = heuristic, else 10*TM + BK/32 (e.g. 42 = TM 4, BK 64)
 // variant: 0 = heuristic, else 10*TM + BK/32.  splits: 0 = heuristic (needs a
 // workspace), 1 = no split-K.  Heuristic from tools/kbench_densenet.py on
@@ -1117,6 +1423,20 @@ int pick_1x1(const Conv1x1Params& p, int variant, int splits, size_t ws_bytes, h
     if (!PRO || p.K % 32) return hipErrorInvalidValue;
     hipLaunchKernelGGL((conv1x1_sk_kernel<POOL>), dim3((p.M + 31) / 32, p.N / 128), dim3(256), 0, s, p);
     return hipGetLastError();
+  }
+  if (variant > 100) {  // K8p: 100 + 10*TM + pipeline depth (no split-K, no pool)
+    if (POOL || p.K % 32 || p.N > kMaxK) return hipErrorInvalidValue;
+    switch (variant) {
+      case 112: return launch_1x1_pipe<1, 2, PRO>(p, s);
+      case 113: return launch_1x1_pipe<1, 3, PRO>(p, s);
+      case 114: return launch_1x1_pipe<1, 4, PRO>(p, s);
+      case 122: return launch_1x1_pipe<2, 2, PRO>(p, s);
+      case 123: return launch_1x1_pipe<2, 3, PRO>(p, s);
+      case 124: return launch_1x1_pipe<2, 4, PRO>(p, s);
+      case 142: return launch_1x1_pipe<4, 2, PRO>(p, s);
+      case 143: return launch_1x1_pipe<4, 3, PRO>(p, s);
+      default: return hipErrorInvalidValue;
+    }
   }
   const int tm = variant / 10, bk = (variant % 10) * 32;
   const long blocks = (long)((p.M + 32 * tm - 1) / (32 * tm)) * (p.N / 128);
@@ -1168,6 +1488,23 @@ int launch_3x3_m32(Conv3x3Params p, hipStream_t s) {
   p.tiles = (p.M + 128 * TM - 1) / (128 * TM);
   const int grid = p.tiles < 512 ? p.tiles : 512;
   hipLaunchKernelGGL((conv3x3_m32_kernel<TM>), dim3(grid), dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
+int launch_3x3_kr(Conv3x3Params p, hipStream_t s) {
+  if (p.W > 56) return hipErrorInvalidValue;
+  const int act = (kTileP + 2 * (p.W + 1)) * kActStride * 2;
+  const int lds = std::max(act, kRedFloats * 4);
+  static int attr = 0;
+  const int lmax = std::max((kTileP + 2 * 57) * kActStride * 2, kRedFloats * 4);
+  if (attr < lmax) {
+    int rc = hipFuncSetAttribute((const void*)conv3x3_kr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lmax);
+    if (rc != hipSuccess) return rc;
+    attr = lmax;
+  }
+  p.tiles = (p.M + kTileP - 1) / kTileP;
+  const int grid = p.tiles < 512 ? p.tiles : 512;  // two resident blocks per CU
+  hipLaunchKernelGGL(conv3x3_kr_kernel, dim3(grid), dim3(256), lds, s, p);
   return hipGetLastError();
 }
 
@@ -1264,7 +1601,11 @@ int tcamd_dn_conv3x3_v(const void* z, int imgs, int H, int W, const void* w, voi
   // wins once there are enough 128-pixel tiles to fill the CUs; tiny problems
   // keep the 64-pixel-tile direct-load kernel
   // (M <= 8192: the 7x7 / 14x14 layers of small batches) the wave-split K9s
-  if (variant == 0) variant = M <= 8192 ? 70 : (W <= 56 && (M + 127) / 128 >= 96) ? 60 : 11;
+  // (M <= 8192: the 7x7 / 14x14 layers of small batches) the wave-split K9s;
+  // once there are >= 512 tiles (two per CU) the register-weight K9r, whose
+  // 66 KB LDS footprint also lets other streams' kernels share the CU
+  if (variant == 0)
+    variant = M <= 8192 ? 70 : (W <= 56 && (M + 127) / 128 >= 512) ? 80 : (W <= 56 && (M + 127) / 128 >= 96) ? 60 : 11;
   switch (variant) {
     case 10: return launch_3x3<1, 0>(p, s);  // channel-major tap walk
     case 16: return launch_3x3<1, 6>(p, s);   // 6-deep load ring
@@ -1278,6 +1619,7 @@ int tcamd_dn_conv3x3_v(const void* z, int imgs, int H, int W, const void* w, voi
     case 23: return launch_3x3<2, 3>(p, s);
     case 41: return launch_3x3<4, 1>(p, s);
     case 60: return launch_3x3_lds(p, s);     // LDS-staged activations, 32x32x16 MFMA
+    case 80: return launch_3x3_kr(p, s);      // K9r: weights in registers, K split over waves
     case 70:                                  // K9s: waves split the input channels
       hipLaunchKernelGGL(conv3x3_sk_kernel, dim3((p.M + 31) / 32), dim3(256), 0, s, p);
       return hipGetLastError();

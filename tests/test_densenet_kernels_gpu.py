@@ -37,7 +37,7 @@ def _close(got, ref, tol=2e-2):
 
 @pytest.mark.parametrize("M,K,ldx,N,off", [(100, 64, 96, 128, 32), (40000, 224, 256, 128, 0),
                                            (70000, 96, 128, 128, 0), (3000, 512, 512, 256, 0)])
-@pytest.mark.parametrize("variant", [0, 70])
+@pytest.mark.parametrize("variant", [0, 70, 112, 113, 114, 122, 123, 124, 142, 143])
 def test_conv1x1_prologue_epilogue(M, K, ldx, N, off, variant):
     _need_gpu()
     hip = _hip()
@@ -126,7 +126,7 @@ def test_conv1x1_transition_pool(imgs, H, C, N):
     assert (y[:, N:] == 0).all()
 
 
-@pytest.mark.parametrize("variant", [0, 10, 11, 13, 16, 19, 21, 41, 51, 52, 60, 70])
+@pytest.mark.parametrize("variant", [0, 10, 11, 13, 16, 19, 21, 41, 51, 52, 60, 70, 80])
 @pytest.mark.parametrize("imgs,H", [(1, 7), (3, 14), (8, 56), (48, 56), (5, 28)])
 def test_conv3x3(imgs, H, variant):
     _need_gpu()

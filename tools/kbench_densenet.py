@@ -14,8 +14,8 @@ import torch
 
 from triton_client_amd.ops import hip
 
-V1 = (11, 12, 21, 22, 41, 42, 70)
-V3 = (0, 11, 60, 70)
+V1 = (11, 12, 21, 22, 41, 112, 113, 114, 122, 123, 124, 142, 143)
+V3 = (0, 60, 70, 80)
 
 
 def cs():
@@ -46,6 +46,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--only", default="", help="'1x1' or '3x3'")
     a = ap.parse_args()
     dev = "cuda"
     b = a.batch
@@ -56,7 +57,7 @@ def main():
         M = b * hw * hw
         x = torch.randn(M, ctot, device=dev).bfloat16()
         z = torch.randn(M, 128, device=dev).bfloat16()
-        for K in sorted({c0, c0 + 32 * (n // 2), c0 + 32 * (n - 1)}):
+        for K in sorted({c0, c0 + 32 * (n // 2), c0 + 32 * (n - 1)}) if a.only != "3x3" else []:
             s1 = torch.rand(K, device=dev) + 0.5
             t1 = torch.randn(K, device=dev)
             w = torch.randn(128, K, device=dev).bfloat16()
@@ -71,6 +72,8 @@ def main():
             row["best"] = best
             res["conv1x1"].append(row)
             print("1x1", row, flush=True)
+        if a.only == "1x1":
+            continue
         w2 = torch.randn(32, 3, 3, 128, device=dev).bfloat16()
         row = {"hw": hw, "M": M}
         for v in V3:
