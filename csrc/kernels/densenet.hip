@@ -93,13 +93,14 @@ struct Conv1x1Params {
 // double-buffered with register prefetch (global loads of tile k+1 are in
 // flight during the MFMAs on tile k).  K need not be a multiple of BK: the
 // tail chunk is zero-filled (K % 32 == 0 always holds).
-template <int TM, int BK, bool PRO, bool POOL>
+template <int TM, int BK, bool PRO, bool POOL, int BN = 128>
 __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
-  constexpr int BM = 32 * TM, BN = 128;
+  constexpr int BM = 32 * TM, NJ = BN / 32, WN = BN / 2;  // wave: 16*TM pixels x BN/2 channels
   constexpr int CPR = BK / 8;                 // 16-B chunks per row of a K tile
   constexpr int LDK = BK + 8;                 // LDS row stride (elements): conflict-free b128 reads
   constexpr int A_CHUNKS = BM * CPR, AI = (A_CHUNKS + 255) / 256;
-  constexpr int BI = BN * CPR / 256;
+  constexpr int BI = (BN * CPR + 255) / 256;
+  static_assert(BN * CPR % 256 == 0, "B chunks per thread");
   constexpr int NS = POOL ? 4 : 1;
   __shared__ __attribute__((aligned(16))) uint16_t sA[2][BM * LDK];
   __shared__ __attribute__((aligned(16))) uint16_t sB[2][BN * LDK];
@@ -201,9 +202,9 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
     }
   };
 
-  f32x4 acc[4][TM];
+  f32x4 acc[NJ][TM];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -220,15 +221,15 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
     if (kt + 1 < KT) load_tile(kt + 1);
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 fa[4], fb[TM];
+      bf16x8 fa[NJ], fb[TM];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        fa[j] = *reinterpret_cast<const bf16x8*>(&sB[buf][(wn * 64 + j * 16 + fr) * LDK + ks * 32 + fk]);
+      for (int j = 0; j < NJ; ++j)
+        fa[j] = *reinterpret_cast<const bf16x8*>(&sB[buf][(wn * WN + j * 16 + fr) * LDK + ks * 32 + fk]);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
         fb[i] = *reinterpret_cast<const bf16x8*>(&sA[buf][(wm * 16 * TM + i * 16 + fr) * LDK + ks * 32 + fk]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int i = 0; i < TM; ++i) acc[j][i] = mfma16(fa[j], fb[i], acc[j][i]);
     }
@@ -239,8 +240,8 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
   if (p.ws) {  // split-K: raw fp32 partials, epilogue in dn_splitk_reduce
     float* ws = p.ws + (size_t)blockIdx.z * p.M * p.N;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int nb = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
+    for (int j = 0; j < NJ; ++j) {
+      const int nb = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int m = m0 + wm * 16 * TM + i * 16 + fr;
@@ -251,8 +252,8 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
   }
   // epilogue: lane holds out channels nb..nb+3 of pixel m
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int nb = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
+  for (int j = 0; j < NJ; ++j) {
+    const int nb = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
     float bias[4] = {0.f, 0.f, 0.f, 0.f};
     if (p.out_bias) {
 #pragma unroll
@@ -1371,9 +1372,9 @@ __global__ void __launch_bounds__(256) conv3x3_sk_kernel(Conv3x3Params p) {
   }
 }
 
-template <int TM, int BK, bool PRO, bool POOL>
+template <int TM, int BK, bool PRO, bool POOL, int BN = 128>
 int launch_1x1(Conv1x1Params p, int splits, hipStream_t s) {
-  const int mb = (p.M + 32 * TM - 1) / (32 * TM), nb = p.N / 128;
+  const int mb = (p.M + 32 * TM - 1) / (32 * TM), nb = p.N / BN;
   if (splits > 1) {
     const int kts = (p.K + BK - 1) / BK;
     const int per = (kts + splits - 1) / splits;
@@ -1383,7 +1384,7 @@ int launch_1x1(Conv1x1Params p, int splits, hipStream_t s) {
     p.ws = nullptr;
   }
   dim3 g(mb, nb, splits > 1 ? splits : 1);
-  hipLaunchKernelGGL((conv1x1_kernel<TM, BK, PRO, POOL>), g, dim3(256), 0, s, p);
+  hipLaunchKernelGGL((conv1x1_kernel<TM, BK, PRO, POOL, BN>), g, dim3(256), 0, s, p);
   if (splits > 1) {
     const size_t total = (size_t)p.M * (p.N / 4);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(tcamd::grid_for(total)), dim3(256), 0, s, p.ws, splits, p.M, p.N,
@@ -1418,11 +1419,33 @@ int launch_1x1_pipe(const Conv1x1Params& p, hipStream_t s) {
 // blocks run (the reduce launch costs ~2 us, so only when it pays).
 template <bool PRO, bool POOL>
 int pick_1x1(const Conv1x1Params& p, int variant, int splits, size_t ws_bytes, hipStream_t s) {
-  if (variant == 0) variant = p.M >= 32768 ? 21 : p.M >= 8192 ? 11 : 12;
+  if (variant == 0) variant = p.M >= 32768 ? 21 : p.M >= 8192 ? 11 : (p.M > 4096 && !POOL) ? 212 : 12;
   if (variant == 70) {  // K8s: waves split K (needs the BN prologue)
     if (!PRO || p.K % 32) return hipErrorInvalidValue;
     hipLaunchKernelGGL((conv1x1_sk_kernel<POOL>), dim3((p.M + 31) / 32, p.N / 128), dim3(256), 0, s, p);
     return hipGetLastError();
+  }
+  if (variant > 200) {  // K8 with 64-channel block tiles: 200 + 10*TM + BK/32 (2x the blocks for small M)
+    if (p.N % 64) return hipErrorInvalidValue;
+    const int tm = (variant - 200) / 10, bk = (variant % 10) * 32;
+    const long blocks = (long)((p.M + 32 * tm - 1) / (32 * tm)) * (p.N / 64);
+    const int kts = (p.K + bk - 1) / bk;
+    if (splits == 0) {
+      splits = 1;
+      if (p.ws && blocks < 128 && kts >= 4) {
+        splits = (int)((256 + blocks - 1) / blocks);
+        if (splits > kts / 2) splits = kts / 2;
+        if (splits > 16) splits = 16;
+      }
+    }
+    if (splits > 1 && (!p.ws || ws_bytes < (size_t)splits * p.M * p.N * sizeof(float))) splits = 1;
+    switch (variant) {
+      case 211: return launch_1x1<1, 32, PRO, POOL, 64>(p, splits, s);
+      case 212: return launch_1x1<1, 64, PRO, POOL, 64>(p, splits, s);
+      case 221: return launch_1x1<2, 32, PRO, POOL, 64>(p, splits, s);
+      case 222: return launch_1x1<2, 64, PRO, POOL, 64>(p, splits, s);
+      default: return hipErrorInvalidValue;
+    }
   }
   if (variant > 100) {  // K8p: 100 + 10*TM + pipeline depth (no split-K, no pool)
     if (POOL || p.K % 32 || p.N > kMaxK) return hipErrorInvalidValue;

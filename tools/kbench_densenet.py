@@ -14,7 +14,7 @@ import torch
 
 from triton_client_amd.ops import hip
 
-V1 = (11, 12, 21, 22, 41, 112, 113, 114, 122, 123, 124, 142, 143)
+V1 = (11, 12, 21, 22, 41, 211, 212, 221, 222)
 V3 = (0, 60, 70, 80)
 
 
