@@ -1,4 +1,6 @@
 // perf_analyzer CLI entry point (see perf.h for the architecture).
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 
 #include "perf.h"
@@ -32,9 +34,22 @@ int main(int argc, char** argv)
     for (uint64_t c = o.conc_start; c <= o.conc_end; c += o.conc_step) loads.push_back(static_cast<double>(c));
   }
   std::vector<tcperf::PointResult> pts;
+  e = tcperf::LoadCheckpoint(o, &pts);
+  if (!e.IsOk()) {
+    fprintf(stderr, "error: %s\n", e.Message().c_str());
+    return 1;
+  }
+  for (const auto& p : pts) {
+    printf("Resumed from %s: %s %g (already measured)\n", o.json_file.c_str(),
+           o.rate_mode ? "request rate" : "concurrency", p.load);
+    tcperf::PrintPoint(o, p);
+  }
   tcperf::Profiler prof(o, s->backend.get(), s->engine.get());
   int rc = 0;
   for (double load : loads) {
+    bool done = false;
+    for (const auto& q : pts) done = done || std::fabs(q.load - load) < 1e-9;
+    if (done) continue;
     tcperf::PointResult p;
     e = prof.Profile(load, &p);
     if (!e.IsOk()) {
@@ -44,6 +59,9 @@ int main(int argc, char** argv)
     }
     tcperf::PrintPoint(o, p);
     pts.push_back(p);
+    // checkpoint after every point: a killed sweep resumes with --resume
+    tcperf::Error ce = tcperf::WriteJson(o, pts, s->data->Describe());
+    if (!ce.IsOk()) fprintf(stderr, "error: %s\n", ce.Message().c_str());
     const double lat = o.percentile > 0 ? p.p99_us : p.avg_us;
     if (o.latency_threshold_ms && lat > o.latency_threshold_ms * 1000.0) {
       printf("Measured latency went over the set limit of %lu msec.\n",
@@ -52,6 +70,8 @@ int main(int argc, char** argv)
     }
   }
   s->engine->Stop();
+  std::sort(pts.begin(), pts.end(),
+            [](const tcperf::PointResult& a, const tcperf::PointResult& b) { return a.load < b.load; });
   if (!pts.empty()) tcperf::PrintSummary(o, pts);
   e = tcperf::WriteCsv(o, pts);
   if (!e.IsOk()) fprintf(stderr, "error: %s\n", e.Message().c_str());

@@ -14,7 +14,7 @@ namespace {
 enum LongOnly {
   OPT_SYNC = 1000, OPT_ASYNC, OPT_STREAMING, OPT_SHAPE, OPT_CONC_RANGE, OPT_RATE_RANGE, OPT_DIST, OPT_INTERVALS,
   OPT_SEQ_LEN, OPT_SEQ_RANGE, OPT_INPUT_DATA, OPT_STR_LEN, OPT_STR_DATA, OPT_SHM, OPT_OUT_SHM_SIZE, OPT_MEAS_MODE,
-  OPT_MEAS_COUNT, OPT_PERCENTILE, OPT_WARMUP, OPT_VERBOSE_CSV, OPT_JSON, OPT_SHM_INPUT, OPT_DEVICE, OPT_SEED,
+  OPT_MEAS_COUNT, OPT_PERCENTILE, OPT_WARMUP, OPT_VERBOSE_CSV, OPT_JSON, OPT_RESUME, OPT_SHM_INPUT, OPT_DEVICE, OPT_SEED,
   OPT_NUM_CLIENTS, OPT_NO_SERVER_STATS, OPT_MEAS_INTERVAL, OPT_STABILITY, OPT_MAX_TRIALS, OPT_LAT_THRESH,
 };
 
@@ -87,7 +87,9 @@ std::string Usage()
       "  --warmup-request-count <n>       requests before the first window\n"
       "  -f <file.csv>                    CSV report;  --verbose-csv adds per-point percentiles\n"
       "  -v                               verbose\n"
-      "  [ext] --json-report <file>       machine-readable report\n"
+      "  [ext] --json-report <file>       machine-readable report (rewritten after every sweep point)\n"
+      "  [ext] --resume                   skip sweep points already in --json-report (same model/batch/\n"
+      "                                   protocol/shm/mode) and keep them in the reports\n"
       "  [ext] --shared-memory-input NAME=REGION  use a region the caller already registered\n"
       "  [ext] --device <gpu>             GPU for hip shared memory (default 0)\n"
       "  [ext] --seed <n>                 synthetic data seed (K1 Philox stream)\n"
@@ -129,6 +131,7 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
       {"warmup-request-count", required_argument, nullptr, OPT_WARMUP},
       {"verbose-csv", no_argument, nullptr, OPT_VERBOSE_CSV},
       {"json-report", required_argument, nullptr, OPT_JSON},
+      {"resume", no_argument, nullptr, OPT_RESUME},
       {"shared-memory-input", required_argument, nullptr, OPT_SHM_INPUT},
       {"device", required_argument, nullptr, OPT_DEVICE},
       {"seed", required_argument, nullptr, OPT_SEED},
@@ -267,6 +270,7 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
       case 'f': o->csv_file = arg; break;
       case OPT_VERBOSE_CSV: o->verbose_csv = true; break;
       case OPT_JSON: o->json_file = arg; break;
+      case OPT_RESUME: o->resume = true; break;
       case OPT_SHM_INPUT: {
         auto p = arg.find('=');
         if (p == std::string::npos) return Error("--shared-memory-input expects NAME=REGION");

@@ -93,6 +93,7 @@ struct Options {
   uint64_t warmup_requests = 0;
   std::string csv_file;
   std::string json_file;
+  bool resume = false;  // --resume: continue a sweep checkpointed in json_file
   bool verbose_csv = false;
   bool collect_server_stats = true;
 };
@@ -298,6 +299,8 @@ void PrintPoint(const Options& o, const PointResult& p);
 void PrintSummary(const Options& o, const std::vector<PointResult>& pts);
 Error WriteCsv(const Options& o, const std::vector<PointResult>& pts);
 Error WriteJson(const Options& o, const std::vector<PointResult>& pts, const std::string& data_desc);
+/// --resume: sweep points already completed in o.json_file (empty if none / other config).
+Error LoadCheckpoint(const Options& o, std::vector<PointResult>* pts);
 double Percentile(std::vector<uint64_t>& v, double p);
 
 /// Everything one perf run needs; used by main() and the C API.

@@ -6,10 +6,13 @@
 #include <cmath>
 #include <cstdio>
 #include <fstream>
+#include <iterator>
 #include <numeric>
 #include <sstream>
 
+#include "json.h"
 #include "perf.h"
+#include "trace.h"
 
 namespace tcperf {
 
@@ -85,6 +88,9 @@ static double StabilityLatency(const Options& o, const PointResult& r)
 
 Error Profiler::Window(PointResult* w, std::vector<uint64_t>* lat)
 {
+  char tag[96];
+  snprintf(tag, sizeof(tag), "perf.window %s=%g", o_.rate_mode ? "rate" : "concurrency", w->load);
+  triton::client::trace::Range range(tag);
   ServerStats s0, s1;
   triton::client::InferStat c0, c1;
   if (o_.collect_server_stats) {
@@ -147,6 +153,7 @@ Error Profiler::Profile(double load, PointResult* out)
   std::vector<std::vector<uint64_t>> lats;
   for (int trial = 0; trial < o_.max_trials; ++trial) {
     PointResult w;
+    w.load = load;
     std::vector<uint64_t> lat;
     e = Window(&w, &lat);
     if (!e.IsOk()) return e;
@@ -333,6 +340,64 @@ Error WriteJson(const Options& o, const std::vector<PointResult>& pts, const std
     f << buf;
   }
   f << "]}\n";
+  return Error::Success;
+}
+
+Error LoadCheckpoint(const Options& o, std::vector<PointResult>* pts)
+{
+  pts->clear();
+  if (!o.resume || o.json_file.empty()) return Error::Success;
+  std::ifstream f(o.json_file);
+  if (!f) return Error::Success;  // nothing to resume yet
+  std::string text((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  namespace js = triton::client::json;
+  js::Value root;
+  std::string err;
+  if (!js::Parse(text, &root, &err)) return Error("--resume: cannot parse " + o.json_file + ": " + err);
+  auto str = [&](const char* k) {
+    const js::Value* v = root.Find(k);
+    return v && v->IsString() ? v->AsString() : std::string();
+  };
+  const js::Value* b = root.Find("batch_size");
+  if (str("model") != o.model || !b || b->AsInt() != static_cast<int64_t>(o.batch) || str("protocol") != o.protocol ||
+      str("shared_memory") != o.shared_memory || str("mode") != (o.rate_mode ? "request_rate" : "concurrency"))
+    return Error("--resume: " + o.json_file + " holds a different sweep (model/batch/protocol/shm/mode)");
+  const js::Value* arr = root.Find("points");
+  if (!arr || !arr->IsArray()) return Error::Success;
+  auto num = [](const js::Value& o, const char* k) {
+    const js::Value* v = o.Find(k);
+    return v ? v->AsDouble() : 0.0;
+  };
+  for (const js::Value& e : arr->Elements()) {
+    PointResult p;
+    p.load = num(e, "load");
+    p.rate_mode = o.rate_mode;
+    const js::Value* st = e.Find("stable");
+    p.stable = st && st->AsBool();
+    p.request_count = static_cast<uint64_t>(num(e, "request_count"));
+    p.window_s = num(e, "window_s");
+    p.throughput = num(e, "throughput");
+    p.avg_us = num(e, "avg_us");
+    p.std_us = num(e, "std_us");
+    p.p50_us = num(e, "p50_us");
+    p.p90_us = num(e, "p90_us");
+    p.p95_us = num(e, "p95_us");
+    p.p99_us = num(e, "p99_us");
+    p.client_send_us = num(e, "client_send_us");
+    p.client_recv_us = num(e, "client_recv_us");
+    p.errors = static_cast<uint64_t>(num(e, "errors"));
+    if (const js::Value* sv = e.Find("server")) {
+      p.has_server = true;
+      p.server.inference_count = static_cast<uint64_t>(num(*sv, "inference_count"));
+      p.server.execution_count = static_cast<uint64_t>(num(*sv, "execution_count"));
+      p.server.success_count = static_cast<uint64_t>(num(*sv, "success_count"));
+      p.server.queue_ns = static_cast<uint64_t>(num(*sv, "queue_ns"));
+      p.server.compute_input_ns = static_cast<uint64_t>(num(*sv, "compute_input_ns"));
+      p.server.compute_infer_ns = static_cast<uint64_t>(num(*sv, "compute_infer_ns"));
+      p.server.compute_output_ns = static_cast<uint64_t>(num(*sv, "compute_output_ns"));
+    }
+    pts->push_back(p);
+  }
   return Error::Success;
 }
 

@@ -31,6 +31,7 @@
 #include "h2.h"
 #include "net.h"
 #include "tcserve.h"
+#include "trace.h"
 
 namespace tcserve {
 
@@ -1142,7 +1143,13 @@ void Server::Execute(NativeModel* m, int instance, std::vector<std::unique_ptr<P
   b.timing_ns = timing;
   char err[1024] = {0};
   const uint64_t t_exec = NowNs();
-  const int rc = m->fn(m->user, instance, &b, err, sizeof(err));
+  int rc;
+  {
+    char tag[160];
+    snprintf(tag, sizeof(tag), "tcserve.batch %s inst=%d requests=%d rows=%d", m->name.c_str(), instance, n, total);
+    triton::client::trace::Range range(tag);
+    rc = m->fn(m->user, instance, &b, err, sizeof(err));
+  }
   const uint64_t t_done = NowNs();
   {
     std::lock_guard<std::mutex> lk(m->smu);

@@ -15,6 +15,7 @@
 
 #include "h2.h"
 #include "net.h"
+#include "trace.h"
 
 namespace triton { namespace client {
 
@@ -636,6 +637,7 @@ InferenceServerGrpcClient::Infer(
     const std::vector<const InferRequestedOutput*>& outputs, const Headers& headers,
     grpc_compression_algorithm compression_algorithm)
 {
+  trace::Range range("tc.grpc.Infer");
   RequestTimers timers;
   timers.CaptureTimestamp(K::REQUEST_START);
   timers.CaptureTimestamp(K::SEND_START);

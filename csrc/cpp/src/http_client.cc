@@ -20,6 +20,7 @@
 
 #include "json.h"
 #include "net.h"
+#include "trace.h"
 
 namespace triton { namespace client {
 
@@ -1179,6 +1180,7 @@ InferenceServerHttpClient::Infer(
     const std::vector<const InferRequestedOutput*>& outputs, const Headers& headers, const Parameters& query_params,
     const CompressionType request_compression_algorithm, const CompressionType response_compression_algorithm)
 {
+  trace::Range range("tc.http.Infer");
   RequestTimers timers;
   timers.CaptureTimestamp(K::REQUEST_START);
   HttpPreparedRequest req;

@@ -53,6 +53,44 @@ def test_concurrency_sweep_csv(cpu_server, tmp_path, proto):
     assert rep["points"][0]["server"]["success_count"] > 0
 
 
+def test_sweep_checkpoint_and_resume(cpu_server, tmp_path):
+    """The JSON report is a checkpoint: --resume skips completed points, keeps
+    them in the reports, and refuses a checkpoint of a different sweep."""
+    j = tmp_path / "sweep.json"
+    base = ["-m", "simple", "-i", "grpc", "-u", cpu_server.grpc_url, "-p", "200", "-r", "3", "--json-report", j]
+    r = _pa(base + ["--concurrency-range", "1:2:1"])
+    assert r.returncode == 0, r.stderr
+    first = json.load(open(j))
+    assert [p["load"] for p in first["points"]] == [1, 2]
+    # a sweep that died after concurrency 1
+    partial = dict(first, points=first["points"][:1])
+    json.dump(partial, open(j, "w"))
+    f = tmp_path / "sweep.csv"
+    r = _pa(base + ["--concurrency-range", "1:3:1", "--resume", "-f", f])
+    assert r.returncode == 0, r.stderr
+    assert "Resumed from" in r.stdout and "concurrency 1 (already measured)" in r.stdout
+    assert r.stdout.count("Request concurrency: 1") == 1  # reprinted from the checkpoint, not re-measured
+    assert "Request concurrency: 2" in r.stdout and "Request concurrency: 3" in r.stdout
+    done = json.load(open(j))
+    assert [p["load"] for p in done["points"]] == [1, 2, 3]
+    assert done["points"][0]["throughput"] == pytest.approx(first["points"][0]["throughput"], rel=1e-3)
+    assert [row["Concurrency"] for row in csv.DictReader(open(f))] == ["1", "2", "3"]
+    # a checkpoint from another model is refused
+    r = _pa(["-m", "simple_string", "-i", "grpc", "-u", cpu_server.grpc_url, "-p", "200", "--json-report", j,
+             "--resume"])
+    assert r.returncode == 1 and "different sweep" in r.stderr
+
+
+def test_roctx_ranges_enabled_without_profiler(cpu_server):
+    """TC_ROCTX=1 loads roctx and pushes ranges (perf windows, client Infer);
+    without a profiler attached they are no-ops and the run is unchanged."""
+    env = dict(os.environ, TC_ROCTX="1")
+    r = subprocess.run([native.BIN_PATH, "-m", "simple", "-i", "grpc", "-u", cpu_server.grpc_url, "-p", "200", "-r",
+                        "3", "--sync"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    assert "Request concurrency: 1" in r.stdout
+
+
 def test_system_shm_sync_count_windows(cpu_server):
     r = _pa(["-m", "simple", "-u", cpu_server.http_url, "--sync", "--shared-memory", "system",
              "--measurement-mode", "count_windows", "--measurement-request-count", "60",

@@ -8,9 +8,12 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
 rm -f gpurun_out/prof/*.csv
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o server -- \
+# MARKERS=1: also record roctx ranges (tcserve batches, model forwards; TC_ROCTX=1 turns them on)
+TRACE="--kernel-trace --stats"
+if [ "${MARKERS:-0}" = 1 ]; then export TC_ROCTX=1; TRACE="$TRACE --marker-trace"; fi
+timeout -k 10 900 rocprofv3 $TRACE --output-format csv -d gpurun_out/prof -o server -- \
   python3 -m triton_client_amd.server --http-port 18000 --grpc-port 18001 --gpu --models densenet_onnx \
-  --instance-count 2 > gpurun_out/prof_server.log 2>&1 &
+  --instance-count 3 --preferred-batch-sizes 128 --max-queue-delay-us 2000 > gpurun_out/prof_server.log 2>&1 &
 PROF_PID=$!
 timeout -k 10 600 python3 bench.py --server-url 127.0.0.1:18001 --http-url 127.0.0.1:18000 "$@" \
   > gpurun_out/prof_bench.log 2>&1

@@ -19,6 +19,8 @@ For a few-MB batch the broadcast is latency-bound (densenet bs=8: 4.8 MB is
 
 import numpy as np
 
+from triton_client_amd.utils import roctx
+
 
 def _dist():
     import torch.distributed as dist
@@ -57,11 +59,13 @@ def fill_and_fanout(region, datatype, n_elems, seed=0, mode="random", lo=0.0, hi
         import torch
 
         t = region_tensor(region, nbytes)
-        dist.broadcast(t, src=0)
+        with roctx.range("fanout.rccl_broadcast bytes=%d" % t.numel()):
+            dist.broadcast(t, src=0)
         torch.cuda.synchronize()
         return "rccl"
     if method == "p2p":
-        return _p2p_star(region, nbytes, dist)
+        with roctx.range("fanout.p2p_star bytes=%d" % nbytes):
+            return _p2p_star(region, nbytes, dist)
     raise ValueError("unknown fan-out method %s" % method)
 
 

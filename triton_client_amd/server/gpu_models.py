@@ -24,6 +24,8 @@ import threading
 
 import numpy as np
 
+from triton_client_amd.utils import roctx
+
 from .model_base import Model, TensorSpec
 from .types import DeviceView, OutputTensor, ServerError
 
@@ -154,6 +156,10 @@ class DensenetOnnx(Model):
 
     def forward_device(self, slot, srcs, rows):
         """Assemble ``rows`` images from device pointers and run the model."""
+        with roctx.range("densenet_onnx.forward rows=%d" % rows):
+            return self._forward_device(slot, srcs, rows)
+
+    def _forward_device(self, slot, srcs, rows):
         torch = self.torch
         from triton_client_amd.ops import hip
 
