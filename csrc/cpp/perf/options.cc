@@ -14,7 +14,7 @@ namespace {
 enum LongOnly {
   OPT_SYNC = 1000, OPT_ASYNC, OPT_STREAMING, OPT_SHAPE, OPT_CONC_RANGE, OPT_RATE_RANGE, OPT_DIST, OPT_INTERVALS,
   OPT_SEQ_LEN, OPT_SEQ_RANGE, OPT_INPUT_DATA, OPT_STR_LEN, OPT_STR_DATA, OPT_SHM, OPT_OUT_SHM_SIZE, OPT_MEAS_MODE,
-  OPT_MEAS_COUNT, OPT_PERCENTILE, OPT_WARMUP, OPT_VERBOSE_CSV, OPT_JSON, OPT_RESUME, OPT_SHM_INPUT, OPT_DEVICE, OPT_SEED,
+  OPT_MEAS_COUNT, OPT_PERCENTILE, OPT_WARMUP, OPT_VERBOSE_CSV, OPT_JSON, OPT_RESUME, OPT_COLLECT_METRICS, OPT_METRICS_INTERVAL, OPT_METRICS_SYSFS, OPT_SHM_INPUT, OPT_DEVICE, OPT_SEED,
   OPT_NUM_CLIENTS, OPT_NO_SERVER_STATS, OPT_MEAS_INTERVAL, OPT_STABILITY, OPT_MAX_TRIALS, OPT_LAT_THRESH,
 };
 
@@ -88,6 +88,8 @@ std::string Usage()
       "  -f <file.csv>                    CSV report;  --verbose-csv adds per-point percentiles\n"
       "  -v                               verbose\n"
       "  [ext] --json-report <file>       machine-readable report (rewritten after every sweep point)\n"
+      "  --collect-metrics                GPU utilization / power / VRAM of --device (amdgpu sysfs)\n"
+      "  --metrics-interval <ms>          GPU metrics sampling interval (default 1000)\n"
       "  [ext] --resume                   skip sweep points already in --json-report (same model/batch/\n"
       "                                   protocol/shm/mode) and keep them in the reports\n"
       "  [ext] --shared-memory-input NAME=REGION  use a region the caller already registered\n"
@@ -132,6 +134,9 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
       {"verbose-csv", no_argument, nullptr, OPT_VERBOSE_CSV},
       {"json-report", required_argument, nullptr, OPT_JSON},
       {"resume", no_argument, nullptr, OPT_RESUME},
+      {"collect-metrics", no_argument, nullptr, OPT_COLLECT_METRICS},
+      {"metrics-interval", required_argument, nullptr, OPT_METRICS_INTERVAL},
+      {"metrics-sysfs-root", required_argument, nullptr, OPT_METRICS_SYSFS},
       {"shared-memory-input", required_argument, nullptr, OPT_SHM_INPUT},
       {"device", required_argument, nullptr, OPT_DEVICE},
       {"seed", required_argument, nullptr, OPT_SEED},
@@ -271,6 +276,9 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
       case OPT_VERBOSE_CSV: o->verbose_csv = true; break;
       case OPT_JSON: o->json_file = arg; break;
       case OPT_RESUME: o->resume = true; break;
+      case OPT_COLLECT_METRICS: o->collect_metrics = true; break;
+      case OPT_METRICS_INTERVAL: o->metrics_interval_ms = std::stoull(arg); break;
+      case OPT_METRICS_SYSFS: o->metrics_sysfs_root = arg; break;
       case OPT_SHM_INPUT: {
         auto p = arg.find('=');
         if (p == std::string::npos) return Error("--shared-memory-input expects NAME=REGION");

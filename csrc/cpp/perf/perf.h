@@ -93,6 +93,9 @@ struct Options {
   uint64_t warmup_requests = 0;
   std::string csv_file;
   std::string json_file;
+  bool collect_metrics = false;     // --collect-metrics: GPU busy %, power, VRAM (amdgpu sysfs)
+  uint64_t metrics_interval_ms = 1000;
+  std::string metrics_sysfs_root;   // default /sys/class/drm (tests point it at a fake tree)
   bool resume = false;  // --resume: continue a sweep checkpointed in json_file
   bool verbose_csv = false;
   bool collect_server_stats = true;
@@ -114,6 +117,28 @@ struct ModelInfo {
   int max_batch_size = 0;
   bool sequential = false;
   bool decoupled = false;
+};
+
+// GPU metrics sampler (metrics.cc): amdgpu sysfs counters of GPU `device`.
+class GpuMetrics {
+ public:
+  GpuMetrics(int device, uint64_t interval_ms, const std::string& sysfs_root);
+  ~GpuMetrics();
+  bool Available() const;
+  void Start();
+  void Stop();
+  /// Averages over the samples since Start (false if none).
+  bool Summary(double* util_pct, double* power_w, double* mem_mib) const;
+
+ private:
+  std::string dev_, power_file_;
+  uint64_t interval_ms_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::thread th_;
+  bool running_ = false, stop_ = false;
+  uint64_t samples_ = 0, mem_max_ = 0;
+  double busy_sum_ = 0, power_sum_ = 0;
 };
 
 struct ServerStats {
@@ -279,11 +304,16 @@ struct PointResult {
   uint64_t errors = 0;
   ServerStats server;  // delta over the windows
   bool has_server = false;
+  bool has_gpu = false;  // --collect-metrics
+  double gpu_util_pct = 0, gpu_power_w = 0, gpu_mem_mib = 0;
 };
 
 class Profiler {
  public:
-  Profiler(const Options& o, Backend* be, LoadEngine* eng) : o_(o), be_(be), eng_(eng) {}
+  Profiler(const Options& o, Backend* be, LoadEngine* eng) : o_(o), be_(be), eng_(eng)
+  {
+    if (o.collect_metrics) gpu_.reset(new GpuMetrics(o.device, o.metrics_interval_ms, o.metrics_sysfs_root));
+  }
   Error Profile(double load, PointResult* out);
 
  private:
@@ -292,6 +322,7 @@ class Profiler {
   Backend* be_;
   LoadEngine* eng_;
   size_t rec_index_ = 0;
+  std::unique_ptr<GpuMetrics> gpu_;
 };
 
 void PrintSettings(const Options& o, const ModelInfo& info, const std::string& data_desc);

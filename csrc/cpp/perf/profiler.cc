@@ -149,6 +149,7 @@ Error Profiler::Profile(double load, PointResult* out)
     while (eng_->CompletedCount() - c0 < o_.warmup_requests && eng_->FirstError().empty()) SleepMs(1);
   }
   rec_index_ = eng_->CompletedCount();
+  if (gpu_) gpu_->Start();  // samples over this point's windows
   std::vector<PointResult> wins;
   std::vector<std::vector<uint64_t>> lats;
   for (int trial = 0; trial < o_.max_trials; ++trial) {
@@ -201,6 +202,10 @@ Error Profiler::Profile(double load, PointResult* out)
   }
   out->throughput = out->window_s > 0 ? out->request_count * static_cast<double>(o_.batch) / out->window_s : 0;
   FillLatency(out, all);
+  if (gpu_) {
+    gpu_->Stop();
+    out->has_gpu = gpu_->Summary(&out->gpu_util_pct, &out->gpu_power_w, &out->gpu_mem_mib);
+  }
   return Error::Success;
 }
 
@@ -274,6 +279,9 @@ void PrintPoint(const Options& o, const PointResult& p)
   if (!p.stable) printf("  [WARNING] measurement did not stabilise within %d windows\n", o.max_trials);
   printf("\n");
   fflush(stdout);
+  if (p.has_gpu)
+    printf("    GPU: utilization %.1f%%, power %.1f W, max memory used %.0f MiB\n", p.gpu_util_pct, p.gpu_power_w,
+           p.gpu_mem_mib);
 }
 
 void PrintSummary(const Options& o, const std::vector<PointResult>& pts)
@@ -294,6 +302,7 @@ Error WriteCsv(const Options& o, const std::vector<PointResult>& pts)
     << ",Inferences/Second,Client Send,Network+Server Send/Recv,Server Queue,Server Compute Input,"
        "Server Compute Infer,Server Compute Output,Client Recv,p50 latency,p90 latency,p95 latency,p99 latency,"
        "Avg latency,request/response,response wait";
+  if (o.collect_metrics) f << ",Avg GPU Utilization,Avg GPU Power Usage,Max GPU Memory Usage";
   if (o.verbose_csv) f << ",Failed requests,Stable";
   f << "\n";
   for (const auto& p : pts) {
@@ -307,6 +316,12 @@ Error WriteCsv(const Options& o, const std::vector<PointResult>& pts)
              p.load, p.throughput, p.client_send_us, net, q, ci, cf, co, p.client_recv_us, p.p50_us, p.p90_us,
              p.p95_us, p.p99_us, p.avg_us, p.client_send_us, p.client_recv_us);
     f << line;
+    if (o.collect_metrics) {
+      // perf_analyzer's units: utilization as a fraction, power in W, memory in bytes
+      char g[160];
+      snprintf(g, sizeof(g), ",%.4f,%.1f,%.0f", p.gpu_util_pct / 100.0, p.gpu_power_w, p.gpu_mem_mib * 1048576.0);
+      f << g;
+    }
     if (o.verbose_csv) f << "," << p.errors << "," << (p.stable ? 1 : 0);
     f << "\n";
   }
@@ -337,7 +352,15 @@ Error WriteJson(const Options& o, const std::vector<PointResult>& pts, const std
              static_cast<unsigned long>(s.execution_count), static_cast<unsigned long>(s.success_count),
              static_cast<unsigned long>(s.queue_ns), static_cast<unsigned long>(s.compute_input_ns),
              static_cast<unsigned long>(s.compute_infer_ns), static_cast<unsigned long>(s.compute_output_ns));
-    f << buf;
+    std::string pt(buf);
+    if (p.has_gpu) {
+      char g[200];
+      snprintf(g, sizeof(g), ",\"gpu\":{\"util_pct\":%.2f,\"power_w\":%.2f,\"mem_mib\":%.1f}}", p.gpu_util_pct,
+               p.gpu_power_w, p.gpu_mem_mib);
+      pt.pop_back();  // reopen the point object
+      pt += g;
+    }
+    f << pt;
   }
   f << "]}\n";
   return Error::Success;
@@ -395,6 +418,12 @@ Error LoadCheckpoint(const Options& o, std::vector<PointResult>* pts)
       p.server.compute_input_ns = static_cast<uint64_t>(num(*sv, "compute_input_ns"));
       p.server.compute_infer_ns = static_cast<uint64_t>(num(*sv, "compute_infer_ns"));
       p.server.compute_output_ns = static_cast<uint64_t>(num(*sv, "compute_output_ns"));
+    }
+    if (const js::Value* g = e.Find("gpu")) {
+      p.has_gpu = true;
+      p.gpu_util_pct = num(*g, "util_pct");
+      p.gpu_power_w = num(*g, "power_w");
+      p.gpu_mem_mib = num(*g, "mem_mib");
     }
     pts->push_back(p);
   }

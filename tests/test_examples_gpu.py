@@ -3,6 +3,7 @@ classification (image_client / grpc_image_client / ensemble_image_client)
 against the GPU server."""
 
 import os
+import subprocess
 
 import numpy as np
 import pytest
@@ -85,3 +86,25 @@ def test_cpp_ensemble_image_client(gpu_server, image_dir, proto):
     r = run_bin("ensemble_image_client", url, ["-c", "2", "-i", proto, os.path.join(image_dir, "img1.ppm")],
                 timeout=300)
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]
+
+
+@pytest.mark.gpu
+def test_perf_analyzer_hip_shm_with_gpu_metrics(gpu_server, tmp_path):
+    """Native perf_analyzer against densenet_onnx over HIP shm with the real
+    amdgpu sysfs metrics of GPU 0 (--collect-metrics)."""
+    import json
+
+    from triton_client_amd.perf import native
+
+    j = tmp_path / "pa.json"
+    r = subprocess.run([native.BIN_PATH, "-m", "densenet_onnx", "-b", "8", "-i", "grpc", "-u", gpu_server.grpc_url,
+                        "--shared-memory", "hip", "--output-shared-memory-size", str(8 * 1000 * 4),
+                        "--concurrency-range", "8", "-p", "500", "-r", "4", "--collect-metrics",
+                        "--metrics-interval", "50", "--json-report", str(j)],
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    pt = json.load(open(j))["points"][0]
+    assert pt["throughput"] > 0 and pt["errors"] == 0
+    print("densenet bs8 c8:", pt["throughput"], "infer/s", pt.get("gpu"))
+    assert "gpu" in pt, r.stdout[-1500:]
+    assert pt["gpu"]["util_pct"] > 0 and pt["gpu"]["mem_mib"] > 100

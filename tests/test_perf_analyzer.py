@@ -91,6 +91,35 @@ def test_roctx_ranges_enabled_without_profiler(cpu_server):
     assert "Request concurrency: 1" in r.stdout
 
 
+def _fake_amdgpu(root, busy, watts, vram):
+    dev = root / "card{}".format(len(list(root.iterdir()))) / "device"
+    (dev / "hwmon" / "hwmon7").mkdir(parents=True)
+    (dev / "vendor").write_text("0x1002\n")
+    (dev / "gpu_busy_percent").write_text("%d\n" % busy)
+    (dev / "mem_info_vram_used").write_text("%d\n" % vram)
+    (dev / "hwmon" / "hwmon7" / "power1_average").write_text("%d\n" % (watts * 1000000))
+
+
+def test_collect_metrics_from_amdgpu_sysfs(cpu_server, tmp_path):
+    """--collect-metrics samples the amdgpu sysfs counters of --device (a fake
+    tree here; /sys/class/drm on the GPU box) into stdout, CSV and JSON."""
+    root = tmp_path / "drm"
+    root.mkdir()
+    _fake_amdgpu(root, 10, 200, 1 << 30)
+    _fake_amdgpu(root, 73, 615, 3 << 30)
+    (root / "card1-DP-1").mkdir()  # connectors are skipped
+    f, j = tmp_path / "m.csv", tmp_path / "m.json"
+    r = _pa(["-m", "simple", "-i", "grpc", "-u", cpu_server.grpc_url, "-p", "200", "-r", "3", "--collect-metrics",
+             "--metrics-interval", "20", "--metrics-sysfs-root", root, "--device", "1", "-f", f, "--json-report", j])
+    assert r.returncode == 0, r.stderr
+    assert "GPU: utilization 73.0%, power 615.0 W, max memory used 3072 MiB" in r.stdout
+    row = next(csv.DictReader(open(f)))
+    assert float(row["Avg GPU Utilization"]) == pytest.approx(0.73)
+    assert float(row["Avg GPU Power Usage"]) == pytest.approx(615.0)
+    assert float(row["Max GPU Memory Usage"]) == 3 << 30
+    assert json.load(open(j))["points"][0]["gpu"] == {"util_pct": 73.0, "power_w": 615.0, "mem_mib": 3072.0}
+
+
 def test_system_shm_sync_count_windows(cpu_server):
     r = _pa(["-m", "simple", "-u", cpu_server.http_url, "--sync", "--shared-memory", "system",
              "--measurement-mode", "count_windows", "--measurement-request-count", "60",
