@@ -54,8 +54,13 @@ __device__ __forceinline__ void unpack8(v4u v, float* f) {
   }
 }
 
+// two fp32 -> packed bf16 (RNE) in ONE instruction: gfx950's v_cvt_pk_bf16_f32
+// (the software RNE costs ~6 VALU per element; this runs in every prologue
+// and epilogue of the engine)
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return (uint32_t)tcamd::f32_to_bf16_rne(a) | ((uint32_t)tcamd::f32_to_bf16_rne(b) << 16);
+  const bf16x2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 __device__ __forceinline__ v4u pack8(const float* f) {
@@ -173,8 +178,6 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
         v4u v;
         if constexpr (PRO) {
           float o[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = 0.f;
           if (kin) {
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
@@ -183,9 +186,14 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
 #pragma unroll
               for (int e = 0; e < 8; ++e) {
                 const float t = fmaxf(f[e] * sS[k0 + kc + e] + sT[k0 + kc + e], 0.f);
-                o[e] += POOL ? 0.25f * t : t;
+                // (no "0 + t" for the plain prologue: IEEE forbids folding it away)
+                if constexpr (POOL) o[e] = s ? o[e] + 0.25f * t : 0.25f * t;
+                else o[e] = t;
               }
             }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = 0.f;
           }
           v = pack8(o);
         } else {
@@ -906,13 +914,18 @@ __device__ __forceinline__ void stage_weights(const uint16_t* __restrict__ w, ui
 
 constexpr int kActStride = kC3 + 8;  // 272-B rows
 constexpr int kTileP = 128;          // output pixels per tile (4 waves x 32)
+// An all-zero activation row after the largest band: out-of-image taps read
+// it (one address select per tap) instead of masking every fragment (four
+// v_cndmask per MFMA).
+constexpr int kZeroRow = kTileP + 2 * 57;
 
 __global__ void __launch_bounds__(256) conv3x3_lds_kernel(Conv3x3Params p) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Ws = smem;                   // [32][kWsK]
-  uint16_t* As = smem + kN3 * kWsK;      // [rows][kActStride]
+  uint16_t* As = smem + kN3 * kWsK;      // [rows][kActStride], row kZeroRow = 0
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   stage_weights(p.w, Ws, tid);
+  if (tid < kActStride / 8) *reinterpret_cast<v4u*>(&As[kZeroRow * kActStride + tid * 8]) = v4u{0, 0, 0, 0};
   const int W = p.W, HW = p.H * p.W;
   const int halo = W + 1, rows = kTileP + 2 * halo, chunks = rows * 16;
   constexpr int kMaxChunks = (kTileP + 2 * 57) * 16;       // W <= 56
@@ -954,16 +967,16 @@ __global__ void __launch_bounds__(256) conv3x3_lds_kernel(Conv3x3Params p) {
     f32x16 acc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    const bool up = h > 0, down = h + 1 < p.H, left = w > 0, right = w + 1 < W, in = m < p.M;
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
       const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-      const bool ok = m < p.M && h + dy >= 0 && h + dy < p.H && w + dx >= 0 && w + dx < W;
-      const uint16_t* arow = &As[(tp + halo + dy * W + dx) * kActStride + kh];
+      const bool ok = in && (dy < 0 ? up : dy > 0 ? down : true) && (dx < 0 ? left : dx > 0 ? right : true);
+      const uint16_t* arow = &As[(ok ? tp + halo + dy * W + dx : kZeroRow) * kActStride + kh];
       const uint16_t* wrow = &Ws[col * kWsK + tap * kC3 + kh];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        v4u b = *reinterpret_cast<const v4u*>(arow + c * 16);
-        if (!ok) b = v4u{0, 0, 0, 0};
+        const v4u b = *reinterpret_cast<const v4u*>(arow + c * 16);
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(wrow + c * 16);
         acc = mfma32(a, as_frag(b), acc);
       }
@@ -991,9 +1004,11 @@ constexpr int kRedFloats = 4 * 3 * 64 * 16;  // [subtile][3 other waves][lane][1
 
 __global__ void __launch_bounds__(256, 2) conv3x3_kr_kernel(Conv3x3Params p) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* As = smem;                                  // [rows][kActStride] bf16
-  float* red = reinterpret_cast<float*>(smem);          // aliases As after the taps
+  uint16_t* As = smem;                                  // [rows][kActStride] bf16, row kZeroRow = 0
+  float* red = reinterpret_cast<float*>(smem);          // aliases As after the taps (below kZeroRow)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  static_assert(kRedFloats * 4 <= kZeroRow * kActStride * 2, "reduction scratch must not reach the zero row");
+  if (tid < kActStride / 8) *reinterpret_cast<v4u*>(&As[kZeroRow * kActStride + tid * 8]) = v4u{0, 0, 0, 0};
   const int col = lane & 31, kh = 8 * (lane >> 5);
   v4u wr[18];
 #pragma unroll
@@ -1029,15 +1044,17 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kr_kernel(Conv3x3Params p) {
       if (c < chunks) *reinterpret_cast<v4u*>(&As[(c >> 4) * kActStride + (c & 15) * 8]) = st[i];
     }
     __syncthreads();
-    int ph[4], pw[4];
-    bool pv[4];
+    bool pv[4], up[4], down[4], left[4], right[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = tile * kTileP + i * 32 + col;
       pv[i] = m < p.M;
       const int r = (pv[i] ? m : 0) % HW;
-      ph[i] = r / W;
-      pw[i] = r - ph[i] * W;
+      const int ph = r / W, pw = r - ph * W;
+      up[i] = ph > 0;
+      down[i] = ph + 1 < p.H;
+      left[i] = pw > 0;
+      right[i] = pw + 1 < W;
     }
     f32x16 acc[4];
 #pragma unroll
@@ -1049,12 +1066,12 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kr_kernel(Conv3x3Params p) {
       const int dy = t / 3 - 1, dx = t % 3 - 1;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const bool ok = pv[i] && ph[i] + dy >= 0 && ph[i] + dy < p.H && pw[i] + dx >= 0 && pw[i] + dx < W;
-        const uint16_t* arow = &As[(i * 32 + col + halo + dy * W + dx) * kActStride + 32 * wave + kh];
+        const bool ok = pv[i] && (dy < 0 ? up[i] : dy > 0 ? down[i] : true) &&
+                        (dx < 0 ? left[i] : dx > 0 ? right[i] : true);
+        const uint16_t* arow = &As[(ok ? i * 32 + col + halo + dy * W + dx : kZeroRow) * kActStride + 32 * wave + kh];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          v4u b = *reinterpret_cast<const v4u*>(arow + 16 * h);
-          if (!ok) b = v4u{0, 0, 0, 0};
+          const v4u b = *reinterpret_cast<const v4u*>(arow + 16 * h);
           acc[i] = mfma32(as_frag(wr[t * 2 + h]), as_frag(b), acc[i]);
         }
       }
@@ -1516,10 +1533,9 @@ int launch_3x3_m32(Conv3x3Params p, hipStream_t s) {
 
 int launch_3x3_kr(Conv3x3Params p, hipStream_t s) {
   if (p.W > 56) return hipErrorInvalidValue;
-  const int act = (kTileP + 2 * (p.W + 1)) * kActStride * 2;
-  const int lds = std::max(act, kRedFloats * 4);
+  const int lds = (kZeroRow + 1) * kActStride * 2;  // band + zero row (the reduction aliases the band)
   static int attr = 0;
-  const int lmax = std::max((kTileP + 2 * 57) * kActStride * 2, kRedFloats * 4);
+  const int lmax = lds;
   if (attr < lmax) {
     int rc = hipFuncSetAttribute((const void*)conv3x3_kr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lmax);
     if (rc != hipSuccess) return rc;
@@ -1533,13 +1549,13 @@ int launch_3x3_kr(Conv3x3Params p, hipStream_t s) {
 
 int launch_3x3_lds(Conv3x3Params p, hipStream_t s) {
   if (p.W > 56) return hipErrorInvalidValue;
-  const int lds = (kN3 * kWsK + (kTileP + 2 * (p.W + 1)) * kActStride) * 2;
+  const int lds = (kN3 * kWsK + (kZeroRow + 1) * kActStride) * 2;
   static int attr = 0;
   if (attr < lds) {
     int rc = hipFuncSetAttribute((const void*)conv3x3_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (kN3 * kWsK + (kTileP + 2 * 57) * kActStride) * 2);
+                                 (kN3 * kWsK + (kZeroRow + 1) * kActStride) * 2);
     if (rc != hipSuccess) return rc;
-    attr = (kN3 * kWsK + (kTileP + 2 * 57) * kActStride) * 2;
+    attr = (kN3 * kWsK + (kZeroRow + 1) * kActStride) * 2;
   }
   p.tiles = (p.M + kTileP - 1) / kTileP;
   const int grid = p.tiles < 256 ? p.tiles : 256;  // one resident block per CU (LDS-limited)
