@@ -63,6 +63,15 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
+// ReLU on two packed bf16 values as ONE v_pk_max_i16: a bf16 with the sign
+// bit set is a negative int16, so max(x, 0) in int16 zeroes exactly the
+// negative (and -0 / negative-NaN) halves.  relu(bf16(x)) == bf16(relu(x)).
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t relu_pk(uint32_t v) {
+  const s16x2 z = {0, 0};
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, v), z));
+}
+
 __device__ __forceinline__ v4u pack8(const float* f) {
   v4u v;
 #pragma unroll
@@ -185,9 +194,10 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
               unpack8(ra[i][s], f);
 #pragma unroll
               for (int e = 0; e < 8; ++e) {
-                const float t = fmaxf(f[e] * sS[k0 + kc + e] + sT[k0 + kc + e], 0.f);
-                // (no "0 + t" for the plain prologue: IEEE forbids folding it away)
-                if constexpr (POOL) o[e] = s ? o[e] + 0.25f * t : 0.25f * t;
+                const float t = f[e] * sS[k0 + kc + e] + sT[k0 + kc + e];
+                // pool: average of ReLUs (fp32); plain: ReLU after the pack, packed
+                // (no "0 + t" either: IEEE forbids folding it away)
+                if constexpr (POOL) o[e] = s ? o[e] + 0.25f * fmaxf(t, 0.f) : 0.25f * fmaxf(t, 0.f);
                 else o[e] = t;
               }
             }
@@ -196,6 +206,10 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
             for (int e = 0; e < 8; ++e) o[e] = 0.f;
           }
           v = pack8(o);
+          if constexpr (!POOL) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = relu_pk(v[q]);
+          }
         } else {
           v = ra[i][0];
         }
@@ -210,11 +224,18 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
     }
   };
 
+  // the output bias starts the accumulators (split-K adds it in the reduce)
   f32x4 acc[NJ][TM];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j)
+  for (int j = 0; j < NJ; ++j) {
+    f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (p.out_bias && !p.ws) {
+      const int nb = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
+      b0 = f32x4{p.out_bias[nb], p.out_bias[nb + 1], p.out_bias[nb + 2], p.out_bias[nb + 3]};
+    }
 #pragma unroll
-    for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < TM; ++i) acc[j][i] = b0;
+  }
 
   // K tiles of this block: all of K, or one split's range
   const int kt0 = p.ws ? (int)blockIdx.z * (p.k_per_split / BK) : 0;
@@ -258,26 +279,17 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
     }
     return;
   }
-  // epilogue: lane holds out channels nb..nb+3 of pixel m
+  // epilogue: lane holds out channels nb..nb+3 of pixel m (bias already in acc)
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int nb = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-    float bias[4] = {0.f, 0.f, 0.f, 0.f};
-    if (p.out_bias) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bias[r] = p.out_bias[nb + r];
-    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + wm * 16 * TM + i * 16 + fr;
       if (m < p.M) {
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = acc[j][i][r] + bias[r];
-          if (p.relu_out) v[r] = fmaxf(v[r], 0.f);
-        }
-        *reinterpret_cast<v2u*>(p.y + (size_t)m * p.ldy + nb) = v2u{pack2(v[0], v[1]), pack2(v[2], v[3])};
+        v2u o = v2u{pack2(acc[j][i][0], acc[j][i][1]), pack2(acc[j][i][2], acc[j][i][3])};
+        if (p.relu_out) o = v2u{relu_pk(o[0]), relu_pk(o[1])};
+        *reinterpret_cast<v2u*>(p.y + (size_t)m * p.ldy + nb) = o;
       }
     }
   }
