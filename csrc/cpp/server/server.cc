@@ -124,6 +124,8 @@ struct NativeModel {
   int max_batch = 0;
   uint64_t delay_ns = 0;
   std::vector<int> preferred;  // ascending; dynamic_batching.preferred_batch_size
+  bool idle_dispatch = true;   // no queue delay while every instance is idle
+  int busy = 0;                // instances executing a batch (under mu)
   int instances = 1;
   std::vector<TensorDef> inputs, outputs;
   tcserve_exec_fn fn = nullptr;
@@ -1087,10 +1089,14 @@ void Server::Worker(std::shared_ptr<NativeModel> m, int instance)
       // size dispatches at once; otherwise wait up to the queue delay for a
       // full batch.  Whatever is queued then goes out, capped at the largest
       // preferred size that fits (so pipelined instances keep alternating).
+      // Idle-aware: the delay only buys batching while another instance
+      // keeps the GPU busy; with every instance idle the queue goes out now
+      // (a lone request never waits out the delay on an idle GPU).
       const int pref_max = m->preferred.empty() ? cap : std::min(cap, m->preferred.back());
       if (m->max_batch > 0 && m->delay_ns > 0) {
         const uint64_t deadline = m->q.front()->t_arrive + m->delay_ns;
         while (!m->stopping && m->q_rows < pref_max) {
+          if (m->idle_dispatch && m->busy == 0) break;
           const uint64_t now = NowNs();
           if (now >= deadline) break;
           m->cv.wait_for(lk, std::chrono::nanoseconds(deadline - now));
@@ -1113,8 +1119,14 @@ void Server::Worker(std::shared_ptr<NativeModel> m, int instance)
         m->q.pop_front();
       }
       if (!m->q.empty()) m->cv.notify_one();
+      m->busy++;
     }
     Execute(m.get(), instance, batch);
+    {
+      std::lock_guard<std::mutex> lk(m->mu);
+      m->busy--;
+    }
+    m->cv.notify_all();  // a worker holding a partial batch may dispatch now
   }
 }
 
@@ -1354,6 +1366,21 @@ int32_t tcserve_add_model(void* server, const char* name, const char* version, i
 }
 
 int32_t tcserve_remove_model(void* server, const char* name) { return static_cast<Server*>(server)->RemoveModel(name); }
+
+int32_t tcserve_set_idle_dispatch(void* server, const char* name, int32_t on)
+{
+  Server* s = static_cast<Server*>(server);
+  std::shared_ptr<NativeModel> m;
+  {
+    std::lock_guard<std::mutex> lk(s->models_mu);
+    auto it = s->models.find(name);
+    if (it == s->models.end()) return 1;
+    m = it->second;
+  }
+  std::lock_guard<std::mutex> lk(m->mu);
+  m->idle_dispatch = on != 0;
+  return 0;
+}
 
 int32_t tcserve_set_preferred(void* server, const char* name, const int32_t* sizes, int32_t n)
 {

@@ -56,6 +56,8 @@ int32_t tcserve_add_model(void* server, const char* name, const char* version, i
                           const char** out_names, const char** out_dtypes, const int32_t* out_ndims,
                           const int64_t* out_dims, tcserve_exec_fn fn, void* user, char* err, int32_t errlen);
 int32_t tcserve_remove_model(void* server, const char* name);
+/// Idle-aware batching (default on): skip the queue delay while no instance is executing.
+int32_t tcserve_set_idle_dispatch(void* server, const char* name, int32_t on);
 /// dynamic_batching.preferred_batch_size for a registered model (n = 0 clears).
 int32_t tcserve_set_preferred(void* server, const char* name, const int32_t* sizes, int32_t n);
 /// Mirror of the Python shared-memory registries; kind 0 = system (ptr = host mapping), 1 = device.

@@ -104,6 +104,19 @@ def test_preferred_batch_size_caps_batches(cpu_server):
     assert new.get(2, 0) > 0, new
     with pytest.raises(KeyError):
         nf.set_preferred("no_such_model", [2])
+    with pytest.raises(KeyError):
+        nf.set_idle_dispatch("no_such_model", False)
+
+
+def test_idle_dispatch_toggle_keeps_results(cpu_server):
+    """Idle-aware dispatch on/off only changes when batches go out, never results."""
+    nf = cpu_server.server.native_frontend
+    c = grpcclient.InferenceServerClient(cpu_server.grpc_url)
+    for on in (False, True):
+        nf.set_idle_dispatch("add_sub_batched", on)
+        a = np.arange(16, dtype=np.int32).reshape(1, 16)
+        r = c.infer("add_sub_batched", _inputs(a, a))
+        np.testing.assert_array_equal(r.as_numpy("OUTPUT0"), 2 * a)
 
 
 def test_fast_path_system_shm(cpu_server):

@@ -21,6 +21,8 @@ def main(argv=None):
     ap.add_argument("--models", default="", help="comma-separated subset of models to load")
     ap.add_argument("--instance-count", type=int, default=0, help="override GPU model instance count")
     ap.add_argument("--max-queue-delay-us", type=int, default=-1)
+    ap.add_argument("--idle-dispatch", default="on", choices=["on", "off"],
+                    help="dispatch queued requests at once while every model instance is idle (else wait the delay)")
     ap.add_argument("--preferred-batch-sizes", default="",
                     help="override dynamic_batching.preferred_batch_size of the GPU models (comma-separated)")
     ap.add_argument("--no-graphs", action="store_true", help="disable HIP graph capture")
@@ -51,6 +53,8 @@ def main(argv=None):
                 m.instance_count = args.instance_count
             if args.max_queue_delay_us >= 0 and m.dynamic_batching is not None:
                 m.dynamic_batching = dict(m.dynamic_batching, max_queue_delay_us=args.max_queue_delay_us)
+            if m.dynamic_batching is not None:
+                m.dynamic_batching = dict(m.dynamic_batching, idle_dispatch=args.idle_dispatch == "on")
             if args.preferred_batch_sizes and m.dynamic_batching is not None:
                 pref = sorted(int(x) for x in args.preferred_batch_sizes.split(",") if x)
                 m.dynamic_batching = dict(m.dynamic_batching, preferred=pref)

@@ -895,6 +895,9 @@ class DynamicBatcher(DirectScheduler):
         self.max_bs = inst.max_batch_size
         self.preferred = sorted(cfg.get("preferred", []))
         self.delay_s = cfg.get("max_queue_delay_us", 0) / 1e6
+        # idle-aware: wait for more rows only while another batch keeps the device busy
+        self.idle_dispatch = bool(cfg.get("idle_dispatch", True))
+        self.busy = 0
         self.queue = None
         self.tasks = []
         self.closed = False
@@ -917,6 +920,8 @@ class DynamicBatcher(DirectScheduler):
             while rows < self.max_bs:
                 if self.preferred and rows in self.preferred and self.queue.empty():
                     break
+                if self.idle_dispatch and self.busy == 0 and self.queue.empty():
+                    break
                 try:
                     if self.queue.empty():
                         timeout = deadline - loop.time()
@@ -935,10 +940,13 @@ class DynamicBatcher(DirectScheduler):
                 rows += n
             reqs = [b[0] for b in batch]
             t_enq = min(b[1] for b in batch)
+            self.busy += 1
             try:
                 results, _ = await loop.run_in_executor(self.server.executor, self._run, reqs, t_enq)
             except Exception as e:  # noqa: BLE001
                 results = [e] * len(reqs)
+            finally:
+                self.busy -= 1
             now = _now_ns()
             for (req, t_in, fut), res in zip(batch, results):
                 ok = not isinstance(res, Exception)

@@ -61,6 +61,8 @@ def _load():
             ctypes.POINTER(ctypes.c_int64),
             EXEC_FN, ctypes.c_void_p, cp, ctypes.c_int32]
         lib.tcserve_add_model.restype = ctypes.c_int32
+        lib.tcserve_set_idle_dispatch.argtypes = [ctypes.c_void_p, cp, ctypes.c_int32]
+        lib.tcserve_set_idle_dispatch.restype = ctypes.c_int32
         lib.tcserve_set_preferred.argtypes = [ctypes.c_void_p, cp, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]
         lib.tcserve_set_preferred.restype = ctypes.c_int32
         lib.tcserve_remove_model.argtypes = [ctypes.c_void_p, cp]
@@ -180,9 +182,15 @@ class NativeFrontend:
         pref = [int(x) for x in (inst.dynamic_batching or {}).get("preferred", [])]
         if pref:
             self.set_preferred(name, pref)
+        self.set_idle_dispatch(name, bool((inst.dynamic_batching or {}).get("idle_dispatch", True)))
         with self._lock:
             self._cbs[name] = cb
             self._versions[name] = str(inst.version)
+
+    def set_idle_dispatch(self, name, on):
+        """Skip the queue delay while every instance of the model is idle."""
+        if _load().tcserve_set_idle_dispatch(self._h, name.encode(), int(bool(on))) != 0:
+            raise KeyError(name)
 
     def set_preferred(self, name, sizes):
         """dynamic_batching.preferred_batch_size of a registered model ([] clears)."""
