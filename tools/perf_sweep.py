@@ -54,14 +54,14 @@ def main():
     log = os.path.join(REPO, "gpurun_out", "sweep_server.log")
     os.makedirs(os.path.dirname(log), exist_ok=True)
     srv = ServerProcess(device=0, models="densenet_onnx,bert_large", log_path=log,
-                        extra_args=["--instance-count", "2", "--max-queue-delay-us", "500"])
+                        extra_args=["--instance-count", "3", "--max-queue-delay-us", "500"])
     rows = []
     try:
         srv.wait_ready(timeout=1200, model="densenet_onnx")
         srv.wait_ready(timeout=1200, model="bert_large")
         print("server ready", flush=True)
         modes = [("grpc", "none"), ("http", "none"), ("grpc", "system"), ("grpc", "hip")]
-        concs = {1: [1, 16, 64], 8: [1, 16]} if not a.quick else {1: [16], 8: [16]}
+        concs = {1: [1, 16, 64], 8: [1, 16, 48]} if not a.quick else {1: [16], 8: [16]}
         for bs in (1, 8):
             for proto, shm in modes:
                 for conc in concs[bs]:
@@ -83,7 +83,8 @@ def main():
     with open(a.out, "w") as f:
         f.write("# perf_analyzer sweep on 1x MI355X (measured)\n\n")
         f.write("git %s; server: `python -m triton_client_amd.server --gpu --models densenet_onnx,bert_large "
-                "--instance-count 2 --max-queue-delay-us 500` (tcserve native gRPC front end, aiohttp HTTP); "
+                "--instance-count 3 --max-queue-delay-us 500` (idle-aware dynamic batching; tcserve native gRPC front end, "
+                "aiohttp HTTP); "
                 "client: native `perf_analyzer` (csrc/cpp/perf), %d ms windows, stability on p99; synthetic data, "
                 "random-init weights, bf16 compute.\n\n" % (sha, a.interval_ms))
         f.write("| model | bs | protocol | tensors | concurrency | infer/s | p50 us | p99 us | stable |\n")
