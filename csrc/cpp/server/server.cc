@@ -29,6 +29,7 @@
 
 #include "grpc_service.pb.h"
 #include "h2.h"
+#include "json.h"
 #include "net.h"
 #include "tcserve.h"
 #include "trace.h"
@@ -76,7 +77,14 @@ struct Conn {
   uint64_t id = 0;
   int fd = -1;
   Loop* loop = nullptr;
-  nghttp2_session* s = nullptr;
+  nghttp2_session* s = nullptr;  // gRPC (h2c) connections
+  // HTTP/1.1 (KServe REST) connections: requests parsed from `hin`, answered
+  // strictly in request order (pipelining) through `ready`
+  bool http1 = false;
+  std::string hin;
+  uint64_t req_seq = 0, resp_seq = 0;
+  std::map<uint64_t, std::string> ready;
+  bool close_after = false;
   std::unordered_map<int32_t, std::unique_ptr<Stream>> streams;
   std::string sendbuf;
   size_t sendpos = 0;
@@ -97,6 +105,9 @@ struct PendingReq {
   uint64_t conn_id;
   Loop* loop;
   int32_t stream_id;
+  bool http = false;      // KServe REST request: reply as JSON header + binary outputs
+  uint64_t http_seq = 0;  // position in its connection's request order
+  bool http_close = false;
   std::string id;
   int32_t rows;
   std::vector<tcserve_ref> in;    // [n_inputs]
@@ -165,7 +176,8 @@ class Loop {
   bool Start(std::string* err);
   void Stop();
   void Post(std::function<void()> fn);
-  void AddConn(int fd);
+  void AddConn(int fd, bool http1 = false);
+  void AddListener(int fd, uint64_t tag);
   Conn* Find(uint64_t id)
   {
     auto it = conns_.find(id);
@@ -175,12 +187,13 @@ class Loop {
   void Close(Conn* c);
   int idx() const { return idx_; }
   Server* srv() { return srv_; }
-  int listen_fd = -1;  // only loop 0 accepts
+  int listen_fd = -1;       // only loop 0 accepts (gRPC)
+  int http_listen_fd = -1;  // loop 0, KServe REST (tcserve_listen_http)
 
  private:
   void Run();
   void OnReadable(Conn* c);
-  void DoAccept();
+  void DoAccept(bool http);
   Server* srv_;
   int idx_;
   int ep_ = -1, ev_ = -1;
@@ -199,6 +212,7 @@ class Server {
   int port() const { return port_; }
 
   // transport hooks (loop thread)
+  void OnHttpData(Conn* c);
   void OnRequestComplete(Conn* c, Stream* st);
   void OnStreamMessage(Conn* c, Stream* st, std::string&& msg);
   void OnStreamEnd(Conn* c, Stream* st);
@@ -208,6 +222,9 @@ class Server {
   void Reply(Conn* c, Stream* st, std::string* msg, int status, const std::string& message);
   void PostReply(Loop* loop, uint64_t conn_id, int32_t stream_id, std::string&& msg, int status,
                  const std::string& message);
+  void PostHttp(Loop* loop, uint64_t conn_id, uint64_t seq, std::string&& bytes, bool close);
+  bool ListenHttp(const std::string& host, int port, const std::string& up_host, int up_port, std::string* err);
+  int http_port() const { return http_port_; }
 
   // native models / shm mirror
   int AddModel(std::unique_ptr<NativeModel> m, std::string* err);
@@ -225,14 +242,20 @@ class Server {
 
  private:
   bool TryNative(Conn* c, Stream* st, const char* msg, size_t len, std::string* owner);
+  bool TryNativeHttp(Conn* c, uint64_t seq, bool close, const std::string& name, const std::string& version,
+                     std::string* body, size_t json_len);
+  void ProxyHttp(Conn* c, uint64_t seq, bool close, std::string&& raw);
+  void FailPending(PendingReq* pr, int grpc_status, int http_status, const std::string& msg);
   void Proxy(Conn* c, Stream* st, bool streaming);
   std::shared_ptr<tc::H2Channel> Upstream();
   void Worker(std::shared_ptr<NativeModel> m, int instance);
   void Execute(NativeModel* m, int instance, std::vector<std::unique_ptr<PendingReq>>& batch);
+  static std::string HttpInferResponse(NativeModel* m, PendingReq* pr);
 
-  int port_ = 0;
-  std::string up_host_;
-  int up_port_ = 0;
+  int port_ = 0, http_port_ = 0;
+  std::string up_host_, up_http_host_;
+  int up_port_ = 0, up_http_port_ = 0;
+  std::atomic<int> proxies_{0};  // in-flight HTTP proxy threads
   std::mutex up_mu_;
   std::vector<std::shared_ptr<tc::H2Channel>> up_;
   std::atomic<uint32_t> up_rr_{0};
@@ -451,12 +474,30 @@ void Loop::Post(std::function<void()> fn)
   (void)!write(ev_, &one, 8);
 }
 
-void Loop::AddConn(int fd)
+void Loop::AddListener(int fd, uint64_t tag)
+{
+  epoll_event e{};
+  e.events = EPOLLIN;
+  e.data.u64 = tag;
+  epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &e);
+}
+
+void Loop::AddConn(int fd, bool http1)
 {
   std::unique_ptr<Conn> c(new Conn());
   c->id = srv_->next_conn_id++;
   c->fd = fd;
   c->loop = this;
+  c->http1 = http1;
+  if (http1) {
+    epoll_event e{};
+    e.events = EPOLLIN;
+    e.data.u64 = c->id + 16;
+    epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &e);
+    conns_[c->id] = std::move(c);
+    srv_->n_conns++;
+    return;
+  }
   nghttp2_session_callbacks* cbs;
   nghttp2_session_callbacks_new(&cbs);
   nghttp2_session_callbacks_set_on_begin_headers_callback(cbs, OnBeginHeaders);
@@ -486,7 +527,7 @@ void Loop::Close(Conn* c)
   epoll_ctl(ep_, EPOLL_CTL_DEL, c->fd, nullptr);
   for (auto& kv : c->streams) srv_->OnStreamClosed(c, kv.second.get());
   c->streams.clear();
-  nghttp2_session_del(c->s);
+  if (c->s) nghttp2_session_del(c->s);
   close(c->fd);
   conns_.erase(c->id);
 }
@@ -494,6 +535,11 @@ void Loop::Close(Conn* c)
 void Loop::Flush(Conn* c)
 {
   while (true) {
+    if (c->sendpos == c->sendbuf.size() && c->http1) {
+      c->sendbuf.clear();
+      c->sendpos = 0;
+      break;
+    }
     if (c->sendpos == c->sendbuf.size()) {
       c->sendbuf.clear();
       c->sendpos = 0;
@@ -526,6 +572,11 @@ void Loop::Flush(Conn* c)
     epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &e);
     c->want_write = pending;
   }
+  if (c->http1) {
+    // Connection: close -> close once every response before it has gone out
+    if (c->closing || (c->close_after && !pending && c->resp_seq == c->req_seq)) Close(c);
+    return;
+  }
   if (c->closing ||
       (!nghttp2_session_want_read(c->s) && !nghttp2_session_want_write(c->s) && !pending)) {
     Close(c);
@@ -537,6 +588,10 @@ void Loop::OnReadable(Conn* c)
   uint8_t buf[65536];
   while (true) {
     ssize_t n = recv(c->fd, buf, sizeof(buf), 0);
+    if (n > 0 && c->http1) {
+      c->hin.append(reinterpret_cast<const char*>(buf), n);
+      continue;
+    }
     if (n > 0) {
       ssize_t r = nghttp2_session_mem_recv(c->s, buf, n);
       if (r < 0) {
@@ -554,6 +609,12 @@ void Loop::OnReadable(Conn* c)
     c->closing = true;
     break;
   }
+  if (c->http1 && !c->hin.empty() && !c->closing) {
+    const uint64_t id = c->id;
+    srv_->OnHttpData(c);
+    c = Find(id);
+    if (!c) return;
+  }
   if (c->closing) {
     Close(c);
     return;
@@ -561,17 +622,17 @@ void Loop::OnReadable(Conn* c)
   Flush(c);
 }
 
-void Loop::DoAccept()
+void Loop::DoAccept(bool http)
 {
   while (true) {
-    int fd = accept4(listen_fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+    int fd = accept4(http ? http_listen_fd : listen_fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
     if (fd < 0) break;
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
     const int li = srv_->next_loop++ % static_cast<int>(srv_->loops.size());
     Loop* l = srv_->loops[li].get();
-    if (l == this) AddConn(fd);
-    else l->Post([l, fd] { l->AddConn(fd); });
+    if (l == this) AddConn(fd, http);
+    else l->Post([l, fd, http] { l->AddConn(fd, http); });
   }
 }
 
@@ -592,8 +653,8 @@ void Loop::Run()
           tasks.swap(tasks_);
         }
         for (auto& t : tasks) t();
-      } else if (tag == 1) {
-        DoAccept();
+      } else if (tag == 1 || tag == 2) {
+        DoAccept(tag == 2);
       } else {
         Conn* c = Find(tag - 16);
         if (!c) continue;
@@ -659,8 +720,10 @@ Server::~Server()
     for (auto& t : m->workers)
       if (t.joinable()) t.join();
   }
+  for (int i = 0; i < 3000 && proxies_.load() > 0; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(1));
   for (auto& l : loops) l->Stop();
   if (!loops.empty() && loops[0]->listen_fd >= 0) close(loops[0]->listen_fd);
+  if (!loops.empty() && loops[0]->http_listen_fd >= 0) close(loops[0]->http_listen_fd);
   loops.clear();
   std::lock_guard<std::mutex> lk(up_mu_);
   up_.clear();
@@ -719,6 +782,544 @@ void Server::PostReply(Loop* loop, uint64_t conn_id, int32_t stream_id, std::str
     Reply(c, it->second.get(), status == kOk ? m.get() : nullptr, status, message);
     loop->Flush(c);
   });
+}
+
+// ---------------------------------------------------------------------------
+// KServe REST (HTTP/1.1) front end: POST /v2/models/<m>[/versions/<v>]/infer
+// for native models with binary-tensor or shared-memory I/O runs on the same
+// batcher as gRPC; every other request is relayed byte-for-byte to the
+// aiohttp server behind it (one upstream connection per relayed request).
+// ---------------------------------------------------------------------------
+namespace {
+
+std::string Lower(std::string v)
+{
+  for (auto& ch : v) ch = static_cast<char>(tolower(static_cast<unsigned char>(ch)));
+  return v;
+}
+
+std::string HttpStatusLine(int code)
+{
+  switch (code) {
+    case 200: return "HTTP/1.1 200 OK\r\n";
+    case 400: return "HTTP/1.1 400 Bad Request\r\n";
+    case 500: return "HTTP/1.1 500 Internal Server Error\r\n";
+    case 502: return "HTTP/1.1 502 Bad Gateway\r\n";
+    case 503: return "HTTP/1.1 503 Service Unavailable\r\n";
+    default: return "HTTP/1.1 " + std::to_string(code) + " Error\r\n";
+  }
+}
+
+std::string HttpError(int code, const std::string& msg, bool close)
+{
+  std::string body = "{\"error\":";
+  tc::json::AppendEscapedString(&body, msg);
+  body += "}";
+  std::string r = HttpStatusLine(code);
+  r += "Content-Type: application/json\r\nContent-Length: " + std::to_string(body.size()) + "\r\n";
+  if (close) r += "Connection: close\r\n";
+  r += "\r\n";
+  return r + body;
+}
+
+struct HttpHead {
+  std::string method, target;
+  std::vector<std::pair<std::string, std::string>> headers;  // lower-case names
+  size_t head_len = 0;
+  const std::string* Get(const char* name) const
+  {
+    for (const auto& kv : headers)
+      if (kv.first == name) return &kv.second;
+    return nullptr;
+  }
+};
+
+// Parse a request head ending at "\r\n\r\n"; 0 = need more, -1 = malformed, 1 = ok.
+int ParseHead(const std::string& in, HttpHead* h)
+{
+  const size_t end = in.find("\r\n\r\n");
+  if (end == std::string::npos) return in.size() > (1u << 20) ? -1 : 0;
+  h->head_len = end + 4;
+  size_t pos = in.find("\r\n");
+  const std::string line = in.substr(0, pos);
+  const size_t sp1 = line.find(' '), sp2 = line.rfind(' ');
+  if (sp1 == std::string::npos || sp2 == sp1) return -1;
+  h->method = line.substr(0, sp1);
+  h->target = line.substr(sp1 + 1, sp2 - sp1 - 1);
+  pos += 2;
+  while (pos < end) {
+    const size_t eol = in.find("\r\n", pos);
+    const std::string l = in.substr(pos, eol - pos);
+    const size_t colon = l.find(':');
+    if (colon != std::string::npos) {
+      size_t v = colon + 1;
+      while (v < l.size() && (l[v] == ' ' || l[v] == '\t')) ++v;
+      size_t ve = l.size();
+      while (ve > v && (l[ve - 1] == ' ' || l[ve - 1] == '\t')) --ve;
+      h->headers.emplace_back(Lower(l.substr(0, colon)), l.substr(v, ve - v));
+    }
+    pos = eol + 2;
+  }
+  return 1;
+}
+
+// Decode a chunked body starting at `from`; 0 = need more, -1 = malformed, else bytes consumed.
+long DecodeChunked(const std::string& in, size_t from, std::string* body)
+{
+  size_t pos = from;
+  body->clear();
+  while (true) {
+    const size_t eol = in.find("\r\n", pos);
+    if (eol == std::string::npos) return 0;
+    char* e = nullptr;
+    const unsigned long n = strtoul(in.c_str() + pos, &e, 16);
+    if (e == in.c_str() + pos) return -1;
+    pos = eol + 2;
+    if (n == 0) {
+      const size_t fin = in.find("\r\n", pos);  // (no trailers expected)
+      if (fin == std::string::npos) return 0;
+      return static_cast<long>(fin + 2 - from);
+    }
+    if (in.size() < pos + n + 2) return 0;
+    body->append(in, pos, n);
+    pos += n + 2;
+  }
+}
+
+// /v2/models/<m>[/versions/<v>]/infer -> (m, v)
+bool InferTarget(const std::string& target, std::string* model, std::string* version)
+{
+  static const std::string pre = "/v2/models/", suf = "/infer";
+  if (target.compare(0, pre.size(), pre) != 0 || target.size() <= pre.size() + suf.size() ||
+      target.compare(target.size() - suf.size(), suf.size(), suf) != 0 || target.find('?') != std::string::npos)
+    return false;
+  const std::string mid = target.substr(pre.size(), target.size() - pre.size() - suf.size());
+  const size_t vpos = mid.find("/versions/");
+  if (vpos == std::string::npos) {
+    if (mid.find('/') != std::string::npos) return false;
+    *model = mid;
+    version->clear();
+  } else {
+    *model = mid.substr(0, vpos);
+    *version = mid.substr(vpos + 10);
+    if (model->find('/') != std::string::npos || version->find('/') != std::string::npos) return false;
+  }
+  return !model->empty();
+}
+
+}  // namespace
+
+void Server::OnHttpData(Conn* c)
+{
+  while (!c->hin.empty() && !c->close_after) {
+    HttpHead h;
+    const int ph = ParseHead(c->hin, &h);
+    if (ph == 0) return;
+    if (ph < 0) {
+      c->closing = true;
+      return;
+    }
+    std::string body;
+    size_t consumed = h.head_len;
+    const std::string* te = h.Get("transfer-encoding");
+    const std::string* cl = h.Get("content-length");
+    bool rebuilt = false;
+    if (te && Lower(*te).find("chunked") != std::string::npos) {
+      const long n = DecodeChunked(c->hin, h.head_len, &body);
+      if (n == 0) return;
+      if (n < 0) {
+        c->closing = true;
+        return;
+      }
+      consumed += static_cast<size_t>(n);
+      rebuilt = true;  // relay with Content-Length instead of chunks
+    } else if (cl) {
+      const size_t n = strtoull(cl->c_str(), nullptr, 10);
+      if (c->hin.size() < h.head_len + n) return;
+      body.assign(c->hin, h.head_len, n);
+      consumed += n;
+    }
+    const std::string* conn_hdr = h.Get("connection");
+    const bool close = conn_hdr && Lower(*conn_hdr) == "close";
+    const uint64_t seq = c->req_seq++;
+    if (close) c->close_after = true;
+    std::string model, version;
+    const std::string* ihcl = h.Get("inference-header-content-length");
+    const std::string* ce = h.Get("content-encoding");
+    const std::string* ae = h.Get("accept-encoding");
+    bool handled = false;
+    if (h.method == "POST" && InferTarget(h.target, &model, &version) && ihcl && !ce &&
+        !(ae && (Lower(*ae).find("gzip") != std::string::npos || Lower(*ae).find("deflate") != std::string::npos))) {
+      const size_t jl = strtoull(ihcl->c_str(), nullptr, 10);
+      if (jl <= body.size()) handled = TryNativeHttp(c, seq, close, model, version, &body, jl);
+    }
+    if (!handled) {
+      std::string raw;
+      if (rebuilt) {
+        // head without Transfer-Encoding + Content-Length, then the decoded body
+        raw = h.method + " " + h.target + " HTTP/1.1\r\n";
+        const std::string head = c->hin.substr(0, h.head_len);
+        for (const auto& kv : h.headers)
+          if (kv.first != "transfer-encoding" && kv.first != "content-length") raw += kv.first + ": " + kv.second + "\r\n";
+        raw += "Content-Length: " + std::to_string(body.size()) + "\r\n\r\n" + body;
+      } else {
+        raw.assign(c->hin, 0, consumed);
+      }
+      ProxyHttp(c, seq, close, std::move(raw));
+    }
+    c->hin.erase(0, consumed);
+  }
+}
+
+bool Server::TryNativeHttp(Conn* c, uint64_t seq, bool close, const std::string& name, const std::string& version,
+                           std::string* body, size_t json_len)
+{
+  std::shared_ptr<NativeModel> m;
+  {
+    std::lock_guard<std::mutex> lk(models_mu);
+    auto it = models.find(name);
+    if (it == models.end()) return false;
+    m = it->second;
+  }
+  if (!version.empty() && version != m->version) return false;
+  namespace js = tc::json;
+  js::Value root;
+  std::string perr;
+  if (!js::Parse(body->data(), json_len, &root, &perr) || !root.IsObject()) return false;
+  bool binary_out_default = false;
+  if (const js::Value* params = root.Find("parameters")) {
+    for (const auto& kv : params->Members()) {
+      if (kv.first == "binary_data_output") binary_out_default = kv.second.AsBool();
+      else if (kv.first != "priority" && kv.first != "timeout") return false;  // sequences etc.: Python server
+    }
+  }
+  const js::Value* inputs = root.Find("inputs");
+  if (!inputs || !inputs->IsArray() || inputs->Size() != m->inputs.size()) return false;
+  std::unique_ptr<PendingReq> pr(new PendingReq());
+  pr->http = true;
+  pr->http_seq = seq;
+  pr->http_close = close;
+  pr->conn_id = c->id;
+  pr->loop = c->loop;
+  pr->stream_id = 0;
+  if (const js::Value* id = root.Find("id")) pr->id = id->AsString();
+  pr->t_arrive = NowNs();
+  pr->in.resize(m->inputs.size());
+  pr->rows = -1;
+  size_t data_off = json_len;
+  auto fail = [&](const std::string& msg) {
+    PostHttp(c->loop, c->id, seq, HttpError(400, msg, close), close);
+    std::lock_guard<std::mutex> lk(m->smu);
+    m->fail.count++;
+    m->fail.ns += NowNs() - pr->t_arrive;
+    return true;
+  };
+  auto lookup = [&](const std::string& region, ShmEntry* e) {
+    std::lock_guard<std::mutex> lk(shm_mu_);
+    for (int kk = 0; kk < 2; ++kk) {
+      auto it = shm_[kk].find(region);
+      if (it != shm_[kk].end()) {
+        *e = it->second;
+        return kk;
+      }
+    }
+    return -1;
+  };
+  for (const js::Value& t : inputs->Elements()) {
+    const js::Value* nm = t.Find("name");
+    const js::Value* dt = t.Find("datatype");
+    const js::Value* shape = t.Find("shape");
+    if (!nm || !dt || !shape || !shape->IsArray() || t.Find("data")) return false;  // JSON tensor data: Python
+    int idx = -1;
+    for (size_t k = 0; k < m->inputs.size(); ++k)
+      if (m->inputs[k].name == nm->AsString()) idx = static_cast<int>(k);
+    if (idx < 0) return false;
+    const TensorDef& d = m->inputs[idx];
+    if (dt->AsString() != d.dtype) return false;
+    if (shape->Size() != d.dims.size() + (m->max_batch > 0 ? 1 : 0)) return false;
+    int rows = 1;
+    size_t off = 0;
+    if (m->max_batch > 0) {
+      rows = static_cast<int>((*shape)[0].AsInt());
+      off = 1;
+    }
+    for (size_t k = 0; k < d.dims.size(); ++k)
+      if ((*shape)[k + off].AsInt() != d.dims[k]) return false;
+    if (rows < 1 || (m->max_batch > 0 && rows > m->max_batch)) return false;
+    if (pr->rows >= 0 && pr->rows != rows) return false;
+    pr->rows = rows;
+    const uint64_t need = static_cast<uint64_t>(rows) * d.sample_bytes;
+    std::string region;
+    int64_t rbytes = 0, roff = 0, bsize = -1;
+    bool has_shm = false;
+    if (const js::Value* tp = t.Find("parameters")) {
+      for (const auto& kv : tp->Members()) {
+        if (kv.first == "shared_memory_region") {
+          region = kv.second.AsString();
+          has_shm = true;
+        } else if (kv.first == "shared_memory_byte_size") {
+          rbytes = kv.second.AsInt();
+        } else if (kv.first == "shared_memory_offset") {
+          roff = kv.second.AsInt();
+        } else if (kv.first == "binary_data_size") {
+          bsize = kv.second.AsInt();
+        } else {
+          return false;
+        }
+      }
+    }
+    tcserve_ref& ref = pr->in[idx];
+    if (has_shm) {
+      ShmEntry e;
+      const int kind = lookup(region, &e);
+      if (kind < 0) return fail("Unable to find shared memory region: '" + region + "'");
+      if (roff < 0 || static_cast<uint64_t>(roff + rbytes) > e.bytes)
+        return fail("Invalid offset + byte size for shared memory region: '" + region + "'");
+      if (static_cast<uint64_t>(rbytes) < need)
+        return fail("input '" + d.name + "' shared memory region is smaller than the tensor");
+      ref = tcserve_ref{kind, e.device, e.ptr + roff, need};
+    } else {
+      if (bsize < 0) return false;
+      if (static_cast<uint64_t>(bsize) != need) return fail("unexpected byte size for input '" + d.name + "'");
+      if (data_off + need > body->size()) return fail("input '" + d.name + "' has no data");
+      pr->host_in_off.emplace_back(idx, data_off);
+      data_off += need;
+      ref = tcserve_ref{0, 0, 0, need};
+    }
+  }
+  const size_t no = m->outputs.size();
+  pr->out.assign(no, tcserve_ref{0, 0, 0, 0});
+  pr->out_shm.assign(no, false);
+  pr->out_region.assign(no, "");
+  pr->out_region_bytes.assign(no, 0);
+  pr->out_region_offset.assign(no, 0);
+  pr->host_out.resize(no);
+  const js::Value* outputs = root.Find("outputs");
+  pr->out_requested.assign(no, !outputs || outputs->Size() == 0);
+  if (!outputs || outputs->Size() == 0) {
+    if (!binary_out_default) return false;  // JSON output data: Python server
+  } else {
+    for (const js::Value& o : outputs->Elements()) {
+      const js::Value* nm = o.Find("name");
+      if (!nm) return false;
+      int idx = -1;
+      for (size_t k = 0; k < no; ++k)
+        if (m->outputs[k].name == nm->AsString()) idx = static_cast<int>(k);
+      if (idx < 0) return false;
+      pr->out_requested[idx] = true;
+      std::string region;
+      int64_t rbytes = 0, roff = 0;
+      bool has_shm = false, binary = binary_out_default;
+      if (const js::Value* op = o.Find("parameters")) {
+        for (const auto& kv : op->Members()) {
+          if (kv.first == "shared_memory_region") {
+            region = kv.second.AsString();
+            has_shm = true;
+          } else if (kv.first == "shared_memory_byte_size") {
+            rbytes = kv.second.AsInt();
+          } else if (kv.first == "shared_memory_offset") {
+            roff = kv.second.AsInt();
+          } else if (kv.first == "binary_data") {
+            binary = kv.second.AsBool();
+          } else {
+            return false;  // classification
+          }
+        }
+      }
+      const uint64_t need = static_cast<uint64_t>(pr->rows) * m->outputs[idx].sample_bytes;
+      if (has_shm) {
+        ShmEntry e;
+        const int kind = lookup(region, &e);
+        if (kind < 0) return fail("Unable to find shared memory region: '" + region + "'");
+        if (roff < 0 || static_cast<uint64_t>(roff + rbytes) > e.bytes)
+          return fail("Invalid offset + byte size for shared memory region: '" + region + "'");
+        if (static_cast<uint64_t>(rbytes) < need)
+          return fail("shared memory size specified with the request for output '" + m->outputs[idx].name + "' (" +
+                      std::to_string(rbytes) + " bytes) should be at least " + std::to_string(need) + " bytes");
+        pr->out[idx] = tcserve_ref{kind, e.device, e.ptr + roff, need};
+        pr->out_shm[idx] = true;
+        pr->out_region[idx] = region;
+        pr->out_region_bytes[idx] = rbytes;
+        pr->out_region_offset[idx] = roff;
+      } else if (!binary) {
+        return false;  // JSON output data: Python server
+      }
+    }
+  }
+  for (size_t k = 0; k < no; ++k) {
+    if (pr->out_requested[k] && !pr->out_shm[k]) {
+      const uint64_t need = static_cast<uint64_t>(pr->rows) * m->outputs[k].sample_bytes;
+      pr->host_out[k].resize(need);
+      pr->out[k] = tcserve_ref{0, 0, reinterpret_cast<uint64_t>(&pr->host_out[k][0]), need};
+    }
+  }
+  if (!pr->host_in_off.empty()) {
+    pr->body = std::move(*body);
+    for (const auto& io : pr->host_in_off)
+      pr->in[io.first].ptr = reinterpret_cast<uint64_t>(pr->body.data() + io.second);
+  }
+  n_native++;
+  {
+    std::lock_guard<std::mutex> lk(m->mu);
+    m->q_rows += pr->rows;
+    m->q.push_back(std::move(pr));
+  }
+  m->cv.notify_one();
+  return true;
+}
+
+std::string Server::HttpInferResponse(NativeModel* m, PendingReq* pr)
+{
+  std::string js = "{\"model_name\":";
+  tc::json::AppendEscapedString(&js, m->name);
+  js += ",\"model_version\":";
+  tc::json::AppendEscapedString(&js, m->version);
+  if (!pr->id.empty()) {
+    js += ",\"id\":";
+    tc::json::AppendEscapedString(&js, pr->id);
+  }
+  js += ",\"outputs\":[";
+  size_t binary = 0;
+  bool first = true;
+  for (size_t k = 0; k < m->outputs.size(); ++k) {
+    if (!pr->out_requested[k]) continue;
+    const TensorDef& d = m->outputs[k];
+    js += first ? "{\"name\":" : ",{\"name\":";
+    first = false;
+    tc::json::AppendEscapedString(&js, d.name);
+    js += ",\"datatype\":\"" + d.dtype + "\",\"shape\":[";
+    bool fd = true;
+    if (m->max_batch > 0) {
+      js += std::to_string(pr->rows);
+      fd = false;
+    }
+    for (auto dim : d.dims) {
+      js += (fd ? "" : ",") + std::to_string(dim);
+      fd = false;
+    }
+    js += "],\"parameters\":{";
+    if (pr->out_shm[k]) {
+      js += "\"shared_memory_region\":";
+      tc::json::AppendEscapedString(&js, pr->out_region[k]);
+      js += ",\"shared_memory_byte_size\":" + std::to_string(pr->out_region_bytes[k]);
+      if (pr->out_region_offset[k]) js += ",\"shared_memory_offset\":" + std::to_string(pr->out_region_offset[k]);
+    } else {
+      js += "\"binary_data_size\":" + std::to_string(pr->host_out[k].size());
+      binary += pr->host_out[k].size();
+    }
+    js += "}}";
+  }
+  js += "]}";
+  std::string r = HttpStatusLine(200);
+  if (binary) {
+    r += "Content-Type: application/octet-stream\r\nInference-Header-Content-Length: " + std::to_string(js.size()) +
+         "\r\n";
+  } else {
+    r += "Content-Type: application/json\r\n";
+  }
+  r += "Content-Length: " + std::to_string(js.size() + binary) + "\r\n";
+  if (pr->http_close) r += "Connection: close\r\n";
+  r += "\r\n";
+  r.reserve(r.size() + js.size() + binary);
+  r += js;
+  for (size_t k = 0; k < m->outputs.size(); ++k)
+    if (pr->out_requested[k] && !pr->out_shm[k]) r += pr->host_out[k];
+  return r;
+}
+
+void Server::FailPending(PendingReq* pr, int grpc_status, int http_status, const std::string& msg)
+{
+  if (pr->http) PostHttp(pr->loop, pr->conn_id, pr->http_seq, HttpError(http_status, msg, pr->http_close), pr->http_close);
+  else PostReply(pr->loop, pr->conn_id, pr->stream_id, std::string(), grpc_status, msg);
+}
+
+void Server::PostHttp(Loop* loop, uint64_t conn_id, uint64_t seq, std::string&& bytes, bool close)
+{
+  auto b = std::make_shared<std::string>(std::move(bytes));
+  loop->Post([loop, conn_id, seq, b, close] {
+    Conn* c = loop->Find(conn_id);
+    if (!c) return;
+    c->ready[seq] = std::move(*b);
+    for (auto it = c->ready.find(c->resp_seq); it != c->ready.end(); it = c->ready.find(c->resp_seq)) {
+      if (c->sendpos == c->sendbuf.size()) {
+        c->sendbuf.clear();
+        c->sendpos = 0;
+      }
+      c->sendbuf += it->second;
+      c->ready.erase(it);
+      c->resp_seq++;
+    }
+    if (close) c->close_after = true;
+    loop->Flush(c);
+  });
+}
+
+void Server::ProxyHttp(Conn* c, uint64_t seq, bool close, std::string&& raw)
+{
+  n_proxied++;
+  proxies_++;
+  Loop* loop = c->loop;
+  const uint64_t conn_id = c->id;
+  auto req = std::make_shared<std::string>(std::move(raw));
+  std::thread([this, loop, conn_id, seq, close, req] {
+    std::string resp;
+    std::string e = [&]() -> std::string {
+      tc::Socket sock;
+      std::string err = sock.Connect(up_http_host_, up_http_port_, 60000000, tc::TlsConfig());
+      if (!err.empty()) return err;
+      size_t sent = 0;
+      while (sent < req->size()) {
+        struct iovec iov = {const_cast<char*>(req->data()) + sent, req->size() - sent};
+        const ssize_t w = sock.Writev(&iov, 1);
+        if (w < 0) return "upstream write failed";
+        if (w == 0 && !sock.Wait(true, 60000000)) return "upstream write timed out";
+        sent += static_cast<size_t>(w);
+      }
+      // relay the raw response bytes; the parser only finds where it ends
+      tc::HttpResponseParser parser;
+      parser.Reset(false);
+      char buf[65536];
+      while (parser.state() != tc::HttpResponseParser::State::Done) {
+        if (parser.state() == tc::HttpResponseParser::State::Error) return "malformed upstream response: " + parser.error();
+        const ssize_t n = sock.Read(buf, sizeof(buf));
+        if (n == -2) {
+          if (!sock.Wait(false, 60000000)) return "upstream read timed out";
+          continue;
+        }
+        if (n <= 0) return resp.empty() ? "upstream closed the connection" : "";
+        resp.append(buf, n);
+        parser.Feed(buf, static_cast<size_t>(n));
+      }
+      return "";
+    }();
+    if (!e.empty()) resp = HttpError(502, "tcserve: upstream HTTP server: " + e, close);
+    PostHttp(loop, conn_id, seq, std::move(resp), close);
+    proxies_--;
+  }).detach();
+}
+
+bool Server::ListenHttp(const std::string& host, int port, const std::string& up_host, int up_port, std::string* err)
+{
+  up_http_host_ = up_host;
+  up_http_port_ = up_port;
+  int fd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  int one = 1;
+  setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(port));
+  if (inet_pton(AF_INET, host.c_str(), &a.sin_addr) != 1) a.sin_addr.s_addr = htonl(INADDR_ANY);
+  if (bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 || listen(fd, 1024) != 0) {
+    *err = "cannot bind/listen on HTTP port " + std::to_string(port) + ": " + strerror(errno);
+    close(fd);
+    return false;
+  }
+  socklen_t al = sizeof(a);
+  getsockname(fd, reinterpret_cast<sockaddr*>(&a), &al);
+  http_port_ = ntohs(a.sin_port);
+  loops[0]->http_listen_fd = fd;
+  loops[0]->AddListener(fd, 2);
+  return true;
 }
 
 void Server::OnRequestComplete(Conn* c, Stream* st)
@@ -1195,7 +1796,11 @@ void Server::Execute(NativeModel* m, int instance, std::vector<std::unique_ptr<P
   }
   for (auto& pr : batch) {
     if (rc != 0) {
-      PostReply(pr->loop, pr->conn_id, pr->stream_id, std::string(), kInternal, err);
+      FailPending(pr.get(), kInternal, 500, err);
+      continue;
+    }
+    if (pr->http) {
+      PostHttp(pr->loop, pr->conn_id, pr->http_seq, HttpInferResponse(m, pr.get()), pr->http_close);
       continue;
     }
     inference::ModelInferResponse resp;
@@ -1266,7 +1871,7 @@ int Server::RemoveModel(const std::string& name)
   for (auto& t : m->workers)
     if (t.joinable()) t.join();
   // fail what was still queued
-  for (auto& pr : m->q) PostReply(pr->loop, pr->conn_id, pr->stream_id, std::string(), kUnavailable, "model unloaded");
+  for (auto& pr : m->q) FailPending(pr.get(), kUnavailable, 503, "model unloaded");
   m->q.clear();
   return 0;
 }
@@ -1316,6 +1921,18 @@ void* tcserve_create(const char* host, int32_t port, const char* upstream_host, 
 }
 
 int32_t tcserve_port(void* server) { return static_cast<Server*>(server)->port(); }
+
+int32_t tcserve_listen_http(void* server, const char* host, int32_t port, const char* upstream_host,
+                            int32_t upstream_port, char* err, int32_t errlen)
+{
+  std::string e;
+  Server* s = static_cast<Server*>(server);
+  if (!s->ListenHttp(host ? host : "0.0.0.0", port, upstream_host ? upstream_host : "127.0.0.1", upstream_port, &e)) {
+    SetErr(err, errlen, e);
+    return -1;
+  }
+  return s->http_port();
+}
 
 int32_t tcserve_add_model(void* server, const char* name, const char* version, int32_t max_batch,
                           int32_t max_queue_delay_us, int32_t instances, int32_t n_inputs, const char** in_names,

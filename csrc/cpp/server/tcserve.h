@@ -49,6 +49,10 @@ typedef int (*tcserve_exec_fn)(void* user, int32_t instance, const tcserve_batch
 void* tcserve_create(const char* host, int32_t port, const char* upstream_host, int32_t upstream_port,
                      int32_t io_threads, char* err, int32_t errlen);
 int32_t tcserve_port(void* server);
+/// Also serve KServe REST on host:port (native infer fast path; everything else is
+/// relayed to the HTTP server at upstream_host:upstream_port).  Returns the bound port or -1.
+int32_t tcserve_listen_http(void* server, const char* host, int32_t port, const char* upstream_host,
+                            int32_t upstream_port, char* err, int32_t errlen);
 /// dims are per-sample (without the batch dimension), flattened; ndims[i] gives each tensor's rank.
 int32_t tcserve_add_model(void* server, const char* name, const char* version, int32_t max_batch,
                           int32_t max_queue_delay_us, int32_t instances, int32_t n_inputs, const char** in_names,

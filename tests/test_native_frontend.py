@@ -5,6 +5,8 @@ indistinguishable on the wire from the Python path; everything else is
 proxied to the grpc.aio server behind it.
 """
 
+import json
+
 import numpy as np
 import pytest
 
@@ -44,6 +46,14 @@ def test_fast_path_results_and_counters(cpu_server):
 
 
 def test_fast_path_async_batches(cpu_server):
+    cpu_server.server.native_frontend.set_idle_dispatch("add_sub_batched", False)
+    try:
+        _async_batches(cpu_server)
+    finally:
+        cpu_server.server.native_frontend.set_idle_dispatch("add_sub_batched", True)
+
+
+def _async_batches(cpu_server):
     c = grpcclient.InferenceServerClient(cpu_server.grpc_url)
     results = []
     import threading
@@ -82,6 +92,7 @@ def test_preferred_batch_size_caps_batches(cpu_server):
 
     before = sizes()
     nf.set_preferred("add_sub_batched", [2])
+    nf.set_idle_dispatch("add_sub_batched", False)  # batch even while the (fast) model is idle
     try:
         done = threading.Event()
         got = []
@@ -98,6 +109,7 @@ def test_preferred_batch_size_caps_batches(cpu_server):
         assert all(e is None for e in got)
     finally:
         nf.set_preferred("add_sub_batched", [])
+        nf.set_idle_dispatch("add_sub_batched", True)
     after = sizes()
     new = {bs: after.get(bs, 0) - before.get(bs, 0) for bs in after}
     assert all(n == 0 for bs, n in new.items() if bs > 2), new
@@ -225,3 +237,131 @@ def test_fast_path_large_inband_tensor(cpu_server):
     i._raw_content = x.tobytes()
     with pytest.raises(InferenceServerException, match="unexpected byte size"):
         c.infer("frontend_sink", [i])
+
+
+# -- KServe REST through tcserve (csrc/cpp/server: native infer path + relay) ----------------
+import socket  # noqa: E402
+
+import tritonclient.http as httpclient  # noqa: E402
+
+
+def _http_inputs(a, b, binary=True):
+    i0 = httpclient.InferInput("INPUT0", list(a.shape), "INT32")
+    i0.set_data_from_numpy(a, binary_data=binary)
+    i1 = httpclient.InferInput("INPUT1", list(b.shape), "INT32")
+    i1.set_data_from_numpy(b, binary_data=binary)
+    return [i0, i1]
+
+
+def test_http_binary_infer_runs_native(cpu_server):
+    nf = cpu_server.server.native_frontend
+    c = httpclient.InferenceServerClient(cpu_server.http_url)
+    a = np.arange(32, dtype=np.int32).reshape(2, 16)
+    b = np.full((2, 16), 3, dtype=np.int32)
+    before = nf.counters()
+    outs = [httpclient.InferRequestedOutput("OUTPUT0", binary_data=True),
+            httpclient.InferRequestedOutput("OUTPUT1", binary_data=True)]
+    r = c.infer("add_sub_batched", _http_inputs(a, b), outputs=outs, request_id="r1")
+    np.testing.assert_array_equal(r.as_numpy("OUTPUT0"), a + b)
+    np.testing.assert_array_equal(r.as_numpy("OUTPUT1"), a - b)
+    resp = r.get_response()
+    assert resp["model_name"] == "add_sub_batched" and resp["id"] == "r1"
+    assert resp["outputs"][0]["shape"] == [2, 16] and resp["outputs"][0]["datatype"] == "INT32"
+    # no outputs listed: binary_data_output (the client's default) -> native too
+    r = c.infer("add_sub_batched", _http_inputs(a, b))
+    np.testing.assert_array_equal(r.as_numpy("OUTPUT1"), a - b)
+    after = nf.counters()
+    assert after["native_requests"] == before["native_requests"] + 2
+    assert after["proxied_calls"] == before["proxied_calls"]
+
+
+def test_http_json_tensors_and_control_plane_are_relayed(cpu_server):
+    nf = cpu_server.server.native_frontend
+    c = httpclient.InferenceServerClient(cpu_server.http_url)
+    a = np.arange(16, dtype=np.int32).reshape(1, 16)
+    before = nf.counters()
+    # JSON input data and JSON outputs: the Python server answers, same results
+    r = c.infer("add_sub_batched", _http_inputs(a, a, binary=False),
+                outputs=[httpclient.InferRequestedOutput("OUTPUT0", binary_data=False)])
+    np.testing.assert_array_equal(r.as_numpy("OUTPUT0"), 2 * a)
+    assert c.is_server_live() and c.is_model_ready("add_sub_batched")
+    assert c.get_model_metadata("add_sub_batched")["name"] == "add_sub_batched"
+    with pytest.raises(InferenceServerException):
+        c.get_model_metadata("no_such_model")
+    # gzip'd request body: relayed (the native path takes identity bodies only)
+    r = c.infer("add_sub_batched", _http_inputs(a, a), request_compression_algorithm="gzip",
+                response_compression_algorithm="gzip")
+    np.testing.assert_array_equal(r.as_numpy("OUTPUT1"), 0 * a)
+    assert nf.counters()["proxied_calls"] >= before["proxied_calls"] + 5
+
+
+def test_http_native_errors_and_system_shm(cpu_server):
+    c = httpclient.InferenceServerClient(cpu_server.http_url)
+    a = np.arange(16, dtype=np.int32).reshape(1, 16)
+    i0 = httpclient.InferInput("INPUT0", [1, 16], "INT32")
+    i0.set_shared_memory("no_such_region", 64)
+    i1 = _http_inputs(a, a)[1]
+    with pytest.raises(InferenceServerException, match="Unable to find shared memory region"):
+        c.infer("add_sub_batched", [i0, i1])
+    h = shm.create_shared_memory_region("http_in0", "/http_in0_native", 64)
+    ho = shm.create_shared_memory_region("http_out0", "/http_out0_native", 64)
+    try:
+        shm.set_shared_memory_region(h, [a])
+        c.register_system_shared_memory("http_in0", "/http_in0_native", 64)
+        c.register_system_shared_memory("http_out0", "/http_out0_native", 64)
+        i0 = httpclient.InferInput("INPUT0", [1, 16], "INT32")
+        i0.set_shared_memory("http_in0", 64)
+        o0 = httpclient.InferRequestedOutput("OUTPUT0")
+        o0.set_shared_memory("http_out0", 64)
+        r = c.infer("add_sub_batched", [i0, i1], outputs=[o0])
+        assert r.get_output("OUTPUT0")["parameters"]["shared_memory_region"] == "http_out0"
+        np.testing.assert_array_equal(shm.get_contents_as_numpy(ho, np.int32, [1, 16]), 2 * a)
+    finally:
+        c.unregister_system_shared_memory()
+        shm.destroy_shared_memory_region(h)
+        shm.destroy_shared_memory_region(ho)
+
+
+def test_http_pipelined_requests_keep_order_and_connection_close(cpu_server):
+    """Raw HTTP/1.1: two pipelined requests (native + relayed) answered in
+    order on one connection, then Connection: close honoured."""
+    host, port = cpu_server.http_url.split(":")
+    a = np.arange(16, dtype=np.int32)
+    hdr = json.dumps({"inputs": [{"name": n, "shape": [1, 16], "datatype": "INT32",
+                                  "parameters": {"binary_data_size": 64}} for n in ("INPUT0", "INPUT1")],
+                      "parameters": {"binary_data_output": True}}).encode()
+    body = hdr + a.tobytes() + a.tobytes()
+    infer = (b"POST /v2/models/add_sub_batched/infer HTTP/1.1\r\nHost: x\r\nInference-Header-Content-Length: %d\r\n"
+             b"Content-Length: %d\r\n\r\n" % (len(hdr), len(body))) + body
+    live = b"GET /v2/health/live HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n"
+    s = socket.create_connection((host, int(port)))
+    s.sendall(infer + live)
+    data = b""
+    while True:
+        chunk = s.recv(65536)
+        if not chunk:
+            break
+        data += chunk
+    s.close()
+    first, rest = data.split(b"\r\n\r\n", 1)
+    assert first.startswith(b"HTTP/1.1 200") and b"inference-header-content-length" in first.lower()
+    clen = int([ln.split(b":")[1] for ln in first.split(b"\r\n") if ln.lower().startswith(b"content-length")][0])
+    second = rest[clen:]
+    assert second.startswith(b"HTTP/1.1 200")  # the relayed /live answer, after the infer
+
+
+def test_http_chunked_upload_is_decoded_and_relayed(cpu_server):
+    host, port = cpu_server.http_url.split(":")
+    body = json.dumps({"log_verbose_level": 0}).encode()
+    req = (b"POST /v2/logging HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\n" +
+           b"%x\r\n%s\r\n0\r\n\r\n" % (len(body), body))
+    s = socket.create_connection((host, int(port)))
+    s.sendall(req)
+    data = b""
+    while True:
+        chunk = s.recv(65536)
+        if not chunk:
+            break
+        data += chunk
+    s.close()
+    assert data.startswith(b"HTTP/1.1 200"), data[:200]

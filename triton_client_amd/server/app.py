@@ -1,6 +1,7 @@
 """Server process wiring: asyncio loop running the HTTP + gRPC front ends."""
 
 import asyncio
+import os
 import socket
 import threading
 
@@ -54,11 +55,20 @@ async def serve(server, http_port, grpc_port, host="127.0.0.1", ready_evt=None, 
     if native_grpc is None:
         native_grpc = native_grpc_available()
     runner = None
+    native_http = native_grpc and http_port is not None and grpc_port is not None and \
+        os.environ.get("TCSERVE_HTTP", "1") != "0"
+    inner_http = None
     if http_port is not None:
         runner = web.AppRunner(HttpFrontend(server).app, access_log=None)
         await runner.setup()
-        site = web.TCPSite(runner, host, http_port, reuse_address=True)
-        await site.start()
+        if native_http:
+            # the public HTTP port is tcserve's; aiohttp serves what it relays
+            site = web.TCPSite(runner, "127.0.0.1", 0, reuse_address=True)
+            await site.start()
+            inner_http = site._server.sockets[0].getsockname()[1]
+        else:
+            site = web.TCPSite(runner, host, http_port, reuse_address=True)
+            await site.start()
     gserver = None
     nf = None
     if grpc_port is not None:
@@ -75,6 +85,8 @@ async def serve(server, http_port, grpc_port, host="127.0.0.1", ready_evt=None, 
             nf = NativeFrontend(server, host, grpc_port, inner)
             nf.register_all()
             server.native_frontend = nf
+            if native_http:
+                nf.listen_http(host, http_port, inner_http)
     if ready_evt is not None:
         ready_evt.set()
     stop = stop_evt or asyncio.Event()

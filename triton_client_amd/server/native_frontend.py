@@ -78,6 +78,9 @@ def _load():
         lib.tcserve_batch_stats.restype = ctypes.c_int32
         lib.tcserve_counters.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
         lib.tcserve_counters.restype = ctypes.c_int32
+        lib.tcserve_listen_http.argtypes = [ctypes.c_void_p, cp, ctypes.c_int32, cp, ctypes.c_int32, ctypes.c_char_p,
+                                            ctypes.c_int32]
+        lib.tcserve_listen_http.restype = ctypes.c_int32
         lib.tcserve_destroy.argtypes = [ctypes.c_void_p]
         lib.tcserve_destroy.restype = None
         _lib = lib
@@ -117,6 +120,15 @@ class NativeFrontend:
     @property
     def port(self):
         return _load().tcserve_port(self._h)
+
+    def listen_http(self, host, port, upstream_port):
+        """Serve KServe REST on host:port: native infer fast path, everything
+        else relayed to the aiohttp server on 127.0.0.1:upstream_port."""
+        err = ctypes.create_string_buffer(512)
+        p = _load().tcserve_listen_http(self._h, host.encode(), int(port), b"127.0.0.1", int(upstream_port), err, 512)
+        if p < 0:
+            raise RuntimeError("tcserve: %s" % err.value.decode(errors="replace"))
+        return p
 
     # -- shared memory mirror ------------------------------------------------------
     def _on_shm(self, kind, op, name, ptr=0, nbytes=0, device=0):
