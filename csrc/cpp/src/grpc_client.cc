@@ -304,7 +304,7 @@ InferenceServerGrpcClient::Create(
 Error
 InferenceServerGrpcClient::UnaryRaw(
     const char* method, std::string&& request, std::string* response, const Headers& headers, uint64_t timeout_us,
-    grpc_compression_algorithm comp)
+    grpc_compression_algorithm comp, bool framed)
 {
   if (!channel_) return channel_error_;
   struct Wait {
@@ -324,7 +324,8 @@ InferenceServerGrpcClient::UnaryRaw(
     w->cv.notify_all();
   };
   auto call = channel_->StartCall(std::string(kService) + method, Metadata(headers), timeout_us, ToComp(comp), h);
-  call->Write(std::move(request));
+  if (framed) call->WriteFramed(std::move(request));
+  else call->Write(std::move(request));
   call->WritesDone();
   std::unique_lock<std::mutex> lk(w->mu);
   w->cv.wait(lk, [&] { return w->done; });
@@ -564,10 +565,51 @@ InferenceServerGrpcClient::UnregisterCudaSharedMemory(const std::string& name, c
 }
 
 //==============================================================================
+// One-copy request encoding for uncompressed calls: the gRPC frame prefix,
+// the request without its raw tensors, then every raw tensor as field 7
+// (raw_input_contents) copied once from the caller's buffers — protobuf
+// readers accept fields in any order.  (SerializeAsString + GrpcFrame copy
+// each tensor three times.)
+static void PutVarint(std::string* out, uint64_t v)
+{
+  while (v >= 0x80) {
+    out->push_back(static_cast<char>((v & 0x7f) | 0x80));
+    v >>= 7;
+  }
+  out->push_back(static_cast<char>(v));
+}
+
+static std::string FramedInferRequest(const inference::ModelInferRequest& head, const std::vector<InferInput*>& inputs)
+{
+  size_t raw = 0;
+  for (InferInput* in : inputs)
+    if (!in->IsSharedMemory())
+      for (size_t s : in->BufferSizes()) raw += s + 16;
+  std::string out;
+  out.reserve(5 + 256 + raw);
+  out.append(5, '\0');
+  head.Encode(&out);
+  for (InferInput* in : inputs) {
+    if (in->IsSharedMemory()) continue;
+    size_t total = 0;
+    for (size_t s : in->BufferSizes()) total += s;
+    out.push_back(static_cast<char>((7 << 3) | 2));
+    PutVarint(&out, total);
+    for (size_t i = 0; i < in->Buffers().size(); ++i)
+      out.append(reinterpret_cast<const char*>(in->Buffers()[i]), in->BufferSizes()[i]);
+  }
+  const uint32_t n = static_cast<uint32_t>(out.size() - 5);
+  out[1] = static_cast<char>(n >> 24);
+  out[2] = static_cast<char>(n >> 16);
+  out[3] = static_cast<char>(n >> 8);
+  out[4] = static_cast<char>(n);
+  return out;
+}
+
 Error
 InferenceServerGrpcClient::BuildInferRequest(
     const InferOptions& options, const std::vector<InferInput*>& inputs,
-    const std::vector<const InferRequestedOutput*>& outputs, inference::ModelInferRequest* req)
+    const std::vector<const InferRequestedOutput*>& outputs, inference::ModelInferRequest* req, bool include_raw)
 {
   req->set_model_name(options.model_name_);
   req->set_model_version(options.model_version_);
@@ -605,7 +647,7 @@ InferenceServerGrpcClient::BuildInferRequest(
       (*t->mutable_parameters())["shared_memory_region"].set_string_param(region);
       (*t->mutable_parameters())["shared_memory_byte_size"].set_int64_param(static_cast<int64_t>(bs));
       if (off) (*t->mutable_parameters())["shared_memory_offset"].set_int64_param(static_cast<int64_t>(off));
-    } else {
+    } else if (include_raw) {
       std::string* raw = req->add_raw_input_contents();
       size_t total = 0;
       for (size_t s : in->BufferSizes()) total += s;
@@ -642,16 +684,19 @@ InferenceServerGrpcClient::Infer(
   timers.CaptureTimestamp(K::REQUEST_START);
   timers.CaptureTimestamp(K::SEND_START);
   inference::ModelInferRequest req;
-  Error e = BuildInferRequest(options, inputs, outputs, &req);
+  const bool one_copy = compression_algorithm == GRPC_COMPRESS_NONE;
+  Error e = BuildInferRequest(options, inputs, outputs, &req, !one_copy);
   if (!e.IsOk()) return e;
-  std::string wire = req.SerializeAsString();
-  if (wire.size() > static_cast<size_t>(MAX_GRPC_MESSAGE_SIZE)) {
-    return Error("Request has byte size " + std::to_string(wire.size()) +
+  std::string wire = one_copy ? FramedInferRequest(req, inputs) : req.SerializeAsString();
+  const size_t msg_size = wire.size() - (one_copy ? 5 : 0);
+  if (msg_size > static_cast<size_t>(MAX_GRPC_MESSAGE_SIZE)) {
+    return Error("Request has byte size " + std::to_string(msg_size) +
                  " which exceed gRPC's byte size limit " + std::to_string(INT32_MAX) + ".");
   }
   timers.CaptureTimestamp(K::SEND_END);
   std::string out;
-  e = UnaryRaw("ModelInfer", std::move(wire), &out, headers, options.client_timeout_, compression_algorithm);
+  e = UnaryRaw("ModelInfer", std::move(wire), &out, headers, options.client_timeout_, compression_algorithm,
+               one_copy);
   timers.CaptureTimestamp(K::RECV_START);
   auto resp = std::make_shared<inference::ModelInferResponse>();
   if (e.IsOk() && !resp->ParseFromString(out)) e = Error("failed to parse ModelInferResponse");
@@ -675,9 +720,13 @@ InferenceServerGrpcClient::AsyncInfer(
   timers->CaptureTimestamp(K::REQUEST_START);
   timers->CaptureTimestamp(K::SEND_START);
   inference::ModelInferRequest req;
-  Error e = BuildInferRequest(options, inputs, outputs, &req);
+  const bool one_copy = compression_algorithm == GRPC_COMPRESS_NONE;
+  Error e = BuildInferRequest(options, inputs, outputs, &req, !one_copy);
   if (!e.IsOk()) return e;
-  std::string wire = req.SerializeAsString();
+  std::string wire = one_copy ? FramedInferRequest(req, inputs) : req.SerializeAsString();
+  if (wire.size() - (one_copy ? 5 : 0) > static_cast<size_t>(MAX_GRPC_MESSAGE_SIZE))
+    return Error("Request has byte size " + std::to_string(wire.size() - (one_copy ? 5 : 0)) +
+                 " which exceed gRPC's byte size limit " + std::to_string(INT32_MAX) + ".");
   timers->CaptureTimestamp(K::SEND_END);
   auto msg = std::make_shared<std::string>();
   H2CallHandlers h;
@@ -697,7 +746,8 @@ InferenceServerGrpcClient::AsyncInfer(
   };
   auto call = channel_->StartCall(std::string(kService) + "ModelInfer", Metadata(headers), options.client_timeout_,
                                   ToComp(compression_algorithm), h);
-  call->Write(std::move(wire));
+  if (one_copy) call->WriteFramed(std::move(wire));
+  else call->Write(std::move(wire));
   call->WritesDone();
   return Error::Success;
 }

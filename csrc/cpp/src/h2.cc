@@ -293,6 +293,21 @@ H2Channel::StartCall(
 }
 
 void
+H2Call::WriteFramed(std::string&& framed)
+{
+  auto ch = chan_.lock();
+  if (!ch) return;
+  auto self = shared_from_this();
+  ch->Post([ch, self, framed = std::move(framed)]() mutable {
+    self->out_.push_back(std::move(framed));
+    if (self->deferred_ && self->stream_id_ > 0 && !self->closed_) {
+      self->deferred_ = false;
+      nghttp2_session_resume_data(S(ch->session_), self->stream_id_);
+    }
+  });
+}
+
+void
 H2Call::Write(std::string&& message)
 {
   auto ch = chan_.lock();

@@ -110,6 +110,8 @@ class H2Call : public std::enable_shared_from_this<H2Call> {
  public:
   /// Queue one request message (serialised protobuf).
   void Write(std::string&& message);
+  /// A message already carrying its 5-byte gRPC prefix (uncompressed calls only).
+  void WriteFramed(std::string&& framed);
   /// No more messages from the client (END_STREAM).
   void WritesDone();
   /// Abort the call (RST_STREAM CANCEL); on_close gets CANCELLED.
