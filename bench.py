@@ -40,11 +40,14 @@ def main():
     ap.add_argument("--concurrency", type=int, default=48, help="requests in flight per GPU")
     ap.add_argument("--fanout", default="rccl", choices=["rccl", "p2p", "local"])
     # operating point from tools/gpu_bench_sweep.sh on MI355X (profiles/r1_operating_points.md):
-    # three model instances (HIP streams) each running full 128-row batches overlap
-    # well on the 256 CUs (1.3x one stream's throughput)
-    ap.add_argument("--instance-count", type=int, default=3)
+    # four model instances (HIP streams) each running full 128-row batches overlap
+    # well on the 256 CUs (~1.3x one stream's throughput)
+    ap.add_argument("--instance-count", type=int, default=4)
     ap.add_argument("--max-queue-delay-us", type=int, default=2000)
     ap.add_argument("--preferred", default="128", help="server preferred batch sizes (comma-separated rows; '' = none)")
+    # a closed-loop saturation run wants full batches: no early dispatch of partial ones
+    ap.add_argument("--idle-dispatch", default="off", choices=["on", "off"],
+                    help="server: dispatch partial batches at once while every instance is idle")
     ap.add_argument("--engine", default="fused", choices=["fused", "torch"],
                     help="densenet_onnx engine in the server (fused HIP/MFMA kernels or torch/MIOpen)")
     ap.add_argument("--loadgen", default="native", choices=["native", "python"],
@@ -73,7 +76,8 @@ def main():
             models="densenet_onnx",
             extra_args=["--instance-count", str(args.instance_count), "--engine", args.engine,
                         "--max-queue-delay-us", str(args.max_queue_delay_us)]
-            + (["--preferred-batch-sizes", args.preferred] if args.preferred else []),
+            + (["--preferred-batch-sizes", args.preferred] if args.preferred else [])
+            + ["--idle-dispatch", args.idle_dispatch],
             log_path=log_path,
         )
 
@@ -207,6 +211,7 @@ def main():
                     "server_instances": args.instance_count,
                     "preferred_batch_rows": args.preferred,
                     "max_queue_delay_us": args.max_queue_delay_us,
+                    "idle_dispatch": args.idle_dispatch,
                 },
                 "p50_latency_us": round(percentile_us(all_lat, 50), 1),
                 "p90_latency_us": round(percentile_us(all_lat, 90), 1),

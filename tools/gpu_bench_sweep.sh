@@ -3,13 +3,13 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/sweep
-while read -r C P D I; do
-  I=${I:-2}
+while read -r C P D I X; do
+  I=${I:-2}; X=${X:-on}
   [ -z "$C" ] && continue
-  tag="c${C}_p${P:-none}_d${D}_i${I}"
+  tag="c${C}_p${P:-none}_d${D}_i${I}_idle${X}"
   extra=""
   [ "$P" != "none" ] && extra="--preferred $P"
-  timeout -k 10 240 python -u bench.py --steps 40 --warmup 10 --concurrency $C --max-queue-delay-us $D --instance-count $I $extra \
+  timeout -k 10 240 python -u bench.py --steps 40 --warmup 10 --concurrency $C --max-queue-delay-us $D --instance-count $I --idle-dispatch $X $extra \
     > gpurun_out/sweep/$tag.log 2>&1 || { echo "FAIL $tag"; exit 1; }
   echo "$tag $(tail -1 gpurun_out/sweep/$tag.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["p50_latency_us"], d["p99_latency_us"], d.get("server_avg_batch_rows_rank0"))')"
 done < "${1:-/dev/stdin}"
