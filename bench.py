@@ -79,6 +79,8 @@ def main():
             + (["--preferred-batch-sizes", args.preferred] if args.preferred else [])
             + ["--idle-dispatch", args.idle_dispatch],
             log_path=log_path,
+            # per-rank port range: N ranks start their servers at once
+            port_stripe=local_rank if world > 1 else None,
         )
 
     import numpy as np

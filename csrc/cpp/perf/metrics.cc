@@ -15,6 +15,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "perf.h"
 
 namespace tcperf {
@@ -87,14 +89,44 @@ std::string PowerFile(const std::string& dev)
   return found;
 }
 
+std::string Lower(std::string s)
+{
+  for (auto& c : s) c = static_cast<char>(tolower(static_cast<unsigned char>(c)));
+  return s;
+}
+
+// PCI address ("0000:75:00.0", lower case) of HIP device `device`, or "".
+std::string HipPciAddress(int device)
+{
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return std::string();
+  return Lower(bus);
+}
+
 }  // namespace
 
 GpuMetrics::GpuMetrics(int device, uint64_t interval_ms, const std::string& sysfs_root)
     : interval_ms_(std::max<uint64_t>(10, interval_ms))
 {
   const auto gpus = AmdGpus(sysfs_root.empty() ? "/sys/class/drm" : sysfs_root);
-  if (device < 0 || device >= static_cast<int>(gpus.size())) return;
-  dev_ = gpus[device];
+  if (sysfs_root.empty()) {
+    // a container or HIP_VISIBLE_DEVICES can hide cards, so HIP device N is
+    // not necessarily the N-th amdgpu card in sysfs: match it by PCI address
+    const std::string pci = HipPciAddress(device);
+    for (const auto& g : gpus) {
+      char rp[4096] = {0};
+      if (pci.empty() || !realpath(g.c_str(), rp)) continue;
+      const std::string r = Lower(rp);
+      if (r.size() >= pci.size() && r.compare(r.size() - pci.size(), pci.size(), pci) == 0) {
+        dev_ = g;
+        break;
+      }
+    }
+  }
+  if (dev_.empty()) {
+    if (device < 0 || device >= static_cast<int>(gpus.size())) return;
+    dev_ = gpus[device];
+  }
   power_file_ = PowerFile(dev_);
 }
 

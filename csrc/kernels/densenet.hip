@@ -1123,6 +1123,95 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kr_kernel(Conv3x3Params p) {
   }
 }
 
+// K9w: K9c with a SLIDING activation band.  K9c re-stages the whole band
+// [m0-W-1, m0+128+W+1) of every 128-pixel tile: 242 rows per 128 output
+// pixels at 56x56 (1.9x the activation bytes through L2 and LDS, and the
+// per-tile load is what bounds it).  Here each block owns a CONTIGUOUS run of
+// tiles and keeps the band in a 256-row LDS ring (pixel q lives in ring row
+// q & 255): after the first tile of its run a block fetches only the 128 rows
+// the next tile adds — issued into registers while the current tile computes,
+// written after the barrier over ring rows no later tile of the run reads
+// (valid while 2 * (W + 1) <= 128).  Weights LDS-resident as in K9c.
+constexpr int kRing = 256;
+
+__global__ void __launch_bounds__(256) conv3x3_ring_kernel(Conv3x3Params p) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Ws = smem;                   // [32][kWsK]
+  uint16_t* As = smem + kN3 * kWsK;      // [kRing + 1][kActStride], row kRing = 0
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  stage_weights(p.w, Ws, tid);
+  if (tid < kActStride / 8) *reinterpret_cast<v4u*>(&As[kRing * kActStride + tid * 8]) = v4u{0, 0, 0, 0};
+  const int W = p.W, HW = p.H * p.W;
+  const int halo = W + 1;
+  const int per = p.tiles / (int)gridDim.x, extra = p.tiles % (int)gridDim.x;
+  const int t0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
+  const int t1 = t0 + per + ((int)blockIdx.x < extra ? 1 : 0);
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.z, (short)0,
+                                                      (int)((size_t)p.M * kC3 * 2), 0x00020000);
+  // chunk c (16 B) of pixel rows [first, first + nrows); out-of-range pixels read as 0
+  auto fetch = [&](int first, int nrows, int c) -> v4u {
+    const int pix = first + (c >> 4);
+    const bool ok = c < nrows * 16 && pix >= 0 && pix < p.M;
+    return __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? (pix * kC3 + (c & 15) * 8) * 2 : 0x40000000, 0, 0);
+  };
+  auto put = [&](int first, int nrows, int c, v4u v) {
+    if (c < nrows * 16)
+      *reinterpret_cast<v4u*>(&As[((first + (c >> 4)) & (kRing - 1)) * kActStride + (c & 15) * 8]) = v;
+  };
+  constexpr int CPT0 = ((kTileP + 2 * 57) * 16 + 255) / 256;  // first band (W <= 56): 16 chunks per thread
+  constexpr int CPT = kTileP * 16 / 256;                       // a step's new rows: 8
+  if (t0 < t1) {
+    const int first = t0 * kTileP - halo, n = kTileP + 2 * halo;
+    v4u st0[CPT0];
+#pragma unroll
+    for (int i = 0; i < CPT0; ++i) st0[i] = fetch(first, n, tid + i * 256);
+#pragma unroll
+    for (int i = 0; i < CPT0; ++i) put(first, n, tid + i * 256, st0[i]);
+  }
+  v4u st[CPT];
+  const int col = lane & 31, kh = 8 * (lane >> 5);
+  for (int tile = t0; tile < t1; ++tile) {
+    __syncthreads();  // previous tile's LDS reads done (first time: weights + first band staged)
+    if (tile > t0) {
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) put(tile * kTileP + halo, kTileP, tid + i * 256, st[i]);
+    }
+    __syncthreads();
+    if (tile + 1 < t1) {
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) st[i] = fetch((tile + 1) * kTileP + halo, kTileP, tid + i * 256);
+    }
+    const int m = tile * kTileP + wave * 32 + col;
+    const int mm = m < p.M ? m : 0;
+    const int img = mm / HW, rr = mm - img * HW;
+    const int h = rr / W, w = rr - h * W;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    const bool up = h > 0, down = h + 1 < p.H, left = w > 0, right = w + 1 < W, in = m < p.M;
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+      const bool ok = in && (dy < 0 ? up : dy > 0 ? down : true) && (dx < 0 ? left : dx > 0 ? right : true);
+      const uint16_t* arow = &As[(ok ? ((m + dy * W + dx) & (kRing - 1)) : kRing) * kActStride + kh];
+      const uint16_t* wrow = &Ws[col * kWsK + tap * kC3 + kh];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const v4u b = *reinterpret_cast<const v4u*>(arow + c * 16);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(wrow + c * 16);
+        acc = mfma32(a, as_frag(b), acc);
+      }
+    }
+    if (m < p.M) {
+      uint16_t* yp = p.y + (size_t)m * p.ldy + 4 * (lane >> 5);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<v2u*>(yp + 8 * g) =
+            v2u{pack2(acc[4 * g], acc[4 * g + 1]), pack2(acc[4 * g + 2], acc[4 * g + 3])};
+    }
+  }
+}
+
 // ============================================================================
 // K10a: stem epilogue  y = relu(maxpool3x3/2(x) + b)  (bias+ReLU commute with max)
 // ============================================================================
@@ -1559,6 +1648,21 @@ int launch_3x3_kr(Conv3x3Params p, hipStream_t s) {
   return hipGetLastError();
 }
 
+int launch_3x3_ring(Conv3x3Params p, hipStream_t s) {
+  if (p.W > 56) return hipErrorInvalidValue;  // ring reuse needs 2 * (W + 1) <= kTileP
+  const int lds = (kN3 * kWsK + (kRing + 1) * kActStride) * 2;
+  static int attr = 0;
+  if (attr < lds) {
+    int rc = hipFuncSetAttribute((const void*)conv3x3_ring_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (rc != hipSuccess) return rc;
+    attr = lds;
+  }
+  p.tiles = (p.M + kTileP - 1) / kTileP;
+  const int grid = p.tiles < 256 ? p.tiles : 256;  // one resident block per CU (LDS-limited)
+  hipLaunchKernelGGL(conv3x3_ring_kernel, dim3(grid), dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
 int launch_3x3_lds(Conv3x3Params p, hipStream_t s) {
   if (p.W > 56) return hipErrorInvalidValue;
   const int lds = (kN3 * kWsK + (kZeroRow + 1) * kActStride) * 2;
@@ -1671,6 +1775,7 @@ int tcamd_dn_conv3x3_v(const void* z, int imgs, int H, int W, const void* w, voi
     case 41: return launch_3x3<4, 1>(p, s);
     case 60: return launch_3x3_lds(p, s);     // LDS-staged activations, 32x32x16 MFMA
     case 80: return launch_3x3_kr(p, s);      // K9r: weights in registers, K split over waves
+    case 90: return launch_3x3_ring(p, s);    // K9w: K9c with a sliding band (contiguous tile runs)
     case 70:                                  // K9s: waves split the input channels
       hipLaunchKernelGGL(conv3x3_sk_kernel, dim3((p.M + 31) / 32), dim3(256), 0, s, p);
       return hipGetLastError();

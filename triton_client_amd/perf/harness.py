@@ -17,11 +17,38 @@ def free_port():
     return p
 
 
+STRIPE_BASE, STRIPE_WIDTH = 20000, 64
+
+
+def free_ports(n, stripe):
+    """``n`` distinct free ports from stripe ``stripe`` (e.g. the local rank):
+    [20000 + 64*stripe, +64), below the kernel's ephemeral range.  Ranks that
+    start servers at the same moment get disjoint numbers, and no port a
+    server or RCCL later binds to 0 can land on a number handed out here
+    between the probe and the server's own bind (a ``free_port()`` race)."""
+    lo = STRIPE_BASE + STRIPE_WIDTH * int(stripe)
+    out = []
+    for p in range(lo, lo + STRIPE_WIDTH):
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+        except OSError:
+            continue
+        finally:
+            s.close()
+        out.append(p)
+        if len(out) == n:
+            return out
+    raise RuntimeError("no %d free ports in stripe %d [%d, %d)" % (n, stripe, lo, lo + STRIPE_WIDTH))
+
+
 class ServerProcess:
     """The KServe-v2 server in a child process (HIP IPC needs a 2nd process)."""
 
     def __init__(self, device=0, gpu=True, models="", http_port=None, grpc_port=None,
-                 extra_args=(), log_path=None, env=None):
+                 extra_args=(), log_path=None, env=None, port_stripe=None):
+        if port_stripe is not None and not (http_port or grpc_port):
+            http_port, grpc_port = free_ports(2, port_stripe)
         self.http_port = http_port or free_port()
         self.grpc_port = grpc_port or free_port()
         self.device = device
