@@ -44,6 +44,7 @@ def main():
     # well on the 256 CUs (~1.3x one stream's throughput)
     ap.add_argument("--instance-count", type=int, default=4)
     ap.add_argument("--max-queue-delay-us", type=int, default=2000)
+    ap.add_argument("--max-batch-size", type=int, default=0, help="server densenet_onnx max_batch_size (0 = model default 128)")
     ap.add_argument("--preferred", default="128", help="server preferred batch sizes (comma-separated rows; '' = none)")
     # a closed-loop saturation run wants full batches: no early dispatch of partial ones
     ap.add_argument("--idle-dispatch", default="off", choices=["on", "off"],
@@ -77,6 +78,7 @@ def main():
             extra_args=["--instance-count", str(args.instance_count), "--engine", args.engine,
                         "--max-queue-delay-us", str(args.max_queue_delay_us)]
             + (["--preferred-batch-sizes", args.preferred] if args.preferred else [])
+            + (["--max-batch-size", str(args.max_batch_size)] if args.max_batch_size else [])
             + ["--idle-dispatch", args.idle_dispatch],
             log_path=log_path,
             # per-rank port range: N ranks start their servers at once
@@ -213,6 +215,7 @@ def main():
                     "server_instances": args.instance_count,
                     "preferred_batch_rows": args.preferred,
                     "max_queue_delay_us": args.max_queue_delay_us,
+                    "server_max_batch_rows": args.max_batch_size or 128,
                     "idle_dispatch": args.idle_dispatch,
                 },
                 "p50_latency_us": round(percentile_us(all_lat, 50), 1),

@@ -1134,6 +1134,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kr_kernel(Conv3x3Params p) {
 // (valid while 2 * (W + 1) <= 128).  Weights LDS-resident as in K9c.
 constexpr int kRing = 256;
 
+template <int TU>  // tap-loop unroll (1: as K9c; 9: LDS reads of tap t+1 can overlap tap t's MFMAs)
 __global__ void __launch_bounds__(256) conv3x3_ring_kernel(Conv3x3Params p) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Ws = smem;                   // [32][kWsK]
@@ -1189,7 +1190,7 @@ __global__ void __launch_bounds__(256) conv3x3_ring_kernel(Conv3x3Params p) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
     const bool up = h > 0, down = h + 1 < p.H, left = w > 0, right = w + 1 < W, in = m < p.M;
-#pragma unroll 1
+#pragma unroll TU
     for (int tap = 0; tap < 9; ++tap) {
       const int dy = tap / 3 - 1, dx = tap % 3 - 1;
       const bool ok = in && (dy < 0 ? up : dy > 0 ? down : true) && (dx < 0 ? left : dx > 0 ? right : true);
@@ -1648,18 +1649,19 @@ int launch_3x3_kr(Conv3x3Params p, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int TU>
 int launch_3x3_ring(Conv3x3Params p, hipStream_t s) {
   if (p.W > 56) return hipErrorInvalidValue;  // ring reuse needs 2 * (W + 1) <= kTileP
   const int lds = (kN3 * kWsK + (kRing + 1) * kActStride) * 2;
   static int attr = 0;
   if (attr < lds) {
-    int rc = hipFuncSetAttribute((const void*)conv3x3_ring_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    int rc = hipFuncSetAttribute((const void*)conv3x3_ring_kernel<TU>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (rc != hipSuccess) return rc;
     attr = lds;
   }
   p.tiles = (p.M + kTileP - 1) / kTileP;
   const int grid = p.tiles < 256 ? p.tiles : 256;  // one resident block per CU (LDS-limited)
-  hipLaunchKernelGGL(conv3x3_ring_kernel, dim3(grid), dim3(256), lds, s, p);
+  hipLaunchKernelGGL(conv3x3_ring_kernel<TU>, dim3(grid), dim3(256), lds, s, p);
   return hipGetLastError();
 }
 
@@ -1752,15 +1754,13 @@ int tcamd_dn_conv3x3_v(const void* z, int imgs, int H, int W, const void* w, voi
   p.W = W;
   p.ldy = ldy;
   hipStream_t s = (hipStream_t)stream;
-  // heuristic from tools/kbench_densenet.py on MI355X: the LDS-staged kernel
-  // wins once there are enough 128-pixel tiles to fill the CUs; tiny problems
-  // keep the 64-pixel-tile direct-load kernel
-  // (M <= 8192: the 7x7 / 14x14 layers of small batches) the wave-split K9s
-  // (M <= 8192: the 7x7 / 14x14 layers of small batches) the wave-split K9s;
-  // once there are >= 512 tiles (two per CU) the register-weight K9r, whose
-  // 66 KB LDS footprint also lets other streams' kernels share the CU
+  // heuristic from tools/kbench_densenet.py on MI355X: tiny problems
+  // (M <= 8192: the 7x7 / 14x14 layers of small batches) take the wave-split
+  // K9s, and above that the sliding-band K9w with its taps unrolled (bs128 on
+  // MI355X: 56x56 44 us vs 55 K9r / 60 K9c, 28x28 16.9 vs 20.3 / 21.9,
+  // 14x14 6.6 vs 8.2 / 7.3; profiles/r1_kbench_3x3_ring.log)
   if (variant == 0)
-    variant = M <= 8192 ? 70 : (W <= 56 && (M + 127) / 128 >= 512) ? 80 : (W <= 56 && (M + 127) / 128 >= 96) ? 60 : 11;
+    variant = M <= 8192 ? 70 : W <= 56 ? 91 : 11;
   switch (variant) {
     case 10: return launch_3x3<1, 0>(p, s);  // channel-major tap walk
     case 16: return launch_3x3<1, 6>(p, s);   // 6-deep load ring
@@ -1775,7 +1775,9 @@ int tcamd_dn_conv3x3_v(const void* z, int imgs, int H, int W, const void* w, voi
     case 41: return launch_3x3<4, 1>(p, s);
     case 60: return launch_3x3_lds(p, s);     // LDS-staged activations, 32x32x16 MFMA
     case 80: return launch_3x3_kr(p, s);      // K9r: weights in registers, K split over waves
-    case 90: return launch_3x3_ring(p, s);    // K9w: K9c with a sliding band (contiguous tile runs)
+    case 90: return launch_3x3_ring<1>(p, s); // K9w: K9c with a sliding band (contiguous tile runs)
+    case 91: return launch_3x3_ring<9>(p, s); // K9w, taps fully unrolled
+    case 93: return launch_3x3_ring<3>(p, s); // K9w, taps unrolled by 3
     case 70:                                  // K9s: waves split the input channels
       hipLaunchKernelGGL(conv3x3_sk_kernel, dim3((p.M + 31) / 32), dim3(256), 0, s, p);
       return hipGetLastError();

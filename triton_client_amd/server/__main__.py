@@ -25,6 +25,8 @@ def main(argv=None):
                     help="dispatch queued requests at once while every model instance is idle (else wait the delay)")
     ap.add_argument("--preferred-batch-sizes", default="",
                     help="override dynamic_batching.preferred_batch_size of the GPU models (comma-separated)")
+    ap.add_argument("--max-batch-size", type=int, default=0,
+                    help="override densenet_onnx max_batch_size (power of two <= 256; HIP-graph buckets up to it)")
     ap.add_argument("--no-graphs", action="store_true", help="disable HIP graph capture")
     ap.add_argument("--engine", default="fused", choices=["fused", "torch"],
                     help="densenet_onnx engine: fused HIP/MFMA kernels or the torch/MIOpen module")
@@ -46,6 +48,8 @@ def main(argv=None):
             o = {"device": args.device}
             if m.name == "densenet_onnx":
                 o["engine"] = args.engine
+                if args.max_batch_size:
+                    o["max_batch_size"] = args.max_batch_size
             if args.no_graphs:
                 o["use_graphs"] = False
             opts[m.name] = o

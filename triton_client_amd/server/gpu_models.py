@@ -29,7 +29,7 @@ from triton_client_amd.utils import roctx
 from .model_base import Model, TensorSpec
 from .types import DeviceView, OutputTensor, ServerError
 
-BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128)
+BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256)
 
 
 class DensenetOnnx(Model):
@@ -48,12 +48,22 @@ class DensenetOnnx(Model):
     C, H, W = 3, 224, 224
     OUT = 1000
 
-    def __init__(self, version=1, device_id=0, buckets=BUCKETS, use_graphs=True, engine="fused", **kw):
+    def __init__(self, version=1, device_id=0, buckets=BUCKETS, use_graphs=True, engine="fused", max_batch_size=0,
+                 **kw):
         super().__init__(version, **kw)
         if engine not in ("fused", "torch"):
             raise ServerError("unknown densenet engine %r" % engine)
         self.engine = engine
         self.device_id = int(kw.get("device", device_id))
+        if max_batch_size:
+            # option max_batch_size: one HIP-graph bucket per power of two up to
+            # it.  The fused engine's device throughput keeps growing with the
+            # rows per forward: on MI355X (tools/engine_streams_bench.py) ~64k
+            # img/s with 128-row forwards on 3-4 streams, ~70k with 256-row
+            # forwards on 2 streams.
+            if int(max_batch_size) not in buckets:
+                raise ServerError("max_batch_size must be one of %s" % (tuple(buckets),))
+            self.max_batch_size = int(max_batch_size)
         self.buckets = tuple(b for b in buckets if b <= self.max_batch_size)
         self.use_graphs = use_graphs
         self._slots = []
