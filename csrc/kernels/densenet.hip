@@ -296,6 +296,169 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
 }
 
 // ============================================================================
+// K8w: weight-resident, whole-K 1x1 conv for the dense layers with K <= 256
+// (all of block 1, the first layers of block 2: M up to 401k rows at bs128).
+// K8 walks K in 32-wide steps with a barrier per step — 2-8 steps of 8 MFMAs
+// per 64-pixel tile — and re-fetches the weight tile for every pixel tile.
+// Here a persistent block (one per CU: 137 KB LDS at K = 256) stages ALL of
+// W [128][K] once, then walks 64-pixel tiles with the whole K of the next
+// tile's activations in flight in registers (KS x 16 B per thread) while the
+// current tile runs its 8*KS MFMAs from LDS: one barrier per tile.  BN1+ReLU
+// prologue on the way into LDS, BN2-folded bias + ReLU epilogue (as K8).
+// ============================================================================
+constexpr int kOStride = 128 + 8;  // K8w output staging row (272 B: conflict-free b64 writes / b128 reads)
+
+template <int KS>  // K / 32
+__global__ void __launch_bounds__(256) conv1x1_wres_kernel(Conv1x1Params p) {
+  constexpr int K = KS * 32, LDK = K + 8, CPR = K / 8;
+  constexpr int BM = 64, BN = 128, NJ = 4, TM = 2, WN = 64;
+  constexpr int AI = BM * CPR / 256;  // = KS: A chunks per thread per tile
+  constexpr int BI = BN * CPR / 256;  // = 2 * KS
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* sB = smem;                       // [BN][LDK]
+  uint16_t* sA = smem + BN * LDK;            // [2][BM][LDK]
+  uint16_t* sO = sA + 2 * BM * LDK;         // [BM][kOStride] output staging
+  float* sS = reinterpret_cast<float*>(sO + BM * kOStride);
+  float* sT = sS + K;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int n0 = blockIdx.y * BN;
+  const int tiles = (p.M + BM - 1) / BM;
+  for (int k = tid; k < K; k += 256) {
+    sS[k] = p.in_scale[k];
+    sT[k] = p.in_bias[k];
+  }
+  {
+    v4u r[BI];
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int c = tid + i * 256;
+      r[i] = ldg16(p.w + (size_t)(n0 + c / CPR) * p.K + (c % CPR) * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int c = tid + i * 256;
+      *reinterpret_cast<v4u*>(&sB[(c / CPR) * LDK + (c % CPR) * 8]) = r[i];
+    }
+  }
+  v4u ra[AI];
+  auto load_a = [&](int tile) {
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int c = tid + i * 256;
+      const int m = tile * BM + c / CPR;
+      ra[i] = m < p.M ? ldg16(p.x + (size_t)m * p.ldx + (c % CPR) * 8) : v4u{0, 0, 0, 0};
+    }
+  };
+  auto store_a = [&](int buf) {  // BN1 + ReLU prologue (rows past M only feed unstored outputs)
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int c = tid + i * 256;
+      const int kc = (c % CPR) * 8;
+      float f[8], o[8];
+      unpack8(ra[i], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f[e] * sS[kc + e] + sT[kc + e];
+      v4u v = pack8(o);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = relu_pk(v[q]);
+      *reinterpret_cast<v4u*>(&sA[buf * BM * LDK + (c / CPR) * LDK + kc]) = v;
+    }
+  };
+  f32x4 bias0[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int nb = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
+    bias0[j] = p.out_bias ? f32x4{p.out_bias[nb], p.out_bias[nb + 1], p.out_bias[nb + 2], p.out_bias[nb + 3]}
+                          : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  int tile = blockIdx.x;
+  if (tile < tiles) load_a(tile);
+  __syncthreads();  // sS / sT / sB staged
+  if (tile < tiles) store_a(0);
+  __syncthreads();
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  int buf = 0;
+  for (; tile < tiles; tile += gridDim.x) {
+    const int nxt = tile + (int)gridDim.x;
+    if (nxt < tiles) load_a(nxt);
+    f32x4 acc[NJ][TM];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = bias0[j];
+    const uint16_t* a_base = sA + buf * BM * LDK;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 fa[NJ], fb[TM];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        fa[j] = *reinterpret_cast<const bf16x8*>(&sB[(wn * WN + j * 16 + fr) * LDK + ks * 32 + fk]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fb[i] = *reinterpret_cast<const bf16x8*>(&a_base[(wm * 16 * TM + i * 16 + fr) * LDK + ks * 32 + fk]);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = mfma16(fa[j], fb[i], acc[j][i]);
+    }
+    // epilogue through LDS: a lane's accumulators are 4 channels of one pixel
+    // (8 B pieces, 32 B per row per store instruction); staged as the 64 x 128
+    // tile, every output row leaves as one 256-B run (16 lanes x 16 B)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int nb = wn * WN + j * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        v2u o = v2u{pack2(acc[j][i][0], acc[j][i][1]), pack2(acc[j][i][2], acc[j][i][3])};
+        if (p.relu_out) o = v2u{relu_pk(o[0]), relu_pk(o[1])};
+        *reinterpret_cast<v2u*>(&sO[(wm * 16 * TM + i * 16 + fr) * kOStride + nb]) = o;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < BM * 16 / 256; ++q) {
+      const int c = tid + q * 256, r = c >> 4, m = tile * BM + r;
+      if (m < p.M)
+        *reinterpret_cast<v4u*>(p.y + (size_t)m * p.ldy + n0 + (c & 15) * 8) =
+            *reinterpret_cast<const v4u*>(&sO[r * kOStride + (c & 15) * 8]);
+    }
+    if (nxt < tiles) store_a(buf ^ 1);  // that buffer's last reads were before the previous barrier
+    __syncthreads();
+    buf ^= 1;
+  }
+}
+
+template <int KS>
+int launch_1x1_wres(const Conv1x1Params& p, hipStream_t s) {
+  constexpr int LDK = KS * 32 + 8;
+  const int lds = ((128 + 2 * 64) * LDK + 64 * kOStride) * 2 + 2 * KS * 32 * 4;  // sB, 2 x sA, sO, sS/sT
+  static int attr = 0;
+  if (attr < lds) {
+    int rc = hipFuncSetAttribute((const void*)conv1x1_wres_kernel<KS>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (rc != hipSuccess) return rc;
+    attr = lds;
+  }
+  const int tiles = (p.M + 63) / 64;
+  hipLaunchKernelGGL(conv1x1_wres_kernel<KS>, dim3(tiles < 256 ? tiles : 256, p.N / 128), dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
+int launch_1x1_wres_k(const Conv1x1Params& p, hipStream_t s) {
+  switch (p.K / 32) {
+    case 1: return launch_1x1_wres<1>(p, s);
+    case 2: return launch_1x1_wres<2>(p, s);
+    case 3: return launch_1x1_wres<3>(p, s);
+    case 4: return launch_1x1_wres<4>(p, s);
+    case 5: return launch_1x1_wres<5>(p, s);
+    case 6: return launch_1x1_wres<6>(p, s);
+    case 7: return launch_1x1_wres<7>(p, s);
+    case 8: return launch_1x1_wres<8>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// ============================================================================
 // K8p: persistent, software-pipelined 1x1 conv.  Profiling K8 showed every
 // dense-layer 1x1 latency-bound: each block walks K in 32-wide steps with one
 // tile of loads in flight, so a 14x14 layer (K up to 992) waits ~31 global
@@ -1538,7 +1701,15 @@ int launch_1x1_pipe(const Conv1x1Params& p, hipStream_t s) {
 // blocks run (the reduce launch costs ~2 us, so only when it pays).
 template <bool PRO, bool POOL>
 int pick_1x1(const Conv1x1Params& p, int variant, int splits, size_t ws_bytes, hipStream_t s) {
-  if (variant == 0) variant = p.M >= 32768 ? 21 : p.M >= 8192 ? 11 : (p.M > 4096 && !POOL) ? 212 : 12;
+  // measured (tools/kbench_densenet.py, bs128): the 56x56 layers (M >= 196k) run
+  // 10-15% faster on 128-pixel tiles (TM=4) than on 64 (K=224: 80 vs 95 us)
+  if (variant == 0)
+    variant = p.M >= 196608 ? 41 : p.M >= 32768 ? 21 : p.M >= 8192 ? 11 : (p.M > 4096 && !POOL) ? 212 : 12;
+  if (variant == 300) {  // K8w: weight-resident whole-K (K <= 256, BN prologue, no pool / split)
+    if (!PRO || POOL || p.K % 32 || p.K > 256 || p.N % 128) return hipErrorInvalidValue;
+    if (p.ldy % 8 || ((uintptr_t)p.y) % 16) return hipErrorInvalidValue;  // 16-B output rows
+    return launch_1x1_wres_k(p, s);
+  }
   if (variant == 70) {  // K8s: waves split K (needs the BN prologue)
     if (!PRO || p.K % 32) return hipErrorInvalidValue;
     hipLaunchKernelGGL((conv1x1_sk_kernel<POOL>), dim3((p.M + 31) / 32, p.N / 128), dim3(256), 0, s, p);
