@@ -1702,9 +1702,11 @@ int launch_1x1_pipe(const Conv1x1Params& p, hipStream_t s) {
 template <bool PRO, bool POOL>
 int pick_1x1(const Conv1x1Params& p, int variant, int splits, size_t ws_bytes, hipStream_t s) {
   // measured (tools/kbench_densenet.py, bs128): the 56x56 layers (M >= 196k) run
-  // 10-15% faster on 128-pixel tiles (TM=4) than on 64 (K=224: 80 vs 95 us)
+  // 10-15% faster on 128-pixel tiles (TM=4) than on 64 (K=224: 80 vs 95 us);
+  // the 14x14 layers (M = 25k) ~12% faster on 64-pixel tiles than on 32
+  // (K=992: 23.6 vs 27.7 us)
   if (variant == 0)
-    variant = p.M >= 196608 ? 41 : p.M >= 32768 ? 21 : p.M >= 8192 ? 11 : (p.M > 4096 && !POOL) ? 212 : 12;
+    variant = p.M >= 196608 ? 41 : p.M >= 16384 ? 21 : p.M >= 8192 ? 11 : (p.M > 4096 && !POOL) ? 212 : 12;
   if (variant == 300) {  // K8w: weight-resident whole-K (K <= 256, BN prologue, no pool / split)
     if (!PRO || POOL || p.K % 32 || p.K > 256 || p.N % 128) return hipErrorInvalidValue;
     if (p.ldy % 8 || ((uintptr_t)p.y) % 16) return hipErrorInvalidValue;  // 16-B output rows
