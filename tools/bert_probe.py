@@ -1,0 +1,45 @@
+"""Time one BERT-large (seq 384) forward per batch size on the GPU; run under
+``rocprofv3 --kernel-trace --stats`` for the per-kernel split.
+
+  python tools/bert_probe.py --batch 64 --iters 10
+"""
+
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from triton_client_amd.models import bert  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, nargs="+", default=[64])
+    ap.add_argument("--seq", type=int, default=384)
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    model = bert.build(device=dev)
+    for b in a.batch:
+        ids = torch.randint(0, bert.VOCAB, (b, a.seq), device=dev)
+        mask = torch.ones(b, a.seq, device=dev, dtype=torch.int64)
+        tt = torch.zeros(b, a.seq, device=dev, dtype=torch.int64)
+        with torch.no_grad():
+            for _ in range(2):
+                model(ids, mask, tt)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.iters):
+                model(ids, mask, tt)
+            torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / a.iters
+        tf = bert.flops_per_sequence(a.seq) * b / dt / 1e12
+        print({"batch": b, "ms": round(dt * 1e3, 3), "seq_per_s": round(b / dt, 1), "tflops": round(tf, 1)}, flush=True)
+
+
+if __name__ == "__main__":
+    main()

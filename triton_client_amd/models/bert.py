@@ -9,11 +9,15 @@ on the box.
 Compute layout for MI355X: bf16 everywhere, fused QKV projection (one
 [3H, H] GEMM per layer instead of three), attention through
 ``F.scaled_dot_product_attention`` with an additive key-padding mask (the
-fused attention kernels of torch-ROCm), plain GEMMs on hipBLASLt.  The
-serving wrapper captures one HIP graph per batch bucket.
+fused attention kernels of torch-ROCm), plain GEMMs on hipBLASLt, the GELU
+in the FFN-up GEMM's epilogue (``torch._addmm_activation``) and every
+residual add + LayerNorm as ONE hand-written HIP kernel (K11,
+csrc/kernels/bert.hip).  The serving wrapper captures one HIP graph per
+batch bucket.
 """
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -26,6 +30,31 @@ HEADS = 16
 FFN = 4096
 MAX_POS = 512
 TYPES = 2
+
+
+# fused paths on the GPU (bf16 CUDA tensors); TC_BERT_FUSED=0 runs plain torch ops
+FUSED = os.environ.get("TC_BERT_FUSED", "1") != "0"
+
+
+def _add_ln(x, y, ln):
+    """LayerNorm(x + y): K11 on the GPU, torch ops elsewhere."""
+    if FUSED and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and y.is_contiguous():
+        from triton_client_amd.ops import hip
+
+        out = torch.empty_like(x)
+        hip.add_layernorm(x.data_ptr(), y.data_ptr(), ln.weight.data_ptr(), ln.bias.data_ptr(), out.data_ptr(),
+                          x.numel() // x.shape[-1], x.shape[-1], ln.eps,
+                          stream=torch.cuda.current_stream(x.device).cuda_stream)
+        return out
+    return ln(x + y)
+
+
+def _linear_gelu(x, lin):
+    """gelu(lin(x)); on the GPU the GELU runs in the GEMM epilogue."""
+    if FUSED and x.is_cuda:
+        y = torch._addmm_activation(lin.bias, x.reshape(-1, x.shape[-1]), lin.weight.t(), use_gelu=True)
+        return y.view(*x.shape[:-1], y.shape[-1])
+    return F.gelu(lin(x))
 
 
 class _Layer(nn.Module):
@@ -42,8 +71,8 @@ class _Layer(nn.Module):
         b, s, _ = x.shape
         q, k, v = self.qkv(x).view(b, s, 3, HEADS, HIDDEN // HEADS).permute(2, 0, 3, 1, 4)
         a = F.scaled_dot_product_attention(q, k, v, attn_mask=bias)
-        x = self.ln1(x + self.out(a.transpose(1, 2).reshape(b, s, HIDDEN)))
-        return self.ln2(x + self.ffn2(F.gelu(self.ffn1(x))))
+        x = _add_ln(x, self.out(a.transpose(1, 2).reshape(b, s, HIDDEN)), self.ln1)
+        return _add_ln(x, self.ffn2(_linear_gelu(x, self.ffn1)), self.ln2)
 
 
 class BertLargeQA(nn.Module):

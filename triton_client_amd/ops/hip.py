@@ -159,6 +159,11 @@ _SIGS = {
          ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "tcamd_add_layernorm": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+         ctypes.c_int, ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_pack_bytes_workspace": ([ctypes.c_uint64], ctypes.c_uint64),
     "tcamd_pack_bytes": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
@@ -481,6 +486,11 @@ def dn_stem_fused(srcs, x, w, bias, y, imgs, ldy, stream=None):
     ``srcs``: device array of per-image fp32 NCHW pointers (or None with ``x`` = bf16 NHWC batch);
     ``w``: [64][7][8][4] bf16 packed weights."""
     _check(_load().tcamd_dn_stem_fused(_vp(srcs), _vp(x), w, bias, y, imgs, ldy, _vp(stream)), "dn_stem_fused")
+
+
+def add_layernorm(x, y, gamma, beta, out, rows, H, eps, stream=None):
+    """K11: out = LayerNorm(x + y) * gamma + beta over ``rows`` rows of H bf16 (H in 512/1024/2048/4096)."""
+    _check(_load().tcamd_add_layernorm(x, y, gamma, beta, out, rows, H, float(eps), _vp(stream)), "add_layernorm")
 
 
 def dn_head_pool(x, scale, bias, out, imgs, HW, C, stream=None):
