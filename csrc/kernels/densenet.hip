@@ -1377,6 +1377,109 @@ __global__ void __launch_bounds__(256) conv3x3_ring_kernel(Conv3x3Params p) {
 }
 
 // ============================================================================
+// K9w2: K9w with 8 waves (2 per SIMD) instead of 4.  K9w keeps one wave per
+// SIMD, so every LDS read an MFMA waits on and every barrier is exposed.
+// Here the two waves of a SIMD share one 32-pixel subtile and split its nine
+// taps (0-4 / 5-8); the second half's accumulators are added through a 16 KB
+// LDS scratch (weights 74 KB + ring 70 KB + scratch 16 KB = 157 KB).
+// ============================================================================
+constexpr int kRed2Floats = 4 * 64 * 16;  // [subtile][lane][16]
+
+__global__ void __launch_bounds__(512) conv3x3_ring2_kernel(Conv3x3Params p) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Ws = smem;                                                 // [32][kWsK]
+  uint16_t* As = smem + kN3 * kWsK;                                    // [kRing + 1][kActStride]
+  float* red = reinterpret_cast<float*>(As + (kRing + 1) * kActStride);  // [4][64][16]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sub = wave & 3, half = wave >> 2;
+  if (tid < 256) stage_weights(p.w, Ws, tid);
+  if (tid < kActStride / 8) *reinterpret_cast<v4u*>(&As[kRing * kActStride + tid * 8]) = v4u{0, 0, 0, 0};
+  const int W = p.W, HW = p.H * p.W;
+  const int halo = W + 1;
+  const int per = p.tiles / (int)gridDim.x, extra = p.tiles % (int)gridDim.x;
+  const int t0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
+  const int t1 = t0 + per + ((int)blockIdx.x < extra ? 1 : 0);
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.z, (short)0,
+                                                      (int)((size_t)p.M * kC3 * 2), 0x00020000);
+  auto fetch = [&](int first, int nrows, int c) -> v4u {
+    const int pix = first + (c >> 4);
+    const bool ok = c < nrows * 16 && pix >= 0 && pix < p.M;
+    return __builtin_amdgcn_raw_buffer_load_b128(rsrc, ok ? (pix * kC3 + (c & 15) * 8) * 2 : 0x40000000, 0, 0);
+  };
+  auto put = [&](int first, int nrows, int c, v4u v) {
+    if (c < nrows * 16)
+      *reinterpret_cast<v4u*>(&As[((first + (c >> 4)) & (kRing - 1)) * kActStride + (c & 15) * 8]) = v;
+  };
+  constexpr int CPT0 = ((kTileP + 2 * 57) * 16 + 511) / 512;  // first band: 8 chunks per thread
+  constexpr int CPT = kTileP * 16 / 512;                       // a step's new rows: 4
+  if (t0 < t1) {
+    const int first = t0 * kTileP - halo, n = kTileP + 2 * halo;
+    v4u st0[CPT0];
+#pragma unroll
+    for (int i = 0; i < CPT0; ++i) st0[i] = fetch(first, n, tid + i * 512);
+#pragma unroll
+    for (int i = 0; i < CPT0; ++i) put(first, n, tid + i * 512, st0[i]);
+  }
+  v4u st[CPT];
+  const int col = lane & 31, kh = 8 * (lane >> 5);
+  for (int tile = t0; tile < t1; ++tile) {
+    __syncthreads();  // previous tile's LDS reads (ring and scratch) done
+    if (tile > t0) {
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) put(tile * kTileP + halo, kTileP, tid + i * 512, st[i]);
+    }
+    __syncthreads();
+    if (tile + 1 < t1) {
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) st[i] = fetch((tile + 1) * kTileP + halo, kTileP, tid + i * 512);
+    }
+    const int m = tile * kTileP + sub * 32 + col;
+    const int mm = m < p.M ? m : 0;
+    const int img = mm / HW, rr = mm - img * HW;
+    const int h = rr / W, w = rr - h * W;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    const bool up = h > 0, down = h + 1 < p.H, left = w > 0, right = w + 1 < W, in = m < p.M;
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const int tap = half * 5 + t;  // wave-uniform
+      if (tap < 9) {
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        const bool ok = in && (dy < 0 ? up : dy > 0 ? down : true) && (dx < 0 ? left : dx > 0 ? right : true);
+        const uint16_t* arow = &As[(ok ? ((m + dy * W + dx) & (kRing - 1)) : kRing) * kActStride + kh];
+        const uint16_t* wrow = &Ws[col * kWsK + tap * kC3 + kh];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const v4u b = *reinterpret_cast<const v4u*>(arow + c * 16);
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(wrow + c * 16);
+          acc = mfma32(a, as_frag(b), acc);
+        }
+      }
+    }
+    f32x4* rp = reinterpret_cast<f32x4*>(red + (sub * 64 + lane) * 16);
+    if (half) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rp[q] = f32x4{acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
+    }
+    __syncthreads();
+    if (!half && m < p.M) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 o = rp[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[4 * q + e] += o[e];
+      }
+      uint16_t* yp = p.y + (size_t)m * p.ldy + 4 * (lane >> 5);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<v2u*>(yp + 8 * g) =
+            v2u{pack2(acc[4 * g], acc[4 * g + 1]), pack2(acc[4 * g + 2], acc[4 * g + 3])};
+    }
+  }
+}
+
+// ============================================================================
 // K10a: stem epilogue  y = relu(maxpool3x3/2(x) + b)  (bias+ReLU commute with max)
 // ============================================================================
 // x: [imgs][H][W][C] bf16 (conv0 output without bias), y: [imgs][Ho][Wo] rows of ldy.
@@ -1822,6 +1925,21 @@ int launch_3x3_kr(Conv3x3Params p, hipStream_t s) {
   return hipGetLastError();
 }
 
+int launch_3x3_ring2(Conv3x3Params p, hipStream_t s) {
+  if (p.W > 56) return hipErrorInvalidValue;
+  const int lds = (kN3 * kWsK + (kRing + 1) * kActStride) * 2 + kRed2Floats * 4;
+  static int attr = 0;
+  if (attr < lds) {
+    int rc = hipFuncSetAttribute((const void*)conv3x3_ring2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (rc != hipSuccess) return rc;
+    attr = lds;
+  }
+  p.tiles = (p.M + kTileP - 1) / kTileP;
+  const int grid = p.tiles < 256 ? p.tiles : 256;
+  hipLaunchKernelGGL(conv3x3_ring2_kernel, dim3(grid), dim3(512), lds, s, p);
+  return hipGetLastError();
+}
+
 template <int TU>
 int launch_3x3_ring(Conv3x3Params p, hipStream_t s) {
   if (p.W > 56) return hipErrorInvalidValue;  // ring reuse needs 2 * (W + 1) <= kTileP
@@ -1929,11 +2047,12 @@ int tcamd_dn_conv3x3_v(const void* z, int imgs, int H, int W, const void* w, voi
   hipStream_t s = (hipStream_t)stream;
   // heuristic from tools/kbench_densenet.py on MI355X: tiny problems
   // (M <= 8192: the 7x7 / 14x14 layers of small batches) take the wave-split
-  // K9s, and above that the sliding-band K9w with its taps unrolled (bs128 on
-  // MI355X: 56x56 44 us vs 55 K9r / 60 K9c, 28x28 16.9 vs 20.3 / 21.9,
-  // 14x14 6.6 vs 8.2 / 7.3; profiles/r1_kbench_3x3_ring.log)
+  // K9s, and above that the sliding-band K9w2 (8 waves, taps split between
+  // SIMD-mates; bs128 on MI355X: 56x56 43 us vs 45 K9w / 55 K9r / 60 K9c,
+  // 28x28 15.8 vs 16.7 / 20.3 / 21.9, 14x14 6.3 vs 6.6 / 8.2 / 7.3;
+  // profiles/r1_kbench_3x3_ring.log)
   if (variant == 0)
-    variant = M <= 8192 ? 70 : W <= 56 ? 91 : 11;
+    variant = M <= 8192 ? 70 : W <= 56 ? 92 : 11;
   switch (variant) {
     case 10: return launch_3x3<1, 0>(p, s);  // channel-major tap walk
     case 16: return launch_3x3<1, 6>(p, s);   // 6-deep load ring
@@ -1951,6 +2070,7 @@ int tcamd_dn_conv3x3_v(const void* z, int imgs, int H, int W, const void* w, voi
     case 90: return launch_3x3_ring<1>(p, s); // K9w: K9c with a sliding band (contiguous tile runs)
     case 91: return launch_3x3_ring<9>(p, s); // K9w, taps fully unrolled
     case 93: return launch_3x3_ring<3>(p, s); // K9w, taps unrolled by 3
+    case 92: return launch_3x3_ring2(p, s);   // K9w2: 8 waves, taps split between SIMD-mates
     case 70:                                  // K9s: waves split the input channels
       hipLaunchKernelGGL(conv3x3_sk_kernel, dim3((p.M + 31) / 32), dim3(256), 0, s, p);
       return hipGetLastError();

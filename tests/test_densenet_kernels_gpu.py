@@ -128,7 +128,7 @@ def test_conv1x1_transition_pool(imgs, H, C, N):
     assert (y[:, N:] == 0).all()
 
 
-@pytest.mark.parametrize("variant", [0, 10, 11, 13, 16, 19, 21, 41, 51, 52, 60, 70, 80, 90, 91, 93])
+@pytest.mark.parametrize("variant", [0, 10, 11, 13, 16, 19, 21, 41, 51, 52, 60, 70, 80, 90, 91, 92, 93])
 @pytest.mark.parametrize("imgs,H", [(1, 7), (3, 14), (8, 56), (48, 56), (5, 28)])
 def test_conv3x3(imgs, H, variant):
     _need_gpu()

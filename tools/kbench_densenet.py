@@ -15,7 +15,7 @@ import torch
 from triton_client_amd.ops import hip
 
 V1 = (11, 12, 21, 22, 41, 211, 212, 221, 222, 300)
-V3 = (0, 60, 70, 80, 90, 91, 93)
+V3 = (0, 60, 70, 80, 90, 91, 92, 93)
 
 
 def cs():
