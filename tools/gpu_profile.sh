@@ -13,7 +13,8 @@ TRACE="--kernel-trace --stats"
 if [ "${MARKERS:-0}" = 1 ]; then export TC_ROCTX=1; TRACE="$TRACE --marker-trace"; fi
 timeout -k 10 900 rocprofv3 $TRACE --output-format csv -d gpurun_out/prof -o server -- \
   python3 -m triton_client_amd.server --http-port 18000 --grpc-port 18001 --gpu --models densenet_onnx \
-  --instance-count 3 --preferred-batch-sizes 128 --max-queue-delay-us 2000 > gpurun_out/prof_server.log 2>&1 &
+  --instance-count ${INSTANCES:-4} --preferred-batch-sizes 128 --max-queue-delay-us 2000 --idle-dispatch off \
+  > gpurun_out/prof_server.log 2>&1 &
 PROF_PID=$!
 timeout -k 10 600 python3 bench.py --server-url 127.0.0.1:18001 --http-url 127.0.0.1:18000 "$@" \
   > gpurun_out/prof_bench.log 2>&1
