@@ -18,7 +18,10 @@
 //    the prologue, 4x fewer GEMM rows;
 //  * K9 conv3x3 (128->32, pad 1): implicit GEMM, the whole 73 KB weight
 //    tensor resident in LDS for a persistent block, activations fetched
-//    with bounds-checked buffer loads (out-of-image taps read as 0);
+//    with bounds-checked buffer loads (out-of-image taps read as 0); the
+//    default for M > 8192 is K9w2: the activation band lives in a 256-row
+//    LDS ring sliding over a contiguous run of tiles (128 new rows per
+//    tile) and 8 waves, two per SIMD, split the nine taps;
 //  * K10 stem epilogue (bias+ReLU+3x3/2 max-pool) and head (BN+ReLU+global
 //    avg-pool).
 //
