@@ -66,3 +66,20 @@ def test_bert_fused_layers_match_torch_ops():
     for got, want in ((s_fused, s_ref), (e_fused, e_ref)):
         err = (got.float() - want).norm() / want.norm()
         assert err.item() < 5e-2, err.item()
+
+
+def test_bert_dense_path_matches_masked_when_no_padding():
+    """dense=True (attention without the key-padding bias) is what the server
+    replays for batches with no padding: same logits as the masked graph."""
+    _need_gpu()
+    from triton_client_amd.models import bert
+
+    m = bert.build(device=DEV, layers=2)
+    ids = torch.randint(0, bert.VOCAB, (4, 384), device=DEV)
+    mask = torch.ones(4, 384, device=DEV, dtype=torch.int64)
+    tt = torch.zeros(4, 384, device=DEV, dtype=torch.int64)
+    with torch.no_grad():
+        a = m(ids, mask, tt)
+        b = m(ids, mask, tt, dense=True)
+    for x, y in zip(a, b):
+        assert ((x - y).norm() / x.norm()).item() < 2e-2

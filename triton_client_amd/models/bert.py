@@ -85,12 +85,15 @@ class BertLargeQA(nn.Module):
         self.layers = nn.ModuleList(_Layer() for _ in range(layers))
         self.qa = nn.Linear(HIDDEN, 2)
 
-    def forward(self, input_ids, attention_mask, token_type_ids):
+    def forward(self, input_ids, attention_mask, token_type_ids, dense=False):
+        """dense=True: the caller guarantees attention_mask is all ones, so
+        attention runs without a bias (torch-ROCm's unmasked fused kernel is
+        ~1.8x faster at bs64 x 384, tools/attn_probe.py)."""
         b, s = input_ids.shape
         pos = torch.arange(s, device=input_ids.device)
         x = self.ln(self.word(input_ids) + self.pos(pos)[None] + self.tok_type(token_type_ids))
         # additive key-padding mask [b, 1, 1, s] in the compute dtype
-        bias = ((1.0 - attention_mask[:, None, None, :].to(x.dtype)) * -10000.0).to(x.dtype)
+        bias = None if dense else ((1.0 - attention_mask[:, None, None, :].to(x.dtype)) * -10000.0).to(x.dtype)
         for layer in self.layers:
             x = layer(x, bias)
         logits = self.qa(x).float()
