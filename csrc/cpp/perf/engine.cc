@@ -360,6 +360,18 @@ void LoadEngine::RateLoop(double rate, uint64_t gen)
     else if (o_.distribution == "poisson") gap = static_cast<uint64_t>(expo(rng) * 1e9);
     else gap = static_cast<uint64_t>(1e9 / rate);
     next += gap;
+    // Open loop: send times do not wait for responses.  If the scheduler itself
+    // fell behind (descheduled, CPU-starved host) by more than a bounded lag,
+    // drop the backlog instead of bursting it into the next window, which
+    // would report a rate the schedule never asked for.
+    {
+      const uint64_t now = NowNs();
+      const uint64_t max_lag = std::max<uint64_t>(20ull * 1000000ull, 4 * gap);
+      if (now > next + max_lag) {
+        delayed_.fetch_add(1);
+        next = now;
+      }
+    }
     // sleep until the scheduled send time (not blocked by responses)
     while (true) {
       const uint64_t now = NowNs();

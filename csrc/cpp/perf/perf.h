@@ -282,6 +282,7 @@ class LoadEngine {
   std::thread rate_thread_;
   std::vector<std::thread> sync_threads_;
   std::atomic<uint64_t> rate_gen_{0};
+  std::atomic<uint64_t> delayed_{0};  // rate mode: schedule slips that dropped the backlog
   uint64_t next_seq_ = 0;
   std::string first_error_;
   std::vector<uint64_t> intervals_ns_;

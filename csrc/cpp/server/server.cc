@@ -119,6 +119,7 @@ struct PendingReq {
   std::vector<std::string> host_out;  // host output buffers (non-shm)
   std::string body;                   // request message; raw inputs point into it
   std::vector<std::pair<int, size_t>> host_in_off;  // (input index, offset of its bytes in body)
+  std::vector<std::shared_ptr<int>> pins;            // shm regions this request reads/writes
   uint64_t t_arrive = 0;
 };
 
@@ -167,7 +168,18 @@ static size_t DtypeSize(const std::string& dt)
 struct ShmEntry {
   uint64_t ptr = 0, bytes = 0;
   int device = 0;
+  // one reference per queued/executing request that points into the region;
+  // unregister waits for the requests to drop theirs before the caller unmaps
+  std::shared_ptr<int> pin = std::make_shared<int>(0);
 };
+
+// [off, off + len) inside a region of `size` bytes, with no signed overflow:
+// a negative byte size or offset is rejected before any arithmetic.
+static bool ShmRangeOk(int64_t off, int64_t len, uint64_t size)
+{
+  if (off < 0 || len < 0) return false;
+  return static_cast<uint64_t>(off) <= size && static_cast<uint64_t>(len) <= size - static_cast<uint64_t>(off);
+}
 
 // ---------------------------------------------------------------------------
 class Loop {
@@ -213,6 +225,7 @@ class Server {
 
   // transport hooks (loop thread)
   void OnHttpData(Conn* c);
+  void RejectTooLarge(Conn* c);
   void OnRequestComplete(Conn* c, Stream* st);
   void OnStreamMessage(Conn* c, Stream* st, std::string&& msg);
   void OnStreamEnd(Conn* c, Stream* st);
@@ -805,6 +818,7 @@ std::string HttpStatusLine(int code)
     case 400: return "HTTP/1.1 400 Bad Request\r\n";
     case 500: return "HTTP/1.1 500 Internal Server Error\r\n";
     case 502: return "HTTP/1.1 502 Bad Gateway\r\n";
+    case 413: return "HTTP/1.1 413 Payload Too Large\r\n";
     case 503: return "HTTP/1.1 503 Service Unavailable\r\n";
     default: return "HTTP/1.1 " + std::to_string(code) + " Error\r\n";
   }
@@ -864,6 +878,12 @@ int ParseHead(const std::string& in, HttpHead* h)
 }
 
 // Decode a chunked body starting at `from`; 0 = need more, -1 = malformed, else bytes consumed.
+// Largest request body tcserve buffers (Content-Length or de-chunked); larger
+// requests get 413 and the connection is closed.  KServe gRPC messages are
+// capped at INT32_MAX too (reference src/c++/library/common.h:53).
+constexpr uint64_t kMaxHttpBody = 0x7fffffffull;
+
+// returns bytes consumed, 0 = need more input, -1 = malformed, -2 = too large
 long DecodeChunked(const std::string& in, size_t from, std::string* body)
 {
   size_t pos = from;
@@ -880,7 +900,8 @@ long DecodeChunked(const std::string& in, size_t from, std::string* body)
       if (fin == std::string::npos) return 0;
       return static_cast<long>(fin + 2 - from);
     }
-    if (in.size() < pos + n + 2) return 0;
+    if (n > kMaxHttpBody || body->size() + n > kMaxHttpBody) return -2;
+    if (in.size() < pos || n + 2 > in.size() - pos) return 0;
     body->append(in, pos, n);
     pos += n + 2;
   }
@@ -909,6 +930,15 @@ bool InferTarget(const std::string& target, std::string* model, std::string* ver
 
 }  // namespace
 
+void Server::RejectTooLarge(Conn* c)
+{
+  const uint64_t seq = c->req_seq++;
+  c->close_after = true;
+  c->hin.clear();
+  PostHttp(c->loop, c->id, seq, HttpError(413, "request body exceeds " + std::to_string(kMaxHttpBody) + " bytes", true),
+           true);
+}
+
 void Server::OnHttpData(Conn* c)
 {
   while (!c->hin.empty() && !c->close_after) {
@@ -927,6 +957,7 @@ void Server::OnHttpData(Conn* c)
     if (te && Lower(*te).find("chunked") != std::string::npos) {
       const long n = DecodeChunked(c->hin, h.head_len, &body);
       if (n == 0) return;
+      if (n == -2) return RejectTooLarge(c);
       if (n < 0) {
         c->closing = true;
         return;
@@ -934,7 +965,8 @@ void Server::OnHttpData(Conn* c)
       consumed += static_cast<size_t>(n);
       rebuilt = true;  // relay with Content-Length instead of chunks
     } else if (cl) {
-      const size_t n = strtoull(cl->c_str(), nullptr, 10);
+      const uint64_t n = strtoull(cl->c_str(), nullptr, 10);
+      if (n > kMaxHttpBody) return RejectTooLarge(c);
       if (c->hin.size() < h.head_len + n) return;
       body.assign(c->hin, h.head_len, n);
       consumed += n;
@@ -1025,6 +1057,7 @@ bool Server::TryNativeHttp(Conn* c, uint64_t seq, bool close, const std::string&
     }
     return -1;
   };
+  std::vector<bool> seen(m->inputs.size(), false);
   for (const js::Value& t : inputs->Elements()) {
     const js::Value* nm = t.Find("name");
     const js::Value* dt = t.Find("datatype");
@@ -1034,6 +1067,8 @@ bool Server::TryNativeHttp(Conn* c, uint64_t seq, bool close, const std::string&
     for (size_t k = 0; k < m->inputs.size(); ++k)
       if (m->inputs[k].name == nm->AsString()) idx = static_cast<int>(k);
     if (idx < 0) return false;
+    if (seen[idx]) return fail("input '" + nm->AsString() + "' is specified more than once");
+    seen[idx] = true;
     const TensorDef& d = m->inputs[idx];
     if (dt->AsString() != d.dtype) return false;
     if (shape->Size() != d.dims.size() + (m->max_batch > 0 ? 1 : 0)) return false;
@@ -1073,11 +1108,12 @@ bool Server::TryNativeHttp(Conn* c, uint64_t seq, bool close, const std::string&
       ShmEntry e;
       const int kind = lookup(region, &e);
       if (kind < 0) return fail("Unable to find shared memory region: '" + region + "'");
-      if (roff < 0 || static_cast<uint64_t>(roff + rbytes) > e.bytes)
+      if (!ShmRangeOk(roff, rbytes, e.bytes))
         return fail("Invalid offset + byte size for shared memory region: '" + region + "'");
       if (static_cast<uint64_t>(rbytes) < need)
         return fail("input '" + d.name + "' shared memory region is smaller than the tensor");
       ref = tcserve_ref{kind, e.device, e.ptr + roff, need};
+      pr->pins.push_back(e.pin);
     } else {
       if (bsize < 0) return false;
       if (static_cast<uint64_t>(bsize) != need) return fail("unexpected byte size for input '" + d.name + "'");
@@ -1131,12 +1167,13 @@ bool Server::TryNativeHttp(Conn* c, uint64_t seq, bool close, const std::string&
         ShmEntry e;
         const int kind = lookup(region, &e);
         if (kind < 0) return fail("Unable to find shared memory region: '" + region + "'");
-        if (roff < 0 || static_cast<uint64_t>(roff + rbytes) > e.bytes)
+        if (!ShmRangeOk(roff, rbytes, e.bytes))
           return fail("Invalid offset + byte size for shared memory region: '" + region + "'");
         if (static_cast<uint64_t>(rbytes) < need)
           return fail("shared memory size specified with the request for output '" + m->outputs[idx].name + "' (" +
                       std::to_string(rbytes) + " bytes) should be at least " + std::to_string(need) + " bytes");
         pr->out[idx] = tcserve_ref{kind, e.device, e.ptr + roff, need};
+        pr->pins.push_back(e.pin);
         pr->out_shm[idx] = true;
         pr->out_region[idx] = region;
         pr->out_region_bytes[idx] = rbytes;
@@ -1524,12 +1561,15 @@ bool Server::TryNative(Conn* c, Stream* st, const char* msg, size_t len, std::st
     m->fail.ns += NowNs() - pr->t_arrive;
     return true;
   };
+  std::vector<bool> seen(m->inputs.size(), false);
   for (int i = 0; i < req.inputs_size(); ++i) {
     const auto& t = req.inputs(i);
     int idx = -1;
     for (size_t k = 0; k < m->inputs.size(); ++k)
       if (m->inputs[k].name == t.name()) idx = static_cast<int>(k);
     if (idx < 0) return false;
+    if (seen[idx]) return fail("input '" + t.name() + "' is specified more than once");
+    seen[idx] = true;
     const TensorDef& d = m->inputs[idx];
     if (t.datatype() != d.dtype || t.has_contents()) return false;
     const auto& shape = t.shape();
@@ -1576,13 +1616,14 @@ bool Server::TryNative(Conn* c, Stream* st, const char* msg, size_t len, std::st
         }
       }
       if (kind < 0) return fail("Unable to find shared memory region: '" + region + "'");
-      if (roff < 0 || static_cast<uint64_t>(roff + rbytes) > e.bytes)
+      if (!ShmRangeOk(roff, rbytes, e.bytes))
         return fail("Invalid offset + byte size for shared memory region: '" + region + "'");
       if (static_cast<uint64_t>(rbytes) < need)
         return fail("input '" + d.name + "' shared memory region is smaller than the tensor");
       ref.kind = kind;
       ref.device = e.device;
       ref.ptr = e.ptr + roff;
+      pr->pins.push_back(e.pin);
       ref.bytes = need;
     } else {
       if (raw_idx >= static_cast<int>(raws.size())) return fail("input '" + d.name + "' has no data");
@@ -1642,12 +1683,13 @@ bool Server::TryNative(Conn* c, Stream* st, const char* msg, size_t len, std::st
         }
       }
       if (kind < 0) return fail("Unable to find shared memory region: '" + region + "'");
-      if (roff < 0 || static_cast<uint64_t>(roff + rbytes) > e.bytes)
+      if (!ShmRangeOk(roff, rbytes, e.bytes))
         return fail("Invalid offset + byte size for shared memory region: '" + region + "'");
       if (static_cast<uint64_t>(rbytes) < need)
         return fail("shared memory size specified with the request for output '" + m->outputs[idx].name + "' (" +
                     std::to_string(rbytes) + " bytes) should be at least " + std::to_string(need) + " bytes");
       pr->out[idx] = tcserve_ref{kind, e.device, e.ptr + roff, need};
+      pr->pins.push_back(e.pin);
       pr->out_shm[idx] = true;
       pr->out_region[idx] = region;
       pr->out_region_bytes[idx] = rbytes;
@@ -1884,9 +1926,27 @@ void Server::ShmAdd(int kind, const std::string& name, const ShmEntry& e)
 
 void Server::ShmRemove(int kind, const std::string& name)
 {
-  std::lock_guard<std::mutex> lk(shm_mu_);
-  if (name.empty()) shm_[kind].clear();
-  else shm_[kind].erase(name);
+  // Take the entries out of the map (no new request can pin them), then wait
+  // until every queued or executing request that pinned one has finished, so
+  // the caller may unmap / hipIpcCloseMemHandle right after this returns.
+  std::vector<std::shared_ptr<int>> pins;
+  {
+    std::lock_guard<std::mutex> lk(shm_mu_);
+    if (name.empty()) {
+      for (auto& kv : shm_[kind]) pins.push_back(kv.second.pin);
+      shm_[kind].clear();
+    } else {
+      auto it = shm_[kind].find(name);
+      if (it != shm_[kind].end()) {
+        pins.push_back(it->second.pin);
+        shm_[kind].erase(it);
+      }
+    }
+  }
+  const uint64_t deadline = NowNs() + 60ull * 1000000000ull;
+  for (auto& p : pins) {
+    while (p.use_count() > 1 && NowNs() < deadline) std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
 }
 
 }  // namespace tcserve

@@ -365,3 +365,106 @@ def test_http_chunked_upload_is_decoded_and_relayed(cpu_server):
         data += chunk
     s.close()
     assert data.startswith(b"HTTP/1.1 200"), data[:200]
+
+
+def test_shm_negative_size_and_huge_offset_rejected(cpu_server):
+    """A negative shared_memory_byte_size must not slip past the bounds check
+    (offset + size overflow) on either the gRPC or the HTTP fast path."""
+    g = grpcclient.InferenceServerClient(cpu_server.grpc_url)
+    h = httpclient.InferenceServerClient(cpu_server.http_url)
+    region = shm.create_shared_memory_region("neg_in", "/neg_in_native", 128)
+    try:
+        g.register_system_shared_memory("neg_in", "/neg_in_native", 128)
+        a = np.zeros((1, 16), np.int32)
+        for off, size in ((128, -1), (2 ** 62, -(2 ** 62)), (-64, 128), (64, 2 ** 63 - 1)):
+            for mod, cli in ((grpcclient, g), (httpclient, h)):
+                i0 = mod.InferInput("INPUT0", [1, 16], "INT32")
+                i0.set_shared_memory("neg_in", size, offset=off)
+                i1 = mod.InferInput("INPUT1", [1, 16], "INT32")
+                i1.set_data_from_numpy(a)
+                with pytest.raises(InferenceServerException, match="(?i)invalid offset|smaller|byte size"):
+                    cli.infer("add_sub_batched", [i0, i1])
+                o = mod.InferRequestedOutput("OUTPUT0")
+                o.set_shared_memory("neg_in", size, offset=off)
+                ok = _inputs(a, a) if mod is grpcclient else _http_inputs(a, a)
+                with pytest.raises(InferenceServerException, match="(?i)invalid offset|should be at least|byte size"):
+                    cli.infer("add_sub_batched", ok, outputs=[o])
+        assert g.is_server_live()
+    finally:
+        g.unregister_system_shared_memory()
+        shm.destroy_shared_memory_region(region)
+
+
+def test_duplicate_input_rejected_on_fast_path(cpu_server):
+    g = grpcclient.InferenceServerClient(cpu_server.grpc_url)
+    h = httpclient.InferenceServerClient(cpu_server.http_url)
+    a = np.ones((1, 16), np.int32)
+    dup = _inputs(a, a)
+    dup[1] = grpcclient.InferInput("INPUT0", [1, 16], "INT32")
+    dup[1].set_data_from_numpy(a)
+    with pytest.raises(InferenceServerException, match="more than once"):
+        g.infer("add_sub_batched", dup)
+    hd = _http_inputs(a, a)
+    hd[1] = httpclient.InferInput("INPUT0", [1, 16], "INT32")
+    hd[1].set_data_from_numpy(a)
+    with pytest.raises(InferenceServerException, match="more than once"):
+        h.infer("add_sub_batched", hd)
+    assert g.is_server_live()
+
+
+def test_unregister_waits_for_inflight_request(cpu_server):
+    """Unregistering a region while a native request that writes into it is
+    executing must not unmap it under the request: the unregister returns
+    only once the request is done, and the output landed."""
+    import threading
+    import time
+
+    from triton_client_amd.server.cpu_models import AddSubBatched
+
+    g = grpcclient.InferenceServerClient(cpu_server.grpc_url)
+    out = shm.create_shared_memory_region("inflight_out", "/inflight_out", 64)
+    AddSubBatched.native_delay_s = 0.6
+    try:
+        g.register_system_shared_memory("inflight_out", "/inflight_out", 64)
+        a = np.arange(16, dtype=np.int32).reshape(1, 16)
+        o = grpcclient.InferRequestedOutput("OUTPUT0")
+        o.set_shared_memory("inflight_out", 64)
+        done = threading.Event()
+        res = []
+
+        def cb(result, error):
+            res.append((result, error))
+            done.set()
+
+        g.async_infer("add_sub_batched", _inputs(a, a), cb, outputs=[o])
+        time.sleep(0.2)  # the batch is executing (holding the region)
+        t0 = time.monotonic()
+        g.unregister_system_shared_memory("inflight_out")
+        waited = time.monotonic() - t0
+        assert done.wait(10)
+        assert res[0][1] is None, res[0][1]
+        assert waited > 0.2, "unregister returned while the request still held the region"
+        np.testing.assert_array_equal(shm.get_contents_as_numpy(out, np.int32, [1, 16]), 2 * a)
+    finally:
+        AddSubBatched.native_delay_s = 0.0
+        g.unregister_system_shared_memory()
+        shm.destroy_shared_memory_region(out)
+
+
+def test_oversized_content_length_gets_413(cpu_server):
+    host, port = cpu_server.http_url.split(":")
+    for hdr in (b"Content-Length: 99999999999\r\n", b"Transfer-Encoding: chunked\r\n"):
+        req = b"POST /v2/models/add_sub_batched/infer HTTP/1.1\r\nHost: x\r\n" + hdr + b"\r\n"
+        if b"chunked" in hdr:
+            req += b"ffffffffffffffff\r\nabc"
+        s = socket.create_connection((host, int(port)))
+        s.sendall(req)
+        s.settimeout(10)
+        data = b""
+        while True:
+            chunk = s.recv(65536)
+            if not chunk:
+                break
+            data += chunk
+        s.close()
+        assert data.startswith(b"HTTP/1.1 413"), data[:200]

@@ -268,6 +268,7 @@ class AddSubBatched(Model):
     dynamic_batching = {"preferred": [], "max_queue_delay_us": 200}
     instance_count = 2
     supports_native = True
+    native_delay_s = 0.0  # tests: hold each native batch this long (region-lifetime checks)
 
     def execute(self, requests):
         out = []
@@ -285,6 +286,8 @@ class AddSubBatched(Model):
         import time
 
         t0 = time.monotonic_ns()
+        if self.native_delay_s:
+            time.sleep(self.native_delay_s)
         ni, no = b.n_inputs, b.n_outputs
         for r in range(b.n_requests):
             rows = b.rows[r]
