@@ -1,0 +1,748 @@
+// K8x/K9x/K10x — fp32-parity DenseNet-121 inference kernels for CDNA4 (gfx950).
+//
+// The reference's densenet_onnx contract is FP32 in, FP32 out, FP32 compute
+// (reference src/python/examples/image_client.py:84-86 builds FP32 inputs for
+// an fp32 ONNX graph).  gfx950 has no xf32 MFMA and its f32-input MFMA runs at
+// 1/16 of the bf16 rate, so these kernels compute every conv as a
+// split-precision "bf16x3" product on the bf16 MFMA:
+//
+//     a = a_hi + a_lo,  a_hi = bf16_rne(a),  a_lo = bf16_rne(a - a_hi)
+//     a*b ~= a_hi*b_hi + a_hi*b_lo + a_lo*b_hi          (fp32 accumulate)
+//
+// a_hi + a_lo carries 16 significant bits (|a - a_hi - a_lo| <= 2^-17 |a|)
+// and the dropped a_lo*b_lo term is <= 2^-16 of the product, so each conv is
+// within ~1e-5 relative of an fp32 conv at 3/16 of the f32-MFMA cost.
+//
+// Layout (all activations stay fp32 in HBM — 288 GB leaves room to spare):
+//  * every dense block owns ONE NHWC fp32 feature buffer [pixels][C_block];
+//    a layer's 3x3 conv writes its 32 new channels into its slice (the concat
+//    is free) and the next layer's 1x1 conv reads the first K channels;
+//  * K8x conv1x1: the BN1+ReLU pre-activation (consumer specific) is applied
+//    to the fp32 X tile while it is staged global->LDS and split into hi/lo
+//    tiles there; BN2 is folded into W (pre-split on the host) and its bias +
+//    ReLU run in the epilogue, which writes the 128-channel bottleneck z as
+//    TWO bf16 planes z_hi/z_lo (the 3x3 conv's operands, already split:
+//    same bytes as fp32).  POOL=true is the transition: BN+ReLU+2x2 avg-pool
+//    in the prologue, fp32 output into the next block's buffer;
+//  * K9x conv3x3 (128->32): eight waves split the 128 input channels (16
+//    each = one 32x32x16 MFMA K), so each wave's hi/lo weight fragments for
+//    all nine taps live in 72 VGPRs for the whole persistent kernel; the
+//    block stages the z_hi/z_lo band its 128-pixel tile needs in LDS (the
+//    next tile's band is prefetched into registers during the MFMAs) and the
+//    8 partial tiles are summed through LDS;
+//  * K10x stem (7x7/2 conv + BN + ReLU + 3x3/2 max-pool, fp32 images read
+//    through a device pointer table) and head (BN+ReLU+global avg-pool).
+//
+// MFMA operand orientation as in densenet.hip: WEIGHTS are operand A (rows =
+// output channels), activations operand B (cols = pixels), so a lane's
+// accumulators are consecutive output channels of one pixel.
+
+#include <algorithm>
+
+#include "kernels/common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v4u ld16(const void* p) { return *reinterpret_cast<const v4u*>(p); }
+__device__ __forceinline__ f32x4 ldf4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+// two fp32 -> packed bf16, RNE (gfx950 v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pk(float a, float b) {
+  const bf16x2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+// hi/lo split of two fp32: a ~= hi + lo to 2^-17 relative (a - hi is exact)
+__device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  hi = pk(a, b);
+  lo = pk(a - __uint_as_float(hi << 16), b - __uint_as_float(hi & 0xffff0000u));
+}
+
+__device__ __forceinline__ void split4(f32x4 v, v2u& hi, v2u& lo) {
+  uint32_t h0, l0, h1, l1;
+  split2(v[0], v[1], h0, l0);
+  split2(v[2], v[3], h1, l1);
+  hi = v2u{h0, h1};
+  lo = v2u{l0, l1};
+}
+
+__device__ __forceinline__ bf16x8 fr(v4u v) { return __builtin_bit_cast(bf16x8, v); }
+
+// bf16x3 products; the two small cross terms go in first
+__device__ __forceinline__ f32x4 x3_16(v4u ah, v4u al, v4u bh, v4u bl, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr(al), fr(bh), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr(ah), fr(bl), c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr(ah), fr(bh), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 x3_32(v4u ah, v4u al, v4u bh, v4u bl, f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr(al), fr(bh), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr(ah), fr(bl), c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr(ah), fr(bh), c, 0, 0, 0);
+}
+
+// ============================================================================
+// K8x: 1x1 conv, split-precision GEMM with fused pre-activation
+// ============================================================================
+struct X3Conv1x1Params {
+  const float* x;        // [rows][ldx] fp32 (rows = M, or the pre-pool pixels)
+  const float* in_scale; // [K] BN scale of the pre-activation
+  const float* in_bias;  // [K]
+  const uint16_t* w_hi;  // [128][K] bf16
+  const uint16_t* w_lo;  // [128][K] bf16
+  const float* out_bias; // [128] (SPLIT epilogue: bias + ReLU)
+  uint16_t* z_hi;        // SPLIT: [M][128] bf16 planes
+  uint16_t* z_lo;
+  float* y;              // !SPLIT: [M][ldy] fp32, raw conv output
+  float* ws;             // split-K partials [splits][M][128] (null = whole K per block)
+  int ldx, M, K, ldy, H, W, k_per_split;
+};
+
+constexpr int kBM = 128, kBN = 128, kBK = 32, kLDK = kBK + 8;  // 80-B LDS rows: conflict-free b128 reads
+
+// Block = 4 waves as 2 (pixels) x 2 (channels): block tile 128 x 128, wave
+// tile 64 x 64 = 4 x 4 16x16x32 MFMA tiles (x3 = 48 MFMAs per K step).  The
+// LDS tiles are double-buffered and the next K step's global loads are in
+// flight in registers while this step's MFMAs run (one barrier per step).
+template <bool POOL, bool SPLIT>
+__global__ void __launch_bounds__(256, 2) x3_conv1x1_kernel(X3Conv1x1Params p) {
+  constexpr int NS = POOL ? 4 : 1;
+  __shared__ __attribute__((aligned(16))) uint16_t sXh[2][kBM * kLDK];
+  __shared__ __attribute__((aligned(16))) uint16_t sXl[2][kBM * kLDK];
+  __shared__ __attribute__((aligned(16))) uint16_t sWh[2][kBN * kLDK];
+  __shared__ __attribute__((aligned(16))) uint16_t sWl[2][kBN * kLDK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int m0 = blockIdx.x * kBM;
+
+  // X: 128 rows x 8 chunks of 4 fp32 per K step -> 4 chunks per thread, all
+  // at the same K offset (tid & 7); POOL: each chunk averages 4 source rows
+  const int xk = (tid & 7) * 4;
+  const float* xs[4][NS];
+  bool xok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (tid >> 3) + 32 * i;
+    const int m = m0 + r;
+    xok[i] = m < p.M;
+    const int mm = xok[i] ? m : 0;
+    if constexpr (POOL) {
+      const int wo = p.W >> 1, ho = p.H >> 1;
+      const int img = mm / (ho * wo), rr = mm - img * ho * wo;
+      const int oh = rr / wo, ow = rr - oh * wo;
+      const size_t base = ((size_t)img * p.H + 2 * oh) * p.W + 2 * ow;
+      xs[i][0] = p.x + base * p.ldx + xk;
+      xs[i][1] = p.x + (base + 1) * p.ldx + xk;
+      xs[i][2] = p.x + (base + p.W) * p.ldx + xk;
+      xs[i][3] = p.x + (base + p.W + 1) * p.ldx + xk;
+    } else {
+      xs[i][0] = p.x + (size_t)mm * p.ldx + xk;
+    }
+  }
+  // W: 128 rows x 4 chunks of 8 bf16 per plane -> 2 chunks per thread per plane
+  const int wk = (tid & 3) * 8;
+  const uint16_t* wsh[2];
+  const uint16_t* wsl[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (tid >> 2) + 64 * i;
+    wsh[i] = p.w_hi + (size_t)r * p.K + wk;
+    wsl[i] = p.w_lo + (size_t)r * p.K + wk;
+  }
+
+  f32x4 rx[4][NS], rs, rt;
+  v4u rwh[2], rwl[2];
+  auto load_step = [&](int k0) {
+    rs = ldf4(p.in_scale + k0 + xk);
+    rt = ldf4(p.in_bias + k0 + xk);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) rx[i][s] = xok[i] ? ldf4(xs[i][s] + k0) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      rwh[i] = ld16(wsh[i] + k0);
+      rwl[i] = ld16(wsl[i] + k0);
+    }
+  };
+  auto store_step = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if constexpr (POOL) {
+          float a = 0.f;
+#pragma unroll
+          for (int s = 0; s < NS; ++s) a += fmaxf(rx[i][s][e] * rs[e] + rt[e], 0.f);
+          v[e] = 0.25f * a;
+        } else {
+          v[e] = fmaxf(rx[i][0][e] * rs[e] + rt[e], 0.f);
+        }
+        if (!xok[i]) v[e] = 0.f;
+      }
+      v2u h, l;
+      split4(v, h, l);
+      const int off = ((tid >> 3) + 32 * i) * kLDK + xk;
+      *reinterpret_cast<v2u*>(&sXh[buf][off]) = h;
+      *reinterpret_cast<v2u*>(&sXl[buf][off]) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int off = ((tid >> 2) + 64 * i) * kLDK + wk;
+      *reinterpret_cast<v4u*>(&sWh[buf][off]) = rwh[i];
+      *reinterpret_cast<v4u*>(&sWl[buf][off]) = rwl[i];
+    }
+  };
+
+  const int fr16 = lane & 15, fk = 8 * (lane >> 4);
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (SPLIT && !p.ws) b0 = ldf4(p.out_bias + wn * 64 + j * 16 + (lane >> 4) * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = b0;
+  }
+
+  const int k_begin = p.ws ? (int)blockIdx.y * p.k_per_split : 0;
+  const int k_end = p.ws ? min(p.K, k_begin + p.k_per_split) : p.K;
+  load_step(k_begin);
+  store_step(0);
+  __syncthreads();
+  for (int k0 = k_begin, buf = 0; k0 < k_end; k0 += kBK, buf ^= 1) {
+    const bool more = k0 + kBK < k_end;
+    if (more) load_step(k0 + kBK);
+    v4u ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int off = (wn * 64 + j * 16 + fr16) * kLDK + fk;
+      ah[j] = ld16(&sWh[buf][off]);
+      al[j] = ld16(&sWl[buf][off]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int off = (wm * 64 + i * 16 + fr16) * kLDK + fk;
+      bh[i] = ld16(&sXh[buf][off]);
+      bl[i] = ld16(&sXl[buf][off]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[j][i] = x3_16(ah[j], al[j], bh[i], bl[i], acc[j][i]);
+    if (more) store_step(buf ^ 1);
+    __syncthreads();
+  }
+
+  // lane holds output channels nb..nb+3 of pixel m
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int nb = wn * 64 + j * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + fr16;
+      if (m >= p.M) continue;
+      const f32x4 a = acc[j][i];
+      if (p.ws) {
+        *reinterpret_cast<f32x4*>(p.ws + ((size_t)blockIdx.y * p.M + m) * kBN + nb) = a;
+      } else if constexpr (SPLIT) {
+        const f32x4 r = f32x4{fmaxf(a[0], 0.f), fmaxf(a[1], 0.f), fmaxf(a[2], 0.f), fmaxf(a[3], 0.f)};
+        v2u h, l;
+        split4(r, h, l);
+        *reinterpret_cast<v2u*>(p.z_hi + (size_t)m * kBN + nb) = h;
+        *reinterpret_cast<v2u*>(p.z_lo + (size_t)m * kBN + nb) = l;
+      } else {
+        *reinterpret_cast<f32x4*>(p.y + (size_t)m * p.ldy + nb) = a;
+      }
+    }
+  }
+}
+
+// split-K combine: out[m][n..n+3] = epi(sum_s ws[s][m][n..n+3] (+ bias))
+template <bool SPLIT>
+__global__ void __launch_bounds__(256) x3_splitk_reduce_kernel(X3Conv1x1Params p, int splits) {
+  const size_t total = (size_t)p.M * (kBN / 4);
+  for (size_t q = blockIdx.x * 256ull + threadIdx.x; q < total; q += (size_t)gridDim.x * 256) {
+    const int m = (int)(q / (kBN / 4)), nb = (int)(q % (kBN / 4)) * 4;
+    f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (SPLIT) a = ldf4(p.out_bias + nb);
+    for (int s = 0; s < splits; ++s) a += ldf4(p.ws + ((size_t)s * p.M + m) * kBN + nb);
+    if constexpr (SPLIT) {
+      const f32x4 r = f32x4{fmaxf(a[0], 0.f), fmaxf(a[1], 0.f), fmaxf(a[2], 0.f), fmaxf(a[3], 0.f)};
+      v2u h, l;
+      split4(r, h, l);
+      *reinterpret_cast<v2u*>(p.z_hi + (size_t)m * kBN + nb) = h;
+      *reinterpret_cast<v2u*>(p.z_lo + (size_t)m * kBN + nb) = l;
+    } else {
+      *reinterpret_cast<f32x4*>(p.y + (size_t)m * p.ldy + nb) = a;
+    }
+  }
+}
+
+// ============================================================================
+// K9x: 3x3 conv 128 -> 32 (stride 1, pad 1) on the split bottleneck
+// ============================================================================
+constexpr int kC3 = 128, kTaps = 9;  // 32 output channels (growth) per conv
+constexpr int kTile3 = 128;            // output pixels per tile
+constexpr int kRow3 = kC3 + 8;         // LDS ring row stride (bf16): 272 B, conflict-free b128 reads
+constexpr int kRing = 256;             // ring rows per plane (a band is 128 + 2(W+1) <= 242 rows)
+constexpr int kMaxW3 = 56;
+constexpr int kNew3 = kTile3 * (kC3 / 8) / 512;  // 16-B chunks per thread per plane of a tile's new rows: 4
+constexpr int kLds3 = 2 * (kRing + 1) * kRow3 * 2;  // both planes + one zero row each: 139,808 B
+
+struct X3Conv3x3Params {
+  const uint16_t* z_hi;  // [M][128] bf16
+  const uint16_t* z_lo;
+  const uint16_t* w_hi;  // [32][9][128] bf16 (tap-major K)
+  const uint16_t* w_lo;
+  float* y;              // [M][ldy] fp32, offset to the layer's 32-channel slice
+  int ldy, M, H, W;
+  int tiles, tiles_per_block;
+};
+
+// 8 waves (2 per SIMD); wave w owns input channels [16w, 16w+16) of all nine
+// taps, so its hi/lo weight fragments are 18 x 16 B in registers for the
+// whole kernel.  A block walks a CONTIGUOUS run of 128-pixel tiles with the
+// activation band [m0-W-1, m0+128+W+1) of both planes in a 256-row LDS ring
+// (global row g lives in ring row (g + W + 1) & 255; row 256 is zeros, read
+// by out-of-image taps): after its first tile a block fetches only the 128
+// rows the next tile adds, into registers while the current tile's MFMAs
+// run.  The 8 partial tiles are summed through LDS in two rounds (waves 4-7
+// -> 0-3, then 4 slots -> all threads) in the ring rows only the current
+// tile reads, which are then overwritten by the prefetched rows.
+__global__ void __launch_bounds__(512, 1) x3_conv3x3_kernel(X3Conv3x3Params p) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds3[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int W = p.W, HW = p.H * p.W;
+  uint16_t* rh = lds3;                       // [257][kRow3]
+  uint16_t* rl = lds3 + (kRing + 1) * kRow3;
+
+  const int h = lane >> 5, col = lane & 31;
+  const int ci = 16 * wave + 8 * h;
+  v4u wh[kTaps], wl[kTaps];
+#pragma unroll
+  for (int t = 0; t < kTaps; ++t) {
+    wh[t] = ld16(p.w_hi + (size_t)col * (kTaps * kC3) + t * kC3 + ci);
+    wl[t] = ld16(p.w_lo + (size_t)col * (kTaps * kC3) + t * kC3 + ci);
+  }
+
+  const int t_begin = blockIdx.x * p.tiles_per_block;
+  const int t_end = min(p.tiles, t_begin + p.tiles_per_block);
+  if (t_begin >= t_end) return;
+
+  auto ring = [&](int g) { return (g + W + 1) & (kRing - 1); };
+  // first band of the run: rows [m0-W-1, m0+128+W+1), loaded straight to LDS
+  {
+    const int m0 = t_begin * kTile3;
+    const int nch = (kTile3 + 2 * (W + 1)) * (kC3 / 8);
+    for (int e = tid; e < nch; e += 512) {
+      const int g = m0 - (W + 1) + (e >> 4);
+      const bool ok = g >= 0 && g < p.M;
+      const size_t off = (size_t)(ok ? g : 0) * kC3 + (e & 15) * 8;
+      const v4u vh = ok ? ld16(p.z_hi + off) : v4u{0, 0, 0, 0};
+      const v4u vl = ok ? ld16(p.z_lo + off) : v4u{0, 0, 0, 0};
+      const int lo = ring(g) * kRow3 + (e & 15) * 8;
+      *reinterpret_cast<v4u*>(&rh[lo]) = vh;
+      *reinterpret_cast<v4u*>(&rl[lo]) = vl;
+    }
+    if (tid < kC3 / 8) {
+      *reinterpret_cast<v4u*>(&rh[kRing * kRow3 + tid * 8]) = v4u{0, 0, 0, 0};
+      *reinterpret_cast<v4u*>(&rl[kRing * kRow3 + tid * 8]) = v4u{0, 0, 0, 0};
+    }
+  }
+  __syncthreads();
+
+  v4u ph[kNew3], pl[kNew3];
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int m0 = tile * kTile3;
+    const bool more = tile + 1 < t_end;
+    // the next tile's new rows [m0+128+W+1, m0+256+W+1)
+    const int g0 = m0 + kTile3 + W + 1;
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < kNew3; ++i) {
+        const int e = tid + 512 * i;
+        const int g = g0 + (e >> 4);
+        const bool ok = g < p.M;
+        const size_t off = (size_t)(ok ? g : 0) * kC3 + (e & 15) * 8;
+        ph[i] = ok ? ld16(p.z_hi + off) : v4u{0, 0, 0, 0};
+        pl[i] = ok ? ld16(p.z_lo + off) : v4u{0, 0, 0, 0};
+      }
+    }
+    f32x16 acc[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[s][e] = 0.f;
+      const int m = m0 + 32 * s + col;
+      const int r = m % HW, yy = r / W, xx = r - yy * W;
+      const bool in = m < p.M;
+#pragma unroll
+      for (int t = 0; t < kTaps; ++t) {
+        const int dy = t / 3 - 1, dx = t % 3 - 1;
+        const bool ok = in && yy + dy >= 0 && yy + dy < p.H && xx + dx >= 0 && xx + dx < W;
+        const int row = ok ? ring(m + dy * W + dx) : kRing;
+        const v4u b_hi = ld16(&rh[row * kRow3 + ci]);
+        const v4u b_lo = ld16(&rl[row * kRow3 + ci]);
+        acc[s] = x3_32(wh[t], wl[t], b_hi, b_lo, acc[s]);
+      }
+    }
+    __syncthreads();  // ring reads done
+    // scratch = the ring rows of global rows [m0-W-1, m0+127-W) (read by this
+    // tile only): pixel q's slot k (32 fp32) at ring row ring(m0-W-1+q),
+    // slots 0/1 in the hi plane's 272 B, slots 2/3 in the lo plane's
+    auto slot = [&](int q, int k) {
+      uint16_t* base = (k < 2 ? rh : rl) + ring(m0 - W - 1 + q) * kRow3;
+      return reinterpret_cast<float*>(base) + 32 * (k & 1);
+    };
+    // C layout (32x32): lane col = pixel, reg r -> channel (r&3) + 8*(r>>2) + 4*h
+    if (wave >= 4) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        float* q = slot(32 * s + col, wave - 4);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(q + 8 * g + 4 * h) =
+              f32x4{acc[s][4 * g], acc[s][4 * g + 1], acc[s][4 * g + 2], acc[s][4 * g + 3]};
+      }
+    }
+    __syncthreads();
+    if (wave < 4) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        float* q = slot(32 * s + col, wave);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4* d = reinterpret_cast<f32x4*>(q + 8 * g + 4 * h);
+          const f32x4 o = *d;
+          *d = f32x4{acc[s][4 * g] + o[0], acc[s][4 * g + 1] + o[1], acc[s][4 * g + 2] + o[2],
+                     acc[s][4 * g + 3] + o[3]};
+        }
+      }
+    }
+    __syncthreads();
+    {
+      const int px = tid >> 2, c0 = (tid & 3) * 8;
+      f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float* q = slot(px, k) + c0;
+        s0 += *reinterpret_cast<const f32x4*>(q);
+        s1 += *reinterpret_cast<const f32x4*>(q + 4);
+      }
+      const int m = m0 + px;
+      if (m < p.M) {
+        float* o = p.y + (size_t)m * p.ldy + c0;
+        *reinterpret_cast<f32x4*>(o) = s0;
+        *reinterpret_cast<f32x4*>(o + 4) = s1;
+      }
+    }
+    if (more) {
+      __syncthreads();  // scratch reads done before the new rows land on them
+#pragma unroll
+      for (int i = 0; i < kNew3; ++i) {
+        const int e = tid + 512 * i;
+        const int lo = ring(g0 + (e >> 4)) * kRow3 + (e & 15) * 8;
+        *reinterpret_cast<v4u*>(&rh[lo]) = ph[i];
+        *reinterpret_cast<v4u*>(&rl[lo]) = pl[i];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ============================================================================
+// K10x stem: y = relu(maxpool3x3/2(conv7x7/2(x)) + b), 3 -> 64 channels, fp32
+// ============================================================================
+// As K10s in densenet.hip (patch staged once per block, conv as an implicit
+// GEMM on v_mfma_f32_32x32x16 with weights [64][kh 7][kw 8][ch 4] as operand
+// A), with the patch split into hi/lo planes, the weights' hi/lo fragments in
+// registers, and the conv tile kept in fp32 for the max-pool.
+constexpr int kSPR = 4, kSPC = 14;       // pooled outputs per block
+constexpr int kSCR = 2 * kSPR + 1;       // 9 conv rows
+constexpr int kSCC = 32;                 // conv cols computed (2*PC+1 = 29 used)
+constexpr int kSIR = 2 * kSCR + 5;       // 23 input rows
+constexpr int kSIC = 72;                 // input cols
+constexpr int kSK = 7 * 32;              // (kh, kw[8], ch[4])
+constexpr int kSOS = 64 + 4;             // conv-tile pixel stride (fp32)
+constexpr int kSHin = 224, kSHo = 56;
+
+struct X3StemParams {
+  const float* const* srcs;  // per-image fp32 NCHW [3][224][224] (device pointer table)
+  const uint16_t* w_hi;      // [64][kSK] bf16 (BN0 scale folded)
+  const uint16_t* w_lo;
+  const float* bias;         // [64] BN0 shift
+  float* y;                  // [imgs][56][56] pixels, rows of ldy fp32
+  int ldy;
+};
+
+__global__ void __launch_bounds__(256) x3_stem_kernel(X3StemParams p) {
+  __shared__ __attribute__((aligned(16))) uint16_t Ih[kSIR * kSIC * 4];  // 13.2 KB
+  __shared__ __attribute__((aligned(16))) uint16_t Il[kSIR * kSIC * 4];
+  __shared__ __attribute__((aligned(16))) float Cv[kSCR * kSCC * kSOS];   // 78 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int img = blockIdx.z, pr0 = blockIdx.y * kSPR, pc0 = blockIdx.x * kSPC;
+  const int ir0 = 4 * pr0 - 5, ic0 = 4 * pc0 - 5;
+  const float* src = p.srcs[img];
+  constexpr int kStage = (kSIR * kSIC + 255) / 256;
+  float v[kStage][3];
+#pragma unroll
+  for (int i = 0; i < kStage; ++i) {
+    const int e = tid + i * 256;
+    const int r = e / kSIC, c = e - r * kSIC;
+    const int ih = ir0 + r, iw = ic0 + c;
+    v[i][0] = v[i][1] = v[i][2] = 0.f;
+    if (e < kSIR * kSIC && ih >= 0 && ih < kSHin && iw >= 0 && iw < kSHin) {
+      const float* s = src + ih * kSHin + iw;
+      v[i][0] = __builtin_nontemporal_load(s);
+      v[i][1] = __builtin_nontemporal_load(s + kSHin * kSHin);
+      v[i][2] = __builtin_nontemporal_load(s + 2 * kSHin * kSHin);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kStage; ++i) {
+    const int e = tid + i * 256;
+    if (e < kSIR * kSIC) {
+      uint32_t h0, l0, h1, l1;
+      split2(v[i][0], v[i][1], h0, l0);
+      split2(v[i][2], 0.f, h1, l1);
+      *reinterpret_cast<v2u*>(&Ih[e * 4]) = v2u{h0, h1};
+      *reinterpret_cast<v2u*>(&Il[e * 4]) = v2u{l0, l1};
+    }
+  }
+  // wave = (channel half nh) x (conv-row group mg: rows 0-4 / 5-8)
+  const int nh = wave & 1, mg = wave >> 1;
+  v4u wh[kSK / 16], wl[kSK / 16];
+  const size_t wrow = (size_t)(nh * 32 + (lane & 31)) * kSK + 8 * (lane >> 5);
+#pragma unroll
+  for (int s = 0; s < kSK / 16; ++s) {
+    wh[s] = ld16(p.w_hi + wrow + s * 16);
+    wl[s] = ld16(p.w_lo + wrow + s * 16);
+  }
+  __syncthreads();
+  const int jj = lane & 31, hh = lane >> 5;
+  const int r_lo = mg ? 5 : 0, r_hi = mg ? kSCR : 5;
+  for (int cr = r_lo; cr < r_hi; ++cr) {
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < kSK / 16; ++s) {
+      const int kh = s >> 1, q = (s & 1) * 2 + hh;
+      const int off = ((2 * cr + kh) * kSIC + 2 * jj + 2 * q) * 4;
+      acc = x3_32(wh[s], wl[s], ld16(&Ih[off]), ld16(&Il[off]), acc);
+    }
+    float* cp = &Cv[(cr * kSCC + jj) * kSOS + nh * 32 + 4 * hh];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(cp + 8 * g) = f32x4{acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+  }
+  __syncthreads();
+  for (int t = tid; t < kSPR * kSPC * 16; t += 256) {
+    const int cc = t & 15, px = t >> 4;  // 4-channel chunk, pooled pixel
+    const int a = px / kSPC, b = px - a * kSPC;
+    const int pr = pr0 + a, pc = pc0 + b;
+    f32x4 mx = f32x4{-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      if (2 * pr - 1 + dy < 0) continue;
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        if (2 * pc - 1 + dx < 0) continue;
+        const f32x4 f = *reinterpret_cast<const f32x4*>(&Cv[((2 * a + dy) * kSCC + 2 * b + dx) * kSOS + cc * 4]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mx[e] = fmaxf(mx[e], f[e]);
+      }
+    }
+    const f32x4 bb = ldf4(p.bias + cc * 4);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = fmaxf(mx[e] + bb[e], 0.f);
+    *reinterpret_cast<f32x4*>(p.y + (((size_t)img * kSHo + pr) * kSHo + pc) * p.ldy + cc * 4) = o;
+  }
+}
+
+// ============================================================================
+// K10x head: out[img][c] = mean_p relu(x[img][p][c]*s[c] + b[c])   (fp32)
+// ============================================================================
+__global__ void __launch_bounds__(256) x3_head_pool_kernel(const float* __restrict__ x, const float* __restrict__ s,
+                                                           const float* __restrict__ b, float* __restrict__ out, int HW,
+                                                           int C) {
+  const int img = blockIdx.x;
+  for (int c4 = threadIdx.x; c4 < C / 4; c4 += blockDim.x) {
+    const f32x4 sc = ldf4(s + c4 * 4), bi = ldf4(b + c4 * 4);
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < HW; ++q) {
+      const f32x4 f = ldf4(x + ((size_t)img * HW + q) * C + c4 * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += fmaxf(f[e] * sc[e] + bi[e], 0.f);
+    }
+    const float inv = 1.0f / (float)HW;
+    *reinterpret_cast<f32x4*>(out + (size_t)img * C + c4 * 4) = acc * inv;
+  }
+}
+
+// weight hi/lo split on device (fp32 [n] -> two bf16 planes)
+__global__ void x3_split_kernel(const float* __restrict__ w, uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
+                                size_t n) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    uint32_t h, l;
+    split2(w[i], 0.f, h, l);
+    hi[i] = (uint16_t)h;
+    lo[i] = (uint16_t)l;
+  }
+}
+
+bool aligned16(const void* q) { return ((uintptr_t)q & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+// Split-K workspace bytes the 1x1 conv wants for an M x K problem (0 = none).
+size_t tcamd_x3_conv1x1_ws_bytes(int M, int K) {
+  const int tiles = (M + kBM - 1) / kBM;
+  if (tiles >= 384 || K < 2 * kBK) return 0;
+  const int splits = std::min(K / kBK, (768 + tiles - 1) / tiles);
+  return splits > 1 ? (size_t)splits * M * kBN * sizeof(float) : 0;
+}
+
+// 1x1 conv (128 output channels).  split_out: z_hi/z_lo [M][128] bf16 with
+// bias+ReLU; else y fp32 [M][ldy] raw.  pool: x holds the pre-pool H x W
+// pixels, M = imgs * H/2 * W/2.  ws: split-K workspace (may be null).
+int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, const float* in_scale, const float* in_bias,
+                     const void* w_hi, const void* w_lo, const float* out_bias, void* z_hi, void* z_lo, float* y,
+                     int ldy, int pool, int H, int W, float* ws, size_t ws_bytes, void* stream) {
+  if (M <= 0) return hipSuccess;
+  const bool split_out = z_hi != nullptr;
+  if (K % kBK || K <= 0 || ldx % 4 || ldx < K || !x || !in_scale || !in_bias || !w_hi || !w_lo)
+    return hipErrorInvalidValue;
+  if (split_out ? (!z_lo || !out_bias || !aligned16(z_hi) || !aligned16(z_lo)) : (!y || ldy % 4 || ldy < kBN))
+    return hipErrorInvalidValue;
+  if (!aligned16(x) || !aligned16(w_hi) || !aligned16(w_lo) || !aligned16(in_scale) || !aligned16(in_bias))
+    return hipErrorInvalidValue;
+  if (pool && (H % 2 || W % 2 || (size_t)M % ((size_t)(H / 2) * (W / 2)))) return hipErrorInvalidValue;
+  X3Conv1x1Params p;
+  p.x = x;
+  p.in_scale = in_scale;
+  p.in_bias = in_bias;
+  p.w_hi = (const uint16_t*)w_hi;
+  p.w_lo = (const uint16_t*)w_lo;
+  p.out_bias = out_bias;
+  p.z_hi = (uint16_t*)z_hi;
+  p.z_lo = (uint16_t*)z_lo;
+  p.y = y;
+  p.ws = nullptr;
+  p.ldx = ldx;
+  p.M = M;
+  p.K = K;
+  p.ldy = ldy;
+  p.H = H;
+  p.W = W;
+  p.k_per_split = K;
+  const int tiles = (M + kBM - 1) / kBM;
+  int splits = 1;
+  const size_t want = tcamd_x3_conv1x1_ws_bytes(M, K);
+  if (want && ws && ws_bytes >= want && aligned16(ws)) {
+    splits = (int)(want / ((size_t)M * kBN * sizeof(float)));
+    const int steps = K / kBK;
+    p.k_per_split = ((steps + splits - 1) / splits) * kBK;
+    splits = (K + p.k_per_split - 1) / p.k_per_split;
+    if (splits > 1) p.ws = ws;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g(tiles, splits);
+  if (pool) {
+    if (split_out) hipLaunchKernelGGL((x3_conv1x1_kernel<true, true>), g, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((x3_conv1x1_kernel<true, false>), g, dim3(256), 0, s, p);
+  } else {
+    if (split_out) hipLaunchKernelGGL((x3_conv1x1_kernel<false, true>), g, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((x3_conv1x1_kernel<false, false>), g, dim3(256), 0, s, p);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !p.ws) return e;
+  const int rg = tcamd::grid_for((size_t)M * (kBN / 4));
+  if (split_out) hipLaunchKernelGGL(x3_splitk_reduce_kernel<true>, dim3(rg), dim3(256), 0, s, p, splits);
+  else hipLaunchKernelGGL(x3_splitk_reduce_kernel<false>, dim3(rg), dim3(256), 0, s, p, splits);
+  return hipGetLastError();
+}
+
+// 3x3 conv 128 -> 32 over imgs x H x W pixels (W <= 56); z_hi/z_lo [M][128]
+// bf16, w_hi/w_lo [32][9][128] bf16, y fp32 rows of ldy (offset to the slice).
+int tcamd_x3_conv3x3(const void* z_hi, const void* z_lo, int imgs, int H, int W, const void* w_hi, const void* w_lo,
+                     float* y, int ldy, void* stream) {
+  if (imgs <= 0) return hipSuccess;
+  if (W > kMaxW3 || W < 1 || H < 1 || ldy % 4 || !z_hi || !z_lo || !w_hi || !w_lo || !y) return hipErrorInvalidValue;
+  if (!aligned16(z_hi) || !aligned16(z_lo) || !aligned16(w_hi) || !aligned16(w_lo) || !aligned16(y))
+    return hipErrorInvalidValue;
+  X3Conv3x3Params p;
+  p.z_hi = (const uint16_t*)z_hi;
+  p.z_lo = (const uint16_t*)z_lo;
+  p.w_hi = (const uint16_t*)w_hi;
+  p.w_lo = (const uint16_t*)w_lo;
+  p.y = y;
+  p.ldy = ldy;
+  p.M = imgs * H * W;
+  p.H = H;
+  p.W = W;
+  p.tiles = (p.M + kTile3 - 1) / kTile3;
+  // one block (8 waves) per CU; each walks a contiguous run of tiles so the
+  // halo rows its neighbour tile re-reads are still in this XCD's L2
+  const int grid = std::min(p.tiles, 256);
+  p.tiles_per_block = (p.tiles + grid - 1) / grid;
+  const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
+  const size_t lds = kLds3;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e =
+        hipFuncSetAttribute((const void*)x3_conv3x3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kLds3);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(x3_conv3x3_kernel, dim3(blocks), dim3(512), lds, (hipStream_t)stream, p);
+  return hipGetLastError();
+}
+
+// fp32 stem over fp32 NCHW 224x224x3 images (device pointer table srcs)
+// -> y fp32 [imgs][56][56] rows of ldy (channels 0..63).
+int tcamd_x3_stem(const void* srcs, const void* w_hi, const void* w_lo, const float* bias, float* y, int imgs, int ldy,
+                  void* stream) {
+  if (imgs <= 0) return hipSuccess;
+  if (ldy % 4 || ldy < 64 || !srcs || !w_hi || !w_lo || !bias || !y) return hipErrorInvalidValue;
+  if (!aligned16(w_hi) || !aligned16(w_lo) || !aligned16(y) || !aligned16(bias) || (uintptr_t)srcs % 8)
+    return hipErrorInvalidValue;
+  X3StemParams p;
+  p.srcs = (const float* const*)srcs;
+  p.w_hi = (const uint16_t*)w_hi;
+  p.w_lo = (const uint16_t*)w_lo;
+  p.bias = bias;
+  p.y = y;
+  p.ldy = ldy;
+  hipLaunchKernelGGL(x3_stem_kernel, dim3(kSHo / kSPC, kSHo / kSPR, imgs), dim3(256), 0, (hipStream_t)stream, p);
+  return hipGetLastError();
+}
+
+int tcamd_x3_head_pool(const float* x, const float* s, const float* b, float* out, int imgs, int HW, int C,
+                       void* stream) {
+  if (imgs <= 0) return hipSuccess;
+  if (C % 4 || !aligned16(x) || !aligned16(s) || !aligned16(b) || !aligned16(out)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(x3_head_pool_kernel, dim3(imgs), dim3(256), 0, (hipStream_t)stream, x, s, b, out, HW, C);
+  return hipGetLastError();
+}
+
+int tcamd_x3_split(const float* w, void* hi, void* lo, size_t n, void* stream) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(x3_split_kernel, dim3(tcamd::grid_for(n)), dim3(256), 0, (hipStream_t)stream, w, (uint16_t*)hi,
+                     (uint16_t*)lo, n);
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,227 @@
+"""Numerics of the fp32-parity DenseNet kernels (K8x/K9x/K10x, bf16x3 split
+precision) against plain PyTorch fp32 / fp64 references of the same op.
+
+The split-precision product is accurate to ~2^-16 relative per term, so the
+tolerances here are fp32-class (1e-5 .. 1e-4), three orders of magnitude
+tighter than the bf16 engine's tests (tests/test_densenet_kernels_gpu.py).
+"""
+
+import pytest
+
+torch = pytest.importorskip("torch")
+F = torch.nn.functional
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _hip():
+    from triton_client_amd.ops import hip
+
+    hip.lib()
+    return hip
+
+
+def _rel(got, ref):
+    got, ref = got.double(), ref.double()
+    assert torch.isfinite(got).all()
+    return ((got - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+
+
+def _split(t):
+    hi = t.to(torch.bfloat16)
+    lo = (t - hi.float()).to(torch.bfloat16)
+    return hi.contiguous(), lo.contiguous()
+
+
+def _st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def test_split_is_exact_to_2e17():
+    _need_gpu()
+    hip = _hip()
+    w = torch.randn(100003, device=DEV) * 3
+    hi = torch.empty(w.numel(), device=DEV, dtype=torch.bfloat16)
+    lo = torch.empty_like(hi)
+    hip.x3_split(w.data_ptr(), hi.data_ptr(), lo.data_ptr(), w.numel(), stream=_st())
+    torch.cuda.synchronize()
+    rh, rl = _split(w)
+    assert torch.equal(hi, rh) and torch.equal(lo, rl)
+    err = ((hi.double() + lo.double()) - w.double()).abs() / w.double().abs().clamp_min(1e-30)
+    assert err.max().item() <= 2.0 ** -17
+
+
+@pytest.mark.parametrize("M,K,ldx", [(100, 64, 96), (37, 992, 1024), (6272, 512, 1024), (50000, 224, 256),
+                                     (401408, 96, 256)])
+def test_x3_conv1x1_split_out(M, K, ldx):
+    """Dense-layer 1x1: z = relu(relu(x*s+t) @ W^T + b) as hi/lo planes
+    (large M: whole-K blocks; small M: split-K workspace + reduce)."""
+    _need_gpu()
+    hip = _hip()
+    g = torch.Generator(device=DEV).manual_seed(M + K)
+    x = torch.randn(M, ldx, device=DEV, generator=g)
+    s = torch.rand(K, device=DEV, generator=g) + 0.5
+    t = torch.randn(K, device=DEV, generator=g) * 0.2
+    w = torch.randn(128, K, device=DEV, generator=g) / K ** 0.5
+    b = torch.randn(128, device=DEV, generator=g) * 0.1
+    wh, wl = _split(w)
+    zh = torch.empty(M, 128, device=DEV, dtype=torch.bfloat16)
+    zl = torch.empty_like(zh)
+    wsb = hip.x3_conv1x1_ws_bytes(M, K)
+    ws = torch.empty(max(wsb, 16), device=DEV, dtype=torch.uint8)
+    hip.x3_conv1x1(x.data_ptr(), ldx, M, K, s.data_ptr(), t.data_ptr(), wh.data_ptr(), wl.data_ptr(),
+                   out_bias=b.data_ptr(), z_hi=zh.data_ptr(), z_lo=zl.data_ptr(), ws=ws.data_ptr(), ws_bytes=wsb,
+                   stream=_st())
+    torch.cuda.synchronize()
+    a = torch.relu(x[:, :K].double() * s.double() + t.double())
+    ref = torch.relu(a @ w.double().t() + b.double())
+    got = zh.double() + zl.double()
+    assert _rel(got, ref) < 3e-5
+
+
+@pytest.mark.parametrize("imgs,H,C,ldy", [(2, 56, 256, 128), (1, 14, 1024, 512), (16, 28, 512, 256),
+                                          (128, 7, 1024, 1024)])
+def test_x3_conv1x1_transition_pool(imgs, H, C, ldy):
+    """Transition: y = avgpool2x2(relu(x*s+t)) @ W^T, fp32 into the next block buffer."""
+    _need_gpu()
+    if H % 2:
+        H += 1
+    hip = _hip()
+    g = torch.Generator(device=DEV).manual_seed(imgs * H + C)
+    x = torch.randn(imgs * H * H, C, device=DEV, generator=g)
+    s = torch.rand(C, device=DEV, generator=g) + 0.5
+    t = torch.randn(C, device=DEV, generator=g) * 0.2
+    w = torch.randn(128, C, device=DEV, generator=g) / C ** 0.5
+    wh, wl = _split(w)
+    Mo = imgs * (H // 2) * (H // 2)
+    y = torch.full((Mo, ldy), 7.0, device=DEV)
+    wsb = hip.x3_conv1x1_ws_bytes(Mo, C)
+    ws = torch.empty(max(wsb, 16), device=DEV, dtype=torch.uint8)
+    hip.x3_conv1x1(x.data_ptr(), C, Mo, C, s.data_ptr(), t.data_ptr(), wh.data_ptr(), wl.data_ptr(),
+                   y=y.data_ptr(), ldy=ldy, pool=1, H=H, W=H, ws=ws.data_ptr(), ws_bytes=wsb, stream=_st())
+    torch.cuda.synchronize()
+    a = torch.relu(x.double() * s.double() + t.double()).reshape(imgs, H, H, C).permute(0, 3, 1, 2)
+    a = F.avg_pool2d(a, 2).permute(0, 2, 3, 1).reshape(Mo, C)
+    ref = a @ w.double().t()
+    assert _rel(y[:, :128], ref) < 3e-5
+    assert (y[:, 128:] == 7.0).all(), "wrote outside the 128-channel slice"
+
+
+@pytest.mark.parametrize("imgs,H", [(1, 7), (3, 14), (2, 56), (48, 28), (24, 56), (1, 28)])
+def test_x3_conv3x3(imgs, H):
+    """3x3 128->32 pad 1 on split planes into an fp32 channel slice (the
+    multi-tile cases exercise the sliding LDS ring across tile runs)."""
+    _need_gpu()
+    hip = _hip()
+    g = torch.Generator(device=DEV).manual_seed(imgs * 100 + H)
+    M = imgs * H * H
+    z = torch.relu(torch.randn(M, 128, device=DEV, generator=g))
+    w = torch.randn(32, 128, 3, 3, device=DEV, generator=g) / (9 * 128) ** 0.5
+    zh, zl = _split(z)
+    wh, wl = _split(w.permute(0, 2, 3, 1).reshape(32, -1))
+    ldy, off = 96, 32
+    y = torch.full((M, ldy), 7.0, device=DEV)
+    hip.x3_conv3x3(zh.data_ptr(), zl.data_ptr(), imgs, H, H, wh.data_ptr(), wl.data_ptr(), y.data_ptr() + 4 * off,
+                   ldy, stream=_st())
+    torch.cuda.synchronize()
+    zin = (zh.double() + zl.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
+    ref = F.conv2d(zin, w.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 32)
+    assert _rel(y[:, off:off + 32], ref) < 2e-5
+    assert (y[:, :off] == 7.0).all() and (y[:, off + 32:] == 7.0).all()
+
+
+def test_x3_stem():
+    _need_gpu()
+    hip = _hip()
+    g = torch.Generator(device=DEV).manual_seed(5)
+    imgs = 3
+    x = torch.randn(imgs, 3, 224, 224, device=DEV, generator=g)
+    w = torch.randn(64, 3, 7, 7, device=DEV, generator=g) / 12
+    bias = torch.randn(64, device=DEV, generator=g) * 0.1
+    wp = torch.zeros(64, 7, 8, 4, device=DEV)
+    wp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
+    wh, wl = _split(wp.reshape(64, -1))
+    ptrs = torch.tensor([x[i].data_ptr() for i in range(imgs)], device=DEV, dtype=torch.int64)
+    ldy = 96
+    y = torch.full((imgs * 56 * 56, ldy), 7.0, device=DEV)
+    hip.x3_stem(ptrs.data_ptr(), wh.data_ptr(), wl.data_ptr(), bias.data_ptr(), y.data_ptr(), imgs, ldy, stream=_st())
+    torch.cuda.synchronize()
+    c = F.conv2d(x.double(), w.double(), stride=2, padding=3)
+    ref = torch.relu(F.max_pool2d(c, 3, 2, 1) + bias.double().view(1, -1, 1, 1))
+    ref = ref.permute(0, 2, 3, 1).reshape(-1, 64)
+    assert _rel(y[:, :64], ref) < 2e-5
+    assert (y[:, 64:] == 7.0).all()
+
+
+def test_x3_head_pool():
+    _need_gpu()
+    hip = _hip()
+    x = torch.randn(5 * 49, 1024, device=DEV)
+    s = torch.rand(1024, device=DEV) + 0.5
+    b = torch.randn(1024, device=DEV)
+    out = torch.empty(5, 1024, device=DEV)
+    hip.x3_head_pool(x.data_ptr(), s.data_ptr(), b.data_ptr(), out.data_ptr(), 5, 49, 1024, stream=_st())
+    torch.cuda.synchronize()
+    ref = torch.relu(x.double() * s.double() + b.double()).reshape(5, 49, 1024).mean(1)
+    assert _rel(out, ref) < 1e-6
+
+
+@pytest.fixture(scope="module")
+def fp32_engine():
+    _need_gpu()
+    from triton_client_amd.models import densenet_fp32
+
+    eng, model = densenet_fp32.build(max_batch=32, device=DEV)
+    return eng, model
+
+
+@pytest.mark.parametrize("b", [1, 8, 19])
+def test_fp32_engine_matches_fp32_module(fp32_engine, b):
+    """The headline engine: rel-L2 of the logits vs the fp32 torch module
+    (same folded weights) must be fp32-class, < 1e-3 (measured ~1e-5)."""
+    eng, model = fp32_engine
+    g = torch.Generator(device=DEV).manual_seed(100 + b)
+    x = torch.randn(b, 3, 224, 224, device=DEV, generator=g)
+    with torch.no_grad():
+        got = eng(x)
+        ref = model.to(DEV).float()(x)
+    torch.cuda.synchronize()
+    err = _rel(got, ref)
+    print("fp32 engine b=%d rel-L2 vs fp32 module: %.3g" % (b, err))
+    assert err < 1e-3
+
+
+def test_fp32_engine_vs_fp64_and_graph_capture(fp32_engine):
+    """Against an fp64 CPU reference the engine must be as close as torch's
+    own fp32 GPU forward (within 10x); and a captured HIP graph replays the
+    same logits bit for bit."""
+    eng, model = fp32_engine
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = torch.randn(2, 3, 224, 224, device=DEV, generator=g)
+    with torch.no_grad():
+        got = eng(x).clone()
+        ref32 = model.to(DEV).float()(x)
+        ref64 = model.to("cpu").double()(x.cpu().double())
+        model.float()
+    e_eng, e_torch = _rel(got.cpu(), ref64), _rel(ref32.cpu(), ref64)
+    print("vs fp64: engine %.3g, torch fp32 %.3g" % (e_eng, e_torch))
+    assert e_eng < max(10 * e_torch, 1e-5)
+    s = torch.cuda.Stream()
+    out = torch.zeros(32, 1000, device=DEV)
+    eng.ptrs[:2] = eng._img_off[:2] + x.data_ptr()
+    with torch.cuda.stream(s), torch.no_grad():
+        eng.forward_ptrs(2, out=out)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            eng.forward_ptrs(2, out=out)
+        out.zero_()
+        gr.replay()
+    s.synchronize()
+    assert torch.equal(out[:2], got)

@@ -159,6 +159,36 @@ _SIGS = {
          ctypes.c_void_p],
         ctypes.c_int,
     ),
+    # fp32-parity (bf16x3 split-precision) DenseNet kernels (csrc/kernels/densenet_x3.hip)
+    "tcamd_x3_conv1x1_ws_bytes": ([ctypes.c_int, ctypes.c_int], ctypes.c_size_t),
+    "tcamd_x3_conv1x1": (
+        [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+            ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
+    "tcamd_x3_conv3x3": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "tcamd_x3_stem": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+         ctypes.c_int, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "tcamd_x3_head_pool": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+         ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "tcamd_x3_split": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_add_layernorm": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
          ctypes.c_int, ctypes.c_float, ctypes.c_void_p],
@@ -491,6 +521,40 @@ def dn_stem_fused(srcs, x, w, bias, y, imgs, ldy, stream=None):
 def add_layernorm(x, y, gamma, beta, out, rows, H, eps, stream=None):
     """K11: out = LayerNorm(x + y) * gamma + beta over ``rows`` rows of H bf16 (H in 512/1024/2048/4096)."""
     _check(_load().tcamd_add_layernorm(x, y, gamma, beta, out, rows, H, float(eps), _vp(stream)), "add_layernorm")
+
+
+def x3_conv1x1_ws_bytes(M, K):
+    """Split-K workspace bytes K8x wants for an M x K 1x1 conv (0: none)."""
+    return int(_load().tcamd_x3_conv1x1_ws_bytes(int(M), int(K)))
+
+
+def x3_conv1x1(x, ldx, M, K, in_scale, in_bias, w_hi, w_lo, out_bias=None, z_hi=None, z_lo=None, y=None, ldy=0,
+               pool=0, H=0, W=0, ws=None, ws_bytes=0, stream=None):
+    """K8x fp32-parity 1x1 conv (128 out channels): z_hi/z_lo split bf16 planes
+    with bias+ReLU, or raw fp32 into ``y`` rows of ``ldy``."""
+    _check(_load().tcamd_x3_conv1x1(x, ldx, M, K, in_scale, in_bias, w_hi, w_lo, _vp(out_bias), _vp(z_hi),
+                                    _vp(z_lo), _vp(y), int(ldy), int(pool), int(H), int(W), _vp(ws),
+                                    int(ws_bytes), _vp(stream)), "x3_conv1x1")
+
+
+def x3_conv3x3(z_hi, z_lo, imgs, H, W, w_hi, w_lo, y, ldy, stream=None):
+    """K9x fp32-parity 3x3 conv 128 -> 32 into fp32 rows of ``ldy``."""
+    _check(_load().tcamd_x3_conv3x3(z_hi, z_lo, imgs, H, W, w_hi, w_lo, y, ldy, _vp(stream)), "x3_conv3x3")
+
+
+def x3_stem(srcs, w_hi, w_lo, bias, y, imgs, ldy, stream=None):
+    """K10x fp32 stem from a device table of fp32 NCHW image pointers."""
+    _check(_load().tcamd_x3_stem(srcs, w_hi, w_lo, bias, y, imgs, ldy, _vp(stream)), "x3_stem")
+
+
+def x3_head_pool(x, scale, bias, out, imgs, HW, C, stream=None):
+    """K10x head: out[i, c] = mean_p relu(x[i, p, c]*scale[c] + bias[c]), fp32."""
+    _check(_load().tcamd_x3_head_pool(x, scale, bias, out, imgs, HW, C, _vp(stream)), "x3_head_pool")
+
+
+def x3_split(w, hi, lo, n, stream=None):
+    """fp32 -> (bf16 hi, bf16 lo) planes on the device: w ~= hi + lo to 2^-17."""
+    _check(_load().tcamd_x3_split(w, hi, lo, int(n), _vp(stream)), "x3_split")
 
 
 def dn_head_pool(x, scale, bias, out, imgs, HW, C, stream=None):
