@@ -405,6 +405,11 @@ static Error LoadJsonData(const std::string& path, js::Value* first)
 Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t max_slots)
 {
   o_ = o;
+  {
+    static std::atomic<int> seq{0};
+    const int n = seq.fetch_add(1);
+    prefix_ = n == 0 ? std::string("perf_") : "perf" + std::to_string(getpid()) + "_" + std::to_string(n) + "_";
+  }
   const bool shm = o.shared_memory != "none";
   const bool dev = o.shared_memory == "hip";
   const bool json_data = o.input_data != "random" && o.input_data != "zero";
@@ -493,7 +498,7 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
       continue;
     }
     Region r;
-    e = MakeRegion(be, "perf_in_" + t.name, batch_bytes.size(), dev, &r);
+    e = MakeRegion(be, prefix_ + "in_" + t.name, batch_bytes.size(), dev, &r);
     regions_.push_back(r);
     if (!e.IsOk()) return e;
     if (dev) {
@@ -533,7 +538,7 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
       for (auto d : t.shape) fixed = fixed && d >= 0;
       if (fixed) bytes = std::max<size_t>(bytes, static_cast<size_t>(Elements(t.shape)) * es * bs);
       Region r;
-      e = MakeRegion(be, "perf_out_" + t.name + "_" + std::to_string(s), bytes, dev, &r);
+      e = MakeRegion(be, prefix_ + "out_" + t.name + "_" + std::to_string(s), bytes, dev, &r);
       regions_.push_back(r);
       if (!e.IsOk()) return e;
       out->SetSharedMemory(r.name, r.bytes, 0);

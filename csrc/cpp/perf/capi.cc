@@ -54,6 +54,24 @@ int tcperf_run_fixed(void* h, int concurrency, uint64_t total, uint64_t* lat_ns,
   return 0;
 }
 
+// As tcperf_run_fixed, plus each request's completion time (ns after the
+// start) in end_ns, in completion order: lets a caller cut one continuous
+// closed-loop run into back-to-back measurement windows with no drain between.
+int tcperf_run_fixed_timed(void* h, int concurrency, uint64_t total, uint64_t* lat_ns, uint64_t* end_ns,
+                           double* elapsed_s, char* err, int errlen)
+{
+  auto* s = static_cast<tcperf::Session*>(h);
+  std::vector<uint64_t> lat, end;
+  tcperf::Error e = s->engine->RunFixed(static_cast<size_t>(concurrency), total, &lat, elapsed_s, &end);
+  if (lat_ns) memcpy(lat_ns, lat.data(), std::min<size_t>(lat.size(), total) * sizeof(uint64_t));
+  if (end_ns) memcpy(end_ns, end.data(), std::min<size_t>(end.size(), total) * sizeof(uint64_t));
+  if (!e.IsOk()) {
+    SetErr(err, errlen, e.Message());
+    return 1;
+  }
+  return 0;
+}
+
 // out[0..7]: inference_count, execution_count, success_count, success_ns,
 // queue_ns, compute_input_ns, compute_infer_ns, compute_output_ns
 int tcperf_server_stats(void* h, uint64_t* out, char* err, int errlen)

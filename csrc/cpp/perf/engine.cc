@@ -194,6 +194,7 @@ void LoadEngine::Worker()
         std::lock_guard<std::mutex> rl(rec_mu_);
         records_.push_back(d.second);
         if (fixed_lat_) fixed_lat_->push_back(d.second.end_ns - d.second.start_ns);
+        if (fixed_end_) fixed_end_->push_back(d.second.end_ns);
       }
       const size_t slot = d.first;
       slots_[slot].busy = false;
@@ -252,6 +253,7 @@ void LoadEngine::SyncLoop(size_t slot)
       if (!rec.ok && first_error_.empty()) first_error_ = e.IsOk() ? "request failed" : e.Message();
       records_.push_back(rec);
       if (fixed_lat_) fixed_lat_->push_back(rec.end_ns - rec.start_ns);
+      if (fixed_end_) fixed_end_->push_back(rec.end_ns);
     }
     fixed_cv_.notify_all();
   }
@@ -289,7 +291,8 @@ Error LoadEngine::SetConcurrency(size_t n)
   return Error::Success;
 }
 
-Error LoadEngine::RunFixed(size_t concurrency, uint64_t total, std::vector<uint64_t>* lat_ns, double* elapsed_s)
+Error LoadEngine::RunFixed(size_t concurrency, uint64_t total, std::vector<uint64_t>* lat_ns, double* elapsed_s,
+                          std::vector<uint64_t>* end_ns)
 {
   if (concurrency == 0 || concurrency > slots_.size()) return Error("bad concurrency for the prepared slots");
   // quiesce any previous load
@@ -305,6 +308,10 @@ Error LoadEngine::RunFixed(size_t concurrency, uint64_t total, std::vector<uint6
   if (!e.IsOk()) return e;
   lat_ns->clear();
   lat_ns->reserve(total);
+  if (end_ns) {
+    end_ns->clear();
+    end_ns->reserve(total);
+  }
   const size_t first = std::min<uint64_t>(concurrency, total);
   std::unique_lock<std::mutex> lk(mu_);
   fixed_mode_ = true;
@@ -312,6 +319,7 @@ Error LoadEngine::RunFixed(size_t concurrency, uint64_t total, std::vector<uint6
   {
     std::lock_guard<std::mutex> rl(rec_mu_);
     fixed_lat_ = lat_ns;
+    fixed_end_ = end_ns;
   }
   const uint64_t t0 = NowNs();
   if (!o_.async && !o_.streaming) {
@@ -337,7 +345,10 @@ Error LoadEngine::RunFixed(size_t concurrency, uint64_t total, std::vector<uint6
   {
     std::lock_guard<std::mutex> rl(rec_mu_);
     fixed_lat_ = nullptr;
+    fixed_end_ = nullptr;
   }
+  if (end_ns)
+    for (auto& t : *end_ns) t = t > t0 ? t - t0 : 0;
   lk.unlock();
   for (auto& t : sync_threads_)
     if (t.joinable()) t.join();

@@ -203,6 +203,7 @@ class DataSet {
   Error FillHost(const TensorSpec& t, const std::vector<int64_t>& shape, std::vector<uint8_t>* bytes,
                  std::vector<std::string>* strs);
   Options o_;
+  std::string prefix_;  // region names: unique per DataSet (several sessions may share one server)
   std::vector<InferInput*> inputs_;
   std::vector<std::vector<InferRequestedOutput*>> outputs_;  // [slot][output]
   std::vector<std::vector<const InferRequestedOutput*>> outputs_c_;
@@ -228,8 +229,10 @@ class LoadEngine {
   /// Open loop at `rate` requests/sec (distribution from options).
   Error SetRequestRate(double rate);
   /// Closed loop that issues exactly `total` requests and waits for all of
-  /// them; latencies (ns) of those requests are returned in issue order.
-  Error RunFixed(size_t concurrency, uint64_t total, std::vector<uint64_t>* lat_ns, double* elapsed_s);
+  /// them; latencies (ns) are returned in completion order, and with
+  /// `end_ns` each one's completion time (ns after the run started).
+  Error RunFixed(size_t concurrency, uint64_t total, std::vector<uint64_t>* lat_ns, double* elapsed_s,
+                 std::vector<uint64_t>* end_ns = nullptr);
   void Stop();
   /// Records completed since `since_index`; returns the new end index.
   size_t Snapshot(size_t since_index, std::vector<Record>* out);
@@ -272,6 +275,7 @@ class LoadEngine {
   uint64_t fixed_left_ = 0;  // fixed-count mode: requests still to issue
   bool fixed_mode_ = false;
   std::vector<uint64_t>* fixed_lat_ = nullptr;
+  std::vector<uint64_t>* fixed_end_ = nullptr;
   std::atomic<size_t> in_flight_{0};
   std::atomic<bool> stop_{false};
   bool exiting_ = false;

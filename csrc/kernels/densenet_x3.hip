@@ -95,14 +95,14 @@ struct X3Conv1x1Params {
   const float* x;        // [rows][ldx] fp32 (rows = M, or the pre-pool pixels)
   const float* in_scale; // [K] BN scale of the pre-activation
   const float* in_bias;  // [K]
-  const uint16_t* w_hi;  // [128][K] bf16
-  const uint16_t* w_lo;  // [128][K] bf16
-  const float* out_bias; // [128] (SPLIT epilogue: bias + ReLU)
+  const uint16_t* w_hi;  // [N][K] bf16
+  const uint16_t* w_lo;  // [N][K] bf16
+  const float* out_bias; // [N] (SPLIT epilogue: bias + ReLU)
   uint16_t* z_hi;        // SPLIT: [M][128] bf16 planes
   uint16_t* z_lo;
   float* y;              // !SPLIT: [M][ldy] fp32, raw conv output
-  float* ws;             // split-K partials [splits][M][128] (null = whole K per block)
-  int ldx, M, K, ldy, H, W, k_per_split;
+  float* ws;             // split-K partials [splits][M][N] (null = whole K per block)
+  int ldx, M, K, N, ldy, H, W, k_per_split;
 };
 
 constexpr int kBM = 128, kBN = 128, kBK = 32, kLDK = kBK + 8;  // 80-B LDS rows: conflict-free b128 reads
@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(256, 2) x3_conv1x1_kernel(X3Conv1x1Params p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
-  const int m0 = blockIdx.x * kBM;
+  const int m0 = blockIdx.x * kBM, n0 = blockIdx.z * kBN;
 
   // X: 128 rows x 8 chunks of 4 fp32 per K step -> 4 chunks per thread, all
   // at the same K offset (tid & 7); POOL: each chunk averages 4 source rows
@@ -154,8 +154,8 @@ __global__ void __launch_bounds__(256, 2) x3_conv1x1_kernel(X3Conv1x1Params p) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int r = (tid >> 2) + 64 * i;
-    wsh[i] = p.w_hi + (size_t)r * p.K + wk;
-    wsl[i] = p.w_lo + (size_t)r * p.K + wk;
+    wsh[i] = p.w_hi + (size_t)(n0 + r) * p.K + wk;
+    wsl[i] = p.w_lo + (size_t)(n0 + r) * p.K + wk;
   }
 
   f32x4 rx[4][NS], rs, rt;
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(256, 2) x3_conv1x1_kernel(X3Conv1x1Params p) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (SPLIT && !p.ws) b0 = ldf4(p.out_bias + wn * 64 + j * 16 + (lane >> 4) * 4);
+    if (SPLIT && !p.ws) b0 = ldf4(p.out_bias + n0 + wn * 64 + j * 16 + (lane >> 4) * 4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = b0;
   }
@@ -245,14 +245,14 @@ __global__ void __launch_bounds__(256, 2) x3_conv1x1_kernel(X3Conv1x1Params p) {
   // lane holds output channels nb..nb+3 of pixel m
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int nb = wn * 64 + j * 16 + (lane >> 4) * 4;
+    const int nb = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + wm * 64 + i * 16 + fr16;
       if (m >= p.M) continue;
       const f32x4 a = acc[j][i];
       if (p.ws) {
-        *reinterpret_cast<f32x4*>(p.ws + ((size_t)blockIdx.y * p.M + m) * kBN + nb) = a;
+        *reinterpret_cast<f32x4*>(p.ws + ((size_t)blockIdx.y * p.M + m) * p.N + nb) = a;
       } else if constexpr (SPLIT) {
         const f32x4 r = f32x4{fmaxf(a[0], 0.f), fmaxf(a[1], 0.f), fmaxf(a[2], 0.f), fmaxf(a[3], 0.f)};
         v2u h, l;
@@ -269,12 +269,13 @@ __global__ void __launch_bounds__(256, 2) x3_conv1x1_kernel(X3Conv1x1Params p) {
 // split-K combine: out[m][n..n+3] = epi(sum_s ws[s][m][n..n+3] (+ bias))
 template <bool SPLIT>
 __global__ void __launch_bounds__(256) x3_splitk_reduce_kernel(X3Conv1x1Params p, int splits) {
-  const size_t total = (size_t)p.M * (kBN / 4);
+  const int n4 = p.N / 4;
+  const size_t total = (size_t)p.M * n4;
   for (size_t q = blockIdx.x * 256ull + threadIdx.x; q < total; q += (size_t)gridDim.x * 256) {
-    const int m = (int)(q / (kBN / 4)), nb = (int)(q % (kBN / 4)) * 4;
+    const int m = (int)(q / n4), nb = (int)(q % n4) * 4;
     f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
     if (SPLIT) a = ldf4(p.out_bias + nb);
-    for (int s = 0; s < splits; ++s) a += ldf4(p.ws + ((size_t)s * p.M + m) * kBN + nb);
+    for (int s = 0; s < splits; ++s) a += ldf4(p.ws + ((size_t)s * p.M + m) * p.N + nb);
     if constexpr (SPLIT) {
       const f32x4 r = f32x4{fmaxf(a[0], 0.f), fmaxf(a[1], 0.f), fmaxf(a[2], 0.f), fmaxf(a[3], 0.f)};
       v2u h, l;
@@ -607,25 +608,28 @@ bool aligned16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
 extern "C" {
 
-// Split-K workspace bytes the 1x1 conv wants for an M x K problem (0 = none).
-size_t tcamd_x3_conv1x1_ws_bytes(int M, int K) {
-  const int tiles = (M + kBM - 1) / kBM;
+// Split-K workspace bytes the 1x1 conv wants for an M x K -> N problem (0 = none).
+size_t tcamd_x3_conv1x1_ws_bytes(int M, int K, int N) {
+  const int tiles = ((M + kBM - 1) / kBM) * std::max(1, N / kBN);
   if (tiles >= 384 || K < 2 * kBK) return 0;
   const int splits = std::min(K / kBK, (768 + tiles - 1) / tiles);
-  return splits > 1 ? (size_t)splits * M * kBN * sizeof(float) : 0;
+  return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
 }
 
-// 1x1 conv (128 output channels).  split_out: z_hi/z_lo [M][128] bf16 with
-// bias+ReLU; else y fp32 [M][ldy] raw.  pool: x holds the pre-pool H x W
-// pixels, M = imgs * H/2 * W/2.  ws: split-K workspace (may be null).
-int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, const float* in_scale, const float* in_bias,
+// 1x1 conv, N output channels (a multiple of 128).  split_out: z_hi/z_lo
+// [M][128] bf16 with bias+ReLU (N = 128); else y fp32 [M][ldy] raw.  pool: x
+// holds the pre-pool H x W pixels, M = imgs * H/2 * W/2.  ws: split-K
+// workspace (may be null).
+int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, int N, const float* in_scale, const float* in_bias,
                      const void* w_hi, const void* w_lo, const float* out_bias, void* z_hi, void* z_lo, float* y,
                      int ldy, int pool, int H, int W, float* ws, size_t ws_bytes, void* stream) {
   if (M <= 0) return hipSuccess;
   const bool split_out = z_hi != nullptr;
   if (K % kBK || K <= 0 || ldx % 4 || ldx < K || !x || !in_scale || !in_bias || !w_hi || !w_lo)
     return hipErrorInvalidValue;
-  if (split_out ? (!z_lo || !out_bias || !aligned16(z_hi) || !aligned16(z_lo)) : (!y || ldy % 4 || ldy < kBN))
+  if (N <= 0 || N % kBN) return hipErrorInvalidValue;
+  if (split_out ? (N != kBN || !z_lo || !out_bias || !aligned16(z_hi) || !aligned16(z_lo))
+                : (!y || ldy % 4 || ldy < N || !aligned16(y)))
     return hipErrorInvalidValue;
   if (!aligned16(x) || !aligned16(w_hi) || !aligned16(w_lo) || !aligned16(in_scale) || !aligned16(in_bias))
     return hipErrorInvalidValue;
@@ -644,22 +648,23 @@ int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, const float* in_scal
   p.ldx = ldx;
   p.M = M;
   p.K = K;
+  p.N = N;
   p.ldy = ldy;
   p.H = H;
   p.W = W;
   p.k_per_split = K;
   const int tiles = (M + kBM - 1) / kBM;
   int splits = 1;
-  const size_t want = tcamd_x3_conv1x1_ws_bytes(M, K);
+  const size_t want = tcamd_x3_conv1x1_ws_bytes(M, K, N);
   if (want && ws && ws_bytes >= want && aligned16(ws)) {
-    splits = (int)(want / ((size_t)M * kBN * sizeof(float)));
+    splits = (int)(want / ((size_t)M * N * sizeof(float)));
     const int steps = K / kBK;
     p.k_per_split = ((steps + splits - 1) / splits) * kBK;
     splits = (K + p.k_per_split - 1) / p.k_per_split;
     if (splits > 1) p.ws = ws;
   }
   hipStream_t s = (hipStream_t)stream;
-  const dim3 g(tiles, splits);
+  const dim3 g(tiles, splits, N / kBN);
   if (pool) {
     if (split_out) hipLaunchKernelGGL((x3_conv1x1_kernel<true, true>), g, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((x3_conv1x1_kernel<true, false>), g, dim3(256), 0, s, p);
@@ -669,7 +674,7 @@ int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, const float* in_scal
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !p.ws) return e;
-  const int rg = tcamd::grid_for((size_t)M * (kBN / 4));
+  const int rg = tcamd::grid_for((size_t)M * (N / 4));
   if (split_out) hipLaunchKernelGGL(x3_splitk_reduce_kernel<true>, dim3(rg), dim3(256), 0, s, p, splits);
   else hipLaunchKernelGGL(x3_splitk_reduce_kernel<false>, dim3(rg), dim3(256), 0, s, p, splits);
   return hipGetLastError();

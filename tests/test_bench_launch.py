@@ -1,0 +1,55 @@
+"""bench.py's launch contract on CPU: ``--gpus N`` without WORLD_SIZE spawns
+N ranks (torch.distributed.run as a child process), every rank runs the full
+pipeline (server, fan-out of the synthetic batch, native load generator,
+timed windows) and rank 0 prints ONE JSON line aggregated over the ranks.
+``--cpu`` swaps the GPU pieces for the CPU frontend_sink model, system shm
+and gloo, so this runs without a GPU."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from triton_client_amd.perf import native
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.skipif(not native.available(), reason="libperfanalyzer.so not built")
+
+
+def _bench(*args, timeout=240):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.pop("LOCAL_RANK", None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--cpu", "--warmup", "1",
+                        "--concurrency", "4", "--bs1-concurrency", "4", *args],
+                       capture_output=True, text=True, timeout=timeout, cwd=REPO, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0]), r.stderr
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_bench_spawns_ranks_and_aggregates(gpus):
+    res, err = _bench("--gpus", str(gpus), "--steps", "5")
+    assert res["n_gpus"] == gpus
+    assert res["world_size_reported_by_process_group"] == gpus
+    assert res["config"]["parallelism"] == "dp%d" % gpus
+    assert res["steps"] == 5 and res["warmup"] == 1
+    assert res["value"] > 0 and res["p99_latency_us"] >= res["p50_latency_us"] > 0
+    assert len(res["window_infer_per_sec_rank0"]) == 5
+    assert res["bs1"]["infer_per_sec"] > 0
+    if gpus > 1:
+        assert "spawning %d ranks" % gpus in err
+        assert "fanned out by gloo" in res["data"]
+
+
+def test_bench_rejects_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--cpu", "--gpus", "2"],
+                       capture_output=True, text=True, timeout=60, cwd=REPO, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr

@@ -116,7 +116,7 @@ class FusedDenseNetFP32:
                 need = max(need, hip.x3_conv1x1_ws_bytes(n * hw * hw, L["cin"]))
             if bi < len(self.trans):
                 nhw = self.block_dims[bi + 1][0]
-                need = max(need, hip.x3_conv1x1_ws_bytes(n * nhw * nhw, ctot))
+                need = max(need, hip.x3_conv1x1_ws_bytes(n * nhw * nhw, ctot, ctot // 2))
         self.ws = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
 
     def with_workspace(self, max_batch=None):
@@ -163,7 +163,7 @@ class FusedDenseNetFP32:
                 nhw, nct = self.block_dims[bi + 1]
                 hip.x3_conv1x1(fp, ctot, b * nhw * nhw, ctot, T["s"].data_ptr(), T["t"].data_ptr(),
                                T["wh"].data_ptr(), T["wl"].data_ptr(), y=self.feat[bi + 1].data_ptr(), ldy=nct,
-                               pool=1, H=hw, W=hw, ws=ws, ws_bytes=wsb, stream=st)
+                               pool=1, H=hw, W=hw, ws=ws, ws_bytes=wsb, stream=st, N=ctot // 2)
         hw4, c4 = self.block_dims[-1]
         hip.x3_head_pool(self.feat[-1].data_ptr(), self.s5.data_ptr(), self.t5.data_ptr(), self.pooled.data_ptr(),
                          b, hw4 * hw4, c4, stream=st)

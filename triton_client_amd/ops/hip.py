@@ -160,10 +160,10 @@ _SIGS = {
         ctypes.c_int,
     ),
     # fp32-parity (bf16x3 split-precision) DenseNet kernels (csrc/kernels/densenet_x3.hip)
-    "tcamd_x3_conv1x1_ws_bytes": ([ctypes.c_int, ctypes.c_int], ctypes.c_size_t),
+    "tcamd_x3_conv1x1_ws_bytes": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_size_t),
     "tcamd_x3_conv1x1": (
         [
-            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
             ctypes.c_void_p,
@@ -523,16 +523,16 @@ def add_layernorm(x, y, gamma, beta, out, rows, H, eps, stream=None):
     _check(_load().tcamd_add_layernorm(x, y, gamma, beta, out, rows, H, float(eps), _vp(stream)), "add_layernorm")
 
 
-def x3_conv1x1_ws_bytes(M, K):
-    """Split-K workspace bytes K8x wants for an M x K 1x1 conv (0: none)."""
-    return int(_load().tcamd_x3_conv1x1_ws_bytes(int(M), int(K)))
+def x3_conv1x1_ws_bytes(M, K, N=128):
+    """Split-K workspace bytes K8x wants for an M x K -> N 1x1 conv (0: none)."""
+    return int(_load().tcamd_x3_conv1x1_ws_bytes(int(M), int(K), int(N)))
 
 
 def x3_conv1x1(x, ldx, M, K, in_scale, in_bias, w_hi, w_lo, out_bias=None, z_hi=None, z_lo=None, y=None, ldy=0,
-               pool=0, H=0, W=0, ws=None, ws_bytes=0, stream=None):
-    """K8x fp32-parity 1x1 conv (128 out channels): z_hi/z_lo split bf16 planes
-    with bias+ReLU, or raw fp32 into ``y`` rows of ``ldy``."""
-    _check(_load().tcamd_x3_conv1x1(x, ldx, M, K, in_scale, in_bias, w_hi, w_lo, _vp(out_bias), _vp(z_hi),
+               pool=0, H=0, W=0, ws=None, ws_bytes=0, stream=None, N=128):
+    """K8x fp32-parity 1x1 conv (N out channels, a multiple of 128): z_hi/z_lo
+    split bf16 planes with bias+ReLU (N = 128), or raw fp32 into ``y`` rows of ``ldy``."""
+    _check(_load().tcamd_x3_conv1x1(x, ldx, M, K, int(N), in_scale, in_bias, w_hi, w_lo, _vp(out_bias), _vp(z_hi),
                                     _vp(z_lo), _vp(y), int(ldy), int(pool), int(H), int(W), _vp(ws),
                                     int(ws_bytes), _vp(stream)), "x3_conv1x1")
 

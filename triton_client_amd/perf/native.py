@@ -36,6 +36,10 @@ def _load():
                                          ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double),
                                          ctypes.c_char_p, ctypes.c_int]
         lib.tcperf_run_fixed.restype = ctypes.c_int
+        lib.tcperf_run_fixed_timed.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64,
+                                               ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                               ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ctypes.c_int]
+        lib.tcperf_run_fixed_timed.restype = ctypes.c_int
         lib.tcperf_server_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_char_p,
                                             ctypes.c_int]
         lib.tcperf_server_stats.restype = ctypes.c_int
@@ -81,6 +85,20 @@ class PerfSession:
         if rc != 0:
             raise PerfError(err.value.decode(errors="replace"))
         return lat, el.value
+
+    def run_timed(self, concurrency, total):
+        """As :meth:`run_fixed`, plus each request's completion time (ns since
+        the run started); both arrays in completion order."""
+        lat = np.zeros(int(total), dtype=np.uint64)
+        end = np.zeros(int(total), dtype=np.uint64)
+        el = ctypes.c_double(0.0)
+        err = ctypes.create_string_buffer(1024)
+        p64 = ctypes.POINTER(ctypes.c_uint64)
+        rc = _load().tcperf_run_fixed_timed(self._h, int(concurrency), int(total), lat.ctypes.data_as(p64),
+                                            end.ctypes.data_as(p64), ctypes.byref(el), err, 1024)
+        if rc != 0:
+            raise PerfError(err.value.decode(errors="replace"))
+        return lat, end, el.value
 
     def server_stats(self):
         out = (ctypes.c_uint64 * 8)()

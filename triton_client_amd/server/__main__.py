@@ -28,8 +28,9 @@ def main(argv=None):
     ap.add_argument("--max-batch-size", type=int, default=0,
                     help="override densenet_onnx max_batch_size (power of two <= 256; HIP-graph buckets up to it)")
     ap.add_argument("--no-graphs", action="store_true", help="disable HIP graph capture")
-    ap.add_argument("--engine", default="fused", choices=["fused", "torch"],
-                    help="densenet_onnx engine: fused HIP/MFMA kernels or the torch/MIOpen module")
+    ap.add_argument("--engine", default="fp32", choices=["fp32", "fused", "torch"],
+                    help="densenet_onnx engine: fp32 = fp32-parity split-precision HIP/MFMA kernels (default), "
+                         "fused = bf16 HIP/MFMA kernels, torch = the bf16 torch/MIOpen module")
     ap.add_argument("--ready-file", default="", help="touch this file once serving")
     ap.add_argument("--native-grpc", default="auto", choices=["auto", "on", "off"],
                     help="serve the gRPC port with tcserve (C++ front end, csrc/cpp/server)")

@@ -5,12 +5,16 @@ FP32 ``fc6_1`` [1000] out; same I/O contract as Triton's densenet_onnx example)
 served with dynamic batching on one MI355X:
 
   request inputs (device shm views / host tensors)
-    --pointer table (one 1 KB H2D)--> HIP graph replay of DenseNet-121 on the
-        fused K8-K10 MFMA kernels (models/densenet_fused.py); its first
-        kernel (K10s) reads every image straight from its request's fp32
-        NCHW region, so the batch is never assembled.  engine="torch" keeps
-        the MIOpen per-op module, fed by K6 layout_pack (gather+transpose+cvt
-        into one bf16 NHWC batch buffer), for comparison
+    --pointer table (one 1 KB H2D)--> HIP graph replay of DenseNet-121 on
+        hand-written MFMA kernels whose first kernel reads every image
+        straight from its request's fp32 NCHW region (the batch is never
+        assembled).  engine="fp32" (default, the model's FP32 contract):
+        split-precision bf16x3 kernels K8x-K10x (models/densenet_fp32.py),
+        logits within ~4e-5 rel-L2 of the fp32 module.  engine="fused": the
+        bf16 K8-K10 kernels (models/densenet_fused.py), ~2.2x faster, ~3e-2
+        off fp32 — a labelled reduced-precision operating point.
+        engine="torch" keeps the MIOpen per-op bf16 module, fed by K6
+        layout_pack (gather+transpose+cvt into one bf16 NHWC batch buffer)
     --K7 batched_copy--> each request's fp32 logits straight into its output
                          device-shm region (one launch per batch)
 
@@ -48,10 +52,12 @@ class DensenetOnnx(Model):
     C, H, W = 3, 224, 224
     OUT = 1000
 
-    def __init__(self, version=1, device_id=0, buckets=BUCKETS, use_graphs=True, engine="fused", max_batch_size=0,
+    ENGINES = ("fp32", "fused", "torch")
+
+    def __init__(self, version=1, device_id=0, buckets=BUCKETS, use_graphs=True, engine="fp32", max_batch_size=0,
                  **kw):
         super().__init__(version, **kw)
-        if engine not in ("fused", "torch"):
+        if engine not in self.ENGINES:
             raise ServerError("unknown densenet engine %r" % engine)
         self.engine = engine
         self.device_id = int(kw.get("device", device_id))
@@ -83,7 +89,11 @@ class DensenetOnnx(Model):
         torch.cuda.set_device(self.device_id)
         self.torch = torch
         dev = torch.device("cuda", self.device_id)
-        if self.engine == "fused":
+        if self.engine == "fp32":
+            from triton_client_amd.models import densenet_fp32
+
+            self.model, _ = densenet_fp32.build(max(self.buckets), device=dev)
+        elif self.engine == "fused":
             from triton_client_amd.models import densenet_fused
 
             self.model, _ = densenet_fused.build(max(self.buckets), device=dev)
@@ -99,13 +109,13 @@ class DensenetOnnx(Model):
         from triton_client_amd.ops import hip
 
         net = self.model
-        if self.engine == "fused" and self._slots:
+        if self.engine != "torch" and self._slots:
             net = self.model.with_workspace()  # own activation buffers per concurrent stream
         slot = {"stream": torch.cuda.Stream(device=dev), "graphs": {}, "net": net,
                 "ev": [torch.cuda.Event(enable_timing=True) for _ in range(4)]}
         maxb = max(self.buckets)
         img_bytes = self.C * self.H * self.W * 4
-        fused = self.engine == "fused"
+        fused = self.engine != "torch"  # pointer-table engines (fp32 / bf16 fused kernels)
         slot["out"] = torch.zeros(maxb, self.OUT, device=dev, dtype=torch.float32)
         slot["stage_host"] = hip.host_alloc(maxb * img_bytes)
         slot["stage_dev"] = torch.zeros(maxb * self.C * self.H * self.W, device=dev, dtype=torch.float32)
@@ -176,7 +186,7 @@ class DensenetOnnx(Model):
         bucket = next(b for b in self.buckets if b >= rows)
         stream = slot["stream"]
         sh = stream.cuda_stream
-        fused = self.engine == "fused"
+        fused = self.engine != "torch"
         slot["ev"][0].record(stream)
         if fused:
             tbl = slot["ptrs_tbl"]
