@@ -7,6 +7,7 @@ settings update/clear; reference src/c++/tests/cc_client_test.cc)."""
 
 import base64
 import queue
+import threading
 import time
 
 import numpy as np
@@ -293,6 +294,59 @@ def test_grpc_stream_sequence_and_decoupled(cpu_server):
     c.stop_stream()
     with pytest.raises(InferenceServerException):
         c.async_stream_infer("simple", [])
+    c.close()
+
+
+def _repeat_inputs(vals, delay_ms):
+    ins = [grpcclient.InferInput("IN", [len(vals)], "INT32"), grpcclient.InferInput("DELAY", [len(vals)], "UINT32"),
+           grpcclient.InferInput("WAIT", [1], "UINT32")]
+    ins[0].set_data_from_numpy(np.asarray(vals, np.int32))
+    ins[1].set_data_from_numpy(np.full(len(vals), delay_ms, np.uint32))
+    ins[2].set_data_from_numpy(np.zeros(1, np.uint32))
+    return ins
+
+
+def test_grpc_stream_drain_cancel_and_restart(cpu_server):
+    from tritonclient.grpc._infer_stream import StreamState
+
+    c = grpcclient.InferenceServerClient(cpu_server.grpc_url)
+    # stop_stream() without cancel half-closes and waits for every response
+    got = []
+    c.start_stream(lambda result, error: got.append((result, error)))
+    c.async_stream_infer("repeat_int32", _repeat_inputs(list(range(6)), 20))
+    s = c._stream
+    c.stop_stream()
+    assert s.state is StreamState.CLOSED
+    assert [int(r.as_numpy("OUT")[0]) for r, e in got if e is None] == list(range(6))
+    # cancel while responses are still pending: the rpc ends CANCELLED, the
+    # callback sees the cancellation once, and stop returns promptly
+    got2 = []
+    c.start_stream(lambda result, error: got2.append((result, error)))
+    c.async_stream_infer("repeat_int32", _repeat_inputs(list(range(50)), 50))
+    time.sleep(0.2)
+    s2 = c._stream
+    t0 = time.time()
+    c.stop_stream(cancel_requests=True)
+    assert time.time() - t0 < 2.0
+    assert s2.state is StreamState.CANCELLED
+    errs = [e for r, e in got2 if e is not None]
+    assert len(errs) == 1 and "cancel" in str(errs[0]).lower()
+    assert len([r for r, e in got2 if e is None]) < 50
+    with pytest.raises(InferenceServerException):
+        s2.submit(None)
+    # a fresh stream works after a cancelled one; closing from inside the
+    # callback does not deadlock
+    done = threading.Event()
+
+    def cb(result, error):
+        if result is not None and int(result.as_numpy("OUT")[0]) == 2:
+            c._stream.close()
+            done.set()
+
+    c.start_stream(cb)
+    c.async_stream_infer("repeat_int32", _repeat_inputs([0, 1, 2], 1))
+    assert done.wait(10)
+    c.stop_stream()
     c.close()
 
 

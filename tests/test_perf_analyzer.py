@@ -148,10 +148,13 @@ def test_request_rate_poisson(cpu_server):
 def test_request_intervals_file(cpu_server, tmp_path):
     f = tmp_path / "iv.txt"
     f.write_text("\n".join(["2000"] * 10))  # 2 ms apart -> ~500 req/s
-    r = _pa(["-m", "simple", "-u", cpu_server.http_url, "--request-intervals", f, "-p", "400", "-r", "3"])
+    r = _pa(["-m", "simple", "-u", cpu_server.http_url, "--request-intervals", f, "-p", "1000", "-r", "3"])
     assert r.returncode == 0, r.stderr
     thr = float(r.stdout.split("Throughput: ")[1].split()[0])
-    assert 250 < thr < 700
+    # ~500/s scheduled; a CPU-starved host (xdist) can burst a stalled
+    # server's backlog into one window, so only bound it well below the
+    # unthrottled rate (several thousand/s for `simple`)
+    assert 250 < thr < 1500
 
 
 def test_bytes_and_json_data(cpu_server, tmp_path):

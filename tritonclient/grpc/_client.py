@@ -19,7 +19,7 @@ from tritonclient.utils import raise_error
 from .._client import InferenceServerClientBase
 from .._request import Request
 from ._infer_result import InferResult
-from ._infer_stream import _InferStream, _RequestIterator
+from ._infer_stream import StreamSession
 from ._utils import (
     _get_inference_request,
     _grpc_compression_type,
@@ -511,15 +511,15 @@ class InferenceServerClient(InferenceServerClientBase):
         metadata = self._get_metadata(headers)
         if self._verbose:
             print("start_stream, metadata {}".format(metadata))
-        self._stream = _InferStream(callback, self._verbose)
+        self._stream = StreamSession(callback, self._verbose)
         try:
             response_iterator = self._client_stub.ModelStreamInfer(
-                _RequestIterator(self._stream),
+                self._stream.outgoing(),
                 metadata=metadata,
                 timeout=stream_timeout,
                 compression=_grpc_compression_type(compression_algorithm),
             )
-            self._stream._init_handler(response_iterator)
+            self._stream.attach(response_iterator)
         except grpc.RpcError as rpc_error:
             raise_error_grpc(rpc_error)
 
@@ -566,6 +566,6 @@ class InferenceServerClient(InferenceServerClientBase):
             request.parameters["triton_enable_empty_final_response"].bool_param = True
         if self._verbose:
             print("async_stream_infer\n{}".format(request))
-        self._stream._enqueue_request(request)
+        self._stream.submit(request)
         if self._verbose:
             print("enqueued request {} to stream...".format(request_id))

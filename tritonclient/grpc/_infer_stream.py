@@ -1,10 +1,29 @@
-"""Bidirectional ModelStreamInfer engine (reference tritonclient/grpc/_infer_stream.py:39-191).
+"""Bidirectional ModelStreamInfer session.
 
-A request queue feeds grpcio's request iterator; one response thread invokes
-``callback(result=..., error=...)`` for every stream response (decoupled
-models may produce 0..N responses per request).
+Behaviour contract: reference ``tritonclient/grpc/_infer_stream.py:39-191``
+(one active stream per client, responses delivered as
+``callback(result=..., error=...)``, 0..N responses per request for decoupled
+models, ``stop_stream(cancel_requests=...)``).  The design here is our own:
+
+* a :class:`StreamSession` owns an outbox (``deque`` guarded by one
+  ``Condition``) and an explicit lifecycle state::
+
+      IDLE --attach--> OPEN --close()--> DRAINING --server EOF--> CLOSED
+                        |  \\--close(cancel)--> CANCELLED ----------/
+                        \\--rpc error--> FAILED
+
+* grpcio pulls requests from :meth:`StreamSession.outgoing`, a generator that
+  blocks on the condition until a request arrives or the session stops
+  accepting work (the half-close is the generator returning, not a sentinel
+  object in the queue).
+* one dispatch thread consumes the response iterator and runs the user
+  callback; the terminal rpc status (if not a clean EOF) is delivered once
+  through the same callback and moves the session to FAILED/CANCELLED.
+* ``close()`` is idempotent and safe from inside the callback (it never
+  joins the dispatch thread from itself).
 """
-import queue
+import collections
+import enum
 import threading
 
 import grpc
@@ -15,15 +34,92 @@ from ._infer_result import InferResult
 from ._utils import get_cancelled_error, get_error_grpc
 
 
-class _InferStream:
-    def __init__(self, callback, verbose):
+class StreamState(enum.Enum):
+    IDLE = "idle"            # created, no rpc attached yet
+    OPEN = "open"            # accepting requests
+    DRAINING = "draining"    # half-closed: no new requests, waiting for the server's EOF
+    CANCELLED = "cancelled"  # rpc cancelled by the client
+    FAILED = "failed"        # rpc ended with an error (reported via callback)
+    CLOSED = "closed"        # clean end of stream
+
+
+_TERMINAL = (StreamState.CANCELLED, StreamState.FAILED, StreamState.CLOSED)
+
+
+class StreamSession:
+    """One ModelStreamInfer rpc: outbox, dispatch thread and lifecycle."""
+
+    def __init__(self, callback, verbose=False):
         self._callback = callback
         self._verbose = verbose
-        self._request_queue = queue.Queue()
-        self._handler = None
-        self._cancelled = False
-        self._active = True
-        self._response_iterator = None
+        self._cv = threading.Condition()
+        self._outbox = collections.deque()
+        self._state = StreamState.IDLE
+        self._call = None
+        self._dispatcher = None
+
+    # -- lifecycle ------------------------------------------------------------
+    @property
+    def state(self):
+        return self._state
+
+    def _set_state(self, new):
+        # caller holds self._cv
+        if self._state in _TERMINAL:
+            return
+        self._state = new
+        self._cv.notify_all()
+
+    def attach(self, call):
+        """Bind the rpc returned by ``stub.ModelStreamInfer(self.outgoing())``."""
+        with self._cv:
+            if self._state is not StreamState.IDLE:
+                raise_error("stream session is already attached to an rpc")
+            self._call = call
+            self._state = StreamState.OPEN
+        self._dispatcher = threading.Thread(target=self._dispatch, name="triton-grpc-stream", daemon=True)
+        self._dispatcher.start()
+        if self._verbose:
+            print("stream started...")
+
+    def submit(self, request):
+        """Queue one ModelInferRequest for sending."""
+        with self._cv:
+            if self._state is not StreamState.OPEN:
+                raise_error(
+                    "The stream is no longer in valid state (%s); the error detail was "
+                    "reported through the stream callback. Stop this stream and start a "
+                    "new one." % self._state.value
+                )
+            self._outbox.append(request)
+            self._cv.notify_all()
+
+    def close(self, cancel_requests=False):
+        """Stop the session.
+
+        ``cancel_requests=False`` half-closes (requests already queued are
+        still sent) and waits for every response; ``True`` cancels the rpc,
+        dropping queued requests and in-flight responses.
+        """
+        with self._cv:
+            if self._state is StreamState.IDLE:
+                self._state = StreamState.CLOSED
+                return
+            if cancel_requests and self._state not in _TERMINAL:
+                self._outbox.clear()
+                self._set_state(StreamState.CANCELLED)
+                call = self._call
+            else:
+                call = None
+                if self._state is StreamState.OPEN:
+                    self._set_state(StreamState.DRAINING)
+        if call is not None:
+            call.cancel()
+        t = self._dispatcher
+        if t is not None and t is not threading.current_thread() and t.is_alive():
+            t.join()
+            if self._verbose:
+                print("stream stopped...")
 
     def __del__(self):
         try:
@@ -31,71 +127,48 @@ class _InferStream:
         except Exception:
             pass
 
-    def close(self, cancel_requests=False):
-        """Close the stream; optionally cancel pending requests."""
-        if cancel_requests and self._response_iterator:
-            self._response_iterator.cancel()
-            self._cancelled = True
-        if self._handler is not None:
-            if not self._cancelled:
-                self._request_queue.put(None)
-            if self._handler.is_alive() and self._handler is not threading.current_thread():
-                self._handler.join()
-                if self._verbose:
-                    print("stream stopped...")
-            self._handler = None
+    # -- grpc side ------------------------------------------------------------
+    def outgoing(self):
+        """Request generator handed to grpcio (runs on grpcio's sender thread)."""
+        while True:
+            with self._cv:
+                while not self._outbox and self._state in (StreamState.IDLE, StreamState.OPEN):
+                    self._cv.wait()
+                if self._outbox and self._state not in (StreamState.CANCELLED, StreamState.FAILED):
+                    req = self._outbox.popleft()
+                else:
+                    return  # half-close (DRAINING with an empty outbox) or terminal
+            yield req
 
-    def _init_handler(self, response_iterator):
-        self._response_iterator = response_iterator
-        if self._handler is not None:
-            raise_error("Attempted to initialize already initialized InferStream")
-        self._handler = threading.Thread(target=self._process_response, daemon=True)
-        self._handler.start()
-        if self._verbose:
-            print("stream started...")
-
-    def _enqueue_request(self, request):
-        if self._active:
-            self._request_queue.put(request)
-        else:
-            raise_error(
-                "The stream is no longer in valid state, the error detail "
-                "is reported through provided callback. A new stream should "
-                "be started after stopping the current stream."
-            )
-
-    def _get_request(self):
-        return self._request_queue.get()
-
-    def _process_response(self):
+    def _deliver(self, result, error):
         try:
-            for response in self._response_iterator:
+            self._callback(result=result, error=error)
+        except Exception as e:  # a faulty callback must not kill the session silently
+            if self._verbose:
+                print("stream callback raised: %r" % (e,))
+
+    def _dispatch(self):
+        call = self._call
+        try:
+            for response in call:
                 if self._verbose:
                     print(response)
-                result = error = None
-                if response.error_message != "":
-                    error = InferenceServerException(msg=response.error_message)
+                if response.error_message:
+                    self._deliver(None, InferenceServerException(msg=response.error_message))
                 else:
-                    result = InferResult(response.infer_response)
-                self._callback(result=result, error=error)
+                    self._deliver(InferResult(response.infer_response), None)
         except grpc.RpcError as rpc_error:
-            self._active = self._response_iterator.is_active()
-            if rpc_error.code() == grpc.StatusCode.CANCELLED:
-                error = get_cancelled_error(rpc_error.details())
-            else:
-                error = get_error_grpc(rpc_error)
-            self._callback(result=None, error=error)
+            cancelled = rpc_error.code() == grpc.StatusCode.CANCELLED
+            with self._cv:
+                self._set_state(StreamState.CANCELLED if cancelled else StreamState.FAILED)
+            # a cancel the client asked for is reported too (reference
+            # behaviour: the callback sees the CANCELLED status once)
+            err = get_cancelled_error(rpc_error.details()) if cancelled else get_error_grpc(rpc_error)
+            self._deliver(None, err)
+            return
+        with self._cv:
+            self._set_state(StreamState.CLOSED)
 
 
-class _RequestIterator:
-    def __init__(self, stream):
-        self._stream = stream
-
-    def __iter__(self):
-        return self
-
-    def __next__(self):
-        request = self._stream._get_request()
-        if request is None:
-            raise StopIteration
-        return request
+# Names the client module imports (kept for code that reached into them).
+_InferStream = StreamSession
