@@ -42,7 +42,9 @@ def main():
         print("| `%s` | %d | %.1f | %.1f |" % (k, n, ns / 1e3, 100.0 * ns / busy))
     if a.order:
         for r in fwd:
-            print("%8.1f %s" % ((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3, short(r["Kernel_Name"])))
+            print("%8.1f %-40s grid %s wg %s" % ((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3,
+                                                short(r["Kernel_Name"]), r.get("Grid_Size", "?"),
+                                                r.get("Workgroup_Size", "?")))
 
 
 if __name__ == "__main__":
