@@ -269,39 +269,45 @@ int64_t Elements(const std::vector<int64_t>& s)
 }
 
 typedef int (*SynthFillFn)(void*, size_t, int, int, double, double, uint64_t, uint64_t, void*);
+typedef int (*PackBytesFn)(const void*, const uint32_t*, uint64_t, void*, void*, void*);
+typedef uint64_t (*PackBytesWsFn)(uint64_t);
 
-// K1 lives in the framework's libtcamd_hip.so; find it next to this binary's
-// tree (csrc/cpp/build/{bin,lib} -> triton_client_amd/ops/lib) or via
+// K1/K2 live in the framework's libtcamd_hip.so; find it next to this
+// binary's tree (csrc/cpp/build/{bin,lib} -> triton_client_amd/ops/lib) or via
 // $TCAMD_HIP_LIB.
-SynthFillFn FindSynthFill()
+void* HipKernelLib()
 {
-  static SynthFillFn fn = []() -> SynthFillFn {
+  static void* handle = []() -> void* {
     std::vector<std::string> cands;
     if (const char* env = getenv("TCAMD_HIP_LIB")) cands.push_back(env);
     Dl_info info;
-    if (dladdr(reinterpret_cast<void*>(&FindSynthFill), &info) && info.dli_fname) {
+    if (dladdr(reinterpret_cast<void*>(&HipKernelLib), &info) && info.dli_fname) {
       std::string p = info.dli_fname;
       auto slash = p.rfind('/');
       std::string dir = slash == std::string::npos ? "." : p.substr(0, slash);
       cands.push_back(dir + "/../../../../triton_client_amd/ops/lib/libtcamd_hip.so");
     }
-    for (const auto& c : cands) {
-      void* h = dlopen(c.c_str(), RTLD_NOW | RTLD_GLOBAL);
-      if (h) {
-        auto f = reinterpret_cast<SynthFillFn>(dlsym(h, "tcamd_synth_fill"));
-        if (f) return f;
-      }
-    }
+    for (const auto& c : cands)
+      if (void* h = dlopen(c.c_str(), RTLD_NOW | RTLD_GLOBAL)) return h;
     return nullptr;
   }();
-  return fn;
+  return handle;
+}
+
+template <typename F>
+F HipKernel(const char* sym)
+{
+  void* h = HipKernelLib();
+  return h ? reinterpret_cast<F>(dlsym(h, sym)) : nullptr;
 }
 
 }  // namespace
 
 DataSet::~DataSet()
 {
-  for (auto* i : inputs_) delete i;
+  for (auto& v : inputs_)
+    for (auto* i : v) delete i;
+  if (stream_) (void)hipStreamDestroy(static_cast<hipStream_t>(stream_));
   for (auto& v : outputs_)
     for (auto* o : v) delete o;
 }
@@ -337,7 +343,7 @@ Error DataSet::MakeRegion(Backend* be, const std::string& name, size_t bytes, bo
 Error DataSet::FillHost(const TensorSpec& t, const std::vector<int64_t>& shape, std::vector<uint8_t>* bytes,
                         std::vector<std::string>* strs)
 {
-  const int64_t n = Elements(shape);
+  const int64_t n = Elements(shape);  // the whole batch: every element drawn, not one sample replicated
   std::mt19937_64 rng(o_.seed * 1000003ull + std::hash<std::string>()(t.name));
   if (t.datatype == "BYTES") {
     strs->clear();
@@ -387,7 +393,7 @@ Error DataSet::FillHost(const TensorSpec& t, const std::vector<int64_t>& shape, 
   return Error::Success;
 }
 
-static Error LoadJsonData(const std::string& path, js::Value* first)
+static Error LoadJsonData(const std::string& path, std::vector<js::Value>* entries)
 {
   std::ifstream f(path);
   if (!f) return Error("cannot open --input-data file " + path);
@@ -398,11 +404,18 @@ static Error LoadJsonData(const std::string& path, js::Value* first)
   if (!js::Parse(ss.str(), &v, &err)) return Error("bad --input-data JSON: " + err);
   const js::Value* d = v.Find("data");
   if (!d || !d->IsArray() || d->Size() == 0) return Error("--input-data JSON needs a non-empty \"data\" array");
-  *first = (*d)[0];
+  // perf_analyzer's layout: "data": [ {step 0}, {step 1}, ... ] (a nested
+  // array per stream is flattened: every request cycles through all steps)
+  for (const auto& e : d->Elements()) {
+    if (e.IsArray())
+      for (const auto& x : e.Elements()) entries->push_back(x);
+    else
+      entries->push_back(e);
+  }
   return Error::Success;
 }
 
-Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t max_slots)
+Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t max_slots, bool fill_inputs)
 {
   o_ = o;
   {
@@ -413,112 +426,170 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
   const bool shm = o.shared_memory != "none";
   const bool dev = o.shared_memory == "hip";
   const bool json_data = o.input_data != "random" && o.input_data != "zero";
-  js::Value jd;
+  std::vector<js::Value> entries;
   if (json_data) {
-    Error e = LoadJsonData(o.input_data, &jd);
+    Error e = LoadJsonData(o.input_data, &entries);
     if (!e.IsOk()) return e;
   }
+  const size_t n_entries = json_data ? entries.size() : 1;
   const int bs = info.max_batch_size > 0 ? o.batch : 1;
   if (info.max_batch_size == 0 && o.batch > 1) return Error("model does not support batching; use -b 1");
   if (info.max_batch_size > 0 && o.batch > info.max_batch_size)
     return Error("batch " + std::to_string(o.batch) + " exceeds max_batch_size " +
                  std::to_string(info.max_batch_size));
+  hipStream_t st = nullptr;
+  if (dev) {
+    hipError_t he = hipSetDevice(o.device);
+    if (he == hipSuccess) he = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (he != hipSuccess) return Error(std::string("hipStreamCreate failed: ") + hipGetErrorString(he));
+    stream_ = st;
+  }
   std::ostringstream desc;
-  bool used_k1 = false;
-  for (const auto& t : info.inputs) {
-    std::vector<int64_t> shape = t.shape;
-    auto so = o.shapes.find(t.name);
-    if (so != o.shapes.end()) shape = so->second;
-    for (auto d : shape)
-      if (d < 0) return Error("input " + t.name + " has a variable dim; pass --shape " + t.name + ":...");
-    std::vector<int64_t> full = shape;
-    if (info.max_batch_size > 0) full.insert(full.begin(), bs);
-    InferInput* in;
-    Error e = InferInput::Create(&in, t.name, full, t.datatype);
-    if (!e.IsOk()) return e;
-    inputs_.push_back(in);
-
-    // sample data: one sample, replicated over the batch
-    std::vector<uint8_t> sample;
-    std::vector<std::string> strs;
-    if (json_data) {
-      const js::Value* v = jd.Find(t.name);
-      if (!v) return Error("--input-data JSON has no entry for input " + t.name);
-      const js::Value* content = v->IsObject() ? v->Find("content") : v;
-      if (v->IsObject())
-        if (const js::Value* sh = v->Find("shape")) {
-          shape.clear();
-          for (const auto& x : sh->Elements()) shape.push_back(x.AsInt());
-          full = shape;
-          if (info.max_batch_size > 0) full.insert(full.begin(), bs);
-          in->SetShape(full);
-        }
-      if (!content || !content->IsArray()) return Error("--input-data: bad content for " + t.name);
-      const size_t es = DtypeSize(t.datatype);
-      for (const auto& x : content->Elements()) {
-        if (t.datatype == "BYTES") {
-          strs.push_back(x.AsString());
-          continue;
-        }
-        uint8_t buf[8] = {0};
-        if (t.datatype == "FP32") { float f = static_cast<float>(x.AsDouble()); memcpy(buf, &f, 4); }
-        else if (t.datatype == "FP64") { double f = x.AsDouble(); memcpy(buf, &f, 8); }
-        else if (t.datatype == "FP16") { uint16_t f = F32ToF16(static_cast<float>(x.AsDouble())); memcpy(buf, &f, 2); }
-        else if (t.datatype == "BOOL") { buf[0] = x.AsBool() ? 1 : 0; }
-        else { int64_t iv = x.AsInt(); memcpy(buf, &iv, es); }
-        sample.insert(sample.end(), buf, buf + es);
-      }
-      if (t.datatype != "BYTES" && static_cast<int64_t>(sample.size()) != Elements(shape) * (int64_t)es)
-        return Error("--input-data: element count of " + t.name + " does not match its shape");
-    } else {
-      e = FillHost(t, shape, &sample, &strs);
+  bool used_k1 = false, used_k2 = false;
+  inputs_.resize(n_entries);
+  for (size_t ent = 0; ent < n_entries; ++ent) {
+    for (const auto& t : info.inputs) {
+      std::vector<int64_t> shape = t.shape;
+      auto so = o.shapes.find(t.name);
+      if (so != o.shapes.end()) shape = so->second;
+      for (auto d : shape)
+        if (d < 0) return Error("input " + t.name + " has a variable dim; pass --shape " + t.name + ":...");
+      std::vector<int64_t> full = shape;
+      if (info.max_batch_size > 0) full.insert(full.begin(), bs);
+      InferInput* in;
+      Error e = InferInput::Create(&in, t.name, full, t.datatype);
       if (!e.IsOk()) return e;
-    }
-    std::vector<uint8_t> batch_bytes;
-    if (t.datatype == "BYTES") {
-      for (int b = 0; b < bs; ++b)
-        for (const auto& s : strs) {
-          uint32_t len = static_cast<uint32_t>(s.size());
-          const uint8_t* lp = reinterpret_cast<const uint8_t*>(&len);
-          batch_bytes.insert(batch_bytes.end(), lp, lp + 4);
-          batch_bytes.insert(batch_bytes.end(), s.begin(), s.end());
+      inputs_[ent].push_back(in);
+      const std::string rname = prefix_ + "in_" + t.name + (ent ? "_e" + std::to_string(ent) : std::string());
+
+      // device-synthesised data (HIP shm, random): K1 numeric fill, or K1
+      // characters + K2 length-prefixed packing for BYTES; nothing is built
+      // on the host and the batch is NOT one sample replicated
+      const bool k1_numeric = dev && !json_data && t.datatype != "BYTES" && o.input_data == "random";
+      const bool k2_bytes = dev && !json_data && t.datatype == "BYTES" && o.string_data.empty();
+      if ((k1_numeric || k2_bytes) && !o.preregistered_inputs.count(t.name)) {
+        const int64_t n = Elements(full);
+        const size_t bytes = k2_bytes ? static_cast<size_t>(n) * (4 + o.string_length)
+                                      : static_cast<size_t>(n) * DtypeSize(t.datatype);
+        Region r;
+        e = MakeRegion(be, rname, bytes, true, &r);
+        regions_.push_back(r);
+        input_regions_.push_back(regions_.size() - 1);
+        if (!e.IsOk()) return e;
+        if (fill_inputs) {
+          auto k1 = HipKernel<SynthFillFn>("tcamd_synth_fill");
+          if (!k1) return Error("HIP shm synthetic data needs K1 (tcamd_synth_fill in libtcamd_hip.so)");
+          int rc = 0;
+          if (k1_numeric) {
+            const bool fp = t.datatype == "FP32" || t.datatype == "FP16" || t.datatype == "BF16" || t.datatype == "FP64";
+            rc = k1(r.dev, n, DtypeCode(t.datatype), 2 /*uniform*/, 0.0, fp ? 1.0 : 100.0, o.seed, ent, st);
+          } else {
+            auto k2 = HipKernel<PackBytesFn>("tcamd_pack_bytes");
+            auto k2ws = HipKernel<PackBytesWsFn>("tcamd_pack_bytes_workspace");
+            if (!k2 || !k2ws) return Error("HIP shm BYTES data needs K2 (tcamd_pack_bytes in libtcamd_hip.so)");
+            // chars: K1 uniform u8 in ['a', 'a'+26) ('0' for zero data); lens: K1 constant
+            const size_t chars = static_cast<size_t>(n) * o.string_length;
+            void *payload = nullptr, *lens = nullptr, *ws = nullptr;
+            const uint64_t wsb = k2ws(n);
+            hipError_t he = hipMallocAsync(&payload, std::max<size_t>(16, chars), st);
+            if (he == hipSuccess) he = hipMallocAsync(&lens, 4 * static_cast<size_t>(n), st);
+            if (he == hipSuccess) he = hipMallocAsync(&ws, wsb, st);
+            if (he != hipSuccess) return Error(std::string("hipMallocAsync failed: ") + hipGetErrorString(he));
+            if (o.input_data == "zero") rc = k1(payload, chars, DtypeCode("UINT8"), 1 /*const*/, '0', 0, o.seed, ent, st);
+            else rc = k1(payload, chars, DtypeCode("UINT8"), 2 /*uniform*/, 'a', 'a' + 26, o.seed, ent, st);
+            if (rc == 0) rc = k1(lens, n, DtypeCode("UINT32"), 1 /*const*/, o.string_length, 0, 0, 0, st);
+            if (rc == 0) rc = k2(payload, static_cast<const uint32_t*>(lens), n, r.dev, ws, st);
+            (void)hipFreeAsync(payload, st);
+            (void)hipFreeAsync(lens, st);
+            (void)hipFreeAsync(ws, st);
+            used_k2 = true;
+          }
+          if (rc == 0) rc = hipStreamSynchronize(st);
+          if (rc != 0) return Error("device synthetic fill failed: " + std::to_string(rc));
+          used_k1 = true;
         }
-    } else {
-      for (int b = 0; b < bs; ++b) batch_bytes.insert(batch_bytes.end(), sample.begin(), sample.end());
-    }
-    if (!shm) {
-      host_data_.push_back(std::move(batch_bytes));
-      in->AppendRaw(host_data_.back().data(), host_data_.back().size());
-      continue;
-    }
-    auto pre = o.preregistered_inputs.find(t.name);
-    if (pre != o.preregistered_inputs.end()) {
-      in->SetSharedMemory(pre->second, batch_bytes.size(), 0);
-      desc << t.name << ": caller region '" << pre->second << "'; ";
-      continue;
-    }
-    Region r;
-    e = MakeRegion(be, prefix_ + "in_" + t.name, batch_bytes.size(), dev, &r);
-    regions_.push_back(r);
-    if (!e.IsOk()) return e;
-    if (dev) {
-      SynthFillFn k1 = (!json_data && t.datatype != "BYTES") ? FindSynthFill() : nullptr;
-      if (k1 && o.input_data == "random") {
-        // K1: counter-based Philox on the device; identical on every GPU for one seed
-        const size_t n = batch_bytes.size() / DtypeSize(t.datatype);
-        const bool fp = t.datatype == "FP32" || t.datatype == "FP16" || t.datatype == "BF16" || t.datatype == "FP64";
-        int rc = k1(r.dev, n, DtypeCode(t.datatype), 2 /*uniform*/, 0.0, fp ? 1.0 : 100.0, o.seed, 0, nullptr);
-        if (rc == 0) rc = hipDeviceSynchronize();
-        if (rc != 0) return Error("K1 synth_fill failed: " + std::to_string(rc));
-        used_k1 = true;
-      } else {
-        hipError_t he = hipMemcpy(r.dev, batch_bytes.data(), batch_bytes.size(), hipMemcpyHostToDevice);
-        if (he != hipSuccess) return Error(std::string("hipMemcpy failed: ") + hipGetErrorString(he));
+        in->SetSharedMemory(r.name, r.bytes, 0);
+        continue;
       }
-    } else {
-      memcpy(r.host, batch_bytes.data(), batch_bytes.size());
+
+      // host-built data: JSON content, or random/zero without HIP shm
+      std::vector<uint8_t> sample;
+      std::vector<std::string> strs;
+      if (json_data) {
+        const js::Value& jd = entries[ent];
+        const js::Value* v = jd.Find(t.name);
+        if (!v) return Error("--input-data JSON has no entry for input " + t.name);
+        const js::Value* content = v->IsObject() ? v->Find("content") : v;
+        if (v->IsObject())
+          if (const js::Value* sh = v->Find("shape")) {
+            shape.clear();
+            for (const auto& x : sh->Elements()) shape.push_back(x.AsInt());
+            full = shape;
+            if (info.max_batch_size > 0) full.insert(full.begin(), bs);
+            in->SetShape(full);
+          }
+        if (!content || !content->IsArray()) return Error("--input-data: bad content for " + t.name);
+        const size_t es = DtypeSize(t.datatype);
+        for (const auto& x : content->Elements()) {
+          if (t.datatype == "BYTES") {
+            strs.push_back(x.AsString());
+            continue;
+          }
+          uint8_t buf[8] = {0};
+          if (t.datatype == "FP32") { float f = static_cast<float>(x.AsDouble()); memcpy(buf, &f, 4); }
+          else if (t.datatype == "FP64") { double f = x.AsDouble(); memcpy(buf, &f, 8); }
+          else if (t.datatype == "FP16") { uint16_t f = F32ToF16(static_cast<float>(x.AsDouble())); memcpy(buf, &f, 2); }
+          else if (t.datatype == "BOOL") { buf[0] = x.AsBool() ? 1 : 0; }
+          else { int64_t iv = x.AsInt(); memcpy(buf, &iv, es); }
+          sample.insert(sample.end(), buf, buf + es);
+        }
+        if (t.datatype != "BYTES" && static_cast<int64_t>(sample.size()) != Elements(shape) * (int64_t)es)
+          return Error("--input-data: element count of " + t.name + " does not match its shape");
+      } else {
+        // the whole batch (JSON content is one sample: replicated below)
+        e = FillHost(t, full, &sample, &strs);
+        if (!e.IsOk()) return e;
+      }
+      const int reps = json_data ? bs : 1;
+      std::vector<uint8_t> batch_bytes;
+      if (t.datatype == "BYTES") {
+        for (int b = 0; b < reps; ++b)
+          for (const auto& s : strs) {
+            uint32_t len = static_cast<uint32_t>(s.size());
+            const uint8_t* lp = reinterpret_cast<const uint8_t*>(&len);
+            batch_bytes.insert(batch_bytes.end(), lp, lp + 4);
+            batch_bytes.insert(batch_bytes.end(), s.begin(), s.end());
+          }
+      } else {
+        for (int b = 0; b < reps; ++b) batch_bytes.insert(batch_bytes.end(), sample.begin(), sample.end());
+      }
+      if (!shm) {
+        host_data_.push_back(std::move(batch_bytes));
+        in->AppendRaw(host_data_.back().data(), host_data_.back().size());
+        continue;
+      }
+      auto pre = o.preregistered_inputs.find(t.name);
+      if (pre != o.preregistered_inputs.end()) {
+        in->SetSharedMemory(pre->second, batch_bytes.size(), 0);
+        desc << t.name << ": caller region '" << pre->second << "'; ";
+        continue;
+      }
+      Region r;
+      e = MakeRegion(be, rname, batch_bytes.size(), dev, &r);
+      regions_.push_back(r);
+      input_regions_.push_back(regions_.size() - 1);
+      if (!e.IsOk()) return e;
+      if (fill_inputs) {
+        if (dev) {
+          hipError_t he = hipMemcpyAsync(r.dev, batch_bytes.data(), batch_bytes.size(), hipMemcpyHostToDevice, st);
+          if (he == hipSuccess) he = hipStreamSynchronize(st);
+          if (he != hipSuccess) return Error(std::string("hipMemcpy failed: ") + hipGetErrorString(he));
+        } else {
+          memcpy(r.host, batch_bytes.data(), batch_bytes.size());
+        }
+      }
+      in->SetSharedMemory(r.name, r.bytes, 0);
     }
-    in->SetSharedMemory(r.name, r.bytes, 0);
   }
   // outputs: one region per slot per output in shm mode
   const size_t nslot = shm ? std::max<size_t>(1, max_slots) : 1;
@@ -545,13 +616,27 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
     }
   }
   std::ostringstream d2;
-  d2 << (json_data ? "json:" + o.input_data : o.input_data) << " data, ";
+  d2 << (json_data ? "json:" + o.input_data : o.input_data) << " data";
+  if (n_entries > 1) d2 << " (" << n_entries << " entries, cycled per request)";
+  d2 << ", ";
   d2 << (shm ? (dev ? "HIP shared memory (device " + std::to_string(o.device) + ")" : std::string("system shared memory"))
              : std::string("in-band tensors"));
   if (used_k1) d2 << ", inputs filled on device by K1 Philox (seed " << o.seed << ")";
+  if (used_k2) d2 << " + K2 BYTES packing";
+  if (!fill_inputs && !input_regions_.empty()) d2 << ", inputs replicated by fan-out";
   if (!desc.str().empty()) d2 << "; " << desc.str();
   describe_ = d2.str();
   return Error::Success;
+}
+
+std::vector<DataSet::RegionView> DataSet::InputRegions() const
+{
+  std::vector<RegionView> v;
+  for (size_t i : input_regions_) {
+    const Region& r = regions_[i];
+    v.push_back({r.device ? r.dev : r.host, r.bytes, r.device, o_.device});
+  }
+  return v;
 }
 
 void DataSet::Release(Backend* be)

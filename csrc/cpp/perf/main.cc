@@ -18,13 +18,15 @@ int main(int argc, char** argv)
     fprintf(stderr, "error: %s\n\n%s", e.Message().c_str(), tcperf::Usage().c_str());
     return 1;
   }
-  std::unique_ptr<tcperf::Session> s;
-  e = tcperf::Session::Create(o, &s);
+  // one lane per GPU (a single lane without --gpus/--devices)
+  std::unique_ptr<tcperf::MultiSession> s;
+  e = tcperf::MultiSession::Create(o, &s);
   if (!e.IsOk()) {
     fprintf(stderr, "error: %s\n", e.Message().c_str());
     return 1;
   }
-  tcperf::PrintSettings(o, s->info, s->data->Describe());
+  const std::string desc = s->Describe();
+  tcperf::PrintSettings(o, s->lanes[0]->info, desc);
   std::vector<double> loads;
   if (o.rate_mode && o.request_intervals_file.empty()) {
     for (double r = o.rate_start; r <= o.rate_end + 1e-9; r += o.rate_step) loads.push_back(r);
@@ -44,7 +46,7 @@ int main(int argc, char** argv)
            o.rate_mode ? "request rate" : "concurrency", p.load);
     tcperf::PrintPoint(o, p);
   }
-  tcperf::Profiler prof(o, s->backend.get(), s->engine.get());
+  tcperf::Profiler prof(o, s->LanePtrs());
   int rc = 0;
   for (double load : loads) {
     bool done = false;
@@ -60,7 +62,7 @@ int main(int argc, char** argv)
     tcperf::PrintPoint(o, p);
     pts.push_back(p);
     // checkpoint after every point: a killed sweep resumes with --resume
-    tcperf::Error ce = tcperf::WriteJson(o, pts, s->data->Describe());
+    tcperf::Error ce = tcperf::WriteJson(o, pts, desc);
     if (!ce.IsOk()) fprintf(stderr, "error: %s\n", ce.Message().c_str());
     const double lat = o.percentile > 0 ? p.p99_us : p.avg_us;
     if (o.latency_threshold_ms && lat > o.latency_threshold_ms * 1000.0) {
@@ -69,13 +71,13 @@ int main(int argc, char** argv)
       break;
     }
   }
-  s->engine->Stop();
+  for (auto& l : s->lanes) l->engine->Stop();
   std::sort(pts.begin(), pts.end(),
             [](const tcperf::PointResult& a, const tcperf::PointResult& b) { return a.load < b.load; });
   if (!pts.empty()) tcperf::PrintSummary(o, pts);
   e = tcperf::WriteCsv(o, pts);
   if (!e.IsOk()) fprintf(stderr, "error: %s\n", e.Message().c_str());
-  e = tcperf::WriteJson(o, pts, s->data->Describe());
+  e = tcperf::WriteJson(o, pts, desc);
   if (!e.IsOk()) fprintf(stderr, "error: %s\n", e.Message().c_str());
   s.reset();
   return rc;

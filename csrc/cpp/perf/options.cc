@@ -15,7 +15,7 @@ enum LongOnly {
   OPT_SYNC = 1000, OPT_ASYNC, OPT_STREAMING, OPT_SHAPE, OPT_CONC_RANGE, OPT_RATE_RANGE, OPT_DIST, OPT_INTERVALS,
   OPT_SEQ_LEN, OPT_SEQ_RANGE, OPT_INPUT_DATA, OPT_STR_LEN, OPT_STR_DATA, OPT_SHM, OPT_OUT_SHM_SIZE, OPT_MEAS_MODE,
   OPT_MEAS_COUNT, OPT_PERCENTILE, OPT_WARMUP, OPT_VERBOSE_CSV, OPT_JSON, OPT_RESUME, OPT_COLLECT_METRICS, OPT_METRICS_INTERVAL, OPT_METRICS_SYSFS, OPT_SHM_INPUT, OPT_DEVICE, OPT_SEED,
-  OPT_NUM_CLIENTS, OPT_NO_SERVER_STATS, OPT_MEAS_INTERVAL, OPT_STABILITY, OPT_MAX_TRIALS, OPT_LAT_THRESH,
+  OPT_NUM_CLIENTS, OPT_NO_SERVER_STATS, OPT_GPUS, OPT_DEVICES, OPT_FANOUT, OPT_LOAD_PER_GPU, OPT_MEAS_INTERVAL, OPT_STABILITY, OPT_MAX_TRIALS, OPT_LAT_THRESH,
 };
 
 bool ParseU64(const std::string& s, uint64_t* v)
@@ -96,7 +96,14 @@ std::string Usage()
       "  [ext] --device <gpu>             GPU for hip shared memory (default 0)\n"
       "  [ext] --seed <n>                 synthetic data seed (K1 Philox stream)\n"
       "  [ext] --num-clients <n>          protocol clients (connections) to spread requests over\n"
-      "  [ext] --no-server-stats          skip ModelInferenceStatistics deltas\n";
+      "  [ext] --no-server-stats          skip ModelInferenceStatistics deltas\n"
+      "  [ext] --gpus <n> | --devices a,b,c   multi-GPU load: one lane (client, worker thread, HIP stream,\n"
+      "                                   shm regions) per GPU; per-GPU rows + an aggregate row\n"
+      "  [ext] -u url0,url1,...           with several GPUs, lane i talks to url[i mod n]\n"
+      "  [ext] --fanout rccl|p2p|host     how the synthetic batch made once on the first GPU reaches the\n"
+      "                                   others (RCCL broadcast / xGMI peer-copy star / host copies)\n"
+      "  [ext] --load-per-gpu             every GPU gets the full concurrency / rate (weak scaling);\n"
+      "                                   default: the load is split over the GPUs\n";
 }
 
 Error ParseOptions(int argc, char** argv, Options* o, bool* help)
@@ -142,6 +149,10 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
       {"seed", required_argument, nullptr, OPT_SEED},
       {"num-clients", required_argument, nullptr, OPT_NUM_CLIENTS},
       {"no-server-stats", no_argument, nullptr, OPT_NO_SERVER_STATS},
+      {"gpus", required_argument, nullptr, OPT_GPUS},
+      {"devices", required_argument, nullptr, OPT_DEVICES},
+      {"fanout", required_argument, nullptr, OPT_FANOUT},
+      {"load-per-gpu", no_argument, nullptr, OPT_LOAD_PER_GPU},
       {"verbose", no_argument, nullptr, 'v'},
       {"help", no_argument, nullptr, 'h'},
       {nullptr, 0, nullptr, 0}};
@@ -297,6 +308,27 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
         o->num_clients = static_cast<int>(u);
         break;
       case OPT_NO_SERVER_STATS: o->collect_server_stats = false; break;
+      case OPT_GPUS:
+        if (!ParseU64(arg, &u) || u == 0 || u > 64) return Error("bad --gpus (1..64)");
+        o->devices.clear();
+        for (uint64_t d = 0; d < u; ++d) o->devices.push_back(static_cast<int>(d));
+        break;
+      case OPT_DEVICES: {
+        o->devices.clear();
+        std::stringstream ss(arg);
+        std::string tok;
+        while (std::getline(ss, tok, ',')) {
+          if (!ParseU64(tok, &u) || u > 63) return Error("bad --devices entry '" + tok + "'");
+          o->devices.push_back(static_cast<int>(u));
+        }
+        if (o->devices.empty()) return Error("--devices needs at least one GPU");
+        break;
+      }
+      case OPT_FANOUT:
+        if (arg != "rccl" && arg != "p2p" && arg != "host" && arg != "auto") return Error("--fanout: rccl|p2p|host");
+        o->fanout = arg;
+        break;
+      case OPT_LOAD_PER_GPU: o->load_per_gpu = true; break;
       case 'v': o->verbose = true; break;
       case 'h': *help = true; return Error::Success;
       default: {
@@ -308,6 +340,20 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
   if (optind < argc) return Error(std::string("unexpected argument '") + argv[optind] + "'");
   if (o->model.empty()) return Error("-m <model> is required");
   if (o->url.empty()) o->url = o->protocol == "grpc" ? "localhost:8001" : "localhost:8000";
+  {
+    std::stringstream ss(o->url);
+    std::string tok;
+    o->urls.clear();
+    while (std::getline(ss, tok, ','))
+      if (!tok.empty()) o->urls.push_back(tok);
+    if (o->urls.empty()) return Error("bad -u");
+    o->url = o->urls[0];
+  }
+  if (o->devices.empty()) o->devices.push_back(o->device);
+  o->device = o->devices[0];
+  if (o->urls.size() > 1 && o->urls.size() != o->devices.size())
+    return Error("-u lists " + std::to_string(o->urls.size()) + " URLs for " + std::to_string(o->devices.size()) +
+                 " GPUs (give one URL, or one per GPU)");
   if (o->streaming && o->protocol != "grpc") return Error("--streaming requires -i grpc");
   if (!o->preregistered_inputs.empty() && o->shared_memory == "none")
     return Error("--shared-memory-input requires --shared-memory system|hip");

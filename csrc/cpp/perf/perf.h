@@ -25,6 +25,13 @@
 //   Profiler     measurement windows, 3-window stability, percentiles,
 //                server-side breakdown from ModelInferenceStatistics deltas
 //   Reporter     perf_analyzer-style stdout, CSV (-f) and JSON reports
+//   MultiSession (multigpu.cc) --gpus N / --devices: one Session (client,
+//                regions, LoadEngine worker thread, HIP stream) per GPU; the
+//                synthetic batch is made ONCE (K1 on the first GPU) and
+//                replicated into every GPU's regions by a Fanout (RCCL
+//                broadcast, xGMI peer-copy star, or host copies); the
+//                Profiler measures all lanes over common windows and reports
+//                per-GPU rows plus the aggregate row.
 #pragma once
 
 #include <atomic>
@@ -52,6 +59,7 @@ using triton::client::InferRequestedOutput;
 using triton::client::InferResult;
 
 uint64_t NowNs();
+struct Session;
 
 struct Options {
   std::string model;
@@ -82,6 +90,11 @@ struct Options {
   std::map<std::string, std::string> preregistered_inputs;  // input -> registered region name
   int device = 0;
   uint64_t seed = 0;
+  // multi-GPU: one lane per device
+  std::vector<int> devices;        // --gpus N -> 0..N-1, --devices a,b,c; empty -> {device}
+  std::vector<std::string> urls;   // -u a,b,...: lane i talks to urls[i % n]
+  std::string fanout = "auto";     // rccl | p2p | host | auto (rccl for hip shm, host otherwise)
+  bool load_per_gpu = false;       // --load-per-gpu: each lane gets the full load (weak scaling)
   // measurement
   std::string measurement_mode = "time_windows";
   uint64_t measurement_interval_ms = 5000;
@@ -181,9 +194,23 @@ class Backend {
 class DataSet {
  public:
   ~DataSet();
-  Error Init(const Options& o, const ModelInfo& info, Backend* be, size_t max_slots);
-  /// Inputs / outputs of one slot (slots only differ in output regions).
-  const std::vector<InferInput*>& Inputs() const { return inputs_; }
+  /// `fill_inputs` false: input regions are allocated and registered but
+  /// left for a Fanout to fill (the replicas of a multi-GPU run).
+  Error Init(const Options& o, const ModelInfo& info, Backend* be, size_t max_slots, bool fill_inputs = true);
+  /// Inputs of request number `seq` (JSON data with several entries cycles
+  /// through them; synthetic data has one entry).
+  const std::vector<InferInput*>& Inputs(uint64_t seq = 0) const { return inputs_[seq % inputs_.size()]; }
+  size_t Entries() const { return inputs_.size(); }
+  /// Shared-memory input regions in creation order (what a Fanout replicates).
+  struct RegionView {
+    void* ptr;     // device pointer (HIP) or host mapping (system)
+    size_t bytes;
+    bool device;
+    int dev;
+  };
+  std::vector<RegionView> InputRegions() const;
+  /// The lane's HIP stream (K1 fill, fan-out copies), null when not HIP.
+  void* Stream() const { return stream_; }
   const std::vector<const InferRequestedOutput*>& Outputs(size_t slot) const;
   std::string Describe() const { return describe_; }
   void Release(Backend* be);
@@ -204,11 +231,13 @@ class DataSet {
                  std::vector<std::string>* strs);
   Options o_;
   std::string prefix_;  // region names: unique per DataSet (several sessions may share one server)
-  std::vector<InferInput*> inputs_;
+  std::vector<std::vector<InferInput*>> inputs_;              // [entry][input]
   std::vector<std::vector<InferRequestedOutput*>> outputs_;  // [slot][output]
   std::vector<std::vector<const InferRequestedOutput*>> outputs_c_;
   std::vector<std::vector<uint8_t>> host_data_;
   std::vector<Region> regions_;
+  std::vector<size_t> input_regions_;  // indices into regions_
+  void* stream_ = nullptr;             // hipStream_t on o_.device
   std::string describe_;
 };
 
@@ -288,6 +317,7 @@ class LoadEngine {
   std::atomic<uint64_t> rate_gen_{0};
   std::atomic<uint64_t> delayed_{0};  // rate mode: schedule slips that dropped the backlog
   uint64_t next_seq_ = 0;
+  std::atomic<uint64_t> issued_{0};  // request counter (selects the JSON data entry)
   std::string first_error_;
   std::vector<uint64_t> intervals_ns_;
   // streaming: request id -> (slot, send time)
@@ -311,23 +341,35 @@ struct PointResult {
   bool has_server = false;
   bool has_gpu = false;  // --collect-metrics
   double gpu_util_pct = 0, gpu_power_w = 0, gpu_mem_mib = 0;
+  int gpu = -1;                      // lane device (per-GPU rows), -1 = aggregate / single
+  std::vector<PointResult> per_gpu;  // multi-GPU: one row per lane
 };
 
+/// Measures one or more lanes (one per GPU) over COMMON windows: every lane's
+/// records, client and server stats are cut at the same t0/t1, stability is
+/// judged on the aggregate, and a multi-lane point carries per-GPU rows.
 class Profiler {
  public:
-  Profiler(const Options& o, Backend* be, LoadEngine* eng) : o_(o), be_(be), eng_(eng)
-  {
-    if (o.collect_metrics) gpu_.reset(new GpuMetrics(o.device, o.metrics_interval_ms, o.metrics_sysfs_root));
-  }
+  Profiler(const Options& o, Backend* be, LoadEngine* eng) : o_(o) { AddLane(be, eng, o.device, o.url); }
+  Profiler(const Options& o, const std::vector<Session*>& lanes);
   Error Profile(double load, PointResult* out);
+  /// Share of `load` lane i runs (the full load with --load-per-gpu).
+  double LaneLoad(double load, size_t i) const;
 
  private:
-  Error Window(PointResult* w, std::vector<uint64_t>* lat);
+  struct Lane {
+    Backend* be;
+    LoadEngine* eng;
+    int device;
+    bool first_of_url;  // lanes sharing a server count its statistics once in the aggregate
+    size_t rec_index = 0;
+    std::unique_ptr<GpuMetrics> gpu;
+  };
+  void AddLane(Backend* be, LoadEngine* eng, int device, const std::string& url);
+  std::vector<std::string> urls_;
+  Error Window(std::vector<PointResult>* w, std::vector<std::vector<uint64_t>>* lat);
   Options o_;
-  Backend* be_;
-  LoadEngine* eng_;
-  size_t rec_index_ = 0;
-  std::unique_ptr<GpuMetrics> gpu_;
+  std::vector<Lane> lanes_;
 };
 
 void PrintSettings(const Options& o, const ModelInfo& info, const std::string& data_desc);
@@ -347,8 +389,42 @@ struct Session {
   std::unique_ptr<DataSet> data;
   std::unique_ptr<LoadEngine> engine;
   size_t max_slots = 0;
-  static Error Create(const Options& o, std::unique_ptr<Session>* out);
+  static Error Create(const Options& o, std::unique_ptr<Session>* out, bool fill_inputs = true);
   ~Session();
+};
+
+/// Replicates device (or host) buffers from the first lane to the others.
+class Fanout {
+ public:
+  /// mode: rccl | p2p | host.  `devices[0]` is the root.
+  static Error Create(const std::string& mode, const std::vector<int>& devices, std::unique_ptr<Fanout>* out);
+  ~Fanout();
+  /// dst[i] (on devices[i], i >= 1) <- src (on devices[0]); `device` false:
+  /// host buffers (system shm).  Blocks until every copy has landed.
+  Error Broadcast(const void* src, const std::vector<void*>& dst, size_t bytes, bool device);
+  const std::string& Mode() const { return mode_; }
+  double LastUs() const { return last_us_; }
+  double TotalBytes() const { return total_bytes_; }
+
+ private:
+  std::string mode_;
+  std::vector<int> devices_;
+  std::vector<void*> streams_;  // hipStream_t per device
+  std::vector<void*> comms_;    // ncclComm_t per device (rccl)
+  double last_us_ = 0, total_bytes_ = 0;
+};
+
+/// --gpus N: one Session per GPU plus the fan-out of the synthetic batch.
+struct MultiSession {
+  Options opts;
+  std::vector<std::unique_ptr<Session>> lanes;
+  std::unique_ptr<Fanout> fanout;
+  double fanout_us = 0;        // replication wall time (all input regions)
+  bool replicas_verified = false;
+  static Error Create(const Options& o, std::unique_ptr<MultiSession>* out);
+  std::vector<Session*> LanePtrs() const;
+  std::string Describe() const;
+  ~MultiSession();
 };
 
 }  // namespace tcperf

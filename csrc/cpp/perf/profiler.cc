@@ -86,55 +86,126 @@ static double StabilityLatency(const Options& o, const PointResult& r)
   }
 }
 
-Error Profiler::Window(PointResult* w, std::vector<uint64_t>* lat)
+Profiler::Profiler(const Options& o, const std::vector<Session*>& lanes) : o_(o)
+{
+  for (Session* s : lanes) AddLane(s->backend.get(), s->engine.get(), s->opts.device, s->opts.url);
+}
+
+void Profiler::AddLane(Backend* be, LoadEngine* eng, int device, const std::string& url)
+{
+  Lane l;
+  l.be = be;
+  l.eng = eng;
+  l.device = device;
+  l.first_of_url = std::find(urls_.begin(), urls_.end(), url) == urls_.end();
+  urls_.push_back(url);
+  if (o_.collect_metrics) l.gpu.reset(new GpuMetrics(device, o_.metrics_interval_ms, o_.metrics_sysfs_root));
+  lanes_.push_back(std::move(l));
+}
+
+double Profiler::LaneLoad(double load, size_t i) const
+{
+  const size_t n = lanes_.size();
+  if (n <= 1 || o_.load_per_gpu) return load;
+  if (o_.rate_mode) return load / n;
+  // concurrency: integral split, the remainder on the first lanes
+  const uint64_t c = static_cast<uint64_t>(load);
+  return static_cast<double>(c / n + (i < c % n ? 1 : 0));
+}
+
+// One window over every lane, cut at common t0/t1.  w[i] / lat[i] per lane.
+Error Profiler::Window(std::vector<PointResult>* w, std::vector<std::vector<uint64_t>>* lat)
 {
   char tag[96];
-  snprintf(tag, sizeof(tag), "perf.window %s=%g", o_.rate_mode ? "rate" : "concurrency", w->load);
+  snprintf(tag, sizeof(tag), "perf.window %s=%g", o_.rate_mode ? "rate" : "concurrency", (*w)[0].load);
   triton::client::trace::Range range(tag);
-  ServerStats s0, s1;
-  triton::client::InferStat c0, c1;
-  if (o_.collect_server_stats) {
-    Error e = be_->Stats(&s0);
-    if (!e.IsOk()) return e;
+  const size_t n = lanes_.size();
+  std::vector<ServerStats> s0(n), s1(n);
+  std::vector<triton::client::InferStat> c0(n), c1(n);
+  std::vector<size_t> start_count(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (o_.collect_server_stats) {
+      Error e = lanes_[i].be->Stats(&s0[i]);
+      if (!e.IsOk()) return e;
+    }
+    lanes_[i].be->ClientStat(&c0[i]);
   }
-  be_->ClientStat(&c0);
   const uint64_t t0 = NowNs();
-  const size_t start_count = eng_->CompletedCount();
+  for (size_t i = 0; i < n; ++i) start_count[i] = lanes_[i].eng->CompletedCount();
   if (o_.measurement_mode == "count_windows") {
     const uint64_t limit = t0 + 600ull * 1000000000ull;
-    while (eng_->CompletedCount() - start_count < o_.measurement_request_count && NowNs() < limit) {
-      if (!eng_->FirstError().empty()) break;
+    while (NowNs() < limit) {
+      size_t done = 0;
+      bool err = false;
+      for (size_t i = 0; i < n; ++i) {
+        done += lanes_[i].eng->CompletedCount() - start_count[i];
+        err = err || !lanes_[i].eng->FirstError().empty();
+      }
+      if (err || done >= o_.measurement_request_count) break;
       SleepMs(1);
     }
   } else {
     SleepMs(o_.measurement_interval_ms);
   }
   const uint64_t t1 = NowNs();
-  be_->ClientStat(&c1);
-  if (o_.collect_server_stats) {
-    Error e = be_->Stats(&s1);
-    if (!e.IsOk()) return e;
-    w->server = Delta(s0, s1);
-    w->has_server = true;
+  for (size_t i = 0; i < n; ++i) {
+    Lane& L = lanes_[i];
+    PointResult& r = (*w)[i];
+    L.be->ClientStat(&c1[i]);
+    if (o_.collect_server_stats) {
+      Error e = L.be->Stats(&s1[i]);
+      if (!e.IsOk()) return e;
+      r.server = Delta(s0[i], s1[i]);
+      r.has_server = true;
+    }
+    std::vector<Record> recs;
+    L.rec_index = L.eng->Snapshot(L.rec_index, &recs);
+    (*lat)[i].clear();
+    for (const auto& rc : recs) {
+      if (rc.ok) (*lat)[i].push_back(rc.end_ns - rc.start_ns);
+      else r.errors++;
+    }
+    r.request_count = (*lat)[i].size();
+    r.window_s = (t1 - t0) * 1e-9;
+    r.throughput = r.window_s > 0 ? r.request_count * static_cast<double>(o_.batch) / r.window_s : 0;
+    const uint64_t dn = c1[i].completed_request_count - c0[i].completed_request_count;
+    if (dn) {
+      r.client_send_us = (c1[i].cumulative_send_time_ns - c0[i].cumulative_send_time_ns) / 1000.0 / dn;
+      r.client_recv_us = (c1[i].cumulative_receive_time_ns - c0[i].cumulative_receive_time_ns) / 1000.0 / dn;
+    }
+    std::vector<uint64_t> tmp = (*lat)[i];
+    FillLatency(&r, tmp);
   }
-  std::vector<Record> recs;
-  rec_index_ = eng_->Snapshot(rec_index_, &recs);
-  lat->clear();
-  for (const auto& r : recs) {
-    if (r.ok) lat->push_back(r.end_ns - r.start_ns);
-    else w->errors++;
-  }
-  w->request_count = lat->size();
-  w->window_s = (t1 - t0) * 1e-9;
-  w->throughput = w->window_s > 0 ? w->request_count * static_cast<double>(o_.batch) / w->window_s : 0;
-  const uint64_t dn = c1.completed_request_count - c0.completed_request_count;
-  if (dn) {
-    w->client_send_us = (c1.cumulative_send_time_ns - c0.cumulative_send_time_ns) / 1000.0 / dn;
-    w->client_recv_us = (c1.cumulative_receive_time_ns - c0.cumulative_receive_time_ns) / 1000.0 / dn;
-  }
-  std::vector<uint64_t> tmp = *lat;
-  FillLatency(w, tmp);
   return Error::Success;
+}
+
+// Sum lane rows (same window) into one aggregate row.
+static PointResult Aggregate(const std::vector<PointResult>& rows, const std::vector<bool>& count_server,
+                             std::vector<uint64_t>* all_lat)
+{
+  PointResult a;
+  a.load = rows[0].load;
+  a.window_s = rows[0].window_s;
+  double sends = 0, recvs = 0;
+  for (size_t k = 0; k < rows.size(); ++k) {
+    const PointResult& r = rows[k];
+    a.request_count += r.request_count;
+    a.throughput += r.throughput;
+    a.errors += r.errors;
+    sends += r.client_send_us * r.request_count;
+    recvs += r.client_recv_us * r.request_count;
+    if (r.has_server && count_server[k]) {
+      Accumulate(&a.server, r.server);
+      a.has_server = true;
+    }
+  }
+  if (a.request_count) {
+    a.client_send_us = sends / a.request_count;
+    a.client_recv_us = recvs / a.request_count;
+  }
+  std::vector<uint64_t> tmp = *all_lat;
+  FillLatency(&a, tmp);
+  return a;
 }
 
 Error Profiler::Profile(double load, PointResult* out)
@@ -142,39 +213,61 @@ Error Profiler::Profile(double load, PointResult* out)
   *out = PointResult();
   out->load = load;
   out->rate_mode = o_.rate_mode;
-  Error e = o_.rate_mode ? eng_->SetRequestRate(load) : eng_->SetConcurrency(static_cast<size_t>(load));
-  if (!e.IsOk()) return e;
-  if (o_.warmup_requests) {
-    const size_t c0 = eng_->CompletedCount();
-    while (eng_->CompletedCount() - c0 < o_.warmup_requests && eng_->FirstError().empty()) SleepMs(1);
-  }
-  rec_index_ = eng_->CompletedCount();
-  if (gpu_) gpu_->Start();  // samples over this point's windows
-  std::vector<PointResult> wins;
-  std::vector<std::vector<uint64_t>> lats;
-  for (int trial = 0; trial < o_.max_trials; ++trial) {
-    PointResult w;
-    w.load = load;
-    std::vector<uint64_t> lat;
-    e = Window(&w, &lat);
+  const size_t n = lanes_.size();
+  for (size_t i = 0; i < n; ++i) {
+    const double l = LaneLoad(load, i);
+    Error e = o_.rate_mode ? lanes_[i].eng->SetRequestRate(l) : lanes_[i].eng->SetConcurrency(static_cast<size_t>(l));
     if (!e.IsOk()) return e;
-    const std::string err = eng_->FirstError();
-    if (!err.empty()) return Error("request failed: " + err);
+  }
+  if (o_.warmup_requests) {
+    for (auto& L : lanes_) {
+      const size_t c0 = L.eng->CompletedCount();
+      while (L.eng->CompletedCount() - c0 < o_.warmup_requests && L.eng->FirstError().empty()) SleepMs(1);
+    }
+  }
+  for (auto& L : lanes_) {
+    L.rec_index = L.eng->CompletedCount();
+    if (L.gpu) L.gpu->Start();  // samples over this point's windows
+  }
+  std::vector<PointResult> wins;                      // aggregate per window
+  std::vector<std::vector<PointResult>> lane_wins;    // [window][lane]
+  std::vector<std::vector<std::vector<uint64_t>>> lats;  // [window][lane]
+  for (int trial = 0; trial < o_.max_trials; ++trial) {
+    std::vector<PointResult> w(n);
+    for (size_t i = 0; i < n; ++i) {
+      w[i].load = LaneLoad(load, i);
+      w[i].rate_mode = o_.rate_mode;
+      w[i].gpu = lanes_[i].device;
+    }
+    std::vector<std::vector<uint64_t>> lat(n);
+    Error e = Window(&w, &lat);
+    if (!e.IsOk()) return e;
+    for (auto& L : lanes_) {
+      const std::string err = L.eng->FirstError();
+      if (!err.empty()) return Error("request failed: " + err);
+    }
+    std::vector<uint64_t> all;
+    for (const auto& l : lat) all.insert(all.end(), l.begin(), l.end());
+    std::vector<bool> count_server;
+    for (const auto& L : lanes_) count_server.push_back(L.first_of_url);
+    PointResult agg = n == 1 ? w[0] : Aggregate(w, count_server, &all);
+    agg.load = load;
     if (o_.verbose)
       fprintf(stderr, "  window %d: %lu requests, %.1f infer/sec, latency %.0f usec\n", trial,
-              static_cast<unsigned long>(w.request_count), w.throughput, StabilityLatency(o_, w));
-    wins.push_back(w);
+              static_cast<unsigned long>(agg.request_count), agg.throughput, StabilityLatency(o_, agg));
+    wins.push_back(agg);
+    lane_wins.push_back(std::move(w));
     lats.push_back(std::move(lat));
     if (wins.size() >= 3) {
-      const size_t n = wins.size();
+      const size_t m = wins.size();
       double tsum = 0, lsum = 0;
-      for (size_t i = n - 3; i < n; ++i) {
+      for (size_t i = m - 3; i < m; ++i) {
         tsum += wins[i].throughput;
         lsum += StabilityLatency(o_, wins[i]);
       }
       const double tmean = tsum / 3, lmean = lsum / 3, pct = o_.stability_pct / 100.0;
       bool stable = tmean > 0;
-      for (size_t i = n - 3; i < n && stable; ++i) {
+      for (size_t i = m - 3; i < m && stable; ++i) {
         if (std::fabs(wins[i].throughput - tmean) > pct * tmean) stable = false;
         if (std::fabs(StabilityLatency(o_, wins[i]) - lmean) > pct * lmean) stable = false;
       }
@@ -184,27 +277,55 @@ Error Profiler::Profile(double load, PointResult* out)
       }
     }
   }
-  // merge the last (up to) 3 windows
-  const size_t n = wins.size();
-  const size_t from = n >= 3 ? n - 3 : 0;
-  std::vector<uint64_t> all;
-  for (size_t i = from; i < n; ++i) {
-    out->request_count += wins[i].request_count;
-    out->window_s += wins[i].window_s;
-    out->errors += wins[i].errors;
-    out->client_send_us += wins[i].client_send_us / (n - from);
-    out->client_recv_us += wins[i].client_recv_us / (n - from);
-    if (wins[i].has_server) {
-      Accumulate(&out->server, wins[i].server);
-      out->has_server = true;
+  // merge the last (up to) 3 windows, per lane and in aggregate
+  const size_t m = wins.size();
+  const size_t from = m >= 3 ? m - 3 : 0;
+  auto merge = [&](PointResult* dst, auto get_row, auto get_lat) {
+    std::vector<uint64_t> all;
+    for (size_t i = from; i < m; ++i) {
+      const PointResult& r = get_row(i);
+      dst->request_count += r.request_count;
+      dst->window_s += r.window_s;
+      dst->errors += r.errors;
+      dst->client_send_us += r.client_send_us / (m - from);
+      dst->client_recv_us += r.client_recv_us / (m - from);
+      if (r.has_server) {
+        Accumulate(&dst->server, r.server);
+        dst->has_server = true;
+      }
+      get_lat(i, &all);
     }
-    all.insert(all.end(), lats[i].begin(), lats[i].end());
+    dst->throughput = dst->window_s > 0 ? dst->request_count * static_cast<double>(o_.batch) / dst->window_s : 0;
+    FillLatency(dst, all);
+  };
+  merge(out, [&](size_t i) -> const PointResult& { return wins[i]; },
+        [&](size_t i, std::vector<uint64_t>* all) {
+          for (const auto& l : lats[i]) all->insert(all->end(), l.begin(), l.end());
+        });
+  if (n > 1) {
+    for (size_t k = 0; k < n; ++k) {
+      PointResult r;
+      r.load = LaneLoad(load, k);
+      r.rate_mode = o_.rate_mode;
+      r.gpu = lanes_[k].device;
+      r.stable = out->stable;
+      merge(&r, [&](size_t i) -> const PointResult& { return lane_wins[i][k]; },
+            [&](size_t i, std::vector<uint64_t>* all) { all->insert(all->end(), lats[i][k].begin(), lats[i][k].end()); });
+      out->per_gpu.push_back(r);
+    }
   }
-  out->throughput = out->window_s > 0 ? out->request_count * static_cast<double>(o_.batch) / out->window_s : 0;
-  FillLatency(out, all);
-  if (gpu_) {
-    gpu_->Stop();
-    out->has_gpu = gpu_->Summary(&out->gpu_util_pct, &out->gpu_power_w, &out->gpu_mem_mib);
+  for (size_t k = 0; k < n; ++k) {
+    Lane& L = lanes_[k];
+    if (!L.gpu) continue;
+    L.gpu->Stop();
+    PointResult& dst = n > 1 ? out->per_gpu[k] : *out;
+    dst.has_gpu = L.gpu->Summary(&dst.gpu_util_pct, &dst.gpu_power_w, &dst.gpu_mem_mib);
+    if (n > 1 && dst.has_gpu) {  // aggregate: mean utilisation, summed power / memory
+      out->has_gpu = true;
+      out->gpu_util_pct += dst.gpu_util_pct / n;
+      out->gpu_power_w += dst.gpu_power_w;
+      out->gpu_mem_mib += dst.gpu_mem_mib;
+    }
   }
   return Error::Success;
 }
@@ -277,11 +398,24 @@ void PrintPoint(const Options& o, const PointResult& p)
            req, std::max(0.0, req - q - ci - cf - co), q, ci, cf, co);
   }
   if (!p.stable) printf("  [WARNING] measurement did not stabilise within %d windows\n", o.max_trials);
-  printf("\n");
-  fflush(stdout);
   if (p.has_gpu)
     printf("    GPU: utilization %.1f%%, power %.1f W, max memory used %.0f MiB\n", p.gpu_util_pct, p.gpu_power_w,
            p.gpu_mem_mib);
+  if (!p.per_gpu.empty()) {
+    printf("  Per-GPU (%zu lanes, common windows):\n", p.per_gpu.size());
+    for (const auto& g : p.per_gpu) {
+      printf("    GPU %d: %s %g, requests %lu, throughput %.2f infer/sec, p50 %.0f / p90 %.0f / p99 %.0f usec",
+             g.gpu, g.rate_mode ? "rate" : "concurrency", g.load, static_cast<unsigned long>(g.request_count),
+             g.throughput, g.p50_us, g.p90_us, g.p99_us);
+      if (g.has_server && g.server.execution_count)
+        printf(", server batches %lu (avg %.1f rows)", static_cast<unsigned long>(g.server.execution_count),
+               static_cast<double>(g.server.inference_count) / g.server.execution_count);
+      if (g.has_gpu) printf(", GPU util %.1f%%", g.gpu_util_pct);
+      printf("\n");
+    }
+  }
+  printf("\n");
+  fflush(stdout);
 }
 
 void PrintSummary(const Options& o, const std::vector<PointResult>& pts)
@@ -298,6 +432,9 @@ Error WriteCsv(const Options& o, const std::vector<PointResult>& pts)
   if (o.csv_file.empty()) return Error::Success;
   std::ofstream f(o.csv_file);
   if (!f) return Error("cannot write " + o.csv_file);
+  // multi-GPU: a leading GPU column, the aggregate row ("all") then one row per GPU
+  const bool multi = o.devices.size() > 1;
+  if (multi) f << "GPU,";
   f << (o.rate_mode ? "Request Rate" : "Concurrency")
     << ",Inferences/Second,Client Send,Network+Server Send/Recv,Server Queue,Server Compute Input,"
        "Server Compute Infer,Server Compute Output,Client Recv,p50 latency,p90 latency,p95 latency,p99 latency,"
@@ -305,7 +442,7 @@ Error WriteCsv(const Options& o, const std::vector<PointResult>& pts)
   if (o.collect_metrics) f << ",Avg GPU Utilization,Avg GPU Power Usage,Max GPU Memory Usage";
   if (o.verbose_csv) f << ",Failed requests,Stable";
   f << "\n";
-  for (const auto& p : pts) {
+  auto row = [&](const PointResult& p, const std::string& gpu) {
     const ServerStats& s = p.server;
     const double n = s.success_count ? static_cast<double>(s.success_count) : 1.0;
     const double q = s.queue_ns / n / 1000.0, ci = s.compute_input_ns / n / 1000.0,
@@ -315,6 +452,7 @@ Error WriteCsv(const Options& o, const std::vector<PointResult>& pts)
     snprintf(line, sizeof(line), "%g,%.2f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f,%.0f",
              p.load, p.throughput, p.client_send_us, net, q, ci, cf, co, p.client_recv_us, p.p50_us, p.p90_us,
              p.p95_us, p.p99_us, p.avg_us, p.client_send_us, p.client_recv_us);
+    if (multi) f << gpu << ",";
     f << line;
     if (o.collect_metrics) {
       // perf_analyzer's units: utilization as a fraction, power in W, memory in bytes
@@ -324,6 +462,10 @@ Error WriteCsv(const Options& o, const std::vector<PointResult>& pts)
     }
     if (o.verbose_csv) f << "," << p.errors << "," << (p.stable ? 1 : 0);
     f << "\n";
+  };
+  for (const auto& p : pts) {
+    row(p, "all");
+    for (const auto& g : p.per_gpu) row(g, std::to_string(g.gpu));
   }
   return Error::Success;
 }
@@ -333,7 +475,8 @@ Error WriteJson(const Options& o, const std::vector<PointResult>& pts, const std
   if (o.json_file.empty()) return Error::Success;
   std::ofstream f(o.json_file);
   if (!f) return Error("cannot write " + o.json_file);
-  f << "{\"model\":\"" << o.model << "\",\"batch_size\":" << o.batch << ",\"protocol\":\"" << o.protocol
+  f << "{\"model\":\"" << o.model << "\",\"gpus\":" << std::max<size_t>(1, o.devices.size())
+    << ",\"batch_size\":" << o.batch << ",\"protocol\":\"" << o.protocol
     << "\",\"shared_memory\":\"" << o.shared_memory << "\",\"mode\":\"" << (o.rate_mode ? "request_rate" : "concurrency")
     << "\",\"data\":\"" << data_desc << "\",\"points\":[";
   for (size_t i = 0; i < pts.size(); ++i) {
@@ -359,6 +502,25 @@ Error WriteJson(const Options& o, const std::vector<PointResult>& pts, const std
                p.gpu_power_w, p.gpu_mem_mib);
       pt.pop_back();  // reopen the point object
       pt += g;
+    }
+    if (!p.per_gpu.empty()) {
+      std::string rows = ",\"per_gpu\":[";
+      for (size_t k = 0; k < p.per_gpu.size(); ++k) {
+        const auto& g = p.per_gpu[k];
+        char r[512];
+        snprintf(r, sizeof(r),
+                 "%s{\"gpu\":%d,\"load\":%g,\"request_count\":%lu,\"throughput\":%.3f,\"avg_us\":%.1f,"
+                 "\"p50_us\":%.1f,\"p90_us\":%.1f,\"p95_us\":%.1f,\"p99_us\":%.1f,\"errors\":%lu,"
+                 "\"server_inference_count\":%lu,\"server_execution_count\":%lu%s}",
+                 k ? "," : "", g.gpu, g.load, static_cast<unsigned long>(g.request_count), g.throughput, g.avg_us,
+                 g.p50_us, g.p90_us, g.p95_us, g.p99_us, static_cast<unsigned long>(g.errors),
+                 static_cast<unsigned long>(g.server.inference_count),
+                 static_cast<unsigned long>(g.server.execution_count), "");
+        rows += r;
+      }
+      rows += "]}";
+      pt.pop_back();
+      pt += rows;
     }
     f << pt;
   }
@@ -433,7 +595,7 @@ Error LoadCheckpoint(const Options& o, std::vector<PointResult>* pts)
 // ============================================================================
 // Session
 // ============================================================================
-Error Session::Create(const Options& o, std::unique_ptr<Session>* out)
+Error Session::Create(const Options& o, std::unique_ptr<Session>* out, bool fill_inputs)
 {
   std::unique_ptr<Session> s(new Session());
   s->opts = o;
@@ -444,7 +606,7 @@ Error Session::Create(const Options& o, std::unique_ptr<Session>* out)
   if (s->info.decoupled && !o.streaming) return Error("model is decoupled; use --streaming with -i grpc");
   s->max_slots = o.rate_mode ? 64 : static_cast<size_t>(std::max<uint64_t>(1, o.conc_end));
   s->data.reset(new DataSet());
-  e = s->data->Init(o, s->info, s->backend.get(), s->max_slots);
+  e = s->data->Init(o, s->info, s->backend.get(), s->max_slots, fill_inputs);
   if (!e.IsOk()) {
     s->data->Release(s->backend.get());
     return e;

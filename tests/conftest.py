@@ -49,7 +49,7 @@ def gpu_server():
 
     log = os.path.join(os.environ.get("GRAFT_REPO_ROOT", REPO), "gpurun_out", "pytest_gpu_server.log")
     os.makedirs(os.path.dirname(log), exist_ok=True)
-    srv = ServerProcess(device=0, models="simple,densenet_onnx,preprocess_inception,preprocess_inception_ensemble,bert_large",
+    srv = ServerProcess(device=0, models="simple,simple_identity,densenet_onnx,preprocess_inception,preprocess_inception_ensemble,bert_large",
                         log_path=log, extra_args=["--instance-count", "1"])
     try:
         srv.wait_ready(timeout=900, model="densenet_onnx")

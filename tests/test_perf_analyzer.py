@@ -194,3 +194,52 @@ def test_native_session_errors():
         native.PerfSession(["-m", "simple", "-u", "127.0.0.1:1", "--concurrency-range", "1"])
     with pytest.raises(native.PerfError):
         native.PerfSession(["--concurrency-range", "1"])
+
+
+@pytest.mark.parametrize("shm", ["system", "none"])
+def test_multi_lane_host_fanout_per_gpu_rows(cpu_server, tmp_path, shm):
+    """--gpus 2 on CPU: two lanes (clients, worker threads, regions), the
+    synthetic batch made once and host-fanned into lane 1's region (verified
+    byte for byte), per-GPU rows + the aggregate in stdout / CSV / JSON."""
+    f, j = tmp_path / "mg.csv", tmp_path / "mg.json"
+    url = cpu_server.grpc_url
+    r = _pa(["-m", "simple", "-i", "grpc", "-u", "%s,%s" % (url, url), "--gpus", "2", "--shared-memory", shm,
+             "--concurrency-range", "4:6:2", "-p", "300", "-r", "4", "-s", "50", "-f", f, "--json-report", j,
+             "--fanout", "host"])
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "2 GPUs [0,1]" in r.stdout and "load split over GPUs" in r.stdout
+    if shm == "system":
+        assert "fanned out by host" in r.stdout and "replicas verified" in r.stdout
+    assert r.stdout.count("Per-GPU (2 lanes") == 2
+    rows = list(csv.DictReader(open(f)))
+    assert [x["GPU"] for x in rows] == ["all", "0", "1", "all", "0", "1"]
+    for k in (0, 3):
+        agg, g0, g1 = rows[k:k + 3]
+        assert abs(float(agg["Inferences/Second"]) - float(g0["Inferences/Second"]) - float(g1["Inferences/Second"])) \
+            < 0.02 * float(agg["Inferences/Second"]) + 1
+    rep = json.load(open(j))
+    assert rep["gpus"] == 2
+    for p, conc in zip(rep["points"], (4, 6)):
+        assert p["load"] == conc
+        assert [g["gpu"] for g in p["per_gpu"]] == [0, 1]
+        assert sum(g["load"] for g in p["per_gpu"]) == conc
+        assert sum(g["request_count"] for g in p["per_gpu"]) == p["request_count"]
+
+
+def test_multi_lane_full_load_per_gpu_and_url_count(cpu_server):
+    url = cpu_server.http_url
+    r = _pa(["-m", "simple", "-u", url, "--gpus", "3", "--load-per-gpu", "--concurrency-range", "2", "-p", "250",
+             "-r", "3", "-s", "60"])
+    assert r.returncode == 0, r.stderr
+    assert "full load per GPU" in r.stdout
+    assert r.stdout.count("concurrency 2,") == 3  # every lane runs the full concurrency
+    r = _pa(["-m", "simple", "-u", "%s,%s" % (url, url), "--gpus", "3"])
+    assert r.returncode == 1 and "2 URLs for 3 GPUs" in r.stderr
+
+
+def test_json_data_multiple_entries_cycle(cpu_server, tmp_path):
+    d = tmp_path / "steps.json"
+    d.write_text(json.dumps({"data": [{"INPUT0": [i] * 16, "INPUT1": [1] * 16} for i in range(3)]}))
+    r = _pa(["-m", "simple", "-u", cpu_server.http_url, "--input-data", d, "-p", "200", "-r", "3", "-s", "60"])
+    assert r.returncode == 0, r.stderr
+    assert "3 entries, cycled per request" in r.stdout
