@@ -6,13 +6,27 @@
 // pack: 3 launches
 //   1. per-block exclusive scan of the u32 lengths in LDS (1024 per block:
 //      256 threads x 4, Hillis-Steele over wave partials)
-//   2. single-block scan of the block totals
-//   3. scatter: element i goes to out + in_off[i] + 4*i (prefix + payload)
-// unpack (index): one workgroup walks the length chain; the buffer is staged
-//   through a 32 KiB LDS window loaded cooperatively with 16-B loads, so each
-//   hop costs an LDS read instead of a dependent HBM round trip.  The walk is
-//   inherently sequential — the index lets every later consumer run in
-//   parallel.
+//   2. single-block scan of the block totals (+ the grand total)
+//   3. OUTPUT-centric emit: every thread builds one 16-B chunk of the packed
+//      stream and writes it with one dwordx4 store (fully coalesced whatever
+//      the length distribution: one long string is spread over all lanes,
+//      many short ones are packed by one lane).  The owner element of a chunk
+//      is found by a two-level binary search over the element start offsets
+//      (block level, then inside the 1024-element block; neighbouring lanes
+//      search the same lines), then the chunk walks forward across element
+//      boundaries (length prefix bytes, then payload bytes).
+// unpack (index), by size:
+//   * <= 64 KiB: one workgroup walks the length chain through a 32 KiB LDS
+//     window (each hop an LDS read, not a dependent HBM round trip);
+//   * larger: a parallel 3-phase walk over 8 KiB blocks —
+//     1. every byte position p of a block is a candidate element start:
+//        next(p) = p + 4 + len(p); pointer DOUBLING in LDS (11 rounds) gives,
+//        for every p, the first chain position at or past the block end and
+//        the number of elements started on the way (exit/count tables);
+//     2. one lane chains the blocks: entry(b+1) = exit(entry(b)), element
+//        base index += count — one hop per 8 KiB instead of one per element;
+//     3. every block re-walks from its entry in LDS and writes its elements'
+//        offsets/lengths at base(b) + k.
 
 #include "kernels/common.h"
 
@@ -85,25 +99,67 @@ __global__ void __launch_bounds__(kBlock) scan_block_sums(uint64_t* __restrict__
     carry += total;
     __syncthreads();
   }
+  if (threadIdx.x == 0) block_sums[nb] = carry;  // total payload bytes
 }
 
-__global__ void __launch_bounds__(kBlock) scatter_elements(const uint8_t* __restrict__ data,
-                                                           const uint32_t* __restrict__ lens,
-                                                           const uint64_t* __restrict__ offs,
-                                                           const uint64_t* __restrict__ block_sums,
-                                                           uint64_t n, uint8_t* __restrict__ out) {
+// Packed-stream start of element i: payload bytes before it + 4 per prefix.
+__device__ __forceinline__ uint64_t in_start(const uint64_t* offs, const uint64_t* bsum, uint64_t i) {
+  return offs[i] + bsum[i / kSpan];
+}
+
+__global__ void __launch_bounds__(kBlock) emit_packed(const uint8_t* __restrict__ data,
+                                                      const uint32_t* __restrict__ lens,
+                                                      const uint64_t* __restrict__ offs,
+                                                      const uint64_t* __restrict__ bsum, uint64_t n, uint64_t nb,
+                                                      uint8_t* __restrict__ out) {
+  const uint64_t total = bsum[nb] + 4 * n;
+  const uint64_t nchunks = (total + 15) / 16;
+  const bool out_aligned = (((uintptr_t)out) & 15) == 0;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint64_t in_off = offs[i] + block_sums[i / kSpan];
-    const uint64_t out_off = in_off + 4 * i;
-    const uint32_t L = lens[i];
-    out[out_off + 0] = (uint8_t)(L);
-    out[out_off + 1] = (uint8_t)(L >> 8);
-    out[out_off + 2] = (uint8_t)(L >> 16);
-    out[out_off + 3] = (uint8_t)(L >> 24);
-    const uint8_t* s = data + in_off;
-    uint8_t* d = out + out_off + 4;
-    for (uint32_t j = 0; j < L; ++j) d[j] = s[j];
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += stride) {
+    const uint64_t pos0 = c * 16;
+    // block level: last block whose first element starts at or before pos0
+    uint64_t lo = 0, hi = nb;  // invariant: ostart(first of lo) <= pos0
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (bsum[mid] + 4 * mid * (uint64_t)kSpan <= pos0) lo = mid;
+      else hi = mid;
+    }
+    uint64_t elo = lo * kSpan, ehi = (lo + 1) * (uint64_t)kSpan < n ? (lo + 1) * (uint64_t)kSpan : n;
+    while (ehi - elo > 1) {
+      const uint64_t mid = (elo + ehi) >> 1;
+      if (in_start(offs, bsum, mid) + 4 * mid <= pos0) elo = mid;
+      else ehi = mid;
+    }
+    uint64_t e = elo;
+    uint64_t es = in_start(offs, bsum, e);        // payload start of e in `data`
+    uint64_t os = es + 4 * e;                     // packed start of e
+    uint32_t L = lens[e];
+    uint64_t oe = os + 4 + L;                     // packed end of e
+    union {
+      uint4 v;
+      uint8_t b[16];
+    } chunk;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint64_t pos = pos0 + k;
+      while (pos >= oe && e + 1 < n) {  // cross into the next element(s)
+        ++e;
+        es = in_start(offs, bsum, e);
+        os = es + 4 * e;
+        L = lens[e];
+        oe = os + 4 + L;
+      }
+      const uint64_t local = pos - os;
+      uint8_t byte = 0;
+      if (pos < total) byte = local < 4 ? (uint8_t)(L >> (8 * local)) : data[es + (local - 4)];
+      chunk.b[k] = byte;
+    }
+    if (out_aligned && pos0 + 16 <= total) {
+      *reinterpret_cast<uint4*>(out + pos0) = chunk.v;
+    } else {
+      for (int k = 0; k < 16 && pos0 + k < total; ++k) out[pos0 + k] = chunk.b[k];
+    }
   }
 }
 
@@ -168,6 +224,143 @@ __global__ void __launch_bounds__(kBlock) index_bytes(const uint8_t* __restrict_
   }
 }
 
+// ---- K3 large inputs: parallel 3-phase walk over 8 KiB blocks --------------
+constexpr int kIdxB = 8192;                 // bytes per block
+constexpr int kIdxPer = kIdxB / kBlock;     // positions per thread (32)
+constexpr uint64_t kBad = ~(uint64_t)0;     // malformed element on the chain
+constexpr uint64_t kNone = ~(uint64_t)0 - 1;  // block not entered / past n_expected
+
+__device__ __forceinline__ void stage_block(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t b0,
+                                            uint8_t* win) {
+  // kIdxB + 16 bytes (a length prefix may straddle the block end); zero past nbytes
+  const bool aligned = ((((uintptr_t)buf) + b0) & 15) == 0;
+  for (int v = threadIdx.x; v < (kIdxB + 16) / 16; v += blockDim.x) {
+    const uint64_t g = b0 + 16 * (uint64_t)v;
+    if (aligned && g + 16 <= nbytes) {
+      reinterpret_cast<uint4*>(win)[v] = *reinterpret_cast<const uint4*>(buf + g);
+    } else {
+      for (int k = 0; k < 16; ++k) win[16 * v + k] = (g + k < nbytes) ? buf[g + k] : 0;
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t le32(const uint8_t* q) {
+  return (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+}
+
+// Phase 1: exit/count of every candidate start position of one block.
+__global__ void __launch_bounds__(kBlock) idx_blocks(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                     uint64_t* __restrict__ exit_pos,
+                                                     uint16_t* __restrict__ count) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[kIdxB + 16];
+  __shared__ uint64_t nxt[kIdxB];
+  __shared__ uint16_t cnt[kIdxB];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kIdxB;
+  const uint64_t bend = b0 + kIdxB;
+  stage_block(buf, nbytes, b0, win);
+  __syncthreads();
+  // interleaved ownership (q = threadIdx.x + k*256): conflict-free LDS rows
+#pragma unroll 4
+  for (int k = 0; k < kIdxPer; ++k) {
+    const int q = threadIdx.x + k * kBlock;
+    const uint64_t p = b0 + q;
+    uint64_t x = kBad;
+    if (p + 4 <= nbytes) {
+      const uint64_t e = p + 4 + (uint64_t)le32(win + q);
+      if (e <= nbytes) x = e;
+    }
+    nxt[q] = (p < nbytes) ? x : kNone;
+    cnt[q] = (x == kBad || p >= nbytes) ? 0 : 1;
+  }
+  __syncthreads();
+  // pointer doubling: 2^11 = 2048 >= kIdxB/4 hops per block
+  for (int round = 0; round < 11; ++round) {
+    uint64_t nx[kIdxPer];
+    uint16_t nc[kIdxPer];
+#pragma unroll
+    for (int k = 0; k < kIdxPer; ++k) {
+      const int q = threadIdx.x + k * kBlock;
+      uint64_t x = nxt[q];
+      uint16_t c = cnt[q];
+      if (x != kBad && x != kNone && x < bend) {
+        const int j = (int)(x - b0);
+        c = (uint16_t)(c + cnt[j]);
+        x = nxt[j];
+      }
+      nx[k] = x;
+      nc[k] = c;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kIdxPer; ++k) {
+      const int q = threadIdx.x + k * kBlock;
+      nxt[q] = nx[k];
+      cnt[q] = nc[k];
+    }
+    __syncthreads();
+  }
+#pragma unroll 4
+  for (int k = 0; k < kIdxPer; ++k) {
+    const int q = threadIdx.x + k * kBlock;
+    if (b0 + q < nbytes) {
+      exit_pos[b0 + q] = nxt[q];
+      count[b0 + q] = cnt[q];
+    }
+  }
+}
+
+// Phase 2: one lane chains the blocks.  entry[b] = first chain position in
+// block b (kNone if the chain skips it or is done), base[b] = its element index.
+__global__ void idx_chain(const uint64_t* __restrict__ exit_pos, const uint16_t* __restrict__ count,
+                          uint64_t nbytes, uint64_t nblk, uint64_t n_expected, uint64_t* __restrict__ entry,
+                          uint64_t* __restrict__ base, int* __restrict__ status) {
+  if (threadIdx.x != 0) return;
+  uint64_t p = 0, idx = 0;
+  int err = 0;
+  for (uint64_t b = 0; b < nblk; ++b) {
+    const uint64_t bend = (b + 1) * (uint64_t)kIdxB;
+    if (err || idx >= n_expected || p >= nbytes || p >= bend) {
+      entry[b] = kNone;
+      continue;
+    }
+    entry[b] = p;
+    base[b] = idx;
+    const uint64_t x = exit_pos[p];
+    idx += count[p];
+    if (x == kBad) {
+      if (idx < n_expected) err = 1;  // the malformed element is one the caller asked for
+      p = nbytes;
+    } else {
+      p = x;
+    }
+  }
+  status[0] = err ? -1 : (idx >= n_expected ? 0 : 1);
+  reinterpret_cast<uint64_t*>(status + 2)[0] = idx < n_expected ? idx : n_expected;
+}
+
+// Phase 3: each entered block re-walks its elements from the entry in LDS.
+__global__ void __launch_bounds__(kBlock) idx_emit(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                   const uint64_t* __restrict__ entry,
+                                                   const uint64_t* __restrict__ base, uint64_t n_expected,
+                                                   uint64_t* __restrict__ offs, uint32_t* __restrict__ lens) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[kIdxB + 16];
+  const uint64_t p0 = entry[blockIdx.x];
+  if (p0 == kNone) return;  // uniform per block
+  const uint64_t b0 = (uint64_t)blockIdx.x * kIdxB, bend = b0 + kIdxB;
+  stage_block(buf, nbytes, b0, win);
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  uint64_t p = p0, idx = base[blockIdx.x];
+  while (p < bend && p + 4 <= nbytes && idx < n_expected) {
+    const uint32_t L = le32(win + (p - b0));
+    if (p + 4 + (uint64_t)L > nbytes) break;  // reported by phase 2
+    offs[idx] = p + 4;
+    lens[idx] = L;
+    ++idx;
+    p += 4 + (uint64_t)L;
+  }
+}
+
 }  // namespace
 
 // workspace must hold n*8 + ceil(n/1024)*8 bytes (see tcamd_pack_bytes_workspace).
@@ -184,8 +377,8 @@ extern "C" int tcamd_pack_bytes(const void* data, const uint32_t* lens, uint64_t
   uint64_t* bsum = offs + n;
   hipLaunchKernelGGL(scan_lengths, dim3((unsigned)nb), dim3(kBlock), 0, s, lens, n, offs, bsum);
   hipLaunchKernelGGL(scan_block_sums, dim3(1), dim3(kBlock), 0, s, bsum, nb);
-  hipLaunchKernelGGL(scatter_elements, dim3(grid_for(n)), dim3(kBlock), 0, s, (const uint8_t*)data, lens,
-                     offs, bsum, n, (uint8_t*)out);
+  hipLaunchKernelGGL(emit_packed, dim3(grid_for(n < 4096 ? 4096 : n)), dim3(kBlock), 0, s,
+                     (const uint8_t*)data, lens, offs, bsum, n, nb, (uint8_t*)out);
   return hipGetLastError();
 }
 
@@ -194,7 +387,28 @@ extern "C" int tcamd_pack_bytes(const void* data, const uint32_t* lens, uint64_t
 extern "C" int tcamd_index_bytes(const void* buf, uint64_t nbytes, uint64_t n_expected, uint64_t* offs,
                                  uint32_t* lens, int* status, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(index_bytes, dim3(1), dim3(kBlock), 0, s, (const uint8_t*)buf, nbytes, n_expected, offs,
-                     lens, status);
-  return hipGetLastError();
+  if (nbytes <= 65536 || n_expected < 2048) {
+    hipLaunchKernelGGL(index_bytes, dim3(1), dim3(kBlock), 0, s, (const uint8_t*)buf, nbytes, n_expected, offs,
+                       lens, status);
+    return hipGetLastError();
+  }
+  // parallel path: stream-ordered scratch (exit u64 + count u16 per byte, entry/base per block)
+  const uint64_t nblk = (nbytes + kIdxB - 1) / kIdxB;
+  void* ws = nullptr;
+  const size_t wsb = nbytes * 8 + nbytes * 2 + 16 + nblk * 16;
+  hipError_t e = hipMallocAsync(&ws, wsb, s);
+  if (e != hipSuccess) return e;
+  uint64_t* exit_pos = (uint64_t*)ws;
+  uint16_t* count = (uint16_t*)(exit_pos + nbytes);
+  uint64_t* entry = (uint64_t*)(((uintptr_t)(count + nbytes) + 15) & ~(uintptr_t)15);
+  uint64_t* base = entry + nblk;
+  hipLaunchKernelGGL(idx_blocks, dim3((unsigned)nblk), dim3(kBlock), 0, s, (const uint8_t*)buf, nbytes, exit_pos,
+                     count);
+  hipLaunchKernelGGL(idx_chain, dim3(1), dim3(64), 0, s, exit_pos, count, nbytes, nblk, n_expected, entry, base,
+                     status);
+  hipLaunchKernelGGL(idx_emit, dim3((unsigned)nblk), dim3(kBlock), 0, s, (const uint8_t*)buf, nbytes, entry, base,
+                     n_expected, offs, lens);
+  e = hipGetLastError();
+  hipError_t f = hipFreeAsync(ws, s);
+  return e != hipSuccess ? e : f;
 }

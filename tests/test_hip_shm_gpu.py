@@ -49,6 +49,32 @@ def test_bytes_roundtrip(hipshm):
     hipshm.destroy_shared_memory_region(h)
 
 
+def test_unserialized_bytes_packed_by_k2_and_indexed_by_k3(hipshm):
+    """set_shared_memory_region with a raw BYTES tensor serialises it on the
+    device (K2) into the region; get_contents_as_numpy indexes it on the device
+    (K3, parallel block walk at this size).  Bytes must equal the host codec's."""
+    from tritonclient.utils import serialize_byte_tensor
+
+    rng = np.random.default_rng(3)
+    data = np.array([bytes(rng.integers(0, 256, int(rng.integers(0, 60)), dtype=np.uint8)) for _ in range(20000)],
+                    dtype=np.object_).reshape(100, 200)
+    ser = serialize_byte_tensor(data).item()
+    head = np.arange(8, dtype=np.int32)
+    h = hipshm.create_shared_memory_region("rk2", 32 + len(ser) + 256, 0)
+    hipshm.set_shared_memory_region(h, [head, data])  # int32 head, then K2 at offset 32
+    raw = hipshm.get_contents_as_numpy(h, np.uint8, [32 + len(ser)])
+    assert raw[32:].tobytes() == ser
+    out = hipshm.get_contents_as_numpy(h, np.object_, [100, 200], offset=32)
+    assert out.shape == (100, 200) and list(out.ravel()) == list(data.ravel())
+    # asking for more elements than the region holds is an error, not garbage
+    small = hipshm.create_shared_memory_region("rk3", len(serialize_byte_tensor(data[:1]).item()), 0)
+    hipshm.set_shared_memory_region(small, [data[:1]])
+    with pytest.raises(hipshm.CudaSharedMemoryException):
+        hipshm.get_contents_as_numpy(small, np.object_, [400])
+    hipshm.destroy_shared_memory_region(small)
+    hipshm.destroy_shared_memory_region(h)
+
+
 def test_dlpack_roundtrip_torch(hipshm):
     import torch
 

@@ -230,6 +230,51 @@ def test_pack_and_index_bytes_match_wire_format(env):
     np.testing.assert_array_equal(offs.cpu().numpy(), exp_offs)
 
 
+@pytest.mark.parametrize("n,maxlen,seed", [(300000, 24, 5), (4000, 6000, 6), (70000, 1, 7)])
+def test_pack_and_index_bytes_large(env, n, maxlen, seed):
+    """K2 output-centric emit and the K3 parallel block walk on large inputs:
+    many short strings, few very long ones (each spans many 16-B chunks and
+    several 8 KiB index blocks), and all-but-empty elements."""
+    torch, hip = env
+    from tritonclient.utils import serialize_byte_tensor
+
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, maxlen + 1, n).astype(np.uint32)
+    payload = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    d_payload = torch.from_numpy(payload).cuda() if payload.size else torch.zeros(16, device="cuda", dtype=torch.uint8)
+    d_lens = torch.from_numpy(lens.view(np.int32).copy()).cuda()
+    total = int(lens.sum()) + 4 * n
+    out = torch.zeros(total + 64, device="cuda", dtype=torch.uint8)
+    ws = torch.empty(hip.pack_bytes_workspace(n), device="cuda", dtype=torch.uint8)
+    hip.pack_bytes(d_payload.data_ptr(), d_lens.data_ptr(), n, out.data_ptr(), ws.data_ptr(), _stream(torch))
+    starts = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    elems = [payload[starts[i]:starts[i + 1]].tobytes() for i in range(n)]
+    ref = serialize_byte_tensor(np.array(elems, dtype=np.object_)).item()
+    got = out.cpu().numpy()
+    assert got[:total].tobytes() == ref and not got[total:].any()
+    offs = torch.empty(n, device="cuda", dtype=torch.int64)
+    lns = torch.empty(n, device="cuda", dtype=torch.int32)
+    status = torch.zeros(4, device="cuda", dtype=torch.int32)
+    # index over the whole (zero-padded) buffer: trailing zeros are not asked for
+    hip.index_bytes(out.data_ptr(), total + 64, n, offs.data_ptr(), lns.data_ptr(), status.data_ptr(), _stream(torch))
+    st = status.cpu().numpy()
+    assert st[0] == 0 and int(st[2:4].view(np.uint64)[0]) == n
+    np.testing.assert_array_equal(lns.cpu().numpy().view(np.uint32), lens)
+    exp_offs = starts[:-1] + 4 * np.arange(1, n + 1)
+    np.testing.assert_array_equal(offs.cpu().numpy(), exp_offs)
+    # truncate the buffer inside element n//2: malformed (the element is requested)
+    e = n // 2
+    cut = int(exp_offs[e]) + int(lens[e]) - 1 if lens[e] > 0 else int(exp_offs[e]) - 2
+    status.zero_()
+    hip.index_bytes(out.data_ptr(), cut, n, offs.data_ptr(), lns.data_ptr(), status.data_ptr(), _stream(torch))
+    assert int(status[0].item()) == -1
+    # fewer elements asked than present: status ok, only those indexed
+    status.zero_()
+    hip.index_bytes(out.data_ptr(), total, n // 3, offs.data_ptr(), lns.data_ptr(), status.data_ptr(), _stream(torch))
+    assert int(status[0].item()) == 0
+    np.testing.assert_array_equal(offs.cpu().numpy()[: n // 3], exp_offs[: n // 3])
+
+
 def test_index_bytes_detects_malformed(env):
     torch, hip = env
     buf = torch.tensor([5, 0, 0, 0, 1, 2], device="cuda", dtype=torch.uint8)

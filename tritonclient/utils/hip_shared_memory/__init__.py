@@ -22,7 +22,6 @@ Differences by design:
 """
 
 import base64
-import struct
 
 import numpy as np
 
@@ -113,15 +112,56 @@ def get_raw_handle(cuda_shm_handle):
 
 def _as_bytes(v):
     v = np.ascontiguousarray(v)
-    if v.dtype == np.object_:
-        # a tensor already serialised with serialize_byte_tensor
+    if v.dtype == np.object_ or v.dtype.type == np.bytes_:
+        # a tensor already serialised with serialize_byte_tensor (0-d / 1 element)
         raw = v.item() if v.size == 1 else b"".join(v.ravel().tolist())
         return np.frombuffer(raw, dtype=np.uint8)
     return v.reshape(-1).view(np.uint8)
 
 
+def _is_unserialized_bytes(v):
+    """An object/bytes tensor of several elements that is NOT the output of
+    serialize_byte_tensor (which is a single bytes blob)."""
+    return (v.dtype == np.object_ or v.dtype.type == np.bytes_) and v.size > 1
+
+
+def _pack_bytes_on_device(hip, handle, dst, elems):
+    """K2: serialise a BYTES tensor straight into device memory.  The payload
+    bytes and u32 lengths go H2D once; the <u32 len>||bytes stream is built by
+    the pack kernel inside the region (no host-side serialisation pass)."""
+    n = len(elems)
+    lens = np.fromiter((len(e) for e in elems), dtype="<u4", count=n)
+    payload = np.frombuffer(b"".join(elems), dtype=np.uint8)
+    dev = handle._device_id
+    nbytes = int(lens.sum()) + 4 * n
+    ws_n = hip.pack_bytes_workspace(n)
+    scratch = hip.malloc(dev, max(16, payload.size) + 4 * n + ws_n + 32)
+    try:
+        d_payload = scratch
+        d_lens = (scratch + max(16, payload.size) + 15) & ~15
+        d_ws = (d_lens + 4 * n + 15) & ~15
+        if payload.size:
+            hip.memcpy_h2d(d_payload, payload, payload.size, dev)
+        hip.memcpy_h2d(d_lens, lens, 4 * n, dev)
+        s = hip.Stream(dev)
+        try:
+            hip.pack_bytes(d_payload, d_lens, n, dst, d_ws, s.handle)
+            s.synchronize()
+        finally:
+            s.close()
+    finally:
+        hip.free(dev, scratch)
+    return nbytes
+
+
 def set_shared_memory_region(cuda_shm_handle, input_values, offset=0):
-    """Copy numpy arrays back-to-back into the region starting at ``offset``."""
+    """Copy numpy arrays back-to-back into the region starting at ``offset``.
+
+    BYTES arrays already serialised with ``serialize_byte_tensor`` are copied
+    as-is (reference behaviour, tc/utils/cuda_shared_memory/__init__.py:199-231).
+    An UNserialised BYTES tensor (object/bytes array of several elements) is
+    serialised on the device by K2 directly into the region.
+    """
     _check_handle(cuda_shm_handle)
     if not isinstance(input_values, (list, tuple)):
         raise CudaSharedMemoryException("input_values must be specified as a numpy array")
@@ -129,8 +169,17 @@ def set_shared_memory_region(cuda_shm_handle, input_values, offset=0):
         if not isinstance(v, np.ndarray):
             raise CudaSharedMemoryException("input_values must be specified as a list/tuple of numpy arrays")
     hip = _hip()
-    bufs = [_as_bytes(v) for v in input_values]
-    total = offset + sum(b.size for b in bufs)
+    from tritonclient.utils import _element_bytes
+
+    plan = []  # (kind, payload, nbytes)
+    for v in input_values:
+        if _is_unserialized_bytes(v):
+            elems = _element_bytes(np.ascontiguousarray(v))
+            plan.append(("k2", elems, sum(len(e) for e in elems) + 4 * len(elems)))
+        else:
+            b = _as_bytes(v)
+            plan.append(("copy", b, b.size))
+    total = offset + sum(nb for _, _, nb in plan)
     if total > cuda_shm_handle._byte_size:
         raise CudaSharedMemoryException(
             "unable to set values in cuda shared memory: %d bytes exceed the region size %d"
@@ -138,9 +187,12 @@ def set_shared_memory_region(cuda_shm_handle, input_values, offset=0):
         )
     try:
         cur = cuda_shm_handle._base_addr + offset
-        for b in bufs:
-            hip.memcpy_h2d(cur, b, b.size, cuda_shm_handle._device_id)
-            cur += b.size
+        for kind, b, nb in plan:
+            if kind == "k2":
+                _pack_bytes_on_device(hip, cuda_shm_handle, cur, b)
+            elif nb:
+                hip.memcpy_h2d(cur, b, nb, cuda_shm_handle._device_id)
+            cur += nb
     except Exception as ex:
         raise CudaSharedMemoryException("unable to set values in cuda shared memory") from ex
 
@@ -165,22 +217,48 @@ def get_contents_as_numpy(cuda_shm_handle, datatype, shape, offset=0):
             except Exception as ex:
                 raise CudaSharedMemoryException("failed to read cuda shared memory results") from ex
         return out
-    host = np.empty(size - offset, dtype=np.uint8)
+    # BYTES: K3 indexes the <u32 len>||bytes chain on the device (parallel
+    # block walk for large tensors), then only the bytes the elements span
+    # come back to the host and are sliced without a host-side walk
+    dev = cuda_shm_handle._device_id
+    nbytes = size - offset
+    out = np.empty(n, dtype=np.object_)
+    if n == 0:
+        return out.reshape(shape)
+    scratch = hip.malloc(dev, 12 * n + 32)
     try:
-        hip.memcpy_d2h(host, cuda_shm_handle._base_addr + offset, host.size, cuda_shm_handle._device_id)
+        d_offs, d_lens = scratch, scratch + 8 * n
+        d_status = (d_lens + 4 * n + 15) & ~15
+        s = hip.Stream(dev)
+        try:
+            hip.index_bytes(cuda_shm_handle._base_addr + offset, nbytes, n, d_offs, d_lens, d_status, s.handle)
+            s.synchronize()
+        finally:
+            s.close()
+        status = np.empty(4, dtype=np.int32)
+        hip.memcpy_d2h(status, d_status, 16, dev)
+        if status[0] != 0:
+            raise CudaSharedMemoryException(
+                "BYTES element runs past the end of the region" if status[0] < 0 else
+                "the region holds %d BYTES elements, %d requested" % (int(status[2:4].view(np.uint64)[0]), n))
+        offs = np.empty(n, dtype=np.uint64)
+        lens = np.empty(n, dtype=np.uint32)
+        hip.memcpy_d2h(offs, d_offs, 8 * n, dev)
+        hip.memcpy_d2h(lens, d_lens, 4 * n, dev)
+    except CudaSharedMemoryException:
+        raise
     except Exception as ex:
         raise CudaSharedMemoryException("failed to read cuda shared memory results") from ex
-    strs = []
-    pos = 0
-    for _ in range(n):
-        if pos + 4 > host.size:
-            raise CudaSharedMemoryException("BYTES element runs past the end of the region")
-        (ln,) = struct.unpack_from("<I", host, pos)
-        pos += 4
-        strs.append(host[pos : pos + ln].tobytes())
-        pos += ln
-    out = np.empty(n, dtype=np.object_)
-    out[:] = strs
+    finally:
+        hip.free(dev, scratch)
+    end = int(offs[-1]) + int(lens[-1])
+    host = np.empty(end, dtype=np.uint8)
+    try:
+        hip.memcpy_d2h(host, cuda_shm_handle._base_addr + offset, end, dev)
+    except Exception as ex:
+        raise CudaSharedMemoryException("failed to read cuda shared memory results") from ex
+    mv = memoryview(host)
+    out[:] = [bytes(mv[o:o + ln]) for o, ln in zip(offs.tolist(), lens.tolist())]
     return out.reshape(shape)
 
 
