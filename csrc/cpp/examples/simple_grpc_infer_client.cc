@@ -14,19 +14,34 @@ int main(int argc, char** argv)
   tc::Headers headers;
   uint64_t client_timeout = 0;
   grpc_compression_algorithm comp = GRPC_COMPRESS_NONE;
+  bool use_ssl = false;
+  tc::SslOptions ssl_options;
+  // TLS flags of the reference example: --ssl --root-certificates --private-key --certificate-chain
+  static const struct option longopts[] = {{"ssl", no_argument, nullptr, 1000},
+                                           {"root-certificates", required_argument, nullptr, 1001},
+                                           {"private-key", required_argument, nullptr, 1002},
+                                           {"certificate-chain", required_argument, nullptr, 1003},
+                                           {nullptr, 0, nullptr, 0}};
   int opt;
-  while ((opt = getopt(argc, argv, "vu:H:t:C:")) != -1) {
+  while ((opt = getopt_long(argc, argv, "vu:H:t:C:", longopts, nullptr)) != -1) {
     switch (opt) {
+      case 1000: use_ssl = true; break;
+      case 1001: ssl_options.root_certificates = optarg; break;
+      case 1002: ssl_options.private_key = optarg; break;
+      case 1003: ssl_options.certificate_chain = optarg; break;
       case 'v': verbose = true; break;
       case 'u': url = optarg; break;
       case 'H': example::AddHeader(&headers, optarg); break;
       case 't': client_timeout = std::stoul(optarg); break;
       case 'C': comp = std::string(optarg) == "gzip" ? GRPC_COMPRESS_GZIP : GRPC_COMPRESS_DEFLATE; break;
-      default: example::Usage(argv, "\t-t <client timeout in microseconds>\n\t-C <grpc compression: gzip|deflate>");
+      default:
+        example::Usage(argv, "\t-t <client timeout in microseconds>\n\t-C <grpc compression: gzip|deflate>\n"
+                             "\t--ssl --root-certificates <pem> --private-key <pem> --certificate-chain <pem>");
     }
   }
   std::unique_ptr<tc::InferenceServerGrpcClient> client;
-  FAIL_IF_ERR(tc::InferenceServerGrpcClient::Create(&client, url, verbose), "unable to create grpc client");
+  FAIL_IF_ERR(tc::InferenceServerGrpcClient::Create(&client, url, verbose, use_ssl, ssl_options),
+              "unable to create grpc client");
   example::SimpleData d;
   tc::InferInput *in0, *in1;
   FAIL_IF_ERR(tc::InferInput::Create(&in0, "INPUT0", {1, 16}, "INT32"), "unable to get INPUT0");

@@ -13,9 +13,22 @@ int main(int argc, char** argv)
   tc::Headers headers;
   tc::InferenceServerHttpClient::CompressionType req_comp = tc::InferenceServerHttpClient::CompressionType::NONE;
   tc::InferenceServerHttpClient::CompressionType resp_comp = tc::InferenceServerHttpClient::CompressionType::NONE;
+  tc::HttpSslOptions ssl_options;
+  // TLS flags of the reference example (an https:// URL turns TLS on)
+  static const struct option longopts[] = {{"verify-peer", required_argument, nullptr, 1000},
+                                           {"verify-host", required_argument, nullptr, 1001},
+                                           {"ca-certs", required_argument, nullptr, 1002},
+                                           {"cert-file", required_argument, nullptr, 1003},
+                                           {"key-file", required_argument, nullptr, 1004},
+                                           {nullptr, 0, nullptr, 0}};
   int opt;
-  while ((opt = getopt(argc, argv, "vu:H:i:o:")) != -1) {
+  while ((opt = getopt_long(argc, argv, "vu:H:i:o:", longopts, nullptr)) != -1) {
     switch (opt) {
+      case 1000: ssl_options.verify_peer = std::stol(optarg); break;
+      case 1001: ssl_options.verify_host = std::stol(optarg); break;
+      case 1002: ssl_options.ca_info = optarg; break;
+      case 1003: ssl_options.cert = optarg; break;
+      case 1004: ssl_options.key = optarg; break;
       case 'v': verbose = true; break;
       case 'u': url = optarg; break;
       case 'H': example::AddHeader(&headers, optarg); break;
@@ -28,11 +41,15 @@ int main(int argc, char** argv)
         (opt == 'i' ? req_comp : resp_comp) = c;
         break;
       }
-      default: example::Usage(argv, "\t-i <request compression: gzip|deflate>\n\t-o <response compression>");
+      default:
+        example::Usage(argv, "\t-i <request compression: gzip|deflate>\n\t-o <response compression>\n"
+                             "\t--verify-peer <0|1> --verify-host <0|2> --ca-certs <pem> --cert-file <pem> "
+                             "--key-file <pem>");
     }
   }
   std::unique_ptr<tc::InferenceServerHttpClient> client;
-  FAIL_IF_ERR(tc::InferenceServerHttpClient::Create(&client, url, verbose), "unable to create http client");
+  FAIL_IF_ERR(tc::InferenceServerHttpClient::Create(&client, url, verbose, ssl_options),
+              "unable to create http client");
   example::SimpleData d;
   tc::InferInput *in0, *in1;
   FAIL_IF_ERR(tc::InferInput::Create(&in0, "INPUT0", {1, 16}, "INT32"), "unable to get INPUT0");

@@ -216,6 +216,7 @@ InferenceServerGrpcClient::InferenceServerGrpcClient(
   opts.tls.ca_info = ssl_options.root_certificates;
   opts.tls.cert = ssl_options.certificate_chain;
   opts.tls.key = ssl_options.private_key;
+  opts.tls.alpn = "h2";
   opts.keepalive_time_ms = keepalive.keepalive_time_ms;
   opts.keepalive_timeout_ms = keepalive.keepalive_timeout_ms;
   opts.keepalive_permit_without_calls = keepalive.keepalive_permit_without_calls;

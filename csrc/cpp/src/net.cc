@@ -10,6 +10,8 @@
 #include <openssl/err.h>
 #include <openssl/ssl.h>
 #include <poll.h>
+#include <pthread.h>
+#include <signal.h>
 #include <sys/socket.h>
 #include <unistd.h>
 #include <zlib.h>
@@ -19,6 +21,45 @@
 #include <cstring>
 
 namespace triton { namespace client {
+
+namespace {
+// Blocks SIGPIPE on this thread for the guard's lifetime and discards one
+// that a failed write raised meanwhile, leaving the process's handlers alone
+// (a client library must not change global signal dispositions).
+class SigpipeGuard {
+ public:
+  SigpipeGuard()
+  {
+    sigset_t pipe;
+    sigemptyset(&pipe);
+    sigaddset(&pipe, SIGPIPE);
+    sigpending(&pending_before_);
+    blocked_ = pthread_sigmask(SIG_BLOCK, &pipe, &old_) == 0;
+  }
+  ~SigpipeGuard()
+  {
+    if (!blocked_) return;
+    if (!sigismember(&pending_before_, SIGPIPE)) {
+      sigset_t pend;
+      sigpending(&pend);
+      if (sigismember(&pend, SIGPIPE)) {
+        sigset_t pipe;
+        sigemptyset(&pipe);
+        sigaddset(&pipe, SIGPIPE);
+        struct timespec zero = {0, 0};
+        while (sigtimedwait(&pipe, nullptr, &zero) < 0 && errno == EINTR) {
+        }
+      }
+    }
+    pthread_sigmask(SIG_SETMASK, &old_, nullptr);
+  }
+
+ private:
+  sigset_t old_, pending_before_;
+  bool blocked_ = false;
+};
+}  // namespace
+
 
 namespace {
 
@@ -140,15 +181,35 @@ Socket::Connect(const std::string& host, int port, uint64_t timeout_us, const Tl
         SSL_CTX_use_PrivateKey_file(ctx_, tls.key.c_str(), tls.key_der ? SSL_FILETYPE_ASN1 : SSL_FILETYPE_PEM) != 1)
       return "failed to load client key " + tls.key;
     SSL_CTX_set_verify(ctx_, tls.verify_peer ? SSL_VERIFY_PEER : SSL_VERIFY_NONE, nullptr);
+    if (!tls.alpn.empty() && tls.alpn.size() < 256) {
+      std::string wire(1, static_cast<char>(tls.alpn.size()));
+      wire += tls.alpn;
+      SSL_CTX_set_alpn_protos(ctx_, reinterpret_cast<const unsigned char*>(wire.data()),
+                              static_cast<unsigned>(wire.size()));
+    }
     ssl_ = SSL_new(ctx_);
     SSL_set_fd(ssl_, fd_);
     SSL_set_tlsext_host_name(ssl_, host.c_str());
     if (tls.verify_host) SSL_set1_host(ssl_, host.c_str());
-    if (SSL_connect(ssl_) != 1) {
+    int rc;
+    {
+      SigpipeGuard g;  // a peer that hangs up mid-handshake must not kill the process
+      rc = SSL_connect(ssl_);
+    }
+    if (rc != 1) {
       char buf[256];
       ERR_error_string_n(ERR_get_error(), buf, sizeof(buf));
       Close();
       return std::string("TLS handshake failed: ") + buf;
+    }
+    if (!tls.alpn.empty()) {
+      const unsigned char* got = nullptr;
+      unsigned len = 0;
+      SSL_get0_alpn_selected(ssl_, &got, &len);
+      if (len != tls.alpn.size() || memcmp(got, tls.alpn.data(), len) != 0) {
+        Close();
+        return "TLS: server did not negotiate ALPN " + tls.alpn;
+      }
     }
   }
   return "";
@@ -158,6 +219,7 @@ ssize_t
 Socket::Writev(struct iovec* iov, int iovcnt)
 {
   if (ssl_) {
+    SigpipeGuard g;  // OpenSSL writes with write(2): a closed peer raises SIGPIPE
     ssize_t total = 0;
     for (int i = 0; i < iovcnt; ++i) {
       if (iov[i].iov_len == 0) continue;
@@ -173,8 +235,12 @@ Socket::Writev(struct iovec* iov, int iovcnt)
     return total;
   }
   ssize_t n;
+  struct msghdr mh;
+  memset(&mh, 0, sizeof(mh));
+  mh.msg_iov = iov;
+  mh.msg_iovlen = std::min(iovcnt, 1024);
   do {
-    n = ::writev(fd_, iov, std::min(iovcnt, 1024));
+    n = ::sendmsg(fd_, &mh, MSG_NOSIGNAL);  // EPIPE instead of SIGPIPE on a closed peer
   } while (n < 0 && errno == EINTR);
   if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return 0;
   return n;

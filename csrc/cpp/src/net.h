@@ -20,6 +20,7 @@ struct TlsConfig {
   bool verify_host = true;
   std::string ca_info, cert, key;
   bool cert_der = false, key_der = false;
+  std::string alpn;  // ALPN protocol to offer ("h2" for gRPC: servers refuse TLS without it)
 };
 
 /// A connected TCP (optionally TLS) stream socket.

@@ -38,6 +38,7 @@
 // accumulators are consecutive output channels of one pixel.
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "kernels/common.h"
 
@@ -105,31 +106,42 @@ struct X3Conv1x1Params {
   int ldx, M, K, N, ldy, H, W, k_per_split;
 };
 
-constexpr int kBM = 128, kBN = 128, kBK = 32, kLDK = kBK + 8;  // 80-B LDS rows: conflict-free b128 reads
+constexpr int kBN = 128, kBK = 32, kLDK = kBK + 8;  // 80-B LDS rows: conflict-free b128 reads
 
-// Block = 4 waves as 2 (pixels) x 2 (channels): block tile 128 x 128, wave
-// tile 64 x 64 = 4 x 4 16x16x32 MFMA tiles (x3 = 48 MFMAs per K step).  The
-// LDS tiles are double-buffered and the next K step's global loads are in
-// flight in registers while this step's MFMAs run (one barrier per step).
-template <bool POOL, bool SPLIT>
+// Block = 4 waves as WM (pixels) x 4/WM (channels) over a BM x 128 tile:
+//   BM 128, WM 2: wave tile 64 x 64 = 4 x 4 16x16x32 MFMA tiles (48 MFMAs per
+//                 K step) — the big-M layers (56x56 / 28x28 at bs128);
+//   BM 32,  WM 1: wave tile 32 x 32 = 2 x 2 tiles — small M (14x14 / 7x7,
+//                 small batches): 4x the blocks of BM 128 so the whole K runs
+//                 in one block instead of split-K partials + a reduce kernel
+//                 (the partials cost more HBM traffic than the conv's input).
+// The LDS tiles are double-buffered; the global loads of the next PF K steps
+// are in flight in a register ring while this step's MFMAs run (one barrier
+// per step).  PF 1 for BM 128 (its registers are full); PF 4 for the small
+// tiles, whose per-step MFMA work is far shorter than an HBM round trip.
+template <bool POOL, bool SPLIT, int BM, int WM, int PF>
 __global__ void __launch_bounds__(256, 2) x3_conv1x1_kernel(X3Conv1x1Params p) {
   constexpr int NS = POOL ? 4 : 1;
-  __shared__ __attribute__((aligned(16))) uint16_t sXh[2][kBM * kLDK];
-  __shared__ __attribute__((aligned(16))) uint16_t sXl[2][kBM * kLDK];
+  constexpr int WN = 4 / WM;
+  constexpr int TI = BM / WM / 16;   // pixel tiles per wave
+  constexpr int TJ = kBN / WN / 16;  // channel tiles per wave
+  constexpr int XC = BM / 32;        // X 16-B chunks per thread per K step
+  __shared__ __attribute__((aligned(16))) uint16_t sXh[2][BM * kLDK];
+  __shared__ __attribute__((aligned(16))) uint16_t sXl[2][BM * kLDK];
   __shared__ __attribute__((aligned(16))) uint16_t sWh[2][kBN * kLDK];
   __shared__ __attribute__((aligned(16))) uint16_t sWl[2][kBN * kLDK];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;
-  const int m0 = blockIdx.x * kBM, n0 = blockIdx.z * kBN;
+  const int wm = wave % WM, wn = wave / WM;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.z * kBN;
 
-  // X: 128 rows x 8 chunks of 4 fp32 per K step -> 4 chunks per thread, all
-  // at the same K offset (tid & 7); POOL: each chunk averages 4 source rows
+  // X: BM rows x 8 chunks of 4 fp32 per K step, all of a thread's chunks at
+  // the same K offset (tid & 7); POOL: each chunk averages 4 source rows
   const int xk = (tid & 7) * 4;
-  const float* xs[4][NS];
-  bool xok[4];
+  const float* xs[XC][NS];
+  bool xok[XC];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < XC; ++i) {
     const int r = (tid >> 3) + 32 * i;
     const int m = m0 + r;
     xok[i] = m < p.M;
@@ -158,34 +170,34 @@ __global__ void __launch_bounds__(256, 2) x3_conv1x1_kernel(X3Conv1x1Params p) {
     wsl[i] = p.w_lo + (size_t)(n0 + r) * p.K + wk;
   }
 
-  f32x4 rx[4][NS], rs, rt;
-  v4u rwh[2], rwl[2];
-  auto load_step = [&](int k0) {
-    rs = ldf4(p.in_scale + k0 + xk);
-    rt = ldf4(p.in_bias + k0 + xk);
+  f32x4 rx[PF][XC][NS], rs[PF], rt[PF];
+  v4u rwh[PF][2], rwl[PF][2];
+  auto load_step = [&](int slot, int k0) {
+    rs[slot] = ldf4(p.in_scale + k0 + xk);
+    rt[slot] = ldf4(p.in_bias + k0 + xk);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < XC; ++i)
 #pragma unroll
-      for (int s = 0; s < NS; ++s) rx[i][s] = xok[i] ? ldf4(xs[i][s] + k0) : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < NS; ++s) rx[slot][i][s] = xok[i] ? ldf4(xs[i][s] + k0) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      rwh[i] = ld16(wsh[i] + k0);
-      rwl[i] = ld16(wsl[i] + k0);
+      rwh[slot][i] = ld16(wsh[i] + k0);
+      rwl[slot][i] = ld16(wsl[i] + k0);
     }
   };
-  auto store_step = [&](int buf) {
+  auto store_step = [&](int slot, int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < XC; ++i) {
       f32x4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         if constexpr (POOL) {
           float a = 0.f;
 #pragma unroll
-          for (int s = 0; s < NS; ++s) a += fmaxf(rx[i][s][e] * rs[e] + rt[e], 0.f);
+          for (int s = 0; s < NS; ++s) a += fmaxf(rx[slot][i][s][e] * rs[slot][e] + rt[slot][e], 0.f);
           v[e] = 0.25f * a;
         } else {
-          v[e] = fmaxf(rx[i][0][e] * rs[e] + rt[e], 0.f);
+          v[e] = fmaxf(rx[slot][i][0][e] * rs[slot][e] + rt[slot][e], 0.f);
         }
         if (!xok[i]) v[e] = 0.f;
       }
@@ -198,57 +210,76 @@ __global__ void __launch_bounds__(256, 2) x3_conv1x1_kernel(X3Conv1x1Params p) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int off = ((tid >> 2) + 64 * i) * kLDK + wk;
-      *reinterpret_cast<v4u*>(&sWh[buf][off]) = rwh[i];
-      *reinterpret_cast<v4u*>(&sWl[buf][off]) = rwl[i];
+      *reinterpret_cast<v4u*>(&sWh[buf][off]) = rwh[slot][i];
+      *reinterpret_cast<v4u*>(&sWl[buf][off]) = rwl[slot][i];
     }
   };
 
   const int fr16 = lane & 15, fk = 8 * (lane >> 4);
-  f32x4 acc[4][4];
+  f32x4 acc[TJ][TI];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < TJ; ++j) {
     f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (SPLIT && !p.ws) b0 = ldf4(p.out_bias + n0 + wn * 64 + j * 16 + (lane >> 4) * 4);
+    if (SPLIT && !p.ws) b0 = ldf4(p.out_bias + n0 + wn * (kBN / WN) + j * 16 + (lane >> 4) * 4);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = b0;
+    for (int i = 0; i < TI; ++i) acc[j][i] = b0;
   }
 
   const int k_begin = p.ws ? (int)blockIdx.y * p.k_per_split : 0;
   const int k_end = p.ws ? min(p.K, k_begin + p.k_per_split) : p.K;
-  load_step(k_begin);
-  store_step(0);
+  // Loads are unconditional (tail steps re-load the last step) so the
+  // number of loads in flight is static and the compiler's vmcnt waits can
+  // leave the younger PF-1 steps outstanding; the compute is what is
+  // predicated on the step being live.
+  const int nsteps = (k_end - k_begin) / kBK;
+  auto kstep = [&](int st) { return k_begin + min(st, nsteps - 1) * kBK; };
+  // prologue: steps 0..PF-1 in flight, step 0 staged
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load_step(u, kstep(u));
+  store_step(0, 0);
   __syncthreads();
-  for (int k0 = k_begin, buf = 0; k0 < k_end; k0 += kBK, buf ^= 1) {
-    const bool more = k0 + kBK < k_end;
-    if (more) load_step(k0 + kBK);
-    v4u ah[4], al[4], bh[4], bl[4];
+  for (int s0 = 0; s0 < nsteps; s0 += PF) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int off = (wn * 64 + j * 16 + fr16) * kLDK + fk;
-      ah[j] = ld16(&sWh[buf][off]);
-      al[j] = ld16(&sWl[buf][off]);
+    for (int u = 0; u < PF; ++u) {
+      const int st = s0 + u;
+      const bool live = st < nsteps;  // uniform over the block
+      const int buf = (PF == 1) ? (st & 1) : (u & 1);
+      if (PF == 1) load_step(0, kstep(st + 1));
+      v4u ah[TJ], al[TJ], bh[TI], bl[TI];
+      if (live) {
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int off = (wn * (kBN / WN) + j * 16 + fr16) * kLDK + fk;
+          ah[j] = ld16(&sWh[buf][off]);
+          al[j] = ld16(&sWl[buf][off]);
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int off = (wm * (BM / WM) + i * 16 + fr16) * kLDK + fk;
+          bh[i] = ld16(&sXh[buf][off]);
+          bl[i] = ld16(&sXl[buf][off]);
+        }
+      }
+      // slot u (step st, already in LDS) refills with step st + PF
+      if (PF > 1) load_step(u, kstep(st + PF));
+      if (live) {
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int i = 0; i < TI; ++i) acc[j][i] = x3_16(ah[j], al[j], bh[i], bl[i], acc[j][i]);
+      }
+      if (st + 1 < nsteps) store_step((u + 1) % PF, buf ^ 1);
+      __syncthreads();
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int off = (wm * 64 + i * 16 + fr16) * kLDK + fk;
-      bh[i] = ld16(&sXh[buf][off]);
-      bl[i] = ld16(&sXl[buf][off]);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[j][i] = x3_16(ah[j], al[j], bh[i], bl[i], acc[j][i]);
-    if (more) store_step(buf ^ 1);
-    __syncthreads();
   }
 
   // lane holds output channels nb..nb+3 of pixel m
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int nb = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
+  for (int j = 0; j < TJ; ++j) {
+    const int nb = n0 + wn * (kBN / WN) + j * 16 + (lane >> 4) * 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm * 64 + i * 16 + fr16;
+    for (int i = 0; i < TI; ++i) {
+      const int m = m0 + wm * (BM / WM) + i * 16 + fr16;
       if (m >= p.M) continue;
       const f32x4 a = acc[j][i];
       if (p.ws) {
@@ -293,11 +324,14 @@ __global__ void __launch_bounds__(256) x3_splitk_reduce_kernel(X3Conv1x1Params p
 // ============================================================================
 constexpr int kC3 = 128, kTaps = 9;  // 32 output channels (growth) per conv
 constexpr int kTile3 = 128;            // output pixels per tile
-constexpr int kRow3 = kC3 + 8;         // LDS ring row stride (bf16): 272 B, conflict-free b128 reads
+// ring row = [hi 128 bf16 | lo 128 bf16 | 8 pad]: 528 B = 132 dwords (== 4 mod
+// 64 banks: conflict-free b128 reads by consecutive pixels), the lo plane at a
+// constant +256 B (an immediate ds_read offset, no second address)
+constexpr int kRow3 = 2 * kC3 + 8;
 constexpr int kRing = 256;             // ring rows per plane (a band is 128 + 2(W+1) <= 242 rows)
 constexpr int kMaxW3 = 56;
 constexpr int kNew3 = kTile3 * (kC3 / 8) / 512;  // 16-B chunks per thread per plane of a tile's new rows: 4
-constexpr int kLds3 = 2 * (kRing + 1) * kRow3 * 2;  // both planes + one zero row each: 139,808 B
+constexpr int kLds3 = (kRing + 1) * kRow3 * 2;  // ring + one zero row: 135,696 B
 
 struct X3Conv3x3Params {
   const uint16_t* z_hi;  // [M][128] bf16
@@ -307,7 +341,23 @@ struct X3Conv3x3Params {
   float* y;              // [M][ldy] fp32, offset to the layer's 32-channel slice
   int ldy, M, H, W;
   int tiles, tiles_per_block;
+  uint32_t mag_hw, mag_w;  // ceil(2^32 / (H*W)), ceil(2^32 / W): division by multiply-high
 };
+
+// n / d and n % d for n < 2^24 via a multiply-high estimate and one correction
+__device__ __forceinline__ int fast_divmod(int n, int d, uint32_t mag, int& rem) {
+  int q = (int)__umulhi((uint32_t)n, mag);
+  int r = n - q * d;
+  if (r < 0) {
+    --q;
+    r += d;
+  } else if (r >= d) {
+    ++q;
+    r -= d;
+  }
+  rem = r;
+  return q;
+}
 
 // 8 waves (2 per SIMD); wave w owns input channels [16w, 16w+16) of all nine
 // taps, so its hi/lo weight fragments are 18 x 16 B in registers for the
@@ -323,8 +373,8 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_kernel(X3Conv3x3Params p) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds3[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int W = p.W, HW = p.H * p.W;
-  uint16_t* rh = lds3;                       // [257][kRow3]
-  uint16_t* rl = lds3 + (kRing + 1) * kRow3;
+  uint16_t* rh = lds3;        // [257][kRow3]: hi at +0, lo at +kC3
+  uint16_t* rl = lds3 + kC3;
 
   const int h = lane >> 5, col = lane & 31;
   const int ci = 16 * wave + 8 * h;
@@ -354,7 +404,7 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_kernel(X3Conv3x3Params p) {
       *reinterpret_cast<v4u*>(&rh[lo]) = vh;
       *reinterpret_cast<v4u*>(&rl[lo]) = vl;
     }
-    if (tid < kC3 / 8) {
+    if (tid < kC3 / 8) {  // the zero row read by out-of-image taps
       *reinterpret_cast<v4u*>(&rh[kRing * kRow3 + tid * 8]) = v4u{0, 0, 0, 0};
       *reinterpret_cast<v4u*>(&rl[kRing * kRow3 + tid * 8]) = v4u{0, 0, 0, 0};
     }
@@ -384,25 +434,29 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_kernel(X3Conv3x3Params p) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[s][e] = 0.f;
       const int m = m0 + 32 * s + col;
-      const int r = m % HW, yy = r / W, xx = r - yy * W;
+      int r, xx;
+      (void)fast_divmod(m, HW, p.mag_hw, r);
+      const int yy = fast_divmod(r, W, p.mag_w, xx);
       const bool in = m < p.M;
+      const bool up = in && yy > 0, dn = in && yy < p.H - 1, lf = xx > 0, rt = xx < W - 1;
+      const int base = m + W + 1;
 #pragma unroll
       for (int t = 0; t < kTaps; ++t) {
         const int dy = t / 3 - 1, dx = t % 3 - 1;
-        const bool ok = in && yy + dy >= 0 && yy + dy < p.H && xx + dx >= 0 && xx + dx < W;
-        const int row = ok ? ring(m + dy * W + dx) : kRing;
-        const v4u b_hi = ld16(&rh[row * kRow3 + ci]);
-        const v4u b_lo = ld16(&rl[row * kRow3 + ci]);
-        acc[s] = x3_32(wh[t], wl[t], b_hi, b_lo, acc[s]);
+        bool ok = dy < 0 ? up : (dy > 0 ? dn : in);
+        if (dx < 0) ok = ok && lf;
+        if (dx > 0) ok = ok && rt;
+        const int row = ok ? ((base + dy * W + dx) & (kRing - 1)) : kRing;
+        const uint16_t* q = &rh[row * kRow3 + ci];
+        acc[s] = x3_32(wh[t], wl[t], ld16(q), ld16(q + kC3), acc[s]);
       }
     }
     __syncthreads();  // ring reads done
     // scratch = the ring rows of global rows [m0-W-1, m0+127-W) (read by this
-    // tile only): pixel q's slot k (32 fp32) at ring row ring(m0-W-1+q),
-    // slots 0/1 in the hi plane's 272 B, slots 2/3 in the lo plane's
+    // tile only): pixel q's slot k (32 fp32 = 128 B) at byte 128k of ring row
+    // ring(m0-W-1+q)
     auto slot = [&](int q, int k) {
-      uint16_t* base = (k < 2 ? rh : rl) + ring(m0 - W - 1 + q) * kRow3;
-      return reinterpret_cast<float*>(base) + 32 * (k & 1);
+      return reinterpret_cast<float*>(rh + ring(m0 - W - 1 + q) * kRow3) + 32 * k;
     };
     // C layout (32x32): lane col = pixel, reg r -> channel (r&3) + 8*(r>>2) + 4*h
     if (wave >= 4) {
@@ -457,6 +511,129 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_kernel(X3Conv3x3Params p) {
       }
       __syncthreads();
     }
+  }
+}
+
+// ---- K9x (v2): 64-pixel tiles, LDS-DMA band ring, one-round reduction ------
+// 8 waves = 2 pixel halves (ph) x 4 input-channel quarters (kq): wave (ph, kq)
+// computes the 32 output channels of 32 pixels over 32 input channels x 9
+// taps, its hi/lo weight fragments (36 x 16 B) in registers for the whole
+// persistent kernel.  A block walks a contiguous run of 64-pixel tiles:
+//   * the band [m0-W-1, m0+64+W+1) lives in a 256-row LDS ring (512-B rows =
+//     hi|lo planes, 16-B chunks XOR-swizzled by ring row: conflict-free
+//     b128 reads by consecutive pixels); the 64 rows the NEXT tile adds are
+//     written by global_load_lds (LDS-DMA, no VGPR staging, swizzle applied
+//     on the source address) right after the tile starts, into ring rows the
+//     current band does not use (64 + 2(W+1) + 64 <= 256), so the fetch
+//     overlaps the whole MFMA phase;
+//   * the 4 input-channel partials of each 32x32 output block are summed in
+//     ONE balanced round: wave (ph, kq) owns output channels [8kq, 8kq+8) of
+//     its 32 pixels; it writes its partials of the other three 8-channel
+//     groups (3 x 1 KB) to the scratch, barrier, adds the three partials of
+//     its own group and stores fp32 straight to HBM;
+//   * the 4 reads of tap t+1 are issued before the 6 MFMAs of tap t.
+// Two barriers per tile.
+constexpr int kT2 = 64;
+constexpr int kRowB = 2 * kC3 * 2;          // 512 B per ring row
+constexpr int kScrSlot = 32 * 8;            // floats per (group, ph, source) slot: 32 px x 8 channels
+constexpr int kLdsV2 = (kRing + 1) * kRowB + 4 * 2 * 3 * kScrSlot * 4;  // 131,584 + 24,576 B
+
+__global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds2[];
+  float* scr = reinterpret_cast<float*>(lds2 + (kRing + 1) * kRowB);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ph = wave & 1, kq = wave >> 1;
+  const int W = p.W, HW = p.H * p.W;
+  const int col = lane & 31, h = lane >> 5;
+
+  v4u wh[kTaps][2], wl[kTaps][2];
+#pragma unroll
+  for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      const size_t off = (size_t)col * (kTaps * kC3) + t * kC3 + 32 * kq + 16 * kc + 8 * h;
+      wh[t][kc] = ld16(p.w_hi + off);
+      wl[t][kc] = ld16(p.w_lo + off);
+    }
+
+  const int t_begin = blockIdx.x * p.tiles_per_block;
+  const int t_end = min(p.tiles, t_begin + p.tiles_per_block);
+  if (t_begin >= t_end) return;
+
+  if (tid < kRowB / 16) *reinterpret_cast<v4u*>(lds2 + kRing * kRowB + tid * 16) = v4u{0, 0, 0, 0};
+  // rows [g0, g0+nrows) -> ring, two rows per wave-instruction (ring row of g0 even)
+  auto dma_rows = [&](int g0, int nrows) {
+    const int plane = (lane >> 4) & 1, j = lane & 15;
+    for (int pr = wave; 2 * pr < nrows; pr += 8) {
+      const int ga = g0 + 2 * pr;
+      const int g = ga + (lane >> 5);
+      const int pos = (g + W + 1) & (kRing - 1);
+      const int gc = min(max(g, 0), p.M - 1);
+      const uint16_t* src = (plane ? p.z_lo : p.z_hi) + (size_t)gc * kC3 + ((j ^ (pos & 15)) << 3);
+      const int pos0 = (ga + W + 1) & (kRing - 1);
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(lds2 + pos0 * kRowB), 16, 0, 0);
+    }
+  };
+  dma_rows(t_begin * kT2 - W - 1, kT2 + 2 * (W + 1));
+
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int m0 = tile * kT2;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // B0: this band is in LDS everywhere; the scratch is free
+    if (tile + 1 < t_end) dma_rows(m0 + kT2 + W + 1, kT2);
+
+    const int m = m0 + 32 * ph + col;
+    int r, xx;
+    (void)fast_divmod(m, HW, p.mag_hw, r);
+    const int yy = fast_divmod(r, W, p.mag_w, xx);
+    const bool in = m < p.M;
+    const bool up = in && yy > 0, dn = in && yy < p.H - 1, lf = xx > 0, rt = xx < W - 1;
+    const int base = m + W + 1;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    v4u bq[2][2][2];  // [tap parity][kc][plane]
+    auto rd = [&](int t, int slot) {
+      const int dy = t / 3 - 1, dx = t % 3 - 1;
+      bool ok = dy < 0 ? up : (dy > 0 ? dn : in);
+      if (dx < 0) ok = ok && lf;
+      if (dx > 0) ok = ok && rt;
+      const int row = ok ? ((base + dy * W + dx) & (kRing - 1)) : kRing;
+      const uint8_t* rp = lds2 + row * kRowB;
+      const int sw = row & 15;
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc) {
+        const uint8_t* q = rp + (((4 * kq + 2 * kc + h) ^ sw) << 4);
+        bq[slot][kc][0] = ld16(q);
+        bq[slot][kc][1] = ld16(q + 256);
+      }
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int t = 0; t < kTaps; ++t) {
+      if (t + 1 < kTaps) rd(t + 1, (t + 1) & 1);
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc) acc = x3_32(wh[t][kc], wl[t][kc], bq[t & 1][kc][0], bq[t & 1][kc][1], acc);
+    }
+    // C layout (32x32): lane col = pixel, reg 4g+e -> channel 8g + 4h + e.
+    // scratch slot (group g, ph, source kq != g) at index (g*2 + ph)*3 + (kq - g + 3) % 4
+    auto slot = [&](int g, int src) {
+      return scr + ((g * 2 + ph) * 3 + (src - g + 3) % 4) * kScrSlot + col * 8 + 4 * h;
+    };
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      if (g != kq)
+        *reinterpret_cast<f32x4*>(slot(g, kq)) = f32x4{acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // B1 (raw: the next band's DMA stays in flight)
+    f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      if (g == kq) o = f32x4{acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+#pragma unroll
+    for (int src = 0; src < 4; ++src)
+      if (src != kq) o += *reinterpret_cast<const f32x4*>(slot(kq, src));
+    if (in) *reinterpret_cast<f32x4*>(p.y + (size_t)m * p.ldy + 8 * kq + 4 * h) = o;
   }
 }
 
@@ -606,20 +783,60 @@ bool aligned16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
 }  // namespace
 
+namespace {
+// Tile plan of one 1x1 conv: BM 128 while that fills the chip, else BM 32
+// with the whole K per block; split-K (partials + reduce) only when even
+// 32-row tiles leave most CUs idle (7x7 layers, small batches).
+struct X3Plan {
+  int bm, tiles, splits, k_per_split;
+};
+
+X3Plan x3_plan(int M, int K, int N) {
+  X3Plan pl;
+  const int nt = std::max(1, N / kBN);
+  const int big = ((M + 127) / 128) * nt;
+  const int mid = ((M + 63) / 64) * nt;
+  pl.bm = big >= 384 ? 128 : (mid >= 256 ? 64 : 32);
+  static const int force_bm = [] {  // A/B knob for tools/x3_kbench.py
+    const char* e = getenv("TCAMD_X3_BM");
+    return e ? atoi(e) : 0;
+  }();
+  if (force_bm == 32 || force_bm == 64 || force_bm == 128) pl.bm = force_bm;
+  pl.tiles = ((M + pl.bm - 1) / pl.bm) * nt;
+  pl.splits = 1;
+  pl.k_per_split = K;
+  if (pl.tiles < 192 && K >= 4 * kBK) {
+    const int steps = K / kBK;
+    int want = std::min(steps / 2, (384 + pl.tiles - 1) / pl.tiles);
+    if (want > 1) {
+      pl.k_per_split = ((steps + want - 1) / want) * kBK;
+      pl.splits = (K + pl.k_per_split - 1) / pl.k_per_split;
+    }
+  }
+  return pl;
+}
+
+template <bool POOL, bool SPLIT>
+void launch_x3_1x1(const X3Plan& pl, const dim3& g, hipStream_t s, const X3Conv1x1Params& p) {
+  if (pl.bm == 128) hipLaunchKernelGGL((x3_conv1x1_kernel<POOL, SPLIT, 128, 2, 1>), g, dim3(256), 0, s, p);
+  // the pooled prologue holds 4 source rows per chunk: a shallower ring
+  else if (pl.bm == 64) hipLaunchKernelGGL((x3_conv1x1_kernel<POOL, SPLIT, 64, 1, POOL ? 2 : 4>), g, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((x3_conv1x1_kernel<POOL, SPLIT, 32, 1, POOL ? 2 : 4>), g, dim3(256), 0, s, p);
+}
+}  // namespace
+
 extern "C" {
 
 // Split-K workspace bytes the 1x1 conv wants for an M x K -> N problem (0 = none).
 size_t tcamd_x3_conv1x1_ws_bytes(int M, int K, int N) {
-  const int tiles = ((M + kBM - 1) / kBM) * std::max(1, N / kBN);
-  if (tiles >= 384 || K < 2 * kBK) return 0;
-  const int splits = std::min(K / kBK, (768 + tiles - 1) / tiles);
-  return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
+  const X3Plan pl = x3_plan(M, K, N);
+  return pl.splits > 1 ? (size_t)pl.splits * M * N * sizeof(float) : 0;
 }
 
 // 1x1 conv, N output channels (a multiple of 128).  split_out: z_hi/z_lo
 // [M][128] bf16 with bias+ReLU (N = 128); else y fp32 [M][ldy] raw.  pool: x
 // holds the pre-pool H x W pixels, M = imgs * H/2 * W/2.  ws: split-K
-// workspace (may be null).
+// workspace (may be null: then the whole K runs in each block).
 int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, int N, const float* in_scale, const float* in_bias,
                      const void* w_hi, const void* w_lo, const float* out_bias, void* z_hi, void* z_lo, float* y,
                      int ldy, int pool, int H, int W, float* ws, size_t ws_bytes, void* stream) {
@@ -652,31 +869,28 @@ int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, int N, const float* 
   p.ldy = ldy;
   p.H = H;
   p.W = W;
-  p.k_per_split = K;
-  const int tiles = (M + kBM - 1) / kBM;
-  int splits = 1;
-  const size_t want = tcamd_x3_conv1x1_ws_bytes(M, K, N);
-  if (want && ws && ws_bytes >= want && aligned16(ws)) {
-    splits = (int)(want / ((size_t)M * N * sizeof(float)));
-    const int steps = K / kBK;
-    p.k_per_split = ((steps + splits - 1) / splits) * kBK;
-    splits = (K + p.k_per_split - 1) / p.k_per_split;
-    if (splits > 1) p.ws = ws;
+  X3Plan pl = x3_plan(M, K, N);
+  if (pl.splits > 1 && ws && ws_bytes >= (size_t)pl.splits * M * N * sizeof(float) && aligned16(ws)) {
+    p.ws = ws;
+    p.k_per_split = pl.k_per_split;
+  } else {
+    pl.splits = 1;
+    p.k_per_split = K;
   }
   hipStream_t s = (hipStream_t)stream;
-  const dim3 g(tiles, splits, N / kBN);
+  const dim3 g((M + pl.bm - 1) / pl.bm, pl.splits, N / kBN);
   if (pool) {
-    if (split_out) hipLaunchKernelGGL((x3_conv1x1_kernel<true, true>), g, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((x3_conv1x1_kernel<true, false>), g, dim3(256), 0, s, p);
+    if (split_out) launch_x3_1x1<true, true>(pl, g, s, p);
+    else launch_x3_1x1<true, false>(pl, g, s, p);
   } else {
-    if (split_out) hipLaunchKernelGGL((x3_conv1x1_kernel<false, true>), g, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((x3_conv1x1_kernel<false, false>), g, dim3(256), 0, s, p);
+    if (split_out) launch_x3_1x1<false, true>(pl, g, s, p);
+    else launch_x3_1x1<false, false>(pl, g, s, p);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !p.ws) return e;
   const int rg = tcamd::grid_for((size_t)M * (N / 4));
-  if (split_out) hipLaunchKernelGGL(x3_splitk_reduce_kernel<true>, dim3(rg), dim3(256), 0, s, p, splits);
-  else hipLaunchKernelGGL(x3_splitk_reduce_kernel<false>, dim3(rg), dim3(256), 0, s, p, splits);
+  if (split_out) hipLaunchKernelGGL(x3_splitk_reduce_kernel<true>, dim3(rg), dim3(256), 0, s, p, pl.splits);
+  else hipLaunchKernelGGL(x3_splitk_reduce_kernel<false>, dim3(rg), dim3(256), 0, s, p, pl.splits);
   return hipGetLastError();
 }
 
@@ -699,20 +913,34 @@ int tcamd_x3_conv3x3(const void* z_hi, const void* z_lo, int imgs, int H, int W,
   p.H = H;
   p.W = W;
   p.tiles = (p.M + kTile3 - 1) / kTile3;
+  p.mag_hw = (uint32_t)((0x100000000ull + H * W - 1) / (uint64_t)(H * W));
+  p.mag_w = (uint32_t)((0x100000000ull + W - 1) / (uint64_t)W);
+  if (p.M >= (1 << 24)) return hipErrorInvalidValue;  // fast_divmod range
   // one block (8 waves) per CU; each walks a contiguous run of tiles so the
   // halo rows its neighbour tile re-reads are still in this XCD's L2
-  const int grid = std::min(p.tiles, 256);
-  p.tiles_per_block = (p.tiles + grid - 1) / grid;
-  const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
-  const size_t lds = kLds3;
+  static const bool v1 = getenv("TCAMD_X3_K9") && atoi(getenv("TCAMD_X3_K9")) == 1;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e =
+    hipError_t e =
         hipFuncSetAttribute((const void*)x3_conv3x3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kLds3);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kLdsV2);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(x3_conv3x3_kernel, dim3(blocks), dim3(512), lds, (hipStream_t)stream, p);
+  if (!v1) {
+    p.tiles = (p.M + kT2 - 1) / kT2;
+    const int grid = std::min(p.tiles, 256);
+    p.tiles_per_block = (p.tiles + grid - 1) / grid;
+    const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
+    hipLaunchKernelGGL(x3_conv3x3_v2_kernel, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
+    return hipGetLastError();
+  }
+  const int grid = std::min(p.tiles, 256);
+  p.tiles_per_block = (p.tiles + grid - 1) / grid;
+  const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
+  hipLaunchKernelGGL(x3_conv3x3_kernel, dim3(blocks), dim3(512), kLds3, (hipStream_t)stream, p);
   return hipGetLastError();
 }
 

@@ -59,7 +59,7 @@ def test_split_is_exact_to_2e17():
 
 
 @pytest.mark.parametrize("M,K,ldx", [(100, 64, 96), (37, 992, 1024), (6272, 512, 1024), (50000, 224, 256),
-                                     (401408, 96, 256)])
+                                     (401408, 96, 256), (25088, 640, 1024), (1568, 768, 1024), (392, 992, 1024)])
 def test_x3_conv1x1_split_out(M, K, ldx):
     """Dense-layer 1x1: z = relu(relu(x*s+t) @ W^T + b) as hi/lo planes
     (large M: whole-K blocks; small M: split-K workspace + reduce)."""

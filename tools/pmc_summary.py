@@ -1,0 +1,30 @@
+#!/usr/bin/env python3
+"""Per-kernel averages of rocprofv3 --pmc CSV passes (one or more dirs)."""
+import collections
+import csv
+import glob
+import sys
+
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+for d in sys.argv[1:]:
+    for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+        per = collections.defaultdict(lambda: collections.defaultdict(float))
+        for r in csv.DictReader(open(f)):
+            per[(r["Kernel_Name"], r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+        for (k, _), cs in per.items():
+            for c, v in cs.items():
+                agg[k][c].append(v)
+for k, cs in agg.items():
+    name = k.replace("(anonymous namespace)::", "").split("(")[0]
+    print("##", name)
+    m = {c: sum(v) / len(v) for c, v in cs.items()}
+    for c in sorted(m):
+        print("  %-28s %16.0f" % (c, m[c]))
+    if "SQ_WAVE_CYCLES" in m and m["SQ_WAVE_CYCLES"]:
+        w = m["SQ_WAVE_CYCLES"]
+        print("  -> wait_any %.0f%%  wait_inst %.0f%%  active %.0f%%" % (
+            100 * m.get("SQ_WAIT_ANY", 0) / w, 100 * m.get("SQ_WAIT_INST_ANY", 0) / w,
+            100 * m.get("SQ_ACTIVE_INST_ANY", 0) / w))
+    if "SQ_BUSY_CYCLES" in m and "SQ_VALU_MFMA_BUSY_CYCLES" in m and m["SQ_BUSY_CYCLES"]:
+        # MFMA busy cycles are per SIMD summed over the chip; busy cycles per SE (x? ) -> report raw ratio
+        print("  -> mfma_busy / busy = %.3f" % (m["SQ_VALU_MFMA_BUSY_CYCLES"] / m["SQ_BUSY_CYCLES"]))

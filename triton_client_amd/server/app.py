@@ -47,11 +47,18 @@ def native_grpc_available():
     return native_frontend.available()
 
 
-async def serve(server, http_port, grpc_port, host="127.0.0.1", ready_evt=None, stop_evt=None, native_grpc=None):
+async def serve(server, http_port, grpc_port, host="127.0.0.1", ready_evt=None, stop_evt=None, native_grpc=None,
+                tls=None):
     """Serve HTTP (aiohttp) and gRPC.  With ``native_grpc`` (default: when
     libtcserve.so is built) the public gRPC port is tcserve, the C++ front
-    end, and grpc.aio listens on a loopback port behind it."""
+    end, and grpc.aio listens on a loopback port behind it.
+
+    ``tls``: dict(cert=PEM path, key=PEM path[, client_ca=PEM path]) serves
+    HTTPS and gRPC over TLS (mutual TLS when ``client_ca`` is given) from the
+    Python front ends (tcserve speaks plaintext only)."""
     server.loop = asyncio.get_running_loop()
+    if tls:
+        native_grpc = False
     if native_grpc is None:
         native_grpc = native_grpc_available()
     runner = None
@@ -67,7 +74,16 @@ async def serve(server, http_port, grpc_port, host="127.0.0.1", ready_evt=None, 
             await site.start()
             inner_http = site._server.sockets[0].getsockname()[1]
         else:
-            site = web.TCPSite(runner, host, http_port, reuse_address=True)
+            ctx = None
+            if tls:
+                import ssl
+
+                ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+                ctx.load_cert_chain(tls["cert"], tls["key"])
+                if tls.get("client_ca"):
+                    ctx.load_verify_locations(tls["client_ca"])
+                    ctx.verify_mode = ssl.CERT_REQUIRED
+            site = web.TCPSite(runner, host, http_port, reuse_address=True, ssl_context=ctx)
             await site.start()
     gserver = None
     nf = None
@@ -76,6 +92,17 @@ async def serve(server, http_port, grpc_port, host="127.0.0.1", ready_evt=None, 
         service_pb2_grpc.add_GRPCInferenceServiceServicer_to_server(GrpcFrontend(server), gserver)
         if native_grpc:
             inner = gserver.add_insecure_port("127.0.0.1:0")
+        elif tls:
+            with open(tls["key"], "rb") as f:
+                key = f.read()
+            with open(tls["cert"], "rb") as f:
+                cert = f.read()
+            ca = None
+            if tls.get("client_ca"):
+                with open(tls["client_ca"], "rb") as f:
+                    ca = f.read()
+            creds = grpc.ssl_server_credentials([(key, cert)], root_certificates=ca, require_client_auth=ca is not None)
+            gserver.add_secure_port("%s:%d" % (host, grpc_port), creds)
         else:
             gserver.add_insecure_port("%s:%d" % (host, grpc_port))
         await gserver.start()
@@ -105,8 +132,10 @@ async def serve(server, http_port, grpc_port, host="127.0.0.1", ready_evt=None, 
 class ServerHandle:
     """Runs an InferenceServer on a background thread (tests, benches)."""
 
-    def __init__(self, models=None, http_port=None, grpc_port=None, model_options=None, load=True, native_grpc=None):
+    def __init__(self, models=None, http_port=None, grpc_port=None, model_options=None, load=True, native_grpc=None,
+                 tls=None):
         self.native_grpc = native_grpc
+        self.tls = tls
         self.http_port = http_port or _free_port()
         self.grpc_port = grpc_port or _free_port()
         self.server = InferenceServer(models if models is not None else default_models(), model_options)
@@ -133,7 +162,7 @@ class ServerHandle:
         async def main():
             self._stop = asyncio.Event()
             await serve(self.server, self.http_port, self.grpc_port, ready_evt=self._ready, stop_evt=self._stop,
-                        native_grpc=self.native_grpc)
+                        native_grpc=self.native_grpc, tls=self.tls)
 
         loop.run_until_complete(main())
         loop.close()
