@@ -561,6 +561,7 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p
   if (t_begin >= t_end) return;
 
   if (tid < kRowB / 16) *reinterpret_cast<v4u*>(lds2 + kRing * kRowB + tid * 16) = v4u{0, 0, 0, 0};
+  const ptrdiff_t lo_off = p.z_lo - p.z_hi;
   // rows [g0, g0+nrows) -> ring, two rows per wave-instruction (ring row of g0 even)
   auto dma_rows = [&](int g0, int nrows) {
     const int plane = (lane >> 4) & 1, j = lane & 15;
@@ -569,7 +570,10 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p
       const int g = ga + (lane >> 5);
       const int pos = (g + W + 1) & (kRing - 1);
       const int gc = min(max(g, 0), p.M - 1);
-      const uint16_t* src = (plane ? p.z_lo : p.z_hi) + (size_t)gc * kC3 + ((j ^ (pos & 15)) << 3);
+      // plane select as an offset: a select between the two pointer fields
+      // makes hipcc reload one from the kernarg segment per lane (a vector
+      // load, whose vmcnt wait would drain the in-flight y stores)
+      const uint16_t* src = p.z_hi + (plane ? lo_off : 0) + (size_t)gc * kC3 + ((j ^ (pos & 15)) << 3);
       const int pos0 = (ga + W + 1) & (kRing - 1);
       __builtin_amdgcn_global_load_lds((const void*)src, (void*)(lds2 + pos0 * kRowB), 16, 0, 0);
     }
@@ -578,8 +582,13 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p
 
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int m0 = tile * kT2;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // B0: this band is in LDS everywhere; the scratch is free
+    // B0: this band is in LDS everywhere and the scratch is free.  The vm
+    // counter retires in issue order: [this band's DMA..., last tile's y
+    // store], so vmcnt(1) waits for the DMA and leaves the store (an HBM
+    // write round trip) in flight; the first tile has no store behind it.
+    if (tile == t_begin) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     if (tile + 1 < t_end) dma_rows(m0 + kT2 + W + 1, kT2);
 
     const int m = m0 + 32 * ph + col;
@@ -611,7 +620,11 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p
     rd(0, 0);
 #pragma unroll
     for (int t = 0; t < kTaps; ++t) {
+      // pin the order: tap t+1's 4 reads are issued before tap t's 6 MFMAs
+      // (a scheduling fence, so the two tap buffers stay in distinct
+      // registers), and each read's LDS latency hides behind a tap of MFMAs
       if (t + 1 < kTaps) rd(t + 1, (t + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int kc = 0; kc < 2; ++kc) acc = x3_32(wh[t][kc], wl[t][kc], bq[t & 1][kc][0], bq[t & 1][kc][1], acc);
     }
