@@ -23,6 +23,7 @@
 
 #include "grpc_client.h"
 #include "http_client.h"
+#include "json.h"
 #include "shm_utils.h"
 
 namespace tc = triton::client;
@@ -492,6 +493,144 @@ TestHttpSpecific(tc::InferenceServerHttpClient* c)
   CHECK(logs.find("\"log_verbose_level\":1") != std::string::npos, "log settings " << logs);
 }
 
+// Binary <-> JSON data conversion for every datatype, both directions, plus
+// the invalid cases (behaviour matrix of reference
+// src/c++/tests/cc_client_test.cc:1641-2171, exercised through the public
+// GenerateRequestBody / ParseResponseBody entry points; no server).
+namespace js = triton::client::json;
+
+template <typename T>
+static std::vector<uint8_t>
+Bytes(std::initializer_list<T> v)
+{
+  std::vector<uint8_t> b(v.size() * sizeof(T));
+  std::memcpy(b.data(), std::data(v), b.size());
+  return b;
+}
+
+// input (two AppendRaw chunks, sent as JSON) -> the request header's data array
+static bool
+InputJsonData(const std::string& dt, const std::vector<uint8_t>& a, const std::vector<uint8_t>& b, int64_t n,
+              js::Value* data, std::string* err)
+{
+  tc::InferInput* in;
+  tc::InferInput::Create(&in, "INPUT", {n}, dt);
+  std::unique_ptr<tc::InferInput> own(in);
+  in->AppendRaw(a);
+  in->AppendRaw(b);
+  in->SetBinaryData(false);
+  std::vector<char> body;
+  size_t hl = 0;
+  tc::Error e = tc::InferenceServerHttpClient::GenerateRequestBody(&body, &hl, tc::InferOptions("m"), {in});
+  if (!e.IsOk()) {
+    *err = e.Message();
+    return false;
+  }
+  js::Value root;
+  if (!js::Parse(body.data(), hl, &root, err)) return false;
+  const js::Value* ins = root.Find("inputs");
+  if (!ins || ins->Size() != 1) return false;
+  const js::Value* d = (*ins)[0].Find("data");
+  if (!d || (*ins)[0].Find("parameters") && (*ins)[0].Find("parameters")->Find("binary_data_size")) return false;
+  *data = *d;
+  return body.size() == hl;  // nothing sent in the binary section
+}
+
+// JSON output (a response body) -> the binary the result hands out
+static bool
+OutputBinary(const std::string& dt, const std::string& json_data, size_t n, std::vector<uint8_t>* out)
+{
+  std::string resp = "{\"model_name\":\"m\",\"outputs\":[{\"name\":\"o\",\"datatype\":\"" + dt + "\",\"shape\":[" +
+                     std::to_string(n) + "],\"data\":" + json_data + "}]}";
+  tc::InferResult* r = nullptr;
+  tc::Error e = tc::InferenceServerHttpClient::ParseResponseBody(&r, std::vector<char>(resp.begin(), resp.end()));
+  std::unique_ptr<tc::InferResult> own(r);
+  if (!e.IsOk() || !r || !r->RequestStatus().IsOk()) return false;
+  const uint8_t* b;
+  size_t sz;
+  if (!r->RawData("o", &b, &sz).IsOk()) return false;
+  out->assign(b, b + sz);
+  return true;
+}
+
+static void
+TestJsonDataMatrix()
+{
+  js::Value d;
+  std::string err;
+  // input -> JSON: the two appended chunks flatten into one array, in order
+  CHECK(InputJsonData("INT32", Bytes<int32_t>({1, 3, 5, 7}), Bytes<int32_t>({2, 4, 6, 8}), 8, &d, &err), err);
+  CHECK(d.Size() == 8 && d[0].AsInt() == 1 && d[3].AsInt() == 7 && d[4].AsInt() == 2 && d[7].AsInt() == 8,
+        "flattened AppendRaw chain");
+  struct Case {
+    const char* dt;
+    std::vector<uint8_t> a, b;
+    std::function<bool(const js::Value&)> check;
+  };
+  const std::vector<Case> cases = {
+      {"BOOL", Bytes<uint8_t>({0}), Bytes<uint8_t>({1}),
+       [](const js::Value& v) { return v[0].type() == js::Value::Type::Bool && !v[0].AsBool() && v[1].AsBool(); }},
+      {"UINT8", Bytes<uint8_t>({1}), Bytes<uint8_t>({UINT8_MAX}),
+       [](const js::Value& v) { return v[0].AsUInt() == 1 && v[1].AsUInt() == UINT8_MAX; }},
+      {"UINT16", Bytes<uint16_t>({1}), Bytes<uint16_t>({UINT16_MAX}),
+       [](const js::Value& v) { return v[0].AsUInt() == 1 && v[1].AsUInt() == UINT16_MAX; }},
+      {"UINT32", Bytes<uint32_t>({1}), Bytes<uint32_t>({UINT32_MAX}),
+       [](const js::Value& v) { return v[0].AsUInt() == 1 && v[1].AsUInt() == UINT32_MAX; }},
+      {"UINT64", Bytes<uint64_t>({1}), Bytes<uint64_t>({UINT64_MAX}),
+       [](const js::Value& v) { return v[0].AsUInt() == 1 && v[1].AsUInt() == UINT64_MAX; }},
+      {"INT8", Bytes<int8_t>({INT8_MIN}), Bytes<int8_t>({INT8_MAX}),
+       [](const js::Value& v) { return v[0].AsInt() == INT8_MIN && v[1].AsInt() == INT8_MAX; }},
+      {"INT16", Bytes<int16_t>({INT16_MIN}), Bytes<int16_t>({INT16_MAX}),
+       [](const js::Value& v) { return v[0].AsInt() == INT16_MIN && v[1].AsInt() == INT16_MAX; }},
+      {"INT32", Bytes<int32_t>({INT32_MIN}), Bytes<int32_t>({INT32_MAX}),
+       [](const js::Value& v) { return v[0].AsInt() == INT32_MIN && v[1].AsInt() == INT32_MAX; }},
+      {"INT64", Bytes<int64_t>({INT64_MIN}), Bytes<int64_t>({INT64_MAX}),
+       [](const js::Value& v) { return v[0].AsInt() == INT64_MIN && v[1].AsInt() == INT64_MAX; }},
+      {"FP32", Bytes<float>({-1.5f}), Bytes<float>({3.25e7f}),
+       [](const js::Value& v) { return v[0].AsDouble() == -1.5 && (float)v[1].AsDouble() == 3.25e7f; }},
+      {"FP64", Bytes<double>({-0.125}), Bytes<double>({1e300}),
+       [](const js::Value& v) { return v[0].AsDouble() == -0.125 && v[1].AsDouble() == 1e300; }},
+  };
+  for (const auto& c : cases) {
+    const bool ok = InputJsonData(c.dt, c.a, c.b, 2, &d, &err);
+    CHECK(ok && d.Size() == 2 && c.check(d), "input " << c.dt << " -> JSON " << err);
+  }
+  // BYTES: two length-prefixed elements in separate chunks -> two JSON strings
+  {
+    std::vector<uint8_t> a = {2, 0, 0, 0, 'a', 'b'}, b = {3, 0, 0, 0, 'c', 'd', 'e'};
+    const bool ok = InputJsonData("BYTES", a, b, 2, &d, &err);
+    CHECK(ok && d.Size() == 2 && d[0].AsString() == "ab" && d[1].AsString() == "cde", "input BYTES -> JSON " << err);
+  }
+  // invalid: half/bfloat16/fp8 cannot be JSON numbers; unknown datatypes fail
+  for (const char* bad : {"FP16", "BF16", "FP8_E4M3", "invaliddatatype"})
+    CHECK(!InputJsonData(bad, Bytes<uint16_t>({1}), Bytes<uint16_t>({2}), 2, &d, &err), "input " << bad << " must fail");
+
+  // JSON -> binary (response data arrays)
+  std::vector<uint8_t> out;
+  auto same = [&](const std::vector<uint8_t>& want) { return out == want; };
+  CHECK(OutputBinary("BOOL", "[false,true]", 2, &out) && same({0, 1}), "output BOOL");
+  CHECK(OutputBinary("UINT8", "[1,255]", 2, &out) && same(Bytes<uint8_t>({1, 255})), "output UINT8");
+  CHECK(OutputBinary("UINT16", "[1,65535]", 2, &out) && same(Bytes<uint16_t>({1, 65535})), "output UINT16");
+  CHECK(OutputBinary("UINT32", "[1,4294967295]", 2, &out) && same(Bytes<uint32_t>({1, 4294967295u})),
+        "output UINT32");
+  CHECK(OutputBinary("UINT64", "[1,18446744073709551615]", 2, &out) && same(Bytes<uint64_t>({1, UINT64_MAX})),
+        "output UINT64");
+  CHECK(OutputBinary("INT8", "[-128,127]", 2, &out) && same(Bytes<int8_t>({-128, 127})), "output INT8");
+  CHECK(OutputBinary("INT16", "[-32768,32767]", 2, &out) && same(Bytes<int16_t>({-32768, 32767})), "output INT16");
+  CHECK(OutputBinary("INT32", "[-2147483648,2147483647]", 2, &out) && same(Bytes<int32_t>({INT32_MIN, INT32_MAX})),
+        "output INT32");
+  CHECK(OutputBinary("INT64", "[-9223372036854775808,9223372036854775807]", 2, &out) &&
+            same(Bytes<int64_t>({INT64_MIN, INT64_MAX})),
+        "output INT64");
+  CHECK(OutputBinary("FP32", "[-1.5,3.25e7]", 2, &out) && same(Bytes<float>({-1.5f, 3.25e7f})), "output FP32");
+  CHECK(OutputBinary("FP64", "[-0.125,1e300]", 2, &out) && same(Bytes<double>({-0.125, 1e300})), "output FP64");
+  CHECK(OutputBinary("INT32", "[[1,2],[3,4]]", 4, &out) && same(Bytes<int32_t>({1, 2, 3, 4})),
+        "nested JSON arrays flatten row-major");
+  CHECK(OutputBinary("BYTES", "[\"ab\",\"\"]", 2, &out) && same({2, 0, 0, 0, 'a', 'b', 0, 0, 0, 0}), "output BYTES");
+  for (const char* bad : {"FP16", "BF16", "invaliddatatype"})
+    CHECK(!OutputBinary(bad, "[1,2]", 2, &out), "output " << bad << " must fail");
+}
+
 // InferInput buffer chain state, through the friend hook (reference
 // src/c++/tests/cc_client_test.cc:29-33 uses the same mechanism).
 static void
@@ -537,6 +676,7 @@ main(int argc, char** argv)
   };
   std::vector<T> tests = {
       {"friend hook", [&] { TestFriendHook(); }},
+      {"json data matrix", [&] { TestJsonDataMatrix(); }},
       {"health/metadata", [&] { TestHealthAndMetadata(http.get(), "http"); TestHealthAndMetadata(grpc.get(), "grpc"); }},
       {"infer", [&] { TestInfer(http.get(), "http"); TestInfer(grpc.get(), "grpc"); }},
       {"async/multi", [&] { TestAsyncAndMulti(http.get(), "http"); TestAsyncAndMulti(grpc.get(), "grpc"); }},
