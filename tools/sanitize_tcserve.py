@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""Run tcserve (the native gRPC + HTTP front end, csrc/cpp/server) built with a
+sanitizer preset inside the Python test server, and drive it with the native
+clients on every path it serves: gRPC unary/async/streaming, pipelined
+HTTP/1.1 (binary + JSON bodies, gzip), system shared memory, BYTES tensors,
+malformed and oversized requests, connection churn.
+
+The server runs as a child process with the sanitizer runtime preloaded
+(``LD_PRELOAD`` = the runtime of the preset, prepended to any existing
+value) and ``TCSERVE_LIB`` pointing at the instrumented ``libtcserve.so``;
+Python itself is not instrumented, so ASan's leak checker is off (the
+interpreter's own allocations would drown it) and reports are filtered to
+frames in our code.
+
+    make -C csrc/cpp asan && python tools/sanitize_tcserve.py --preset asan --out profiles/r2_sanitize_tcserve.md
+"""
+
+import argparse
+import glob
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def runtime(preset):
+    if preset == "asan":
+        libs = ["libasan.so", "libubsan.so"]
+        out = []
+        for name in libs:
+            p = subprocess.run(["gcc", "-print-file-name=" + name], capture_output=True, text=True).stdout.strip()
+            if os.path.isabs(p) and os.path.exists(p):
+                out.append(p)
+        return out
+    clang_rt = glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.tsan-x86_64.so")
+    return clang_rt[:1]
+
+
+def raw_http(port, payload, timeout=5.0):
+    """Send raw bytes over HTTP/1.1 and return the status line (malformed-input probes)."""
+    s = socket.create_connection(("127.0.0.1", port), timeout=timeout)
+    try:
+        s.sendall(payload)
+        data = b""
+        while b"\r\n" not in data:
+            chunk = s.recv(4096)
+            if not chunk:
+                break
+            data += chunk
+        return data.split(b"\r\n", 1)[0].decode(errors="replace")
+    except OSError as e:
+        return "error: %s" % e
+    finally:
+        s.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--preset", default="asan", choices=["asan", "tsan"])
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    build = os.path.join(REPO, "csrc", "cpp", "build-" + a.preset)
+    lib = os.path.join(build, "lib", "libtcserve.so")
+    if not os.path.exists(lib):
+        raise SystemExit("build the preset first: make -C csrc/cpp %s" % a.preset)
+    rt = runtime(a.preset)
+    if not rt:
+        raise SystemExit("no %s runtime found" % a.preset)
+    http_port, grpc_port = free_port(), free_port()
+    log_dir = os.path.join(REPO, "gpurun_out", "sanitize_tcserve_" + a.preset)
+    os.makedirs(log_dir, exist_ok=True)
+    for f in glob.glob(os.path.join(log_dir, "*")):
+        os.remove(f)
+    env = dict(os.environ, TCSERVE_LIB=lib,
+               LD_PRELOAD=":".join(rt + ([os.environ["LD_PRELOAD"]] if os.environ.get("LD_PRELOAD") else [])),
+               ASAN_OPTIONS="detect_leaks=0:halt_on_error=0:log_path=%s/asan" % log_dir,
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=0:log_path=%s/ubsan" % log_dir,
+               TSAN_OPTIONS="halt_on_error=0:report_signal_unsafe=0:log_path=%s/tsan" % log_dir,
+               PYTHONPATH=REPO)
+    ready = os.path.join(log_dir, "ready")
+    srv = subprocess.Popen([sys.executable, "-m", "triton_client_amd.server", "--http-port", str(http_port),
+                            "--grpc-port", str(grpc_port), "--native-grpc", "on", "--ready-file", ready],
+                           env=env, stdout=open(os.path.join(log_dir, "server.out"), "w"),
+                           stderr=subprocess.STDOUT, cwd=REPO)
+    t0 = time.time()
+    while not os.path.exists(ready):
+        if srv.poll() is not None or time.time() - t0 > 120:
+            raise SystemExit("server did not start; see %s/server.out" % log_dir)
+        time.sleep(0.2)
+    # prove the instrumented objects are the ones mapped into the server
+    maps = open("/proc/%d/maps" % srv.pid).read()
+    mapped = {"runtime": any(os.path.basename(r) in maps for r in rt), "instrumented libtcserve": lib in maps}
+    print("mapped into the server:", mapped, flush=True)
+    http, grpc = "127.0.0.1:%d" % http_port, "127.0.0.1:%d" % grpc_port
+    bindir = os.path.join(REPO, "csrc", "cpp", "build", "bin")
+    pa = os.path.join(bindir, "perf_analyzer")
+    drive = [
+        ("cc_client_test", [os.path.join(bindir, "cc_client_test"), http, grpc]),
+        ("perf gRPC async c8", [pa, "-m", "simple", "-i", "grpc", "-u", grpc, "--concurrency-range", "8", "-p", "400",
+                                "-r", "3", "-s", "80"]),
+        ("perf gRPC streaming", [pa, "-m", "simple", "-i", "grpc", "-u", grpc, "--streaming", "--concurrency-range",
+                                 "4", "-p", "300", "-r", "3", "-s", "80"]),
+        ("perf gRPC system shm", [pa, "-m", "simple", "-i", "grpc", "-u", grpc, "--shared-memory", "system",
+                                  "--concurrency-range", "4", "-p", "300", "-r", "3", "-s", "80"]),
+        ("perf HTTP pipelined c8", [pa, "-m", "simple", "-i", "http", "-u", http, "--concurrency-range", "8", "-p",
+                                    "400", "-r", "3", "-s", "80"]),
+        ("perf HTTP system shm", [pa, "-m", "simple", "-i", "http", "-u", http, "--shared-memory", "system",
+                                  "--concurrency-range", "4", "-p", "300", "-r", "3", "-s", "80"]),
+        ("perf HTTP BYTES", [pa, "-m", "simple_string", "-i", "http", "-u", http, "--string-data", "7", "-p", "300",
+                             "-r", "3", "-s", "80"]),
+        ("perf gRPC sync x4 clients", [pa, "-m", "simple", "-i", "grpc", "-u", grpc, "--sync", "--concurrency-range",
+                                       "4", "-p", "300", "-r", "3", "-s", "80"]),
+    ]
+    for ex in ("simple_http_infer_client", "simple_grpc_infer_client", "simple_http_shm_client",
+               "simple_grpc_shm_client", "simple_grpc_async_infer_client", "simple_http_async_infer_client",
+               "simple_grpc_sequence_stream_infer_client", "simple_http_string_infer_client"):
+        drive.append((ex, [os.path.join(bindir, ex), "-u", grpc if "grpc" in ex else http]))
+    rows = []
+    for name, cmd in drive:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
+        rows.append((name, r.returncode))
+        print("%-32s rc=%d" % (name, r.returncode), flush=True)
+    # malformed / hostile input on the native HTTP port
+    probes = [
+        ("negative shm byte size", b"POST /v2/models/simple/infer HTTP/1.1\r\nHost: x\r\nContent-Length: 160\r\n\r\n"
+         b'{"inputs":[{"name":"INPUT0","shape":[1,16],"datatype":"INT32","parameters":{"shared_memory_region":"r",'
+         b'"shared_memory_byte_size":-1}}]}' + b" " * 40),
+        ("huge chunk size", b"POST /v2/models/simple/infer HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n"
+         b"ffffffffffffffff\r\nab\r\n0\r\n\r\n"),
+        ("oversized content-length", b"POST /v2/models/simple/infer HTTP/1.1\r\nHost: x\r\n"
+         b"Content-Length: 99999999999\r\n\r\n{}"),
+        ("garbage request line", b"\x00\x01\x02 nonsense\r\n\r\n"),
+        ("truncated binary body", b"POST /v2/models/simple/infer HTTP/1.1\r\nHost: x\r\n"
+         b"Inference-Header-Content-Length: 500\r\nContent-Length: 10\r\n\r\n0123456789"),
+    ]
+    for name, payload in probes:
+        status = raw_http(http_port, payload)
+        rows.append(("probe: " + name, 0 if srv.poll() is None else 1))
+        print("%-32s %s" % ("probe: " + name, status), flush=True)
+    alive = srv.poll() is None
+    srv.send_signal(signal.SIGINT)
+    try:
+        srv.wait(30)
+    except subprocess.TimeoutExpired:
+        srv.kill()
+    # a report is ours when any of its frames is in the instrumented library;
+    # races between uninstrumented third-party threads (grpcio's cygrpc event
+    # engine, CPython) are TSan false positives: their synchronisation is
+    # invisible to it.  They are counted and listed, not failed on.
+    reports, foreign = [], 0
+    for f in sorted(glob.glob(os.path.join(log_dir, "*san*"))):
+        text = open(f, errors="replace").read()
+        for blk in text.split("=================="):
+            if not ("ERROR: AddressSanitizer" in blk or "runtime error:" in blk or "WARNING: ThreadSanitizer" in blk):
+                continue
+            if "libtcserve" in blk or "csrc/cpp" in blk:
+                reports.append((os.path.basename(f), blk[:3000]))
+            else:
+                foreign += 1
+    lines = ["# tcserve under %s (round 2)" % a.preset.upper(), "",
+             "`tools/sanitize_tcserve.py --preset %s`: the instrumented `libtcserve.so` (`make -C csrc/cpp %s`) "
+             "loaded by the Python test server (runtime preloaded, leak checker off: Python is not instrumented), "
+             "driven by the native clients and hostile HTTP inputs." % (a.preset, a.preset), "",
+             "| driver | result |", "|---|---|"]
+    for name, rc in rows:
+        lines.append("| %s | %s |" % (name, "ok" if rc == 0 else "rc=%d" % rc))
+    lines += ["", "Mapped into the server process (/proc/PID/maps): sanitizer runtime **%s**, instrumented "
+              "`%s` **%s**." % (mapped["runtime"], os.path.relpath(lib, REPO), mapped["instrumented libtcserve"]),
+              "", "Server alive after all drivers and probes: **%s**." % alive, "",
+              "Sanitizer reports with a frame in the instrumented `libtcserve.so`: **%d**." % len(reports),
+              "", "Reports entirely inside uninstrumented third-party code (grpcio cygrpc / CPython threads; "
+              "their synchronisation is invisible to the sanitizer): %d." % foreign]
+    for fname, text in reports:
+        lines += ["", "### %s" % fname, "", "```", text, "```"]
+    md = "\n".join(lines) + "\n"
+    print(md)
+    if a.out:
+        open(a.out, "w").write(md)
+    ok = alive and not reports and all(rc == 0 for _, rc in rows) and all(mapped.values())
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

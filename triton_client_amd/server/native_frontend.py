@@ -19,7 +19,8 @@ import os
 import threading
 
 _REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-LIB_PATH = os.path.join(_REPO, "csrc", "cpp", "build", "lib", "libtcserve.so")
+# TCSERVE_LIB: an alternative build (the sanitizer presets, tools/sanitize_tcserve.py)
+LIB_PATH = os.environ.get("TCSERVE_LIB") or os.path.join(_REPO, "csrc", "cpp", "build", "lib", "libtcserve.so")
 
 
 class TcRef(ctypes.Structure):
