@@ -279,10 +279,16 @@ def main():
         pc1 = Point(srv, model, 1, 1, "data_1_in", in1, local_rank, cpu)
         points.append(pc1)
         pc1.run(20)
+        sc0 = pc1.s.server_stats()
         lc, _, _ = pc1.run(200)
+        sc1 = pc1.s.server_stats()
         lcg = fanout.gather_arrays(lc.astype(np.int64)).astype(np.float64)
         bs1["concurrency1_p50_latency_us"] = round(percentile_us(lcg, 50), 1)
         bs1["concurrency1_p99_latency_us"] = round(percentile_us(lcg, 99), 1)
+        # where one bs=1 request's latency goes (server-stat deltas over the 200 requests)
+        bd1 = stats_delta(sc0, sc1)
+        bd1["client_overhead_us_per_request"] = round(float(np.mean(lc)) / 1e3 - bd1["server_us_per_request"], 1)
+        bs1["concurrency1_breakdown_rank0"] = bd1
 
         res = {
             "metric": METRIC,
