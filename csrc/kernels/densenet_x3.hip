@@ -931,7 +931,13 @@ int tcamd_x3_conv3x3(const void* z_hi, const void* z_lo, int imgs, int H, int W,
   if (p.M >= (1 << 24)) return hipErrorInvalidValue;  // fast_divmod range
   // one block (8 waves) per CU; each walks a contiguous run of tiles so the
   // halo rows its neighbour tile re-reads are still in this XCD's L2
-  static const bool v1 = getenv("TCAMD_X3_K9") && atoi(getenv("TCAMD_X3_K9")) == 1;
+  // v2 (64-px tiles, LDS-DMA ring, one-round reduction) for the big layers;
+  // v1 (128-px tiles) where a block walks only a tile or two and v2's extra
+  // per-tile barrier pair is not amortised (MI355X, tools/gpu_x3_3x3.sh:
+  // 56x56 bs128 104 vs 123 us, 28x28 33 vs 39; 14x14 bs128 16.3 vs 14.3).
+  // TCAMD_X3_K9=1/2 forces one (A/B runs).
+  static const int force = getenv("TCAMD_X3_K9") ? atoi(getenv("TCAMD_X3_K9")) : 0;
+  const bool v1 = force == 1 || (force != 2 && p.M <= 32768);
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e =

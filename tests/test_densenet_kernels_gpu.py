@@ -37,7 +37,7 @@ def _close(got, ref, tol=2e-2):
 
 @pytest.mark.parametrize("M,K,ldx,N,off", [(100, 64, 96, 128, 32), (40000, 224, 256, 128, 0),
                                            (70000, 96, 128, 128, 0), (3000, 512, 512, 256, 0)])
-@pytest.mark.parametrize("variant", [0, 70, 112, 114, 124, 143, 211, 212, 221, 222, 300])
+@pytest.mark.parametrize("variant", [0, 11, 21, 41, 211, 212, 221, 222])
 def test_conv1x1_prologue_epilogue(M, K, ldx, N, off, variant):
     _need_gpu()
     if variant == 300 and K > 256:
@@ -63,7 +63,7 @@ def test_conv1x1_prologue_epilogue(M, K, ldx, N, off, variant):
 
 @pytest.mark.parametrize("M,K,N,pool,splits", [(49, 992, 128, 0, 0), (196, 640, 128, 0, 4), (49, 1024, 512, 1, 0),
                                                (300, 96, 128, 0, 3), (1000, 512, 256, 0, 16)])
-@pytest.mark.parametrize("variant", [0, 11, 12, 21, 42, 70])
+@pytest.mark.parametrize("variant", [0, 11, 12, 21, 42])
 def test_conv1x1_split_k(M, K, N, pool, splits, variant):
     """Split-K partials + reduce must equal the single-pass kernel's math."""
     _need_gpu()
@@ -128,7 +128,7 @@ def test_conv1x1_transition_pool(imgs, H, C, N):
     assert (y[:, N:] == 0).all()
 
 
-@pytest.mark.parametrize("variant", [0, 10, 11, 13, 16, 19, 21, 41, 51, 52, 60, 70, 80, 90, 91, 92, 93])
+@pytest.mark.parametrize("variant", [0, 11, 70, 92])
 @pytest.mark.parametrize("imgs,H", [(1, 7), (3, 14), (8, 56), (48, 56), (5, 28)])
 def test_conv3x3(imgs, H, variant):
     _need_gpu()
