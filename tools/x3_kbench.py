@@ -46,6 +46,7 @@ def main():
             hip.x3_conv3x3(zh.data_ptr(), zl.data_ptr(), args.imgs, args.hw, args.hw, wh.data_ptr(), wl.data_ptr(),
                            y.data_ptr(), ldy, stream=st)
         flop = 2.0 * M * 1152 * 32
+        hbm = 4.0 * M * (128 + 32)
     else:
         pool = args.op == "pool"
         K = args.k
@@ -73,6 +74,7 @@ def main():
                                out_bias=b.data_ptr(), z_hi=zh.data_ptr(), z_lo=zl.data_ptr(), ws=ws.data_ptr(),
                                ws_bytes=wsb, stream=st)
         flop = 2.0 * Mo * K * N
+        hbm = 4.0 * (M * K + Mo * N)
     for _ in range(3):
         run()
     torch.cuda.synchronize()
@@ -81,8 +83,8 @@ def main():
         run()
     torch.cuda.synchronize()
     us = 1e6 * (time.perf_counter() - t0) / args.iters
-    print("%s hw=%d imgs=%d k=%d: %.1f us/launch, %.0f TFLOP/s fp32-equivalent (x3 on MFMA: %.0f)" % (
-        args.op, args.hw, args.imgs, args.k, us, flop / us / 1e6, 3 * flop / us / 1e6), flush=True)
+    print("%s hw=%d imgs=%d k=%d: %.1f us/launch, %.0f TFLOP/s fp32-equivalent (x3 on MFMA: %.0f), %.2f TB/s" % (
+        args.op, args.hw, args.imgs, args.k, us, flop / us / 1e6, 3 * flop / us / 1e6, hbm / us / 1e6), flush=True)
 
 
 if __name__ == "__main__":
