@@ -319,6 +319,261 @@ __global__ void __launch_bounds__(256) x3_splitk_reduce_kernel(X3Conv1x1Params p
   }
 }
 
+// ---- K8x (ws): warp-specialised persistent 1x1 for the big dense layers ----
+// The tiled kernel above runs every phase of a K step in lockstep (global
+// loads -> BN/ReLU/split VALU -> LDS -> MFMA -> barrier), so per SIMD the MFMA
+// and the conversion VALU take turns and a block's loads are exposed every
+// step (MI355X, 56x56 K=256 bs128: MFMA 19% busy, ~3.1 TB/s).  Here a block
+// of 8 waves (one per CU) splits the work by role:
+//   * waves 0-3 (consumers) own a 64 x 64 quarter of the 128-pixel x 128-
+//     channel tile: 2 x 2 blocks of 32x32x16 MFMA, 24 per K step (768 cycles),
+//     operands read from the LDS stage of the step;
+//   * waves 4-7 (producers) keep PF K steps of X in flight in registers,
+//     apply BN1+ReLU and the hi/lo split to one step per iteration into the
+//     LDS stage two steps ahead, and copy the W hi/lo slices with LDS-DMA
+//     (global_load_lds) S-1 steps ahead;
+// so the conversion of step q+1 runs on the same SIMDs as the MFMAs of step
+// q, and the only per-step synchronisation is one raw s_barrier (counted
+// vmcnt: the younger X loads and W copies stay in flight across it).
+// A block walks a contiguous run of pixels (whole 16-pixel units: every
+// block moves the same bytes), the K steps of its consecutive tiles form one
+// flat stream, so the pipeline never drains between tiles.
+// LDS stage = X hi|lo + W hi|lo, each [128 rows][32 bf16] with the 16-B
+// chunks XOR-swizzled by (row >> 2) & 3 (conflict-free b128 reads by 16
+// consecutive rows).
+constexpr int kWsS = 4;                          // LDS stages
+constexpr int kWsPlane = 128 * kBK * 2;          // 8 KB: one [128][32] bf16 plane
+constexpr int kWsStage = 4 * kWsPlane;           // Xh Xl Wh Wl
+constexpr int kLdsWs = kWsS * kWsStage + 4 * 8192;  // 128 KB stages + 4 x 8 KB epilogue slabs = 160 KB
+
+struct X3WsParams {
+  X3Conv1x1Params c;
+  int units_per_block;  // 16-pixel units per block
+  int dbg;              // ablation (tools/x3_kbench.py): 1 = no MFMA, 2 = no z stores
+};
+
+// s_waitcnt immediates for gfx9-family (vmcnt 6 bits split [3:0]+[15:14],
+// expcnt [6:4], lgkmcnt [11:8]); as a builtin (not inline asm) the
+// compiler's own wait insertion knows the wait happened
+constexpr int ws_vmcnt(int n) { return (((n >> 4) & 3) << 14) | (0xF << 8) | (7 << 4) | (n & 15); }
+constexpr int ws_vmcnt_lgkm0(int n) { return (((n >> 4) & 3) << 14) | (7 << 4) | (n & 15); }
+
+// raw s_barrier (no implicit vmcnt(0)) that the compiler may not move LDS
+// accesses across; the caller issues the s_waitcnt it needs first
+__device__ __forceinline__ void ws_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ int ws_chunk(int row, int c) { return row * 64 + ((c ^ ((row >> 2) & 3)) << 4); }
+
+// kWsPF: X steps in flight in the producers' registers
+template <int kWsPF>
+__global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t ldsw[];
+  const X3Conv1x1Params& p = wp.c;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int u0 = blockIdx.x * wp.units_per_block;
+  const int mbeg = 16 * u0;
+  const int mend = min(p.M, 16 * (u0 + wp.units_per_block));
+  if (mbeg >= mend) return;
+  const int nst = p.K / kBK;
+  const int ntiles = (mend - mbeg + 127) / 128;
+  const int Q = ntiles * nst;  // K steps of this block
+  const int Qp = (Q + kWsPF - 1) / kWsPF * kWsPF;  // both roles run Qp barrier rounds
+
+  if (wave >= 4) {
+    // ------------------------------ producer ------------------------------
+    const int pt = tid - 256, pw = wave - 4;
+    const int pj = pt & 7, prow = pt >> 3;  // X: rows prow + 32i, k offset 4 pj
+    const ptrdiff_t lo_off = p.w_lo - p.w_hi;
+    f32x4 xr[kWsPF][4], xs[kWsPF], xt[kWsPF];
+    // step q -> (tile, k0); q past the end re-loads the last step (static
+    // vmcnt).  BN1 scale/shift ride with the X slot: an LDS copy would be
+    // read after the W DMA, and the compiler orders every LDS read after all
+    // in-flight LDS-DMA (vmcnt(0)), which would drain the pipeline.
+    // K steps of a tile run in a block-rotated order: at any moment the blocks
+    // then read different column offsets of their X rows (all blocks on the
+    // same offset would camp on a subset of the HBM channels)
+    const int rot = (wp.dbg & 4) ? 0 : (int)(blockIdx.x % (unsigned)nst);
+    auto kofs = [&](int ks) { ks += rot; return (ks >= nst ? ks - nst : ks) * kBK; };
+    auto issue_x = [&](int q, int slot) {
+      q = min(q, Q - 1);
+      const int tile = q / nst, k0 = kofs(q - tile * nst);
+      xs[slot] = ldf4(p.in_scale + k0 + 4 * pj);
+      xt[slot] = ldf4(p.in_bias + k0 + 4 * pj);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = min(mbeg + tile * 128 + prow + 32 * i, mend - 1);
+        xr[slot][i] = ldf4(p.x + (size_t)m * p.ldx + k0 + 4 * pj);
+      }
+    };
+    // W hi/lo slice of step q -> stage q % S: 16 x 1 KB DMA, 4 per producer wave
+    auto issue_w = [&](int q) {
+      q = min(q, Q - 1);
+      const int k0 = kofs(q % nst);
+      uint8_t* st = ldsw + (q % kWsS) * kWsStage + 2 * kWsPlane;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ii = 4 * pw + i, plane = ii >> 3, rb = ii & 7;
+        const int row = 16 * rb + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 3);
+        const uint16_t* src = p.w_hi + (plane ? lo_off : 0) + (size_t)row * p.K + k0 + 8 * c;
+        __builtin_amdgcn_global_load_lds((const void*)src, (void*)(st + plane * kWsPlane + rb * 1024), 16, 0, 0);
+      }
+    };
+    auto write_x = [&](int q, int slot) {
+      const int qq = min(q, Q - 1);
+      const int tile = qq / nst;
+      uint8_t* st = ldsw + (q % kWsS) * kWsStage;
+      const f32x4 sc = xs[slot], sb = xt[slot];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = prow + 32 * i;
+        const bool ok = mbeg + tile * 128 + row < mend;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = ok ? fmaxf(xr[slot][i][e] * sc[e] + sb[e], 0.f) : 0.f;
+        v2u h, l;
+        split4(v, h, l);
+        const int off = ws_chunk(row, pj >> 1) + (pj & 1) * 8;
+        *reinterpret_cast<v2u*>(st + off) = h;
+        *reinterpret_cast<v2u*>(st + kWsPlane + off) = l;
+      }
+    };
+    // prologue: X steps 0..PF-1, W steps 0..S-3, step 0 staged; then the
+    // steady-state issue of "iteration -1" (X step PF, W step S-2)
+#pragma unroll
+    for (int s = 0; s < kWsPF; ++s) issue_x(s, s);
+    for (int s = 0; s <= kWsS - 3; ++s) issue_w(s);
+    __builtin_amdgcn_s_waitcnt(ws_vmcnt(0));
+    write_x(0, 0);
+    issue_x(kWsPF, 0);
+    issue_w(kWsS - 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ws_barrier();  // B0
+    // iteration q (consumers on step q): stage step q+1's X, refill its
+    // register slot with step q+1+PF, DMA W of step q+S-1, then wait for
+    // W of step q+1 (issued S-2 iterations ago: 10 younger ops per iteration:
+    // 6 X-slot loads, 4 W copies)
+    // Qp steps (a multiple of PF: no early exit out of the unrolled body,
+    // whose merge would make the compiler's own wait insertion drain vmcnt)
+    for (int q0 = 0; q0 < Qp; q0 += kWsPF) {
+#pragma unroll
+      for (int u = 0; u < kWsPF; ++u) {
+        const int q = q0 + u;
+        const int slot = (u + 1) % kWsPF;
+        // X of step q+1 was issued PF iterations back (4 + 10 (PF-1) younger ops)
+        __builtin_amdgcn_s_waitcnt(ws_vmcnt(4 + 10 * (kWsPF - 1)));
+        __builtin_amdgcn_sched_barrier(0);
+        write_x(q + 1, slot);
+        issue_x(q + 1 + kWsPF, slot);
+        issue_w(q + kWsS - 1);
+        __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0(20));
+        ws_barrier();  // B(q+1)
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA into LDS after the block ends
+    return;
+  }
+
+  // ------------------------------- consumer -------------------------------
+  const int wm = wave & 1, wn = wave >> 1;  // 64-pixel half, 64-channel half
+  const int col = lane & 31, h = lane >> 5;
+  f32x16 acc[2][2];  // [channel block][pixel block]
+  f32x4 ob[2][4];    // BN2 shift of this lane's 32 output channels
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) ob[a][g] = ldf4(p.out_bias + 64 * wn + 32 * a + 8 * g + 4 * h);
+  ws_barrier();  // B0
+  int tile = 0, ks = 0;
+  for (int q = 0; q < Qp; ++q) {
+    if (q >= Q) {  // padding rounds: keep the barrier count of the producers
+      ws_barrier();
+      continue;
+    }
+    if (ks == 0) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+    }
+    const uint8_t* st = ldsw + (q % kWsS) * kWsStage;
+    v4u ah[2][2], al[2][2], bh[2][2], bl[2][2];  // [ksub][block]
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int xo = ws_chunk(64 * wm + 32 * b + col, 2 * kk + h);
+        const int wo = ws_chunk(64 * wn + 32 * b + col, 2 * kk + h);
+        bh[kk][b] = ld16(st + xo);
+        bl[kk][b] = ld16(st + kWsPlane + xo);
+        ah[kk][b] = ld16(st + 2 * kWsPlane + wo);
+        al[kk][b] = ld16(st + 3 * kWsPlane + wo);
+      }
+    if (!(wp.dbg & 1)) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = x3_32(ah[kk][a], al[kk][a], bh[kk][b], bl[kk][b], acc[a][b]);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int a = 0; a < 2; ++a) acc[a][0][0] += __builtin_bit_cast(float, ah[kk][a][0] ^ al[kk][a][1] ^ bh[kk][a][2] ^ bl[kk][a][3]);
+    }
+    if (ks == nst - 1 && !(wp.dbg & 2)) {
+      // epilogue through this wave's 8 KB LDS slab: per 32-pixel block, the
+      // bias+ReLU+split 64-channel rows land as [32 px][64 ch] hi and lo
+      // (16-B chunks XOR-swizzled by pixel), then leave as 16-B-per-lane
+      // stores that cover whole 128-B lines of z (8 pixels per instruction)
+      // instead of 32 scattered 16-B pieces
+      uint8_t* slab = ldsw + kWsS * kWsStage + wave * 8192;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 bb = ob[a][g];
+            const f32x4 r = f32x4{fmaxf(acc[a][b][4 * g] + bb[0], 0.f), fmaxf(acc[a][b][4 * g + 1] + bb[1], 0.f),
+                                  fmaxf(acc[a][b][4 * g + 2] + bb[2], 0.f), fmaxf(acc[a][b][4 * g + 3] + bb[3], 0.f)};
+            v2u hh, ll;
+            split4(r, hh, ll);
+            const int off = col * 128 + (((4 * a + g) ^ (col & 7)) << 4) + 8 * h;
+            *reinterpret_cast<v2u*>(slab + off) = hh;
+            *reinterpret_cast<v2u*>(slab + 4096 + off) = ll;
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int pass = 0; pass < 4; ++pass) {
+          const int px = 8 * pass + (lane >> 3), c = lane & 7;
+          const int off = px * 128 + ((c ^ (px & 7)) << 4);
+          const v4u vh = ld16(slab + off), vl = ld16(slab + 4096 + off);
+          const int m = mbeg + tile * 128 + 64 * wm + 32 * b + px;
+          if (m < mend) {
+            *reinterpret_cast<v4u*>(p.z_hi + (size_t)m * kBN + 64 * wn + 8 * c) = vh;
+            *reinterpret_cast<v4u*>(p.z_lo + (size_t)m * kBN + 64 * wn + 8 * c) = vl;
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab reads done before block b+1 rewrites it
+      }
+    }
+    if (ks == nst - 1) {
+      ks = 0;
+      ++tile;
+    } else {
+      ++ks;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ws_barrier();  // B(q+1): stage q is free
+  }
+}
+
 // ============================================================================
 // K9x: 3x3 conv 128 -> 32 (stride 1, pad 1) on the split bottleneck
 // ============================================================================
@@ -901,6 +1156,33 @@ int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, int N, const float* 
     p.k_per_split = K;
   }
   hipStream_t s = (hipStream_t)stream;
+  // warp-specialised persistent kernel for the big dense-layer 1x1s
+  // (TCAMD_X3_WS=0 turns it off for A/B runs)
+  static const int ws_mode = getenv("TCAMD_X3_WS") ? atoi(getenv("TCAMD_X3_WS")) : 1;
+  if (ws_mode && !pool && split_out && N == kBN && M >= 65536) {
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      hipError_t e = hipGetDevice(&dev);
+      if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      if (e == hipSuccess) e = hipFuncSetAttribute((const void*)x3_conv1x1_ws_kernel<3>,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, kLdsWs);
+      if (e == hipSuccess) e = hipFuncSetAttribute((const void*)x3_conv1x1_ws_kernel<5>,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, kLdsWs);
+      if (e != hipSuccess) return e;
+    }
+    X3WsParams wp;
+    wp.c = p;
+    static const int dbg = getenv("TCAMD_X3_WS_DBG") ? atoi(getenv("TCAMD_X3_WS_DBG")) : 0;
+    wp.dbg = dbg;
+    const int units = (M + 15) / 16;
+    wp.units_per_block = (units + ncu - 1) / ncu;
+    const int blocks = (units + wp.units_per_block - 1) / wp.units_per_block;
+    static const int ws_pf = getenv("TCAMD_X3_WS_PF") ? atoi(getenv("TCAMD_X3_WS_PF")) : 3;
+    if (ws_pf == 5) hipLaunchKernelGGL(x3_conv1x1_ws_kernel<5>, dim3(blocks), dim3(512), kLdsWs, s, wp);
+    else hipLaunchKernelGGL(x3_conv1x1_ws_kernel<3>, dim3(blocks), dim3(512), kLdsWs, s, wp);
+    return hipGetLastError();
+  }
   const dim3 g((M + pl.bm - 1) / pl.bm, pl.splits, N / kBN);
   if (pool) {
     if (split_out) launch_x3_1x1<true, true>(pl, g, s, p);
@@ -941,13 +1223,12 @@ int tcamd_x3_conv3x3(const void* z_hi, const void* z_lo, int imgs, int H, int W,
   if (p.M >= (1 << 24)) return hipErrorInvalidValue;  // fast_divmod range
   // one block (8 waves) per CU; each walks a contiguous run of tiles so the
   // halo rows its neighbour tile re-reads are still in this XCD's L2
-  // v2 (64-px tiles, LDS-DMA ring, one-round reduction) for the big layers;
-  // v1 (128-px tiles) where a block walks only a tile or two and v2's extra
-  // per-tile barrier pair is not amortised (MI355X, tools/gpu_x3_3x3.sh:
-  // 56x56 bs128 104 vs 123 us, 28x28 33 vs 39; 14x14 bs128 16.3 vs 14.3).
-  // TCAMD_X3_K9=1/2 forces one (A/B runs).
+  // v2 (64-px tiles, LDS-DMA ring, one-round reduction) everywhere: in the
+  // bs128 forward (profiles/r2_x3_forward_b128_ws.md) it beats v1 at every
+  // size (56x56 104 vs 123 us, 28x28 33 vs 39, 14x14 ~17.5 vs 18.2, 7x7 13.8
+  // vs 14.8).  TCAMD_X3_K9=1 forces v1 (A/B runs).
   static const int force = getenv("TCAMD_X3_K9") ? atoi(getenv("TCAMD_X3_K9")) : 0;
-  const bool v1 = force == 1 || (force != 2 && p.M <= 32768);
+  const bool v1 = force == 1;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e =

@@ -59,10 +59,13 @@ def test_split_is_exact_to_2e17():
 
 
 @pytest.mark.parametrize("M,K,ldx", [(100, 64, 96), (37, 992, 1024), (6272, 512, 1024), (50000, 224, 256),
-                                     (401408, 96, 256), (25088, 640, 1024), (1568, 768, 1024), (392, 992, 1024)])
+                                     (401408, 96, 256), (25088, 640, 1024), (1568, 768, 1024), (392, 992, 1024),
+                                     (65555, 32, 32), (100352, 480, 512), (70001, 1024, 1024)])
 def test_x3_conv1x1_split_out(M, K, ldx):
     """Dense-layer 1x1: z = relu(relu(x*s+t) @ W^T + b) as hi/lo planes
-    (large M: whole-K blocks; small M: split-K workspace + reduce)."""
+    (M >= 65536: the warp-specialised persistent kernel, incl. ragged block
+    ranges and a single K step; mid M: whole-K tiles; small M: split-K
+    workspace + reduce)."""
     _need_gpu()
     hip = _hip()
     g = torch.Generator(device=DEV).manual_seed(M + K)
