@@ -930,10 +930,11 @@ struct X3StemParams {
   int ldy;
 };
 
+template <bool V2>
 __global__ void __launch_bounds__(256) x3_stem_kernel(X3StemParams p) {
   __shared__ __attribute__((aligned(16))) uint16_t Ih[kSIR * kSIC * 4];  // 13.2 KB
   __shared__ __attribute__((aligned(16))) uint16_t Il[kSIR * kSIC * 4];
-  __shared__ __attribute__((aligned(16))) float Cv[kSCR * kSCC * kSOS];   // 78 KB
+  __shared__ __attribute__((aligned(16))) float Cv[V2 ? 4 : kSCR * kSCC * kSOS];   // v1: 78 KB conv tile
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int img = blockIdx.z, pr0 = blockIdx.y * kSPR, pc0 = blockIdx.x * kSPC;
   const int ir0 = 4 * pr0 - 5, ic0 = 4 * pc0 - 5;
@@ -964,7 +965,7 @@ __global__ void __launch_bounds__(256) x3_stem_kernel(X3StemParams p) {
       *reinterpret_cast<v2u*>(&Il[e * 4]) = v2u{l0, l1};
     }
   }
-  // wave = (channel half nh) x (conv-row group mg: rows 0-4 / 5-8)
+  // wave = (channel half nh) x (conv-row group mg)
   const int nh = wave & 1, mg = wave >> 1;
   v4u wh[kSK / 16], wl[kSK / 16];
   const size_t wrow = (size_t)(nh * 32 + (lane & 31)) * kSK + 8 * (lane >> 5);
@@ -975,8 +976,7 @@ __global__ void __launch_bounds__(256) x3_stem_kernel(X3StemParams p) {
   }
   __syncthreads();
   const int jj = lane & 31, hh = lane >> 5;
-  const int r_lo = mg ? 5 : 0, r_hi = mg ? kSCR : 5;
-  for (int cr = r_lo; cr < r_hi; ++cr) {
+  auto conv_row = [&](int cr) {
     f32x16 acc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
@@ -986,6 +986,68 @@ __global__ void __launch_bounds__(256) x3_stem_kernel(X3StemParams p) {
       const int off = ((2 * cr + kh) * kSIC + 2 * jj + 2 * q) * 4;
       acc = x3_32(wh[s], wl[s], ld16(&Ih[off]), ld16(&Il[off]), acc);
     }
+    return acc;
+  };
+  if constexpr (V2) {
+    // v2: no conv tile in LDS (26 KB per block: several blocks per CU, so
+    // one block's staging overlaps another's MFMAs).  Waves mg = 0/1 own conv
+    // rows 0-4 / 4-8 (row 4 twice: 5 rows each, as the old 5/4 split's
+    // critical path) = pooled rows 2mg, 2mg+1; the 3-wide column max runs
+    // across lanes (shuffles within each 32-lane half), the 3-tall row max
+    // in registers.  C layout: lane col jj = conv col, reg 4g+e -> channel
+    // 8g + 4h + e of this wave's 32.
+    const float ninf = -3.0e38f;
+    f32x16 pm[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) pm[i][e] = ninf;
+    const bool left_pad = pc0 == 0 && jj == 0;  // conv col -1
+#pragma unroll 1
+    for (int r = 0; r < 5; ++r) {
+      const int cr = 4 * mg + r;
+      f32x16 acc = conv_row(cr);
+      if (left_pad) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = ninf;
+      }
+      // column max over conv cols jj, jj+1, jj+2 (read by even lanes jj = 2b)
+      f32x16 cm;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const float a1 = __shfl_down(acc[e], 1, 32), a2 = __shfl_down(acc[e], 2, 32);
+        cm[e] = fmaxf(acc[e], fmaxf(a1, a2));
+      }
+      if (pr0 == 0 && cr == 0) continue;  // conv row -1 (top padding)
+      if (r <= 2) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) pm[0][e] = fmaxf(pm[0][e], cm[e]);
+      }
+      if (r >= 2) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) pm[1][e] = fmaxf(pm[1][e], cm[e]);
+      }
+    }
+    if ((jj & 1) == 0 && jj < 2 * kSPC) {
+      const int pc = pc0 + (jj >> 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int pr = pr0 + 2 * mg + i;
+        float* o = p.y + (((size_t)img * kSHo + pr) * kSHo + pc) * p.ldy + nh * 32 + 4 * hh;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 bb = ldf4(p.bias + nh * 32 + 8 * g + 4 * hh);
+          *reinterpret_cast<f32x4*>(o + 8 * g) =
+              f32x4{fmaxf(pm[i][4 * g] + bb[0], 0.f), fmaxf(pm[i][4 * g + 1] + bb[1], 0.f),
+                    fmaxf(pm[i][4 * g + 2] + bb[2], 0.f), fmaxf(pm[i][4 * g + 3] + bb[3], 0.f)};
+        }
+      }
+    }
+    return;
+  }
+  const int r_lo = mg ? 5 : 0, r_hi = mg ? kSCR : 5;
+  for (int cr = r_lo; cr < r_hi; ++cr) {
+    const f32x16 acc = conv_row(cr);
     float* cp = &Cv[(cr * kSCC + jj) * kSOS + nh * 32 + 4 * hh];
 #pragma unroll
     for (int g = 0; g < 4; ++g)
@@ -1269,7 +1331,11 @@ int tcamd_x3_stem(const void* srcs, const void* w_hi, const void* w_lo, const fl
   p.bias = bias;
   p.y = y;
   p.ldy = ldy;
-  hipLaunchKernelGGL(x3_stem_kernel, dim3(kSHo / kSPC, kSHo / kSPR, imgs), dim3(256), 0, (hipStream_t)stream, p);
+  // v2 (pool in registers, 26 KB LDS) unless TCAMD_X3_STEM=1 (A/B runs)
+  static const int stem_v = getenv("TCAMD_X3_STEM") ? atoi(getenv("TCAMD_X3_STEM")) : 2;
+  const dim3 g(kSHo / kSPC, kSHo / kSPR, imgs);
+  if (stem_v == 1) hipLaunchKernelGGL(x3_stem_kernel<false>, g, dim3(256), 0, (hipStream_t)stream, p);
+  else hipLaunchKernelGGL(x3_stem_kernel<true>, g, dim3(256), 0, (hipStream_t)stream, p);
   return hipGetLastError();
 }
 
