@@ -513,13 +513,23 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
         ah[kk][b] = ld16(st + 2 * kWsPlane + wo);
         al[kk][b] = ld16(st + 3 * kWsPlane + wo);
       }
+    // pixel blocks wholly past the block's last row (the ragged last tile)
+    // skip their MFMAs
+    const int mb = mbeg + tile * 128 + 64 * wm;
     if (!(wp.dbg & 1)) {
+      if (mb + 32 < mend) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+        for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+          for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = x3_32(ah[kk][a], al[kk][a], bh[kk][b], bl[kk][b], acc[a][b]);
+            for (int b = 0; b < 2; ++b) acc[a][b] = x3_32(ah[kk][a], al[kk][a], bh[kk][b], bl[kk][b], acc[a][b]);
+      } else if (mb < mend) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int a = 0; a < 2; ++a) acc[a][0] = x3_32(ah[kk][a], al[kk][a], bh[kk][0], bl[kk][0], acc[a][0]);
+      }
     } else {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
@@ -1221,7 +1231,9 @@ int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, int N, const float* 
   // warp-specialised persistent kernel for the big dense-layer 1x1s
   // (TCAMD_X3_WS=0 turns it off for A/B runs)
   static const int ws_mode = getenv("TCAMD_X3_WS") ? atoi(getenv("TCAMD_X3_WS")) : 1;
-  if (ws_mode && !pool && split_out && N == kBN && M >= 65536) {
+  // (M floor: TCAMD_X3_WS_MIN, A/B runs)
+  static const int ws_min = getenv("TCAMD_X3_WS_MIN") ? atoi(getenv("TCAMD_X3_WS_MIN")) : 16384;
+  if (ws_mode && !pool && split_out && N == kBN && M >= ws_min) {
     static int ncu = 0;
     if (!ncu) {
       int dev = 0;

@@ -63,7 +63,7 @@ def test_split_is_exact_to_2e17():
                                      (65555, 32, 32), (100352, 480, 512), (70001, 1024, 1024)])
 def test_x3_conv1x1_split_out(M, K, ldx):
     """Dense-layer 1x1: z = relu(relu(x*s+t) @ W^T + b) as hi/lo planes
-    (M >= 65536: the warp-specialised persistent kernel, incl. ragged block
+    (M >= 16384: the warp-specialised persistent kernel, incl. ragged block
     ranges and a single K step; mid M: whole-K tiles; small M: split-K
     workspace + reduce)."""
     _need_gpu()
