@@ -31,6 +31,16 @@ reduced-precision operating point.
 
 ``--cpu`` runs the same pipeline with no GPU (CPU ``frontend_sink`` model,
 system shm, gloo): the multi-rank CPU test of the launch/aggregation path.
+
+``--model bert_large`` is BASELINE.json's concurrency-sweep config instead
+(bert-large seq 384, HIP shm fanned out over RCCL): the three INT32 input
+regions are filled on rank 0 (K1: random token ids, all-ones mask, zero
+segment ids) and broadcast to every rank, then each rank sweeps
+``--sweep`` concurrencies against its own server; per point ``--steps``
+windows of max(64, 8 x concurrency) requests, aggregated over ranks.  The
+JSON ``value`` is the aggregate infer/s at the highest concurrency; every
+point is listed under ``sweep``.  (``--cpu`` covers it on the CPU with the
+``bert_sink`` shape model.)
 """
 
 import argparse
@@ -44,6 +54,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "perf_analyzer inferences/sec + p99 latency, densenet_onnx bs=1/8 via HIP shm"
+BERT_METRIC = "perf_analyzer concurrency sweep 1-256 inferences/sec + p99 latency, bert_large seq384 via HIP shm"
 
 
 def log(*a):
@@ -70,6 +81,10 @@ def parse_args(argv=None):
     ap.add_argument("--idle-dispatch", default="off", choices=["on", "off"])
     ap.add_argument("--cpu", action="store_true", help="no GPU: CPU frontend_sink model, system shm, gloo")
     ap.add_argument("--server-log", default="")
+    ap.add_argument("--model", default="densenet_onnx", choices=["densenet_onnx", "bert_large"])
+    ap.add_argument("--sweep", default="1,4,16,64,256", help="bert_large: concurrencies per GPU")
+    ap.add_argument("--bert-instance-count", type=int, default=3)
+    ap.add_argument("--bert-queue-delay-us", type=int, default=500)
     return ap.parse_args(argv)
 
 
@@ -88,15 +103,16 @@ def spawn_ranks(args):
 class Point:
     """One load point of the native engine against one server."""
 
-    def __init__(self, srv, model, bs, conc, region, nbytes, device, cpu):
+    def __init__(self, srv, model, bs, conc, region, nbytes, device, cpu, inputs=None, out_bytes=None):
         from triton_client_amd.perf.native import PerfSession
 
         self.bs, self.conc = bs, conc
-        out_bytes = bs * 1000 * 4
+        out_bytes = out_bytes or bs * 1000 * 4
         args = ["-m", model, "-i", "grpc", "-u", srv.grpc_url, "-b", bs,
                 "--shared-memory", "system" if cpu else "hip", "--device", device,
-                "--shared-memory-input", "data_0=%s" % region, "--output-shared-memory-size", out_bytes,
-                "--concurrency-range", conc]
+                "--output-shared-memory-size", out_bytes, "--concurrency-range", conc]
+        for name, reg in (inputs or {"data_0": region}).items():
+            args += ["--shared-memory-input", "%s=%s" % (name, reg)]
         self.s = PerfSession(args)
 
     def run(self, n):
@@ -150,15 +166,23 @@ def main():
     from triton_client_amd.perf.loadgen import percentile_us
 
     cpu = args.cpu
-    model = "frontend_sink" if cpu else "densenet_onnx"
+    bert = args.model == "bert_large"
+    if bert:
+        model = "bert_sink" if cpu else "bert_large"
+    else:
+        model = "frontend_sink" if cpu else "densenet_onnx"
     bs, conc = args.batch, args.concurrency
     log_dir = os.path.join(REPO, "gpurun_out")
     os.makedirs(log_dir, exist_ok=True)
 
     def start_server(engine, tag):
-        extra = ["--instance-count", str(args.instance_count), "--max-queue-delay-us", str(args.max_queue_delay_us),
-                 "--idle-dispatch", args.idle_dispatch]
-        if not cpu:
+        if bert:
+            extra = ["--instance-count", str(args.bert_instance_count), "--max-queue-delay-us",
+                     str(args.bert_queue_delay_us)]
+        else:
+            extra = ["--instance-count", str(args.instance_count), "--max-queue-delay-us",
+                     str(args.max_queue_delay_us), "--idle-dispatch", args.idle_dispatch]
+        if not cpu and not bert:
             extra += ["--engine", engine]
             if args.preferred:
                 extra += ["--preferred-batch-sizes", args.preferred]
@@ -169,7 +193,7 @@ def main():
         return ServerProcess(device=local_rank, gpu=not cpu, models=model, extra_args=extra, log_path=path,
                              port_stripe=local_rank if world > 1 else None), path
 
-    srv, srv_log = start_server(args.engine, args.engine)
+    srv, srv_log = start_server(args.engine, "bert" if bert else args.engine)
 
     import torch
     import torch.distributed as dist
@@ -240,6 +264,9 @@ def main():
         log("server ready")
         client = grpcclient.InferenceServerClient(srv.grpc_url)
         state["client"] = client
+        if bert:
+            return bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout, rank, world,
+                              local_rank, cpu)
         method, in_bytes = make_input("data_0_in", bs)
         if not cpu:
             _sanity_check(client, shmod, bs, local_rank, regions)
@@ -378,6 +405,85 @@ def main():
         srv.stop()
         if world > 1 and dist.is_initialized():
             dist.destroy_process_group()
+
+
+BERT_SEQ = 384
+
+
+def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout, rank, world, local_rank, cpu):
+    """Config 4: bert_large seq-384 concurrency sweep, inputs fanned out by RCCL."""
+    import numpy as np
+
+    from triton_client_amd.perf.loadgen import percentile_us
+
+    nbytes = BERT_SEQ * 4  # one request (bs 1) per region
+    specs = (("input_ids", "random", 0.0, 30521.0), ("attention_mask", "constant", 1.0, 1.0),
+             ("token_type_ids", "zero", 0.0, 0.0))
+    inputs, method = {}, "local"
+    for name, mode, lo, hi in specs:
+        reg = "bert_%s" % name
+        if cpu:
+            key = "/%s_r%d_%d" % (reg, rank, os.getpid())
+            r = shmod.create_shared_memory_region(reg, key, nbytes)
+            regions.append(r)
+            if mode == "random":
+                data = np.random.default_rng(1234).integers(0, int(hi) + 1, BERT_SEQ, dtype=np.int32)
+            else:
+                data = np.full(BERT_SEQ, int(lo), np.int32)
+            host = data if rank == 0 else np.zeros(BERT_SEQ, np.int32)
+            method = fanout.fanout_host(host.view(np.uint8))
+            shmod.set_shared_memory_region(r, [host])
+            if not fanout.verify_host_replicas(host.view(np.uint8)):
+                raise RuntimeError("fan-out replicas differ across ranks")
+            client.register_system_shared_memory(reg, key, nbytes)
+        else:
+            r = shmod.create_shared_memory_region(reg, nbytes, local_rank)
+            regions.append(r)
+            method = fanout.fill_and_fanout(r, "INT32", BERT_SEQ, seed=1234, mode=mode, lo=lo, hi=hi,
+                                            method=args.fanout)
+            if not fanout.verify_replicas(r, nbytes):
+                raise RuntimeError("fan-out replicas differ across ranks")
+            client.register_cuda_shared_memory(reg, shmod.get_raw_handle(r), local_rank, nbytes)
+        inputs[name] = reg
+    sweep = []
+    for c in [int(v) for v in args.sweep.split(",") if v]:
+        pt = Point(srv, model, 1, c, None, nbytes, local_rank, cpu, inputs=inputs, out_bytes=BERT_SEQ * 4)
+        points.append(pt)
+        per = max(64, 8 * c)
+        pt.run(max(args.warmup, 1) * per)
+        lat, _, elapsed = measure(pt, args.steps, per)
+        all_lat = fanout.gather_arrays(lat.astype(np.int64)).astype(np.float64)
+        row = {"concurrency": c, "infer_per_sec": round(world * args.steps * per / elapsed, 1),
+               "p50_latency_us": round(percentile_us(all_lat, 50), 1),
+               "p99_latency_us": round(percentile_us(all_lat, 99), 1), "ms_per_step": round(1e3 * elapsed / args.steps, 3)}
+        sweep.append(row)
+        log("bert c%d: %.1f infer/s p99 %.0f us" % (c, row["infer_per_sec"], row["p99_latency_us"]))
+    top = sweep[-1]
+    res = {
+        "metric": BERT_METRIC,
+        "value": top["infer_per_sec"],
+        "unit": "infer/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": top["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32" if cpu else "bf16",
+        "data": ("synthetic INT32 (host, fanned out by %s), CPU %s" % (method, model) if cpu else
+                 "synthetic INT32 token ids / all-ones mask / zero segments (K1 on device, fanned out by %s), "
+                 "random-init weights" % method),
+        "config": {"model": model, "global_batch": world * top["concurrency"], "seq_len": BERT_SEQ,
+                   "parallelism": "dp%d" % world, "batch_size": 1, "protocol": "grpc",
+                   "shared_memory": "system" if cpu else "hip", "loadgen": "native C++ (csrc/cpp/perf)",
+                   "server_instances": args.bert_instance_count, "max_queue_delay_us": args.bert_queue_delay_us},
+        "p99_latency_us": top["p99_latency_us"],
+        "sweep": sweep,
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    return 0
 
 
 def _sanity_check(client, hipshm, bs, dev, regions):

@@ -53,3 +53,17 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--cpu", "--gpus", "2"],
                        capture_output=True, text=True, timeout=60, cwd=REPO, env=env)
     assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_bench_bert_sweep_two_ranks():
+    """Config 4's path (bench.py --model bert_large): three INT32 input regions
+    fanned out from rank 0, a concurrency sweep per rank, one aggregated JSON
+    line with every point (CPU: the bert_sink shape model)."""
+    res, err = _bench("--gpus", "2", "--steps", "3", "--model", "bert_large", "--sweep", "1,4")
+    assert res["n_gpus"] == 2 and res["config"]["model"] == "bert_sink"
+    assert res["config"]["seq_len"] == 384 and res["config"]["parallelism"] == "dp2"
+    assert [p["concurrency"] for p in res["sweep"]] == [1, 4]
+    assert all(p["infer_per_sec"] > 0 and p["p99_latency_us"] >= p["p50_latency_us"] > 0 for p in res["sweep"])
+    assert res["value"] == res["sweep"][-1]["infer_per_sec"]
+    assert "fanned out by gloo" in res["data"]
+    assert "bert c4" in err

@@ -347,8 +347,52 @@ class FrontendSink(Model):
         b.timing_ns[0] = b.timing_ns[1] = b.timing_ns[2] = 0
 
 
+class BertSink(Model):
+    """bert_large-shaped model that does no compute: INT32 [384] input_ids /
+    attention_mask / token_type_ids in, FP32 [384] start/end logits out (the
+    mask as float).  The CPU stand-in of bench.py's bert_large sweep, so the
+    multi-rank launch + fan-out + sweep aggregation path runs without a GPU."""
+
+    name = "bert_sink"
+    max_batch_size = 64
+    SEQ = 384
+    inputs = (TensorSpec("input_ids", "INT32", [384]), TensorSpec("attention_mask", "INT32", [384]),
+              TensorSpec("token_type_ids", "INT32", [384]))
+    outputs = (TensorSpec("start_logits", "FP32", [384]), TensorSpec("end_logits", "FP32", [384]))
+    dynamic_batching = {"preferred": [], "max_queue_delay_us": 100}
+    instance_count = 2
+    supports_native = True
+
+    def execute(self, requests):
+        out = []
+        for r in requests:
+            m = r.input("attention_mask").numpy().astype(np.float32)
+            out.append([self.out("start_logits", m), self.out("end_logits", -m)])
+        return out
+
+    def execute_native(self, instance, b):
+        import ctypes
+
+        n = self.SEQ
+        for r in range(b.n_requests):
+            rows = b.rows[r]
+            src = b.inputs[r * 3 + 1]
+            if src.kind != 0:
+                raise ServerError("bert_sink runs on host memory only")
+            m = np.ctypeslib.as_array((ctypes.c_int32 * (rows * n)).from_address(src.ptr)).astype(np.float32)
+            for k, sign in ((0, 1.0), (1, -1.0)):
+                dst = b.outputs[r * 2 + k]
+                if not dst.ptr:
+                    continue
+                if dst.kind != 0:
+                    raise ServerError("bert_sink runs on host memory only")
+                np.ctypeslib.as_array((ctypes.c_float * (rows * n)).from_address(dst.ptr))[:] = sign * m
+        b.timing_ns[0] = b.timing_ns[1] = b.timing_ns[2] = 0
+
+
 CPU_MODELS = [
     FrontendSink,
+    BertSink,
     SimpleAddSub,
     OnnxInt32,
     SimpleString,
