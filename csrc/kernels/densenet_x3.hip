@@ -368,8 +368,9 @@ __device__ __forceinline__ void ws_barrier() {
 __device__ __forceinline__ int ws_chunk(int row, int c) { return row * 64 + ((c ^ ((row >> 2) & 3)) << 4); }
 
 // kWsPF: X steps in flight in the producers' registers
-template <int kWsPF>
+template <int kWsPF, int DBG>
 __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
+  const int dbg = DBG < 0 ? wp.dbg : DBG;  // ablation flags (DBG -1 only)
   extern __shared__ __attribute__((aligned(16))) uint8_t ldsw[];
   const X3Conv1x1Params& p = wp.c;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -395,7 +396,7 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
     // K steps of a tile run in a block-rotated order: at any moment the blocks
     // then read different column offsets of their X rows (all blocks on the
     // same offset would camp on a subset of the HBM channels)
-    const int rot = (wp.dbg & 4) ? 0 : (int)(blockIdx.x % (unsigned)nst);
+    const int rot = (dbg & 4) ? 0 : (int)(blockIdx.x % (unsigned)nst);
     auto kofs = [&](int ks) { ks += rot; return (ks >= nst ? ks - nst : ks) * kBK; };
     auto issue_x = [&](int q, int slot) {
       q = min(q, Q - 1);
@@ -516,7 +517,7 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
     // pixel blocks wholly past the block's last row (the ragged last tile)
     // skip their MFMAs
     const int mb = mbeg + tile * 128 + 64 * wm;
-    if (!(wp.dbg & 1)) {
+    if (!(dbg & 1)) {
       if (mb + 32 < mend) {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
@@ -536,7 +537,7 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
 #pragma unroll
         for (int a = 0; a < 2; ++a) acc[a][0][0] += __builtin_bit_cast(float, ah[kk][a][0] ^ al[kk][a][1] ^ bh[kk][a][2] ^ bl[kk][a][3]);
     }
-    if (ks == nst - 1 && !(wp.dbg & 2)) {
+    if (ks == nst - 1 && !(dbg & 2)) {
       // epilogue through this wave's 8 KB LDS slab: per 32-pixel block, the
       // bias+ReLU+split 64-channel rows land as [32 px][64 ch] hi and lo
       // (16-B chunks XOR-swizzled by pixel), then leave as 16-B-per-lane
@@ -606,6 +607,7 @@ struct X3Conv3x3Params {
   float* y;              // [M][ldy] fp32, offset to the layer's 32-channel slice
   int ldy, M, H, W;
   int tiles, tiles_per_block;
+  int dbg;  // v2 ablation (TCAMD_X3_K9_DBG): 1 no MFMA, 2 no partial exchange, 4 no operand reads
   uint32_t mag_hw, mag_w;  // ceil(2^32 / (H*W)), ceil(2^32 / W): division by multiply-high
 };
 
@@ -803,7 +805,10 @@ constexpr int kRowB = 2 * kC3 * 2;          // 512 B per ring row
 constexpr int kScrSlot = 32 * 8;            // floats per (group, ph, source) slot: 32 px x 8 channels
 constexpr int kLdsV2 = (kRing + 1) * kRowB + 4 * 2 * 3 * kScrSlot * 4;  // 131,584 + 24,576 B
 
+// DBG: 0 = production; -1 = ablation flags read from p.dbg (tools/gpu_x3_k9abl.sh)
+template <int DBG>
 __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p) {
+  const int dbg = DBG < 0 ? p.dbg : DBG;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds2[];
   float* scr = reinterpret_cast<float*>(lds2 + (kRing + 1) * kRowB);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -875,6 +880,11 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p
       const int row = ok ? ((base + dy * W + dx) & (kRing - 1)) : kRing;
       const uint8_t* rp = lds2 + row * kRowB;
       const int sw = row & 15;
+      if (dbg & 4) {
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc) bq[slot][kc][0] = bq[slot][kc][1] = v4u{(uint32_t)row, 0u, 1u, 2u};
+        return;
+      }
 #pragma unroll
       for (int kc = 0; kc < 2; ++kc) {
         const uint8_t* q = rp + (((4 * kq + 2 * kc + h) ^ sw) << 4);
@@ -890,8 +900,17 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p
       // registers), and each read's LDS latency hides behind a tap of MFMAs
       if (t + 1 < kTaps) rd(t + 1, (t + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);
+      if (dbg & 1) {
 #pragma unroll
-      for (int kc = 0; kc < 2; ++kc) acc = x3_32(wh[t][kc], wl[t][kc], bq[t & 1][kc][0], bq[t & 1][kc][1], acc);
+        for (int kc = 0; kc < 2; ++kc) acc[kc] += __builtin_bit_cast(float, bq[t & 1][kc][0][0] ^ bq[t & 1][kc][1][1]);
+      } else {
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc) acc = x3_32(wh[t][kc], wl[t][kc], bq[t & 1][kc][0], bq[t & 1][kc][1], acc);
+      }
+    }
+    if (dbg & 2) {
+      if (in) *reinterpret_cast<f32x4*>(p.y + (size_t)m * p.ldy + 8 * kq + 4 * h) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+      continue;
     }
     // C layout (32x32): lane col = pixel, reg 4g+e -> channel 8g + 4h + e.
     // scratch slot (group g, ph, source kq != g) at index (g*2 + ph)*3 + (kq - g + 3) % 4
@@ -1145,7 +1164,11 @@ X3Plan x3_plan(int M, int K, int N) {
   pl.tiles = ((M + pl.bm - 1) / pl.bm) * nt;
   pl.splits = 1;
   pl.k_per_split = K;
-  if (pl.tiles < 192 && K >= 4 * kBK) {
+  static const int splitk_below = [] {  // A/B knob: split-K when fewer tiles than this
+    const char* e = getenv("TCAMD_X3_SPLITK_BELOW");
+    return e ? atoi(e) : 192;
+  }();
+  if (pl.tiles < splitk_below && K >= 4 * kBK) {
     const int steps = K / kBK;
     int want = std::min(steps / 2, (384 + pl.tiles - 1) / pl.tiles);
     if (want > 1) {
@@ -1239,10 +1262,9 @@ int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, int N, const float* 
       int dev = 0;
       hipError_t e = hipGetDevice(&dev);
       if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-      if (e == hipSuccess) e = hipFuncSetAttribute((const void*)x3_conv1x1_ws_kernel<3>,
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, kLdsWs);
-      if (e == hipSuccess) e = hipFuncSetAttribute((const void*)x3_conv1x1_ws_kernel<5>,
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, kLdsWs);
+      for (const void* f : {(const void*)x3_conv1x1_ws_kernel<3, 0>, (const void*)x3_conv1x1_ws_kernel<5, 0>,
+                            (const void*)x3_conv1x1_ws_kernel<3, -1>})
+        if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsWs);
       if (e != hipSuccess) return e;
     }
     X3WsParams wp;
@@ -1253,8 +1275,9 @@ int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, int N, const float* 
     wp.units_per_block = (units + ncu - 1) / ncu;
     const int blocks = (units + wp.units_per_block - 1) / wp.units_per_block;
     static const int ws_pf = getenv("TCAMD_X3_WS_PF") ? atoi(getenv("TCAMD_X3_WS_PF")) : 3;
-    if (ws_pf == 5) hipLaunchKernelGGL(x3_conv1x1_ws_kernel<5>, dim3(blocks), dim3(512), kLdsWs, s, wp);
-    else hipLaunchKernelGGL(x3_conv1x1_ws_kernel<3>, dim3(blocks), dim3(512), kLdsWs, s, wp);
+    if (wp.dbg) hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, -1>), dim3(blocks), dim3(512), kLdsWs, s, wp);
+    else if (ws_pf == 5) hipLaunchKernelGGL((x3_conv1x1_ws_kernel<5, 0>), dim3(blocks), dim3(512), kLdsWs, s, wp);
+    else hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, 0>), dim3(blocks), dim3(512), kLdsWs, s, wp);
     return hipGetLastError();
   }
   const dim3 g((M + pl.bm - 1) / pl.bm, pl.splits, N / kBN);
@@ -1308,17 +1331,23 @@ int tcamd_x3_conv3x3(const void* z_hi, const void* z_lo, int imgs, int H, int W,
     hipError_t e =
         hipFuncSetAttribute((const void*)x3_conv3x3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kLds3);
     if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+      e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kLdsV2);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<-1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               kLdsV2);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
+  static const int k9dbg = getenv("TCAMD_X3_K9_DBG") ? atoi(getenv("TCAMD_X3_K9_DBG")) : 0;
+  p.dbg = k9dbg;
   if (!v1) {
     p.tiles = (p.M + kT2 - 1) / kT2;
     const int grid = std::min(p.tiles, 256);
     p.tiles_per_block = (p.tiles + grid - 1) / grid;
     const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
-    hipLaunchKernelGGL(x3_conv3x3_v2_kernel, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
+    if (p.dbg) hipLaunchKernelGGL(x3_conv3x3_v2_kernel<-1>, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
+    else hipLaunchKernelGGL(x3_conv3x3_v2_kernel<0>, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
     return hipGetLastError();
   }
   const int grid = std::min(p.tiles, 256);
