@@ -349,6 +349,7 @@ constexpr int kLdsWs = kWsS * kWsStage + 4 * 8192;  // 128 KB stages + 4 x 8 KB 
 struct X3WsParams {
   X3Conv1x1Params c;
   int units_per_block;  // 16-pixel units per block
+  int tile_rows;        // rows per tile (<= 128): a block's run split into equal tiles
   int dbg;              // ablation (tools/x3_kbench.py): 1 = no MFMA, 2 = no z stores
 };
 
@@ -379,7 +380,8 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
   const int mend = min(p.M, 16 * (u0 + wp.units_per_block));
   if (mbeg >= mend) return;
   const int nst = p.K / kBK;
-  const int ntiles = (mend - mbeg + 127) / 128;
+  const int TR = wp.tile_rows;
+  const int ntiles = (mend - mbeg + TR - 1) / TR;
   const int Q = ntiles * nst;  // K steps of this block
   const int Qp = (Q + kWsPF - 1) / kWsPF * kWsPF;  // both roles run Qp barrier rounds
 
@@ -405,7 +407,8 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
       xt[slot] = ldf4(p.in_bias + k0 + 4 * pj);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int m = min(mbeg + tile * 128 + prow + 32 * i, mend - 1);
+        const int tb = mbeg + tile * TR;
+        const int m = min(tb + prow + 32 * i, min(mend, tb + TR) - 1);
         xr[slot][i] = ldf4(p.x + (size_t)m * p.ldx + k0 + 4 * pj);
       }
     };
@@ -430,7 +433,7 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = prow + 32 * i;
-        const bool ok = mbeg + tile * 128 + row < mend;
+        const bool ok = row < TR && mbeg + tile * TR + row < mend;
         f32x4 v;
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = ok ? fmaxf(xr[slot][i][e] * sc[e] + sb[e], 0.f) : 0.f;
@@ -516,16 +519,16 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
       }
     // pixel blocks wholly past the block's last row (the ragged last tile)
     // skip their MFMAs
-    const int mb = mbeg + tile * 128 + 64 * wm;
+    const int rv = min(TR, mend - (mbeg + tile * TR)) - 64 * wm;  // valid rows from this wave's first
     if (!(dbg & 1)) {
-      if (mb + 32 < mend) {
+      if (rv > 32) {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
           for (int a = 0; a < 2; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b) acc[a][b] = x3_32(ah[kk][a], al[kk][a], bh[kk][b], bl[kk][b], acc[a][b]);
-      } else if (mb < mend) {
+      } else if (rv > 0) {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -565,8 +568,8 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
           const int px = 8 * pass + (lane >> 3), c = lane & 7;
           const int off = px * 128 + ((c ^ (px & 7)) << 4);
           const v4u vh = ld16(slab + off), vl = ld16(slab + 4096 + off);
-          const int m = mbeg + tile * 128 + 64 * wm + 32 * b + px;
-          if (m < mend) {
+          const int m = mbeg + tile * TR + 64 * wm + 32 * b + px;
+          if (32 * b + px < rv) {
             *reinterpret_cast<v4u*>(p.z_hi + (size_t)m * kBN + 64 * wn + 8 * c) = vh;
             *reinterpret_cast<v4u*>(p.z_lo + (size_t)m * kBN + 64 * wn + 8 * c) = vl;
           }
@@ -1273,6 +1276,11 @@ int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, int N, const float* 
     wp.dbg = dbg;
     const int units = (M + 15) / 16;
     wp.units_per_block = (units + ncu - 1) / ncu;
+    // equal tiles: 392 rows -> 4 x 98 instead of 3 x 128 + 8 (every tile
+    // costs nst barrier rounds whatever its row count)
+    const int rpb = 16 * wp.units_per_block;
+    const int nt = (rpb + 127) / 128;
+    wp.tile_rows = (rpb + nt - 1) / nt;
     const int blocks = (units + wp.units_per_block - 1) / wp.units_per_block;
     static const int ws_pf = getenv("TCAMD_X3_WS_PF") ? atoi(getenv("TCAMD_X3_WS_PF")) : 3;
     if (wp.dbg) hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, -1>), dim3(blocks), dim3(512), kLdsWs, s, wp);
