@@ -83,6 +83,168 @@ __global__ void __launch_bounds__(256) add_layernorm_kernel(const uint16_t* x, c
 
 }  // namespace
 
+
+namespace {
+// ============================================================================
+// K12 — fused multi-head attention for bert_large (non-causal, head dim 64,
+// additive key-padding mask), straight from the fused QKV GEMM's output.
+// ============================================================================
+// torch-ROCm's SDPA with a key-padding bias costs 216 us per layer at bs64 x
+// seq384 (120 us unmasked) plus a transpose copy of its output; here one block
+// owns one (sequence, head):
+//   * K [S][64] and V^T [64][S] (bf16) of the head go to LDS once (96 KB at
+//     S = 384): K rows 128 B with 16-B chunks XOR-swizzled by (row >> 1) & 7
+//     (conflict-free b128 reads by 16 consecutive keys), V transposed while it
+//     is staged (pairs of keys -> 32-bit writes), rows padded to S + 4 so the
+//     dim-major b64 reads of 32 lanes hit 32 distinct bank pairs;
+//   * wave w owns queries [32w, 32w + 32) (S/32 waves, 3 per SIMD at S = 384):
+//     its Q^T fragments stay in registers; per 64-key chunk S^T = K Q^T on
+//     v_mfma_f32_32x32x16_bf16 (8 MFMAs), an online softmax in the exp2
+//     domain (per-lane partial row sums, one cross-half max shuffle per
+//     chunk), then O^T += V^T P^T (8 MFMAs) with P^T taken straight from the
+//     S^T accumulators: the MFMA k index is permuted so a lane's 8 keys are
+//     exactly the 8 scores it already holds, and V^T is read in that order;
+//   * O / l leaves as bf16 in [tokens][heads * 64] — the layout the output
+//     projection GEMM reads, so no transpose kernel follows.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
+constexpr int kAD = 64;           // head dim
+constexpr int kAMaxS = 384;       // keys / queries per sequence (multiple of 64)
+
+__device__ __forceinline__ bf16x8 as_bf8(v4u v) { return __builtin_bit_cast(bf16x8, v); }
+
+__global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __restrict__ qkv, const int* __restrict__ mask,
+                                                           uint16_t* __restrict__ out, int S, int heads, float scale) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_a[];
+  const int ldv = S + 4;  // V^T row (elements)
+  uint16_t* Ks = reinterpret_cast<uint16_t*>(lds_a);
+  uint16_t* Vt = Ks + S * kAD;
+  float* kb = reinterpret_cast<float*>(Vt + kAD * ldv);  // per-key log2-domain bias
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nthr = blockDim.x;
+  const int seq = blockIdx.x / heads, head = blockIdx.x % heads;
+  const int HD = heads * kAD, ld = 3 * HD;
+  const uint16_t* base = qkv + (size_t)seq * S * ld + head * kAD;
+  constexpr float kLog2e = 1.4426950408889634f;
+
+  // ---- stage K (swizzled rows) and V^T ----
+  for (int e = tid; e < S * 8; e += nthr) {
+    const int key = e >> 3, c = e & 7;
+    const v4u v = *reinterpret_cast<const v4u*>(base + (size_t)key * ld + HD + 8 * c);
+    *reinterpret_cast<v4u*>(Ks + key * kAD + 8 * (c ^ ((key >> 1) & 7))) = v;
+  }
+  for (int e = tid; e < (S / 2) * 8; e += nthr) {
+    const int kp = e >> 3, c = e & 7, key = 2 * kp;
+    const v4u a = *reinterpret_cast<const v4u*>(base + (size_t)key * ld + 2 * HD + 8 * c);
+    const v4u b = *reinterpret_cast<const v4u*>(base + (size_t)(key + 1) * ld + 2 * HD + 8 * c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t lo = (a[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+      const uint32_t hi = (b[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+      *reinterpret_cast<uint32_t*>(Vt + (8 * c + j) * ldv + key) = lo | (hi << 16);
+    }
+  }
+  for (int k = tid; k < S; k += nthr)
+    kb[k] = (mask && mask[(size_t)seq * S + k] == 0) ? -10000.0f * kLog2e : 0.0f;
+
+  // ---- this wave's queries: Q^T fragments (B operand: lane col = query) ----
+  const int col = lane & 31, h = lane >> 5;
+  const int q = 32 * wave + col;
+  v4u qf[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) qf[kk] = *reinterpret_cast<const v4u*>(base + (size_t)q * ld + 16 * kk + 8 * h);
+  __syncthreads();
+
+  const float sl2 = scale * kLog2e;
+  float m_run = -1.0e30f, l_part = 0.f;
+  f32x16 o[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[r][e] = 0.f;
+
+  for (int c0 = 0; c0 < S; c0 += 64) {
+    // S^T for keys [c0, c0 + 64): two 32-key row blocks; lane (query, h) holds
+    // keys 32 rb + 8 g + 4 h + e
+    f32x16 st[2];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) st[rb][e] = 0.f;
+      const int key = c0 + 32 * rb + col;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const v4u kf = *reinterpret_cast<const v4u*>(Ks + key * kAD + 8 * ((2 * kk + h) ^ ((key >> 1) & 7)));
+        st[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(kf), as_bf8(qf[kk]), st[rb], 0, 0, 0);
+      }
+    }
+    float mx = -1.0e30f;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(kb + c0 + 32 * rb + 8 * g + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = st[rb][4 * g + e] * sl2 + bb[e];
+          st[rb][4 * g + e] = x;
+          mx = fmaxf(mx, x);
+        }
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    float ls = 0.f;
+    v4u pf[4];  // P^T fragments per 16-key step: keys 16 kk2 + {4h..4h+3, 8+4h..8+4h+3}
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float pv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pv[e] = exp2f(st[rb][4 * g + e] - m_new);
+          ls += pv[e];
+        }
+        const int kk2 = 2 * rb + (g >> 1), half = g & 1;
+        pf[kk2][2 * half] = pack2(pv[0], pv[1]);
+        pf[kk2][2 * half + 1] = pack2(pv[2], pv[3]);
+      }
+    l_part = l_part * alpha + ls;
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) o[r][e] *= alpha;
+    // O^T += V^T P^T: A = V^T rows (dims 32 rd + col), keys in the permuted order
+#pragma unroll
+    for (int kk2 = 0; kk2 < 4; ++kk2)
+#pragma unroll
+      for (int rd = 0; rd < 2; ++rd) {
+        const uint16_t* vr = Vt + (32 * rd + col) * ldv + c0 + 16 * kk2 + 4 * h;
+        const v2u a0 = *reinterpret_cast<const v2u*>(vr);
+        const v2u a1 = *reinterpret_cast<const v2u*>(vr + 8);
+        const v4u af = v4u{a0[0], a0[1], a1[0], a1[1]};
+        o[rd] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(af), as_bf8(pf[kk2]), o[rd], 0, 0, 0);
+      }
+  }
+  const float inv = 1.0f / (l_part + __shfl_xor(l_part, 32, 64));
+  uint16_t* orow = out + ((size_t)seq * S + q) * HD + head * kAD;
+#pragma unroll
+  for (int rd = 0; rd < 2; ++rd)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 32 * rd + 8 * g + 4 * h;
+      *reinterpret_cast<v2u*>(orow + d) =
+          v2u{pack2(o[rd][4 * g] * inv, o[rd][4 * g + 1] * inv), pack2(o[rd][4 * g + 2] * inv, o[rd][4 * g + 3] * inv)};
+    }
+}
+
+}  // namespace
+
 extern "C" {
 
 // out = LayerNorm(x + y) * gamma + beta over rows of H bf16 elements
@@ -106,6 +268,28 @@ int tcamd_add_layernorm(const void* x, const void* y, const void* gamma, const v
     case 4096: hipLaunchKernelGGL(add_layernorm_kernel<64>, grid, block, 0, s, px, py, pg, pb, po, rows, eps); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// K12: multi-head attention over qkv [seqs * S][3 * heads * 64] bf16 (the fused
+// QKV projection's output: q | k | v, each [heads][64]) -> out [seqs * S][heads *
+// 64] bf16.  mask: int32 [seqs][S] key-padding mask (0 = padded) or null.
+// S % 64 == 0 and S <= 384; pointers 16-B aligned.
+int tcamd_attention(const void* qkv, const int* mask, void* out, int seqs, int S, int heads, float scale,
+                    void* stream) {
+  if (seqs <= 0) return hipSuccess;
+  if (S <= 0 || S % 64 || S > kAMaxS || heads <= 0 || ((uintptr_t)qkv | (uintptr_t)out) % 16 || (uintptr_t)mask % 16)
+    return hipErrorInvalidValue;
+  const size_t lds = (size_t)S * kAD * 2 + (size_t)kAD * (S + 4) * 2 + (size_t)S * 4;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e =
+        hipFuncSetAttribute((const void*)attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(attention_kernel, dim3(seqs * heads), dim3(2 * S), lds, (hipStream_t)stream,
+                     (const uint16_t*)qkv, mask, (uint16_t*)out, S, heads, scale);
   return hipGetLastError();
 }
 

@@ -83,3 +83,48 @@ def test_bert_dense_path_matches_masked_when_no_padding():
         b = m(ids, mask, tt, dense=True)
     for x, y in zip(a, b):
         assert ((x - y).norm() / x.norm()).item() < 2e-2
+
+
+def _attn_ref(qkv, mask, seqs, S, heads=16, D=64):
+    x = qkv.float().view(seqs, S, 3, heads, D).permute(2, 0, 3, 1, 4)
+    q, k, v = x[0], x[1], x[2]
+    s = q @ k.transpose(-1, -2) / D ** 0.5
+    if mask is not None:
+        s = s + ((1.0 - mask.float()) * -10000.0)[:, None, None, :]
+    a = torch.softmax(s, dim=-1) @ v
+    return a.transpose(1, 2).reshape(seqs, S, heads * D)
+
+
+@pytest.mark.parametrize("seqs,S,masked", [(1, 64, False), (3, 128, True), (2, 384, True), (5, 192, False),
+                                           (4, 384, False)])
+def test_attention_kernel_matches_fp32(seqs, S, masked):
+    """K12 vs softmax(QK^T/8 + key-padding bias) V in fp32, reading the fused QKV layout."""
+    _need_gpu()
+    from triton_client_amd.ops import hip
+
+    g = torch.Generator(device=DEV).manual_seed(seqs * 1000 + S)
+    qkv = (torch.randn(seqs * S, 3 * 1024, device=DEV, generator=g) * 1.5).bfloat16()
+    mask = None
+    if masked:
+        mask = torch.ones(seqs, S, device=DEV, dtype=torch.int32)
+        for i in range(seqs):
+            mask[i, S - 7 * (i + 1) * (S // 64):] = 0  # padded tails of different lengths
+        mask[0, 5] = 0  # and one hole inside a sequence
+    out = torch.empty(seqs * S, 1024, device=DEV, dtype=torch.bfloat16)
+    hip.attention(qkv.data_ptr(), None if mask is None else mask.data_ptr(), out.data_ptr(), seqs, S, 16, 0.125)
+    torch.cuda.synchronize()
+    ref = _attn_ref(qkv, mask, seqs, S).reshape(seqs * S, 1024)
+    err = (out.float() - ref).norm() / ref.norm()
+    assert err.item() < 1e-2, err.item()
+    assert torch.isfinite(out.float()).all()
+
+
+def test_attention_rejects_unsupported_shapes():
+    _need_gpu()
+    from triton_client_amd.ops import hip
+
+    x = torch.zeros(448, 3 * 1024, device=DEV, dtype=torch.bfloat16)
+    o = torch.zeros(448, 1024, device=DEV, dtype=torch.bfloat16)
+    for S in (100, 448):
+        with pytest.raises(hip.HipError):
+            hip.attention(x.data_ptr(), None, o.data_ptr(), 1, S, 16, 0.125)

@@ -1,5 +1,8 @@
-"""SDPA timing for the bert_large attention shape under different key-padding
-mask encodings (which fused kernel torch-ROCm picks depends on it).
+"""Attention timing for the bert_large shape: torch SDPA under different
+key-padding mask encodings (which fused kernel torch-ROCm picks depends on
+it; the SDPA cases exclude the transpose copy the model needs after them) vs
+K12 (csrc/kernels/bert.hip), which reads the fused QKV layout and writes
+[tokens, hidden] directly.
 
   python tools/attn_probe.py --batch 64
 """
@@ -7,8 +10,13 @@ mask encodings (which fused kernel torch-ROCm picks depends on it).
 import argparse
 import time
 
+import os
+import sys
+
 import torch
 import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def timed(fn, iters=20):
@@ -37,6 +45,15 @@ def main():
         "bool_b11s": lambda: F.scaled_dot_product_attention(q, k, v, attn_mask=keep[:, None, None, :]),
         "additive_bhss": lambda: F.scaled_dot_product_attention(q, k, v, attn_mask=add.expand(b, h, s, s).contiguous()),
     }
+    from triton_client_amd.ops import hip
+
+    qkv = torch.randn(b * s, 3 * h * d, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty(b * s, h * d, device="cuda", dtype=torch.bfloat16)
+    mask = keep.to(torch.int32)
+    st = torch.cuda.current_stream().cuda_stream
+    cases["K12 none"] = lambda: hip.attention(qkv.data_ptr(), None, out.data_ptr(), b, s, h, 0.125, stream=st)
+    cases["K12 masked"] = lambda: hip.attention(qkv.data_ptr(), mask.data_ptr(), out.data_ptr(), b, s, h, 0.125,
+                                                stream=st)
     flops = 4 * b * h * s * s * d
     for name, fn in cases.items():
         us = timed(fn)

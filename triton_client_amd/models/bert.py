@@ -7,9 +7,11 @@ random (seeded, std 0.02 as in BERT's initializer) — there is no checkpoint
 on the box.
 
 Compute layout for MI355X: bf16 everywhere, fused QKV projection (one
-[3H, H] GEMM per layer instead of three), attention through
-``F.scaled_dot_product_attention`` with an additive key-padding mask (the
-fused attention kernels of torch-ROCm), plain GEMMs on hipBLASLt, the GELU
+[3H, H] GEMM per layer instead of three), attention as ONE hand-written HIP
+kernel (K12, csrc/kernels/bert.hip) that reads Q/K/V straight from the QKV
+GEMM's output, applies the key-padding mask and writes the [tokens, hidden]
+layout the output projection reads (torch SDPA is the fallback for sequences
+over 384 or off the GPU), plain GEMMs on hipBLASLt, the GELU
 in the FFN-up GEMM's epilogue (``torch._addmm_activation``) and every
 residual add + LayerNorm as ONE hand-written HIP kernel (K11,
 csrc/kernels/bert.hip).  The serving wrapper captures one HIP graph per
@@ -57,6 +59,23 @@ def _linear_gelu(x, lin):
     return F.gelu(lin(x))
 
 
+def _attention(qkv, b, s, mask_i32, bias):
+    """Multi-head attention over the QKV projection [b, s, 3H]: K12 on the GPU
+    (mask_i32: int32 [b, s] key-padding mask or None), SDPA elsewhere."""
+    if FUSED and qkv.is_cuda and qkv.dtype == torch.bfloat16 and s % 64 == 0 and qkv.is_contiguous():
+        from triton_client_amd.ops import hip
+
+        if s <= hip.ATTENTION_MAX_SEQ:
+            out = torch.empty(b, s, HIDDEN, device=qkv.device, dtype=qkv.dtype)
+            hip.attention(qkv.data_ptr(), None if mask_i32 is None else mask_i32.data_ptr(), out.data_ptr(), b, s,
+                          HEADS, 1.0 / math.sqrt(HIDDEN // HEADS),
+                          stream=torch.cuda.current_stream(qkv.device).cuda_stream)
+            return out
+    q, k, v = qkv.view(b, s, 3, HEADS, HIDDEN // HEADS).permute(2, 0, 3, 1, 4)
+    a = F.scaled_dot_product_attention(q, k, v, attn_mask=bias)
+    return a.transpose(1, 2).reshape(b, s, HIDDEN)
+
+
 class _Layer(nn.Module):
     def __init__(self):
         super().__init__()
@@ -67,11 +86,10 @@ class _Layer(nn.Module):
         self.ffn2 = nn.Linear(FFN, HIDDEN)
         self.ln2 = nn.LayerNorm(HIDDEN, eps=1e-12)
 
-    def forward(self, x, bias):
+    def forward(self, x, bias, mask_i32=None):
         b, s, _ = x.shape
-        q, k, v = self.qkv(x).view(b, s, 3, HEADS, HIDDEN // HEADS).permute(2, 0, 3, 1, 4)
-        a = F.scaled_dot_product_attention(q, k, v, attn_mask=bias)
-        x = _add_ln(x, self.out(a.transpose(1, 2).reshape(b, s, HIDDEN)), self.ln1)
+        a = _attention(self.qkv(x), b, s, mask_i32, bias)
+        x = _add_ln(x, self.out(a), self.ln1)
         return _add_ln(x, self.ffn2(_linear_gelu(x, self.ffn1)), self.ln2)
 
 
@@ -94,8 +112,9 @@ class BertLargeQA(nn.Module):
         x = self.ln(self.word(input_ids) + self.pos(pos)[None] + self.tok_type(token_type_ids))
         # additive key-padding mask [b, 1, 1, s] in the compute dtype
         bias = None if dense else ((1.0 - attention_mask[:, None, None, :].to(x.dtype)) * -10000.0).to(x.dtype)
+        mask_i32 = None if dense else attention_mask.to(torch.int32).contiguous()
         for layer in self.layers:
-            x = layer(x, bias)
+            x = layer(x, bias, mask_i32)
         logits = self.qa(x).float()
         return logits[..., 0], logits[..., 1]
 

@@ -194,6 +194,11 @@ _SIGS = {
          ctypes.c_int, ctypes.c_float, ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "tcamd_attention": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+         ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_pack_bytes_workspace": ([ctypes.c_uint64], ctypes.c_uint64),
     "tcamd_pack_bytes": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
@@ -521,6 +526,18 @@ def dn_stem_fused(srcs, x, w, bias, y, imgs, ldy, stream=None):
 def add_layernorm(x, y, gamma, beta, out, rows, H, eps, stream=None):
     """K11: out = LayerNorm(x + y) * gamma + beta over ``rows`` rows of H bf16 (H in 512/1024/2048/4096)."""
     _check(_load().tcamd_add_layernorm(x, y, gamma, beta, out, rows, H, float(eps), _vp(stream)), "add_layernorm")
+
+
+ATTENTION_MAX_SEQ = 384
+
+
+def attention(qkv, mask, out, seqs, S, heads, scale, stream=None):
+    """K12: multi-head attention (head dim 64, non-causal) over the fused QKV
+    projection's output ``qkv`` [seqs*S][3*heads*64] bf16 into ``out``
+    [seqs*S][heads*64] bf16; ``mask`` int32 [seqs][S] key-padding mask (0 =
+    padded key) or None.  S % 64 == 0 and S <= ATTENTION_MAX_SEQ."""
+    _check(_load().tcamd_attention(qkv, _vp(mask), out, int(seqs), int(S), int(heads), float(scale), _vp(stream)),
+           "attention")
 
 
 def x3_conv1x1_ws_bytes(M, K, N=128):
