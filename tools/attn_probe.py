@@ -32,6 +32,7 @@ def timed(fn, iters=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--k12-only", action="store_true")
     ap.add_argument("--seq", type=int, default=384)
     a = ap.parse_args()
     b, s, h, d = a.batch, a.seq, 16, 64
@@ -51,6 +52,8 @@ def main():
     out = torch.empty(b * s, h * d, device="cuda", dtype=torch.bfloat16)
     mask = keep.to(torch.int32)
     st = torch.cuda.current_stream().cuda_stream
+    if a.k12_only:
+        cases = {}
     cases["K12 none"] = lambda: hip.attention(qkv.data_ptr(), None, out.data_ptr(), b, s, h, 0.125, stream=st)
     cases["K12 masked"] = lambda: hip.attention(qkv.data_ptr(), mask.data_ptr(), out.data_ptr(), b, s, h, 0.125,
                                                 stream=st)
