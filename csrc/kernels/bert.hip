@@ -104,6 +104,8 @@ namespace {
 //     chunk), then O^T += V^T P^T (8 MFMAs) with P^T taken straight from the
 //     S^T accumulators: the MFMA k index is permuted so a lane's 8 keys are
 //     exactly the 8 scores it already holds, and V^T is read in that order;
+//   * exponentials are raw v_exp_f32 (flushed denormals are exactly what a
+//     softmax wants; exp2f adds a range fix-up of ~4 VALU per score);
 //   * O / l leaves as bf16 in [tokens][heads * 64] — the layout the output
 //     projection GEMM reads, so no transpose kernel follows.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -196,7 +198,7 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
       }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f(m_run - m_new);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     m_run = m_new;
     float ls = 0.f;
     v4u pf[4];  // P^T fragments per 16-key step: keys 16 kk2 + {4h..4h+3, 8+4h..8+4h+3}
@@ -207,7 +209,7 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
         float pv[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          pv[e] = exp2f(st[rb][4 * g + e] - m_new);
+          pv[e] = __builtin_amdgcn_exp2f(st[rb][4 * g + e] - m_new);
           ls += pv[e];
         }
         const int kk2 = 2 * rb + (g >> 1), half = g & 1;
