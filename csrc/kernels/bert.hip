@@ -110,6 +110,7 @@ namespace {
 //     projection GEMM reads, so no transpose kernel follows.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
@@ -118,6 +119,7 @@ constexpr int kAMaxS = 384;       // keys / queries per sequence (multiple of 64
 
 __device__ __forceinline__ bf16x8 as_bf8(v4u v) { return __builtin_bit_cast(bf16x8, v); }
 
+template <bool MASKED>
 __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __restrict__ qkv, const int* __restrict__ mask,
                                                            uint16_t* __restrict__ out, int S, int heads, float scale) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_a[];
@@ -149,8 +151,8 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
       *reinterpret_cast<uint32_t*>(Vt + (8 * c + j) * ldv + key) = lo | (hi << 16);
     }
   }
-  for (int k = tid; k < S; k += nthr)
-    kb[k] = (mask && mask[(size_t)seq * S + k] == 0) ? -10000.0f * kLog2e : 0.0f;
+  if (MASKED)
+    for (int k = tid; k < S; k += nthr) kb[k] = mask[(size_t)seq * S + k] == 0 ? -10000.0f * kLog2e : 0.0f;
 
   // ---- this wave's queries: Q^T fragments (B operand: lane col = query) ----
   const int col = lane & 31, h = lane >> 5;
@@ -183,24 +185,35 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
         st[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(kf), as_bf8(qf[kk]), st[rb], 0, 0, 0);
       }
     }
+    // masked: x = s * scale * log2e + bias, max and exp2(x - m) on x;
+    // unmasked: max on the raw scores (scale > 0 commutes with max) and
+    // p = exp2(s * c - m * c) as one FMA per score
     float mx = -1.0e30f;
+    if constexpr (MASKED) {
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+      for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 bb = *reinterpret_cast<const f32x4*>(kb + c0 + 32 * rb + 8 * g + 4 * h);
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 bb = *reinterpret_cast<const f32x4*>(kb + c0 + 32 * rb + 8 * g + 4 * h);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float x = st[rb][4 * g + e] * sl2 + bb[e];
-          st[rb][4 * g + e] = x;
-          mx = fmaxf(mx, x);
+          for (int e = 0; e < 4; ++e) {
+            const float x = st[rb][4 * g + e] * sl2 + bb[e];
+            st[rb][4 * g + e] = x;
+            mx = fmaxf(mx, x);
+          }
         }
-      }
+    } else {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, st[rb][e]);
+      mx *= sl2;
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, mx);
     const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     m_run = m_new;
-    float ls = 0.f;
+    f32x2 ls2 = f32x2{0.f, 0.f};
     v4u pf[4];  // P^T fragments per 16-key step: keys 16 kk2 + {4h..4h+3, 8+4h..8+4h+3}
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
@@ -208,14 +221,15 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
       for (int g = 0; g < 4; ++g) {
         float pv[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          pv[e] = __builtin_amdgcn_exp2f(st[rb][4 * g + e] - m_new);
-          ls += pv[e];
-        }
+        for (int e = 0; e < 4; ++e)
+          pv[e] = MASKED ? __builtin_amdgcn_exp2f(st[rb][4 * g + e] - m_new)
+                         : __builtin_amdgcn_exp2f(__builtin_fmaf(st[rb][4 * g + e], sl2, -m_new));
+        ls2 += f32x2{pv[0], pv[1]} + f32x2{pv[2], pv[3]};
         const int kk2 = 2 * rb + (g >> 1), half = g & 1;
         pf[kk2][2 * half] = pack2(pv[0], pv[1]);
         pf[kk2][2 * half + 1] = pack2(pv[2], pv[3]);
       }
+    const float ls = ls2[0] + ls2[1];
     l_part = l_part * alpha + ls;
 #pragma unroll
     for (int r = 0; r < 2; ++r)
@@ -285,8 +299,11 @@ int tcamd_attention(const void* qkv, const int* mask, void* out, int seqs, int S
   const size_t lds = (size_t)S * kAD * 2 + (size_t)kAD * (S + 4) * 2 + (size_t)S * 4;
   static bool attr = false;
   if (!attr) {
-    const hipError_t e =
-        hipFuncSetAttribute((const void*)attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipError_t e =
+        hipFuncSetAttribute((const void*)attention_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)attention_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     if (e != hipSuccess) return e;
     attr = true;
   }
@@ -302,8 +319,13 @@ int tcamd_attention(const void* qkv, const int* mask, void* out, int seqs, int S
   for (int sp : {3, 2})
     if (splits == 1 && nw % sp == 0 && nw / sp >= 2 && seqs * heads * sp <= 256) splits = sp;
   const int qw = nw / splits;
-  hipLaunchKernelGGL(attention_kernel, dim3(seqs * heads, S / (32 * qw)), dim3(64 * qw), lds, (hipStream_t)stream,
-                     (const uint16_t*)qkv, mask, (uint16_t*)out, S, heads, scale);
+  const dim3 grid(seqs * heads, S / (32 * qw)), block(64 * qw);
+  if (mask)
+    hipLaunchKernelGGL(attention_kernel<true>, grid, block, lds, (hipStream_t)stream, (const uint16_t*)qkv, mask,
+                       (uint16_t*)out, S, heads, scale);
+  else
+    hipLaunchKernelGGL(attention_kernel<false>, grid, block, lds, (hipStream_t)stream, (const uint16_t*)qkv, mask,
+                       (uint16_t*)out, S, heads, scale);
   return hipGetLastError();
 }
 
