@@ -37,11 +37,28 @@ Error Backend::Create(const Options& o, std::unique_ptr<Backend>* out)
   for (const auto& kv : o.headers) be->headers_[kv.first] = kv.second;
   Error e;
   if (o.protocol == "grpc") {
+    tc::SslOptions ssl;
+    ssl.root_certificates = o.ssl.grpc_root_certs;
+    ssl.private_key = o.ssl.grpc_private_key;
+    ssl.certificate_chain = o.ssl.grpc_cert_chain;
     // a private channel per Backend: perf clients must not share one h2 connection
-    e = tc::InferenceServerGrpcClient::Create(&be->grpc_, o.url, o.verbose, false, tc::SslOptions(),
+    e = tc::InferenceServerGrpcClient::Create(&be->grpc_, o.url, o.verbose, o.ssl.grpc_use_ssl, ssl,
                                               tc::KeepAliveOptions(), false);
   } else {
-    e = tc::InferenceServerHttpClient::Create(&be->http_, o.url, o.verbose);
+    tc::HttpSslOptions ssl;
+    ssl.verify_peer = o.ssl.https_verify_peer;
+    ssl.verify_host = o.ssl.https_verify_host;
+    ssl.ca_info = o.ssl.https_ca;
+    ssl.cert = o.ssl.https_cert;
+    ssl.key = o.ssl.https_key;
+    ssl.cert_type = o.ssl.https_cert_der ? tc::HttpSslOptions::CERT_DER : tc::HttpSslOptions::CERT_PEM;
+    ssl.key_type = o.ssl.https_key_der ? tc::HttpSslOptions::KEY_DER : tc::HttpSslOptions::KEY_PEM;
+    std::string url = o.url;
+    if (o.ssl.https && url.compare(0, 8, "https://") != 0) {
+      if (url.compare(0, 7, "http://") == 0) url = url.substr(7);
+      url = "https://" + url;
+    }
+    e = tc::InferenceServerHttpClient::Create(&be->http_, url, o.verbose, ssl);
   }
   if (!e.IsOk()) return e;
   *out = std::move(be);

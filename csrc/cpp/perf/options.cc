@@ -16,6 +16,8 @@ enum LongOnly {
   OPT_SEQ_LEN, OPT_SEQ_RANGE, OPT_INPUT_DATA, OPT_STR_LEN, OPT_STR_DATA, OPT_SHM, OPT_OUT_SHM_SIZE, OPT_MEAS_MODE,
   OPT_MEAS_COUNT, OPT_PERCENTILE, OPT_WARMUP, OPT_VERBOSE_CSV, OPT_JSON, OPT_RESUME, OPT_COLLECT_METRICS, OPT_METRICS_INTERVAL, OPT_METRICS_SYSFS, OPT_SHM_INPUT, OPT_DEVICE, OPT_SEED,
   OPT_NUM_CLIENTS, OPT_NO_SERVER_STATS, OPT_GPUS, OPT_DEVICES, OPT_FANOUT, OPT_LOAD_PER_GPU, OPT_MEAS_INTERVAL, OPT_STABILITY, OPT_MAX_TRIALS, OPT_LAT_THRESH,
+  OPT_SSL_GRPC_USE, OPT_SSL_GRPC_ROOT, OPT_SSL_GRPC_KEY, OPT_SSL_GRPC_CHAIN, OPT_SSL_HTTPS_PEER, OPT_SSL_HTTPS_HOST,
+  OPT_SSL_HTTPS_CA, OPT_SSL_HTTPS_CERT, OPT_SSL_HTTPS_CERT_TYPE, OPT_SSL_HTTPS_KEY, OPT_SSL_HTTPS_KEY_TYPE,
 };
 
 bool ParseU64(const std::string& s, uint64_t* v)
@@ -103,7 +105,12 @@ std::string Usage()
       "  [ext] --fanout rccl|p2p|host     how the synthetic batch made once on the first GPU reaches the\n"
       "                                   others (RCCL broadcast / xGMI peer-copy star / host copies)\n"
       "  [ext] --load-per-gpu             every GPU gets the full concurrency / rate (weak scaling);\n"
-      "                                   default: the load is split over the GPUs\n";
+      "                                   default: the load is split over the GPUs\n"
+      "  --ssl-grpc-use-ssl, --ssl-grpc-root-certifications-file F, --ssl-grpc-private-key-file F,\n"
+      "  --ssl-grpc-certificate-chain-file F          gRPC over TLS (mutual TLS with key + chain)\n"
+      "  --ssl-https-verify-peer 0|1, --ssl-https-verify-host 0|1|2, --ssl-https-ca-certificates-file F,\n"
+      "  --ssl-https-client-certificate-file F, --ssl-https-client-certificate-type PEM|DER,\n"
+      "  --ssl-https-private-key-file F, --ssl-https-private-key-type PEM|DER   HTTPS (https:// is implied)\n";
 }
 
 Error ParseOptions(int argc, char** argv, Options* o, bool* help)
@@ -153,6 +160,17 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
       {"devices", required_argument, nullptr, OPT_DEVICES},
       {"fanout", required_argument, nullptr, OPT_FANOUT},
       {"load-per-gpu", no_argument, nullptr, OPT_LOAD_PER_GPU},
+      {"ssl-grpc-use-ssl", no_argument, nullptr, OPT_SSL_GRPC_USE},
+      {"ssl-grpc-root-certifications-file", required_argument, nullptr, OPT_SSL_GRPC_ROOT},
+      {"ssl-grpc-private-key-file", required_argument, nullptr, OPT_SSL_GRPC_KEY},
+      {"ssl-grpc-certificate-chain-file", required_argument, nullptr, OPT_SSL_GRPC_CHAIN},
+      {"ssl-https-verify-peer", required_argument, nullptr, OPT_SSL_HTTPS_PEER},
+      {"ssl-https-verify-host", required_argument, nullptr, OPT_SSL_HTTPS_HOST},
+      {"ssl-https-ca-certificates-file", required_argument, nullptr, OPT_SSL_HTTPS_CA},
+      {"ssl-https-client-certificate-file", required_argument, nullptr, OPT_SSL_HTTPS_CERT},
+      {"ssl-https-client-certificate-type", required_argument, nullptr, OPT_SSL_HTTPS_CERT_TYPE},
+      {"ssl-https-private-key-file", required_argument, nullptr, OPT_SSL_HTTPS_KEY},
+      {"ssl-https-private-key-type", required_argument, nullptr, OPT_SSL_HTTPS_KEY_TYPE},
       {"verbose", no_argument, nullptr, 'v'},
       {"help", no_argument, nullptr, 'h'},
       {nullptr, 0, nullptr, 0}};
@@ -329,6 +347,29 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
         o->fanout = arg;
         break;
       case OPT_LOAD_PER_GPU: o->load_per_gpu = true; break;
+      case OPT_SSL_GRPC_USE: o->ssl.grpc_use_ssl = true; break;
+      case OPT_SSL_GRPC_ROOT: o->ssl.grpc_root_certs = arg; o->ssl.grpc_use_ssl = true; break;
+      case OPT_SSL_GRPC_KEY: o->ssl.grpc_private_key = arg; o->ssl.grpc_use_ssl = true; break;
+      case OPT_SSL_GRPC_CHAIN: o->ssl.grpc_cert_chain = arg; o->ssl.grpc_use_ssl = true; break;
+      case OPT_SSL_HTTPS_PEER:
+        if (!ParseU64(arg, &u) || u > 1) return Error("--ssl-https-verify-peer expects 0 or 1");
+        o->ssl.https_verify_peer = static_cast<long>(u);
+        o->ssl.https = true;
+        break;
+      case OPT_SSL_HTTPS_HOST:
+        if (!ParseU64(arg, &u) || u > 2) return Error("--ssl-https-verify-host expects 0, 1 or 2");
+        o->ssl.https_verify_host = static_cast<long>(u);
+        o->ssl.https = true;
+        break;
+      case OPT_SSL_HTTPS_CA: o->ssl.https_ca = arg; o->ssl.https = true; break;
+      case OPT_SSL_HTTPS_CERT: o->ssl.https_cert = arg; o->ssl.https = true; break;
+      case OPT_SSL_HTTPS_KEY: o->ssl.https_key = arg; o->ssl.https = true; break;
+      case OPT_SSL_HTTPS_CERT_TYPE:
+      case OPT_SSL_HTTPS_KEY_TYPE:
+        if (arg != "PEM" && arg != "DER") return Error("certificate / key type must be PEM or DER");
+        (c == OPT_SSL_HTTPS_CERT_TYPE ? o->ssl.https_cert_der : o->ssl.https_key_der) = arg == "DER";
+        o->ssl.https = true;
+        break;
       case 'v': o->verbose = true; break;
       case 'h': *help = true; return Error::Success;
       default: {

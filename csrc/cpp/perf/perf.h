@@ -61,6 +61,15 @@ using triton::client::InferResult;
 uint64_t NowNs();
 struct Session;
 
+struct SslFlags {
+  bool grpc_use_ssl = false;
+  std::string grpc_root_certs, grpc_private_key, grpc_cert_chain;
+  bool https = false;  // any --ssl-https-* flag given
+  long https_verify_peer = 1, https_verify_host = 2;
+  std::string https_ca, https_cert, https_key;
+  bool https_cert_der = false, https_key_der = false;
+};
+
 struct Options {
   std::string model;
   std::string version;
@@ -71,6 +80,7 @@ struct Options {
   int batch = 1;
   std::map<std::string, std::vector<int64_t>> shapes;
   std::map<std::string, std::string> headers;
+  SslFlags ssl;
   bool verbose = false;
   // load
   bool rate_mode = false;

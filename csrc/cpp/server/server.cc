@@ -580,7 +580,7 @@ void Loop::Flush(Conn* c)
   const bool pending = c->sendpos < c->sendbuf.size();
   if (pending != c->want_write && !c->closing) {
     epoll_event e{};
-    e.events = EPOLLIN | (pending ? EPOLLOUT : 0);
+    e.events = EPOLLIN | (pending ? static_cast<uint32_t>(EPOLLOUT) : 0u);
     e.data.u64 = c->id + 16;
     epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &e);
     c->want_write = pending;

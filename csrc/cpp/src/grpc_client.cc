@@ -125,8 +125,8 @@ class InferResultGrpc : public InferResult {
       return Error("This function supports tensors with datatype 'BYTES', requested output tensor '" + name +
                    "' with datatype '" + dt + "'");
     }
-    const uint8_t* buf;
-    size_t n;
+    const uint8_t* buf = nullptr;
+    size_t n = 0;
     e = RawData(name, &buf, &n);
     if (!e.IsOk()) return e;
     out->clear();

@@ -137,8 +137,8 @@ class InferResultHttp : public InferResult {
       return Error("This function supports tensors with datatype 'BYTES', requested output tensor '" +
                    output_name + "' with datatype '" + dt + "'");
     }
-    const uint8_t* buf;
-    size_t n;
+    const uint8_t* buf = nullptr;
+    size_t n = 0;
     e = RawData(output_name, &buf, &n);
     if (!e.IsOk()) return e;
     string_result->clear();

@@ -531,7 +531,7 @@ InputJsonData(const std::string& dt, const std::vector<uint8_t>& a, const std::v
   const js::Value* ins = root.Find("inputs");
   if (!ins || ins->Size() != 1) return false;
   const js::Value* d = (*ins)[0].Find("data");
-  if (!d || (*ins)[0].Find("parameters") && (*ins)[0].Find("parameters")->Find("binary_data_size")) return false;
+  if (!d || ((*ins)[0].Find("parameters") && (*ins)[0].Find("parameters")->Find("binary_data_size"))) return false;
   *data = *d;
   return body.size() == hl;  // nothing sent in the binary section
 }

@@ -179,3 +179,30 @@ def test_cpp_grpc_example_tls_flags(tls_server, mtls_server, certs):
     r = _cpp("simple_grpc_infer_client", "-u", "localhost:%d" % mtls_server.grpc_port, "--ssl", "--root-certificates",
              certs["ca"], "--private-key", certs["client_key"], "--certificate-chain", certs["client"])
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
+
+
+def test_perf_analyzer_ssl_flags(tls_server, mtls_server, certs):
+    """perf_analyzer's --ssl-grpc-* / --ssl-https-* flags against the TLS server."""
+    pa = os.path.join(BIN, "perf_analyzer")
+    if not os.path.exists(pa):
+        pytest.skip("csrc/cpp not built")
+
+    def run(*args):
+        return subprocess.run([pa, "-m", "simple", "--concurrency-range", "2", "-p", "300", "-r", "3", "-s", "80",
+                               *args], capture_output=True, text=True, timeout=120)
+
+    r = run("-i", "grpc", "-u", "localhost:%d" % tls_server.grpc_port, "--ssl-grpc-use-ssl",
+            "--ssl-grpc-root-certifications-file", certs["ca"])
+    assert r.returncode == 0 and "Throughput" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]
+    r = run("-i", "grpc", "-u", "localhost:%d" % mtls_server.grpc_port, "--ssl-grpc-root-certifications-file",
+            certs["ca"], "--ssl-grpc-private-key-file", certs["client_key"], "--ssl-grpc-certificate-chain-file",
+            certs["client"])
+    assert r.returncode == 0 and "Throughput" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]
+    r = run("-i", "http", "-u", "127.0.0.1:%d" % tls_server.http_port, "--ssl-https-ca-certificates-file", certs["ca"])
+    assert r.returncode == 0 and "Throughput" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]
+    r = run("-i", "http", "-u", "127.0.0.1:%d" % tls_server.http_port, "--ssl-https-ca-certificates-file",
+            certs["other"])
+    assert r.returncode != 0
+    r = run("-i", "http", "-u", "127.0.0.1:%d" % tls_server.http_port, "--ssl-https-verify-peer", "0",
+            "--ssl-https-verify-host", "0")
+    assert r.returncode == 0, r.stdout[-1500:] + r.stderr[-1500:]
