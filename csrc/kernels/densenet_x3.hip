@@ -1184,16 +1184,6 @@ X3Plan x3_plan(int M, int K, int N) {
 
 template <bool POOL, bool SPLIT>
 void launch_x3_1x1(const X3Plan& pl, const dim3& g, hipStream_t s, const X3Conv1x1Params& p) {
-  static const int pf128 = [] {  // A/B knob: register-ring depth of the BM 128 tile
-    const char* e = getenv("TCAMD_X3_PF128");
-    return e ? atoi(e) : 1;
-  }();
-  if constexpr (!POOL) {
-    if (pl.bm == 128 && pf128 == 2) {
-      hipLaunchKernelGGL((x3_conv1x1_kernel<POOL, SPLIT, 128, 2, 2>), g, dim3(256), 0, s, p);
-      return;
-    }
-  }
   if (pl.bm == 128) hipLaunchKernelGGL((x3_conv1x1_kernel<POOL, SPLIT, 128, 2, 1>), g, dim3(256), 0, s, p);
   // the pooled prologue holds 4 source rows per chunk: a shallower ring
   else if (pl.bm == 64) hipLaunchKernelGGL((x3_conv1x1_kernel<POOL, SPLIT, 64, 1, POOL ? 2 : 4>), g, dim3(256), 0, s, p);
