@@ -78,7 +78,7 @@ def parse_args(argv=None):
     ap.add_argument("--max-queue-delay-us", type=int, default=2000)
     ap.add_argument("--max-batch-size", type=int, default=0)
     ap.add_argument("--preferred", default="128")
-    ap.add_argument("--idle-dispatch", default="off", choices=["on", "off"])
+    ap.add_argument("--idle-dispatch", default="on", choices=["on", "off"])
     ap.add_argument("--cpu", action="store_true", help="no GPU: CPU frontend_sink model, system shm, gloo")
     ap.add_argument("--server-log", default="")
     ap.add_argument("--model", default="densenet_onnx", choices=["densenet_onnx", "bert_large"])
