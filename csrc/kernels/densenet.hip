@@ -282,19 +282,41 @@ __global__ void __launch_bounds__(256) conv1x1_kernel(Conv1x1Params p) {
     }
     return;
   }
-  // epilogue: lane holds out channels nb..nb+3 of pixel m (bias already in acc)
+  // epilogue: lane holds out channels nb..nb+3 of pixel m (bias already in
+  // acc).  The wave's [16 TM px][WN ch] bf16 tile goes through a slab in the
+  // (now idle) B tile, 16-B chunks XOR-swizzled by pixel, and leaves as
+  // 16-B-per-lane stores covering each pixel's WN*2 contiguous bytes, instead
+  // of 8-B pieces scattered over 16 pixel rows per instruction
+  constexpr int CH = WN / 8;                            // 16-B chunks per slab row
+  constexpr int TG0 = (int)sizeof(sB) / (4 * 16 * WN * 2);  // 16-pixel groups per slab fill
+  constexpr int TG = TG0 < TM ? TG0 : TM;
+  static_assert(TG >= 1 && TM % TG == 0, "epilogue slab fits the B tile");
+  constexpr int PX = 16 * TG;                           // pixels per slab fill
+  uint8_t* slab = reinterpret_cast<uint8_t*>(&sB[0][0]) + wave * PX * WN * 2;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int nb = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
+  for (int i0 = 0; i0 < TM; i0 += TG) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wm * 16 * TM + i * 16 + fr;
-      if (m < p.M) {
-        v2u o = v2u{pack2(acc[j][i][0], acc[j][i][1]), pack2(acc[j][i][2], acc[j][i][3])};
+    for (int j = 0; j < NJ; ++j) {
+      const int q = lane >> 4;  // channel quad: channels j*16 + 4q .. +3 of the wave's WN
+#pragma unroll
+      for (int ii = 0; ii < TG; ++ii) {
+        const int px = ii * 16 + fr;
+        const f32x4 a = acc[j][i0 + ii];
+        v2u o = v2u{pack2(a[0], a[1]), pack2(a[2], a[3])};
         if (p.relu_out) o = v2u{relu_pk(o[0]), relu_pk(o[1])};
-        *reinterpret_cast<v2u*>(p.y + (size_t)m * p.ldy + nb) = o;
+        const int c = 2 * j + (q >> 1);
+        *reinterpret_cast<v2u*>(slab + px * WN * 2 + ((c ^ (px & (CH - 1))) << 4) + 8 * (q & 1)) = o;
       }
     }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's slab writes landed
+#pragma unroll
+    for (int pass = 0; pass < PX * CH / 64; ++pass) {
+      const int px = pass * (64 / CH) + lane / CH, c = lane % CH;
+      const v4u v = *reinterpret_cast<const v4u*>(slab + px * WN * 2 + ((c ^ (px & (CH - 1))) << 4));
+      const int m = m0 + wm * 16 * TM + i0 * 16 + px;
+      if (m < p.M) *reinterpret_cast<v4u*>(p.y + (size_t)m * p.ldy + n0 + wn * WN + 8 * c) = v;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // slab reads done before the next fill
   }
 }
 
