@@ -83,7 +83,7 @@ def parse_args(argv=None):
     ap.add_argument("--server-log", default="")
     ap.add_argument("--model", default="densenet_onnx", choices=["densenet_onnx", "bert_large"])
     ap.add_argument("--sweep", default="1,4,16,64,256", help="bert_large: concurrencies per GPU")
-    ap.add_argument("--bert-instance-count", type=int, default=3)
+    ap.add_argument("--bert-instance-count", type=int, default=2)
     ap.add_argument("--bert-queue-delay-us", type=int, default=500)
     return ap.parse_args(argv)
 
