@@ -26,7 +26,7 @@ windows), and the run is "stable" when the 3 windows before the last (which
 holds the final drain) are within 10% of their mean (perf_analyzer's rule).  value = total
 images/s over all ranks (elapsed = MAX over ranks); p50/p90/p99 over every
 rank's requests.  After the timed bs=8 region: a bs=1 point (HIP shm, same
-server) and, unless ``--no-bf16``, the bf16 engine as a labelled
+server) and, unless ``--no-bf16`` (or on more than one GPU), the bf16 engine as a labelled
 reduced-precision operating point.
 
 ``--cpu`` runs the same pipeline with no GPU (CPU ``frontend_sink`` model,
@@ -363,7 +363,8 @@ def main():
         points.clear()
 
         # ---- bf16 engine: labelled reduced-precision operating point -------------------
-        if not cpu and not args.no_bf16 and args.engine == "fp32":
+        # (one GPU only: a multi-GPU scaling run stays on the headline engine)
+        if not cpu and not args.no_bf16 and args.engine == "fp32" and world == 1:
             client.unregister_cuda_shared_memory()
             client.close()
             state["client"] = None
