@@ -104,6 +104,7 @@ struct X3Conv1x1Params {
   float* y;              // !SPLIT: [M][ldy] fp32, raw conv output
   float* ws;             // split-K partials [splits][M][N] (null = whole K per block)
   int ldx, M, K, N, ldy, H, W, k_per_split;
+  int xcd_group;         // N > 128: sibling N-tiles of an M-tile on one XCD (see the kernel)
 };
 
 constexpr int kBN = 128, kBK = 32, kLDK = kBK + 8;  // 80-B LDS rows: conflict-free b128 reads
@@ -133,7 +134,18 @@ __global__ void __launch_bounds__(256, 2) x3_conv1x1_kernel(X3Conv1x1Params p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.z * kBN;
+  // N-tiles of one M-tile (transitions, N > 128): with p.xcd_group, grid.x =
+  // m-groups x nt x 8 and block L runs (m_tile = (L/8/nt)*8 + L%8, n = L/8 %
+  // nt), so the nt blocks sharing an X tile sit 8 ids apart — the same XCD,
+  // back to back — and the re-reads of X hit that XCD's L2
+  int mt = blockIdx.x, nt_i = blockIdx.z;
+  if (p.xcd_group) {
+    const int nt = p.N / kBN, r = blockIdx.x >> 3;
+    mt = (r / nt) * 8 + (blockIdx.x & 7);
+    nt_i = r % nt;
+    if (mt * BM >= p.M) return;
+  }
+  const int m0 = mt * BM, n0 = nt_i * kBN;
 
   // X: BM rows x 8 chunks of 4 fp32 per K step, all of a thread's chunks at
   // the same K offset (tid & 7); POOL: each chunk averages 4 source rows
@@ -1278,7 +1290,10 @@ int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, int N, const float* 
     else hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, 0>), dim3(blocks), dim3(512), kLdsWs, s, wp);
     return hipGetLastError();
   }
-  const dim3 g((M + pl.bm - 1) / pl.bm, pl.splits, N / kBN);
+  static const int xg = getenv("TCAMD_X3_XCD_GROUP") ? atoi(getenv("TCAMD_X3_XCD_GROUP")) : 1;
+  const int mb = (M + pl.bm - 1) / pl.bm, ntl = N / kBN;
+  p.xcd_group = (xg && ntl > 1 && pl.splits == 1) ? 1 : 0;
+  const dim3 g = p.xcd_group ? dim3((mb + 7) / 8 * 8 * ntl, 1, 1) : dim3(mb, pl.splits, ntl);
   if (pool) {
     if (split_out) launch_x3_1x1<true, true>(pl, g, s, p);
     else launch_x3_1x1<true, false>(pl, g, s, p);
