@@ -28,3 +28,9 @@ for k, cs in agg.items():
     if "SQ_BUSY_CYCLES" in m and "SQ_VALU_MFMA_BUSY_CYCLES" in m and m["SQ_BUSY_CYCLES"]:
         # MFMA busy cycles are per SIMD summed over the chip; busy cycles per SE (x? ) -> report raw ratio
         print("  -> mfma_busy / busy = %.3f" % (m["SQ_VALU_MFMA_BUSY_CYCLES"] / m["SQ_BUSY_CYCLES"]))
+    if "FETCH_SIZE" in m or "WRITE_SIZE" in m:
+        # FETCH_SIZE / WRITE_SIZE are in KiB (L2 <-> memory traffic)
+        print("  -> L2<->HBM fetch %.1f MB  write %.1f MB" % (m.get("FETCH_SIZE", 0) * 1024 / 1e6,
+                                                          m.get("WRITE_SIZE", 0) * 1024 / 1e6))
+    if m.get("TCC_HIT_sum", 0) + m.get("TCC_MISS_sum", 0):
+        print("  -> L2 hit rate %.1f%%" % (100 * m["TCC_HIT_sum"] / (m["TCC_HIT_sum"] + m["TCC_MISS_sum"])))
