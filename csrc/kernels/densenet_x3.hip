@@ -974,30 +974,37 @@ struct X3StemParams {
   int ldy;
 };
 
-template <bool V2>
-__global__ void __launch_bounds__(256) x3_stem_kernel(X3StemParams p) {
-  __shared__ __attribute__((aligned(16))) uint16_t Ih[kSIR * kSIC * 4];  // 13.2 KB
-  __shared__ __attribute__((aligned(16))) uint16_t Il[kSIR * kSIC * 4];
-  __shared__ __attribute__((aligned(16))) float Cv[V2 ? 4 : kSCR * kSCC * kSOS];   // v1: 78 KB conv tile
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int img = blockIdx.z, pr0 = blockIdx.y * kSPR, pc0 = blockIdx.x * kSPC;
+constexpr int kStage = (kSIR * kSIC + 255) / 256;
+
+// The 23x72 input patch (3 channels) of the tile whose pooled origin is
+// (pr0, pc0) into registers, zero outside the image.  Branch-free (clamped
+// addresses, then a select) through a global-address-space pointer: the
+// pointer comes from the srcs table, and as a generic pointer the loads were
+// flat loads under per-element branches, each waited for (vmcnt(0)) before
+// the next was issued, and counted against lgkmcnt too.
+typedef const __attribute__((address_space(1))) float* x3_gptr;
+__device__ __forceinline__ void x3_stem_load(const float* src, int pr0, int pc0, int tid, float (&v)[kStage][3]) {
+  const x3_gptr g = (x3_gptr)src;
   const int ir0 = 4 * pr0 - 5, ic0 = 4 * pc0 - 5;
-  const float* src = p.srcs[img];
-  constexpr int kStage = (kSIR * kSIC + 255) / 256;
-  float v[kStage][3];
 #pragma unroll
   for (int i = 0; i < kStage; ++i) {
     const int e = tid + i * 256;
-    const int r = e / kSIC, c = e - r * kSIC;
+    const int ec = min(e, kSIR * kSIC - 1);
+    const int r = ec / kSIC, c = ec - r * kSIC;
     const int ih = ir0 + r, iw = ic0 + c;
-    v[i][0] = v[i][1] = v[i][2] = 0.f;
-    if (e < kSIR * kSIC && ih >= 0 && ih < kSHin && iw >= 0 && iw < kSHin) {
-      const float* s = src + ih * kSHin + iw;
-      v[i][0] = __builtin_nontemporal_load(s);
-      v[i][1] = __builtin_nontemporal_load(s + kSHin * kSHin);
-      v[i][2] = __builtin_nontemporal_load(s + 2 * kSHin * kSHin);
-    }
+    const bool in = e < kSIR * kSIC && ih >= 0 && ih < kSHin && iw >= 0 && iw < kSHin;
+    const int o = min(max(ih, 0), kSHin - 1) * kSHin + min(max(iw, 0), kSHin - 1);
+    const float a0 = __builtin_nontemporal_load(g + o);
+    const float a1 = __builtin_nontemporal_load(g + o + kSHin * kSHin);
+    const float a2 = __builtin_nontemporal_load(g + o + 2 * kSHin * kSHin);
+    v[i][0] = in ? a0 : 0.f;
+    v[i][1] = in ? a1 : 0.f;
+    v[i][2] = in ? a2 : 0.f;
   }
+}
+
+// The patch, split into hi/lo bf16 planes: pixel e = 4 channels (the 4th 0).
+__device__ __forceinline__ void x3_stem_stage(uint16_t* Ih, uint16_t* Il, int tid, const float (&v)[kStage][3]) {
 #pragma unroll
   for (int i = 0; i < kStage; ++i) {
     const int e = tid + i * 256;
@@ -1009,89 +1016,141 @@ __global__ void __launch_bounds__(256) x3_stem_kernel(X3StemParams p) {
       *reinterpret_cast<v2u*>(&Il[e * 4]) = v2u{l0, l1};
     }
   }
-  // wave = (channel half nh) x (conv-row group mg)
-  const int nh = wave & 1, mg = wave >> 1;
-  v4u wh[kSK / 16], wl[kSK / 16];
+}
+
+// Wave (nh = channel half, mg = conv-row group)'s weight fragments.
+__device__ __forceinline__ void x3_stem_weights(const X3StemParams& p, int lane, int nh, v4u (&wh)[kSK / 16],
+                                                v4u (&wl)[kSK / 16]) {
   const size_t wrow = (size_t)(nh * 32 + (lane & 31)) * kSK + 8 * (lane >> 5);
 #pragma unroll
   for (int s = 0; s < kSK / 16; ++s) {
     wh[s] = ld16(p.w_hi + wrow + s * 16);
     wl[s] = ld16(p.w_lo + wrow + s * 16);
   }
-  __syncthreads();
+}
+
+// One conv row (32 conv cols x this wave's 32 channels) on MFMA.  The next
+// k-step's patch fragments are read from LDS while this step's 3 MFMAs run
+// (reading them just before use left every step waiting on LDS latency).
+__device__ __forceinline__ f32x16 x3_stem_conv_row(const uint16_t* Ih, const uint16_t* Il, const v4u (&wh)[kSK / 16],
+                                                   const v4u (&wl)[kSK / 16], int cr, int lane) {
   const int jj = lane & 31, hh = lane >> 5;
-  auto conv_row = [&](int cr) {
-    f32x16 acc;
+  auto off = [&](int s) { return ((2 * cr + (s >> 1)) * kSIC + 2 * jj + 2 * ((s & 1) * 2 + hh)) * 4; };
+  f32x16 acc;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  v4u bh = ld16(&Ih[off(0)]), bl = ld16(&Il[off(0)]);
 #pragma unroll
-    for (int s = 0; s < kSK / 16; ++s) {
-      const int kh = s >> 1, q = (s & 1) * 2 + hh;
-      const int off = ((2 * cr + kh) * kSIC + 2 * jj + 2 * q) * 4;
-      acc = x3_32(wh[s], wl[s], ld16(&Ih[off]), ld16(&Il[off]), acc);
+  for (int s = 0; s < kSK / 16; ++s) {
+    v4u nh = bh, nl = bl;
+    if (s + 1 < kSK / 16) {
+      nh = ld16(&Ih[off(s + 1)]);
+      nl = ld16(&Il[off(s + 1)]);
     }
-    return acc;
-  };
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs
+    acc = x3_32(wh[s], wl[s], bh, bl, acc);
+    bh = nh;
+    bl = nl;
+  }
+  return acc;
+}
+
+// lane i <- lane i + 1 (DPP wave_shl:1; lanes past the end keep their own value)
+__device__ __forceinline__ float x3_lane_next(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), 0x130, 0xf, 0xf, false));
+}
+
+// v2 pooling: no conv tile in LDS (bias from LDS copy sb: a global load here
+// would make the compiler wait for the next tile's prefetch, vmcnt(0)).  Waves mg = 0/1 own conv rows 0-4 / 4-8
+// (row 4 twice: 5 rows each) = pooled rows 2mg, 2mg+1; the 3-wide column max
+// runs across lanes (shuffles within each 32-lane half), the 3-tall row max
+// in registers.  C layout: lane col jj = conv col, reg 4g+e -> channel
+// 8g + 4h + e of this wave's 32.
+__device__ __forceinline__ void x3_stem_pool_tile(const X3StemParams& p, const uint16_t* Ih, const uint16_t* Il,
+                                                  const float* sb,
+                                                  const v4u (&wh)[kSK / 16], const v4u (&wl)[kSK / 16], int img,
+                                                  int pr0, int pc0, int lane, int wave) {
+  const int nh = wave & 1, mg = wave >> 1;
+  const int jj = lane & 31, hh = lane >> 5;
+  const float ninf = -3.0e38f;
+  f32x16 pm[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) pm[i][e] = ninf;
+  const bool left_pad = pc0 == 0 && jj == 0;  // conv col -1
+#pragma unroll 1
+  for (int r = 0; r < 5; ++r) {
+    const int cr = 4 * mg + r;
+    f32x16 acc = x3_stem_conv_row(Ih, Il, wh, wl, cr, lane);
+    if (left_pad) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = ninf;
+    }
+    // column max over conv cols jj, jj+1, jj+2 (read by even lanes jj = 2b <
+    // 28, so the shift never needs a lane of the other 32-lane half)
+    f32x16 cm;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float a1 = x3_lane_next(acc[e]), a2 = x3_lane_next(a1);
+      cm[e] = fmaxf(acc[e], fmaxf(a1, a2));
+    }
+    if (pr0 == 0 && cr == 0) continue;  // conv row -1 (top padding)
+    if (r <= 2) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) pm[0][e] = fmaxf(pm[0][e], cm[e]);
+    }
+    if (r >= 2) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) pm[1][e] = fmaxf(pm[1][e], cm[e]);
+    }
+  }
+  if ((jj & 1) == 0 && jj < 2 * kSPC) {
+    const int pc = pc0 + (jj >> 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int pr = pr0 + 2 * mg + i;
+      float* o = p.y + (((size_t)img * kSHo + pr) * kSHo + pc) * p.ldy + nh * 32 + 4 * hh;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(sb + nh * 32 + 8 * g + 4 * hh);
+        *reinterpret_cast<f32x4*>(o + 8 * g) =
+            f32x4{fmaxf(pm[i][4 * g] + bb[0], 0.f), fmaxf(pm[i][4 * g + 1] + bb[1], 0.f),
+                  fmaxf(pm[i][4 * g + 2] + bb[2], 0.f), fmaxf(pm[i][4 * g + 3] + bb[3], 0.f)};
+      }
+    }
+  }
+}
+
+template <bool V2>
+__global__ void __launch_bounds__(256) x3_stem_kernel(X3StemParams p) {
+  __shared__ __attribute__((aligned(16))) uint16_t Ih[kSIR * kSIC * 4];  // 13.2 KB
+  __shared__ __attribute__((aligned(16))) uint16_t Il[kSIR * kSIC * 4];
+  __shared__ __attribute__((aligned(16))) float Cv[V2 ? 4 : kSCR * kSCC * kSOS];   // v1: 78 KB conv tile
+  __shared__ __attribute__((aligned(16))) float sb[64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int img = blockIdx.z, pr0 = blockIdx.y * kSPR, pc0 = blockIdx.x * kSPC;
+  if (tid < 16) *reinterpret_cast<f32x4*>(sb + 4 * tid) = ldf4(p.bias + 4 * tid);
+  {
+    float v[kStage][3];
+    x3_stem_load(p.srcs[img], pr0, pc0, tid, v);
+    x3_stem_stage(Ih, Il, tid, v);
+  }
+  // wave = (channel half nh) x (conv-row group mg)
+  const int nh = wave & 1, mg = wave >> 1;
+  v4u wh[kSK / 16], wl[kSK / 16];
+  x3_stem_weights(p, lane, nh, wh, wl);
+  __syncthreads();
   if constexpr (V2) {
     // v2: no conv tile in LDS (26 KB per block: several blocks per CU, so
-    // one block's staging overlaps another's MFMAs).  Waves mg = 0/1 own conv
-    // rows 0-4 / 4-8 (row 4 twice: 5 rows each, as the old 5/4 split's
-    // critical path) = pooled rows 2mg, 2mg+1; the 3-wide column max runs
-    // across lanes (shuffles within each 32-lane half), the 3-tall row max
-    // in registers.  C layout: lane col jj = conv col, reg 4g+e -> channel
-    // 8g + 4h + e of this wave's 32.
-    const float ninf = -3.0e38f;
-    f32x16 pm[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) pm[i][e] = ninf;
-    const bool left_pad = pc0 == 0 && jj == 0;  // conv col -1
-#pragma unroll 1
-    for (int r = 0; r < 5; ++r) {
-      const int cr = 4 * mg + r;
-      f32x16 acc = conv_row(cr);
-      if (left_pad) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[e] = ninf;
-      }
-      // column max over conv cols jj, jj+1, jj+2 (read by even lanes jj = 2b)
-      f32x16 cm;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const float a1 = __shfl_down(acc[e], 1, 32), a2 = __shfl_down(acc[e], 2, 32);
-        cm[e] = fmaxf(acc[e], fmaxf(a1, a2));
-      }
-      if (pr0 == 0 && cr == 0) continue;  // conv row -1 (top padding)
-      if (r <= 2) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) pm[0][e] = fmaxf(pm[0][e], cm[e]);
-      }
-      if (r >= 2) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) pm[1][e] = fmaxf(pm[1][e], cm[e]);
-      }
-    }
-    if ((jj & 1) == 0 && jj < 2 * kSPC) {
-      const int pc = pc0 + (jj >> 1);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int pr = pr0 + 2 * mg + i;
-        float* o = p.y + (((size_t)img * kSHo + pr) * kSHo + pc) * p.ldy + nh * 32 + 4 * hh;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 bb = ldf4(p.bias + nh * 32 + 8 * g + 4 * hh);
-          *reinterpret_cast<f32x4*>(o + 8 * g) =
-              f32x4{fmaxf(pm[i][4 * g] + bb[0], 0.f), fmaxf(pm[i][4 * g + 1] + bb[1], 0.f),
-                    fmaxf(pm[i][4 * g + 2] + bb[2], 0.f), fmaxf(pm[i][4 * g + 3] + bb[3], 0.f)};
-        }
-      }
-    }
+    // one block's staging overlaps another's MFMAs)
+    x3_stem_pool_tile(p, Ih, Il, sb, wh, wl, img, pr0, pc0, lane, wave);
     return;
   }
+  const int jj = lane & 31, hh = lane >> 5;
   const int r_lo = mg ? 5 : 0, r_hi = mg ? kSCR : 5;
   for (int cr = r_lo; cr < r_hi; ++cr) {
-    const f32x16 acc = conv_row(cr);
+    const f32x16 acc = x3_stem_conv_row(Ih, Il, wh, wl, cr, lane);
     float* cp = &Cv[(cr * kSCC + jj) * kSOS + nh * 32 + 4 * hh];
 #pragma unroll
     for (int g = 0; g < 4; ++g)
@@ -1119,6 +1178,41 @@ __global__ void __launch_bounds__(256) x3_stem_kernel(X3StemParams p) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = fmaxf(mx[e] + bb[e], 0.f);
     *reinterpret_cast<f32x4*>(p.y + (((size_t)img * kSHo + pr) * kSHo + pc) * p.ldy + cc * 4) = o;
+  }
+}
+
+// K10x stem v3: persistent.  A block loads its waves' weight fragments once
+// and walks tiles t = blockIdx.x, +gridDim.x, ...; the next tile's input
+// patch is loaded into registers while the current tile's conv rows run on
+// MFMA, so neither the weight prologue nor the patch load sits on the
+// critical path of every tile (v2 pays both per 4x14 tile).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) x3_stem_p_kernel(X3StemParams p, int ntiles) {
+  __shared__ __attribute__((aligned(16))) uint16_t Ih[kSIR * kSIC * 4];
+  __shared__ __attribute__((aligned(16))) uint16_t Il[kSIR * kSIC * 4];
+  __shared__ __attribute__((aligned(16))) float sb[64];
+  constexpr int kTX = kSHo / kSPC, kTY = kSHo / kSPR;  // 4 x 14 tiles per image
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 16) *reinterpret_cast<f32x4*>(sb + 4 * tid) = ldf4(p.bias + 4 * tid);
+  v4u wh[kSK / 16], wl[kSK / 16];
+  x3_stem_weights(p, lane, wave & 1, wh, wl);
+  float v[kStage][3];
+  int t = blockIdx.x;
+  if (t < ntiles) {
+    const int img = t / (kTX * kTY), r = t - img * kTX * kTY;
+    x3_stem_load(p.srcs[img], (r / kTX) * kSPR, (r % kTX) * kSPC, tid, v);
+  }
+  for (; t < ntiles; t += gridDim.x) {
+    const int img = t / (kTX * kTY), r = t - img * kTX * kTY;
+    const int pr0 = (r / kTX) * kSPR, pc0 = (r % kTX) * kSPC;
+    __syncthreads();  // the previous tile's conv rows are done with Ih/Il
+    x3_stem_stage(Ih, Il, tid, v);
+    __syncthreads();
+    const int tn = t + gridDim.x;
+    if (tn < ntiles) {
+      const int imn = tn / (kTX * kTY), rn = tn - imn * kTX * kTY;
+      x3_stem_load(p.srcs[imn], (rn / kTX) * kSPR, (rn % kTX) * kSPC, tid, v);
+    }
+    x3_stem_pool_tile(p, Ih, Il, sb, wh, wl, img, pr0, pc0, lane, wave);
   }
 }
 
@@ -1370,6 +1464,17 @@ int tcamd_x3_conv3x3(const void* z_hi, const void* z_lo, int imgs, int H, int W,
   return hipGetLastError();
 }
 
+static int cu_count() {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  return ncu;
+}
+
 // fp32 stem over fp32 NCHW 224x224x3 images (device pointer table srcs)
 // -> y fp32 [imgs][56][56] rows of ldy (channels 0..63).
 int tcamd_x3_stem(const void* srcs, const void* w_hi, const void* w_lo, const float* bias, float* y, int imgs, int ldy,
@@ -1385,11 +1490,20 @@ int tcamd_x3_stem(const void* srcs, const void* w_hi, const void* w_lo, const fl
   p.bias = bias;
   p.y = y;
   p.ldy = ldy;
-  // v2 (pool in registers, 26 KB LDS) unless TCAMD_X3_STEM=1 (A/B runs)
-  static const int stem_v = getenv("TCAMD_X3_STEM") ? atoi(getenv("TCAMD_X3_STEM")) : 2;
+  // v3 (persistent, TCAMD_X3_STEM_BPC blocks per CU) unless TCAMD_X3_STEM=1/2
+  // (v1: conv tile in LDS, v2: one block per tile; A/B runs)
+  static const int stem_v = getenv("TCAMD_X3_STEM") ? atoi(getenv("TCAMD_X3_STEM")) : 3;
   const dim3 g(kSHo / kSPC, kSHo / kSPR, imgs);
-  if (stem_v == 1) hipLaunchKernelGGL(x3_stem_kernel<false>, g, dim3(256), 0, (hipStream_t)stream, p);
-  else hipLaunchKernelGGL(x3_stem_kernel<true>, g, dim3(256), 0, (hipStream_t)stream, p);
+  if (stem_v == 1) {
+    hipLaunchKernelGGL(x3_stem_kernel<false>, g, dim3(256), 0, (hipStream_t)stream, p);
+  } else if (stem_v == 2) {
+    hipLaunchKernelGGL(x3_stem_kernel<true>, g, dim3(256), 0, (hipStream_t)stream, p);
+  } else {
+    static const int bpc = getenv("TCAMD_X3_STEM_BPC") ? std::max(1, atoi(getenv("TCAMD_X3_STEM_BPC"))) : 2;
+    const int ntiles = (int)(g.x * g.y) * imgs;
+    const int grid = std::min(ntiles, bpc * cu_count());
+    hipLaunchKernelGGL(x3_stem_p_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, ntiles);
+  }
   return hipGetLastError();
 }
 

@@ -141,11 +141,11 @@ def test_x3_conv3x3(imgs, H):
     assert (y[:, :off] == 7.0).all() and (y[:, off + 32:] == 7.0).all()
 
 
-def test_x3_stem():
+@pytest.mark.parametrize("imgs", [3, 20])  # 20: more tiles than the persistent grid (several per block)
+def test_x3_stem(imgs):
     _need_gpu()
     hip = _hip()
     g = torch.Generator(device=DEV).manual_seed(5)
-    imgs = 3
     x = torch.randn(imgs, 3, 224, 224, device=DEV, generator=g)
     w = torch.randn(64, 3, 7, 7, device=DEV, generator=g) / 12
     bias = torch.randn(64, device=DEV, generator=g) * 0.1
