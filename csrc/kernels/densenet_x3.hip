@@ -24,12 +24,12 @@
 //    TWO bf16 planes z_hi/z_lo (the 3x3 conv's operands, already split:
 //    same bytes as fp32).  POOL=true is the transition: BN+ReLU+2x2 avg-pool
 //    in the prologue, fp32 output into the next block's buffer;
-//  * K9x conv3x3 (128->32): eight waves split the 128 input channels (16
-//    each = one 32x32x16 MFMA K), so each wave's hi/lo weight fragments for
-//    all nine taps live in 72 VGPRs for the whole persistent kernel; the
-//    block stages the z_hi/z_lo band its 128-pixel tile needs in LDS (the
-//    next tile's band is prefetched into registers during the MFMAs) and the
-//    8 partial tiles are summed through LDS;
+//  * K9x conv3x3 (128->32): 8 waves = 2 pixel halves x 4 input-channel
+//    quarters, each wave's hi/lo weight fragments for all nine taps in
+//    registers for the whole persistent kernel (loaded from a fragment-major
+//    copy, x3_w3_fragments); a block walks a run of 64-pixel tiles with the
+//    z_hi/z_lo band in an LDS ring fed by LDS-DMA, and the 4 partials are
+//    summed through LDS in one round;
 //  * K10x stem (7x7/2 conv + BN + ReLU + 3x3/2 max-pool, fp32 images read
 //    through a device pointer table) and head (BN+ReLU+global avg-pool).
 //
@@ -604,20 +604,13 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
 // K9x: 3x3 conv 128 -> 32 (stride 1, pad 1) on the split bottleneck
 // ============================================================================
 constexpr int kC3 = 128, kTaps = 9;  // 32 output channels (growth) per conv
-constexpr int kTile3 = 128;            // output pixels per tile
-// ring row = [hi 128 bf16 | lo 128 bf16 | 8 pad]: 528 B = 132 dwords (== 4 mod
-// 64 banks: conflict-free b128 reads by consecutive pixels), the lo plane at a
-// constant +256 B (an immediate ds_read offset, no second address)
-constexpr int kRow3 = 2 * kC3 + 8;
 constexpr int kRing = 256;             // ring rows per plane (a band is 128 + 2(W+1) <= 242 rows)
 constexpr int kMaxW3 = 56;
-constexpr int kNew3 = kTile3 * (kC3 / 8) / 512;  // 16-B chunks per thread per plane of a tile's new rows: 4
-constexpr int kLds3 = (kRing + 1) * kRow3 * 2;  // ring + one zero row: 135,696 B
 
 struct X3Conv3x3Params {
   const uint16_t* z_hi;  // [M][128] bf16
   const uint16_t* z_lo;
-  const uint16_t* w_hi;  // [32][9][128] bf16 (tap-major K)
+  const uint16_t* w_hi;  // bf16 MFMA fragments [tap 9][kq 4][kc 2][lane 64][8] (x3_w3_fragments)
   const uint16_t* w_lo;
   float* y;              // [M][ldy] fp32, offset to the layer's 32-channel slice
   int ldy, M, H, W;
@@ -639,161 +632,6 @@ __device__ __forceinline__ int fast_divmod(int n, int d, uint32_t mag, int& rem)
   }
   rem = r;
   return q;
-}
-
-// 8 waves (2 per SIMD); wave w owns input channels [16w, 16w+16) of all nine
-// taps, so its hi/lo weight fragments are 18 x 16 B in registers for the
-// whole kernel.  A block walks a CONTIGUOUS run of 128-pixel tiles with the
-// activation band [m0-W-1, m0+128+W+1) of both planes in a 256-row LDS ring
-// (global row g lives in ring row (g + W + 1) & 255; row 256 is zeros, read
-// by out-of-image taps): after its first tile a block fetches only the 128
-// rows the next tile adds, into registers while the current tile's MFMAs
-// run.  The 8 partial tiles are summed through LDS in two rounds (waves 4-7
-// -> 0-3, then 4 slots -> all threads) in the ring rows only the current
-// tile reads, which are then overwritten by the prefetched rows.
-__global__ void __launch_bounds__(512, 1) x3_conv3x3_kernel(X3Conv3x3Params p) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t lds3[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int W = p.W, HW = p.H * p.W;
-  uint16_t* rh = lds3;        // [257][kRow3]: hi at +0, lo at +kC3
-  uint16_t* rl = lds3 + kC3;
-
-  const int h = lane >> 5, col = lane & 31;
-  const int ci = 16 * wave + 8 * h;
-  v4u wh[kTaps], wl[kTaps];
-#pragma unroll
-  for (int t = 0; t < kTaps; ++t) {
-    wh[t] = ld16(p.w_hi + (size_t)col * (kTaps * kC3) + t * kC3 + ci);
-    wl[t] = ld16(p.w_lo + (size_t)col * (kTaps * kC3) + t * kC3 + ci);
-  }
-
-  const int t_begin = blockIdx.x * p.tiles_per_block;
-  const int t_end = min(p.tiles, t_begin + p.tiles_per_block);
-  if (t_begin >= t_end) return;
-
-  auto ring = [&](int g) { return (g + W + 1) & (kRing - 1); };
-  // first band of the run: rows [m0-W-1, m0+128+W+1), loaded straight to LDS
-  {
-    const int m0 = t_begin * kTile3;
-    const int nch = (kTile3 + 2 * (W + 1)) * (kC3 / 8);
-    for (int e = tid; e < nch; e += 512) {
-      const int g = m0 - (W + 1) + (e >> 4);
-      const bool ok = g >= 0 && g < p.M;
-      const size_t off = (size_t)(ok ? g : 0) * kC3 + (e & 15) * 8;
-      const v4u vh = ok ? ld16(p.z_hi + off) : v4u{0, 0, 0, 0};
-      const v4u vl = ok ? ld16(p.z_lo + off) : v4u{0, 0, 0, 0};
-      const int lo = ring(g) * kRow3 + (e & 15) * 8;
-      *reinterpret_cast<v4u*>(&rh[lo]) = vh;
-      *reinterpret_cast<v4u*>(&rl[lo]) = vl;
-    }
-    if (tid < kC3 / 8) {  // the zero row read by out-of-image taps
-      *reinterpret_cast<v4u*>(&rh[kRing * kRow3 + tid * 8]) = v4u{0, 0, 0, 0};
-      *reinterpret_cast<v4u*>(&rl[kRing * kRow3 + tid * 8]) = v4u{0, 0, 0, 0};
-    }
-  }
-  __syncthreads();
-
-  v4u ph[kNew3], pl[kNew3];
-  for (int tile = t_begin; tile < t_end; ++tile) {
-    const int m0 = tile * kTile3;
-    const bool more = tile + 1 < t_end;
-    // the next tile's new rows [m0+128+W+1, m0+256+W+1)
-    const int g0 = m0 + kTile3 + W + 1;
-    if (more) {
-#pragma unroll
-      for (int i = 0; i < kNew3; ++i) {
-        const int e = tid + 512 * i;
-        const int g = g0 + (e >> 4);
-        const bool ok = g < p.M;
-        const size_t off = (size_t)(ok ? g : 0) * kC3 + (e & 15) * 8;
-        ph[i] = ok ? ld16(p.z_hi + off) : v4u{0, 0, 0, 0};
-        pl[i] = ok ? ld16(p.z_lo + off) : v4u{0, 0, 0, 0};
-      }
-    }
-    f32x16 acc[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[s][e] = 0.f;
-      const int m = m0 + 32 * s + col;
-      int r, xx;
-      (void)fast_divmod(m, HW, p.mag_hw, r);
-      const int yy = fast_divmod(r, W, p.mag_w, xx);
-      const bool in = m < p.M;
-      const bool up = in && yy > 0, dn = in && yy < p.H - 1, lf = xx > 0, rt = xx < W - 1;
-      const int base = m + W + 1;
-#pragma unroll
-      for (int t = 0; t < kTaps; ++t) {
-        const int dy = t / 3 - 1, dx = t % 3 - 1;
-        bool ok = dy < 0 ? up : (dy > 0 ? dn : in);
-        if (dx < 0) ok = ok && lf;
-        if (dx > 0) ok = ok && rt;
-        const int row = ok ? ((base + dy * W + dx) & (kRing - 1)) : kRing;
-        const uint16_t* q = &rh[row * kRow3 + ci];
-        acc[s] = x3_32(wh[t], wl[t], ld16(q), ld16(q + kC3), acc[s]);
-      }
-    }
-    __syncthreads();  // ring reads done
-    // scratch = the ring rows of global rows [m0-W-1, m0+127-W) (read by this
-    // tile only): pixel q's slot k (32 fp32 = 128 B) at byte 128k of ring row
-    // ring(m0-W-1+q)
-    auto slot = [&](int q, int k) {
-      return reinterpret_cast<float*>(rh + ring(m0 - W - 1 + q) * kRow3) + 32 * k;
-    };
-    // C layout (32x32): lane col = pixel, reg r -> channel (r&3) + 8*(r>>2) + 4*h
-    if (wave >= 4) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        float* q = slot(32 * s + col, wave - 4);
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<f32x4*>(q + 8 * g + 4 * h) =
-              f32x4{acc[s][4 * g], acc[s][4 * g + 1], acc[s][4 * g + 2], acc[s][4 * g + 3]};
-      }
-    }
-    __syncthreads();
-    if (wave < 4) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        float* q = slot(32 * s + col, wave);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          f32x4* d = reinterpret_cast<f32x4*>(q + 8 * g + 4 * h);
-          const f32x4 o = *d;
-          *d = f32x4{acc[s][4 * g] + o[0], acc[s][4 * g + 1] + o[1], acc[s][4 * g + 2] + o[2],
-                     acc[s][4 * g + 3] + o[3]};
-        }
-      }
-    }
-    __syncthreads();
-    {
-      const int px = tid >> 2, c0 = (tid & 3) * 8;
-      f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float* q = slot(px, k) + c0;
-        s0 += *reinterpret_cast<const f32x4*>(q);
-        s1 += *reinterpret_cast<const f32x4*>(q + 4);
-      }
-      const int m = m0 + px;
-      if (m < p.M) {
-        float* o = p.y + (size_t)m * p.ldy + c0;
-        *reinterpret_cast<f32x4*>(o) = s0;
-        *reinterpret_cast<f32x4*>(o + 4) = s1;
-      }
-    }
-    if (more) {
-      __syncthreads();  // scratch reads done before the new rows land on them
-#pragma unroll
-      for (int i = 0; i < kNew3; ++i) {
-        const int e = tid + 512 * i;
-        const int lo = ring(g0 + (e >> 4)) * kRow3 + (e & 15) * 8;
-        *reinterpret_cast<v4u*>(&rh[lo]) = ph[i];
-        *reinterpret_cast<v4u*>(&rl[lo]) = pl[i];
-      }
-      __syncthreads();
-    }
-  }
 }
 
 // ---- K9x (v2): 64-pixel tiles, LDS-DMA band ring, one-round reduction ------
@@ -831,12 +669,16 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p
   const int W = p.W, HW = p.H * p.W;
   const int col = lane & 31, h = lane >> 5;
 
+  // fragment-major weights: each load is the wave's 1 KB contiguous (lane
+  // (h, col) = w[col][t][32kq + 16kc + 8h ..+8]).  From the plain [32][9][128]
+  // layout every load touched 32 lines at 32 B each, and this prologue alone
+  // took ~9 us per block (the whole bs1 kernel was ~12 us).
   v4u wh[kTaps][2], wl[kTaps][2];
 #pragma unroll
   for (int t = 0; t < kTaps; ++t)
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
-      const size_t off = (size_t)col * (kTaps * kC3) + t * kC3 + 32 * kq + 16 * kc + 8 * h;
+      const size_t off = ((size_t)((t * 4 + kq) * 2 + kc) * 64 + lane) * 8;
       wh[t][kc] = ld16(p.w_hi + off);
       wl[t][kc] = ld16(p.w_lo + off);
     }
@@ -967,7 +809,7 @@ constexpr int kSHin = 224, kSHo = 56;
 
 struct X3StemParams {
   const float* const* srcs;  // per-image fp32 NCHW [3][224][224] (device pointer table)
-  const uint16_t* w_hi;      // [64][kSK] bf16 (BN0 scale folded)
+  const uint16_t* w_hi;      // [64][kSK] bf16 (BN0 scale folded), fragment-major (x3_stem_fragments)
   const uint16_t* w_lo;
   const float* bias;         // [64] BN0 shift
   float* y;                  // [imgs][56][56] pixels, rows of ldy fp32
@@ -1018,14 +860,15 @@ __device__ __forceinline__ void x3_stem_stage(uint16_t* Ih, uint16_t* Il, int ti
   }
 }
 
-// Wave (nh = channel half, mg = conv-row group)'s weight fragments.
+// Wave (nh = channel half, mg = conv-row group)'s weight fragments, from the
+// fragment-major copy (x3_stem_fragments: one load = the wave's 1 KB).
 __device__ __forceinline__ void x3_stem_weights(const X3StemParams& p, int lane, int nh, v4u (&wh)[kSK / 16],
                                                 v4u (&wl)[kSK / 16]) {
-  const size_t wrow = (size_t)(nh * 32 + (lane & 31)) * kSK + 8 * (lane >> 5);
 #pragma unroll
   for (int s = 0; s < kSK / 16; ++s) {
-    wh[s] = ld16(p.w_hi + wrow + s * 16);
-    wl[s] = ld16(p.w_lo + wrow + s * 16);
+    const size_t off = ((size_t)(nh * (kSK / 16) + s) * 64 + lane) * 8;
+    wh[s] = ld16(p.w_hi + off);
+    wl[s] = ld16(p.w_lo + off);
   }
 }
 
@@ -1421,25 +1264,15 @@ int tcamd_x3_conv3x3(const void* z_hi, const void* z_lo, int imgs, int H, int W,
   p.M = imgs * H * W;
   p.H = H;
   p.W = W;
-  p.tiles = (p.M + kTile3 - 1) / kTile3;
   p.mag_hw = (uint32_t)((0x100000000ull + H * W - 1) / (uint64_t)(H * W));
   p.mag_w = (uint32_t)((0x100000000ull + W - 1) / (uint64_t)W);
   if (p.M >= (1 << 24)) return hipErrorInvalidValue;  // fast_divmod range
   // one block (8 waves) per CU; each walks a contiguous run of tiles so the
   // halo rows its neighbour tile re-reads are still in this XCD's L2
-  // v2 (64-px tiles, LDS-DMA ring, one-round reduction) everywhere: in the
-  // bs128 forward (profiles/r2_x3_forward_b128_ws.md) it beats v1 at every
-  // size (56x56 104 vs 123 us, 28x28 33 vs 39, 14x14 ~17.5 vs 18.2, 7x7 13.8
-  // vs 14.8).  TCAMD_X3_K9=1 forces v1 (A/B runs).
-  static const int force = getenv("TCAMD_X3_K9") ? atoi(getenv("TCAMD_X3_K9")) : 0;
-  const bool v1 = force == 1;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e =
-        hipFuncSetAttribute((const void*)x3_conv3x3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kLds3);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kLdsV2);
+    hipError_t e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<0>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsV2);
     if (e == hipSuccess)
       e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<-1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               kLdsV2);
@@ -1448,19 +1281,12 @@ int tcamd_x3_conv3x3(const void* z_hi, const void* z_lo, int imgs, int H, int W,
   }
   static const int k9dbg = getenv("TCAMD_X3_K9_DBG") ? atoi(getenv("TCAMD_X3_K9_DBG")) : 0;
   p.dbg = k9dbg;
-  if (!v1) {
-    p.tiles = (p.M + kT2 - 1) / kT2;
-    const int grid = std::min(p.tiles, 256);
-    p.tiles_per_block = (p.tiles + grid - 1) / grid;
-    const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
-    if (p.dbg) hipLaunchKernelGGL(x3_conv3x3_v2_kernel<-1>, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
-    else hipLaunchKernelGGL(x3_conv3x3_v2_kernel<0>, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
-    return hipGetLastError();
-  }
+  p.tiles = (p.M + kT2 - 1) / kT2;
   const int grid = std::min(p.tiles, 256);
   p.tiles_per_block = (p.tiles + grid - 1) / grid;
   const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
-  hipLaunchKernelGGL(x3_conv3x3_kernel, dim3(blocks), dim3(512), kLds3, (hipStream_t)stream, p);
+  if (p.dbg) hipLaunchKernelGGL(x3_conv3x3_v2_kernel<-1>, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
+  else hipLaunchKernelGGL(x3_conv3x3_v2_kernel<0>, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
   return hipGetLastError();
 }
 

@@ -129,7 +129,7 @@ def test_x3_conv3x3(imgs, H):
     z = torch.relu(torch.randn(M, 128, device=DEV, generator=g))
     w = torch.randn(32, 128, 3, 3, device=DEV, generator=g) / (9 * 128) ** 0.5
     zh, zl = _split(z)
-    wh, wl = _split(w.permute(0, 2, 3, 1).reshape(32, -1))
+    wh, wl = (hip.x3_w3_fragments(t) for t in _split(w.permute(0, 2, 3, 1).reshape(32, -1)))
     ldy, off = 96, 32
     y = torch.full((M, ldy), 7.0, device=DEV)
     hip.x3_conv3x3(zh.data_ptr(), zl.data_ptr(), imgs, H, H, wh.data_ptr(), wl.data_ptr(), y.data_ptr() + 4 * off,
@@ -151,7 +151,7 @@ def test_x3_stem(imgs):
     bias = torch.randn(64, device=DEV, generator=g) * 0.1
     wp = torch.zeros(64, 7, 8, 4, device=DEV)
     wp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
-    wh, wl = _split(wp.reshape(64, -1))
+    wh, wl = (hip.x3_stem_fragments(t) for t in _split(wp.reshape(64, -1)))
     ptrs = torch.tensor([x[i].data_ptr() for i in range(imgs)], device=DEV, dtype=torch.int64)
     ldy = 96
     y = torch.full((imgs * 56 * 56, ldy), 7.0, device=DEV)

@@ -1,0 +1,27 @@
+"""Host-side weight layouts of the fp32-parity DenseNet kernels (CPU)."""
+import torch
+
+from triton_client_amd.ops import hip
+
+
+def test_x3_w3_fragments_matches_kernel_indexing():
+    """x3_conv3x3_v2_kernel loads wave (kq) lane (h, col) tap t half kc from
+    offset (((t*4 + kq)*2 + kc)*64 + h*32 + col)*8: that must be
+    w[col][t*128 + 32kq + 16kc + 8h .. +8] of the plain [32][9*128] layout."""
+    w = torch.arange(32 * 9 * 128, dtype=torch.int64).reshape(32, 9 * 128)
+    f = hip.x3_w3_fragments(w).reshape(-1)
+    t, kq, kc, h, col, e = torch.meshgrid(*(torch.arange(n) for n in (9, 4, 2, 2, 32, 8)), indexing="ij")
+    off = ((((t * 4 + kq) * 2 + kc) * 64 + h * 32 + col) * 8 + e).reshape(-1)
+    src = w[col.reshape(-1), (t * 128 + 32 * kq + 16 * kc + 8 * h + e).reshape(-1)]
+    assert torch.equal(f[off], src)
+    assert sorted(f.tolist()) == list(range(w.numel()))  # a permutation
+
+
+def test_x3_stem_fragments_matches_kernel_indexing():
+    """x3_stem_weights loads half nh, k-step s, lane (hh, jj) from offset
+    ((nh*14 + s)*64 + hh*32 + jj)*8: w[nh*32 + jj][16s + 8hh .. +8]."""
+    w = torch.arange(64 * 224, dtype=torch.int64).reshape(64, 224)
+    f = hip.x3_stem_fragments(w).reshape(-1)
+    nh, s, hh, jj, e = torch.meshgrid(*(torch.arange(n) for n in (2, 14, 2, 32, 8)), indexing="ij")
+    off = ((((nh * 14 + s) * 64) + hh * 32 + jj) * 8 + e).reshape(-1)
+    assert torch.equal(f[off], w[(nh * 32 + jj).reshape(-1), (16 * s + 8 * hh + e).reshape(-1)])

@@ -61,7 +61,8 @@ class FusedDenseNetFP32:
             # K10x layout: [64][kh 7][kw 8][ch 4], zero at kw 7 / ch 3
             w0p = torch.zeros(w0.shape[0], 7, 8, 4)
             w0p[:, :, :7, :3] = w0.permute(0, 2, 3, 1).cpu()
-            self.w0_hi, self.w0_lo = (t.to(dev) for t in split_bf16(w0p.reshape(w0.shape[0], -1)))
+            self.w0_hi, self.w0_lo = (hip.x3_stem_fragments(t).to(dev)
+                                      for t in split_bf16(w0p.reshape(w0.shape[0], -1)))
             self.b0 = b0.to(dev).contiguous()
             self.blocks, self.trans, self.block_dims = [], [], []
             hw, c = self.H0 // 4, INIT_FEATURES
@@ -78,7 +79,7 @@ class FusedDenseNetFP32:
                         "cin": cin, "s1": s1.to(dev), "t1": t1.to(dev),
                         "w1h": w1h.to(dev), "w1l": w1l.to(dev),
                         "b1": layer.conv1.bias.float().to(dev).contiguous(),
-                        "w2h": w2h.to(dev), "w2l": w2l.to(dev),
+                        "w2h": hip.x3_w3_fragments(w2h).to(dev), "w2l": hip.x3_w3_fragments(w2l).to(dev),
                     })
                 self.blocks.append(ls)
                 self.block_dims.append((hw, ctot))

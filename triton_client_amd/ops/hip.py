@@ -554,13 +554,29 @@ def x3_conv1x1(x, ldx, M, K, in_scale, in_bias, w_hi, w_lo, out_bias=None, z_hi=
                                     int(ws_bytes), _vp(stream)), "x3_conv1x1")
 
 
+def x3_w3_fragments(w):
+    """K9x weight layout: a [32][9*128] (out, tap-major K) tensor -> the MFMA
+    fragment-major copy the kernel loads, [tap 9][kq 4][kc 2][h 2][col 32][8]
+    (one wave's 16-B-per-lane fragment = 1 KB contiguous).  Apply it to the
+    hi and lo planes alike."""
+    return w.reshape(32, 9, 4, 2, 2, 8).permute(1, 2, 3, 4, 0, 5).contiguous().reshape(32, 9 * 128)
+
+
 def x3_conv3x3(z_hi, z_lo, imgs, H, W, w_hi, w_lo, y, ldy, stream=None):
-    """K9x fp32-parity 3x3 conv 128 -> 32 into fp32 rows of ``ldy``."""
+    """K9x fp32-parity 3x3 conv 128 -> 32 into fp32 rows of ``ldy``; ``w_hi`` /
+    ``w_lo`` in the x3_w3_fragments layout."""
     _check(_load().tcamd_x3_conv3x3(z_hi, z_lo, imgs, H, W, w_hi, w_lo, y, ldy, _vp(stream)), "x3_conv3x3")
 
 
+def x3_stem_fragments(w):
+    """K10x weight layout: [64][224] (out, (kh, kw[8], ch[4])) -> the MFMA
+    fragment-major copy the stem loads, [half 2][k-step 14][h 2][col 32][8]."""
+    return w.reshape(2, 32, 14, 2, 8).permute(0, 2, 3, 1, 4).contiguous().reshape(64, 224)
+
+
 def x3_stem(srcs, w_hi, w_lo, bias, y, imgs, ldy, stream=None):
-    """K10x fp32 stem from a device table of fp32 NCHW image pointers."""
+    """K10x fp32 stem from a device table of fp32 NCHW image pointers;
+    ``w_hi`` / ``w_lo`` in the x3_stem_fragments layout."""
     _check(_load().tcamd_x3_stem(srcs, w_hi, w_lo, bias, y, imgs, ldy, _vp(stream)), "x3_stem")
 
 
