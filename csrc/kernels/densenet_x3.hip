@@ -457,20 +457,27 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
       }
     };
     // prologue: X steps 0..PF-1, W steps 0..S-3, step 0 staged; then the
-    // steady-state issue of "iteration -1" (X step PF, W step S-2)
+    // steady-state issue of "iteration -1" (W step S-2, X step PF)
 #pragma unroll
     for (int s = 0; s < kWsPF; ++s) issue_x(s, s);
     for (int s = 0; s <= kWsS - 3; ++s) issue_w(s);
     __builtin_amdgcn_s_waitcnt(ws_vmcnt(0));
     write_x(0, 0);
-    issue_x(kWsPF, 0);
     issue_w(kWsS - 2);
+    __builtin_amdgcn_sched_barrier(0);
+    issue_x(kWsPF, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     ws_barrier();  // B0
-    // iteration q (consumers on step q): stage step q+1's X, refill its
-    // register slot with step q+1+PF, DMA W of step q+S-1, then wait for
-    // W of step q+1 (issued S-2 iterations ago: 10 younger ops per iteration:
-    // 6 X-slot loads, 4 W copies)
+    // iteration q (consumers on step q): stage step q+1's X, DMA W of step
+    // q+S-1, refill the X register slot with step q+1+PF, then wait for W of
+    // step q+1 before the barrier.  vmcnt retires in issue order, so the W
+    // copies go out BEFORE the X loads of their iteration: the W wait then
+    // only drains X steps up to q+1, and PF X steps stay in flight across
+    // the barrier (with X first, every W wait also drained the X loads
+    // issued beside it, which held the X stream to two steps in flight
+    // whatever PF was: 3.6 TB/s instead of the ~5.8 TB/s a plain persistent
+    // read of the same tiles reaches, profiles/r2_read_pattern_probe.log).
+    // 10 ops per iteration: 4 W copies, then 6 X-slot loads.
     // Qp steps (a multiple of PF: no early exit out of the unrolled body,
     // whose merge would make the compiler's own wait insertion drain vmcnt)
     for (int q0 = 0; q0 < Qp; q0 += kWsPF) {
@@ -478,13 +485,16 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
       for (int u = 0; u < kWsPF; ++u) {
         const int q = q0 + u;
         const int slot = (u + 1) % kWsPF;
-        // X of step q+1 was issued PF iterations back (4 + 10 (PF-1) younger ops)
-        __builtin_amdgcn_s_waitcnt(ws_vmcnt(4 + 10 * (kWsPF - 1)));
+        // X of step q+1 closed iteration q-PF: 10 (PF-1) younger ops
+        __builtin_amdgcn_s_waitcnt(ws_vmcnt(10 * (kWsPF - 1)));
         __builtin_amdgcn_sched_barrier(0);
         write_x(q + 1, slot);
-        issue_x(q + 1 + kWsPF, slot);
         issue_w(q + kWsS - 1);
-        __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0(20));
+        __builtin_amdgcn_sched_barrier(0);  // keep the W copies ahead of the X loads
+        issue_x(q + 1 + kWsPF, slot);
+        // W of step q+1 went out S-2 = 2 iterations back, ahead of that
+        // iteration's 6 X loads: 6 + 2 x 10 younger ops
+        __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0(6 + 10 * (kWsS - 2)));
         ws_barrier();  // B(q+1)
       }
     }
@@ -1205,7 +1215,8 @@ int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, int N, const float* 
       hipError_t e = hipGetDevice(&dev);
       if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
       for (const void* f : {(const void*)x3_conv1x1_ws_kernel<3, 0>, (const void*)x3_conv1x1_ws_kernel<5, 0>,
-                            (const void*)x3_conv1x1_ws_kernel<3, -1>})
+                            (const void*)x3_conv1x1_ws_kernel<6, 0>, (const void*)x3_conv1x1_ws_kernel<3, -1>,
+                            (const void*)x3_conv1x1_ws_kernel<5, -1>, (const void*)x3_conv1x1_ws_kernel<6, -1>})
         if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsWs);
       if (e != hipSuccess) return e;
     }
@@ -1222,9 +1233,17 @@ int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, int N, const float* 
     wp.tile_rows = (rpb + nt - 1) / nt;
     const int blocks = (units + wp.units_per_block - 1) / wp.units_per_block;
     static const int ws_pf = getenv("TCAMD_X3_WS_PF") ? atoi(getenv("TCAMD_X3_WS_PF")) : 3;
-    if (wp.dbg) hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, -1>), dim3(blocks), dim3(512), kLdsWs, s, wp);
-    else if (ws_pf == 5) hipLaunchKernelGGL((x3_conv1x1_ws_kernel<5, 0>), dim3(blocks), dim3(512), kLdsWs, s, wp);
-    else hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, 0>), dim3(blocks), dim3(512), kLdsWs, s, wp);
+    if (wp.dbg) {
+      if (ws_pf == 5) hipLaunchKernelGGL((x3_conv1x1_ws_kernel<5, -1>), dim3(blocks), dim3(512), kLdsWs, s, wp);
+      else if (ws_pf == 6) hipLaunchKernelGGL((x3_conv1x1_ws_kernel<6, -1>), dim3(blocks), dim3(512), kLdsWs, s, wp);
+      else hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, -1>), dim3(blocks), dim3(512), kLdsWs, s, wp);
+    } else if (ws_pf == 5) {
+      hipLaunchKernelGGL((x3_conv1x1_ws_kernel<5, 0>), dim3(blocks), dim3(512), kLdsWs, s, wp);
+    } else if (ws_pf == 6) {
+      hipLaunchKernelGGL((x3_conv1x1_ws_kernel<6, 0>), dim3(blocks), dim3(512), kLdsWs, s, wp);
+    } else {
+      hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, 0>), dim3(blocks), dim3(512), kLdsWs, s, wp);
+    }
     return hipGetLastError();
   }
   static const int xg = getenv("TCAMD_X3_XCD_GROUP") ? atoi(getenv("TCAMD_X3_XCD_GROUP")) : 1;

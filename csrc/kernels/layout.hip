@@ -6,7 +6,7 @@
 //
 //   y[n, ...] = x_n[...] * scale[c] + bias[c],  x_n from its own pointer
 //
-// Layouts: NCHW <-> NHWC.  Source dtypes: FP32 / UINT8 / BF16 / FP16; dest:
+// Layouts: NCHW <-> NHWC (or the same layout: convert + affine only).  Source dtypes: FP32 / UINT8 / BF16 / FP16; dest:
 // FP32 / BF16 / FP16.  Up to 64 images per launch (pointer table passed by
 // value, so there is no H2D copy of descriptors per call).
 //
@@ -189,6 +189,23 @@ __global__ void __launch_bounds__(kBlock) tiled_transpose(LayoutParams p, void* 
   }
 }
 
+// ---- same layout (NCHW -> NCHW, NHWC -> NHWC): convert + per-channel affine ----
+// one element per thread-iteration over the gathered batch; the channel of a
+// flat index is (i / HW) % C for NCHW and i % C for NHWC
+template <int SRC, int DST, bool CHW>
+__global__ void __launch_bounds__(kBlock) same_layout(LayoutParams p, void* __restrict__ dst) {
+  const uint64_t per_img = (uint64_t)p.C * p.HW;
+  const uint64_t total = per_img * p.n_imgs;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const uint64_t n = i / per_img, e = i - n * per_img;
+    const int c = CHW ? (int)(e / p.HW) : (int)(e % p.C);
+    float f = ld<SRC>(p.src[n], e);
+    if (p.affine) f = f * p.scale[c] + p.bias[c];
+    st<DST>(dst, i, f, p.rne);
+  }
+}
+
 template <int SRC, int DST>
 int dispatch_dst(const LayoutParams& p, int src_layout, int dst_layout, void* dst, hipStream_t s) {
   const int C = p.C, HW = p.HW;
@@ -227,6 +244,10 @@ int dispatch_dst(const LayoutParams& p, int src_layout, int dst_layout, void* ds
       dim3 g(tk < 64 ? tk : 64, tr, p.n_imgs);
       hipLaunchKernelGGL((tiled_transpose<SRC, DST, false>), g, dim3(kBlock), 0, s, p, dst, HW, C);
     }
+  } else if (src_layout == dst_layout) {
+    dim3 g(grid_for((uint64_t)C * HW * p.n_imgs));
+    if (src_layout == 0) hipLaunchKernelGGL((same_layout<SRC, DST, true>), g, dim3(kBlock), 0, s, p, dst);
+    else hipLaunchKernelGGL((same_layout<SRC, DST, false>), g, dim3(kBlock), 0, s, p, dst);
   } else {
     return hipErrorInvalidValue;
   }

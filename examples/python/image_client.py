@@ -106,6 +106,8 @@ def main():
     ap.add_argument("-s", "--scaling", choices=["NONE", "INCEPTION", "VGG"], default="NONE")
     ap.add_argument("-u", "--url", default=None)
     ap.add_argument("-i", "--protocol", default="HTTP", choices=["HTTP", "gRPC", "http", "grpc"])
+    ap.add_argument("--device-preprocess", action="store_true",
+                    help="scale/transpose/convert on the GPU with the K6 layout_pack kernel (FP32/FP16 models)")
     ap.add_argument("image_filename")
     a = ap.parse_args()
     protocol = a.protocol.lower()
@@ -130,7 +132,21 @@ def main():
         files = sorted(os.path.join(a.image_filename, f) for f in os.listdir(a.image_filename))
     else:
         files = [a.image_filename]
-    images = [preprocess(load_image(f), fmt, dtype, c, h, w, a.scaling) for f in files]
+    images = None
+    if a.device_preprocess:
+        from triton_client_amd.utils.image import preprocess_batch_device, resize_bilinear
+
+        resized = []
+        for f in files:
+            img = load_image(f)
+            if c == 1:
+                img = img.mean(axis=2, keepdims=True)
+            resized.append(resize_bilinear(img.astype(np.float32), h, w))
+        packed = preprocess_batch_device(resized, a.scaling, fmt, dtype)
+        if packed is not None:
+            images = list(packed)
+    if images is None:
+        images = [preprocess(load_image(f), fmt, dtype, c, h, w, a.scaling) for f in files]
     # batches (cycling over the images to fill the last batch)
     requests, batched_names = [], []
     idx = 0

@@ -35,7 +35,7 @@ def test_cudashm_examples(gpu_server, script, proto):
 
 
 @pytest.mark.parametrize("proto,extra", [("http", []), ("grpc", ["-a"]), ("grpc", ["--streaming"]),
-                                         ("http", ["-a", "-b", "2"])])
+                                         ("http", ["-a", "-b", "2"]), ("http", ["--device-preprocess", "-b", "2"])])
 def test_image_client(gpu_server, image_dir, proto, extra):
     url = gpu_server.http_url if proto == "http" else gpu_server.grpc_url
     r = run_example("image_client.py", url, ["-m", "densenet_onnx", "-s", "INCEPTION", "-c", "3", "-i", proto]

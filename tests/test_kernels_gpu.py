@@ -283,3 +283,20 @@ def test_index_bytes_detects_malformed(env):
     status = torch.zeros(4, device="cuda", dtype=torch.int32)
     hip.index_bytes(buf.data_ptr(), 6, 1, offs.data_ptr(), lns.data_ptr(), status.data_ptr(), _stream(torch))
     assert int(status[0]) == -1
+
+
+@pytest.mark.parametrize("scaling", ["NONE", "INCEPTION", "VGG"])
+@pytest.mark.parametrize("fmt", ["NCHW", "NHWC"])
+@pytest.mark.parametrize("dtype", ["FP32", "FP16"])
+def test_image_preprocess_on_device_matches_host(env, scaling, fmt, dtype):
+    """K6 as image_client's device preprocessing vs the numpy path it replaces."""
+    from triton_client_amd.utils.image import preprocess, preprocess_batch_device, resize_bilinear
+
+    rng = np.random.default_rng(3)
+    raw = [rng.integers(0, 256, size=(37 + 5 * i, 41, 3), dtype=np.uint8) for i in range(3)]
+    npdt = np.float32 if dtype == "FP32" else np.float16
+    want = np.stack([preprocess(r, 3, 32, 48, scaling, fmt, npdt) for r in raw])
+    got = preprocess_batch_device([resize_bilinear(r, 32, 48) for r in raw], scaling, fmt, dtype)
+    assert got.shape == want.shape and got.dtype == want.dtype
+    tol = 1e-5 if dtype == "FP32" else 2e-3
+    np.testing.assert_allclose(got.astype(np.float32), want.astype(np.float32), rtol=tol, atol=tol * 128)

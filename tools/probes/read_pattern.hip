@@ -67,6 +67,41 @@ __global__ void __launch_bounds__(256) probe(const float* __restrict__ x, float*
   if (acc[0] == 1234.5f) out[blockIdx.x * 256 + t] = acc[1] + acc[2] + acc[3];
 }
 
+// D/E: 256 persistent blocks (one per CU, like x3_conv1x1_ws_kernel's producers):
+//   D  each block walks a contiguous run of tiles (the ws kernel's assignment);
+//   E  tiles dealt round-robin (tile = block + i * grid).
+template <int MODE>
+__global__ void __launch_bounds__(256) probe_persist(const float* __restrict__ x, float* __restrict__ out, int M,
+                                                     int ldx, int K, int tiles) {
+  const int t = threadIdx.x;
+  f32x4 acc = {0, 0, 0, 0};
+  const int nst = K / 32;
+  const int per = (tiles + gridDim.x - 1) / gridDim.x;
+  const int rot = blockIdx.x % nst;
+  for (int i = 0; i < per; ++i) {
+    const int tile = MODE == 0 ? blockIdx.x * per + i : blockIdx.x + i * gridDim.x;
+    if (tile >= tiles) break;
+    const int m0 = tile * 128;
+    for (int s0 = 0; s0 < nst; s0 += PF) {
+      f32x4 v[PF][4];
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        int s = min(s0 + u, nst - 1) + rot;
+        if (s >= nst) s -= nst;
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2)
+          v[u][i2] = __builtin_nontemporal_load(
+              reinterpret_cast<const f32x4*>(x + (size_t)(m0 + (t >> 3) + 32 * i2) * ldx + 32 * s + 4 * (t & 7)));
+      }
+#pragma unroll
+      for (int u = 0; u < PF; ++u)
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2) acc += v[u][i2];
+    }
+  }
+  if (acc[0] == 1234.5f) out[blockIdx.x * 256 + t] = acc[1] + acc[2] + acc[3];
+}
+
 // C: whole rows, contiguous sweep of the tile (K == ldx)
 __global__ void __launch_bounds__(256) probe_sweep(const float* __restrict__ x, float* __restrict__ out, int M,
                                                    int ldx, int K, int tiles_per_block) {
@@ -109,8 +144,8 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const int Ks[] = {64, 128, 256};
-  const int tpbs[] = {1, 2, 4, 6};
+  const int Ks[] = {256};
+  const int tpbs[] = {1, 6};
   for (int K : Ks)
     for (int tpb : tpbs)
       for (int mode = 0; mode < 3; ++mode) {
@@ -134,6 +169,27 @@ int main(int argc, char** argv) {
         const double rd = (double)M * K * 4;
         printf("mode %c K %3d tiles/block %d grid %5d: %7.1f us  %.2f TB/s\n", "ABC"[mode], K, tpb, grid, us,
                rd / us / 1e6);
+        fflush(stdout);
+      }
+  for (int K : {128, 224, 256})
+    for (int grid : {256, 512, 1024})
+      for (int mode = 0; mode < 2; ++mode) {
+        auto launch = [&]() {
+          if (mode == 0) probe_persist<0><<<grid, 256>>>(x, out, M, ldx, K, tiles);
+          else probe_persist<1><<<grid, 256>>>(x, out, M, ldx, K, tiles);
+        };
+        for (int w = 0; w < 3; ++w) launch();
+        CK(hipDeviceSynchronize());
+        const int reps = 20;
+        CK(hipEventRecord(e0));
+        for (int r = 0; r < reps; ++r) launch();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        const double us = 1000.0 * ms / reps;
+        printf("persistent %s K %3d grid %4d: %7.1f us  %.2f TB/s\n", mode ? "round-robin" : "contiguous ", K, grid,
+               us, (double)M * K * 4 / us / 1e6);
         fflush(stdout);
       }
   CK(hipFree(x));

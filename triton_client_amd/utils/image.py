@@ -88,3 +88,42 @@ def preprocess(img, c, h, w, scaling="INCEPTION", fmt="NCHW", dtype=np.float32):
 
 def inception_preprocess(img, h, w, fmt="NCHW"):
     return preprocess(img, 3, h, w, "INCEPTION", fmt)
+
+
+_SCALE_BIAS = {
+    "NONE": lambda c: ([1.0] * c, [0.0] * c),
+    "INCEPTION": lambda c: ([1.0 / 127.5] * c, [-1.0] * c),
+    "VGG": lambda c: ([1.0] * c, [-m for m in ([123.0, 117.0, 104.0] if c == 3 else [128.0])]),
+}
+_DEVICE_DTYPES = {"FP32": np.float32, "FP16": np.float16}
+
+
+def preprocess_batch_device(resized, scaling="INCEPTION", fmt="NCHW", dtype="FP32", device=0):
+    """Scale + HWC->CHW transpose + dtype convert of a batch of resized HWC
+    fp32 images in ONE K6 ``layout_pack`` launch on the GPU (LDS-tiled
+    transpose; replaces the numpy scale/transpose of ``preprocess``, reference
+    src/python/examples/image_client.py:154-194 and
+    src/c++/examples/image_client.cc:86-188).  The images are uploaded once as
+    a host->device copy, the packed [n, C, H, W] (or [n, H, W, C]) batch comes
+    back as numpy.  ``dtype`` is the model's Triton datatype (FP32 or FP16).
+    Returns None when the datatype has no device path (integer models)."""
+    if dtype not in _DEVICE_DTYPES:
+        return None
+    import torch
+
+    from triton_client_amd.ops import hip
+
+    imgs = [np.ascontiguousarray(r, dtype=np.float32) for r in resized]
+    h, w, c = imgs[0].shape
+    dev = torch.device("cuda", device)
+    src = torch.from_numpy(np.stack(imgs, axis=0)).to(dev, non_blocking=False)
+    shape = (len(imgs), c, h, w) if fmt == "NCHW" else (len(imgs), h, w, c)
+    dst = torch.empty(shape, device=dev, dtype=torch.float32 if dtype == "FP32" else torch.float16)
+    scale, bias = _SCALE_BIAS[scaling](c)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    per = c * h * w * dst.element_size()
+    for i0 in range(0, len(imgs), 64):  # K6 takes up to 64 source pointers per launch
+        n = min(64, len(imgs) - i0)
+        hip.layout_pack([src[i].data_ptr() for i in range(i0, i0 + n)], "FP32", "NHWC", dst.data_ptr() + i0 * per,
+                        dtype, fmt, c, h, w, scale=scale, bias=bias, stream=stream)
+    return dst.cpu().numpy()
