@@ -6,8 +6,11 @@
 // batching), NONE/INCEPTION/VGG scaling, -b batching, sync / async (-a) /
 // gRPC streaming (--streaming) requests, top-k classification postprocess.
 #include <dirent.h>
+#include <dlfcn.h>
 #include <getopt.h>
+#include <hip/hip_runtime_api.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
@@ -98,6 +101,81 @@ static std::vector<uint8_t> Preprocess(const Image& img, const ModelInfo& m, Sca
   return bytes;
 }
 
+// --device-preprocess: the same resize on the host (no scaling, HWC fp32),
+// then scale + HWC->CHW/HWC + FP32 for the whole batch in ONE launch of the
+// framework's K6 layout_pack kernel (libtcamd_hip.so, found next to this
+// build tree or via $TCAMD_HIP_LIB; hipMemcpy in and out).
+typedef int (*LayoutPackFn)(const void* const*, int, int, int, void*, int, int, int, int, int, const float*,
+                            const float*, int, void*);
+
+static LayoutPackFn LoadLayoutPack()
+{
+  std::vector<std::string> cands;
+  if (const char* env = getenv("TCAMD_HIP_LIB")) cands.push_back(env);
+  char self[4096];
+  const ssize_t n = readlink("/proc/self/exe", self, sizeof(self) - 1);
+  if (n > 0) {
+    std::string p(self, n);
+    cands.push_back(p.substr(0, p.rfind('/')) + "/../../../../triton_client_amd/ops/lib/libtcamd_hip.so");
+  }
+  for (const auto& c : cands)
+    if (void* h = dlopen(c.c_str(), RTLD_NOW | RTLD_GLOBAL))
+      if (void* f = dlsym(h, "tcamd_layout_pack")) return reinterpret_cast<LayoutPackFn>(f);
+  return nullptr;
+}
+
+static std::vector<std::vector<uint8_t>> PreprocessOnDevice(const std::vector<Image>& imgs, const ModelInfo& m,
+                                                            Scale scale)
+{
+  static LayoutPackFn pack = LoadLayoutPack();
+  if (!pack) {
+    std::cerr << "error: --device-preprocess needs tcamd_layout_pack (libtcamd_hip.so)" << std::endl;
+    exit(1);
+  }
+  ModelInfo hwc = m;
+  hwc.nchw = false;
+  const size_t per = static_cast<size_t>(m.c) * m.h * m.w;
+  std::vector<float> scl(m.c, 1.f), bias(m.c, 0.f);
+  for (int ch = 0; ch < m.c; ++ch) {
+    if (scale == Scale::INCEPTION) {
+      scl[ch] = 1.f / 127.5f;
+      bias[ch] = -1.f;
+    } else if (scale == Scale::VGG) {
+      bias[ch] = -(m.c == 3 ? (ch == 0 ? 123.f : ch == 1 ? 117.f : 104.f) : 128.f);
+    }
+  }
+  std::vector<std::vector<uint8_t>> out;
+  for (size_t i0 = 0; i0 < imgs.size(); i0 += 64) {  // K6 takes up to 64 source pointers per launch
+    const size_t cnt = std::min<size_t>(64, imgs.size() - i0);
+    std::vector<uint8_t> host(cnt * per * 4);
+    for (size_t i = 0; i < cnt; ++i) {
+      const std::vector<uint8_t> r = Preprocess(imgs[i0 + i], hwc, Scale::NONE);
+      memcpy(host.data() + i * per * 4, r.data(), r.size());
+    }
+    void *src = nullptr, *dst = nullptr;
+    if (hipMalloc(&src, host.size()) != hipSuccess || hipMalloc(&dst, host.size()) != hipSuccess ||
+        hipMemcpy(src, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess) {
+      std::cerr << "error: device buffers for --device-preprocess" << std::endl;
+      exit(1);
+    }
+    std::vector<const void*> ptrs(cnt);
+    for (size_t i = 0; i < cnt; ++i) ptrs[i] = static_cast<const uint8_t*>(src) + i * per * 4;
+    const int kFp32 = 10, kNchw = 0, kNhwc = 1;
+    int rc = pack(ptrs.data(), static_cast<int>(cnt), kFp32, kNhwc, dst, kFp32, m.nchw ? kNchw : kNhwc, m.c, m.h,
+                  m.w, scl.data(), bias.data(), 1, nullptr);
+    if (rc == 0) rc = hipMemcpy(host.data(), dst, host.size(), hipMemcpyDeviceToHost);
+    (void)hipFree(src);
+    (void)hipFree(dst);
+    if (rc != 0) {
+      std::cerr << "error: layout_pack failed (" << rc << ")" << std::endl;
+      exit(1);
+    }
+    for (size_t i = 0; i < cnt; ++i)
+      out.emplace_back(host.begin() + i * per * 4, host.begin() + (i + 1) * per * 4);
+  }
+  return out;
+}
+
 static void ParseDims(const std::vector<int64_t>& shape, const std::string& fmt, ModelInfo* m)
 {
   std::vector<int64_t> dims(shape.begin() + (m->max_batch > 0 ? 1 : 0), shape.end());
@@ -183,15 +261,18 @@ static void Postprocess(tc::InferResult* r, const std::string& out, const std::v
 
 int main(int argc, char** argv)
 {
-  bool verbose = false, async = false, streaming = false;
+  bool verbose = false, async = false, streaming = false, device_pre = false;
   int batch = 1, topk = 1;
   Scale scale = Scale::NONE;
   std::string model, version, url, protocol = "http";
-  static struct option long_opts[] = {{"streaming", no_argument, nullptr, 0}, {nullptr, 0, nullptr, 0}};
+  static struct option long_opts[] = {{"streaming", no_argument, nullptr, 0},
+                                      {"device-preprocess", no_argument, nullptr, 1},
+                                      {nullptr, 0, nullptr, 0}};
   int opt;
   while ((opt = getopt_long(argc, argv, "vam:x:b:c:s:u:i:", long_opts, nullptr)) != -1) {
     switch (opt) {
       case 0: streaming = true; break;
+      case 1: device_pre = true; break;
       case 'v': verbose = true; break;
       case 'a': async = true; break;
       case 'm': model = optarg; break;
@@ -207,7 +288,7 @@ int main(int argc, char** argv)
       case 'i': protocol = optarg; break;
       default:
         example::Usage(argv, "\t-m <model> -x <version> -b <batch> -c <classes> -s <NONE|INCEPTION|VGG>\n"
-                             "\t-i <http|grpc> -a (async) --streaming <image file or dir>");
+                             "\t-i <http|grpc> -a (async) --streaming --device-preprocess <image file or dir>");
     }
   }
   for (auto& ch : protocol) ch = static_cast<char>(tolower(ch));
@@ -249,14 +330,17 @@ int main(int argc, char** argv)
     exit(1);
   }
   std::vector<std::vector<uint8_t>> images;
+  std::vector<Image> decoded;
   for (const auto& f : files) {
     Image img;
     if (!ReadPnm(f, &img)) {
       std::cerr << "error: unable to decode '" << f << "' (binary PPM/PGM expected)" << std::endl;
       exit(1);
     }
-    images.push_back(Preprocess(img, m, scale));
+    if (device_pre) decoded.push_back(std::move(img));
+    else images.push_back(Preprocess(img, m, scale));
   }
+  if (device_pre) images = PreprocessOnDevice(decoded, m, scale);
   // requests of `batch` images, cycling over the list to fill the last batch
   struct Req {
     std::unique_ptr<tc::InferInput> in;

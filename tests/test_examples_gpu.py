@@ -68,7 +68,8 @@ def test_cpp_cudashm_examples(gpu_server, name, proto):
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]
 
 
-@pytest.mark.parametrize("proto,extra", [("http", []), ("grpc", ["-a"]), ("grpc", ["--streaming", "-b", "2"])])
+@pytest.mark.parametrize("proto,extra", [("http", []), ("grpc", ["-a"]), ("grpc", ["--streaming", "-b", "2"]),
+                                         ("http", ["--device-preprocess", "-b", "2"])])
 def test_cpp_image_client(gpu_server, image_dir, proto, extra):
     from tests.test_cpp_examples import run_bin
 
@@ -109,3 +110,24 @@ def test_perf_analyzer_hip_shm_with_gpu_metrics(gpu_server, tmp_path):
     assert "gpu" in pt, r.stdout[-1500:]
     # the card under test (matched to HIP device 0 by PCI address) holds the server's weights and graphs
     assert pt["gpu"]["util_pct"] >= 0 and pt["gpu"]["mem_mib"] > 100
+
+
+@pytest.mark.parametrize("scaling", ["INCEPTION", "VGG"])
+def test_device_preprocess_gives_host_results(gpu_server, image_dir, scaling):
+    """K6 device preprocessing (Python and C++ image_client) classifies every
+    image exactly like the host preprocessing path."""
+    from tests.test_cpp_examples import run_bin
+
+    args = ["-m", "densenet_onnx", "-s", scaling, "-c", "3", "-i", "grpc"]
+    outs = [run_example("image_client.py", gpu_server.grpc_url, args + extra + [image_dir], timeout=300)
+            for extra in ([], ["--device-preprocess"])]
+    outs += [run_bin("image_client", gpu_server.grpc_url, args + extra + [image_dir], timeout=300)
+             for extra in ([], ["--device-preprocess"])]
+    for r in outs:
+        assert r.returncode == 0 and "PASS" in r.stdout, r.stdout[-1500:] + r.stderr[-1500:]
+    # result lines are "<score> (<class index>) = <label>": scores may differ in
+    # the last digits (x * (1/127.5) on device vs x / 127.5 on the host)
+    classes = [[ln.split("(")[1].split(")")[0] for ln in r.stdout.splitlines() if "(" in ln and ") =" in ln]
+               for r in outs]
+    assert classes[0] and classes[0] == classes[1], (classes[0], classes[1])
+    assert classes[2] and classes[2] == classes[3], (classes[2], classes[3])
