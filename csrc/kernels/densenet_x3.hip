@@ -626,6 +626,11 @@ struct X3Conv3x3Params {
   int ldy, M, H, W;
   int tiles, tiles_per_block;
   int dbg;  // v2 ablation (TCAMD_X3_K9_DBG): 1 no MFMA, 2 no partial exchange, 4 no operand reads
+  // PART kernels: the band comes from the preceding 1x1's split-K partials
+  // [splits][M][128] fp32 (z = relu(sum + bias), split hi/lo while staged)
+  const float* part;
+  const float* part_bias;
+  int splits;
   uint32_t mag_hw, mag_w;  // ceil(2^32 / (H*W)), ceil(2^32 / W): division by multiply-high
 };
 
@@ -668,8 +673,13 @@ constexpr int kRowB = 2 * kC3 * 2;          // 512 B per ring row
 constexpr int kScrSlot = 32 * 8;            // floats per (group, ph, source) slot: 32 px x 8 channels
 constexpr int kLdsV2 = (kRing + 1) * kRowB + 4 * 2 * 3 * kScrSlot * 4;  // 131,584 + 24,576 B
 
-// DBG: 0 = production; -1 = ablation flags read from p.dbg (tools/gpu_x3_k9abl.sh)
-template <int DBG>
+// DBG: 0 = production; -1 = ablation flags read from p.dbg (tools/gpu_x3_k9abl.sh).
+// PART: small-M layers (bs1/bs8 at 14x14 and below, bs1 everywhere) whose
+// 1x1 ran split-K: the band is summed from the fp32 partials, bias+ReLU'd
+// and split while it is staged, which replaces the split-K reduce launch
+// (one ~5 us launch per such layer, 28% of a bs1 forward).  Those layers have
+// one or two tiles per block, so the synchronous staging costs no overlap.
+template <int DBG, bool PART = false>
 __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p) {
   const int dbg = DBG < 0 ? p.dbg : DBG;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds2[];
@@ -701,6 +711,56 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p
   const ptrdiff_t lo_off = p.z_lo - p.z_hi;
   // rows [g0, g0+nrows) -> ring, two rows per wave-instruction (ring row of g0 even)
   auto dma_rows = [&](int g0, int nrows) {
+    if constexpr (PART) {
+      // (row, 8-channel chunk) items, three per thread per pass so that the
+      // 6 x splits partial loads of a pass are in flight together; chunk c of
+      // ring row pos lands in slot c ^ (pos & 15) of both planes, as the DMA
+      // places it
+      const int n = nrows * 16;
+      const size_t sstride = (size_t)p.M * kC3;
+      for (int i0 = tid; i0 < n; i0 += 3 * 512) {
+        f32x4 a[3][2];
+        const float* q[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int it = min(i0 + 512 * j, n - 1);
+          const int g = g0 + (it >> 4), c = it & 15;
+          q[j] = p.part + (size_t)min(max(g, 0), p.M - 1) * kC3 + 8 * c;
+          a[j][0] = ldf4(p.part_bias + 8 * c);
+          a[j][1] = ldf4(p.part_bias + 8 * c + 4);
+        }
+#pragma unroll 4
+        for (int sp = 0; sp < p.splits; ++sp) {
+          f32x4 v[3][2];
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            v[j][0] = ldf4(q[j] + sp * sstride);
+            v[j][1] = ldf4(q[j] + sp * sstride + 4);
+          }
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            a[j][0] += v[j][0];
+            a[j][1] += v[j][1];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int it = i0 + 512 * j;
+          if (it >= n) break;
+          const int g = g0 + (it >> 4), c = it & 15;
+          const int pos = (g + W + 1) & (kRing - 1);
+          uint32_t h0, l0, h1, l1, h2, l2, h3, l3;
+          split2(fmaxf(a[j][0][0], 0.f), fmaxf(a[j][0][1], 0.f), h0, l0);
+          split2(fmaxf(a[j][0][2], 0.f), fmaxf(a[j][0][3], 0.f), h1, l1);
+          split2(fmaxf(a[j][1][0], 0.f), fmaxf(a[j][1][1], 0.f), h2, l2);
+          split2(fmaxf(a[j][1][2], 0.f), fmaxf(a[j][1][3], 0.f), h3, l3);
+          uint8_t* rp = lds2 + pos * kRowB + ((c ^ (pos & 15)) << 4);
+          *reinterpret_cast<v4u*>(rp) = v4u{h0, h1, h2, h3};
+          *reinterpret_cast<v4u*>(rp + 256) = v4u{l0, l1, l2, l3};
+        }
+      }
+      return;
+    }
     const int plane = (lane >> 4) & 1, j = lane & 15;
     for (int pr = wave; 2 * pr < nrows; pr += 8) {
       const int ga = g0 + 2 * pr;
@@ -1150,6 +1210,67 @@ void launch_x3_1x1(const X3Plan& pl, const dim3& g, hipStream_t s, const X3Conv1
 }
 }  // namespace
 
+static int x3_conv1x1_impl(const float* x, int ldx, int M, int K, int N, const float* in_scale, const float* in_bias,
+                           const void* w_hi, const void* w_lo, const float* out_bias, void* z_hi, void* z_lo,
+                           float* y, int ldy, int pool, int H, int W, float* ws, size_t ws_bytes, void* stream,
+                           int* defer_splits);
+
+// part != null: the band comes from `splits` fp32 split-K partials [splits][M][128]
+// plus part_bias (z_hi/z_lo unused)
+static int x3_conv3x3_launch(const void* z_hi, const void* z_lo, const float* part, const float* part_bias, int splits,
+                             int imgs, int H, int W, const void* w_hi, const void* w_lo, float* y, int ldy,
+                             void* stream) {
+  if (imgs <= 0) return hipSuccess;
+  if (W > kMaxW3 || W < 1 || H < 1 || ldy % 4 || !w_hi || !w_lo || !y) return hipErrorInvalidValue;
+  if (part ? (!part_bias || splits < 1 || !aligned16(part) || !aligned16(part_bias))
+           : (!z_hi || !z_lo || !aligned16(z_hi) || !aligned16(z_lo)))
+    return hipErrorInvalidValue;
+  if (!aligned16(w_hi) || !aligned16(w_lo) || !aligned16(y)) return hipErrorInvalidValue;
+  X3Conv3x3Params p;
+  p.z_hi = (const uint16_t*)z_hi;
+  p.z_lo = (const uint16_t*)z_lo;
+  p.w_hi = (const uint16_t*)w_hi;
+  p.w_lo = (const uint16_t*)w_lo;
+  p.part = part;
+  p.part_bias = part_bias;
+  p.splits = splits;
+  p.y = y;
+  p.ldy = ldy;
+  p.M = imgs * H * W;
+  p.H = H;
+  p.W = W;
+  p.mag_hw = (uint32_t)((0x100000000ull + H * W - 1) / (uint64_t)(H * W));
+  p.mag_w = (uint32_t)((0x100000000ull + W - 1) / (uint64_t)W);
+  if (p.M >= (1 << 24)) return hipErrorInvalidValue;  // fast_divmod range
+  // one block (8 waves) per CU; each walks a contiguous run of tiles so the
+  // halo rows its neighbour tile re-reads are still in this XCD's L2
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<0>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsV2);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<-1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kLdsV2);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kLdsV2);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  static const int k9dbg = getenv("TCAMD_X3_K9_DBG") ? atoi(getenv("TCAMD_X3_K9_DBG")) : 0;
+  p.dbg = k9dbg;
+  p.tiles = (p.M + kT2 - 1) / kT2;
+  const int grid = std::min(p.tiles, 256);
+  p.tiles_per_block = (p.tiles + grid - 1) / grid;
+  const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
+  if (part)
+    hipLaunchKernelGGL((x3_conv3x3_v2_kernel<0, true>), dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
+  else if (p.dbg)
+    hipLaunchKernelGGL(x3_conv3x3_v2_kernel<-1>, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
+  else hipLaunchKernelGGL(x3_conv3x3_v2_kernel<0>, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
+  return hipGetLastError();
+}
+
 extern "C" {
 
 // Split-K workspace bytes the 1x1 conv wants for an M x K -> N problem (0 = none).
@@ -1165,6 +1286,20 @@ size_t tcamd_x3_conv1x1_ws_bytes(int M, int K, int N) {
 int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, int N, const float* in_scale, const float* in_bias,
                      const void* w_hi, const void* w_lo, const float* out_bias, void* z_hi, void* z_lo, float* y,
                      int ldy, int pool, int H, int W, float* ws, size_t ws_bytes, void* stream) {
+  return x3_conv1x1_impl(x, ldx, M, K, N, in_scale, in_bias, w_hi, w_lo, out_bias, z_hi, z_lo, y, ldy, pool, H, W,
+                         ws, ws_bytes, stream, nullptr);
+}
+
+}  // extern "C"
+
+// The 1x1 of the host entry points.  defer_splits != null: a split-K plan
+// leaves its fp32 partials in ws WITHOUT the reduce launch and reports the
+// split count there (1 = no split: z was written as usual).
+static int x3_conv1x1_impl(const float* x, int ldx, int M, int K, int N, const float* in_scale, const float* in_bias,
+                           const void* w_hi, const void* w_lo, const float* out_bias, void* z_hi, void* z_lo,
+                           float* y, int ldy, int pool, int H, int W, float* ws, size_t ws_bytes, void* stream,
+                           int* defer_splits) {
+  if (defer_splits) *defer_splits = 1;
   if (M <= 0) return hipSuccess;
   const bool split_out = z_hi != nullptr;
   if (K % kBK || K <= 0 || ldx % 4 || ldx < K || !x || !in_scale || !in_bias || !w_hi || !w_lo)
@@ -1259,54 +1394,39 @@ int tcamd_x3_conv1x1(const float* x, int ldx, int M, int K, int N, const float* 
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !p.ws) return e;
+  if (defer_splits && split_out) {
+    *defer_splits = pl.splits;  // the 3x3 sums the partials while staging its band
+    return hipSuccess;
+  }
   const int rg = tcamd::grid_for((size_t)M * (N / 4));
   if (split_out) hipLaunchKernelGGL(x3_splitk_reduce_kernel<true>, dim3(rg), dim3(256), 0, s, p, pl.splits);
   else hipLaunchKernelGGL(x3_splitk_reduce_kernel<false>, dim3(rg), dim3(256), 0, s, p, pl.splits);
   return hipGetLastError();
 }
 
+extern "C" {
+
 // 3x3 conv 128 -> 32 over imgs x H x W pixels (W <= 56); z_hi/z_lo [M][128]
 // bf16, w_hi/w_lo [32][9][128] bf16, y fp32 rows of ldy (offset to the slice).
 int tcamd_x3_conv3x3(const void* z_hi, const void* z_lo, int imgs, int H, int W, const void* w_hi, const void* w_lo,
                      float* y, int ldy, void* stream) {
-  if (imgs <= 0) return hipSuccess;
-  if (W > kMaxW3 || W < 1 || H < 1 || ldy % 4 || !z_hi || !z_lo || !w_hi || !w_lo || !y) return hipErrorInvalidValue;
-  if (!aligned16(z_hi) || !aligned16(z_lo) || !aligned16(w_hi) || !aligned16(w_lo) || !aligned16(y))
-    return hipErrorInvalidValue;
-  X3Conv3x3Params p;
-  p.z_hi = (const uint16_t*)z_hi;
-  p.z_lo = (const uint16_t*)z_lo;
-  p.w_hi = (const uint16_t*)w_hi;
-  p.w_lo = (const uint16_t*)w_lo;
-  p.y = y;
-  p.ldy = ldy;
-  p.M = imgs * H * W;
-  p.H = H;
-  p.W = W;
-  p.mag_hw = (uint32_t)((0x100000000ull + H * W - 1) / (uint64_t)(H * W));
-  p.mag_w = (uint32_t)((0x100000000ull + W - 1) / (uint64_t)W);
-  if (p.M >= (1 << 24)) return hipErrorInvalidValue;  // fast_divmod range
-  // one block (8 waves) per CU; each walks a contiguous run of tiles so the
-  // halo rows its neighbour tile re-reads are still in this XCD's L2
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<0>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsV2);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<-1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kLdsV2);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  static const int k9dbg = getenv("TCAMD_X3_K9_DBG") ? atoi(getenv("TCAMD_X3_K9_DBG")) : 0;
-  p.dbg = k9dbg;
-  p.tiles = (p.M + kT2 - 1) / kT2;
-  const int grid = std::min(p.tiles, 256);
-  p.tiles_per_block = (p.tiles + grid - 1) / grid;
-  const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
-  if (p.dbg) hipLaunchKernelGGL(x3_conv3x3_v2_kernel<-1>, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
-  else hipLaunchKernelGGL(x3_conv3x3_v2_kernel<0>, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
-  return hipGetLastError();
+  return x3_conv3x3_launch(z_hi, z_lo, nullptr, nullptr, 0, imgs, H, W, w_hi, w_lo, y, ldy, stream);
+}
+
+// One dense layer: BN1+ReLU+1x1 (K -> 128) then the 3x3 (128 -> 32) into the
+// layer's slice of the block buffer.  When the 1x1 plans split-K (small M)
+// its partials go straight to the 3x3, which reduces them while staging its
+// band (no reduce launch, z never written).
+int tcamd_x3_dense_layer(const float* x, int ldx, int imgs, int H, int W, int K, const float* s1, const float* t1,
+                         const void* w1_hi, const void* w1_lo, const float* b1, void* z_hi, void* z_lo,
+                         const void* w2_hi, const void* w2_lo, float* y, int ldy, float* ws, size_t ws_bytes,
+                         void* stream) {
+  int splits = 1;
+  int e = x3_conv1x1_impl(x, ldx, imgs * H * W, K, kBN, s1, t1, w1_hi, w1_lo, b1, z_hi, z_lo, nullptr, 0, 0, 0, 0,
+                          ws, ws_bytes, stream, &splits);
+  if (e != hipSuccess) return e;
+  if (splits > 1) return x3_conv3x3_launch(nullptr, nullptr, ws, b1, splits, imgs, H, W, w2_hi, w2_lo, y, ldy, stream);
+  return x3_conv3x3_launch(z_hi, z_lo, nullptr, nullptr, 0, imgs, H, W, w2_hi, w2_lo, y, ldy, stream);
 }
 
 static int cu_count() {

@@ -141,6 +141,40 @@ def test_x3_conv3x3(imgs, H):
     assert (y[:, :off] == 7.0).all() and (y[:, off + 32:] == 7.0).all()
 
 
+@pytest.mark.parametrize("imgs,H,K", [(1, 56, 224), (1, 28, 480), (8, 14, 992), (1, 7, 992), (8, 7, 512),
+                                      (2, 56, 64), (128, 14, 256), (20, 28, 128)])
+def test_x3_dense_layer(imgs, H, K):
+    """1x1 -> 3x3 dense layer through one entry point: small M plans split-K and
+    the 3x3 sums the partials (+bias, ReLU, split) while staging its band (no
+    reduce launch); big M runs the plain z round trip.  Against fp64 torch."""
+    _need_gpu()
+    hip = _hip()
+    g = torch.Generator(device=DEV).manual_seed(imgs * 1000 + H + K)
+    M, ldx = imgs * H * H, K + 64
+    x = torch.randn(M, ldx, device=DEV, generator=g)
+    s = torch.rand(K, device=DEV, generator=g) + 0.5
+    t = torch.randn(K, device=DEV, generator=g) * 0.2
+    w1 = torch.randn(128, K, device=DEV, generator=g) / K ** 0.5
+    b1 = torch.randn(128, device=DEV, generator=g) * 0.1
+    w2 = torch.randn(32, 128, 3, 3, device=DEV, generator=g) / (9 * 128) ** 0.5
+    w1h, w1l = _split(w1)
+    w2h, w2l = (hip.x3_w3_fragments(u) for u in _split(w2.permute(0, 2, 3, 1).reshape(32, -1)))
+    zh = torch.empty(M, 128, device=DEV, dtype=torch.bfloat16)
+    zl = torch.empty_like(zh)
+    wsb = hip.x3_conv1x1_ws_bytes(M, K)
+    ws = torch.empty(max(wsb, 16), device=DEV, dtype=torch.uint8)
+    xc = x.clone()
+    hip.x3_dense_layer(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), w1h.data_ptr(), w1l.data_ptr(),
+                       b1.data_ptr(), zh.data_ptr(), zl.data_ptr(), w2h.data_ptr(), w2l.data_ptr(),
+                       x.data_ptr() + 4 * K, ldx, ws=ws.data_ptr(), ws_bytes=wsb, stream=_st())
+    torch.cuda.synchronize()
+    a = torch.relu(xc[:, :K].double() * s.double() + t.double())
+    z = torch.relu(a @ w1.double().t() + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
+    ref = F.conv2d(z, w2.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 32)
+    assert _rel(x[:, K:K + 32], ref) < 3e-5
+    assert torch.equal(x[:, :K], xc[:, :K]) and torch.equal(x[:, K + 32:], xc[:, K + 32:])
+
+
 @pytest.mark.parametrize("imgs", [3, 20])  # 20: more tiles than the persistent grid (several per block)
 def test_x3_stem(imgs):
     _need_gpu()

@@ -17,6 +17,8 @@ Network walk (same as :class:`densenet_fused.FusedDenseNet`, fp32 activations):
    -> per dense layer:  K8x conv1x1 (BN1+ReLU prologue; BN2-folded bias+ReLU
                         epilogue) -> z as split bf16 planes [pixels,128] x 2
                         K9x conv3x3 z -> block buffer ch[c_in : c_in+32] (fp32)
+                        (one x3_dense_layer call; small-M layers run the 1x1
+                        split-K and the 3x3 reduces its partials in-kernel)
    -> per transition:   K8x conv1x1 with BN+ReLU+2x2 avg-pool prologue
                         -> next block buffer ch[0 : C/2] (fp32)
    -> K10x head: relu(BN5(x)) global average -> [b,1024] fp32
@@ -154,11 +156,10 @@ class FusedDenseNetFP32:
             fp = self.feat[bi].data_ptr()
             M = b * hw * hw
             for L in layers:
-                hip.x3_conv1x1(fp, ctot, M, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(), L["w1h"].data_ptr(),
-                               L["w1l"].data_ptr(), out_bias=L["b1"].data_ptr(), z_hi=zh, z_lo=zl, ws=ws,
-                               ws_bytes=wsb, stream=st)
-                hip.x3_conv3x3(zh, zl, b, hw, hw, L["w2h"].data_ptr(), L["w2l"].data_ptr(), fp + 4 * L["cin"], ctot,
-                               stream=st)
+                hip.x3_dense_layer(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
+                                   L["w1h"].data_ptr(), L["w1l"].data_ptr(), L["b1"].data_ptr(), zh, zl,
+                                   L["w2h"].data_ptr(), L["w2l"].data_ptr(), fp + 4 * L["cin"], ctot, ws=ws,
+                                   ws_bytes=wsb, stream=st)
             if bi < len(self.trans):
                 T = self.trans[bi]
                 nhw, nct = self.block_dims[bi + 1]

@@ -175,6 +175,15 @@ _SIGS = {
          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "tcamd_x3_dense_layer": (
+        [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+            ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
     "tcamd_x3_stem": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
          ctypes.c_int, ctypes.c_void_p],
@@ -566,6 +575,17 @@ def x3_conv3x3(z_hi, z_lo, imgs, H, W, w_hi, w_lo, y, ldy, stream=None):
     """K9x fp32-parity 3x3 conv 128 -> 32 into fp32 rows of ``ldy``; ``w_hi`` /
     ``w_lo`` in the x3_w3_fragments layout."""
     _check(_load().tcamd_x3_conv3x3(z_hi, z_lo, imgs, H, W, w_hi, w_lo, y, ldy, _vp(stream)), "x3_conv3x3")
+
+
+def x3_dense_layer(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, z_hi, z_lo, w2_hi, w2_lo, y, ldy, ws=None,
+                   ws_bytes=0, stream=None):
+    """One fp32-parity dense layer: K8x BN1+ReLU+1x1 (K -> 128, BN2 folded, bias
+    ``b1``) then K9x 3x3 (128 -> 32) into ``y`` rows of ``ldy`` (the layer's
+    slice).  A split-K 1x1 hands its partials to the 3x3, which reduces them
+    while staging its band (no reduce launch)."""
+    _check(_load().tcamd_x3_dense_layer(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
+                                        z_hi, z_lo, w2_hi, w2_lo, y, int(ldy), _vp(ws), int(ws_bytes), _vp(stream)),
+           "x3_dense_layer")
 
 
 def x3_stem_fragments(w):
