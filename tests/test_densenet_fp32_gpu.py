@@ -264,3 +264,17 @@ def test_fp32_engine_vs_fp64_and_graph_capture(fp32_engine):
         gr.replay()
     s.synchronize()
     assert torch.equal(out[:2], got)
+
+
+def test_fp32_engine_workspace_covers_every_batch(fp32_engine):
+    """The split-K workspace is sized for every batch up to the capacity: a
+    serving engine (capacity 32 here, 256 in the server) must still split
+    (and reduce inside the 3x3) at bs1, where the partials are largest."""
+    from triton_client_amd.ops import hip
+
+    eng, _ = fp32_engine
+    for bi, layers in enumerate(eng.blocks):
+        hw = eng.block_dims[bi][0]
+        for L in layers:
+            for b in (1, 2, 8, eng.max_batch):
+                assert eng.ws.numel() >= hip.x3_conv1x1_ws_bytes(b * hw * hw, L["cin"])

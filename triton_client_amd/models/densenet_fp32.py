@@ -111,15 +111,18 @@ class FusedDenseNetFP32:
         self.pooled = torch.empty(n, self.num_features, device=dev, dtype=torch.float32)
         self.ptrs = torch.zeros(n, device=dev, dtype=torch.int64)
         self._img_off = torch.arange(n, device=dev, dtype=torch.int64) * (IMG_ELEMS * 4)
-        # split-K partials: the largest request over every 1x1 conv at capacity n
+        # split-K partials: the largest request over every 1x1 conv at EVERY
+        # batch size up to n (small batches split the most; sized for n alone,
+        # a capacity-256 serving engine found no room and ran bs1 unsplit)
         need = 0
         for bi, layers in enumerate(self.blocks):
             hw, ctot = self.block_dims[bi]
-            for L in layers:
-                need = max(need, hip.x3_conv1x1_ws_bytes(n * hw * hw, L["cin"]))
+            for cin in sorted({L["cin"] for L in layers}):
+                need = max(need, max(hip.x3_conv1x1_ws_bytes(b * hw * hw, cin) for b in range(1, n + 1)))
             if bi < len(self.trans):
                 nhw = self.block_dims[bi + 1][0]
-                need = max(need, hip.x3_conv1x1_ws_bytes(n * nhw * nhw, ctot, ctot // 2))
+                need = max(need, max(hip.x3_conv1x1_ws_bytes(b * nhw * nhw, ctot, ctot // 2)
+                                     for b in range(1, n + 1)))
         self.ws = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
 
     def with_workspace(self, max_batch=None):
