@@ -23,8 +23,12 @@
 //        next(p) = p + 4 + len(p); pointer DOUBLING in LDS (11 rounds) gives,
 //        for every p, the first chain position at or past the block end and
 //        the number of elements started on the way (exit/count tables);
-//     2. one lane chains the blocks: entry(b+1) = exit(entry(b)), element
-//        base index += count — one hop per 8 KiB instead of one per element;
+//     2. chaining the blocks: entry(b+1) = exit(entry(b)), element base
+//        index += count.  Fast path (every element the chain meets is at most
+//        kR - 4 bytes): compose 32-block superblocks over the first kR entry
+//        offsets in parallel, one lane hops superblocks, one lane per
+//        superblock expands its blocks.  Otherwise one lane hops blocks
+//        through the full exit table (one dependent HBM hop per 8 KiB);
 //     3. every block re-walks from its entry in LDS and writes its elements'
 //        offsets/lengths at base(b) + k.
 
@@ -229,6 +233,11 @@ constexpr int kIdxB = 8192;                 // bytes per block
 constexpr int kIdxPer = kIdxB / kBlock;     // positions per thread (32)
 constexpr uint64_t kBad = ~(uint64_t)0;     // malformed element on the chain
 constexpr uint64_t kNone = ~(uint64_t)0 - 1;  // block not entered / past n_expected
+constexpr int kR = kBlock;                    // compact-table entry offsets per block
+constexpr int kS = 32;                        // blocks per superblock (fast chain)
+constexpr uint32_t kTBad = 0xFFFFFFFFu;       // compact-table sentinels: malformed element,
+constexpr uint32_t kTEnd = 0xFFFFFFFEu;       //   chain ended (past the data),
+constexpr uint32_t kTFar = 0xFFFFFFFDu;       //   exit beyond the next block's first kR bytes
 
 __device__ __forceinline__ void stage_block(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t b0,
                                             uint8_t* win) {
@@ -249,16 +258,59 @@ __device__ __forceinline__ uint32_t le32(const uint8_t* q) {
 }
 
 // Phase 1: exit/count of every candidate start position of one block.
+// FULL = false: the compact tables of the fast chain (exit/count of the first
+// kR positions, one sequential walk per position through the LDS window).
+// FULL = true (run only when the fast chain gave up, *fast == 0): pointer
+// doubling over every position and the whole exit/count tables for
+// idx_chain — 10 bytes written per input byte, which the fast path skips.
+template <bool FULL>
 __global__ void __launch_bounds__(kBlock) idx_blocks(const uint8_t* __restrict__ buf, uint64_t nbytes,
                                                      uint64_t* __restrict__ exit_pos,
-                                                     uint16_t* __restrict__ count) {
+                                                     uint16_t* __restrict__ count, uint32_t* __restrict__ tab,
+                                                     uint16_t* __restrict__ tcnt, const int* __restrict__ fast) {
+  if (FULL && *fast) return;  // uniform per launch
   __shared__ __attribute__((aligned(16))) uint8_t win[kIdxB + 16];
-  __shared__ uint64_t nxt[kIdxB];
-  __shared__ uint16_t cnt[kIdxB];
   const uint64_t b0 = (uint64_t)blockIdx.x * kIdxB;
   const uint64_t bend = b0 + kIdxB;
   stage_block(buf, nbytes, b0, win);
   __syncthreads();
+  if constexpr (!FULL) {
+    // the fast chain needs the exits of the first kR positions only: thread e
+    // walks the chain from b0 + e through the LDS window (no doubling tables)
+    const int e = threadIdx.x;
+    uint64_t p = b0 + e;
+    uint32_t c = 0, v;
+    if (p >= nbytes) {
+      v = kTEnd;
+    } else {
+      for (;;) {
+        if (p + 4 > nbytes) {
+          v = kTBad;
+          break;
+        }
+        const uint64_t x = p + 4 + (uint64_t)le32(win + (p - b0));
+        if (x > nbytes) {
+          v = kTBad;
+          break;
+        }
+        ++c;
+        p = x;
+        if (p >= bend) {
+          v = p - bend < (uint64_t)kR ? (uint32_t)(p - bend) : kTFar;
+          break;
+        }
+        if (p >= nbytes) {
+          v = kTEnd;
+          break;
+        }
+      }
+    }
+    tab[(uint64_t)blockIdx.x * kR + e] = v;
+    tcnt[(uint64_t)blockIdx.x * kR + e] = (uint16_t)c;
+    return;
+  }
+  __shared__ uint64_t nxt[kIdxB];
+  __shared__ uint16_t cnt[kIdxB];
   // interleaved ownership (q = threadIdx.x + k*256): conflict-free LDS rows
 #pragma unroll 4
   for (int k = 0; k < kIdxPer; ++k) {
@@ -309,12 +361,88 @@ __global__ void __launch_bounds__(kBlock) idx_blocks(const uint8_t* __restrict__
   }
 }
 
+// Phase 2 (fast path), in three short steps instead of one dependent HBM hop
+// per 8 KiB block:
+//   a. compose: workgroup sb follows all kR entry offsets through its kS
+//      blocks' compact tables in LDS -> superblock exit offset + count;
+//   b. chain: one lane hops superblocks (kS blocks per hop);
+//   c. expand: one lane per superblock re-walks its kS blocks from the
+//      superblock entry and writes every block's entry / base.
+// A chain that meets an element longer than the compact tables cover (kTFar
+// while elements are still wanted) clears *fast and idx_chain runs instead.
+__global__ void __launch_bounds__(kBlock) idx_sb_compose(const uint32_t* __restrict__ tab,
+                                                         const uint16_t* __restrict__ tcnt, uint64_t nblk,
+                                                         uint32_t* __restrict__ g, uint32_t* __restrict__ gc) {
+  __shared__ uint32_t st[kS][kR];
+  __shared__ uint16_t sc[kS][kR];
+  const uint64_t blk0 = (uint64_t)blockIdx.x * kS;
+  const int nb = (int)min((uint64_t)kS, nblk - blk0);
+  for (int i = threadIdx.x; i < nb * kR; i += kBlock) {
+    st[i / kR][i % kR] = tab[blk0 * kR + i];
+    sc[i / kR][i % kR] = tcnt[blk0 * kR + i];
+  }
+  __syncthreads();
+  uint32_t v = threadIdx.x, c = 0;
+  for (int k = 0; k < nb && v < (uint32_t)kR; ++k) {
+    c += sc[k][v];
+    v = st[k][v];
+  }
+  g[(uint64_t)blockIdx.x * kR + threadIdx.x] = v;
+  gc[(uint64_t)blockIdx.x * kR + threadIdx.x] = c;
+}
+
+__global__ void idx_sb_chain(const uint32_t* __restrict__ g, const uint32_t* __restrict__ gc, uint64_t nsb,
+                             uint64_t n_expected, uint32_t* __restrict__ sb_entry, uint64_t* __restrict__ sb_base,
+                             int* __restrict__ fast, int* __restrict__ status) {
+  if (threadIdx.x != 0) return;
+  uint32_t v = 0;
+  uint64_t idx = 0;
+  for (uint64_t sb = 0; sb < nsb; ++sb) {
+    sb_entry[sb] = v;
+    sb_base[sb] = idx;
+    if (v < (uint32_t)kR && idx < n_expected) {
+      idx += gc[sb * kR + v];
+      v = g[sb * kR + v];
+    }
+  }
+  if (v == kTFar && idx < n_expected) {  // an element longer than the tables cover is still wanted
+    *fast = 0;
+    return;
+  }
+  *fast = 1;
+  const bool err = v == kTBad && idx < n_expected;
+  status[0] = err ? -1 : (idx >= n_expected ? 0 : 1);
+  reinterpret_cast<uint64_t*>(status + 2)[0] = idx < n_expected ? idx : n_expected;
+}
+
+__global__ void idx_sb_expand(const uint32_t* __restrict__ tab, const uint16_t* __restrict__ tcnt, uint64_t nbytes,
+                              uint64_t nblk, uint64_t n_expected, const uint32_t* __restrict__ sb_entry,
+                              const uint64_t* __restrict__ sb_base, const int* __restrict__ fast,
+                              uint64_t* __restrict__ entry, uint64_t* __restrict__ base) {
+  if (threadIdx.x != 0 || !*fast) return;
+  const uint64_t blk0 = (uint64_t)blockIdx.x * kS;
+  const uint64_t bl_end = min(blk0 + kS, nblk);
+  uint32_t v = sb_entry[blockIdx.x];
+  uint64_t idx = sb_base[blockIdx.x];
+  for (uint64_t b = blk0; b < bl_end; ++b) {
+    const uint64_t p = b * (uint64_t)kIdxB + v;
+    if (v >= (uint32_t)kR || idx >= n_expected || p >= nbytes) {
+      entry[b] = kNone;
+      continue;
+    }
+    entry[b] = p;
+    base[b] = idx;
+    idx += tcnt[b * kR + v];
+    v = tab[b * kR + v];
+  }
+}
+
 // Phase 2: one lane chains the blocks.  entry[b] = first chain position in
 // block b (kNone if the chain skips it or is done), base[b] = its element index.
 __global__ void idx_chain(const uint64_t* __restrict__ exit_pos, const uint16_t* __restrict__ count,
                           uint64_t nbytes, uint64_t nblk, uint64_t n_expected, uint64_t* __restrict__ entry,
-                          uint64_t* __restrict__ base, int* __restrict__ status) {
-  if (threadIdx.x != 0) return;
+                          uint64_t* __restrict__ base, int* __restrict__ status, const int* __restrict__ fast) {
+  if (threadIdx.x != 0 || *fast) return;  // the superblock chain already did it
   uint64_t p = 0, idx = 0;
   int err = 0;
   for (uint64_t b = 0; b < nblk; ++b) {
@@ -394,18 +522,32 @@ extern "C" int tcamd_index_bytes(const void* buf, uint64_t nbytes, uint64_t n_ex
   }
   // parallel path: stream-ordered scratch (exit u64 + count u16 per byte, entry/base per block)
   const uint64_t nblk = (nbytes + kIdxB - 1) / kIdxB;
+  const uint64_t nsb = (nblk + kS - 1) / kS;
   void* ws = nullptr;
-  const size_t wsb = nbytes * 8 + nbytes * 2 + 16 + nblk * 16;
+  const size_t wsb = nbytes * 8 + nbytes * 2 + 16 + nblk * 16 + nblk * kR * 6 + nsb * kR * 8 + nsb * 12 + 64;
   hipError_t e = hipMallocAsync(&ws, wsb, s);
   if (e != hipSuccess) return e;
   uint64_t* exit_pos = (uint64_t*)ws;
   uint16_t* count = (uint16_t*)(exit_pos + nbytes);
   uint64_t* entry = (uint64_t*)(((uintptr_t)(count + nbytes) + 15) & ~(uintptr_t)15);
   uint64_t* base = entry + nblk;
-  hipLaunchKernelGGL(idx_blocks, dim3((unsigned)nblk), dim3(kBlock), 0, s, (const uint8_t*)buf, nbytes, exit_pos,
-                     count);
+  uint64_t* sb_base = base + nblk;
+  uint32_t* tab = (uint32_t*)(sb_base + nsb);
+  uint32_t* g = tab + nblk * kR;
+  uint32_t* gc = g + nsb * kR;
+  uint32_t* sb_entry = gc + nsb * kR;
+  int* fast = (int*)(sb_entry + nsb);
+  uint16_t* tcnt = (uint16_t*)(fast + 4);
+  hipLaunchKernelGGL(idx_blocks<false>, dim3((unsigned)nblk), dim3(kBlock), 0, s, (const uint8_t*)buf, nbytes,
+                     exit_pos, count, tab, tcnt, fast);
+  hipLaunchKernelGGL(idx_sb_compose, dim3((unsigned)nsb), dim3(kBlock), 0, s, tab, tcnt, nblk, g, gc);
+  hipLaunchKernelGGL(idx_sb_chain, dim3(1), dim3(64), 0, s, g, gc, nsb, n_expected, sb_entry, sb_base, fast, status);
+  hipLaunchKernelGGL(idx_sb_expand, dim3((unsigned)nsb), dim3(64), 0, s, tab, tcnt, nbytes, nblk, n_expected, sb_entry,
+                     sb_base, fast, entry, base);
+  hipLaunchKernelGGL(idx_blocks<true>, dim3((unsigned)nblk), dim3(kBlock), 0, s, (const uint8_t*)buf, nbytes,
+                     exit_pos, count, tab, tcnt, fast);
   hipLaunchKernelGGL(idx_chain, dim3(1), dim3(64), 0, s, exit_pos, count, nbytes, nblk, n_expected, entry, base,
-                     status);
+                     status, fast);
   hipLaunchKernelGGL(idx_emit, dim3((unsigned)nblk), dim3(kBlock), 0, s, (const uint8_t*)buf, nbytes, entry, base,
                      n_expected, offs, lens);
   e = hipGetLastError();
