@@ -11,6 +11,7 @@
 #include <sys/socket.h>
 #include <time.h>
 #include <unistd.h>
+#include <zlib.h>
 
 #include <algorithm>
 #include <atomic>
@@ -108,6 +109,7 @@ struct PendingReq {
   bool http = false;      // KServe REST request: reply as JSON header + binary outputs
   uint64_t http_seq = 0;  // position in its connection's request order
   bool http_close = false;
+  int http_resp_enc = 0;  // response Content-Encoding: 0 none, 1 gzip, 2 deflate (zlib)
   std::string id;
   int32_t rows;
   std::vector<tcserve_ref> in;    // [n_inputs]
@@ -243,11 +245,14 @@ class Server {
   int AddModel(std::unique_ptr<NativeModel> m, std::string* err);
   int RemoveModel(const std::string& name);
   void ShmAdd(int kind, const std::string& name, const ShmEntry& e);
-  void ShmRemove(int kind, const std::string& name);
+  int ShmRemove(int kind, const std::string& name);
+  int ShmBusy(int kind, uint64_t ptr);
   NativeModel* FindModel(const std::string& name);
   std::mutex models_mu;
   std::map<std::string, std::shared_ptr<NativeModel>> models;
   std::atomic<uint64_t> n_native{0}, n_proxied{0}, n_conns{0};
+  // native REST requests whose body arrived compressed / whose response was compressed
+  std::atomic<uint64_t> n_inflated{0}, n_deflated{0};
 
   std::vector<std::unique_ptr<Loop>> loops;
   std::atomic<uint64_t> next_conn_id{1};
@@ -256,7 +261,7 @@ class Server {
  private:
   bool TryNative(Conn* c, Stream* st, const char* msg, size_t len, std::string* owner);
   bool TryNativeHttp(Conn* c, uint64_t seq, bool close, const std::string& name, const std::string& version,
-                     std::string* body, size_t json_len);
+                     std::string* body, size_t json_len, int resp_enc);
   void ProxyHttp(Conn* c, uint64_t seq, bool close, std::string&& raw);
   void FailPending(PendingReq* pr, int grpc_status, int http_status, const std::string& msg);
   void Proxy(Conn* c, Stream* st, bool streaming);
@@ -274,6 +279,13 @@ class Server {
   std::atomic<uint32_t> up_rr_{0};
   std::mutex shm_mu_;
   std::map<std::string, ShmEntry> shm_[2];
+  // unregistered regions that queued or executing requests still point into
+  struct Draining {
+    int kind;
+    uint64_t ptr;
+    std::shared_ptr<int> pin;
+  };
+  std::vector<Draining> draining_;
 };
 
 // ---------------------------------------------------------------------------
@@ -939,6 +951,127 @@ void Server::RejectTooLarge(Conn* c)
            true);
 }
 
+// Content-Encoding of a request body: 0 identity, 1 gzip, 2 deflate, -1 other (proxied).
+static int ContentCoding(const std::string* ce)
+{
+  if (!ce) return 0;
+  const std::string v = Lower(*ce);
+  if (v.empty() || v == "identity") return 0;
+  if (v == "gzip" || v == "x-gzip") return 1;
+  if (v == "deflate") return 2;
+  return -1;
+}
+
+// Response coding from Accept-Encoding: gzip preferred, then deflate (q=0 excluded).
+static int AcceptCoding(const std::string* ae)
+{
+  if (!ae) return 0;
+  const std::string v = Lower(*ae);
+  auto offered = [&](const char* tok) {
+    size_t p = 0;
+    const size_t n = strlen(tok);
+    while ((p = v.find(tok, p)) != std::string::npos) {
+      const bool start = p == 0 || v[p - 1] == ',' || v[p - 1] == ' ';
+      size_t e = p + n;
+      while (e < v.size() && v[e] == ' ') ++e;
+      const bool end = e == v.size() || v[e] == ',' || v[e] == ';';
+      if (start && end) {
+        const size_t q = v.find("q=", e);
+        const size_t comma = v.find(',', e);
+        if (q != std::string::npos && (comma == std::string::npos || q < comma)) return strtod(v.c_str() + q + 2, nullptr) > 0;
+        return true;
+      }
+      p = e;
+    }
+    return false;
+  };
+  if (offered("gzip")) return 1;
+  if (offered("deflate")) return 2;
+  return 0;
+}
+
+// zlib/gzip inflate (header auto-detected) with an output cap (no decompression bombs).
+static bool InflateBounded(const std::string& in, uint64_t cap, std::string* out)
+{
+  z_stream zs;
+  memset(&zs, 0, sizeof(zs));
+  if (inflateInit2(&zs, 15 | 32) != Z_OK) return false;
+  out->clear();
+  size_t pos = 0;
+  char buf[1 << 16];
+  int rc = Z_OK;
+  while (rc != Z_STREAM_END) {
+    if (zs.avail_in == 0) {
+      if (pos >= in.size()) break;
+      const size_t take = std::min<size_t>(in.size() - pos, 1u << 30);
+      zs.next_in = reinterpret_cast<Bytef*>(const_cast<char*>(in.data() + pos));
+      zs.avail_in = static_cast<uInt>(take);
+      pos += take;
+    }
+    zs.next_out = reinterpret_cast<Bytef*>(buf);
+    zs.avail_out = sizeof(buf);
+    rc = inflate(&zs, Z_NO_FLUSH);
+    if (rc != Z_OK && rc != Z_STREAM_END) break;
+    out->append(buf, sizeof(buf) - zs.avail_out);
+    if (out->size() > cap) {
+      rc = Z_DATA_ERROR;
+      break;
+    }
+  }
+  inflateEnd(&zs);
+  return rc == Z_STREAM_END;
+}
+
+// gzip (enc 1) or zlib "deflate" (enc 2) of parts, fastest level.
+static bool DeflateParts(const std::vector<std::pair<const char*, size_t>>& parts, int enc, std::string* out)
+{
+  z_stream zs;
+  memset(&zs, 0, sizeof(zs));
+  if (deflateInit2(&zs, Z_BEST_SPEED, Z_DEFLATED, enc == 1 ? 15 | 16 : 15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+  size_t total = 0;
+  for (const auto& p : parts) total += p.second;
+  out->clear();
+  out->reserve(deflateBound(&zs, static_cast<uLong>(total)) + 64);
+  char buf[1 << 16];
+  bool ok = true;
+  for (size_t i = 0; i < parts.size() && ok; ++i) {
+    const char* d = parts[i].first;
+    size_t left = parts[i].second;
+    const bool last_part = i + 1 == parts.size();
+    do {
+      const size_t take = std::min<size_t>(left, 1u << 30);
+      zs.next_in = reinterpret_cast<Bytef*>(const_cast<char*>(d));
+      zs.avail_in = static_cast<uInt>(take);
+      d += take;
+      left -= take;
+      const int flush = (last_part && left == 0) ? Z_FINISH : Z_NO_FLUSH;
+      int rc;
+      do {
+        zs.next_out = reinterpret_cast<Bytef*>(buf);
+        zs.avail_out = sizeof(buf);
+        rc = deflate(&zs, flush);
+        if (rc == Z_STREAM_ERROR) {
+          ok = false;
+          break;
+        }
+        out->append(buf, sizeof(buf) - zs.avail_out);
+      } while (zs.avail_out == 0);
+    } while (left > 0 && ok);
+  }
+  if (parts.empty() && ok) {
+    zs.avail_in = 0;
+    int rc;
+    do {
+      zs.next_out = reinterpret_cast<Bytef*>(buf);
+      zs.avail_out = sizeof(buf);
+      rc = deflate(&zs, Z_FINISH);
+      out->append(buf, sizeof(buf) - zs.avail_out);
+    } while (rc == Z_OK);
+  }
+  deflateEnd(&zs);
+  return ok;
+}
+
 void Server::OnHttpData(Conn* c)
 {
   while (!c->hin.empty() && !c->close_after) {
@@ -980,10 +1113,25 @@ void Server::OnHttpData(Conn* c)
     const std::string* ce = h.Get("content-encoding");
     const std::string* ae = h.Get("accept-encoding");
     bool handled = false;
-    if (h.method == "POST" && InferTarget(h.target, &model, &version) && ihcl && !ce &&
-        !(ae && (Lower(*ae).find("gzip") != std::string::npos || Lower(*ae).find("deflate") != std::string::npos))) {
-      const size_t jl = strtoull(ihcl->c_str(), nullptr, 10);
-      if (jl <= body.size()) handled = TryNativeHttp(c, seq, close, model, version, &body, jl);
+    if (h.method == "POST" && InferTarget(h.target, &model, &version) && ihcl) {
+      // KServe REST compression (reference http_client.cc:143-232, Python
+      // _client.py:1440-1460): a gzip / deflate request body is inflated here
+      // and the response compressed to the client's Accept-Encoding, so a
+      // compressed request stays on the native path.  Inference-Header-Content-Length
+      // counts the uncompressed JSON header in both directions.
+      const int req_enc = ContentCoding(ce);
+      const int resp_enc = AcceptCoding(ae);
+      std::string plain;
+      bool ok = req_enc >= 0;
+      if (ok && req_enc > 0) {
+        ok = InflateBounded(body, kMaxHttpBody, &plain);
+        if (ok) n_inflated++;
+      }
+      if (ok) {
+        std::string& b = req_enc > 0 ? plain : body;
+        const size_t jl = strtoull(ihcl->c_str(), nullptr, 10);
+        if (jl <= b.size()) handled = TryNativeHttp(c, seq, close, model, version, &b, jl, resp_enc);
+      }
     }
     if (!handled) {
       std::string raw;
@@ -1004,7 +1152,7 @@ void Server::OnHttpData(Conn* c)
 }
 
 bool Server::TryNativeHttp(Conn* c, uint64_t seq, bool close, const std::string& name, const std::string& version,
-                           std::string* body, size_t json_len)
+                           std::string* body, size_t json_len, int resp_enc)
 {
   std::shared_ptr<NativeModel> m;
   {
@@ -1031,6 +1179,7 @@ bool Server::TryNativeHttp(Conn* c, uint64_t seq, bool close, const std::string&
   pr->http = true;
   pr->http_seq = seq;
   pr->http_close = close;
+  pr->http_resp_enc = resp_enc;
   pr->conn_id = c->id;
   pr->loop = c->loop;
   pr->stream_id = 0;
@@ -1253,6 +1402,20 @@ std::string Server::HttpInferResponse(NativeModel* m, PendingReq* pr)
          "\r\n";
   } else {
     r += "Content-Type: application/json\r\n";
+  }
+  if (pr->http_resp_enc) {
+    std::vector<std::pair<const char*, size_t>> parts{{js.data(), js.size()}};
+    for (size_t k = 0; k < m->outputs.size(); ++k)
+      if (pr->out_requested[k] && !pr->out_shm[k]) parts.emplace_back(pr->host_out[k].data(), pr->host_out[k].size());
+    std::string z;
+    if (DeflateParts(parts, pr->http_resp_enc, &z)) {
+      r += pr->http_resp_enc == 1 ? "Content-Encoding: gzip\r\n" : "Content-Encoding: deflate\r\n";
+      r += "Content-Length: " + std::to_string(z.size()) + "\r\n";
+      if (pr->http_close) r += "Connection: close\r\n";
+      r += "\r\n";
+      r += z;
+      return r;
+    }
   }
   r += "Content-Length: " + std::to_string(js.size() + binary) + "\r\n";
   if (pr->http_close) r += "Connection: close\r\n";
@@ -1842,6 +2005,7 @@ void Server::Execute(NativeModel* m, int instance, std::vector<std::unique_ptr<P
       continue;
     }
     if (pr->http) {
+      if (pr->http_resp_enc) n_deflated++;
       PostHttp(pr->loop, pr->conn_id, pr->http_seq, HttpInferResponse(m, pr.get()), pr->http_close);
       continue;
     }
@@ -1924,29 +2088,43 @@ void Server::ShmAdd(int kind, const std::string& name, const ShmEntry& e)
   shm_[kind][name] = e;
 }
 
-void Server::ShmRemove(int kind, const std::string& name)
+int Server::ShmRemove(int kind, const std::string& name)
 {
-  // Take the entries out of the map (no new request can pin them), then wait
-  // until every queued or executing request that pinned one has finished, so
-  // the caller may unmap / hipIpcCloseMemHandle right after this returns.
-  std::vector<std::shared_ptr<int>> pins;
-  {
-    std::lock_guard<std::mutex> lk(shm_mu_);
-    if (name.empty()) {
-      for (auto& kv : shm_[kind]) pins.push_back(kv.second.pin);
-      shm_[kind].clear();
-    } else {
-      auto it = shm_[kind].find(name);
-      if (it != shm_[kind].end()) {
-        pins.push_back(it->second.pin);
-        shm_[kind].erase(it);
-      }
+  // Take the entries out of the map (no new request can pin them).  Requests
+  // already queued or executing keep their pins; the entry moves to the
+  // draining list and the caller must not unmap / hipIpcCloseMemHandle the
+  // region until ShmBusy() says the last pin has dropped.  Never blocks.
+  std::lock_guard<std::mutex> lk(shm_mu_);
+  std::vector<std::pair<std::string, ShmEntry>> gone;
+  if (name.empty()) {
+    for (auto& kv : shm_[kind]) gone.emplace_back(kv.first, kv.second);
+    shm_[kind].clear();
+  } else {
+    auto it = shm_[kind].find(name);
+    if (it != shm_[kind].end()) {
+      gone.emplace_back(it->first, it->second);
+      shm_[kind].erase(it);
     }
   }
-  const uint64_t deadline = NowNs() + 60ull * 1000000000ull;
-  for (auto& p : pins) {
-    while (p.use_count() > 1 && NowNs() < deadline) std::this_thread::sleep_for(std::chrono::microseconds(100));
+  int busy = 0;
+  for (auto& g : gone) {
+    if (g.second.pin.use_count() > 1) {
+      draining_.push_back(Draining{kind, g.second.ptr, g.second.pin});
+      ++busy;
+    }
   }
+  return busy;
+}
+
+int Server::ShmBusy(int kind, uint64_t ptr)
+{
+  std::lock_guard<std::mutex> lk(shm_mu_);
+  draining_.erase(std::remove_if(draining_.begin(), draining_.end(),
+                                 [](const Draining& d) { return d.pin.use_count() <= 1; }),
+                  draining_.end());
+  for (const auto& d : draining_)
+    if (d.kind == kind && d.ptr == ptr) return 1;
+  return 0;
 }
 
 }  // namespace tcserve
@@ -2091,9 +2269,14 @@ int32_t tcserve_shm_add(void* server, const char* name, int32_t kind, uint64_t p
 
 int32_t tcserve_shm_remove(void* server, int32_t kind, const char* name)
 {
-  if (kind != 0 && kind != 1) return 1;
-  static_cast<Server*>(server)->ShmRemove(kind, name ? name : "");
-  return 0;
+  if (kind != 0 && kind != 1) return -1;
+  return static_cast<Server*>(server)->ShmRemove(kind, name ? name : "");
+}
+
+int32_t tcserve_shm_busy(void* server, int32_t kind, uint64_t ptr)
+{
+  if (kind != 0 && kind != 1) return 0;
+  return static_cast<Server*>(server)->ShmBusy(kind, ptr);
 }
 
 int32_t tcserve_model_stats(void* server, const char* name, uint64_t* out)
@@ -2145,6 +2328,8 @@ int32_t tcserve_counters(void* server, uint64_t* out)
   out[0] = s->n_native.load();
   out[1] = s->n_proxied.load();
   out[2] = s->n_conns.load();
+  out[3] = s->n_inflated.load();
+  out[4] = s->n_deflated.load();
   return 0;
 }
 

@@ -66,13 +66,19 @@ int32_t tcserve_set_idle_dispatch(void* server, const char* name, int32_t on);
 int32_t tcserve_set_preferred(void* server, const char* name, const int32_t* sizes, int32_t n);
 /// Mirror of the Python shared-memory registries; kind 0 = system (ptr = host mapping), 1 = device.
 int32_t tcserve_shm_add(void* server, const char* name, int32_t kind, uint64_t ptr, uint64_t bytes, int32_t device);
-int32_t tcserve_shm_remove(void* server, int32_t kind, const char* name);  // name "" = all of kind
+/// Unregister (name "" = all of kind).  Never blocks: returns how many of the removed regions
+/// are still pinned by queued/executing requests (-1 on a bad kind); poll tcserve_shm_busy
+/// before unmapping / closing such a region.
+int32_t tcserve_shm_remove(void* server, int32_t kind, const char* name);
+/// 1 while a removed region at `ptr` is still referenced by a queued or executing request.
+int32_t tcserve_shm_busy(void* server, int32_t kind, uint64_t ptr);
 /// out[0..9]: inference_count, execution_count, success_count, success_ns, fail_count, fail_ns,
 /// queue_ns, compute_input_ns, compute_infer_ns, compute_output_ns; last_inference_ms at out[10].
 int32_t tcserve_model_stats(void* server, const char* name, uint64_t* out);
 /// Per batch size rows of 7: batch_size, count, in_ns, infer_ns, out_ns, (reserved x2). Returns row count.
 int32_t tcserve_batch_stats(void* server, const char* name, uint64_t* out, int32_t max_rows);
-/// Counters: [0] native requests, [1] proxied calls, [2] connections accepted.
+/// Counters: [0] native requests, [1] proxied calls, [2] connections accepted, [3] native REST
+/// requests with a gzip/deflate body, [4] native REST responses sent compressed.
 int32_t tcserve_counters(void* server, uint64_t* out);
 void tcserve_destroy(void* server);
 

@@ -38,9 +38,19 @@
 // accumulators are consecutive output channels of one pixel.
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 #include "kernels/common.h"
+
+// Host-side per-device caches (CU count, dynamic-LDS opt-ins): indexed by the
+// current HIP device, clamped into the table.
+constexpr int kMaxDevices = 64;
+static int device_slot() {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDevices) d = 0;
+  return d;
+}
 
 namespace {
 
@@ -1244,8 +1254,10 @@ static int x3_conv3x3_launch(const void* z_hi, const void* z_lo, const float* pa
   if (p.M >= (1 << 24)) return hipErrorInvalidValue;  // fast_divmod range
   // one block (8 waves) per CU; each walks a contiguous run of tiles so the
   // halo rows its neighbour tile re-reads are still in this XCD's L2
-  static bool attr_set = false;
-  if (!attr_set) {
+  // the dynamic-LDS opt-in is per device; it is cached only once every call succeeded
+  static std::atomic<bool> attr_set[kMaxDevices];
+  const int dev_slot = device_slot();
+  if (!attr_set[dev_slot].load(std::memory_order_acquire)) {
     hipError_t e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<0>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsV2);
     if (e == hipSuccess)
@@ -1255,7 +1267,7 @@ static int x3_conv3x3_launch(const void* z_hi, const void* z_lo, const float* pa
       e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               kLdsV2);
     if (e != hipSuccess) return e;
-    attr_set = true;
+    attr_set[dev_slot].store(true, std::memory_order_release);
   }
   static const int k9dbg = getenv("TCAMD_X3_K9_DBG") ? atoi(getenv("TCAMD_X3_K9_DBG")) : 0;
   p.dbg = k9dbg;
@@ -1344,16 +1356,23 @@ static int x3_conv1x1_impl(const float* x, int ldx, int M, int K, int N, const f
   // (M floor: TCAMD_X3_WS_MIN, A/B runs)
   static const int ws_min = getenv("TCAMD_X3_WS_MIN") ? atoi(getenv("TCAMD_X3_WS_MIN")) : 16384;
   if (ws_mode && !pool && split_out && N == kBN && M >= ws_min) {
-    static int ncu = 0;
+    // per device: the CU count and the dynamic-LDS opt-in, cached only after
+    // every attribute call succeeded (a failed setup is retried, never launched)
+    static std::atomic<int> ncu_dev[kMaxDevices];
+    const int dev_slot = device_slot();
+    int ncu = ncu_dev[dev_slot].load(std::memory_order_acquire);
     if (!ncu) {
-      int dev = 0;
+      int dev = 0, n = 0;
       hipError_t e = hipGetDevice(&dev);
-      if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      if (e == hipSuccess) e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      if (e == hipSuccess && n <= 0) e = hipErrorInvalidDevice;
       for (const void* f : {(const void*)x3_conv1x1_ws_kernel<3, 0>, (const void*)x3_conv1x1_ws_kernel<5, 0>,
                             (const void*)x3_conv1x1_ws_kernel<6, 0>, (const void*)x3_conv1x1_ws_kernel<3, -1>,
                             (const void*)x3_conv1x1_ws_kernel<5, -1>, (const void*)x3_conv1x1_ws_kernel<6, -1>})
         if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsWs);
       if (e != hipSuccess) return e;
+      ncu = n;
+      ncu_dev[dev_slot].store(ncu, std::memory_order_release);
     }
     X3WsParams wp;
     wp.c = p;
@@ -1430,12 +1449,15 @@ int tcamd_x3_dense_layer(const float* x, int ldx, int imgs, int H, int W, int K,
 }
 
 static int cu_count() {
-  static int ncu = 0;
+  static std::atomic<int> ncu_dev[kMaxDevices];
+  const int dev_slot = device_slot();
+  int ncu = ncu_dev[dev_slot].load(std::memory_order_acquire);
   if (!ncu) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
       ncu = 256;
+    ncu_dev[dev_slot].store(ncu, std::memory_order_release);
   }
   return ncu;
 }

@@ -148,3 +148,54 @@ def test_grpc_aio_stream_infer_sequence(cpu_server):
             assert len(got) == len(values)
 
     run(body())
+
+
+def test_http_aio_stays_on_native_path_and_scales(cpu_server):
+    """The asyncio REST client used to send aiohttp's default
+    ``Accept-Encoding: gzip, deflate`` on every request: the server gzipped
+    every response and tcserve relayed them all to the Python front end
+    (~2.3 ms per request, 968 infer/s at 64 tasks).  Requests must stay on the
+    native path uncompressed unless compression is asked for, compressed
+    requests/responses must be served natively too, and 64 tasks in flight
+    stay clear of the stall (absolute floors: relative rates are noise on a
+    shared CPU)."""
+    import time
+
+    nf = cpu_server.server.native_frontend
+    if nf is None:
+        pytest.skip("native front end not built")
+    a = np.arange(16, dtype=np.int32).reshape(1, 16)
+
+    async def body():
+        async with httpaio.InferenceServerClient(cpu_server.http_url) as c:
+            x = _simple_inputs(httpaio, a, a)
+            for _ in range(20):
+                await c.infer("add_sub_batched", x)
+            before = nf.counters()
+            t0 = time.perf_counter()
+            for _ in range(100):
+                r = await c.infer("add_sub_batched", x)
+            one = 100 / (time.perf_counter() - t0)
+            np.testing.assert_array_equal(r.as_numpy("OUTPUT0"), 2 * a)
+            mid = nf.counters()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                rs = await asyncio.gather(*[c.infer("add_sub_batched", x) for _ in range(64)])
+            many = 320 / (time.perf_counter() - t0)
+            assert all(np.array_equal(q.as_numpy("OUTPUT1"), 0 * a) for q in rs)
+            for comp in ("gzip", "deflate"):
+                r = await c.infer("add_sub_batched", x, request_compression_algorithm=comp,
+                                  response_compression_algorithm=comp)
+                np.testing.assert_array_equal(r.as_numpy("OUTPUT0"), 2 * a)
+            after = nf.counters()
+            return one, many, before, mid, after
+
+    one, many, before, mid, after = run(body())
+    assert mid["native_requests"] - before["native_requests"] == 100
+    assert mid["proxied_calls"] == before["proxied_calls"], "plain aio requests were relayed to Python"
+    assert mid["compressed_responses"] == before["compressed_responses"], "responses compressed unasked"
+    assert after["inflated_requests"] - mid["inflated_requests"] == 2
+    assert after["compressed_responses"] - mid["compressed_responses"] == 2
+    assert after["proxied_calls"] == before["proxied_calls"]
+    assert one > 800, "one aio task: %.0f infer/s (the relayed/gzip path ran ~400)" % one
+    assert many > 800, "64 aio tasks: %.0f infer/s (the relayed/gzip path ran ~970-1300)" % many

@@ -412,16 +412,19 @@ def test_duplicate_input_rejected_on_fast_path(cpu_server):
     assert g.is_server_live()
 
 
-def test_unregister_waits_for_inflight_request(cpu_server):
+def test_unregister_defers_unmap_until_inflight_request_done(cpu_server):
     """Unregistering a region while a native request that writes into it is
-    executing must not unmap it under the request: the unregister returns
-    only once the request is done, and the output landed."""
+    executing must neither block the caller (the wait used to run on the
+    server's event loop under the registry lock) nor unmap the region under
+    the request: the unregister returns at once, the unmap is deferred until
+    the request drops its pin, and the output lands."""
     import threading
     import time
 
     from triton_client_amd.server.cpu_models import AddSubBatched
 
     g = grpcclient.InferenceServerClient(cpu_server.grpc_url)
+    closer = cpu_server.server.shm_closer
     out = shm.create_shared_memory_region("inflight_out", "/inflight_out", 64)
     AddSubBatched.native_delay_s = 0.6
     try:
@@ -441,10 +444,16 @@ def test_unregister_waits_for_inflight_request(cpu_server):
         t0 = time.monotonic()
         g.unregister_system_shared_memory("inflight_out")
         waited = time.monotonic() - t0
+        assert waited < 0.3, "unregister blocked on the in-flight request (%.3f s)" % waited
+        assert closer.pending() == 1, "the region was unmapped under the executing request"
+        assert len(g.get_system_shared_memory_status().regions) == 0
         assert done.wait(10)
         assert res[0][1] is None, res[0][1]
-        assert waited > 0.2, "unregister returned while the request still held the region"
         np.testing.assert_array_equal(shm.get_contents_as_numpy(out, np.int32, [1, 16]), 2 * a)
+        deadline = time.monotonic() + 5
+        while closer.pending() and time.monotonic() < deadline:
+            time.sleep(0.01)
+        assert closer.pending() == 0, "the deferred unmap never ran"
     finally:
         AddSubBatched.native_delay_s = 0.0
         g.unregister_system_shared_memory()

@@ -208,6 +208,22 @@ _SIGS = {
          ctypes.c_void_p],
         ctypes.c_int,
     ),
+    # native batch executor for pointer-table graph models (csrc/runtime/graph_exec.hip)
+    "tcamd_pgx_create": (
+        [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32,
+         ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p, ctypes.c_int32],
+        ctypes.c_void_p,
+    ),
+    "tcamd_pgx_set_instance": (
+        [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64,
+         ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_char_p, ctypes.c_int32],
+        ctypes.c_int32,
+    ),
+    "tcamd_pgx_execute": (
+        [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32], ctypes.c_int,
+    ),
+    "tcamd_pgx_stats": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int32),
+    "tcamd_pgx_destroy": ([ctypes.c_void_p], None),
     "tcamd_pack_bytes_workspace": ([ctypes.c_uint64], ctypes.c_uint64),
     "tcamd_pack_bytes": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
@@ -635,6 +651,63 @@ def index_bytes(buf_ptr, nbytes, n_expected, offs_ptr, lens_ptr, status_ptr, str
         ),
         "index_bytes",
     )
+
+
+class PtrGraphExecutor:
+    """Native per-batch dispatch for a pointer-table graph model
+    (csrc/runtime/graph_exec.hip): the server's C++ batcher calls
+    ``fn_address`` with ``handle`` directly, so no Python runs per batch.
+
+    ``bind(i, stream, graph_execs, tbl_dev, stage_dev, out_dev, pad_ptrs)``
+    hands instance ``i`` its HIP stream, one graph exec per bucket, the
+    engine's device row-pointer table, a device staging area for host rows,
+    the graph's output buffer and per-row padding pointers."""
+
+    STAT_KEYS = ("batches", "prep_ns", "enqueue_ns", "wait_ns", "post_ns", "total_ns", "rows")
+
+    def __init__(self, device, instances, in_row_bytes, out_row_bytes, buckets):
+        lib = _load()
+        self.buckets = [int(b) for b in buckets]
+        self.max_rows = max(self.buckets)
+        err = ctypes.create_string_buffer(512)
+        arr = (ctypes.c_int32 * len(self.buckets))(*self.buckets)
+        h = lib.tcamd_pgx_create(int(device), int(instances), int(in_row_bytes), int(out_row_bytes),
+                                 len(self.buckets), arr, err, 512)
+        if not h:
+            raise RuntimeError(err.value.decode(errors="replace"))
+        self.handle = h
+
+    def bind(self, i, stream, graph_execs, tbl_dev, stage_dev, out_dev, pad_ptrs):
+        if len(graph_execs) != len(self.buckets) or len(pad_ptrs) < self.max_rows:
+            raise ValueError("one graph exec per bucket and max_rows padding pointers are required")
+        err = ctypes.create_string_buffer(512)
+        ge = (ctypes.c_uint64 * len(graph_execs))(*[int(g) for g in graph_execs])
+        pad = (ctypes.c_uint64 * self.max_rows)(*[int(p) for p in pad_ptrs[:self.max_rows]])
+        rc = _load().tcamd_pgx_set_instance(self.handle, int(i), _vp(stream), ge, int(tbl_dev), int(stage_dev),
+                                            int(out_dev), pad, err, 512)
+        if rc != 0:
+            raise RuntimeError(err.value.decode(errors="replace"))
+
+    @property
+    def fn_address(self):
+        return ctypes.cast(_load().tcamd_pgx_execute, ctypes.c_void_p).value
+
+    def execute(self, instance, batch_ptr):
+        """Run one tcserve_batch (a ctypes pointer/address) on ``instance``."""
+        err = ctypes.create_string_buffer(1024)
+        rc = _load().tcamd_pgx_execute(self.handle, int(instance), batch_ptr, err, 1024)
+        if rc != 0:
+            raise RuntimeError(err.value.decode(errors="replace"))
+
+    def stats(self):
+        out = (ctypes.c_uint64 * len(self.STAT_KEYS))()
+        _load().tcamd_pgx_stats(self.handle, out)
+        return dict(zip(self.STAT_KEYS, [int(v) for v in out]))
+
+    def close(self):
+        if self.handle:
+            _load().tcamd_pgx_destroy(self.handle)
+            self.handle = None
 
 
 def available():

@@ -6,6 +6,7 @@ Example::
 """
 import argparse
 import asyncio
+import json
 import os
 import signal
 import sys
@@ -84,6 +85,13 @@ def main(argv=None):
         await task
 
     asyncio.run(run())
+    # host-side phase totals of the native batch executors (graph_exec.hip)
+    for entry in list(server.repo.values()):
+        for inst in list(entry.instances.values()):
+            fn = getattr(inst, "executor_stats", None)
+            st = fn() if fn is not None else None
+            if st and st.get("batches"):
+                print("EXECUTOR STATS %s %s" % (entry.name, json.dumps(st)), flush=True)
     server.sys_shm.unregister()
     server.dev_shm.unregister()
     return 0

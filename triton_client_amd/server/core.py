@@ -165,11 +165,70 @@ def _merge_native_stats(d, ns):
     d["batch_stats"].sort(key=lambda b: b["batch_size"])
 
 
+class DeferredCloser:
+    """Closes unregistered shared-memory regions once no queued or executing
+    native request points into them any more (tcserve_shm_busy).  The wait
+    runs on this thread, never on the server's event loop or under a registry
+    lock."""
+
+    def __init__(self):
+        self._cv = threading.Condition()
+        self._items = []  # (close_fn, [busy_fn, ...])
+        self._thread = None
+
+    def close_when_idle(self, close_fn, busy_fns):
+        busy_fns = [b for b in busy_fns if b is not None]
+        if not any(b() for b in busy_fns):
+            close_fn()
+            return
+        with self._cv:
+            self._items.append((close_fn, busy_fns))
+            if self._thread is None:
+                self._thread = threading.Thread(target=self._run, name="shm-closer", daemon=True)
+                self._thread.start()
+            self._cv.notify()
+
+    def pending(self):
+        with self._cv:
+            return len(self._items)
+
+    def _run(self):
+        import time
+
+        while True:
+            with self._cv:
+                while not self._items:
+                    self._cv.wait()
+                items = list(self._items)
+            done = [it for it in items if not any(b() for b in it[1])]
+            for close_fn, _ in done:
+                try:
+                    close_fn()
+                except Exception:  # noqa: BLE001 - a failed unmap must not kill the closer
+                    pass
+            with self._cv:
+                self._items = [it for it in self._items if it not in done]
+            if len(done) < len(items):
+                time.sleep(0.0005)
+
+
+def _notify_remove(listeners, kind, name, ptr):
+    """Tell the listeners (the native front end) a region is gone; returns the
+    busy predicates of those that still have requests pointing into it."""
+    busy = []
+    for fn in listeners:
+        r = fn(kind, "remove", name, ptr)
+        if callable(r):
+            busy.append(r)
+    return busy
+
+
 class SystemShmRegistry:
-    def __init__(self, listeners=None):
+    def __init__(self, listeners=None, closer=None):
         self.regions = {}
         self.lock = threading.Lock()
         self.listeners = listeners if listeners is not None else []
+        self.closer = closer or DeferredCloser()
 
     def register(self, name, key, offset, byte_size):
         from tritonclient.utils import shared_memory as shm
@@ -195,9 +254,8 @@ class SystemShmRegistry:
             for n in names:
                 entry = self.regions.pop(n, None)
                 if entry is not None:
-                    for fn in self.listeners:
-                        fn("system", "remove", n)
-                    entry[0].close()
+                    busy = _notify_remove(self.listeners, "system", n, entry[0].address(0))
+                    self.closer.close_when_idle(entry[0].close, busy)
 
     def status(self, name=""):
         with self.lock:
@@ -226,10 +284,11 @@ class SystemShmRegistry:
 class DeviceShmRegistry:
     """HIP IPC regions (wire name: cudasharedmemory)."""
 
-    def __init__(self, listeners=None):
+    def __init__(self, listeners=None, closer=None):
         self.regions = {}
         self.lock = threading.Lock()
         self.listeners = listeners if listeners is not None else []
+        self.closer = closer or DeferredCloser()
 
     def register(self, name, raw_handle, device_id, byte_size):
         from triton_client_amd.ops import hip
@@ -259,12 +318,15 @@ class DeviceShmRegistry:
             for n in names:
                 e = self.regions.pop(n, None)
                 if e is not None:
-                    for fn in self.listeners:
-                        fn("device", "remove", n)
-                    try:
-                        hip.ipc_close(e[0], e[1])
-                    except Exception:
-                        pass
+                    busy = _notify_remove(self.listeners, "device", n, e[0])
+
+                    def close(ptr=e[0], dev=e[1]):
+                        try:
+                            hip.ipc_close(ptr, dev)
+                        except Exception:
+                            pass
+
+                    self.closer.close_when_idle(close, busy)
 
     def status(self, name=""):
         with self.lock:
@@ -342,8 +404,9 @@ class InferenceServer:
         self.shm_listeners = []
         self.model_listeners = []
         self.native_stats = None
-        self.sys_shm = SystemShmRegistry(self.shm_listeners)
-        self.dev_shm = DeviceShmRegistry(self.shm_listeners)
+        self.shm_closer = DeferredCloser()
+        self.sys_shm = SystemShmRegistry(self.shm_listeners, self.shm_closer)
+        self.dev_shm = DeviceShmRegistry(self.shm_listeners, self.shm_closer)
         self.executor = ThreadPoolExecutor(max_workers=executor_workers, thread_name_prefix="tcamd-exec")
         self.trace_settings = {
             "trace_level": ["OFF"],

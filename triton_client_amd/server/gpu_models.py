@@ -24,6 +24,7 @@ graphs (one per batch bucket) and static buffers, so ``instance_count``
 batches pipeline on separate HIP streams.
 """
 
+import os
 import threading
 
 import numpy as np
@@ -103,6 +104,32 @@ class DensenetOnnx(Model):
         for _ in range(max(1, self.instance_count)):
             self._slots.append(self._make_slot(dev))
         self._free = list(range(len(self._slots)))
+        self._pgx = None
+        if self.engine != "torch" and self.use_graphs and os.environ.get("TCAMD_NATIVE_EXEC", "1") != "0":
+            self._pgx = self._make_executor()
+
+    def _make_executor(self):
+        """C++ per-batch dispatch (csrc/runtime/graph_exec.hip): pointer table,
+        graph replay, output scatter and the completion wait run in the server's
+        batcher thread without Python (the GIL stays out of the request path)."""
+        from triton_client_amd.ops import hip
+
+        x = hip.PtrGraphExecutor(self.device_id, len(self._slots), self.C * self.H * self.W * 4, self.OUT * 4,
+                                 self.buckets)
+        for i, slot in enumerate(self._slots):
+            execs = [slot["graphs"][b].raw_cuda_graph_exec() for b in self.buckets]
+            x.bind(i, slot["stream"].cuda_stream, execs, slot["net"].ptrs.data_ptr(), slot["stage_dev"].data_ptr(),
+                   slot["out"].data_ptr(), slot["pad_ptrs"])
+        return x
+
+    def native_executor(self):
+        """(tcserve_exec_fn address, user pointer) of the C++ executor, or None."""
+        if self._pgx is None:
+            return None
+        return self._pgx.fn_address, self._pgx.handle
+
+    def executor_stats(self):
+        return None if self._pgx is None else self._pgx.stats()
 
     def _make_slot(self, dev):
         torch = self.torch
@@ -152,6 +179,9 @@ class DensenetOnnx(Model):
     def unload(self):
         from triton_client_amd.ops import hip
 
+        if getattr(self, "_pgx", None) is not None:
+            self._pgx.close()
+            self._pgx = None
         for s in self._slots:
             try:
                 hip.host_free(s["stage_host"])
@@ -225,6 +255,8 @@ class DensenetOnnx(Model):
             rows += n
         if rows > max(self.buckets):
             return [ServerError("batch of %d rows exceeds the largest bucket" % rows)] * len(requests)
+        if getattr(self, "_pgx", None) is not None:
+            return self._execute_pgx(plan, rows, img_bytes, out_row)
         i = self._acquire()
         slot = self._slots[i]
         try:
@@ -299,6 +331,65 @@ class DensenetOnnx(Model):
             return [e] * len(requests)
         finally:
             self._release(i)
+
+    def _execute_pgx(self, plan, rows, img_bytes, out_row):
+        """Python-scheduled batch through the same C++ executor tcserve uses."""
+        import ctypes
+
+        from .native_frontend import TcBatch, TcRef
+
+        n = len(plan)
+        ins = (TcRef * n)()
+        outs = (TcRef * n)()
+        keep, results = [], []
+        try:
+            for j, (r, first, k) in enumerate(plan):
+                t = r.input("data_0")
+                if isinstance(t.data, DeviceView):
+                    if t.data.nbytes < k * img_bytes:
+                        raise ServerError("input region too small for data_0")
+                    ins[j] = TcRef(1, self.device_id, t.data.ptr, t.data.nbytes)
+                else:
+                    a = np.ascontiguousarray(t.data, dtype=np.float32)
+                    keep.append(a)
+                    ins[j] = TcRef(0, 0, a.ctypes.data, a.nbytes)
+                ro = next((o for o in r.outputs if o.name == "fc6_1"), None)
+                target = None
+                if ro is not None and ro.shm is not None and ro.class_count == 0:
+                    target = self._server_target(r, ro)
+                if isinstance(target, DeviceView):
+                    if target.nbytes < k * out_row:
+                        raise ServerError(
+                            "shared memory size specified with the request for output 'fc6_1' "
+                            "(%d bytes) should be at least %d bytes" % (target.nbytes, k * out_row)
+                        )
+                    outs[j] = TcRef(1, self.device_id, target.ptr, target.nbytes)
+                    results.append(("shm", ro, None))
+                else:
+                    host = np.empty((k, self.OUT), dtype=np.float32)
+                    outs[j] = TcRef(0, 0, host.ctypes.data, host.nbytes)
+                    results.append(("host", None, host))
+            nrows = (ctypes.c_int32 * n)(*[k for _, _, k in plan])
+            timing = (ctypes.c_uint64 * 3)()
+            b = TcBatch(n, rows, nrows, 1, ins, 1, outs, timing)
+            i = self._acquire()
+            try:
+                self._pgx.execute(i, ctypes.addressof(b))
+            except RuntimeError as e:
+                raise ServerError(str(e)) from e
+            finally:
+                self._release(i)
+        except ServerError as e:
+            return [e] * n
+        if self._batch_stats is not None:
+            self._batch_stats(rows, n, int(timing[0]), int(timing[1]), int(timing[2]))
+        out = []
+        for (r, first, k), (kind, ro, host) in zip(plan, results):
+            if kind == "shm":
+                out.append([OutputTensor("fc6_1", "FP32", [k, self.OUT], None, shm=ro.shm)])
+            else:
+                out.append([OutputTensor("fc6_1", "FP32", [k, self.OUT], host)])
+        return out
 
     # -- native fast path (tcserve, csrc/cpp/server) ------------------------------------
     supports_native = True

@@ -73,6 +73,8 @@ def _load():
         lib.tcserve_shm_add.restype = ctypes.c_int32
         lib.tcserve_shm_remove.argtypes = [ctypes.c_void_p, ctypes.c_int32, cp]
         lib.tcserve_shm_remove.restype = ctypes.c_int32
+        lib.tcserve_shm_busy.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64]
+        lib.tcserve_shm_busy.restype = ctypes.c_int32
         lib.tcserve_model_stats.argtypes = [ctypes.c_void_p, cp, ctypes.POINTER(ctypes.c_uint64)]
         lib.tcserve_model_stats.restype = ctypes.c_int32
         lib.tcserve_batch_stats.argtypes = [ctypes.c_void_p, cp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]
@@ -133,11 +135,19 @@ class NativeFrontend:
 
     # -- shared memory mirror ------------------------------------------------------
     def _on_shm(self, kind, op, name, ptr=0, nbytes=0, device=0):
+        """Mirror a registration.  On remove, returns a predicate that is True
+        while queued/executing native requests still point into the region
+        (the registry defers the unmap / IPC close until it is False)."""
         k = 0 if kind == "system" else 1
         if op == "add":
             _load().tcserve_shm_add(self._h, name.encode(), k, int(ptr), int(nbytes), int(device))
-        else:
-            _load().tcserve_shm_remove(self._h, k, (name or "").encode())
+            return None
+        h = self._h
+        if not h:
+            return None
+        if _load().tcserve_shm_remove(h, k, (name or "").encode()) <= 0 or not ptr:
+            return None
+        return lambda: bool(self._h) and _load().tcserve_shm_busy(self._h, k, int(ptr)) != 0
 
     # -- models ----------------------------------------------------------------------
     def register_all(self):
@@ -181,7 +191,16 @@ class NativeFrontend:
                 ctypes.memmove(err, msg + b"\0", len(msg) + 1)
                 return 1
 
-        cb = EXEC_FN(_exec)
+        native = getattr(inst, "native_executor", None)
+        native = native() if native is not None else None
+        if native is not None:
+            # a C executor (e.g. csrc/runtime/graph_exec.hip): tcserve's batcher
+            # threads call it directly, no Python per batch
+            cb = EXEC_FN(native[0])
+            user = ctypes.c_void_p(native[1])
+        else:
+            cb = EXEC_FN(_exec)
+            user = None
         delay = int((inst.dynamic_batching or {}).get("max_queue_delay_us", 0)) if inst.dynamic_batching is not None else 0
         err = ctypes.create_string_buffer(512)
         rc = _load().tcserve_add_model(
@@ -189,7 +208,7 @@ class NativeFrontend:
             int(max(1, inst.instance_count)),
             len(ins), _strs([s.name for s in ins]), _strs([s.datatype for s in ins]), in_nd, in_dims,
             len(outs), _strs([s.name for s in outs]), _strs([s.datatype for s in outs]), out_nd, out_dims,
-            cb, None, err, 512)
+            cb, user, err, 512)
         if rc != 0:
             raise RuntimeError("tcserve: %s" % err.value.decode(errors="replace"))
         pref = [int(x) for x in (inst.dynamic_batching or {}).get("preferred", [])]
@@ -238,9 +257,10 @@ class NativeFrontend:
         return d
 
     def counters(self):
-        out = (ctypes.c_uint64 * 3)()
+        out = (ctypes.c_uint64 * 5)()
         _load().tcserve_counters(self._h, out)
-        return {"native_requests": int(out[0]), "proxied_calls": int(out[1]), "connections": int(out[2])}
+        return {"native_requests": int(out[0]), "proxied_calls": int(out[1]), "connections": int(out[2]),
+                "inflated_requests": int(out[3]), "compressed_responses": int(out[4])}
 
     def close(self):
         if self._h:

@@ -1,4 +1,4 @@
-"""asyncio KServe-v2 REST client on aiohttp.
+"""asyncio KServe-v2 REST client.
 
 API parity with reference ``tritonclient/http/aio/__init__.py:92-775``: the
 same ``InferenceServerClient`` methods as the synchronous client, as
@@ -6,15 +6,19 @@ coroutines (``async with`` support, ``close()``), ``generate_request_body`` /
 ``parse_response_body`` statics, plugins, gzip/deflate.  The request codec is
 shared with the sync client (``tritonclient/http/_utils.py``); the body is
 sent as one chunked-free payload assembled from the header + tensor buffers.
+
+Transport: an asyncio Protocol keep-alive pool (``_transport.py``) instead of
+the reference's aiohttp session; ``conn_limit`` / ``conn_timeout`` / ``ssl`` /
+``ssl_context`` keep their meaning.
 """
 
+import asyncio
 import base64
 import gzip
 import json
+import ssl as _ssl
 import zlib
 from urllib.parse import quote
-
-import aiohttp
 
 from tritonclient.utils import raise_error
 
@@ -25,6 +29,7 @@ from .._infer_result import InferResult
 from .._requested_output import InferRequestedOutput
 from .._utils import _dumps, _get_error, _get_inference_request, _get_inference_request_parts, _get_query_string
 from ...utils import InferenceServerException  # noqa: F401
+from ._transport import HttpTransportError, Pool
 
 __all__ = ["InferenceServerClient", "InferInput", "InferRequestedOutput", "InferResult", "InferenceServerException"]
 
@@ -56,9 +61,15 @@ class InferenceServerClient(InferenceServerClientBase):
             raise_error("url should not include the scheme")
         scheme = "https://" if ssl else "http://"
         self._url = scheme + (url if url[-1] != "/" else url[:-1])
-        self._conn = aiohttp.TCPConnector(ssl=ssl_context if ssl else False, limit=conn_limit)
-        self._stub = aiohttp.ClientSession(connector=self._conn, timeout=aiohttp.ClientTimeout(total=conn_timeout),
-                                           auto_decompress=False)
+        hostport, _, prefix = url.partition("/")
+        self._prefix = ("/" + prefix.rstrip("/")) if prefix.strip("/") else ""
+        host, _, port = hostport.rpartition(":") if ":" in hostport else (hostport, "", "")
+        if not port:
+            host, port = hostport, ("443" if ssl else "80")
+        if ssl and ssl_context is None:
+            ssl_context = _ssl.create_default_context()
+        self._pool = Pool(host.strip("[]"), int(port), ssl_context if ssl else None, conn_limit)
+        self._timeout = conn_timeout
         self._verbose = verbose
 
     async def __aenter__(self):
@@ -68,8 +79,8 @@ class InferenceServerClient(InferenceServerClientBase):
         await self.close()
 
     async def close(self):
-        """Close the client's HTTP session."""
-        await self._stub.close()
+        """Close the client's HTTP connections."""
+        self._pool.close()
 
     # -- transport ------------------------------------------------------------------
     def _headers(self, headers):
@@ -91,38 +102,43 @@ class InferenceServerClient(InferenceServerClientBase):
             uri = uri + "?" + _get_query_string(query_params)
         return uri
 
+    def _path(self, request_uri, query_params):
+        path = self._prefix + "/" + request_uri
+        if query_params is not None:
+            path = path + "?" + _get_query_string(query_params)
+        return path
+
+    async def _send(self, method, request_uri, headers, query_params, body=None):
+        path = self._path(request_uri, query_params)
+        try:
+            r = await asyncio.wait_for(self._pool.request(method, path, headers, body), self._timeout)
+        except asyncio.TimeoutError:
+            raise_error("HTTP %s %s timed out after %s s" % (method, self._uri(request_uri, query_params),
+                                                             self._timeout))
+        except (HttpTransportError, OSError) as e:
+            raise_error("HTTP %s %s failed: %s" % (method, self._uri(request_uri, query_params), e))
+        return _Resp(r.status, r.body, r.headers)
+
     async def _get(self, request_uri, headers, query_params):
         headers = self._headers(headers)
-        uri = self._uri(request_uri, query_params)
         if self._verbose:
-            print("GET {}, headers {}".format(uri, headers))
-        try:
-            async with self._stub.get(uri, headers=headers) as r:
-                body = await r.read()
-                resp = _Resp(r.status, body, r.headers)
-        except aiohttp.ClientError as e:
-            raise_error("HTTP GET %s failed: %s" % (uri, e))
+            print("GET {}, headers {}".format(self._uri(request_uri, query_params), headers))
+        resp = await self._send("GET", request_uri, headers, query_params)
         if self._verbose:
-            print(resp.status_code, body)
+            print(resp.status_code, resp.read())
         return resp
 
     async def _post(self, request_uri, request_body, headers, query_params):
         headers = self._headers(headers)
-        uri = self._uri(request_uri, query_params)
         if isinstance(request_body, str):
             request_body = request_body.encode()
-        elif isinstance(request_body, (list, tuple)):
-            request_body = b"".join(bytes(p) for p in request_body)
         if self._verbose:
-            print("POST {}, headers {}\n{}".format(uri, headers, request_body[:256]))
-        try:
-            async with self._stub.post(uri, data=request_body, headers=headers) as r:
-                body = await r.read()
-                resp = _Resp(r.status, body, r.headers)
-        except aiohttp.ClientError as e:
-            raise_error("HTTP POST %s failed: %s" % (uri, e))
+            shown = request_body if isinstance(request_body, (bytes, bytearray)) else b"".join(
+                bytes(p) for p in request_body)
+            print("POST {}, headers {}\n{}".format(self._uri(request_uri, query_params), headers, shown[:256]))
+        resp = await self._send("POST", request_uri, headers, query_params, request_body)
         if self._verbose:
-            print(resp.status_code, body[:256])
+            print(resp.status_code, resp.read()[:256])
         return resp
 
     async def _get_json(self, uri, headers, query_params):
@@ -271,14 +287,14 @@ class InferenceServerClient(InferenceServerClientBase):
             inputs, request_id=request_id, outputs=outputs, sequence_id=sequence_id,
             sequence_start=sequence_start, sequence_end=sequence_end, priority=priority, timeout=timeout,
             custom_parameters=parameters)
-        body = b"".join(bytes(p) for p in parts)
+        body = parts  # header + tensor buffers, written with one writelines (no join)
         headers = dict(headers) if headers else {}
         if request_compression_algorithm == "gzip":
             headers["Content-Encoding"] = "gzip"
-            body = gzip.compress(body)
+            body = gzip.compress(b"".join(bytes(p) for p in parts))
         elif request_compression_algorithm == "deflate":
             headers["Content-Encoding"] = "deflate"
-            body = zlib.compress(body)
+            body = zlib.compress(b"".join(bytes(p) for p in parts))
         if response_compression_algorithm == "gzip":
             headers["Accept-Encoding"] = "gzip"
         elif response_compression_algorithm == "deflate":
