@@ -234,7 +234,7 @@ def test_fast_path_large_inband_tensor(cpu_server):
     x = np.zeros((1, 3, 224, 224), np.float32)
     i = grpcclient.InferInput("data_0", [2, 3, 224, 224], "FP32")
     i.set_data_from_numpy(np.zeros((2, 3, 224, 224), np.float32))
-    i._raw_content = x.tobytes()
+    i._raw = x.tobytes()  # bypass the client-side shape check: the server must reject it
     with pytest.raises(InferenceServerException, match="unexpected byte size"):
         c.infer("frontend_sink", [i])
 

@@ -1,58 +1,93 @@
-"""gRPC input-tensor descriptor (reference tritonclient/grpc/_infer_input.py:36-219)."""
-from tritonclient.grpc import service_pb2
+"""gRPC input-tensor descriptor.
+
+Behaviour contract: reference ``tritonclient/grpc/_infer_input.py:36-219``
+(constructor, accessors, ``set_data_from_numpy`` validation and BYTES / BF16
+serialisation, ``set_shared_memory``).  The descriptor keeps typed fields —
+name, datatype, shape, the serialised raw bytes or the shared-memory
+placement — and the request builder renders them into the request's
+``inputs`` entry (``_render``); the raw bytes go to ``raw_input_contents``
+without passing through an intermediate protobuf.  Validation and
+serialisation are shared with the HTTP descriptor
+(``tritonclient/http/_infer_input.py``).
+"""
 from tritonclient.http._infer_input import _check_dtype_shape, _raw_bytes
 
 
 class InferInput:
-    """Describes one input tensor (holds an ``InferInputTensor`` proto)."""
+    """Describes one input tensor of an inference request.
+
+    Parameters
+    ----------
+    name : str
+        Input tensor name.
+    shape : list of int
+        Input shape.
+    datatype : str
+        KServe datatype string (``"FP32"``, ``"BYTES"``, ...).
+    """
+
+    __slots__ = ("_name", "_shape", "_datatype", "_raw", "_shm")
 
     def __init__(self, name, shape, datatype):
-        self._input = service_pb2.ModelInferRequest().InferInputTensor()
-        self._input.name = name
-        self._input.ClearField("shape")
-        self._input.shape.extend(shape)
-        self._input.datatype = datatype
-        self._raw_content = None
+        self._name = name
+        self._shape = [int(d) for d in shape]
+        self._datatype = datatype
+        self._raw = None  # serialised tensor bytes (raw_input_contents)
+        self._shm = None  # (region, byte_size, offset)
 
     def name(self):
         """Input name."""
-        return self._input.name
+        return self._name
 
     def datatype(self):
         """Input datatype."""
-        return self._input.datatype
+        return self._datatype
 
     def shape(self):
         """Input shape."""
-        return list(self._input.shape)
+        return list(self._shape)
 
     def set_shape(self, shape):
         """Set the input shape; returns self."""
-        self._input.ClearField("shape")
-        self._input.shape.extend(shape)
+        self._shape = [int(d) for d in shape]
         return self
 
     def set_data_from_numpy(self, input_tensor):
-        """Attach ``input_tensor`` as ``raw_input_contents``; returns self."""
-        _check_dtype_shape(self._input.datatype, list(self._input.shape), input_tensor)
-        self._input.parameters.pop("shared_memory_region", None)
-        self._input.parameters.pop("shared_memory_byte_size", None)
-        self._input.parameters.pop("shared_memory_offset", None)
-        self._raw_content = _raw_bytes(self._input.datatype, input_tensor)
+        """Serialise ``input_tensor`` as this input's ``raw_input_contents``
+        (BYTES length-prefixed, BF16 truncated); clears any shared-memory
+        placement.  Returns self."""
+        _check_dtype_shape(self._datatype, self._shape, input_tensor)
+        self._shm = None
+        self._raw = _raw_bytes(self._datatype, input_tensor)
         return self
 
     def set_shared_memory(self, region_name, byte_size, offset=0):
-        """Read this input from shared-memory ``region_name``; returns self."""
-        self._input.ClearField("contents")
-        self._raw_content = None
-        self._input.parameters["shared_memory_region"].string_param = region_name
-        self._input.parameters["shared_memory_byte_size"].int64_param = byte_size
-        if offset != 0:
-            self._input.parameters["shared_memory_offset"].int64_param = offset
+        """Read this input from shared-memory ``region_name`` (``byte_size``
+        bytes at ``offset``) instead of the request body.  Returns self."""
+        self._raw = None
+        self._shm = (region_name, int(byte_size), int(offset))
         return self
 
+    def _render(self, tensor):
+        """Fill an ``InferInputTensor`` message (``request.inputs.add()``)."""
+        tensor.name = self._name
+        tensor.datatype = self._datatype
+        tensor.shape.extend(self._shape)
+        if self._shm is not None:
+            region, size, offset = self._shm
+            params = tensor.parameters
+            params["shared_memory_region"].string_param = region
+            params["shared_memory_byte_size"].int64_param = size
+            if offset != 0:
+                params["shared_memory_offset"].int64_param = offset
+        return tensor
+
     def _get_tensor(self):
-        return self._input
+        """A standalone ``InferInputTensor`` for this input."""
+        from tritonclient.grpc import service_pb2
+
+        return self._render(service_pb2.ModelInferRequest.InferInputTensor())
 
     def _get_content(self):
-        return self._raw_content
+        """Serialised bytes for ``raw_input_contents`` (None with shared memory)."""
+        return self._raw

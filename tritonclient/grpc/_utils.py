@@ -61,13 +61,13 @@ def _get_inference_request(
     if request_id != "":
         request.id = request_id
     for infer_input in inputs:
-        request.inputs.append(infer_input._get_tensor())
+        infer_input._render(request.inputs.add())
         content = infer_input._get_content()
         if content is not None:
             request.raw_input_contents.append(content)
     if outputs is not None:
         for infer_output in outputs:
-            request.outputs.append(infer_output._get_tensor())
+            infer_output._render(request.outputs.add())
     if sequence_id != 0 and sequence_id != "":
         if isinstance(sequence_id, str):
             request.parameters["sequence_id"].string_param = sequence_id
