@@ -288,6 +288,27 @@ int64_t Elements(const std::vector<int64_t>& s)
 typedef int (*SynthFillFn)(void*, size_t, int, int, double, double, uint64_t, uint64_t, void*);
 typedef int (*PackBytesFn)(const void*, const uint32_t*, uint64_t, void*, void*, void*);
 typedef uint64_t (*PackBytesWsFn)(uint64_t);
+typedef int (*ConvertFn)(const void*, int, void*, int, size_t, int, void*);
+
+bool NarrowFloat(const std::string& dt) { return dt == "FP16" || dt == "BF16"; }
+
+// host fallback of K4/K5: BF16 by truncation (the wire format of the
+// reference's serialize_bf16_tensor), FP16 round-to-nearest-even
+void NarrowOnHost(const std::string& dt, const std::vector<float>& f, std::vector<uint8_t>* out)
+{
+  out->resize(f.size() * 2);
+  for (size_t i = 0; i < f.size(); ++i) {
+    uint16_t h;
+    if (dt == "BF16") {
+      uint32_t u;
+      memcpy(&u, &f[i], 4);
+      h = static_cast<uint16_t>(u >> 16);
+    } else {
+      h = F32ToF16(f[i]);
+    }
+    memcpy(out->data() + 2 * i, &h, 2);
+  }
+}
 
 // K1/K2 live in the framework's libtcamd_hip.so; find it next to this
 // binary's tree (csrc/cpp/build/{bin,lib} -> triton_client_amd/ops/lib) or via
@@ -462,7 +483,7 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
     stream_ = st;
   }
   std::ostringstream desc;
-  bool used_k1 = false, used_k2 = false;
+  bool used_k1 = false, used_k2 = false, used_k4 = false;
   inputs_.resize(n_entries);
   for (size_t ent = 0; ent < n_entries; ++ent) {
     for (const auto& t : info.inputs) {
@@ -532,6 +553,7 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
       // host-built data: JSON content, or random/zero without HIP shm
       std::vector<uint8_t> sample;
       std::vector<std::string> strs;
+      std::vector<float> narrow;  // JSON FP16/BF16 values, narrowed by K4/K5 on the device (HIP shm)
       if (json_data) {
         const js::Value& jd = entries[ent];
         const js::Value* v = jd.Find(t.name);
@@ -552,13 +574,22 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
             strs.push_back(x.AsString());
             continue;
           }
+          if (NarrowFloat(t.datatype)) {
+            narrow.push_back(static_cast<float>(x.AsDouble()));
+            continue;
+          }
           uint8_t buf[8] = {0};
           if (t.datatype == "FP32") { float f = static_cast<float>(x.AsDouble()); memcpy(buf, &f, 4); }
           else if (t.datatype == "FP64") { double f = x.AsDouble(); memcpy(buf, &f, 8); }
-          else if (t.datatype == "FP16") { uint16_t f = F32ToF16(static_cast<float>(x.AsDouble())); memcpy(buf, &f, 2); }
           else if (t.datatype == "BOOL") { buf[0] = x.AsBool() ? 1 : 0; }
           else { int64_t iv = x.AsInt(); memcpy(buf, &iv, es); }
           sample.insert(sample.end(), buf, buf + es);
+        }
+        if (NarrowFloat(t.datatype)) {
+          if (static_cast<int64_t>(narrow.size()) != Elements(shape))
+            return Error("--input-data: element count of " + t.name + " does not match its shape");
+          if (!(dev && fill_inputs)) NarrowOnHost(t.datatype, narrow, &sample);
+          else sample.assign(narrow.size() * es, 0);  // sized here, written on the device below
         }
         if (t.datatype != "BYTES" && static_cast<int64_t>(sample.size()) != Elements(shape) * (int64_t)es)
           return Error("--input-data: element count of " + t.name + " does not match its shape");
@@ -597,7 +628,22 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
       input_regions_.push_back(regions_.size() - 1);
       if (!e.IsOk()) return e;
       if (fill_inputs) {
-        if (dev) {
+        if (dev && !narrow.empty()) {
+          // K4/K5: the JSON values go up as fp32 once per batch row and are
+          // narrowed straight into the region (BF16 truncation = the wire format)
+          auto cvt = HipKernel<ConvertFn>("tcamd_convert");
+          if (!cvt) return Error("HIP shm FP16/BF16 JSON data needs K4/K5 (tcamd_convert in libtcamd_hip.so)");
+          std::vector<float> rows;
+          for (int b = 0; b < reps; ++b) rows.insert(rows.end(), narrow.begin(), narrow.end());
+          void* tmp = nullptr;
+          hipError_t he = hipMallocAsync(&tmp, std::max<size_t>(16, rows.size() * 4), st);
+          if (he == hipSuccess) he = hipMemcpyAsync(tmp, rows.data(), rows.size() * 4, hipMemcpyHostToDevice, st);
+          int rc = he == hipSuccess ? cvt(tmp, DtypeCode("FP32"), r.dev, DtypeCode(t.datatype), rows.size(), 0, st) : he;
+          (void)hipFreeAsync(tmp, st);
+          if (rc == 0) rc = hipStreamSynchronize(st);
+          if (rc != 0) return Error("device FP16/BF16 conversion failed: " + std::to_string(rc));
+          used_k4 = true;
+        } else if (dev) {
           hipError_t he = hipMemcpyAsync(r.dev, batch_bytes.data(), batch_bytes.size(), hipMemcpyHostToDevice, st);
           if (he == hipSuccess) he = hipStreamSynchronize(st);
           if (he != hipSuccess) return Error(std::string("hipMemcpy failed: ") + hipGetErrorString(he));
@@ -640,6 +686,7 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
              : std::string("in-band tensors"));
   if (used_k1) d2 << ", inputs filled on device by K1 Philox (seed " << o.seed << ")";
   if (used_k2) d2 << " + K2 BYTES packing";
+  if (used_k4) d2 << ", JSON FP16/BF16 values narrowed on device by K4/K5";
   if (!fill_inputs && !input_regions_.empty()) d2 << ", inputs replicated by fan-out";
   if (!desc.str().empty()) d2 << "; " << desc.str();
   describe_ = d2.str();

@@ -3,34 +3,52 @@
 // __init__.py:193-276, src/c++/library/common.cc:168-183): each element is a
 // little-endian u32 length followed by that many bytes, row-major.
 //
-// pack: 3 launches
-//   1. per-block exclusive scan of the u32 lengths in LDS (1024 per block:
-//      256 threads x 4, Hillis-Steele over wave partials)
-//   2. single-block scan of the block totals (+ the grand total)
-//   3. OUTPUT-centric emit: every thread builds one 16-B chunk of the packed
-//      stream and writes it with one dwordx4 store (fully coalesced whatever
-//      the length distribution: one long string is spread over all lanes,
-//      many short ones are packed by one lane).  The owner element of a chunk
-//      is found by a two-level binary search over the element start offsets
-//      (block level, then inside the 1024-element block; neighbouring lanes
-//      search the same lines), then the chunk walks forward across element
-//      boundaries (length prefix bytes, then payload bytes).
-// unpack (index), by size:
-//   * <= 64 KiB: one workgroup walks the length chain through a 32 KiB LDS
-//     window (each hop an LDS read, not a dependent HBM round trip);
-//   * larger: a parallel 3-phase walk over 8 KiB blocks —
-//     1. every byte position p of a block is a candidate element start:
-//        next(p) = p + 4 + len(p); pointer DOUBLING in LDS (11 rounds) gives,
-//        for every p, the first chain position at or past the block end and
-//        the number of elements started on the way (exit/count tables);
-//     2. chaining the blocks: entry(b+1) = exit(entry(b)), element base
-//        index += count.  Fast path (every element the chain meets is at most
-//        kR - 4 bytes): compose 32-block superblocks over the first kR entry
-//        offsets in parallel, one lane hops superblocks, one lane per
-//        superblock expands its blocks.  Otherwise one lane hops blocks
-//        through the full exit table (one dependent HBM hop per 8 KiB);
-//     3. every block re-walks from its entry in LDS and writes its elements'
-//        offsets/lengths at base(b) + k.
+// K2 pack (round 3 design): elements are grouped in blocks of 1024.
+//   1. pk_block_sums: payload bytes of every block (S_b) and how many 64 KiB
+//      output "parts" it makes;
+//   2. pk_scan_chunks / pk_scan_top: two-level exclusive scan of S_b and of
+//      the part counts (no single-workgroup loop over all blocks);
+//   3. pk_emit: a persistent grid takes parts in order.  For its block it
+//      loads the 1024 lengths into LDS and scans them there (element output
+//      starts), then walks its part in 8 KiB tiles: the tile's payload bytes
+//      are one contiguous range of `data`, staged into LDS with dwordx4
+//      loads, and every lane assembles two 16-B output chunks from LDS (owner
+//      element by binary search over the LDS starts) and writes each with one
+//      dwordx4 store (byte stores only on the two ragged edges of a part).
+//   Fixed-width numpy 'S' arrays are packed without a host join: element i's
+//   payload is read at data + i * stride (tcamd_pack_bytes_strided).
+//
+// K3 unpack / index (round 3 design: speculative multi-candidate walk).  The
+// length chain is sequential, but a block's entry offset (where the first
+// element starting in it begins) is one of the first kXR bytes as long as
+// elements are shorter than kXR - 4 bytes, and chains started at every
+// candidate offset converge onto the true chain within a few hops:
+//   1. ix_walk: one WAVE per 4 KiB block, staged in LDS; each lane walks 4
+//      candidate chains interleaved (ILP hides the LDS latency of each hop)
+//      and records per candidate its exit offset into the next block (or
+//      END / BAD / FAR) and its element count; a wave reduction marks the
+//      block "sync" when every live candidate leaves at the same offset;
+//   2. ix_resolve: per block, the entry = the sync exit of the nearest sync
+//      predecessor, followed through the (rare) ambiguous blocks in between;
+//      the first block whose entry dies (END/BAD/FAR) or leaves the scanned
+//      window is the end of the chain (atomicMin);
+//   3. ix_scan_chunks / ix_scan_top: element base index of every block;
+//   4. ix_status: ok / fewer / malformed, or "retry with a larger window",
+//      or "fall back to the general walk" (an element longer than kXR - 4
+//      bytes, or a long run of ambiguous blocks);
+//   5. ix_emit: one wave per block re-walks from its entry through LDS;
+//      lane 0 writes (offset, length) pairs into an LDS ring that the whole
+//      wave flushes with coalesced stores.
+//   The scan starts on a window sized from n_expected (a small tensor in a
+//   large region does not walk the whole region) and grows 8x per retry.
+//   Fallback: the round-2 general path (pointer doubling over every byte
+//   position, idx_* below), whose exit/count tables are only allocated when
+//   it actually runs.
+//
+// Both entry points return after their stream work (K3 synchronises the
+// stream to read its status; K2 is asynchronous).
+
+#include <stdlib.h>
 
 #include "kernels/common.h"
 
@@ -67,102 +85,223 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* l
   return excl;
 }
 
-__global__ void __launch_bounds__(kBlock) scan_lengths(const uint32_t* __restrict__ lens, uint64_t n,
-                                                       uint64_t* __restrict__ offs,
-                                                       uint64_t* __restrict__ block_sums) {
+// ---- K2 pack ------------------------------------------------------------------
+constexpr uint64_t kPkPart = 65536;  // output bytes per part (unit of work of pk_emit)
+constexpr int kPkTile = kBlock * 2 * 16;  // 8 KiB: 2 x 16-B chunks per lane per tile
+
+// S_b (payload bytes) and the part count of every 1024-element block.
+__global__ void __launch_bounds__(kBlock) pk_block_sums(const uint32_t* __restrict__ lens, uint64_t n,
+                                                        uint64_t* __restrict__ S, uint64_t* __restrict__ parts) {
   __shared__ uint64_t lds_warp[kBlock / 64 + 1];
   const uint64_t base = (uint64_t)blockIdx.x * kSpan + (uint64_t)threadIdx.x * kPer;
-  uint64_t local[kPer];
   uint64_t sum = 0;
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
-    uint64_t i = base + k;
-    local[k] = (i < n) ? lens[i] : 0;
-    sum += local[k];
+    const uint64_t i = base + k;
+    if (i < n) sum += lens[i];
   }
   uint64_t total;
-  uint64_t excl = block_exclusive_scan(sum, lds_warp, &total);
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    uint64_t i = base + k;
-    if (i < n) offs[i] = excl;
-    excl += local[k];
+  block_exclusive_scan(sum, lds_warp, &total);
+  if (threadIdx.x == 0) {
+    const uint64_t first = (uint64_t)blockIdx.x * kSpan;
+    const uint64_t cnt = n - first < (uint64_t)kSpan ? n - first : (uint64_t)kSpan;
+    const uint64_t L = total + 4 * cnt;
+    S[blockIdx.x] = total;
+    parts[blockIdx.x] = (L + kPkPart - 1) / kPkPart;
   }
-  if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
 }
 
-__global__ void __launch_bounds__(kBlock) scan_block_sums(uint64_t* __restrict__ block_sums, uint64_t nb) {
+// Two-level exclusive scan of up to two u64 arrays (level 1: 1024 entries per
+// workgroup in place + chunk totals; level 2: one workgroup over the totals).
+__global__ void __launch_bounds__(kBlock) scan2_chunks(uint64_t* __restrict__ a, uint64_t* __restrict__ b, uint64_t n,
+                                                       uint64_t* __restrict__ ta, uint64_t* __restrict__ tb) {
   __shared__ uint64_t lds_warp[kBlock / 64 + 1];
-  uint64_t carry = 0;
-  for (uint64_t base = 0; base < nb; base += kBlock) {
-    uint64_t i = base + threadIdx.x;
-    uint64_t v = i < nb ? block_sums[i] : 0;
+  const uint64_t base = (uint64_t)blockIdx.x * kSpan + (uint64_t)threadIdx.x * kPer;
+  for (int arr = 0; arr < 2; ++arr) {
+    uint64_t* x = arr ? b : a;
+    if (!x) continue;
+    uint64_t loc[kPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      loc[k] = base + k < n ? x[base + k] : 0;
+      sum += loc[k];
+    }
     uint64_t total;
-    uint64_t excl = block_exclusive_scan(v, lds_warp, &total);
-    if (i < nb) block_sums[i] = excl + carry;
-    carry += total;
+    uint64_t excl = block_exclusive_scan(sum, lds_warp, &total);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      if (base + k < n) x[base + k] = excl;
+      excl += loc[k];
+    }
+    if (threadIdx.x == 0) (arr ? tb : ta)[blockIdx.x] = total;
     __syncthreads();
   }
-  if (threadIdx.x == 0) block_sums[nb] = carry;  // total payload bytes
 }
 
-// Packed-stream start of element i: payload bytes before it + 4 per prefix.
-__device__ __forceinline__ uint64_t in_start(const uint64_t* offs, const uint64_t* bsum, uint64_t i) {
-  return offs[i] + bsum[i / kSpan];
+__global__ void __launch_bounds__(kBlock) scan2_top(uint64_t* __restrict__ ta, uint64_t* __restrict__ tb, uint64_t nc) {
+  __shared__ uint64_t lds_warp[kBlock / 64 + 1];
+  for (int arr = 0; arr < 2; ++arr) {
+    uint64_t* x = arr ? tb : ta;
+    if (!x) continue;
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nc; base += kBlock) {
+      const uint64_t i = base + threadIdx.x;
+      const uint64_t v = i < nc ? x[i] : 0;
+      uint64_t total;
+      const uint64_t excl = block_exclusive_scan(v, lds_warp, &total);
+      if (i < nc) x[i] = excl + carry;
+      carry += total;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) x[nc] = carry;
+    __syncthreads();
+  }
 }
 
-__global__ void __launch_bounds__(kBlock) emit_packed(const uint8_t* __restrict__ data,
-                                                      const uint32_t* __restrict__ lens,
-                                                      const uint64_t* __restrict__ offs,
-                                                      const uint64_t* __restrict__ bsum, uint64_t n, uint64_t nb,
-                                                      uint8_t* __restrict__ out) {
-  const uint64_t total = bsum[nb] + 4 * n;
-  const uint64_t nchunks = (total + 15) / 16;
-  const bool out_aligned = (((uintptr_t)out) & 15) == 0;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += stride) {
-    const uint64_t pos0 = c * 16;
-    // block level: last block whose first element starts at or before pos0
-    uint64_t lo = 0, hi = nb;  // invariant: ostart(first of lo) <= pos0
-    while (hi - lo > 1) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if (bsum[mid] + 4 * mid * (uint64_t)kSpan <= pos0) lo = mid;
-      else hi = mid;
-    }
-    uint64_t elo = lo * kSpan, ehi = (lo + 1) * (uint64_t)kSpan < n ? (lo + 1) * (uint64_t)kSpan : n;
-    while (ehi - elo > 1) {
-      const uint64_t mid = (elo + ehi) >> 1;
-      if (in_start(offs, bsum, mid) + 4 * mid <= pos0) elo = mid;
-      else ehi = mid;
-    }
-    uint64_t e = elo;
-    uint64_t es = in_start(offs, bsum, e);        // payload start of e in `data`
-    uint64_t os = es + 4 * e;                     // packed start of e
-    uint32_t L = lens[e];
-    uint64_t oe = os + 4 + L;                     // packed end of e
-    union {
-      uint4 v;
-      uint8_t b[16];
-    } chunk;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint64_t pos = pos0 + k;
-      while (pos >= oe && e + 1 < n) {  // cross into the next element(s)
-        ++e;
-        es = in_start(offs, bsum, e);
-        os = es + 4 * e;
-        L = lens[e];
-        oe = os + 4 + L;
+__device__ __forceinline__ uint64_t scan2_at(const uint64_t* x, const uint64_t* top, uint64_t i) {
+  return x[i] + top[i / kSpan];
+}
+
+__global__ void __launch_bounds__(kBlock) pk_emit(const uint8_t* __restrict__ data, uint64_t stride,
+                                                  const uint32_t* __restrict__ lens, uint64_t n, uint64_t nb,
+                                                  const uint64_t* __restrict__ P, const uint64_t* __restrict__ Ptop,
+                                                  const uint64_t* __restrict__ V, const uint64_t* __restrict__ Vtop,
+                                                  uint8_t* __restrict__ out) {
+  __shared__ uint32_t s_len[kSpan];
+  __shared__ uint64_t s_os[kSpan + 1];  // local output start of every element (+ block end)
+  __shared__ __attribute__((aligned(16))) uint8_t s_pay[kPkTile + 32];
+  __shared__ uint64_t lds_warp[kBlock / 64 + 1];
+  __shared__ uint64_t s_blk;
+  const uint64_t nv = Vtop[(nb + kSpan - 1) / kSpan];  // total parts
+  const bool out16 = (((uintptr_t)out) & 15) == 0;
+  uint64_t cur_blk = ~(uint64_t)0;
+  for (uint64_t v = blockIdx.x; v < nv; v += gridDim.x) {
+    // ---- block of part v: last b with V(b) <= v
+    if (threadIdx.x == 0) {
+      uint64_t lo = 0, hi = nb;
+      while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (scan2_at(V, Vtop, mid) <= v) lo = mid;
+        else hi = mid;
       }
-      const uint64_t local = pos - os;
-      uint8_t byte = 0;
-      if (pos < total) byte = local < 4 ? (uint8_t)(L >> (8 * local)) : data[es + (local - 4)];
-      chunk.b[k] = byte;
+      s_blk = lo;
     }
-    if (out_aligned && pos0 + 16 <= total) {
-      *reinterpret_cast<uint4*>(out + pos0) = chunk.v;
-    } else {
-      for (int k = 0; k < 16 && pos0 + k < total; ++k) out[pos0 + k] = chunk.b[k];
+    __syncthreads();
+    const uint64_t b = s_blk;
+    const uint64_t first = b * kSpan;
+    const int cnt = (int)(n - first < (uint64_t)kSpan ? n - first : (uint64_t)kSpan);
+    if (b != cur_blk) {
+      // lengths -> LDS, exclusive scan -> element output starts
+      uint64_t loc[kPer], sum = 0;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const int e = threadIdx.x * kPer + k;
+        const uint32_t L = e < cnt ? lens[first + e] : 0;
+        loc[k] = e < cnt ? (uint64_t)L + 4 : 0;
+        s_len[e] = L;
+        sum += loc[k];
+      }
+      uint64_t total;
+      uint64_t excl = block_exclusive_scan(sum, lds_warp, &total);
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        s_os[threadIdx.x * kPer + k] = excl;
+        excl += loc[k];
+      }
+      if (threadIdx.x == 0) s_os[kSpan] = total;
+      cur_blk = b;
+      __syncthreads();
+    }
+    const uint64_t Lb = s_os[cnt];                       // block output bytes
+    const uint64_t Ob = scan2_at(P, Ptop, b) + 4 * first;  // block output start (global)
+    const uint64_t Db = stride ? 0 : scan2_at(P, Ptop, b);  // block payload start in data (packed)
+    const uint64_t part = v - scan2_at(V, Vtop, b);
+    const uint64_t q0 = part * kPkPart;
+    const uint64_t q1 = q0 + kPkPart < Lb ? q0 + kPkPart : Lb;
+    // global 16-B chunks overlapping [Ob + q0, Ob + q1)
+    const uint64_t c0 = (Ob + q0) / 16, c1 = (Ob + q1 + 15) / 16;
+    for (uint64_t ct = c0; ct < c1; ct += kPkTile / 16) {
+      const uint64_t ce = ct + kPkTile / 16 < c1 ? ct + kPkTile / 16 : c1;
+      // local output range of this tile, clipped to the part
+      const uint64_t t0 = ct * 16 > Ob + q0 ? ct * 16 - Ob : q0;
+      const uint64_t t1 = ce * 16 < Ob + q1 ? ce * 16 - Ob : q1;
+      uint64_t pay_lo = 0;
+      if (!stride) {
+        // payload range of [t0, t1): from the payload position of byte t0 to
+        // that of byte t1 - 1 (bytes of length prefixes map to no payload)
+        auto owner = [&](uint64_t pos) {
+          int lo = 0, hi = cnt;
+          while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_os[mid] <= pos) lo = mid;
+            else hi = mid;
+          }
+          return lo;
+        };
+        const int ea = owner(t0), ez = owner(t1 - 1);
+        const uint64_t pa = s_os[ea] - 4 * (uint64_t)ea + (t0 - s_os[ea] > 4 ? t0 - s_os[ea] - 4 : 0);
+        const uint64_t pz = s_os[ez] - 4 * (uint64_t)ez + (t1 - 1 - s_os[ez] >= 4 ? t1 - 1 - s_os[ez] - 4 + 1 : 0);
+        pay_lo = (Db + pa) & ~(uint64_t)15;
+        const uint64_t pay_hi = Db + (pz > pa ? pz : pa);
+        const int nbytes = (int)(pay_hi - pay_lo);  // <= kPkTile + 15
+        const bool a16 = (((uintptr_t)data) & 15) == 0;
+        for (int i = threadIdx.x; i < (nbytes + 15) / 16; i += kBlock) {
+          if (a16 && pay_lo + 16 * (uint64_t)(i + 1) <= pay_hi) {
+            *reinterpret_cast<uint4*>(s_pay + 16 * i) = *reinterpret_cast<const uint4*>(data + pay_lo + 16 * (uint64_t)i);
+          } else {
+            for (int k = 0; k < 16 && 16 * i + k < nbytes; ++k) s_pay[16 * i + k] = data[pay_lo + 16 * (uint64_t)i + k];
+          }
+        }
+      }
+      __syncthreads();
+      for (int h = 0; h < 2; ++h) {
+        const uint64_t c = ct + (uint64_t)threadIdx.x + (uint64_t)h * kBlock;
+        if (c < ce) {
+          const int64_t l0 = (int64_t)(c * 16) - (int64_t)Ob;  // local pos of the chunk's byte 0
+          const uint64_t start = l0 < (int64_t)t0 ? t0 : (uint64_t)l0;
+          int lo = 0, hi = cnt;
+          while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_os[mid] <= start) lo = mid;
+            else hi = mid;
+          }
+          int e = lo;
+          union {
+            uint4 v4;
+            uint8_t b[16];
+          } chunk;
+          bool full = true;
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            const int64_t pos = l0 + k;
+            uint8_t byte = 0;
+            if (pos < (int64_t)t0 || pos >= (int64_t)t1) {
+              full = false;
+            } else {
+              while (e + 1 < cnt && s_os[e + 1] <= (uint64_t)pos) ++e;
+              const uint64_t rel = (uint64_t)pos - s_os[e];
+              if (rel < 4) {
+                byte = (uint8_t)(s_len[e] >> (8 * rel));
+              } else if (stride) {
+                byte = data[(first + e) * stride + (rel - 4)];
+              } else {
+                byte = s_pay[Db + s_os[e] - 4 * (uint64_t)e + (rel - 4) - pay_lo];
+              }
+            }
+            chunk.b[k] = byte;
+          }
+          if (full && out16) {
+            *reinterpret_cast<uint4*>(out + c * 16) = chunk.v4;
+          } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+              const int64_t pos = l0 + k;
+              if (pos >= (int64_t)t0 && pos < (int64_t)t1) out[c * 16 + k] = chunk.b[k];
+            }
+          }
+        }
+      }
+      __syncthreads();
     }
   }
 }
@@ -489,37 +628,296 @@ __global__ void __launch_bounds__(kBlock) idx_emit(const uint8_t* __restrict__ b
   }
 }
 
-}  // namespace
+// ---- K3 v3: speculative multi-candidate block walk ----------------------------
+constexpr int kXB = 4096;                 // bytes per block (one wave)
+constexpr int kXR = 256;                  // candidate entry offsets per block
+constexpr int kXC = kXR / 64;             // candidates per lane
+constexpr int kXWaves = kBlock / 64;      // blocks per workgroup
+constexpr uint16_t kXBad = 0xFFFF;        // the chain meets a malformed element
+constexpr uint16_t kXFar = 0xFFFE;        // exit past the next block's first kXR bytes
+constexpr uint16_t kXEnd = 0xFFFD;        // the chain ends exactly at the end of the data
+constexpr uint32_t kSyncAmbig = 0xFFFFFFFFu;
+constexpr uint32_t kSyncNone = 0xFFFFFFFEu;
+constexpr uint32_t kEntryNone = 0xFFFFFFFFu;
+constexpr int kMaxBack = 64;              // ambiguous blocks followed per resolve before falling back
+enum { kEndEnd = 0, kEndBad = 1, kEndFar = 2, kEndWindow = 3 };
 
-// workspace must hold n*8 + ceil(n/1024)*8 bytes (see tcamd_pack_bytes_workspace).
-extern "C" uint64_t tcamd_pack_bytes_workspace(uint64_t n) {
-  return n * 8 + ((n + kSpan - 1) / kSpan) * 8 + 16;
+struct IxCtl {
+  unsigned long long end;   // (block << 2) | reason of the first block where the chain ends (atomicMin)
+  unsigned long long fail;  // first block whose entry could not be resolved (atomicMin)
+};
+
+// Stage [b0, b0 + kXB + 16) of the data into this wave's LDS window (zeros past nbytes).
+__device__ __forceinline__ void ix_stage(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t b0, uint8_t* win,
+                                         int lane) {
+  const bool aligned = ((((uintptr_t)buf) + b0) & 15) == 0;
+  for (int v = lane; v < (kXB + 16) / 16; v += 64) {
+    const uint64_t g = b0 + 16 * (uint64_t)v;
+    if (aligned && g + 16 <= nbytes) {
+      reinterpret_cast<uint4*>(win)[v] = *reinterpret_cast<const uint4*>(buf + g);
+    } else {
+      for (int k = 0; k < 16; ++k) win[16 * v + k] = (g + k < nbytes) ? buf[g + k] : 0;
+    }
+  }
 }
 
-extern "C" int tcamd_pack_bytes(const void* data, const uint32_t* lens, uint64_t n, void* out,
-                                void* workspace, void* stream) {
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, 64));
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+  return x;
+}
+
+__global__ void __launch_bounds__(kBlock) ix_walk(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t nblk,
+                                                  uint16_t* __restrict__ tab, uint16_t* __restrict__ tcnt,
+                                                  uint32_t* __restrict__ sync) {
+  __shared__ __attribute__((aligned(16))) uint8_t win_all[kXWaves][kXB + 16];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t b = (uint64_t)blockIdx.x * kXWaves + wave;
+  if (b >= nblk) return;  // wave-uniform; no workgroup barrier below
+  uint8_t* win = win_all[wave];
+  const uint64_t b0 = b * kXB, bend = b0 + kXB;
+  ix_stage(buf, nbytes, b0, win, lane);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  uint64_t p[kXC];
+  uint32_t code[kXC], cnt[kXC];
+  bool live[kXC];
+#pragma unroll
+  for (int j = 0; j < kXC; ++j) {
+    p[j] = b0 + lane + 64 * j;
+    cnt[j] = 0;
+    code[j] = 0;
+    live[j] = true;
+    if (p[j] >= nbytes) {
+      code[j] = kXEnd;  // at (or past) the end of the data: no element starts here
+      live[j] = false;
+    }
+  }
+  // lockstep hops; the kXC chains of a lane are independent (their LDS reads overlap)
+  bool any = live[0] || live[1] || live[2] || live[3];
+  while (__any(any)) {
+#pragma unroll
+    for (int j = 0; j < kXC; ++j) {
+      if (!live[j]) continue;
+      const uint64_t pj = p[j];
+      if (pj + 4 > nbytes) {
+        code[j] = kXBad;  // truncated length prefix
+        live[j] = false;
+        continue;
+      }
+      const uint8_t* q = win + (pj - b0);
+      const uint32_t L = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+      const uint64_t nx = pj + 4 + (uint64_t)L;
+      if (nx > nbytes) {
+        code[j] = kXBad;  // element runs past the data
+        live[j] = false;
+        continue;
+      }
+      ++cnt[j];
+      p[j] = nx;
+      if (nx == nbytes) {
+        code[j] = kXEnd;
+        live[j] = false;
+      } else if (nx >= bend) {
+        code[j] = nx - bend < (uint64_t)kXR ? (uint32_t)(nx - bend) : kXFar;
+        live[j] = false;
+      }
+    }
+    any = live[0] || live[1] || live[2] || live[3];
+  }
+  uint32_t lmin = 0xFFFFFFFFu, lmax = 0;
+#pragma unroll
+  for (int j = 0; j < kXC; ++j) {
+    tab[b * kXR + lane + 64 * j] = (uint16_t)code[j];
+    tcnt[b * kXR + lane + 64 * j] = (uint16_t)cnt[j];
+    if (code[j] < (uint32_t)kXR) {
+      lmin = min(lmin, code[j]);
+      lmax = max(lmax, code[j]);
+    }
+  }
+  lmin = wave_min_u32(lmin);
+  lmax = wave_max_u32(lmax);
+  if (lane == 0) sync[b] = lmin == 0xFFFFFFFFu ? kSyncNone : (lmin == lmax ? lmin : kSyncAmbig);
+}
+
+__global__ void __launch_bounds__(kBlock) ix_resolve(const uint16_t* __restrict__ tab, const uint16_t* __restrict__ tcnt,
+                                                     const uint32_t* __restrict__ sync, uint64_t nblk,
+                                                     uint32_t* __restrict__ entry, uint64_t* __restrict__ count,
+                                                     IxCtl* __restrict__ ctl) {
+  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblk) return;
+  uint32_t e;
+  uint64_t k;
+  if (b == 0) {
+    e = 0;
+    k = 0;
+  } else {
+    // nearest predecessor j whose exit does not depend on its entry
+    uint64_t j = b - 1;
+    int depth = 0;
+    while (j > 0 && sync[j] == kSyncAmbig && depth < kMaxBack) {
+      --j;
+      ++depth;
+    }
+    if (sync[j] == kSyncAmbig && j > 0) {
+      atomicMin(&ctl->fail, (unsigned long long)b);
+      entry[b] = kEntryNone;
+      count[b] = 0;
+      return;
+    }
+    if (sync[j] == kSyncAmbig) {  // j == 0: the chain starts at offset 0 of block 0
+      e = 0;
+      k = 0;
+    } else {
+      e = sync[j] == kSyncNone ? kEntryNone : sync[j];
+      k = j + 1;
+    }
+    for (; k < b && e != kEntryNone; ++k) {
+      const uint16_t c = tab[k * kXR + e];
+      e = c < kXR ? c : kEntryNone;
+    }
+  }
+  entry[b] = e;
+  if (e == kEntryNone) {
+    count[b] = 0;
+    return;
+  }
+  count[b] = tcnt[b * kXR + e];
+  const uint16_t c = tab[b * kXR + e];
+  int reason = -1;
+  if (c == kXEnd) reason = kEndEnd;
+  else if (c == kXBad) reason = kEndBad;
+  else if (c == kXFar) reason = kEndFar;
+  else if (b == nblk - 1) reason = kEndWindow;  // continues past the scanned window
+  if (reason >= 0) atomicMin(&ctl->end, ((unsigned long long)b << 2) | (unsigned long long)reason);
+}
+
+// count[b] = 0 for blocks after the chain's end (their entries are garbage)
+// and from the first unresolved block on (the chain may end inside it)
+__global__ void __launch_bounds__(kBlock) ix_mask(uint64_t* __restrict__ count, uint64_t nblk,
+                                                  const IxCtl* __restrict__ ctl) {
+  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < nblk && (b > (ctl->end >> 2) || b >= ctl->fail)) count[b] = 0;
+}
+
+// status[0]: 0 ok / 1 fewer elements than expected / -1 malformed / 2 retry
+// with a larger window / 3 fall back to the general walk; [2..3] elements found.
+__global__ void ix_status(const uint64_t* __restrict__ ctop, uint64_t nc, uint64_t n_expected,
+                          const IxCtl* __restrict__ ctl, int* __restrict__ status) {
+  if (threadIdx.x != 0) return;
+  const uint64_t total = ctop[nc];
+  const uint64_t end_blk = ctl->end >> 2;
+  const int reason = (int)(ctl->end & 3);
+  int st;
+  if (total >= n_expected) st = 0;  // every wanted element lies before any unresolved block
+  else if (ctl->fail <= end_blk) st = 3;
+  else if (reason == kEndEnd) st = 1;
+  else if (reason == kEndBad) st = -1;
+  else if (reason == kEndFar) st = 3;
+  else st = 2;
+  status[0] = st;
+  reinterpret_cast<uint64_t*>(status + 2)[0] = total < n_expected ? total : n_expected;
+}
+
+__global__ void __launch_bounds__(kBlock) ix_emit(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t nblk,
+                                                  const uint32_t* __restrict__ entry,
+                                                  const uint64_t* __restrict__ count,
+                                                  const uint64_t* __restrict__ ctop, uint64_t n_expected,
+                                                  uint64_t* __restrict__ offs, uint32_t* __restrict__ lens) {
+  __shared__ __attribute__((aligned(16))) uint8_t win_all[kXWaves][kXB + 16];
+  __shared__ uint64_t ring_off[kXWaves][64];
+  __shared__ uint32_t ring_len[kXWaves][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t b = (uint64_t)blockIdx.x * kXWaves + wave;
+  if (b >= nblk) return;
+  const uint32_t e = entry[b];
+  if (e == kEntryNone) return;
+  const uint64_t base = scan2_at(count, ctop, b);
+  if (base >= n_expected) return;
+  uint64_t want = count[b];  // count[] holds the exclusive scan: the block's own count is the difference
+  const uint64_t next = b + 1 < nblk ? scan2_at(count, ctop, b + 1) : ctop[(nblk + kSpan - 1) / kSpan];
+  want = next - base;
+  if (base + want > n_expected) want = n_expected - base;
+  if (want == 0) return;
+  uint8_t* win = win_all[wave];
+  const uint64_t b0 = b * kXB;
+  ix_stage(buf, nbytes, b0, win, lane);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  uint64_t p = b0 + e;
+  for (uint64_t k0 = 0; k0 < want; k0 += 64) {
+    const int m = (int)(want - k0 < 64 ? want - k0 : 64);
+    if (lane == 0) {
+      for (int i = 0; i < m; ++i) {
+        const uint8_t* q = win + (p - b0);
+        const uint32_t L = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+        ring_off[wave][i] = p + 4;
+        ring_len[wave][i] = L;
+        p += 4 + (uint64_t)L;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (lane < m) {
+      offs[base + k0 + lane] = ring_off[wave][lane];
+      lens[base + k0 + lane] = ring_len[wave][lane];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+}
+
+}  // namespace
+
+// K2 workspace: S and part counts per 1024-element block + their scan tops.
+extern "C" uint64_t tcamd_pack_bytes_workspace(uint64_t n) {
+  const uint64_t nb = (n + kSpan - 1) / kSpan, nc = (nb + kSpan - 1) / kSpan;
+  return (2 * (nb + 1) + 2 * (nc + 1)) * 8 + 64;
+}
+
+static int pack_impl(const void* data, uint64_t stride, const uint32_t* lens, uint64_t n, void* out, void* workspace,
+                     void* stream) {
   if (n == 0) return hipSuccess;
+  if (!data || !lens || !out || !workspace) return hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  uint64_t* offs = (uint64_t*)workspace;
-  uint64_t nb = (n + kSpan - 1) / kSpan;
-  uint64_t* bsum = offs + n;
-  hipLaunchKernelGGL(scan_lengths, dim3((unsigned)nb), dim3(kBlock), 0, s, lens, n, offs, bsum);
-  hipLaunchKernelGGL(scan_block_sums, dim3(1), dim3(kBlock), 0, s, bsum, nb);
-  hipLaunchKernelGGL(emit_packed, dim3(grid_for(n < 4096 ? 4096 : n)), dim3(kBlock), 0, s,
-                     (const uint8_t*)data, lens, offs, bsum, n, nb, (uint8_t*)out);
+  const uint64_t nb = (n + kSpan - 1) / kSpan, nc = (nb + kSpan - 1) / kSpan;
+  uint64_t* S = (uint64_t*)workspace;
+  uint64_t* parts = S + nb + 1;
+  uint64_t* ta = parts + nb + 1;
+  uint64_t* tb = ta + nc + 1;
+  hipLaunchKernelGGL(pk_block_sums, dim3((unsigned)nb), dim3(kBlock), 0, s, lens, n, S, parts);
+  hipLaunchKernelGGL(scan2_chunks, dim3((unsigned)nc), dim3(kBlock), 0, s, S, parts, nb, ta, tb);
+  hipLaunchKernelGGL(scan2_top, dim3(1), dim3(kBlock), 0, s, ta, tb, nc);
+  // persistent grid over the parts (~20 KiB LDS per workgroup: 7 per CU)
+  const uint64_t grid = nb < 1792 ? nb : 1792;
+  hipLaunchKernelGGL(pk_emit, dim3((unsigned)grid), dim3(kBlock), 0, s, (const uint8_t*)data, stride, lens, n, nb, S, ta,
+                     parts, tb, (uint8_t*)out);
   return hipGetLastError();
 }
 
-// status: device int[4]: [0] = 0 ok / 1 fewer elements than expected / -1
-// malformed; [2..3] = u64 element count found.
-extern "C" int tcamd_index_bytes(const void* buf, uint64_t nbytes, uint64_t n_expected, uint64_t* offs,
-                                 uint32_t* lens, int* status, void* stream) {
+// Packed payload (element i's bytes follow element i-1's) -> <u32 len>||bytes stream.
+extern "C" int tcamd_pack_bytes(const void* data, const uint32_t* lens, uint64_t n, void* out, void* workspace,
+                                void* stream) {
+  return pack_impl(data, 0, lens, n, out, workspace, stream);
+}
+
+// Fixed-width payload (numpy 'S' arrays): element i's bytes at data + i * stride.
+extern "C" int tcamd_pack_bytes_strided(const void* data, uint64_t stride, const uint32_t* lens, uint64_t n, void* out,
+                                        void* workspace, void* stream) {
+  if (stride == 0) return hipErrorInvalidValue;
+  return pack_impl(data, stride, lens, n, out, workspace, stream);
+}
+
+// Round-2 general path (every byte position a candidate; 10 B of tables per
+// input byte): only for chains the v3 walk cannot resolve.
+static int index_general(const void* buf, uint64_t nbytes, uint64_t n_expected, uint64_t* offs, uint32_t* lens,
+                         int* status, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (nbytes <= 65536 || n_expected < 2048) {
-    hipLaunchKernelGGL(index_bytes, dim3(1), dim3(kBlock), 0, s, (const uint8_t*)buf, nbytes, n_expected, offs,
-                       lens, status);
-    return hipGetLastError();
-  }
   // parallel path: stream-ordered scratch (exit u64 + count u16 per byte, entry/base per block)
   const uint64_t nblk = (nbytes + kIdxB - 1) / kIdxB;
   const uint64_t nsb = (nblk + kS - 1) / kS;
@@ -553,4 +951,98 @@ extern "C" int tcamd_index_bytes(const void* buf, uint64_t nbytes, uint64_t n_ex
   e = hipGetLastError();
   hipError_t f = hipFreeAsync(ws, s);
   return e != hipSuccess ? e : f;
+}
+
+// v3 speculative walk over a window of the data; returns the (host) status
+// 0 / 1 / -1, or 2 (retry larger window) / 3 (fall back), with the device
+// status written.  Synchronises the stream to read the status.
+static int index_v3(const uint8_t* buf, uint64_t nbytes, uint64_t window, uint64_t n_expected, uint64_t* offs,
+                    uint32_t* lens, int* status, hipStream_t s, int* host_status) {
+  const uint64_t nblk = (window + kXB - 1) / kXB;
+  const uint64_t nc = (nblk + kSpan - 1) / kSpan;
+  const size_t wsb = nblk * kXR * 4 + nblk * 4 + nblk * 4 + nblk * 8 + (nc + 1) * 8 + sizeof(IxCtl) + 256;
+  void* ws = nullptr;
+  hipError_t e = hipMallocAsync(&ws, wsb, s);
+  if (e != hipSuccess) return e;
+  uint64_t* count = (uint64_t*)ws;
+  uint64_t* ctop = count + nblk;
+  IxCtl* ctl = (IxCtl*)(ctop + nc + 1);
+  uint32_t* sync = (uint32_t*)(ctl + 1);
+  uint32_t* entry = sync + nblk;
+  uint16_t* tab = (uint16_t*)(entry + nblk);
+  uint16_t* tcnt = tab + nblk * kXR;
+  e = hipMemsetAsync(ctl, 0xFF, sizeof(IxCtl), s);
+  const unsigned wg = (unsigned)((nblk + kXWaves - 1) / kXWaves);
+  const unsigned tg = (unsigned)((nblk + kBlock - 1) / kBlock);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(ix_walk, dim3(wg), dim3(kBlock), 0, s, buf, nbytes, nblk, tab, tcnt, sync);
+    hipLaunchKernelGGL(ix_resolve, dim3(tg), dim3(kBlock), 0, s, tab, tcnt, sync, nblk, entry, count, ctl);
+    hipLaunchKernelGGL(ix_mask, dim3(tg), dim3(kBlock), 0, s, count, nblk, ctl);
+    hipLaunchKernelGGL(scan2_chunks, dim3((unsigned)nc), dim3(kBlock), 0, s, count, (uint64_t*)nullptr, nblk, ctop,
+                       (uint64_t*)nullptr);
+    hipLaunchKernelGGL(scan2_top, dim3(1), dim3(kBlock), 0, s, ctop, (uint64_t*)nullptr, nc);
+    hipLaunchKernelGGL(ix_status, dim3(1), dim3(64), 0, s, ctop, nc, n_expected, ctl, status);
+    e = hipGetLastError();
+  }
+  int hs[4] = {0, 0, 0, 0};
+  if (e == hipSuccess) e = hipMemcpyAsync(hs, status, sizeof(hs), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess && (hs[0] == 0 || hs[0] == 1)) {
+    hipLaunchKernelGGL(ix_emit, dim3(wg), dim3(kBlock), 0, s, buf, nbytes, nblk, entry, count, ctop, n_expected, offs,
+                       lens);
+    e = hipGetLastError();
+  }
+  hipError_t f = hipFreeAsync(ws, s);
+  if (e != hipSuccess) return e;
+  *host_status = hs[0];
+  return f;
+}
+
+// status: device int[4]: [0] = 0 ok / 1 fewer elements than expected / -1
+// malformed; [2..3] = u64 element count found.  Synchronous w.r.t. `stream`
+// (reads the status to size the scan window / pick the path).
+static thread_local int g_last_path = -1;  // 0 serial LDS walk, 1 v3 speculative walk, 2 general
+static thread_local uint64_t g_last_window = 0;
+
+// Which path the calling thread's last tcamd_index_bytes took (tests, kbench),
+// and the scan window (bytes) of its final v3 attempt.
+extern "C" int tcamd_index_bytes_last_path(uint64_t* window) {
+  if (window) *window = g_last_window;
+  return g_last_path;
+}
+
+extern "C" int tcamd_index_bytes(const void* buf, uint64_t nbytes, uint64_t n_expected, uint64_t* offs,
+                                 uint32_t* lens, int* status, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  g_last_window = 0;
+  if (nbytes <= 8192 || n_expected <= 256) {
+    g_last_path = 0;
+    hipLaunchKernelGGL(index_bytes, dim3(1), dim3(kBlock), 0, s, (const uint8_t*)buf, nbytes, n_expected, offs,
+                       lens, status);
+    return hipGetLastError();
+  }
+  static const int mode = getenv("TCAMD_K3_MODE") ? atoi(getenv("TCAMD_K3_MODE")) : 0;  // 1: general path only
+  if (mode != 1) {
+    uint64_t need = 64 * n_expected;
+    if (need < (1u << 20)) need = 1u << 20;
+    uint64_t window = need < nbytes ? (need + kXB - 1) / kXB * kXB : nbytes;
+    for (;;) {
+      if (window > nbytes) window = nbytes;
+      int st = 0;
+      g_last_window = window;
+      const int e = index_v3((const uint8_t*)buf, nbytes, window, n_expected, offs, lens, status, s, &st);
+      if (e != hipSuccess) return e;
+      if (st == 0 || st == 1 || st == -1) {
+        g_last_path = 1;
+        return hipSuccess;
+      }
+      if (st == 2 && window < nbytes) {
+        window = window * 8 < nbytes ? window * 8 : nbytes;
+        continue;
+      }
+      break;  // 3: fall back (or a window retry that cannot grow)
+    }
+  }
+  g_last_path = 2;
+  return index_general(buf, nbytes, n_expected, offs, lens, status, stream);
 }

@@ -62,11 +62,12 @@ def test_executor_mixed_device_and_host_rows(model, instance):
     model._pgx.execute(instance, ctypes.addressof(b))
     got = np.concatenate([out_d.cpu().numpy(), out_h])
     assert np.isfinite(got).all()
-    # reference: the same engine called eagerly on the whole batch (5 rows -> bucket 8)
+    # reference: the same engine called eagerly on the 5 rows (the executor ran
+    # the bucket-8 graph: split-K plans differ with M, so fp32-parity, not bitwise)
     with torch.no_grad():
         ref = model._slots[instance]["net"](x.to(dev)).cpu().numpy()
     rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
-    assert rel < 1e-5, rel
+    assert rel < 1e-4, rel
     t = keep[3]
     assert t[1] > 0, "graph time missing"
     st = model.executor_stats()

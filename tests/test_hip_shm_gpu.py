@@ -61,18 +61,89 @@ def test_unserialized_bytes_packed_by_k2_and_indexed_by_k3(hipshm):
     ser = serialize_byte_tensor(data).item()
     head = np.arange(8, dtype=np.int32)
     h = hipshm.create_shared_memory_region("rk2", 32 + len(ser) + 256, 0)
-    hipshm.set_shared_memory_region(h, [head, data])  # int32 head, then K2 at offset 32
+    hipshm.set_shared_memory_region(h, [head, data], serialize_bytes=True)  # int32 head, then K2 at offset 32
     raw = hipshm.get_contents_as_numpy(h, np.uint8, [32 + len(ser)])
     assert raw[32:].tobytes() == ser
     out = hipshm.get_contents_as_numpy(h, np.object_, [100, 200], offset=32)
     assert out.shape == (100, 200) and list(out.ravel()) == list(data.ravel())
     # asking for more elements than the region holds is an error, not garbage
     small = hipshm.create_shared_memory_region("rk3", len(serialize_byte_tensor(data[:1]).item()), 0)
-    hipshm.set_shared_memory_region(small, [data[:1]])
+    hipshm.set_shared_memory_region(small, [data[:1]], serialize_bytes=True)
     with pytest.raises(hipshm.CudaSharedMemoryException):
         hipshm.get_contents_as_numpy(small, np.object_, [400])
     hipshm.destroy_shared_memory_region(small)
     hipshm.destroy_shared_memory_region(h)
+
+
+def test_bytes_set_semantics_match_reference_and_system_shm(hipshm):
+    """without serialize_bytes an object array is the output of
+    serialize_byte_tensor (copied as-is, whatever its size) and an np.bytes_
+    array is copied raw (size * itemsize), exactly like the system-shm module
+    and the reference; serialize_bytes=True serialises both on the device
+    (fixed-width np.bytes_ straight from its buffer, no host join)."""
+    from tritonclient.utils import serialize_byte_tensor
+    from tritonclient.utils import shared_memory as sysshm
+
+    one = np.array([b"abc"], dtype=np.object_)  # a 1-element UNserialised tensor
+    fixed = np.array([b"ab", b"xyz\x00", b""], dtype="S5")
+    h = hipshm.create_shared_memory_region("sem", 64, 0)
+    key = "/sem_%d" % os.getpid()
+    sh = sysshm.create_shared_memory_region("sem_sys", key, 64)
+    try:
+        for mod, handle in ((hipshm, h), (sysshm, sh)):
+            mod.set_shared_memory_region(handle, [one, fixed])
+            raw = mod.get_contents_as_numpy(handle, np.uint8, [3 + 15])
+            assert raw.tobytes() == b"abc" + fixed.tobytes()
+            mod.set_shared_memory_region(handle, [one, fixed], serialize_bytes=True)
+            want = serialize_byte_tensor(one).item() + serialize_byte_tensor(fixed).item()
+            raw = mod.get_contents_as_numpy(handle, np.uint8, [len(want)])
+            assert raw.tobytes() == want
+    finally:
+        hipshm.destroy_shared_memory_region(h)
+        sysshm.destroy_shared_memory_region(sh)
+    # a large fixed-width array through the strided K2
+    rng = np.random.default_rng(5)
+    big = np.array([bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(0, 17, 30000)],
+                   dtype="S16")
+    want = serialize_byte_tensor(big).item()
+    h = hipshm.create_shared_memory_region("sem_big", len(want), 0)
+    hipshm.set_shared_memory_region(h, [big], serialize_bytes=True)
+    assert hipshm.get_contents_as_numpy(h, np.uint8, [len(want)]).tobytes() == want
+    back = hipshm.get_contents_as_numpy(h, np.object_, [30000])
+    assert list(back) == list(big)
+    hipshm.destroy_shared_memory_region(h)
+
+
+@pytest.mark.parametrize("dt", ["BF16", "FP16", "FP8_E4M3", "FP8_E5M2"])
+def test_device_dtype_conversion_on_set_and_get(hipshm, dt):
+    """K4/K5 on the HIP-shm set/get paths: float32 in -> narrow region bytes
+    wire-exact with the host codecs (BF16 = serialize_bf16_tensor truncation),
+    and narrow region -> float32 out widened on the device."""
+    from tritonclient.utils import deserialize_bf16_tensor, serialize_bf16_tensor
+    from tritonclient import utils as tu
+
+    rng = np.random.default_rng(11)
+    x = (rng.standard_normal(100003) * 50).astype(np.float32)
+    size = {"BF16": 2, "FP16": 2}.get(dt, 1)
+    h = hipshm.create_shared_memory_region("cvt_" + dt, 16 + x.size * size + 16, 0)
+    try:
+        for off in (0, 16, 3):  # aligned and unaligned region offsets
+            hipshm.set_shared_memory_region(h, [x], offset=off, datatype=dt)
+            raw = hipshm.get_contents_as_numpy(h, np.uint8, [x.size * size], offset=off)
+            if dt == "BF16":
+                want = np.frombuffer(serialize_bf16_tensor(x).item(), np.uint8)
+                back_ref = deserialize_bf16_tensor(want.tobytes())
+            elif dt == "FP16":
+                want = x.astype(np.float16).view(np.uint8)
+                back_ref = x.astype(np.float16).astype(np.float32)
+            else:  # saturating RNE, the host reference of v_cvt_pk_fp8_f32
+                want = np.frombuffer(tu.serialize_fp8_tensor(x, dt).item(), np.uint8)
+                back_ref = tu.deserialize_fp8_tensor(want.tobytes(), dt)
+            np.testing.assert_array_equal(raw, np.asarray(want, np.uint8))
+            back = hipshm.get_contents_as_numpy(h, np.float32, [x.size], offset=off, region_datatype=dt)
+            np.testing.assert_array_equal(back, back_ref)
+    finally:
+        hipshm.destroy_shared_memory_region(h)
 
 
 def test_dlpack_roundtrip_torch(hipshm):
@@ -197,3 +268,28 @@ def test_densenet_zero_copy_matches_fp32_reference(gpu_server, hipshm):
     hipshm.destroy_shared_memory_region(hout)
     g.close()
     h.close()
+
+
+@pytest.mark.parametrize("dt", ["BF16", "FP16", "FP32"])
+def test_infer_input_from_device_tensor(hipshm, dt):
+    """InferInput.set_data_from_dlpack with a torch ROCm FP32 tensor: the
+    request bytes (HTTP binary_data / gRPC raw_input_contents) must equal the
+    numpy path's for the same values (BF16 by K4 truncation on the GPU)."""
+    import torch
+
+    import tritonclient.grpc as grpcclient
+    import tritonclient.http as httpclient
+
+    x = torch.randn(4, 1000, device="cuda") * 3
+    xn = x.cpu().numpy()
+    for mod in (httpclient, grpcclient):
+        a = mod.InferInput("x", [4, 1000], dt)
+        a.set_data_from_dlpack(x[:, :] if dt != "FP16" else x)
+        b = mod.InferInput("x", [4, 1000], dt)
+        b.set_data_from_numpy(xn.astype(np.float16) if dt == "FP16" else xn)
+        get = (lambda i: i._get_binary_data()) if mod is httpclient else (lambda i: i._get_content())
+        assert get(a) == get(b)
+    # a BF16 device tensor goes out as-is (no conversion)
+    xb = x.to(torch.bfloat16)
+    c = httpclient.InferInput("x", [4, 1000], "BF16").set_data_from_dlpack(xb)
+    assert c._get_binary_data() == xb.view(torch.int16).cpu().numpy().tobytes()

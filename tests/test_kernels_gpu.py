@@ -275,6 +275,138 @@ def test_pack_and_index_bytes_large(env, n, maxlen, seed):
     np.testing.assert_array_equal(offs.cpu().numpy()[: n // 3], exp_offs[: n // 3])
 
 
+def _index(torch, hip, buf, nbytes, n):
+    offs = torch.empty(max(n, 1), device="cuda", dtype=torch.int64)
+    lns = torch.empty(max(n, 1), device="cuda", dtype=torch.int32)
+    status = torch.zeros(4, device="cuda", dtype=torch.int32)
+    hip.index_bytes(buf.data_ptr(), nbytes, n, offs.data_ptr(), lns.data_ptr(), status.data_ptr(), _stream(torch))
+    st = status.cpu().numpy()
+    return int(st[0]), int(st[2:4].view(np.uint64)[0]), offs.cpu().numpy()[:n], lns.cpu().numpy().view(np.uint32)[:n]
+
+
+def _wire(elems):
+    from tritonclient.utils import serialize_byte_tensor
+
+    return np.frombuffer(serialize_byte_tensor(np.array(elems, dtype=np.object_)).item(), dtype=np.uint8)
+
+
+def _expect(elems):
+    lens = np.array([len(e) for e in elems], dtype=np.int64)
+    return np.cumsum(np.concatenate([[0], lens[:-1] + 4])) + 4, lens.astype(np.uint32)
+
+
+@pytest.mark.parametrize("kind", ["ascii", "zeros", "binary", "empty"])
+def test_index_bytes_v3_speculative_walk(env, kind):
+    """K3 v3: candidate walks + resolve + emit on ~1.5 MB of BYTES with a
+    tail of unrelated region bytes; must match the host walk and take the
+    v3 path (elements shorter than the 256-B candidate window)."""
+    torch, hip = env
+    rng = np.random.default_rng({"ascii": 1, "zeros": 2, "binary": 3, "empty": 4}[kind])
+    n = 60000
+    if kind == "empty":
+        elems = [b""] * n
+    else:
+        ln = rng.integers(0, 40, n)
+        if kind == "zeros":
+            elems = [bytes(int(k)) for k in ln]
+        elif kind == "binary":
+            elems = [rng.integers(0, 256, int(k), dtype=np.uint8).tobytes() for k in ln]
+        else:
+            elems = [bytes(rng.integers(32, 127, int(k), dtype=np.uint8)) for k in ln]
+    wire = _wire(elems)
+    region = np.concatenate([wire, rng.integers(0, 256, 5000, dtype=np.uint8)])
+    buf = torch.from_numpy(region).cuda()
+    st, found, offs, lens = _index(torch, hip, buf, region.size, n)
+    path, window = hip.index_bytes_last_path()
+    assert st == 0 and found == n
+    eo, el = _expect(elems)
+    np.testing.assert_array_equal(offs, eo)
+    np.testing.assert_array_equal(lens, el)
+    assert path == 1, "expected the v3 speculative walk, got path %d" % path
+
+
+def test_index_bytes_small_tensor_in_large_region_scans_a_window(env):
+    """a small BYTES tensor (>= 2048 elements) at the start of a
+    256 MB region must not walk (or allocate scratch for) the whole region."""
+    torch, hip = env
+    rng = np.random.default_rng(9)
+    elems = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(0, 30, 3000)]
+    wire = _wire(elems)
+    buf = torch.zeros(256 << 20, device="cuda", dtype=torch.uint8)
+    buf[: wire.size] = torch.from_numpy(wire).cuda()
+    st, found, offs, lens = _index(torch, hip, buf, buf.numel(), len(elems))
+    path, window = hip.index_bytes_last_path()
+    assert st == 0 and found == len(elems)
+    eo, el = _expect(elems)
+    np.testing.assert_array_equal(offs, eo)
+    np.testing.assert_array_equal(lens, el)
+    assert path == 1 and window <= (1 << 20), (path, window)
+
+
+def test_index_bytes_window_grows_and_long_elements_fall_back(env):
+    torch, hip = env
+    rng = np.random.default_rng(10)
+    # 4000 elements of ~700 B: 64 * n = 256 KB is too small a first window (retry x8),
+    # and elements longer than 252 B send the chain to the general walk
+    elems = [bytes(rng.integers(0, 256, int(k), dtype=np.uint8)) for k in rng.integers(500, 900, 4000)]
+    wire = _wire(elems)
+    buf = torch.from_numpy(np.concatenate([wire, np.zeros(1 << 22, np.uint8)])).cuda()
+    st, found, offs, lens = _index(torch, hip, buf, buf.numel(), len(elems))
+    path, _ = hip.index_bytes_last_path()
+    assert st == 0 and found == len(elems) and path == 2
+    eo, el = _expect(elems)
+    np.testing.assert_array_equal(offs, eo)
+    np.testing.assert_array_equal(lens, el)
+    # short elements but a first window that is too small: v3 retries with 8x windows
+    elems = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(150, 250, 12000)]
+    wire = _wire(elems)
+    buf = torch.from_numpy(np.concatenate([wire, np.zeros(1 << 22, np.uint8)])).cuda()
+    st, found, offs, lens = _index(torch, hip, buf, buf.numel(), len(elems))
+    path, window = hip.index_bytes_last_path()
+    assert st == 0 and found == len(elems) and path == 1 and window > (1 << 20)
+    eo, el = _expect(elems)
+    np.testing.assert_array_equal(offs, eo)
+
+
+def test_index_bytes_v3_short_and_malformed(env):
+    torch, hip = env
+    elems = [b"abcdefghij"] * 20000
+    wire = _wire(elems)
+    buf = torch.from_numpy(wire.copy()).cuda()
+    st, found, _, _ = _index(torch, hip, buf, wire.size, 20001)
+    assert st == 1 and found == 20000
+    bad = wire.copy()
+    bad[14 * 10000: 14 * 10000 + 4] = np.frombuffer((1 << 30).to_bytes(4, "little"), np.uint8)
+    buf = torch.from_numpy(bad).cuda()
+    st, _, _, _ = _index(torch, hip, buf, bad.size, 20000)
+    assert st == -1
+
+
+@pytest.mark.parametrize("n,width", [(5000, 24), (70000, 7), (3, 40000)])
+def test_pack_bytes_strided_fixed_width(env, n, width):
+    """K2 over a numpy 'S' array's buffer (no host join): lengths are the
+    element lengths with trailing NULs stripped (numpy / serialize_byte_tensor)."""
+    torch, hip = env
+    rng = np.random.default_rng(n)
+    raw = rng.integers(97, 123, (n, width), dtype=np.uint8)
+    cut = rng.integers(0, width + 1, n)
+    raw[np.arange(width)[None, :] >= cut[:, None]] = 0
+    arr = raw.view("S%d" % width).reshape(n)
+    lens = np.char.str_len(arr).astype(np.uint32)
+    d_data = torch.from_numpy(raw.reshape(-1).copy()).cuda()
+    d_lens = torch.from_numpy(lens.view(np.int32).copy()).cuda()
+    total = int(lens.sum()) + 4 * n
+    out = torch.zeros(total + 32, device="cuda", dtype=torch.uint8)
+    ws = torch.empty(hip.pack_bytes_workspace(n), device="cuda", dtype=torch.uint8)
+    hip.pack_bytes_strided(d_data.data_ptr(), width, d_lens.data_ptr(), n, out.data_ptr() + 3, ws.data_ptr(),
+                           _stream(torch))
+    from tritonclient.utils import serialize_byte_tensor
+
+    ref = serialize_byte_tensor(arr).item()
+    got = out.cpu().numpy()
+    assert got[3:3 + total].tobytes() == ref and not got[:3].any() and not got[3 + total:].any()
+
+
 def test_index_bytes_detects_malformed(env):
     torch, hip = env
     buf = torch.tensor([5, 0, 0, 0, 1, 2], device="cuda", dtype=torch.uint8)

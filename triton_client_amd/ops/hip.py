@@ -229,6 +229,12 @@ _SIGS = {
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "tcamd_index_bytes_last_path": ([ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+    "tcamd_pack_bytes_strided": (
+        [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_index_bytes": (
         [
             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
@@ -643,8 +649,26 @@ def pack_bytes(data_ptr, lens_ptr, n, out_ptr, workspace_ptr, stream=None):
     )
 
 
+def pack_bytes_strided(data_ptr, stride, lens_ptr, n, out_ptr, workspace_ptr, stream=None):
+    """K2 over a fixed-width payload (numpy 'S' array): element i's bytes at data + i * stride."""
+    _check(
+        _load().tcamd_pack_bytes_strided(_vp(data_ptr), int(stride), _vp(lens_ptr), n, _vp(out_ptr),
+                                         _vp(workspace_ptr), _vp(stream)),
+        "pack_bytes_strided",
+    )
+
+
+def index_bytes_last_path():
+    """(path, window) of this thread's last index_bytes: 0 serial walk, 1 v3
+    speculative block walk, 2 general pointer-doubling fallback."""
+    w = ctypes.c_uint64(0)
+    p = _load().tcamd_index_bytes_last_path(ctypes.byref(w))
+    return p, w.value
+
+
 def index_bytes(buf_ptr, nbytes, n_expected, offs_ptr, lens_ptr, status_ptr, stream=None):
-    """K3: device BYTES index (offsets/lengths of each element)."""
+    """K3: device BYTES index (offsets/lengths of each element).  Synchronises
+    ``stream`` (it reads its own status to size the scan window)."""
     _check(
         _load().tcamd_index_bytes(
             _vp(buf_ptr), nbytes, n_expected, _vp(offs_ptr), _vp(lens_ptr), _vp(status_ptr), _vp(stream)

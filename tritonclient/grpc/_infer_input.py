@@ -61,6 +61,18 @@ class InferInput:
         self._raw = _raw_bytes(self._datatype, input_tensor)
         return self
 
+    def set_data_from_dlpack(self, tensor):
+        """Attach a DLPack tensor (e.g. a torch ROCm tensor) as raw content.
+
+        MI355X extension: a device tensor is copied D2H once; an FP32 device
+        tensor for a BF16 / FP16 / FP8 input is narrowed on the GPU first
+        (K4/K5; BF16 truncation = ``serialize_bf16_tensor``).  Returns self."""
+        from tritonclient.utils._device_tensor import wire_bytes
+
+        self._raw = wire_bytes(tensor, self._datatype, self._shape)
+        self._shm = None
+        return self
+
     def set_shared_memory(self, region_name, byte_size, offset=0):
         """Read this input from shared-memory ``region_name`` (``byte_size``
         bytes at ``offset``) instead of the request body.  Returns self."""

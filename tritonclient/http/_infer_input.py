@@ -127,6 +127,23 @@ class InferInput:
             self._parameters["binary_data_size"] = len(self._raw_data)
         return self
 
+    def set_data_from_dlpack(self, tensor):
+        """Attach a DLPack tensor (e.g. a torch ROCm tensor) as binary data.
+
+        MI355X extension: a device tensor is copied D2H once; an FP32 device
+        tensor for a BF16 / FP16 / FP8 input is narrowed on the GPU first
+        (K4/K5; BF16 truncation = ``serialize_bf16_tensor``).  Returns self."""
+        from tritonclient.utils._device_tensor import wire_bytes
+
+        raw = wire_bytes(tensor, self._datatype, self._shape)
+        self._parameters.pop("shared_memory_region", None)
+        self._parameters.pop("shared_memory_byte_size", None)
+        self._parameters.pop("shared_memory_offset", None)
+        self._data = None
+        self._raw_data = raw
+        self._parameters["binary_data_size"] = len(raw)
+        return self
+
     def set_shared_memory(self, region_name, byte_size, offset=0):
         """Read this input from shared-memory ``region_name`` at ``offset``."""
         self._data = None

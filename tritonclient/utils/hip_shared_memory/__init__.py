@@ -16,9 +16,24 @@ Differences by design:
   copies the whole region every call, ``__init__.py:266-276``);
 * several device-resident DLPack inputs are concatenated with ONE K7
   ``batched_copy`` launch instead of k memcpys;
-* extras: ``offset`` arguments, ``fill_synthetic_data`` (K1 on device), and
-  ``set_shared_memory_region_from_fp32(..., "BF16"|"FP16"|"FP8_*")`` which
-  converts on the GPU (K4/K5) while writing the region.
+* one cached HIP stream and a grow-only device scratch per device
+  (``tritonclient/utils/_hip_device.py``) instead of a stream per call;
+* extras, all opt-in and on the GPU:
+  - ``offset`` arguments;
+  - ``set_shared_memory_region(..., serialize_bytes=True)``: BYTES tensors
+    serialised by K2 inside the region (fixed-width ``np.bytes_`` arrays with
+    no host join at all);
+  - ``set_shared_memory_region(..., datatype="BF16"|"FP16"|"FP8_E4M3"|"FP8_E5M2")``:
+    float arrays converted by K4/K5 on the way in (BF16 by truncation, the
+    wire format of ``serialize_bf16_tensor``);
+  - ``get_contents_as_numpy(..., datatype=...)``: a BF16/FP16/FP8 region read
+    back as float32, widened on the device;
+  - ``fill_synthetic_data`` (K1 Philox).
+
+BYTES semantics are the reference's (``__init__.py:199-231``): an object array
+is the output of ``serialize_byte_tensor`` (its bytes are copied as-is; a
+multi-element object array is concatenated, like the system-shm module) and an
+``np.bytes_`` array is copied raw (``size * itemsize`` bytes).
 """
 
 import base64
@@ -111,56 +126,94 @@ def get_raw_handle(cuda_shm_handle):
 
 
 def _as_bytes(v):
+    """Raw bytes of one input per the reference semantics (no serialisation)."""
     v = np.ascontiguousarray(v)
-    if v.dtype == np.object_ or v.dtype.type == np.bytes_:
-        # a tensor already serialised with serialize_byte_tensor (0-d / 1 element)
+    if v.dtype == np.object_:
+        # the output of serialize_byte_tensor: 0-d / 1-element wrapper of bytes
         raw = v.item() if v.size == 1 else b"".join(v.ravel().tolist())
         return np.frombuffer(raw, dtype=np.uint8)
-    return v.reshape(-1).view(np.uint8)
+    return v.reshape(-1).view(np.uint8)  # np.bytes_ too: size * itemsize raw bytes
 
 
-def _is_unserialized_bytes(v):
-    """An object/bytes tensor of several elements that is NOT the output of
-    serialize_byte_tensor (which is a single bytes blob)."""
-    return (v.dtype == np.object_ or v.dtype.type == np.bytes_) and v.size > 1
+_NARROW = {"BF16": None, "FP16": np.float16, "FP8_E4M3": None, "FP8_E5M2": None}
 
 
-def _pack_bytes_on_device(hip, handle, dst, elems):
-    """K2: serialise a BYTES tensor straight into device memory.  The payload
-    bytes and u32 lengths go H2D once; the <u32 len>||bytes stream is built by
-    the pack kernel inside the region (no host-side serialisation pass)."""
-    n = len(elems)
-    lens = np.fromiter((len(e) for e in elems), dtype="<u4", count=n)
-    payload = np.frombuffer(b"".join(elems), dtype=np.uint8)
-    dev = handle._device_id
-    nbytes = int(lens.sum()) + 4 * n
+def _ctx(handle):
+    from .. import _hip_device
+
+    return _hip_device.context(handle._device_id)
+
+
+def _pack_bytes_on_device(hip, ctx, dst, v):
+    """K2: serialise a BYTES tensor straight into device memory at ``dst``.
+    ``np.bytes_`` arrays upload their fixed-width buffer as-is (element i at
+    i * itemsize, lengths with trailing NULs stripped as numpy does); object
+    arrays upload one joined payload.  Returns the serialised size."""
+    v = np.ascontiguousarray(v)
+    n = int(v.size)
+    if n == 0:
+        return 0
+    if v.dtype.type == np.bytes_:
+        flat = v.reshape(-1)
+        lens = np.char.str_len(flat).astype("<u4")
+        payload = flat.view(np.uint8)
+        stride = v.dtype.itemsize
+    else:
+        from tritonclient.utils import _element_bytes
+
+        elems = _element_bytes(v)
+        lens = np.fromiter((len(e) for e in elems), dtype="<u4", count=n)
+        payload = np.frombuffer(b"".join(elems), dtype=np.uint8)
+        stride = 0
+    nbytes = int(lens.sum(dtype=np.uint64)) + 4 * n
     ws_n = hip.pack_bytes_workspace(n)
-    scratch = hip.malloc(dev, max(16, payload.size) + 4 * n + ws_n + 32)
-    try:
-        d_payload = scratch
-        d_lens = (scratch + max(16, payload.size) + 15) & ~15
-        d_ws = (d_lens + 4 * n + 15) & ~15
-        if payload.size:
-            hip.memcpy_h2d(d_payload, payload, payload.size, dev)
-        hip.memcpy_h2d(d_lens, lens, 4 * n, dev)
-        s = hip.Stream(dev)
-        try:
-            hip.pack_bytes(d_payload, d_lens, n, dst, d_ws, s.handle)
-            s.synchronize()
-        finally:
-            s.close()
-    finally:
-        hip.free(dev, scratch)
+    pay_n = (max(16, payload.size) + 255) & ~255
+    len_n = (4 * n + 255) & ~255
+    base = ctx.scratch(pay_n + len_n + ws_n)
+    d_payload, d_lens, d_ws = base, base + pay_n, base + pay_n + len_n
+    if payload.size:
+        hip.memcpy_async(d_payload, payload.ctypes.data, payload.size, ctx.stream.handle)
+    hip.memcpy_async(d_lens, lens.ctypes.data, 4 * n, ctx.stream.handle)
+    if stride:
+        hip.pack_bytes_strided(d_payload, stride, d_lens, n, dst, d_ws, ctx.stream.handle)
+    else:
+        hip.pack_bytes(d_payload, d_lens, n, dst, d_ws, ctx.stream.handle)
+    ctx.stream.synchronize()  # the host arrays above must outlive the async copies
     return nbytes
 
 
-def set_shared_memory_region(cuda_shm_handle, input_values, offset=0):
+def _convert_into(hip, ctx, dst, arr, datatype):
+    """K4/K5: float array -> ``datatype`` at device ``dst`` (any alignment)."""
+    from triton_client_amd.ops import dtypes
+
+    a = np.ascontiguousarray(arr, dtype=np.float32)
+    n = a.size
+    out_bytes = n * dtypes.SIZES[datatype]
+    if n == 0:
+        return 0
+    src_n = (a.nbytes + 255) & ~255
+    tmp = ctx.scratch(src_n + (out_bytes + 255 & ~255))
+    hip.memcpy_async(tmp, a.ctypes.data, a.nbytes, ctx.stream.handle)
+    if dst % 16 == 0:
+        hip.convert(tmp, "FP32", dst, datatype, n, "trunc", ctx.stream.handle)
+    else:  # the kernel wants 16-B aligned operands: convert in scratch, then copy
+        hip.convert(tmp, "FP32", tmp + src_n, datatype, n, "trunc", ctx.stream.handle)
+        hip.memcpy_async(dst, tmp + src_n, out_bytes, ctx.stream.handle)
+    ctx.stream.synchronize()
+    return out_bytes
+
+
+def set_shared_memory_region(cuda_shm_handle, input_values, offset=0, serialize_bytes=False, datatype=None):
     """Copy numpy arrays back-to-back into the region starting at ``offset``.
 
-    BYTES arrays already serialised with ``serialize_byte_tensor`` are copied
-    as-is (reference behaviour, tc/utils/cuda_shared_memory/__init__.py:199-231).
-    An UNserialised BYTES tensor (object/bytes array of several elements) is
-    serialised on the device by K2 directly into the region.
+    Reference behaviour (tc/utils/cuda_shared_memory/__init__.py:173-239):
+    arrays are copied as raw bytes; BYTES object arrays are expected to be the
+    output of ``serialize_byte_tensor``.  Opt-in device work (MI355X):
+
+    * ``serialize_bytes=True``: object / ``np.bytes_`` arrays are UNserialised
+      BYTES tensors; K2 writes the ``<u32 len>||bytes`` stream into the region;
+    * ``datatype`` in BF16 / FP16 / FP8_E4M3 / FP8_E5M2: float arrays are
+      converted on the GPU (K4/K5; BF16 truncates like serialize_bf16_tensor).
     """
     _check_handle(cuda_shm_handle)
     if not isinstance(input_values, (list, tuple)):
@@ -168,14 +221,24 @@ def set_shared_memory_region(cuda_shm_handle, input_values, offset=0):
     for v in input_values:
         if not isinstance(v, np.ndarray):
             raise CudaSharedMemoryException("input_values must be specified as a list/tuple of numpy arrays")
+    if datatype is not None and datatype not in _NARROW:
+        raise CudaSharedMemoryException("datatype must be one of %s" % (sorted(_NARROW),))
     hip = _hip()
-    from tritonclient.utils import _element_bytes
+    from triton_client_amd.ops import dtypes
 
-    plan = []  # (kind, payload, nbytes)
+    plan = []  # (kind, value, nbytes)
     for v in input_values:
-        if _is_unserialized_bytes(v):
-            elems = _element_bytes(np.ascontiguousarray(v))
-            plan.append(("k2", elems, sum(len(e) for e in elems) + 4 * len(elems)))
+        is_bytes = v.dtype == np.object_ or v.dtype.type == np.bytes_
+        if is_bytes and serialize_bytes:
+            if v.dtype.type == np.bytes_:
+                nb = int(np.char.str_len(v.reshape(-1)).sum(dtype=np.uint64)) + 4 * v.size
+            else:
+                from tritonclient.utils import _element_bytes
+
+                nb = sum(len(e) for e in _element_bytes(np.ascontiguousarray(v))) + 4 * v.size
+            plan.append(("k2", v, nb))
+        elif datatype is not None and v.dtype.kind == "f" and v.dtype != _NARROW[datatype]:
+            plan.append(("cvt", v, v.size * dtypes.SIZES[datatype]))  # float -> narrow on the GPU
         else:
             b = _as_bytes(v)
             plan.append(("copy", b, b.size))
@@ -185,25 +248,67 @@ def set_shared_memory_region(cuda_shm_handle, input_values, offset=0):
             "unable to set values in cuda shared memory: %d bytes exceed the region size %d"
             % (total, cuda_shm_handle._byte_size)
         )
+    ctx = _ctx(cuda_shm_handle)
     try:
-        cur = cuda_shm_handle._base_addr + offset
-        for kind, b, nb in plan:
-            if kind == "k2":
-                _pack_bytes_on_device(hip, cuda_shm_handle, cur, b)
-            elif nb:
-                hip.memcpy_h2d(cur, b, nb, cuda_shm_handle._device_id)
-            cur += nb
+        with ctx.lock:
+            cur = cuda_shm_handle._base_addr + offset
+            for kind, b, nb in plan:
+                if kind == "k2":
+                    _pack_bytes_on_device(hip, ctx, cur, b)
+                elif kind == "cvt":
+                    _convert_into(hip, ctx, cur, b, datatype)
+                elif nb:
+                    hip.memcpy_async(cur, b.ctypes.data, nb, ctx.stream.handle)
+                cur += nb
+            ctx.stream.synchronize()
     except Exception as ex:
         raise CudaSharedMemoryException("unable to set values in cuda shared memory") from ex
 
 
-def get_contents_as_numpy(cuda_shm_handle, datatype, shape, offset=0):
-    """Copy region contents back to the host as a numpy array."""
+def get_contents_as_numpy(cuda_shm_handle, datatype, shape, offset=0, region_datatype=None):
+    """Copy region contents back to the host as a numpy array.
+
+    Only the requested bytes are copied (the reference copies the whole
+    region every call, tc/utils/cuda_shared_memory/__init__.py:266-276).
+    BYTES: K3 indexes the ``<u32 len>||bytes`` chain on the device, then only
+    the bytes the elements span come back.  ``region_datatype`` (BF16 / FP16 /
+    FP8_E4M3 / FP8_E5M2) with a float32 ``datatype``: the region holds that
+    narrow type and is widened to float32 on the GPU before the copy.
+    """
     _check_handle(cuda_shm_handle)
     hip = _hip()
     dt = np.dtype(datatype)
     n = int(np.prod(shape)) if len(shape) else 1
     size = cuda_shm_handle._byte_size
+    dev = cuda_shm_handle._device_id
+    src = cuda_shm_handle._base_addr + offset
+    if region_datatype is not None and region_datatype != "FP32":
+        from triton_client_amd.ops import dtypes
+
+        if region_datatype not in _NARROW or dt != np.float32:
+            raise CudaSharedMemoryException("region_datatype %r needs datatype float32" % (region_datatype,))
+        need = n * dtypes.SIZES[region_datatype]
+        if size < offset + need:
+            raise CudaSharedMemoryException(
+                "The size of the shared memory region is insufficient to provide numpy array with requested size"
+            )
+        out = np.empty(shape, dtype=np.float32)
+        if n:
+            ctx = _ctx(cuda_shm_handle)
+            try:
+                with ctx.lock:
+                    in_n = (need + 255) & ~255
+                    tmp = ctx.scratch(in_n + 4 * n)
+                    s = ctx.stream.handle
+                    if src % 16:
+                        hip.memcpy_async(tmp, src, need, s)
+                        src = tmp
+                    hip.convert(src, region_datatype, tmp + in_n, "FP32", n, "trunc", s)
+                    hip.memcpy_async(out.ctypes.data, tmp + in_n, 4 * n, s)
+                    ctx.stream.synchronize()
+            except Exception as ex:
+                raise CudaSharedMemoryException("failed to read cuda shared memory results") from ex
+        return out
     if dt != np.object_ and dt.type != np.bytes_:
         need = n * dt.itemsize
         if size < offset + need:
@@ -213,48 +318,43 @@ def get_contents_as_numpy(cuda_shm_handle, datatype, shape, offset=0):
         out = np.empty(shape, dtype=dt)
         if need:
             try:
-                hip.memcpy_d2h(out, cuda_shm_handle._base_addr + offset, need, cuda_shm_handle._device_id)
+                hip.memcpy_d2h(out, src, need, dev)
             except Exception as ex:
                 raise CudaSharedMemoryException("failed to read cuda shared memory results") from ex
         return out
-    # BYTES: K3 indexes the <u32 len>||bytes chain on the device (parallel
-    # block walk for large tensors), then only the bytes the elements span
-    # come back to the host and are sliced without a host-side walk
-    dev = cuda_shm_handle._device_id
     nbytes = size - offset
     out = np.empty(n, dtype=np.object_)
     if n == 0:
         return out.reshape(shape)
-    scratch = hip.malloc(dev, 12 * n + 32)
+    ctx = _ctx(cuda_shm_handle)
     try:
-        d_offs, d_lens = scratch, scratch + 8 * n
-        d_status = (d_lens + 4 * n + 15) & ~15
-        s = hip.Stream(dev)
-        try:
-            hip.index_bytes(cuda_shm_handle._base_addr + offset, nbytes, n, d_offs, d_lens, d_status, s.handle)
-            s.synchronize()
-        finally:
-            s.close()
-        status = np.empty(4, dtype=np.int32)
-        hip.memcpy_d2h(status, d_status, 16, dev)
-        if status[0] != 0:
-            raise CudaSharedMemoryException(
-                "BYTES element runs past the end of the region" if status[0] < 0 else
-                "the region holds %d BYTES elements, %d requested" % (int(status[2:4].view(np.uint64)[0]), n))
-        offs = np.empty(n, dtype=np.uint64)
-        lens = np.empty(n, dtype=np.uint32)
-        hip.memcpy_d2h(offs, d_offs, 8 * n, dev)
-        hip.memcpy_d2h(lens, d_lens, 4 * n, dev)
+        with ctx.lock:
+            base = ctx.scratch(12 * n + 64)
+            d_offs, d_lens = base, base + 8 * n
+            d_status = (d_lens + 4 * n + 15) & ~15
+            # K3 sizes its scan window from n (a small tensor in a large
+            # region is not walked to the region's end) and synchronises
+            hip.index_bytes(src, nbytes, n, d_offs, d_lens, d_status, ctx.stream.handle)
+            status = np.empty(4, dtype=np.int32)
+            hip.memcpy_async(status.ctypes.data, d_status, 16, ctx.stream.handle)
+            ctx.stream.synchronize()
+            if status[0] != 0:
+                raise CudaSharedMemoryException(
+                    "BYTES element runs past the end of the region" if status[0] < 0 else
+                    "the region holds %d BYTES elements, %d requested" % (int(status[2:4].view(np.uint64)[0]), n))
+            offs = np.empty(n, dtype=np.uint64)
+            lens = np.empty(n, dtype=np.uint32)
+            hip.memcpy_async(offs.ctypes.data, d_offs, 8 * n, ctx.stream.handle)
+            hip.memcpy_async(lens.ctypes.data, d_lens, 4 * n, ctx.stream.handle)
+            ctx.stream.synchronize()
     except CudaSharedMemoryException:
         raise
     except Exception as ex:
         raise CudaSharedMemoryException("failed to read cuda shared memory results") from ex
-    finally:
-        hip.free(dev, scratch)
     end = int(offs[-1]) + int(lens[-1])
     host = np.empty(end, dtype=np.uint8)
     try:
-        hip.memcpy_d2h(host, cuda_shm_handle._base_addr + offset, end, dev)
+        hip.memcpy_d2h(host, src, end, dev)
     except Exception as ex:
         raise CudaSharedMemoryException("failed to read cuda shared memory results") from ex
     mv = memoryview(host)
@@ -269,7 +369,9 @@ def set_shared_memory_region_from_dlpack(cuda_shm_handle, input_values, offset=0
     """
     _check_handle(cuda_shm_handle)
     hip = _hip()
-    stream = hip.Stream(cuda_shm_handle._device_id)
+    ctx = _ctx(cuda_shm_handle)
+    stream = ctx.stream
+    ctx.lock.acquire()
     try:
         consumed = []
         for v in input_values:
@@ -309,7 +411,7 @@ def set_shared_memory_region_from_dlpack(cuda_shm_handle, input_values, offset=0
     except Exception as ex:
         raise CudaSharedMemoryException("unable to set values in cuda shared memory") from ex
     finally:
-        stream.close()
+        ctx.lock.release()
 
 
 def as_shared_memory_tensor(cuda_shm_handle, datatype, shape, offset=0):
@@ -352,18 +454,17 @@ def fill_synthetic_data(cuda_shm_handle, datatype, n_elems, mode="random", lo=0.
         raise CudaSharedMemoryException("synthetic data exceeds the region size")
     m = {"zero": hip.SYNTH_ZERO, "constant": hip.SYNTH_CONST, "random": hip.SYNTH_UNIFORM,
          "normal": hip.SYNTH_NORMAL}[mode]
-    s = hip.Stream(cuda_shm_handle._device_id)
-    try:
+    ctx = _ctx(cuda_shm_handle)
+    with ctx.lock:
         hip.synth_fill(cuda_shm_handle._base_addr + offset, n_elems, datatype, m, lo, hi, seed,
-                       stream_id, s.handle)
-        s.synchronize()
-    finally:
-        s.close()
+                       stream_id, ctx.stream.handle)
+        ctx.stream.synchronize()
 
 
 def set_shared_memory_region_from_fp32(cuda_shm_handle, array, datatype, offset=0, rounding="trunc"):
     """Upload an fp32 array and convert it on the GPU into ``datatype``
-    (BF16 truncation by default = the wire format of serialize_bf16_tensor)."""
+    (BF16 truncation by default = the wire format of serialize_bf16_tensor;
+    ``rounding="rne"`` rounds to nearest even)."""
     _check_handle(cuda_shm_handle)
     hip = _hip()
     from triton_client_amd.ops import dtypes
@@ -373,16 +474,12 @@ def set_shared_memory_region_from_fp32(cuda_shm_handle, array, datatype, offset=
     out_bytes = n * dtypes.SIZES[datatype]
     if offset + out_bytes > cuda_shm_handle._byte_size:
         raise CudaSharedMemoryException("converted data exceeds the region size")
-    dev = cuda_shm_handle._device_id
-    tmp = hip.malloc(dev, max(a.nbytes, 16))
-    s = hip.Stream(dev)
-    try:
-        hip.memcpy_h2d(tmp, a, a.nbytes, dev)
-        dst = cuda_shm_handle._base_addr + offset
-        if dst % 16:
-            raise CudaSharedMemoryException("offset must be 16-byte aligned for device conversion")
-        hip.convert(tmp, "FP32", dst, datatype, n, rounding, s.handle)
-        s.synchronize()
-    finally:
-        s.close()
-        hip.free(dev, tmp)
+    dst = cuda_shm_handle._base_addr + offset
+    if dst % 16:
+        raise CudaSharedMemoryException("offset must be 16-byte aligned for device conversion")
+    ctx = _ctx(cuda_shm_handle)
+    with ctx.lock:
+        tmp = ctx.scratch(max(a.nbytes, 16))
+        hip.memcpy_async(tmp, a.ctypes.data, a.nbytes, ctx.stream.handle)
+        hip.convert(tmp, "FP32", dst, datatype, n, rounding, ctx.stream.handle)
+        ctx.stream.synchronize()

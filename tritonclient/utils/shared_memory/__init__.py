@@ -125,8 +125,14 @@ def create_shared_memory_region(triton_shm_name, shm_key, byte_size):
     return handle
 
 
-def set_shared_memory_region(shm_handle, input_values, offset=0):
-    """Copy a list of numpy arrays back-to-back into the region from ``offset``."""
+def set_shared_memory_region(shm_handle, input_values, offset=0, serialize_bytes=False):
+    """Copy a list of numpy arrays back-to-back into the region from ``offset``.
+
+    Reference semantics: object arrays are the output of
+    ``serialize_byte_tensor`` and are copied as-is, ``np.bytes_`` arrays are
+    copied raw.  ``serialize_bytes=True`` (same option as the HIP module)
+    treats object / ``np.bytes_`` arrays as UNserialised BYTES tensors and
+    writes their ``<u32 len>||bytes`` form."""
     if not isinstance(input_values, (list, tuple)):
         _raise_error("input_values must be specified as a list/tuple of numpy arrays")
     for v in input_values:
@@ -135,6 +141,12 @@ def set_shared_memory_region(shm_handle, input_values, offset=0):
     lib = _load()
     cur = offset
     for v in input_values:
+        if serialize_bytes and (v.dtype == np.object_ or v.dtype.type == np.bytes_):
+            from tritonclient.utils import serialize_byte_tensor
+
+            v = serialize_byte_tensor(v) if v.size else np.empty(0, np.uint8)
+            if v.dtype != np.object_:
+                continue
         if v.dtype == np.object_:
             # A serialised BYTES tensor (0-d object array wrapping bytes) or a
             # flat object array of bytes produced by serialize_byte_tensor.
