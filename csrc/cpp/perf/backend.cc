@@ -194,22 +194,38 @@ Error Backend::UnregisterDevice(const std::string& name)
   return grpc_ ? grpc_->UnregisterCudaSharedMemory(name, headers_) : http_->UnregisterCudaSharedMemory(name, headers_);
 }
 
+// --compression-algorithm / --grpc-compression-algorithm
+static grpc_compression_algorithm GrpcCompression(const std::string& c)
+{
+  return c == "gzip" ? GRPC_COMPRESS_GZIP : c == "deflate" ? GRPC_COMPRESS_DEFLATE : GRPC_COMPRESS_NONE;
+}
+
+static tc::InferenceServerHttpClient::CompressionType HttpCompression(const std::string& c)
+{
+  using CT = tc::InferenceServerHttpClient::CompressionType;
+  return c == "gzip" ? CT::GZIP : c == "deflate" ? CT::DEFLATE : CT::NONE;
+}
+
 Error Backend::AsyncInfer(std::function<void(InferResult*)> cb, const InferOptions& opt,
                           const std::vector<InferInput*>& in, const std::vector<const InferRequestedOutput*>& out)
 {
-  return grpc_ ? grpc_->AsyncInfer(cb, opt, in, out, headers_) : http_->AsyncInfer(cb, opt, in, out, headers_);
+  if (grpc_) return grpc_->AsyncInfer(cb, opt, in, out, headers_, GrpcCompression(o_.compression));
+  const auto ct = HttpCompression(o_.compression);
+  return http_->AsyncInfer(cb, opt, in, out, headers_, tc::Parameters(), ct, ct);
 }
 
 Error Backend::SyncInfer(InferResult** r, const InferOptions& opt, const std::vector<InferInput*>& in,
                          const std::vector<const InferRequestedOutput*>& out)
 {
-  return grpc_ ? grpc_->Infer(r, opt, in, out, headers_) : http_->Infer(r, opt, in, out, headers_);
+  if (grpc_) return grpc_->Infer(r, opt, in, out, headers_, GrpcCompression(o_.compression));
+  const auto ct = HttpCompression(o_.compression);
+  return http_->Infer(r, opt, in, out, headers_, tc::Parameters(), ct, ct);
 }
 
 Error Backend::StartStream(std::function<void(InferResult*)> cb)
 {
   if (!grpc_) return Error("streaming requires gRPC");
-  return grpc_->StartStream(cb, true, 0, headers_);
+  return grpc_->StartStream(cb, true, 0, headers_, GrpcCompression(o_.compression));
 }
 
 Error Backend::StreamInfer(const InferOptions& opt, const std::vector<InferInput*>& in,
@@ -498,6 +514,10 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
       Error e = InferInput::Create(&in, t.name, full, t.datatype);
       if (!e.IsOk()) return e;
       inputs_[ent].push_back(in);
+      if (o.input_tensor_format == "json") {
+        e = in->SetBinaryData(false);  // HTTP: the tensor goes as an inline JSON "data" array
+        if (!e.IsOk()) return e;
+      }
       const std::string rname = prefix_ + "in_" + t.name + (ent ? "_e" + std::to_string(ent) : std::string());
 
       // device-synthesised data (HIP shm, random): K1 numeric fill, or K1
@@ -663,6 +683,10 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
       InferRequestedOutput* out;
       Error e = InferRequestedOutput::Create(&out, t.name);
       if (!e.IsOk()) return e;
+      if (o.output_tensor_format == "json" && !shm) {
+        e = out->SetBinaryData(false);
+        if (!e.IsOk()) return e;
+      }
       outputs_[s].push_back(out);
       outputs_c_[s].push_back(out);
       if (!shm) continue;
@@ -687,6 +711,10 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
   if (used_k1) d2 << ", inputs filled on device by K1 Philox (seed " << o.seed << ")";
   if (used_k2) d2 << " + K2 BYTES packing";
   if (used_k4) d2 << ", JSON FP16/BF16 values narrowed on device by K4/K5";
+  if (o.input_tensor_format == "json" || o.output_tensor_format == "json")
+    d2 << ", tensors in/out as " << o.input_tensor_format << "/" << o.output_tensor_format;
+  if (o.compression != "none") d2 << ", " << o.compression << " compression";
+  if (!o.request_parameters.empty()) d2 << ", " << o.request_parameters.size() << " request parameter(s)";
   if (!fill_inputs && !input_regions_.empty()) d2 << ", inputs replicated by fan-out";
   if (!desc.str().empty()) d2 << "; " << desc.str();
   describe_ = d2.str();

@@ -17,6 +17,7 @@ LoadEngine::LoadEngine(const Options& o, Backend* be, DataSet* data, size_t max_
   for (auto& s : slots_) {
     s.opt = InferOptions(o.model);
     s.opt.model_version_ = o.version;
+    for (const auto& kv : o.request_parameters) s.opt.request_parameters[kv.first] = kv.second;  // --request-parameter
   }
   if (!o.request_intervals_file.empty()) {
     std::ifstream f(o.request_intervals_file);

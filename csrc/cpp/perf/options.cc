@@ -18,6 +18,7 @@ enum LongOnly {
   OPT_NUM_CLIENTS, OPT_NO_SERVER_STATS, OPT_GPUS, OPT_DEVICES, OPT_FANOUT, OPT_LOAD_PER_GPU, OPT_MEAS_INTERVAL, OPT_STABILITY, OPT_MAX_TRIALS, OPT_LAT_THRESH,
   OPT_SSL_GRPC_USE, OPT_SSL_GRPC_ROOT, OPT_SSL_GRPC_KEY, OPT_SSL_GRPC_CHAIN, OPT_SSL_HTTPS_PEER, OPT_SSL_HTTPS_HOST,
   OPT_SSL_HTTPS_CA, OPT_SSL_HTTPS_CERT, OPT_SSL_HTTPS_CERT_TYPE, OPT_SSL_HTTPS_KEY, OPT_SSL_HTTPS_KEY_TYPE,
+  OPT_IN_FORMAT, OPT_OUT_FORMAT, OPT_GRPC_COMPRESSION, OPT_COMPRESSION, OPT_REQUEST_PARAM,
 };
 
 bool ParseU64(const std::string& s, uint64_t* v)
@@ -106,6 +107,12 @@ std::string Usage()
       "                                   others (RCCL broadcast / xGMI peer-copy star / host copies)\n"
       "  [ext] --load-per-gpu             every GPU gets the full concurrency / rate (weak scaling);\n"
       "                                   default: the load is split over the GPUs\n"
+      "  --input-tensor-format binary|json, --output-tensor-format binary|json\n"
+      "                                   HTTP tensor encoding (json: inline \"data\" arrays)\n"
+      "  --grpc-compression-algorithm none|gzip|deflate   gRPC message compression\n"
+      "  [ext] --compression-algorithm none|gzip|deflate  the same for gRPC; for HTTP: request body and\n"
+      "                                   response (Content-Encoding / Accept-Encoding)\n"
+      "  --request-parameter name:value:type   custom request parameter (bool|int|string|double), repeatable\n"
       "  --ssl-grpc-use-ssl, --ssl-grpc-root-certifications-file F, --ssl-grpc-private-key-file F,\n"
       "  --ssl-grpc-certificate-chain-file F          gRPC over TLS (mutual TLS with key + chain)\n"
       "  --ssl-https-verify-peer 0|1, --ssl-https-verify-host 0|1|2, --ssl-https-ca-certificates-file F,\n"
@@ -171,6 +178,11 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
       {"ssl-https-client-certificate-type", required_argument, nullptr, OPT_SSL_HTTPS_CERT_TYPE},
       {"ssl-https-private-key-file", required_argument, nullptr, OPT_SSL_HTTPS_KEY},
       {"ssl-https-private-key-type", required_argument, nullptr, OPT_SSL_HTTPS_KEY_TYPE},
+      {"input-tensor-format", required_argument, nullptr, OPT_IN_FORMAT},
+      {"output-tensor-format", required_argument, nullptr, OPT_OUT_FORMAT},
+      {"grpc-compression-algorithm", required_argument, nullptr, OPT_GRPC_COMPRESSION},
+      {"compression-algorithm", required_argument, nullptr, OPT_COMPRESSION},
+      {"request-parameter", required_argument, nullptr, OPT_REQUEST_PARAM},
       {"verbose", no_argument, nullptr, 'v'},
       {"help", no_argument, nullptr, 'h'},
       {nullptr, 0, nullptr, 0}};
@@ -370,6 +382,42 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
         (c == OPT_SSL_HTTPS_CERT_TYPE ? o->ssl.https_cert_der : o->ssl.https_key_der) = arg == "DER";
         o->ssl.https = true;
         break;
+      case OPT_IN_FORMAT:
+      case OPT_OUT_FORMAT:
+        if (arg != "binary" && arg != "json") return Error("tensor formats are binary or json, got '" + arg + "'");
+        (c == OPT_IN_FORMAT ? o->input_tensor_format : o->output_tensor_format) = arg;
+        break;
+      case OPT_GRPC_COMPRESSION:
+      case OPT_COMPRESSION:
+        if (arg != "none" && arg != "gzip" && arg != "deflate")
+          return Error("compression algorithms are none, gzip or deflate, got '" + arg + "'");
+        o->compression = arg;
+        break;
+      case OPT_REQUEST_PARAM: {
+        // name:value:type, type one of bool|int|string|double (value may contain ':')
+        const size_t a = arg.find(':'), b = arg.rfind(':');
+        if (a == std::string::npos || a == b || a == 0) return Error("--request-parameter expects name:value:type");
+        triton::client::RequestParameter rp;
+        rp.name = arg.substr(0, a);
+        rp.value = arg.substr(a + 1, b - a - 1);
+        rp.type = arg.substr(b + 1);
+        if (rp.type != "bool" && rp.type != "int" && rp.type != "string" && rp.type != "double")
+          return Error("--request-parameter type must be bool, int, string or double, got '" + rp.type + "'");
+        if (rp.type == "bool" && rp.value != "true" && rp.value != "false")
+          return Error("--request-parameter bool values are true or false");
+        if (rp.type == "int") {
+          char* end = nullptr;
+          strtoll(rp.value.c_str(), &end, 10);
+          if (rp.value.empty() || *end) return Error("--request-parameter: bad int '" + rp.value + "'");
+        }
+        if (rp.type == "double") {
+          char* end = nullptr;
+          strtod(rp.value.c_str(), &end);
+          if (rp.value.empty() || *end) return Error("--request-parameter: bad double '" + rp.value + "'");
+        }
+        o->request_parameters[rp.name] = rp;
+        break;
+      }
       case 'v': o->verbose = true; break;
       case 'h': *help = true; return Error::Success;
       default: {
@@ -396,6 +444,8 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
     return Error("-u lists " + std::to_string(o->urls.size()) + " URLs for " + std::to_string(o->devices.size()) +
                  " GPUs (give one URL, or one per GPU)");
   if (o->streaming && o->protocol != "grpc") return Error("--streaming requires -i grpc");
+  if ((o->input_tensor_format == "json" || o->output_tensor_format == "json") && o->protocol != "http")
+    return Error("--input-tensor-format / --output-tensor-format json need -i http");
   if (!o->preregistered_inputs.empty() && o->shared_memory == "none")
     return Error("--shared-memory-input requires --shared-memory system|hip");
   return Error::Success;

@@ -122,6 +122,10 @@ struct Options {
   bool resume = false;  // --resume: continue a sweep checkpointed in json_file
   bool verbose_csv = false;
   bool collect_server_stats = true;
+  std::string input_tensor_format = "binary";   // HTTP: binary | json (inline "data")
+  std::string output_tensor_format = "binary";
+  std::string compression = "none";              // none | gzip | deflate (gRPC messages / HTTP bodies)
+  std::map<std::string, triton::client::RequestParameter> request_parameters;
 };
 
 /// Parse perf_analyzer flags.  Returns an error for unknown/invalid flags;

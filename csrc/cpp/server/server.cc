@@ -1540,10 +1540,12 @@ void Server::OnRequestComplete(Conn* c, Stream* st)
     }
     std::vector<std::string> msgs;
     std::string err;
+    const bool compressed = in.size() >= 5 && in[0] != 0;
     if (!PopMessages(st, &msgs, &err) || msgs.size() != 1) {
       Reply(c, st, nullptr, kInternal, err.empty() ? "expected one request message" : err);
       return;
     }
+    if (compressed) n_inflated++;  // a grpc-encoding gzip/deflate message, decompressed here
     if (TryNative(c, st, msgs[0].data(), msgs[0].size(), &msgs[0])) return;
     // not native: forward the (decompressed) message we already popped
     st->inbuf.clear();

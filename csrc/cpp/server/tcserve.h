@@ -77,8 +77,9 @@ int32_t tcserve_shm_busy(void* server, int32_t kind, uint64_t ptr);
 int32_t tcserve_model_stats(void* server, const char* name, uint64_t* out);
 /// Per batch size rows of 7: batch_size, count, in_ns, infer_ns, out_ns, (reserved x2). Returns row count.
 int32_t tcserve_batch_stats(void* server, const char* name, uint64_t* out, int32_t max_rows);
-/// Counters: [0] native requests, [1] proxied calls, [2] connections accepted, [3] native REST
-/// requests with a gzip/deflate body, [4] native REST responses sent compressed.
+/// Counters: [0] native requests, [1] proxied calls, [2] connections accepted, [3] REST requests
+/// with a gzip/deflate body + gRPC infer messages that arrived compressed, [4] native REST
+/// responses sent compressed.
 int32_t tcserve_counters(void* server, uint64_t* out);
 void tcserve_destroy(void* server);
 

@@ -246,3 +246,69 @@ def test_json_data_multiple_entries_cycle(cpu_server, tmp_path):
     r = _pa(["-m", "simple", "-u", cpu_server.http_url, "--input-data", d, "-p", "200", "-r", "3", "-s", "60"])
     assert r.returncode == 0, r.stderr
     assert "3 entries, cycled per request" in r.stdout
+
+
+def _counters(srv):
+    nf = srv.server.native_frontend
+    return nf.counters() if nf is not None else None
+
+
+def test_tensor_format_json_reaches_server_as_json(cpu_server):
+    """--input-tensor-format / --output-tensor-format json: every request
+    carries inline JSON "data" (the reference's ConvertBinaryInputToJSON path,
+    http_client.cc:580-678) and asks for JSON outputs; the server counts both."""
+    ws = cpu_server.server.wire_stats
+    before_in, before_out = ws["json_input_tensors"], ws["json_output_tensors"]
+    r = _pa(["-m", "simple", "-u", cpu_server.http_url, "--input-tensor-format", "json", "--output-tensor-format",
+             "json", "--measurement-mode", "count_windows", "--measurement-request-count", "50", "-r", "3"])
+    assert r.returncode == 0, r.stderr
+    assert "tensors in/out as json/json" in r.stdout
+    n_in, n_out = ws["json_input_tensors"] - before_in, ws["json_output_tensors"] - before_out
+    assert n_in >= 2 * 50 and n_out >= 2 * 50, (n_in, n_out)  # simple: 2 inputs, 2 outputs per request
+    r = _pa(["-m", "simple", "-u", cpu_server.grpc_url, "-i", "grpc", "--input-tensor-format", "json"])
+    assert r.returncode == 1 and "need -i http" in r.stderr
+
+
+@pytest.mark.parametrize("proto,algo", [("http", "gzip"), ("http", "deflate"), ("grpc", "gzip"), ("grpc", "deflate")])
+def test_compression_reaches_server(cpu_server, proto, algo):
+    """--grpc-compression-algorithm / --compression-algorithm: compressed
+    request bodies (and, over HTTP, compressed responses) served on tcserve's
+    native path; its counters verify what arrived."""
+    c0 = _counters(cpu_server)
+    if c0 is None:
+        pytest.skip("native front end not built")
+    url = cpu_server.http_url if proto == "http" else cpu_server.grpc_url
+    flag = "--grpc-compression-algorithm" if proto == "grpc" else "--compression-algorithm"
+    r = _pa(["-m", "add_sub_batched", "-u", url, "-i", proto, flag, algo, "--measurement-mode", "count_windows",
+             "--measurement-request-count", "40", "-r", "3"])
+    assert r.returncode == 0, r.stderr
+    assert "%s compression" % algo in r.stdout
+    c1 = _counters(cpu_server)
+    assert c1["inflated_requests"] - c0["inflated_requests"] >= 120
+    if proto == "http":
+        assert c1["compressed_responses"] - c0["compressed_responses"] >= 120
+    assert c1["native_requests"] - c0["native_requests"] >= 120
+    r = _pa(["-m", "simple", "--compression-algorithm", "brotli"])
+    assert r.returncode == 1 and "compression" in r.stderr
+
+
+@pytest.mark.parametrize("proto", ["http", "grpc"])
+def test_request_parameters_reach_server(cpu_server, proto):
+    """--request-parameter name:value:type (repeatable) arrives typed on every
+    request (reference common.h:155-159, 230)."""
+    ws = cpu_server.server.wire_stats
+    url = cpu_server.http_url if proto == "http" else cpu_server.grpc_url
+    args = ["-m", "simple", "-u", url, "-i", proto, "--request-parameter", "tenant:a:b:string",
+            "--request-parameter", "max_tokens:42:int", "--request-parameter", "stream:true:bool",
+            "--request-parameter", "temperature:0.5:double", "--measurement-mode", "count_windows",
+            "--measurement-request-count", "30", "-r", "3"]
+    keys = ["param:tenant:str:a:b", "param:max_tokens:int:42", "param:stream:bool:True", "param:temperature:float:0.5"]
+    before = {k: ws[k] for k in keys}
+    r = _pa(args)
+    assert r.returncode == 0, r.stderr
+    assert "4 request parameter(s)" in r.stdout
+    for k in keys:
+        assert ws[k] - before[k] >= 90, (k, ws[k] - before[k], dict(ws))
+    for bad in ("x:1", "x:1:float", "x:maybe:bool", "x:abc:int"):
+        r = _pa(["-m", "simple", "--request-parameter", bad])
+        assert r.returncode == 1 and "request-parameter" in r.stderr, bad

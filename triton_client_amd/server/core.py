@@ -12,6 +12,7 @@ Wire semantics mirror what the reference client expects from a Triton server
 import asyncio
 import base64
 import json
+import collections
 import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -405,6 +406,9 @@ class InferenceServer:
         self.model_listeners = []
         self.native_stats = None
         self.shm_closer = DeferredCloser()
+        # what arrived on the wire through the Python front ends (tests verify
+        # client features end to end: JSON tensors, custom parameters)
+        self.wire_stats = collections.Counter()
         self.sys_shm = SystemShmRegistry(self.shm_listeners, self.shm_closer)
         self.dev_shm = DeviceShmRegistry(self.shm_listeners, self.shm_closer)
         self.executor = ThreadPoolExecutor(max_workers=executor_workers, thread_name_prefix="tcamd-exec")
@@ -727,7 +731,13 @@ class InferenceServer:
         return [(o, None) for o in outputs]
 
     # -- inference entry points -----------------------------------------------------
+    _RESERVED_PARAMS = ("sequence_id", "sequence_start", "sequence_end", "priority", "timeout", "binary_data_output",
+                        "triton_enable_empty_final_response")
+
     async def infer(self, request):
+        for k, v in request.parameters.items():
+            if k not in self._RESERVED_PARAMS:  # custom request parameters, by name / type / value
+                self.wire_stats["param:%s:%s:%s" % (k, type(v).__name__, v)] += 1
         entry, version, inst = self.get_instance(request.model_name, request.model_version)
         if inst.decoupled:
             raise ServerError(

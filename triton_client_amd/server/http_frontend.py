@@ -314,6 +314,7 @@ class HttpFrontend:
                 pos += n
             elif "data" in t:
                 tensor.data = _json_to_array(t["data"], tensor.datatype, tensor.shape)
+                self.s.wire_stats["json_input_tensors"] += 1
             else:
                 raise ServerError("input '%s' has no data" % t["name"])
             req.inputs.append(tensor)
@@ -358,6 +359,7 @@ class HttpFrontend:
                 else:
                     data = o.data.detach().cpu().numpy() if hasattr(o.data, "is_cuda") else o.data
                     d["data"] = _array_to_json(data, o.datatype)
+                    self.s.wire_stats["json_output_tensors"] += 1
             outs.append(d)
         header["outputs"] = outs
         hbytes = _dumps(header).encode()
