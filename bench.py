@@ -149,6 +149,35 @@ def stats_delta(a, b):
     }
 
 
+def batch_stats(client, model):
+    """Per batch size: (executions, compute_input_ns, compute_infer_ns, compute_output_ns)."""
+    st = client.get_inference_statistics(model, as_json=True)
+    out = {}
+    for m in st.get("model_stats", []):
+        for b in m.get("batch_stats", []):
+            bs = int(b["batch_size"])
+            cnt = int(b.get("compute_infer", {}).get("count", 0))
+            ns = [int(b.get(k, {}).get("ns", 0)) for k in ("compute_input", "compute_infer", "compute_output")]
+            c0, i0, f0, o0 = out.get(bs, (0, 0, 0, 0))
+            out[bs] = (c0 + cnt, i0 + ns[0], f0 + ns[1], o0 + ns[2])
+    return out
+
+
+def weighted_compute_us(a, b, rows_per_request):
+    """Request-weighted device time of the batches between two batch_stats
+    snapshots: a request of a 128-row batch waits for that batch's whole
+    execution, so per-request server time must be compared with batch times
+    weighted by the requests they carry, not with the plain per-batch mean
+    (large batches run longer and carry more requests)."""
+    num = den = 0.0
+    for bs, (c1, i1, f1, o1) in b.items():
+        c0, i0, f0, o0 = a.get(bs, (0, 0, 0, 0))
+        reqs = max(bs / float(rows_per_request), 1.0)
+        num += reqs * ((i1 - i0) + (f1 - f0) + (o1 - o0))
+        den += reqs * (c1 - c0)
+    return num / den / 1e3 if den else 0.0
+
+
 def main():
     args = parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -278,8 +307,10 @@ def main():
         lat_w, _, _ = p8.run(max(args.warmup, 1) * per)
         log("warmup done: p50 %.0f us" % percentile_us(lat_w.astype(np.float64), 50))
         st0 = p8.s.server_stats()
+        bst0 = batch_stats(client, model)
         lat, end, elapsed = measure(p8, args.steps, per)
         st1 = p8.s.server_stats()
+        bst1 = batch_stats(client, model)
         wins = windows(end, per, args.steps)
         # the last window holds the closed loop's drain (no new issues), so the
         # stability rule looks at the three windows before it
@@ -291,6 +322,34 @@ def main():
         breakdown = stats_delta(st0, st1)
         breakdown["client_overhead_us_per_request"] = round(
             float(np.mean(lat)) / 1e3 - breakdown["server_us_per_request"], 1)
+        # per-request accounting: queue + the request-weighted device time of
+        # the batch it rode in; what is left is host time nobody timed
+        wc = weighted_compute_us(bst0, bst1, bs)
+        breakdown["compute_us_per_request_weighted"] = round(wc, 1)
+        breakdown["unattributed_us_per_request"] = round(
+            breakdown["server_us_per_request"] - breakdown["queue_us_per_request"] - wc, 1)
+
+        # ---- best throughput with p99 <= 10 ms (same server, lower concurrency) ---------
+        p99c = {"p99_target_us": 10000.0, "points": []}
+        if not cpu:
+            for c in (32, 24, 16):
+                pc = Point(srv, model, bs, c, "data_0_in", in_bytes, local_rank, cpu)
+                points.append(pc)
+                perc = 16 * c
+                pc.run(perc)
+                lc_, _, elc = measure(pc, 4, perc)
+                lg = fanout.gather_arrays(lc_.astype(np.int64)).astype(np.float64)
+                row = {"concurrency": c, "infer_per_sec": round(world * 4 * perc * bs / elc, 1),
+                       "p50_latency_us": round(percentile_us(lg, 50), 1),
+                       "p99_latency_us": round(percentile_us(lg, 99), 1)}
+                p99c["points"].append(row)
+                log("p99-constrained probe c%d: %.0f infer/s p99 %.0f us" % (c, row["infer_per_sec"],
+                                                                             row["p99_latency_us"]))
+            ok = [r for r in p99c["points"] if r["p99_latency_us"] <= p99c["p99_target_us"]]
+            if ok:
+                best = max(ok, key=lambda r: r["infer_per_sec"])
+                p99c.update({"concurrency": best["concurrency"], "infer_per_sec": best["infer_per_sec"],
+                             "p99_latency_us": best["p99_latency_us"]})
 
         # ---- bs=1 on the same server -------------------------------------------------
         _, in1 = make_input("data_1_in", 1)
@@ -355,6 +414,7 @@ def main():
             "stable": bool(fanout.max_over_ranks(0.0 if stable else 1.0) == 0.0),
             "window_infer_per_sec_rank0": [round(w * bs, 1) for w in wins],
             "server_breakdown_rank0": breakdown,
+            "p99_constrained": p99c,
             "bs1": bs1,
             "world_size_reported_by_process_group": dist.get_world_size() if world > 1 else 1,
         }

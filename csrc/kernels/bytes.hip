@@ -271,6 +271,25 @@ __global__ void __launch_bounds__(kBlock) pk_emit(const uint8_t* __restrict__ da
             uint8_t b[16];
           } chunk;
           bool full = true;
+          const uint64_t e_end = e + 1 < cnt ? s_os[e + 1] : Lb;
+          if (!stride && l0 >= (int64_t)t0 && l0 + 16 <= (int64_t)t1 && (uint64_t)l0 >= s_os[e] + 4 &&
+              (uint64_t)l0 + 16 <= e_end) {
+            // fast path: the chunk lies inside one element's payload -> 16
+            // contiguous staged bytes, five dword LDS reads + funnel shifts
+            const uint64_t src = Db + s_os[e] - 4 * (uint64_t)e + ((uint64_t)l0 - s_os[e] - 4) - pay_lo;
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(s_pay) + (src >> 2);
+            const uint32_t sh = (uint32_t)(src & 3);
+            const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+            chunk.v4 = make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                                  __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
+            if (out16) {
+              *reinterpret_cast<uint4*>(out + c * 16) = chunk.v4;
+            } else {
+#pragma unroll
+              for (int k = 0; k < 16; ++k) out[c * 16 + k] = chunk.b[k];
+            }
+            continue;
+          }
 #pragma unroll
           for (int k = 0; k < 16; ++k) {
             const int64_t pos = l0 + k;
@@ -672,6 +691,48 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
   return x;
 }
 
+// Little-endian u32 at byte offset `off` of a 16-B aligned LDS window: two
+// adjacent dword reads (one ds_read2_b32) and a byte funnel shift, instead of
+// four ds_read_u8.
+__device__ __forceinline__ uint32_t lds_le32(const uint8_t* win, uint32_t off) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(win);
+  const uint32_t lo = w[off >> 2], hi = w[(off >> 2) + 1];
+  return __builtin_amdgcn_alignbyte(hi, lo, off & 3);
+}
+
+// One hop of a chain at block-relative position p (p < kXB): returns true while
+// the chain is still inside the block; otherwise *code is final.
+__device__ __forceinline__ bool ix_hop(const uint8_t* win, uint64_t b0, uint64_t nbytes, uint32_t* p, uint32_t* cnt,
+                                       uint32_t* code) {
+  const uint64_t abs = b0 + *p;
+  if (abs + 4 > nbytes) {
+    *code = kXBad;  // truncated length prefix
+    return false;
+  }
+  const uint64_t nx = abs + 4 + (uint64_t)lds_le32(win, *p);
+  if (nx > nbytes) {
+    *code = kXBad;  // element runs past the data
+    return false;
+  }
+  ++*cnt;
+  if (nx == nbytes) {
+    *code = kXEnd;
+    return false;
+  }
+  const uint64_t bend = b0 + kXB;
+  if (nx >= bend) {
+    *code = nx - bend < (uint64_t)kXR ? (uint32_t)(nx - bend) : kXFar;
+    return false;
+  }
+  *p = (uint32_t)(nx - b0);
+  return true;
+}
+
+// Per block: every candidate entry c in [0, kXR) walks only until it leaves
+// the candidate window (phase 1, a few hops, all lanes busy).  Chains from
+// true element starts all leave it at the same position, so phase 2 walks
+// once per DISTINCT window-exit position (typically one: lane 0, serial) to
+// the block exit and hands the result to every candidate that left there.
 __global__ void __launch_bounds__(kBlock) ix_walk(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t nblk,
                                                   uint16_t* __restrict__ tab, uint16_t* __restrict__ tcnt,
                                                   uint32_t* __restrict__ sync) {
@@ -680,55 +741,51 @@ __global__ void __launch_bounds__(kBlock) ix_walk(const uint8_t* __restrict__ bu
   const uint64_t b = (uint64_t)blockIdx.x * kXWaves + wave;
   if (b >= nblk) return;  // wave-uniform; no workgroup barrier below
   uint8_t* win = win_all[wave];
-  const uint64_t b0 = b * kXB, bend = b0 + kXB;
+  const uint64_t b0 = b * kXB;
   ix_stage(buf, nbytes, b0, win, lane);
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  uint64_t p[kXC];
-  uint32_t code[kXC], cnt[kXC];
-  bool live[kXC];
+  constexpr uint32_t kWalk = 0xFFFFFFFFu;  // code of a chain still walking (phase 2 pending)
+  uint32_t p[kXC], cnt[kXC], code[kXC];
 #pragma unroll
   for (int j = 0; j < kXC; ++j) {
-    p[j] = b0 + lane + 64 * j;
+    p[j] = (uint32_t)(lane + 64 * j);
     cnt[j] = 0;
-    code[j] = 0;
-    live[j] = true;
-    if (p[j] >= nbytes) {
-      code[j] = kXEnd;  // at (or past) the end of the data: no element starts here
-      live[j] = false;
-    }
+    code[j] = b0 + p[j] >= nbytes ? (uint32_t)kXEnd : kWalk;  // no element starts at/after the data end
   }
-  // lockstep hops; the kXC chains of a lane are independent (their LDS reads overlap)
-  bool any = live[0] || live[1] || live[2] || live[3];
-  while (__any(any)) {
+  // phase 1: walk while inside the candidate window
+  bool any;
+  do {
+    any = false;
 #pragma unroll
     for (int j = 0; j < kXC; ++j) {
-      if (!live[j]) continue;
-      const uint64_t pj = p[j];
-      if (pj + 4 > nbytes) {
-        code[j] = kXBad;  // truncated length prefix
-        live[j] = false;
-        continue;
-      }
-      const uint8_t* q = win + (pj - b0);
-      const uint32_t L = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-      const uint64_t nx = pj + 4 + (uint64_t)L;
-      if (nx > nbytes) {
-        code[j] = kXBad;  // element runs past the data
-        live[j] = false;
-        continue;
-      }
-      ++cnt[j];
-      p[j] = nx;
-      if (nx == nbytes) {
-        code[j] = kXEnd;
-        live[j] = false;
-      } else if (nx >= bend) {
-        code[j] = nx - bend < (uint64_t)kXR ? (uint32_t)(nx - bend) : kXFar;
-        live[j] = false;
+      if (code[j] == kWalk && p[j] < (uint32_t)kXR) {
+        if (ix_hop(win, b0, nbytes, &p[j], &cnt[j], &code[j])) any = any || p[j] < (uint32_t)kXR;
       }
     }
-    any = live[0] || live[1] || live[2] || live[3];
+  } while (__any(any));
+  // phase 2: one serial walk per distinct window-exit position
+  for (;;) {
+    uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = 0; j < kXC; ++j)
+      if (code[j] == kWalk) m = min(m, p[j]);
+    m = wave_min_u32(m);
+    if (m == 0xFFFFFFFFu) break;
+    uint32_t c2 = 0, n2 = 0;
+    if (lane == 0) {
+      uint32_t q = m;
+      while (ix_hop(win, b0, nbytes, &q, &n2, &c2)) {
+      }
+    }
+    c2 = (uint32_t)__shfl((int)c2, 0, 64);
+    n2 = (uint32_t)__shfl((int)n2, 0, 64);
+#pragma unroll
+    for (int j = 0; j < kXC; ++j)
+      if (code[j] == kWalk && p[j] == m) {
+        code[j] = c2;
+        cnt[j] += n2;
+      }
   }
   uint32_t lmin = 0xFFFFFFFFu, lmax = 0;
 #pragma unroll
@@ -854,8 +911,7 @@ __global__ void __launch_bounds__(kBlock) ix_emit(const uint8_t* __restrict__ bu
     const int m = (int)(want - k0 < 64 ? want - k0 : 64);
     if (lane == 0) {
       for (int i = 0; i < m; ++i) {
-        const uint8_t* q = win + (p - b0);
-        const uint32_t L = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+        const uint32_t L = lds_le32(win, (uint32_t)(p - b0));
         ring_off[wave][i] = p + 4;
         ring_len[wave][i] = L;
         p += 4 + (uint64_t)L;
