@@ -80,6 +80,9 @@ def parse_args(argv=None):
     ap.add_argument("--preferred", default="128")
     ap.add_argument("--idle-dispatch", default="on", choices=["on", "off"])
     ap.add_argument("--cpu", action="store_true", help="no GPU: CPU frontend_sink model, system shm, gloo")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="one-GPU rehearsal of the N-GPU launch: every rank (and its server) on GPU 0, gloo "
+                         "process group, p2p/host fan-out (RCCL cannot put two ranks on one device)")
     ap.add_argument("--server-log", default="")
     ap.add_argument("--model", default="densenet_onnx", choices=["densenet_onnx", "bert_large"])
     ap.add_argument("--sweep", default="1,4,16,64,256", help="bert_large: concurrencies per GPU")
@@ -185,6 +188,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    rehearse = args.rehearse and world > 1
+    # the GPU this rank drives (and its server runs on)
+    dev = 0 if args.rehearse else local_rank
+    if rehearse and args.fanout == "rccl":
+        args.fanout = "p2p"
     if world != args.gpus:
         raise SystemExit("WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -219,7 +227,7 @@ def main():
                 extra += ["--max-batch-size", str(args.max_batch_size)]
         path = args.server_log or os.path.join(log_dir, "bench_server_%s_r%d.log" % (tag, rank))
         # spawned before this process touches the GPU; per-rank port stripes
-        return ServerProcess(device=local_rank, gpu=not cpu, models=model, extra_args=extra, log_path=path,
+        return ServerProcess(device=dev, gpu=not cpu, models=model, extra_args=extra, log_path=path,
                              port_stripe=local_rank if world > 1 else None), path
 
     srv, srv_log = start_server(args.engine, "bert" if bert else args.engine)
@@ -228,9 +236,9 @@ def main():
     import torch.distributed as dist
 
     if not cpu:
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(dev)
     if world > 1:
-        if cpu:
+        if cpu or rehearse:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -263,13 +271,13 @@ def main():
                 raise RuntimeError("fan-out replicas differ across ranks")
             state["client"].register_system_shared_memory(name, key, nbytes)
         else:
-            r = shmod.create_shared_memory_region(name, nbytes, local_rank)
+            r = shmod.create_shared_memory_region(name, nbytes, dev)
             regions.append(r)
             method = fanout.fill_and_fanout(r, "FP32", elems, seed=1234, mode="normal", lo=0.0, hi=1.0,
                                             method=args.fanout)
             if not fanout.verify_replicas(r, nbytes):
                 raise RuntimeError("fan-out replicas differ across ranks")
-            state["client"].register_cuda_shared_memory(name, shmod.get_raw_handle(r), local_rank, nbytes)
+            state["client"].register_cuda_shared_memory(name, shmod.get_raw_handle(r), dev, nbytes)
         return method, nbytes
 
     def measure(point, steps, per):
@@ -295,14 +303,25 @@ def main():
         state["client"] = client
         if bert:
             return bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout, rank, world,
-                              local_rank, cpu)
+                              dev, cpu)
         method, in_bytes = make_input("data_0_in", bs)
+        fan = {"method": method, "replicas_verified": True}
+        if not cpu and world > 1:
+            # X1 (RCCL broadcast) vs X2 (xGMI one-hop star), once, on the headline input
+            # region; a rehearsal on one GPU times p2p and host staging
+            fan["timings"] = fanout.time_fanout(regions[0], in_bytes, ["p2p", "host"] if rehearse else ["rccl", "p2p"])
+            if not fanout.verify_replicas(regions[0], in_bytes):
+                raise RuntimeError("fan-out replicas differ across ranks after the fan-out timing")
+            t_used = fan["timings"].get(method, {})
+            if "us" in t_used:
+                fan["fanout_us"] = t_used["us"]
+            log("fan-out timings: %s" % fan["timings"])
         if not cpu:
-            _sanity_check(client, shmod, bs, local_rank, regions)
+            _sanity_check(client, shmod, bs, dev, regions)
 
         # ---- headline: bs=8 -------------------------------------------------------
         per = args.window * conc
-        p8 = Point(srv, model, bs, conc, "data_0_in", in_bytes, local_rank, cpu)
+        p8 = Point(srv, model, bs, conc, "data_0_in", in_bytes, dev, cpu)
         points.append(p8)
         lat_w, _, _ = p8.run(max(args.warmup, 1) * per)
         log("warmup done: p50 %.0f us" % percentile_us(lat_w.astype(np.float64), 50))
@@ -333,7 +352,7 @@ def main():
         p99c = {"p99_target_us": 10000.0, "points": []}
         if not cpu:
             for c in (32, 24, 16):
-                pc = Point(srv, model, bs, c, "data_0_in", in_bytes, local_rank, cpu)
+                pc = Point(srv, model, bs, c, "data_0_in", in_bytes, dev, cpu)
                 points.append(pc)
                 perc = 16 * c
                 pc.run(perc)
@@ -353,7 +372,7 @@ def main():
 
         # ---- bs=1 on the same server -------------------------------------------------
         _, in1 = make_input("data_1_in", 1)
-        p1 = Point(srv, model, 1, args.bs1_concurrency, "data_1_in", in1, local_rank, cpu)
+        p1 = Point(srv, model, 1, args.bs1_concurrency, "data_1_in", in1, dev, cpu)
         points.append(p1)
         n1 = 16 * args.bs1_concurrency
         p1.run(n1 // 4)
@@ -362,7 +381,7 @@ def main():
         l1g = fanout.gather_arrays(l1.astype(np.int64)).astype(np.float64)
         bs1.update({"p50_latency_us": round(percentile_us(l1g, 50), 1),
                     "p99_latency_us": round(percentile_us(l1g, 99), 1)})
-        pc1 = Point(srv, model, 1, 1, "data_1_in", in1, local_rank, cpu)
+        pc1 = Point(srv, model, 1, 1, "data_1_in", in1, dev, cpu)
         points.append(pc1)
         pc1.run(20)
         sc0 = pc1.s.server_stats()
@@ -416,6 +435,7 @@ def main():
             "server_breakdown_rank0": breakdown,
             "p99_constrained": p99c,
             "bs1": bs1,
+            "fanout": fan,
             "world_size_reported_by_process_group": dist.get_world_size() if world > 1 else 1,
         }
         for p in points:
@@ -433,13 +453,16 @@ def main():
             srv.wait_ready(timeout=1500, model=model)
             client = grpcclient.InferenceServerClient(srv.grpc_url)
             state["client"] = client
-            client.register_cuda_shared_memory("data_0_in", shmod.get_raw_handle(regions[0]), local_rank, in_bytes)
-            pb = Point(srv, model, bs, conc, "data_0_in", in_bytes, local_rank, cpu)
+            client.register_cuda_shared_memory("data_0_in", shmod.get_raw_handle(regions[0]), dev, in_bytes)
+            pb = Point(srv, model, bs, conc, "data_0_in", in_bytes, dev, cpu)
             points.append(pb)
             pb.run(per)
             _, _, elb = measure(pb, max(2, args.steps // 4), per)
             res["bf16_engine_infer_per_sec"] = round(world * max(2, args.steps // 4) * per * bs / elb, 1)
             res["bf16_engine_note"] = "same pipeline, bf16 K8-K10 kernels: ~3e-2 rel-L2 off fp32 (not the headline)"
+        if rehearse:
+            res["rehearsal"] = ("%d ranks on ONE GPU over gloo (launch/fan-out/aggregation rehearsal; "
+                                "not a scaling measurement)" % world)
         if rank == 0:
             print(json.dumps(res), flush=True)
         return 0

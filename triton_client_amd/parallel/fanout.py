@@ -69,6 +69,74 @@ def fill_and_fanout(region, datatype, n_elems, seed=0, mode="random", lo=0.0, hi
     raise ValueError("unknown fan-out method %s" % method)
 
 
+def _sync_all(dist):
+    import torch
+
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    dist.barrier()
+
+
+def replicate(region, nbytes, method):
+    """Copy rank 0's first ``nbytes`` of ``region`` into every rank's region
+    (no refill).  rccl: one broadcast collective (X1); p2p: the xGMI one-hop
+    star from rank 0 (X2); host: staged through host memory and a gloo/CPU
+    broadcast (the rehearsal path when several ranks share one GPU)."""
+    dist = _dist()
+    if dist is None or dist.get_world_size() == 1:
+        return "local"
+    if method == "rccl":
+        t = region_tensor(region, nbytes)
+        with roctx.range("fanout.rccl_broadcast bytes=%d" % nbytes):
+            dist.broadcast(t, src=0)
+        return "rccl"
+    if method == "p2p":
+        with roctx.range("fanout.p2p_star bytes=%d" % nbytes):
+            return _p2p_star(region, nbytes, dist)
+    if method == "host":
+        import torch
+
+        t = region_tensor(region, nbytes)
+        h = t.cpu() if dist.get_rank() == 0 else torch.empty(nbytes, dtype=torch.uint8)
+        dist.broadcast(h, src=0)
+        t.copy_(h.to(t.device))
+        return "host"
+    raise ValueError("unknown fan-out method %s" % method)
+
+
+def time_fanout(region, nbytes, methods, reps=5):
+    """Time each fan-out method replicating the (already filled) region:
+    median over ``reps`` of barrier -> replicate -> device sync -> barrier,
+    MAX over ranks.  Returns {method: {"us", "GBps_per_peer", "bytes"}} or an
+    {"error": ...} entry for a method this process group cannot run."""
+    import time
+
+    dist = _dist()
+    out = {}
+    if dist is None or dist.get_world_size() == 1:
+        return out
+    for m in methods:
+        ts = []
+        try:
+            for _ in range(reps + 1):
+                _sync_all(dist)
+                t0 = time.perf_counter()
+                replicate(region, nbytes, m)
+                _sync_all(dist)
+                ts.append(time.perf_counter() - t0)
+        except Exception as e:  # noqa: BLE001 - reported in the JSON, the run goes on
+            out[m] = {"error": str(e)[:200]}
+            try:
+                dist.barrier()
+            except Exception:
+                pass
+            continue
+        med = float(np.median(ts[1:]))
+        med = max_over_ranks(med)
+        out[m] = {"us": round(med * 1e6, 1), "GBps_per_peer": round(nbytes / med / 1e9, 2), "bytes": int(nbytes)}
+    return out
+
+
 def _p2p_star(region, nbytes, dist):
     from tritonclient.utils import hip_shared_memory as hipshm  # noqa: F401
     from triton_client_amd.ops import hip
@@ -153,10 +221,12 @@ def verify_replicas(region, nbytes, sample=4096):
     s = t[idx].to(torch.int64)
     if dist is None:
         return True
+    if dist.get_backend() == "gloo":  # rehearsal: collectives on host copies
+        s = s.cpu()
     ref = s.clone()
     dist.broadcast(ref, src=0)
     ok = torch.equal(s, ref)
-    flag = torch.tensor([1 if ok else 0], device=t.device)
+    flag = torch.tensor([1 if ok else 0], device=s.device)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     return bool(flag.item())
 
