@@ -39,6 +39,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <climits>
 #include <cstdlib>
 
 #include "kernels/common.h"
@@ -872,6 +873,386 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p
 }
 
 // ============================================================================
+// K11x: the whole dense layer in one kernel, z never leaves the CU
+// ============================================================================
+// K8x + K9x write the 128-channel bottleneck z (as hi/lo bf16 planes, 512 B a
+// pixel) to HBM and read it back with a 2(W+1)-row halo per tile: at 56x56 x
+// bs128 that is 205 MB written + 2 x 205 MB read per layer, and two launches.
+// Here one persistent block (8 waves, one per CU) walks a contiguous run of
+// 64-pixel tiles and produces z itself, straight into the 3x3's LDS ring:
+//
+//   for each tile t:  3x3 over band(t) = rows [m0-W-1, m0+64+W+1) of the ring
+//                     1x1 for the 64 rows band(t+1) adds, written over the 64
+//                     ring rows band(t+1) no longer needs
+//
+// so HBM sees only the layer's input X (read once) and its 32 output
+// channels.  The ring is 192 rows (band <= 178 for W <= 56; the rows a 1x1
+// chunk overwrites are always older than the next band, 2W < 127).
+//
+// 1x1 phase (64 pixels x 128 channels, K in 32-wide steps): wave (q1, ph) =
+// output quarter x pixel half on 32x32x16 MFMAs.
+//   * X: fp32 [64 px][32 k] steps by LDS-DMA (global_load_lds, one 1 KB piece
+//     per wave per step) into a 4-deep stage ring, 16-B chunks XOR-swizzled
+//     by pixel (conflict-free b128 reads); the first three steps of the next
+//     chunk are issued before the 3x3 phase, whose MFMAs hide that HBM round
+//     trip.  No VGPR staging: the waits are explicit vmcnt counts over a
+//     static issue order (the compiler's own waits cannot see through
+//     conditional or loop-carried register loads, and drained the prefetch
+//     before every step in a register-staged first version).
+//   * B operand: each lane reads its 8 fp32 of a k16 step, applies BN1+ReLU
+//     (affine from LDS) and splits hi/lo in registers; 4 waves redo the
+//     conversion of a fragment, which costs VALU slots the MFMAs leave idle
+//     and saves a converted-tile LDS pass plus a barrier per step.
+//   * A operand: BN2-folded W1 hi/lo fragments straight from L2 in a
+//     fragment-major copy (1 KB per wave load), one step ahead.
+//   * one barrier per step; epilogue: + bias, ReLU, hi/lo split, into the
+//     ring rows (16-B chunks XOR-swizzled by ring row, as K9x).
+//
+// 3x3 phase: wave (kq, oh) = input-channel quarter x output half on 16x16x32
+// MFMAs, so a wave's resident weights are 9 taps x 16 outputs x 32 inputs x
+// hi/lo = 72 VGPRs (K9x's 32-output waves hold 144, which leaves no room for
+// the 1x1 phase).  Operand reads roll two (tap, pixel-group) steps ahead.
+// The 4 kq partials: lanes holding another wave's 4 channels write them to
+// the owner's scratch slots, barrier, the owner lanes add and store y.
+//
+// LDS: ring 193 x 512 B + scratch 24 KB + X stages 4 x 8 KB + BN1 affine
+// 2 x 480 floats = 160,000 B.
+constexpr int kRingF = 192;
+// physical ring row = logical + 1: [guard = logical -1 (mirrors 191)]
+// [logical 0..191] [guard = logical 192 (mirrors 0)] [logical 193..195: zero]
+constexpr int kZeroF = 194;             // a tap reading logical kZeroF + {-1, 0, 1} reads zeros
+constexpr int kRingRowsF = kZeroF + 3;  // 197 physical rows
+constexpr int kCvtF = 64 * 64;     // one plane of a converted X step: 64 px x 32 k bf16
+constexpr int kPfF = 4;             // X steps in flight (registers)
+constexpr int kMaxKF = 480;         // BN1 affine staged in LDS: K <= 480 (blocks 1-2)
+constexpr int kScrF = 2 * 4 * 3 * 64 * 4;  // floats: [oh][owner][3 sources][px][4]
+constexpr int kLdsF = kRingRowsF * kRowB + kScrF * 4 + 4 * kCvtF + 2 * kMaxKF * 4;
+static_assert(kLdsF <= 160 * 1024, "K11x LDS budget");
+constexpr uint32_t kMagRingF = (uint32_t)((0x100000000ull + kRingF - 1) / kRingF);
+
+struct X3FusedParams {
+  const float* x;         // [M][ldx] fp32, the layer's first K channels
+  const float* s1;        // [K] BN1 affine
+  const float* t1;
+  const uint16_t* w1_hi;  // [K/16][q1 4][lane 64][8] bf16 (x3_w1_fragments)
+  const uint16_t* w1_lo;
+  const float* b1;        // [128] BN2-folded bias
+  const uint16_t* w2_hi;  // [tap 9][kq 4][oh 2][lane 64][8] bf16 (x3_w3f_fragments)
+  const uint16_t* w2_lo;
+  float* y;               // [M][ldy] fp32, offset to the layer's 32-channel slice
+  int ldx, K, ldy, M, H, W;
+  int tiles, tiles_per_block;
+  uint32_t mag_hw, mag_w;
+  int dbg;                 // ablation (TCAMD_X3F_DBG): 1 no 3x3 phase, 2 no tile-loop 1x1 chunks
+  unsigned long long* stamps;  // STAMP builds: per block [8] phase cycle sums (wave 0)
+};
+
+// NST = K / 32 (2..7): the k loop of a chunk is straight-line code, so the
+// compiler's waits for the W1 fragments are exact (through a loop back edge
+// it fell back to draining the whole counter every step).
+template <int NST, bool STAMP = false>
+__global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p) {
+  // STAMP (diagnostic builds, TCAMD_X3F_STAMP=1): shader-clock cycles per
+  // phase, summed over the block's tiles by wave 0: [0] prologue, [1] B0 wait,
+  // [2] 3x3 reads+MFMA, [3] exchange (B1 + owner adds), [4] 1x1 chunks,
+  // [5] tiles, [6] total
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_t = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+  const unsigned long long st_t0 = st_t;
+  auto stamp = [&](int i) {
+    if constexpr (STAMP) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      st_acc[i] += t - st_t;
+      st_t = t;
+    }
+  };
+  extern __shared__ __attribute__((aligned(16))) uint8_t ldsf[];
+  uint8_t* const ring = ldsf;
+  float* const scr = reinterpret_cast<float*>(ldsf + kRingRowsF * kRowB);
+  uint8_t* const cvt = ldsf + kRingRowsF * kRowB + kScrF * 4;             // [buf 2][plane 2][64 px][64 B]
+  float* const bn = reinterpret_cast<float*>(cvt + 4 * kCvtF);            // s1 [kMaxKF] | t1 [kMaxKF]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int W = p.W, HW = p.H * p.W;
+
+  // 3x3 roles and resident weights: A[16oh + (lane&15)][tap t][32kq + 8(lane>>4) ..+8]
+  const int kq = wave & 3, oh = wave >> 2;
+  v4u w2h[kTaps], w2l[kTaps];
+#pragma unroll
+  for (int t = 0; t < kTaps; ++t) {
+    const size_t off = ((size_t)((t * 4 + kq) * 2 + oh) * 64 + lane) * 8;
+    w2h[t] = ld16(p.w2_hi + off);
+    w2l[t] = ld16(p.w2_lo + off);
+  }
+
+  const int t_begin = blockIdx.x * p.tiles_per_block;
+  const int t_end = min(p.tiles, t_begin + p.tiles_per_block);
+  if (t_begin >= t_end) return;
+
+  for (int i = tid; i < p.K; i += 512) {
+    bn[i] = p.s1[i];
+    bn[kMaxKF + i] = p.t1[i];
+  }
+  if (tid < 3 * kRowB / 16) *reinterpret_cast<v4u*>(ring + kZeroF * kRowB + tid * 16) = v4u{0, 0, 0, 0};
+  __syncthreads();
+
+  // ---- 1x1 phase -----------------------------------------------------------
+  const int q1 = wave & 3, ph = wave >> 2;
+  const int col = lane & 31, hh = lane >> 5;
+  constexpr int nst = NST;
+  // X: every thread loads one float4 of a step (pixel cpx, k 4cj..4cj+3) kPfF
+  // steps ahead into registers, applies BN1 + ReLU, splits it and writes the
+  // hi/lo halves into the step's shared bf16 stage; the conversion is done
+  // once per element (a per-wave conversion of the B fragments repeated it
+  // in all 4 output-quarter waves and made the kernel VALU-bound).  All
+  // global loads are plain loads in a static order (fully unrolled chunk),
+  // so the compiler's counted waits keep kPfF steps in flight.
+  const int cpx = tid >> 3, cj = tid & 7;
+  f32x4 xr[kPfF];
+  const float* xrow = p.x;
+  auto xload = [&](int slot, int st) { xr[slot] = ldf4(xrow + min(st, nst - 1) * 32); };
+  auto prime = [&](int g0) {
+    xrow = p.x + (size_t)min(max(g0 + cpx, 0), p.M - 1) * p.ldx + 4 * cj;
+#pragma unroll
+    for (int u = 0; u < kPfF; ++u) xload(u, u);
+  };
+  // stage [buf][plane][64 px][64 B]: 16-B chunk c (k 8c..8c+7) of pixel px at
+  // slot c ^ ((px >> 2) & 3) (conflict-free b128 reads by 16 consecutive pixels)
+  const int cw_off = cpx * 64 + (((cj >> 1) ^ ((cpx >> 2) & 3)) << 4) + 8 * (cj & 1);
+  auto convert = [&](int slot, int buf, int st) {
+    const f32x4 sv = *reinterpret_cast<const f32x4*>(bn + st * 32 + 4 * cj);
+    const f32x4 tv = *reinterpret_cast<const f32x4*>(bn + kMaxKF + st * 32 + 4 * cj);
+    f32x4 v = xr[slot] * sv + tv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    v2u h, l;
+    split4(v, h, l);
+    uint8_t* q = cvt + buf * 2 * kCvtF + cw_off;
+    *reinterpret_cast<v2u*>(q) = h;
+    *reinterpret_cast<v2u*>(q + kCvtF) = l;
+  };
+  v4u a1[2][2][2];  // [step parity][kc][plane]
+  // buffer loads: one lane-constant VGPR offset + the step's offset in an SGPR
+  const auto w1h = __builtin_amdgcn_make_buffer_rsrc((void*)p.w1_hi, (short)0, p.K * 256, 0x00020000);
+  const auto w1l = __builtin_amdgcn_make_buffer_rsrc((void*)p.w1_lo, (short)0, p.K * 256, 0x00020000);
+  const int w1v = (q1 * 64 + lane) * 16;
+  auto wload = [&](int slot, int st) {
+    st = min(st, nst - 1);
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      a1[slot][kc][0] = __builtin_amdgcn_raw_buffer_load_b128(w1h, w1v, (2 * st + kc) * 4096, 0);
+      a1[slot][kc][1] = __builtin_amdgcn_raw_buffer_load_b128(w1l, w1v, (2 * st + kc) * 4096, 0);
+    }
+  };
+  const int bpx = 32 * ph + col;  // this lane's B column (pixel of the chunk)
+  const int bsw = (bpx >> 2) & 3;
+  const int br_off[2] = {bpx * 64 + ((hh ^ bsw) << 4), bpx * 64 + (((2 + hh) ^ bsw) << 4)};  // chunks 2kc + hh
+  // z rows [g0, g0 + nrows) -> ring.  The caller primed the chunk's X and
+  // issued W(0).  Step st: W(st+1) and X(st+1+kPfF) go out, step st+1 is
+  // converted into the other stage buffer while step st's MFMAs run on this
+  // one; one barrier per step.
+  auto z_chunk = [&](int g0, int nrows) {
+    f32x16 acc;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 b = ldf4(p.b1 + 32 * q1 + 8 * g + 4 * hh);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[4 * g + e] = b[e];
+    }
+    convert(0, 0, 0);
+    xload(0, kPfF);
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < nst; ++st) {
+      wload((st + 1) & 1, st + 1);
+      if (st + 1 < nst) {
+        convert((st + 1) % kPfF, (st + 1) & 1, st + 1);
+        xload((st + 1) % kPfF, st + 1 + kPfF);
+      }
+      const uint8_t* cb = cvt + (st & 1) * 2 * kCvtF;
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc) {
+        const uint8_t* q = cb + br_off[kc];
+        acc = x3_32(a1[st & 1][kc][0], a1[st & 1][kc][1], ld16(q), ld16(q + kCvtF), acc);
+      }
+      __syncthreads();
+    }
+    // C (32x32): lane col = pixel, reg 4g+e -> channel 32q1 + 8g + 4hh + e
+    if (bpx < nrows) {
+      int pos;
+      (void)fast_divmod(g0 + bpx + W + 1, kRingF, kMagRingF, pos);
+      // physical row pos + 1; logical rows 0 and 191 also go to the guard
+      // rows 193 / 0 (same swizzle key: 192 is a multiple of 16)
+      uint8_t* rp = ring + (pos + 1) * kRowB + 8 * hh;
+      const int mirror = pos == 0 ? kRingF * kRowB : (pos == kRingF - 1 ? -kRingF * kRowB : 0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[e] = fmaxf(acc[4 * g + e], 0.f);
+        v2u h, l;
+        split4(r, h, l);
+        uint8_t* q = rp + (((4 * q1 + g) ^ (pos & 15)) << 4);
+        *reinterpret_cast<v2u*>(q) = h;
+        *reinterpret_cast<v2u*>(q + 256) = l;
+        if (mirror) {
+          *reinterpret_cast<v2u*>(q + mirror) = h;
+          *reinterpret_cast<v2u*>(q + mirror + 256) = l;
+        }
+      }
+    }
+  };
+
+  // prologue: band(t_begin) in 64-row chunks
+  {
+    const int b0 = t_begin * kT2 - W - 1, b1 = t_begin * kT2 + kT2 + W + 1;
+    for (int g0 = b0; g0 < b1; g0 += 64) {
+      prime(g0);
+      wload(0, 0);
+      z_chunk(g0, min(64, b1 - g0));
+    }
+  }
+  stamp(0);
+
+  // y of the previous tile: stored at the start of the next 3x3 phase, which
+  // consumes no global loads, so the store never sits in front of a W1 wait
+  f32x4 yo[4];
+  int ym0 = -1;
+  const int c4 = lane >> 4;
+  auto store_y = [&]() {
+    if (ym0 < 0 || c4 != kq) return;
+#pragma unroll
+    for (int pg = 0; pg < 4; ++pg) {
+      const int m = ym0 + 16 * pg + (lane & 15);
+      if (m < p.M) *reinterpret_cast<f32x4*>(p.y + (size_t)m * p.ldy + 16 * oh + 4 * kq) = yo[pg];
+    }
+  };
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int m0 = tile * kT2;
+    __syncthreads();  // B0: the ring holds band(tile); the scratch is free
+    stamp(1);
+    store_y();
+    // this iteration's chunk: its first X steps and W(0) go out now and land
+    // while the 3x3 runs (issued and consumed in one tile iteration: a load
+    // carried round the loop is one the compiler's waits cannot follow)
+    if (tile + 1 < t_end && !(p.dbg & 2)) {
+      prime(m0 + kT2 + W + 1);
+      wload(0, 0);
+    }
+
+    // ---- 3x3 phase ----
+    if (!(p.dbg & 1)) {
+    // Per pixel group pg (16 consecutive pixels; the host requires W >= 16,
+    // so +16 pixels wraps an image row at most once) and tap
+    // row dy: the band row R[pg][dy] (logical 0..191), or the zero rows for
+    // an invalid dy; tap (dy, dx) reads logical row R + dx, which the guard
+    // rows (logical -1 and 192) keep in range without a second wrap.  Per
+    // (tap, pg) step that leaves: add dx, swizzle, address, and for dx != 0
+    // a select of the zero row: ~4 VALU beside 3 MFMAs (the first version's
+    // ~15 made the phase issue-bound, not MFMA-bound).
+    int R[4][3];
+    bool lfm[4], rtm[4];
+    {
+      const int m = m0 + (lane & 15);
+      int r, xx, pm;
+      (void)fast_divmod(m, HW, p.mag_hw, r);
+      int yy = fast_divmod(r, W, p.mag_w, xx);
+      (void)fast_divmod(m + W + 1, kRingF, kMagRingF, pm);
+#pragma unroll
+      for (int pg = 0; pg < 4; ++pg) {
+        if (pg) {
+          xx += 16;
+          if (xx >= W) {
+            xx -= W;
+            if (++yy == p.H) yy = 0;
+          }
+          pm += 16;
+          if (pm >= kRingF) pm -= kRingF;
+        }
+        const bool in = m + 16 * pg < p.M;
+        const int rm = pm - W, rp = pm + W;
+        R[pg][0] = (in && yy > 0) ? (rm < 0 ? rm + kRingF : rm) : kZeroF;
+        R[pg][1] = in ? pm : kZeroF;
+        R[pg][2] = (in && yy < p.H - 1) ? (rp >= kRingF ? rp - kRingF : rp) : kZeroF;
+        lfm[pg] = xx > 0;
+        rtm[pg] = xx < W - 1;
+      }
+    }
+    f32x4 acc[4];
+#pragma unroll
+    for (int pg = 0; pg < 4; ++pg) acc[pg] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // operand reads roll over the 36 (tap, pixel group) steps kLead steps
+    // ahead of the MFMAs ((kLead+1) x 8 VGPRs instead of whole taps)
+    constexpr int kLead = 3;
+    v4u bq[kLead + 1][2];
+    const int chunk16 = (4 * kq + (lane >> 4)) << 4;
+    auto rd = [&](int step) {
+      const int t = step >> 2, pg = step & 3;
+      const int dy = t / 3, dx = t % 3 - 1;
+      const int a = R[pg][dy] + dx;  // logical row, -1 .. 192 (or a zero row)
+      int off = (a << 9) + ((((a << 4) & 0xF0)) ^ chunk16);
+      if (dx < 0 && !lfm[pg]) off = kZeroF << 9;
+      if (dx > 0 && !rtm[pg]) off = kZeroF << 9;
+      const uint8_t* q = ring + kRowB + off;  // physical row = logical + 1
+      bq[step % (kLead + 1)][0] = ld16(q);
+      bq[step % (kLead + 1)][1] = ld16(q + 256);
+    };
+#pragma unroll
+    for (int step = 0; step < kLead; ++step) rd(step);
+#pragma unroll
+    for (int step = 0; step < 4 * kTaps; ++step) {
+      if (step + kLead < 4 * kTaps) rd(step + kLead);
+      __builtin_amdgcn_sched_barrier(0);
+      const int t = step >> 2, pg = step & 3;
+      acc[pg] = x3_16(w2h[t], w2l[t], bq[step % (kLead + 1)][0], bq[step % (kLead + 1)][1], acc[pg]);
+    }
+    stamp(2);
+    // C (16x16): lane (lane&15) = pixel of group pg, reg e -> channel 16oh + 4c + e,
+    // c = lane>>4; owner of channels 16oh + 4c .. +4 is wave (kq = c, oh), whose
+    // lanes 16c .. 16c+15 hold their own share and add the other three
+    if (c4 != kq) {
+      float* sw = scr + ((oh * 4 + c4) * 3 + (kq - c4 + 3) % 4) * 256 + (lane & 15) * 4;
+#pragma unroll
+      for (int pg = 0; pg < 4; ++pg) *reinterpret_cast<f32x4*>(sw + pg * 64) = acc[pg];
+    }
+    __syncthreads();  // B1
+    if (c4 == kq) {
+      const float* sr = scr + (oh * 4 + kq) * 3 * 256 + (lane & 15) * 4;
+#pragma unroll
+      for (int pg = 0; pg < 4; ++pg) {
+        yo[pg] = acc[pg];
+#pragma unroll
+        for (int src = 0; src < 3; ++src) yo[pg] += *reinterpret_cast<const f32x4*>(sr + src * 256 + pg * 64);
+      }
+    }
+    ym0 = m0;
+    }
+    stamp(3);
+
+    // ---- 1x1 phase: the 64 rows band(tile+1) adds ----
+    if (tile + 1 < t_end && !(p.dbg & 2)) {
+      const int g0 = m0 + kT2 + W + 1;
+      z_chunk(g0, kT2);
+    }
+    stamp(4);
+  }
+  store_y();
+  if constexpr (STAMP) {
+    st_acc[5] = t_end - t_begin;
+    st_acc[6] = __builtin_amdgcn_s_memtime() - st_t0;
+    if (wave == 0 && lane < 8) {
+      unsigned long long v = st_acc[0];
+#pragma unroll
+      for (int i = 1; i < 8; ++i)
+        if (lane == i) v = st_acc[i];
+      p.stamps[blockIdx.x * 8 + lane] = v;
+    }
+  }
+  // the last chunk's clamped tail DMAs (and, ablated, a primed chunk) must
+  // land before this workgroup's LDS can be handed to the next one
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ============================================================================
 // K10x stem: y = relu(maxpool3x3/2(conv7x7/2(x)) + b), 3 -> 64 channels, fp32
 // ============================================================================
 // As K10s in densenet.hip (patch staged once per block, conv as an implicit
@@ -1446,6 +1827,97 @@ int tcamd_x3_dense_layer(const float* x, int ldx, int imgs, int H, int W, int K,
   if (e != hipSuccess) return e;
   if (splits > 1) return x3_conv3x3_launch(nullptr, nullptr, ws, b1, splits, imgs, H, W, w2_hi, w2_lo, y, ldy, stream);
   return x3_conv3x3_launch(z_hi, z_lo, nullptr, nullptr, 0, imgs, H, W, w2_hi, w2_lo, y, ldy, stream);
+}
+
+static int cu_count();
+
+static unsigned long long* g_x3f_stamps = nullptr;  // TCAMD_X3F_STAMP diagnostic builds
+static int g_x3f_stamp_blocks = 0;
+
+// Copies the last stamped K11x launch's per-block phase cycles ([blocks][8])
+// into out (host, n entries); returns the block count.
+int tcamd_x3_fused_stamps(unsigned long long* out, int n) {
+  if (!g_x3f_stamps || !out) return 0;
+  const int m = std::min(n, 8 * g_x3f_stamp_blocks);
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(out, g_x3f_stamps, m * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return g_x3f_stamp_blocks;
+}
+
+// K11x: the whole dense layer in one kernel (z stays in LDS).  w1 in the
+// x3_w1_fragments layout, w2 in x3_w3f_fragments; W <= 56, K in 64..224.
+int tcamd_x3_dense_fused(const float* x, int ldx, int imgs, int H, int W, int K, const float* s1, const float* t1,
+                         const void* w1_hi, const void* w1_lo, const float* b1, const void* w2_hi, const void* w2_lo,
+                         float* y, int ldy, void* stream) {
+  if (imgs <= 0) return hipSuccess;
+  if (W > kMaxW3 || W < 16 || H < 1 || K <= 0 || K % 32 || K > kMaxKF || ldx < K || ldx % 4 || ldy % 4)
+    return hipErrorInvalidValue;
+  if (!x || !s1 || !t1 || !w1_hi || !w1_lo || !b1 || !w2_hi || !w2_lo || !y) return hipErrorInvalidValue;
+  if (!aligned16(x) || !aligned16(s1) || !aligned16(t1) || !aligned16(w1_hi) || !aligned16(w1_lo) ||
+      !aligned16(b1) || !aligned16(w2_hi) || !aligned16(w2_lo) || !aligned16(y))
+    return hipErrorInvalidValue;
+  X3FusedParams p;
+  p.x = x;
+  p.s1 = s1;
+  p.t1 = t1;
+  p.w1_hi = (const uint16_t*)w1_hi;
+  p.w1_lo = (const uint16_t*)w1_lo;
+  p.b1 = b1;
+  p.w2_hi = (const uint16_t*)w2_hi;
+  p.w2_lo = (const uint16_t*)w2_lo;
+  p.y = y;
+  p.ldx = ldx;
+  p.K = K;
+  p.ldy = ldy;
+  p.M = imgs * H * W;
+  p.H = H;
+  p.W = W;
+  if (p.M >= (1 << 24) - 2 * kRingF) return hipErrorInvalidValue;  // fast_divmod range
+  if ((uint64_t)p.M * ldx * 4 >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit X offsets
+  p.mag_hw = (uint32_t)((0x100000000ull + H * W - 1) / (uint64_t)(H * W));
+  p.mag_w = (uint32_t)((0x100000000ull + W - 1) / (uint64_t)W);
+  // NST 2..7 (K 64..224): past that the fully unrolled chunk no longer fits
+  // the 256-VGPR budget (spills); those layers keep the K8x + K9x pair
+  static const void* const kFns[] = {
+      (const void*)x3_dense_fused_kernel<2>, (const void*)x3_dense_fused_kernel<3>,
+      (const void*)x3_dense_fused_kernel<4>, (const void*)x3_dense_fused_kernel<5>,
+      (const void*)x3_dense_fused_kernel<6>, (const void*)x3_dense_fused_kernel<7>};
+  static const void* const kStampFns[] = {
+      (const void*)x3_dense_fused_kernel<2, true>, (const void*)x3_dense_fused_kernel<3, true>,
+      (const void*)x3_dense_fused_kernel<4, true>, (const void*)x3_dense_fused_kernel<5, true>,
+      (const void*)x3_dense_fused_kernel<6, true>, (const void*)x3_dense_fused_kernel<7, true>};
+  const int nst = K / 32;
+  if (nst < 2 || nst > 7) return hipErrorInvalidValue;
+  static const bool stamp = getenv("TCAMD_X3F_STAMP") && atoi(getenv("TCAMD_X3F_STAMP"));
+  p.stamps = nullptr;
+  if (stamp) {
+    if (!g_x3f_stamps && hipMalloc((void**)&g_x3f_stamps, 8 * 1024 * sizeof(unsigned long long)) != hipSuccess)
+      return hipErrorOutOfMemory;
+    p.stamps = g_x3f_stamps;
+  }
+  static std::atomic<bool> attr_set[kMaxDevices];
+  const int dev_slot = device_slot();
+  if (!attr_set[dev_slot].load(std::memory_order_acquire)) {
+    for (const void* const* fs : {kFns, kStampFns})
+      for (int i = 0; i < 6; ++i) {
+        const hipError_t e = hipFuncSetAttribute(fs[i], hipFuncAttributeMaxDynamicSharedMemorySize, kLdsF);
+        if (e != hipSuccess) return e;
+      }
+    attr_set[dev_slot].store(true, std::memory_order_release);
+  }
+  static const int dbg = getenv("TCAMD_X3F_DBG") ? atoi(getenv("TCAMD_X3F_DBG")) : 0;
+  p.dbg = dbg;
+  p.tiles = (p.M + kT2 - 1) / kT2;
+  const int grid = std::min(p.tiles, cu_count());
+  p.tiles_per_block = (p.tiles + grid - 1) / grid;
+  const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
+  void* args[] = {&p};
+  const hipError_t e = hipLaunchKernel((stamp ? kStampFns : kFns)[nst - 2], dim3(blocks), dim3(512), args, kLdsF,
+                                       (hipStream_t)stream);
+  if (e != hipSuccess) return e;
+  g_x3f_stamp_blocks = blocks;
+  return hipGetLastError();
 }
 
 static int cu_count() {

@@ -175,6 +175,49 @@ def test_x3_dense_layer(imgs, H, K):
     assert torch.equal(x[:, :K], xc[:, :K]) and torch.equal(x[:, K + 32:], xc[:, K + 32:])
 
 
+@pytest.mark.parametrize("imgs,H,K", [(1, 56, 64), (8, 56, 224), (32, 56, 128), (64, 28, 224), (5, 28, 96),
+                                      (3, 28, 192), (2, 16, 160), (128, 28, 128), (40, 56, 192)])
+def test_x3_dense_fused(imgs, H, K):
+    """K11x: the whole dense layer in one kernel (z produced into the 3x3's LDS
+    ring, never written to HBM): one block's band prologue only, several tiles
+    per block, ragged tails, every block width, and every K-step instantiation
+    (K = 64..224, 2..7 steps).  Against fp64
+    torch, and against the two-kernel path (same split products)."""
+    _need_gpu()
+    hip = _hip()
+    g = torch.Generator(device=DEV).manual_seed(imgs * 7919 + H + K)
+    M, ldx = imgs * H * H, K + 64
+    x = torch.randn(M, ldx, device=DEV, generator=g)
+    s = torch.rand(K, device=DEV, generator=g) + 0.5
+    t = torch.randn(K, device=DEV, generator=g) * 0.2
+    w1 = torch.randn(128, K, device=DEV, generator=g) / K ** 0.5
+    b1 = torch.randn(128, device=DEV, generator=g) * 0.1
+    w2 = torch.randn(32, 128, 3, 3, device=DEV, generator=g) / (9 * 128) ** 0.5
+    w1h, w1l = _split(w1)
+    w2p = _split(w2.permute(0, 2, 3, 1).reshape(32, -1))
+    f1h, f1l = (hip.x3_w1_fragments(u) for u in (w1h, w1l))
+    f2h, f2l = (hip.x3_w3f_fragments(u) for u in w2p)
+    xc = x.clone()
+    hip.x3_dense_fused(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), f1h.data_ptr(), f1l.data_ptr(),
+                       b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), x.data_ptr() + 4 * K, ldx, stream=_st())
+    torch.cuda.synchronize()
+    a = torch.relu(xc[:, :K].double() * s.double() + t.double())
+    z = torch.relu(a @ w1.double().t() + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
+    ref = F.conv2d(z, w2.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 32)
+    assert _rel(x[:, K:K + 32], ref) < 3e-5
+    assert torch.equal(x[:, :K], xc[:, :K]) and torch.equal(x[:, K + 32:], xc[:, K + 32:])
+    # the two-kernel path on the same inputs
+    y2 = xc.clone()
+    w2h, w2l = (hip.x3_w3_fragments(u) for u in w2p)
+    zh = torch.empty(M, 128, device=DEV, dtype=torch.bfloat16)
+    zl = torch.empty_like(zh)
+    hip.x3_dense_layer(y2.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), w1h.data_ptr(),
+                       w1l.data_ptr(), b1.data_ptr(), zh.data_ptr(), zl.data_ptr(), w2h.data_ptr(), w2l.data_ptr(),
+                       y2.data_ptr() + 4 * K, ldx, stream=_st())
+    torch.cuda.synchronize()
+    assert _rel(x[:, K:K + 32], y2[:, K:K + 32]) < 2e-5
+
+
 @pytest.mark.parametrize("imgs", [3, 20])  # 20: more tiles than the persistent grid (several per block)
 def test_x3_stem(imgs):
     _need_gpu()

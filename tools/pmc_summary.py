@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-kernel averages of rocprofv3 --pmc CSV passes (one or more dirs)."""
+"""Per-kernel averages of rocprofv3 --pmc passes (one or more dirs): the CSV
+output, or the rocpd SQLite database (run_results.db, the ROCm 7 default)."""
 import collections
 import csv
 import glob
@@ -7,6 +8,16 @@ import sys
 
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for d in sys.argv[1:]:
+    for f in glob.glob(d + "/**/*.db", recursive=True):
+        import sqlite3
+
+        per = collections.defaultdict(lambda: collections.defaultdict(float))
+        db = sqlite3.connect(f)
+        for k, disp, c, v in db.execute("select kernel_name, dispatch_id, counter_name, value from counters_collection"):
+            per[(k, disp)][c] += float(v)
+        for (k, _), cs in per.items():
+            for c, v in cs.items():
+                agg[k][c].append(v)
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         per = collections.defaultdict(lambda: collections.defaultdict(float))
         for r in csv.DictReader(open(f)):

@@ -21,7 +21,16 @@ def main():
     ap.add_argument("--imgs", type=int, default=128)
     ap.add_argument("--chunks", default="128,64,32,16")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--ks", default="", help="comma list of K: loop over them (overrides --k)")
+    ap.add_argument("--fused-dbg", default="", help="comma list of K11x ablation masks (TCAMD_X3F_DBG) to time")
+    ap.add_argument("--stamp", action="store_true", help="also run a TCAMD_X3F_STAMP=1 child (phase cycles)")
     a = ap.parse_args()
+    for K in ([int(v) for v in a.ks.split(",")] if a.ks else [a.k]):
+        a.k = K
+        bench(a)
+
+
+def bench(a):
     import torch
 
     from triton_client_amd.ops import hip
@@ -45,7 +54,7 @@ def main():
     zh = torch.empty(M, 128, device=dev, dtype=torch.bfloat16)
     zl = torch.empty_like(zh)
     ws = torch.empty(64 << 20, device=dev, dtype=torch.uint8)
-    for c in [int(v) for v in a.chunks.split(",")]:
+    for c in [int(v) for v in a.chunks.split(",") if v]:
         def run():
             for i0 in range(0, a.imgs, c):
                 n = min(c, a.imgs - i0)
@@ -67,6 +76,42 @@ def main():
         torch.cuda.synchronize()
         us = 1e6 * (time.perf_counter() - t0) / a.iters
         print("hw=%d k=%d chunk=%d: %.1f us per %d images" % (a.hw, K, c, us, a.imgs), flush=True)
+    # K11x: the same layer in one kernel, z kept in LDS
+    f1h, f1l = hip.x3_w1_fragments(w1h), hip.x3_w1_fragments(w1l)
+    f3h, f3l = hip.x3_w3f_fragments(w3h), hip.x3_w3f_fragments(w3l)
+
+    def fused():
+        hip.x3_dense_fused(x.data_ptr(), a.ldx, a.imgs, a.hw, a.hw, K, s.data_ptr(), t.data_ptr(), f1h.data_ptr(),
+                           f1l.data_ptr(), b1.data_ptr(), f3h.data_ptr(), f3l.data_ptr(), x.data_ptr() + K * 4, a.ldx,
+                           stream=st)
+    for _ in range(3):
+        fused()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        fused()
+    torch.cuda.synchronize()
+    us = 1e6 * (time.perf_counter() - t0) / a.iters
+    print("hw=%d k=%d fused: %.1f us per %d images" % (a.hw, K, us, a.imgs), flush=True)
+    st = hip.x3_fused_stamps() if os.environ.get("TCAMD_X3F_STAMP") else None
+    if st is not None:
+        tiles = st[:, 5].astype(float)
+        full = tiles == tiles.max()
+        names = ["prologue", "B0 wait", "3x3", "exchange", "1x1 chunks"]
+        per_tile = ["%s %.0f" % (nm, st[full, i].mean() / tiles[full].mean()) for i, nm in enumerate(names) if i]
+        print("  stamps (cycles, %d blocks, %d tiles/block): prologue %.0f | per tile: %s | total %.0f" % (
+            st.shape[0], tiles.max(), st[full, 0].mean(), ", ".join(per_tile), st[full, 6].mean()), flush=True)
+    runs = [("TCAMD_X3F_DBG", d) for d in a.fused_dbg.split(",") if d] + ([("TCAMD_X3F_STAMP", "1")] if a.stamp else [])
+    if runs:
+        import subprocess
+        for var, d in runs:
+            # the knobs are read once per process: one child per setting
+            env = dict(os.environ, **{var: d})
+            out = subprocess.run([sys.executable, os.path.abspath(__file__), "--hw", str(a.hw), "--k", str(K),
+                                  "--imgs", str(a.imgs), "--ldx", str(a.ldx), "--chunks", "", "--iters",
+                                  str(a.iters)], env=env, capture_output=True, text=True, timeout=300)
+            line = [ln for ln in out.stdout.splitlines() if "fused" in ln or "stamps" in ln]
+            print("  %s=%s: %s" % (var, d, " / ".join(line) if line else out.stderr[-300:]), flush=True)
 
 
 if __name__ == "__main__":

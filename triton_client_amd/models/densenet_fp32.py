@@ -28,6 +28,8 @@ All launches go to the caller's current HIP stream with no host sync, so a
 forward captures into one HIP graph per batch bucket.
 """
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -37,6 +39,7 @@ from .densenet import BLOCKS, BN_SIZE, GROWTH, INIT_FEATURES  # noqa: F401
 from .densenet_fused import _bn_affine
 
 IMG_ELEMS = 3 * 224 * 224
+FUSE_MAX_K = 224  # K11x instantiations: K 64..224
 
 
 def split_bf16(w):
@@ -82,6 +85,9 @@ class FusedDenseNetFP32:
                         "w1h": w1h.to(dev), "w1l": w1l.to(dev),
                         "b1": layer.conv1.bias.float().to(dev).contiguous(),
                         "w2h": hip.x3_w3_fragments(w2h).to(dev), "w2l": hip.x3_w3_fragments(w2l).to(dev),
+                        # K11x (fused layer) fragment layouts
+                        "w1fh": hip.x3_w1_fragments(w1h).to(dev), "w1fl": hip.x3_w1_fragments(w1l).to(dev),
+                        "w2fh": hip.x3_w3f_fragments(w2h).to(dev), "w2fl": hip.x3_w3f_fragments(w2l).to(dev),
                     })
                 self.blocks.append(ls)
                 self.block_dims.append((hw, ctot))
@@ -98,6 +104,9 @@ class FusedDenseNetFP32:
             self.wc = model.classifier.weight.float().to(dev).contiguous()
             self.bc = model.classifier.bias.float().to(dev).contiguous()
             self.num_features = c
+        # K11x runs a layer when every block gets at least this many 64-pixel
+        # tiles (its per-block prologue recomputes a (2W+2)-row halo of z)
+        self.fuse_min_tiles = int(os.environ.get("TCAMD_X3_FUSE_MIN_TPB", "4"))
         self._alloc(max_batch)
 
     def _alloc(self, n):
@@ -158,7 +167,13 @@ class FusedDenseNetFP32:
             hw, ctot = self.block_dims[bi]
             fp = self.feat[bi].data_ptr()
             M = b * hw * hw
+            fused = self._fuse(M, hw)
             for L in layers:
+                if fused and L["cin"] <= FUSE_MAX_K:
+                    hip.x3_dense_fused(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
+                                       L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(),
+                                       L["w2fh"].data_ptr(), L["w2fl"].data_ptr(), fp + 4 * L["cin"], ctot, stream=st)
+                    continue
                 hip.x3_dense_layer(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
                                    L["w1h"].data_ptr(), L["w1l"].data_ptr(), L["b1"].data_ptr(), zh, zl,
                                    L["w2h"].data_ptr(), L["w2l"].data_ptr(), fp + 4 * L["cin"], ctot, ws=ws,
@@ -178,6 +193,24 @@ class FusedDenseNetFP32:
         return out[:b]
 
     __call__ = forward
+
+    def _fuse(self, M, W):
+        """K11x (whole layer, z in LDS) for this block's layers?"""
+        if self.fuse_min_tiles <= 0 or W > 56 or W < 16:
+            return False
+        tiles = (M + 63) // 64
+        per_block = -(-tiles // min(tiles, _cu_count(self.device)))
+        return per_block >= self.fuse_min_tiles
+
+
+_CU = {}
+
+
+def _cu_count(dev):
+    key = str(dev)
+    if key not in _CU:
+        _CU[key] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return _CU[key]
 
 
 def build(max_batch, device="cuda", seed=0):

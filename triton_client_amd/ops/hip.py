@@ -184,6 +184,15 @@ _SIGS = {
         ],
         ctypes.c_int,
     ),
+    "tcamd_x3_dense_fused": (
+        [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
+    "tcamd_x3_fused_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "tcamd_x3_stem": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
          ctypes.c_int, ctypes.c_void_p],
@@ -608,6 +617,43 @@ def x3_dense_layer(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, z_hi, z_lo, 
     _check(_load().tcamd_x3_dense_layer(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
                                         z_hi, z_lo, w2_hi, w2_lo, y, int(ldy), _vp(ws), int(ws_bytes), _vp(stream)),
            "x3_dense_layer")
+
+
+def x3_w1_fragments(w):
+    """K11x 1x1 weight layout: [128][K] (out, in) -> the 32x32x16 MFMA
+    fragment-major copy the fused layer reads from L2, [K/16][q 4][h 2][col 32][8]
+    (lane (h, col) = w[32q + col][16ks + 8h .. +8]; one wave load = 1 KB)."""
+    n, k = w.shape
+    return w.reshape(4, 32, k // 16, 2, 8).permute(2, 0, 3, 1, 4).contiguous().reshape(n, k)
+
+
+def x3_w3f_fragments(w):
+    """K11x 3x3 weight layout: [32][9*128] (out, tap-major K) -> the 16x16x32
+    MFMA fragment-major copy, [tap 9][kq 4][oh 2][h 4][col 16][8] (lane
+    (h, col) = w[16oh + col][t][32kq + 8h .. +8])."""
+    return w.reshape(2, 16, 9, 4, 4, 8).permute(2, 3, 0, 4, 1, 5).contiguous().reshape(32, 9 * 128)
+
+
+def x3_dense_fused(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None):
+    """K11x: one fp32-parity dense layer in ONE kernel, the 128-channel
+    bottleneck kept in LDS (never written to HBM).  ``w1_*`` in the
+    x3_w1_fragments layout, ``w2_*`` in x3_w3f_fragments; 16 <= W <= 56, K a multiple
+    of 32 in 64..224."""
+    _check(_load().tcamd_x3_dense_fused(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
+                                        w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_fused")
+
+
+def x3_fused_stamps():
+    """Per-block phase cycle sums of the last K11x launch built with
+    TCAMD_X3F_STAMP=1: a [blocks, 8] uint64 array (columns: prologue, B0 wait,
+    3x3, exchange, 1x1 chunks, tiles, total), or None."""
+    import numpy as np
+
+    buf = np.zeros(8 * 1024, dtype=np.uint64)
+    n = _load().tcamd_x3_fused_stamps(buf.ctypes.data, buf.size)
+    if n <= 0:
+        return None
+    return buf[: 8 * n].reshape(n, 8)
 
 
 def x3_stem_fragments(w):
