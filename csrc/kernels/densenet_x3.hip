@@ -943,7 +943,8 @@ struct X3FusedParams {
   int ldx, K, ldy, M, H, W;
   int tiles, tiles_per_block;
   uint32_t mag_hw, mag_w;
-  int dbg;                 // ablation (TCAMD_X3F_DBG): 1 no 3x3 phase, 2 no tile-loop 1x1 chunks
+  int dbg;                 // ablation (TCAMD_X3F_DBG): v1 1 no 3x3 phase, 2 no tile-loop 1x1 chunks;
+                           // v2 STAMP builds 4 no W1 loads, 8 no X loads, 16 no conversion
   unsigned long long* stamps;  // STAMP builds: per block [8] phase cycle sums (wave 0)
 };
 
@@ -1250,6 +1251,361 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
   // the last chunk's clamped tail DMAs (and, ablated, a primed chunk) must
   // land before this workgroup's LDS can be handed to the next one
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---- K11x v2: four waves, one per SIMD, 512-register budget ----------------
+// The 8-wave kernel above pays for its 256-VGPR budget twice: its 3x3 waves
+// hold only 16 outputs (16x16x32 MFMAs, so every B fragment is read from LDS
+// by two waves) and two waves per SIMD contend for one matrix pipe and one
+// issue port.  Here each of the 4 waves owns a SIMD and
+//   * 3x3: input-channel quarter kq, all 32 outputs x 64 pixels (two 32-pixel
+//     halves) on 32x32x16 MFMAs, weights as K9x (x3_w3_fragments, 144 VGPRs):
+//     half the LDS operand reads, 12 MFMAs per tap per wave;
+//   * 1x1: output quarter q1, 32 channels x 64 pixels (two 32x32 tiles);
+//     every thread converts 8 elements of an X step (two float4) per step;
+//   * the 4 input-quarter partials are summed through the 24 KB scratch: wave
+//     kq owns outputs 8kq..8kq+7, writes the other three 8-channel groups of
+//     both halves (6 x 16 B per lane), barrier, adds and stores.
+// Ring, guard and zero rows, X staging and the per-step pipeline as above.
+template <int NST, bool STAMP = false>
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+x3_dense_fused4_kernel(X3FusedParams p) {
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_t = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+  const unsigned long long st_t0 = st_t;
+  auto stamp = [&](int i) {
+    if constexpr (STAMP) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      st_acc[i] += t - st_t;
+      st_t = t;
+    }
+  };
+  extern __shared__ __attribute__((aligned(16))) uint8_t ldsf[];
+  uint8_t* const ring = ldsf;
+  float* const scr = reinterpret_cast<float*>(ldsf + kRingRowsF * kRowB);
+  uint8_t* const cvt = ldsf + kRingRowsF * kRowB + kScrF * 4;  // [buf 2][plane 2][64 px][64 B]
+  float* const bn = reinterpret_cast<float*>(cvt + 4 * kCvtF);  // s1 [kMaxKF] | t1 [kMaxKF]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int W = p.W, HW = p.H * p.W;
+  const int col = lane & 31, hh = lane >> 5;
+
+  // 3x3 weights (K9x layout): lane (hh, col) = w[col][t][32kq + 16kc + 8hh ..+8]
+  const int kq = wave;
+  v4u wh[kTaps][2], wl[kTaps][2];
+#pragma unroll
+  for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      const size_t off = ((size_t)((t * 4 + kq) * 2 + kc) * 64 + lane) * 8;
+      wh[t][kc] = ld16(p.w2_hi + off);
+      wl[t][kc] = ld16(p.w2_lo + off);
+    }
+
+  const int t_begin = blockIdx.x * p.tiles_per_block;
+  const int t_end = min(p.tiles, t_begin + p.tiles_per_block);
+  if (t_begin >= t_end) return;
+
+  for (int i = tid; i < p.K; i += 256) {
+    bn[i] = p.s1[i];
+    bn[kMaxKF + i] = p.t1[i];
+  }
+  if (tid < 3 * kRowB / 16) *reinterpret_cast<v4u*>(ring + kZeroF * kRowB + tid * 16) = v4u{0, 0, 0, 0};
+  __syncthreads();
+
+  // ---- 1x1 phase ----
+  const int q1 = wave;
+  constexpr int nst = NST;
+  // conversion role: pixel cpx, 8-k chunk cc (two float4)
+  const int cpx = tid >> 2, cc = tid & 3;
+  f32x4 xr[kPfF][2];
+  const float* xrow = p.x;
+  auto xload = [&](int slot, int st) {
+    if constexpr (STAMP) {  // ablation (timing only): 8 no X loads
+      if (p.dbg & 8) return;
+    }
+    const float* q = xrow + min(st, nst - 1) * 32;
+    xr[slot][0] = ldf4(q);
+    xr[slot][1] = ldf4(q + 4);
+  };
+  auto prime = [&](int g0) {
+    xrow = p.x + (size_t)min(max(g0 + cpx, 0), p.M - 1) * p.ldx + 8 * cc;
+#pragma unroll
+    for (int u = 0; u < kPfF; ++u) xload(u, u);
+  };
+  const int cw_off = cpx * 64 + ((cc ^ ((cpx >> 2) & 3)) << 4);
+  auto convert = [&](int slot, int buf, int st) {
+    if constexpr (STAMP) {  // ablation (timing only): 16 no conversion
+      if (p.dbg & 16) return;
+    }
+    const float* sb = bn + st * 32 + 8 * cc;
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(sb), s1 = *reinterpret_cast<const f32x4*>(sb + 4);
+    const f32x4 t0 = *reinterpret_cast<const f32x4*>(sb + kMaxKF), t1 = *reinterpret_cast<const f32x4*>(sb + kMaxKF + 4);
+    f32x4 v0 = xr[slot][0] * s0 + t0, v1 = xr[slot][1] * s1 + t1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v0[e] = fmaxf(v0[e], 0.f);
+      v1[e] = fmaxf(v1[e], 0.f);
+    }
+    v2u h0, l0, h1, l1;
+    split4(v0, h0, l0);
+    split4(v1, h1, l1);
+    uint8_t* q = cvt + buf * 2 * kCvtF + cw_off;
+    *reinterpret_cast<v4u*>(q) = v4u{h0[0], h0[1], h1[0], h1[1]};
+    *reinterpret_cast<v4u*>(q + kCvtF) = v4u{l0[0], l0[1], l1[0], l1[1]};
+  };
+  // W1 fragments two steps ahead: [step % 3][kc][plane]
+  v4u a1[3][2][2];
+  const auto w1h = __builtin_amdgcn_make_buffer_rsrc((void*)p.w1_hi, (short)0, p.K * 256, 0x00020000);
+  const auto w1l = __builtin_amdgcn_make_buffer_rsrc((void*)p.w1_lo, (short)0, p.K * 256, 0x00020000);
+  const int w1v = (q1 * 64 + lane) * 16;
+  auto wload = [&](int st) {
+    if constexpr (STAMP) {  // ablation (timing only): 4 no W1 loads
+      if (p.dbg & 4) return;
+    }
+    const int sc = min(st, nst - 1);
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      a1[st % 3][kc][0] = __builtin_amdgcn_raw_buffer_load_b128(w1h, w1v, (2 * sc + kc) * 4096, 0);
+      a1[st % 3][kc][1] = __builtin_amdgcn_raw_buffer_load_b128(w1l, w1v, (2 * sc + kc) * 4096, 0);
+    }
+  };
+  // B reads: pixel 32ph + col, chunk 2kc + hh, swizzled by ((px >> 2) & 3)
+  int br_off[2][2];
+#pragma unroll
+  for (int ph = 0; ph < 2; ++ph)
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      const int px = 32 * ph + col;
+      br_off[ph][kc] = px * 64 + (((2 * kc + hh) ^ ((px >> 2) & 3)) << 4);
+    }
+  v4u bB[2][2][2][2];  // [step parity][ph][kc][plane]
+  auto bread = [&](int st) {
+    const uint8_t* cb = cvt + (st & 1) * 2 * kCvtF;
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph)
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc) {
+        bB[st & 1][ph][kc][0] = ld16(cb + br_off[ph][kc]);
+        bB[st & 1][ph][kc][1] = ld16(cb + br_off[ph][kc] + kCvtF);
+      }
+  };
+  // z rows [g0, g0 + nrows) -> ring.  The caller primed X and issued W(0),
+  // W(1).  One wave per SIMD has no partner to cover its latencies, so the
+  // step is software-pipelined: iteration st reads step st+1's B fragments,
+  // runs step st's 12 MFMAs on fragments read last iteration, converts step
+  // st+2 into the stage buffer step st vacated, and loads W(st+2); one
+  // barrier per step.
+  // the chunk's bias, held for the whole kernel (an L2 round trip at every
+  // chunk start otherwise)
+  f32x16 bias1;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 b = ldf4(p.b1 + 32 * q1 + 8 * g + 4 * hh);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias1[4 * g + e] = b[e];
+  }
+  auto z_chunk = [&](int g0, int nrows) {
+    f32x16 acc[2] = {bias1, bias1};
+    convert(0, 0, 0);
+    xload(0, kPfF);
+    __syncthreads();
+    bread(0);
+    if (nst > 1) {
+      convert(1, 1, 1);
+      xload(1, 1 + kPfF);
+    }
+    __syncthreads();
+    // the stages are pinned with scheduling fences: s_barrier orders memory
+    // operations only, and the scheduler otherwise slides a step's MFMAs past
+    // it onto the next step's fresh reads, undoing the pipeline
+#pragma unroll
+    for (int st = 0; st < nst; ++st) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + 1 < nst) bread(st + 1);
+      wload(st + 2);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph)
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc)
+          acc[ph] = x3_32(a1[st % 3][kc][0], a1[st % 3][kc][1], bB[st & 1][ph][kc][0], bB[st & 1][ph][kc][1],
+                          acc[ph]);
+      if (st + 2 < nst) {
+        convert((st + 2) % kPfF, st & 1, st + 2);
+        xload((st + 2) % kPfF, st + 2 + kPfF);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + 1 < nst) __syncthreads();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // C (32x32): lane col = pixel of half ph, reg 4g+e -> channel 32q1 + 8g + 4hh + e
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      const int px = 32 * ph + col;
+      if (px >= nrows) continue;
+      int pos;
+      (void)fast_divmod(g0 + px + W + 1, kRingF, kMagRingF, pos);
+      uint8_t* rp = ring + (pos + 1) * kRowB + 8 * hh;
+      const int mirror = pos == 0 ? kRingF * kRowB : (pos == kRingF - 1 ? -kRingF * kRowB : 0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[e] = fmaxf(acc[ph][4 * g + e], 0.f);
+        v2u h, l;
+        split4(r, h, l);
+        uint8_t* q = rp + (((4 * q1 + g) ^ (pos & 15)) << 4);
+        *reinterpret_cast<v2u*>(q) = h;
+        *reinterpret_cast<v2u*>(q + 256) = l;
+        if (mirror) {
+          *reinterpret_cast<v2u*>(q + mirror) = h;
+          *reinterpret_cast<v2u*>(q + mirror + 256) = l;
+        }
+      }
+    }
+  };
+
+  {
+    const int b0 = t_begin * kT2 - W - 1, b1 = t_begin * kT2 + kT2 + W + 1;
+    for (int g0 = b0; g0 < b1; g0 += 64) {
+      prime(g0);
+      wload(0);
+      wload(1);
+      z_chunk(g0, min(64, b1 - g0));
+      __syncthreads();  // the stage buffers are free for the next chunk
+    }
+  }
+  stamp(0);
+
+  // y of the previous tile, stored at the start of the next 3x3 phase
+  f32x4 yo[2];
+  int ym0 = -1;
+  auto store_y = [&]() {
+    if (ym0 < 0) return;
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      const int m = ym0 + 32 * ph + col;
+      if (m < p.M) *reinterpret_cast<f32x4*>(p.y + (size_t)m * p.ldy + 8 * kq + 4 * hh) = yo[ph];
+    }
+  };
+  const int chunk16 = (4 * kq + hh) << 4;  // + kc * 32
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int m0 = tile * kT2;
+    __syncthreads();  // B0: the ring holds band(tile); the scratch is free
+    stamp(1);
+    store_y();
+    if (tile + 1 < t_end) {
+      prime(m0 + kT2 + W + 1);
+      wload(0);
+      wload(1);
+    }
+
+    // ---- 3x3 phase: rows per (half, dy) once per tile (see the 8-wave kernel) ----
+    int R[2][3];
+    bool lfm[2], rtm[2];
+    {
+      const int m = m0 + col;
+      int r, xx, pm;
+      (void)fast_divmod(m, HW, p.mag_hw, r);
+      int yy = fast_divmod(r, W, p.mag_w, xx);
+      (void)fast_divmod(m + W + 1, kRingF, kMagRingF, pm);
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph) {
+        if (ph) {
+          xx += 32;
+          while (xx >= W) {  // W >= 16: at most twice
+            xx -= W;
+            if (++yy == p.H) yy = 0;
+          }
+          pm += 32;
+          if (pm >= kRingF) pm -= kRingF;
+        }
+        const bool in = m + 32 * ph < p.M;
+        const int rm = pm - W, rp = pm + W;
+        R[ph][0] = (in && yy > 0) ? (rm < 0 ? rm + kRingF : rm) : kZeroF;
+        R[ph][1] = in ? pm : kZeroF;
+        R[ph][2] = (in && yy < p.H - 1) ? (rp >= kRingF ? rp - kRingF : rp) : kZeroF;
+        lfm[ph] = xx > 0;
+        rtm[ph] = xx < W - 1;
+      }
+    }
+    f32x16 acc[2];
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[ph][e] = 0.f;
+    // 18 (tap, half) steps, operands read two steps ahead
+    constexpr int kLead4 = 2;
+    v4u bq[kLead4 + 1][2][2];  // [slot][kc][plane]
+    auto rd = [&](int step) {
+      const int t = step >> 1, ph = step & 1;
+      const int dy = t / 3, dx = t % 3 - 1;
+      const int a = R[ph][dy] + dx;
+      int off = (a << 9) + ((((a << 4) & 0xF0)) ^ chunk16);
+      if (dx < 0 && !lfm[ph]) off = kZeroF << 9;
+      if (dx > 0 && !rtm[ph]) off = kZeroF << 9;
+      const uint8_t* q = ring + kRowB + off;
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc) {
+        // chunk 4kq + 2kc + hh: the kc bit flips bit 5 of the byte offset (bit 1 of the chunk)
+        const uint8_t* qk = kc ? ring + kRowB + (off ^ 32) : q;
+        bq[step % (kLead4 + 1)][kc][0] = ld16(qk);
+        bq[step % (kLead4 + 1)][kc][1] = ld16(qk + 256);
+      }
+    };
+#pragma unroll
+    for (int step = 0; step < kLead4; ++step) rd(step);
+#pragma unroll
+    for (int step = 0; step < 2 * kTaps; ++step) {
+      if (step + kLead4 < 2 * kTaps) rd(step + kLead4);
+      __builtin_amdgcn_sched_barrier(0);
+      const int t = step >> 1, ph = step & 1;
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc)
+        acc[ph] = x3_32(wh[t][kc], wl[t][kc], bq[step % (kLead4 + 1)][kc][0], bq[step % (kLead4 + 1)][kc][1],
+                        acc[ph]);
+    }
+    stamp(2);
+    // C (32x32): reg 4g+e -> channel 8g + 4hh + e of pixel 32ph + col; owner of
+    // channels 8g..8g+7 is wave g.  scratch [owner][src rank 3][half 2][32 px][8 ch]
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (g == kq) continue;
+      float* sw = scr + ((g * 3 + (kq - g + 3) % 4) * 2) * 256 + col * 8 + 4 * hh;
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph)
+        *reinterpret_cast<f32x4*>(sw + ph * 256) =
+            f32x4{acc[ph][4 * g], acc[ph][4 * g + 1], acc[ph][4 * g + 2], acc[ph][4 * g + 3]};
+    }
+    __syncthreads();  // B1
+    {
+      const float* sr = scr + (kq * 3 * 2) * 256 + col * 8 + 4 * hh;
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph) {
+        f32x4 o = f32x4{acc[ph][4 * kq], acc[ph][4 * kq + 1], acc[ph][4 * kq + 2], acc[ph][4 * kq + 3]};
+#pragma unroll
+        for (int src = 0; src < 3; ++src) o += *reinterpret_cast<const f32x4*>(sr + (src * 2 + ph) * 256);
+        yo[ph] = o;
+      }
+    }
+    ym0 = m0;
+    stamp(3);
+
+    if (tile + 1 < t_end) z_chunk(m0 + kT2 + W + 1, kT2);
+    stamp(4);
+  }
+  store_y();
+  if constexpr (STAMP) {
+    st_acc[5] = t_end - t_begin;
+    st_acc[6] = __builtin_amdgcn_s_memtime() - st_t0;
+    if (wave == 0 && lane < 8) {
+      unsigned long long v = st_acc[0];
+#pragma unroll
+      for (int i = 1; i < 8; ++i)
+        if (lane == i) v = st_acc[i];
+      p.stamps[blockIdx.x * 8 + lane] = v;
+    }
+  }
 }
 
 // ============================================================================
@@ -1845,11 +2201,13 @@ int tcamd_x3_fused_stamps(unsigned long long* out, int n) {
   return g_x3f_stamp_blocks;
 }
 
-// K11x: the whole dense layer in one kernel (z stays in LDS).  w1 in the
-// x3_w1_fragments layout, w2 in x3_w3f_fragments; W <= 56, K in 64..224.
-int tcamd_x3_dense_fused(const float* x, int ldx, int imgs, int H, int W, int K, const float* s1, const float* t1,
-                         const void* w1_hi, const void* w1_lo, const float* b1, const void* w2_hi, const void* w2_lo,
-                         float* y, int ldy, void* stream) {
+// K11x: the whole dense layer in one kernel (z stays in LDS).  v 1: the
+// 8-wave kernel (w2 in x3_w3f_fragments); v 2: the 4-wave kernel (w2 in
+// x3_w3_fragments, K9x's layout).  w1 in x3_w1_fragments; 16 <= W <= 56,
+// K in 64..224.
+static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, int W, int K, const float* s1,
+                               const float* t1, const void* w1_hi, const void* w1_lo, const float* b1,
+                               const void* w2_hi, const void* w2_lo, float* y, int ldy, void* stream) {
   if (imgs <= 0) return hipSuccess;
   if (W > kMaxW3 || W < 16 || H < 1 || K <= 0 || K % 32 || K > kMaxKF || ldx < K || ldx % 4 || ldy % 4)
     return hipErrorInvalidValue;
@@ -1874,21 +2232,25 @@ int tcamd_x3_dense_fused(const float* x, int ldx, int imgs, int H, int W, int K,
   p.H = H;
   p.W = W;
   if (p.M >= (1 << 24) - 2 * kRingF) return hipErrorInvalidValue;  // fast_divmod range
-  if ((uint64_t)p.M * ldx * 4 >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit X offsets
   p.mag_hw = (uint32_t)((0x100000000ull + H * W - 1) / (uint64_t)(H * W));
   p.mag_w = (uint32_t)((0x100000000ull + W - 1) / (uint64_t)W);
   // NST 2..7 (K 64..224): past that the fully unrolled chunk no longer fits
-  // the 256-VGPR budget (spills); those layers keep the K8x + K9x pair
-  static const void* const kFns[] = {
-      (const void*)x3_dense_fused_kernel<2>, (const void*)x3_dense_fused_kernel<3>,
-      (const void*)x3_dense_fused_kernel<4>, (const void*)x3_dense_fused_kernel<5>,
-      (const void*)x3_dense_fused_kernel<6>, (const void*)x3_dense_fused_kernel<7>};
-  static const void* const kStampFns[] = {
-      (const void*)x3_dense_fused_kernel<2, true>, (const void*)x3_dense_fused_kernel<3, true>,
-      (const void*)x3_dense_fused_kernel<4, true>, (const void*)x3_dense_fused_kernel<5, true>,
-      (const void*)x3_dense_fused_kernel<6, true>, (const void*)x3_dense_fused_kernel<7, true>};
+  // the 8-wave kernel's 256-VGPR budget; those layers keep the K8x + K9x pair
+  static const void* const kFns[2][2][6] = {
+      {{(const void*)x3_dense_fused_kernel<2>, (const void*)x3_dense_fused_kernel<3>,
+        (const void*)x3_dense_fused_kernel<4>, (const void*)x3_dense_fused_kernel<5>,
+        (const void*)x3_dense_fused_kernel<6>, (const void*)x3_dense_fused_kernel<7>},
+       {(const void*)x3_dense_fused_kernel<2, true>, (const void*)x3_dense_fused_kernel<3, true>,
+        (const void*)x3_dense_fused_kernel<4, true>, (const void*)x3_dense_fused_kernel<5, true>,
+        (const void*)x3_dense_fused_kernel<6, true>, (const void*)x3_dense_fused_kernel<7, true>}},
+      {{(const void*)x3_dense_fused4_kernel<2>, (const void*)x3_dense_fused4_kernel<3>,
+        (const void*)x3_dense_fused4_kernel<4>, (const void*)x3_dense_fused4_kernel<5>,
+        (const void*)x3_dense_fused4_kernel<6>, (const void*)x3_dense_fused4_kernel<7>},
+       {(const void*)x3_dense_fused4_kernel<2, true>, (const void*)x3_dense_fused4_kernel<3, true>,
+        (const void*)x3_dense_fused4_kernel<4, true>, (const void*)x3_dense_fused4_kernel<5, true>,
+        (const void*)x3_dense_fused4_kernel<6, true>, (const void*)x3_dense_fused4_kernel<7, true>}}};
   const int nst = K / 32;
-  if (nst < 2 || nst > 7) return hipErrorInvalidValue;
+  if (nst < 2 || nst > 7 || (v != 1 && v != 2)) return hipErrorInvalidValue;
   static const bool stamp = getenv("TCAMD_X3F_STAMP") && atoi(getenv("TCAMD_X3F_STAMP"));
   p.stamps = nullptr;
   if (stamp) {
@@ -1899,11 +2261,12 @@ int tcamd_x3_dense_fused(const float* x, int ldx, int imgs, int H, int W, int K,
   static std::atomic<bool> attr_set[kMaxDevices];
   const int dev_slot = device_slot();
   if (!attr_set[dev_slot].load(std::memory_order_acquire)) {
-    for (const void* const* fs : {kFns, kStampFns})
-      for (int i = 0; i < 6; ++i) {
-        const hipError_t e = hipFuncSetAttribute(fs[i], hipFuncAttributeMaxDynamicSharedMemorySize, kLdsF);
-        if (e != hipSuccess) return e;
-      }
+    for (const auto& byv : kFns)
+      for (const auto& fs : byv)
+        for (const void* f : fs) {
+          const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsF);
+          if (e != hipSuccess) return e;
+        }
     attr_set[dev_slot].store(true, std::memory_order_release);
   }
   static const int dbg = getenv("TCAMD_X3F_DBG") ? atoi(getenv("TCAMD_X3F_DBG")) : 0;
@@ -1913,11 +2276,23 @@ int tcamd_x3_dense_fused(const float* x, int ldx, int imgs, int H, int W, int K,
   p.tiles_per_block = (p.tiles + grid - 1) / grid;
   const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
   void* args[] = {&p};
-  const hipError_t e = hipLaunchKernel((stamp ? kStampFns : kFns)[nst - 2], dim3(blocks), dim3(512), args, kLdsF,
-                                       (hipStream_t)stream);
+  const hipError_t e = hipLaunchKernel(kFns[v - 1][stamp ? 1 : 0][nst - 2], dim3(blocks), dim3(v == 2 ? 256 : 512),
+                                       args, kLdsF, (hipStream_t)stream);
   if (e != hipSuccess) return e;
   g_x3f_stamp_blocks = blocks;
   return hipGetLastError();
+}
+
+int tcamd_x3_dense_fused(const float* x, int ldx, int imgs, int H, int W, int K, const float* s1, const float* t1,
+                         const void* w1_hi, const void* w1_lo, const float* b1, const void* w2_hi, const void* w2_lo,
+                         float* y, int ldy, void* stream) {
+  return x3_dense_fused_impl(1, x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream);
+}
+
+int tcamd_x3_dense_fused4(const float* x, int ldx, int imgs, int H, int W, int K, const float* s1, const float* t1,
+                          const void* w1_hi, const void* w1_lo, const float* b1, const void* w2_hi,
+                          const void* w2_lo, float* y, int ldy, void* stream) {
+  return x3_dense_fused_impl(2, x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream);
 }
 
 static int cu_count() {

@@ -177,8 +177,9 @@ def test_x3_dense_layer(imgs, H, K):
 
 @pytest.mark.parametrize("imgs,H,K", [(1, 56, 64), (8, 56, 224), (32, 56, 128), (64, 28, 224), (5, 28, 96),
                                       (3, 28, 192), (2, 16, 160), (128, 28, 128), (40, 56, 192)])
-def test_x3_dense_fused(imgs, H, K):
-    """K11x: the whole dense layer in one kernel (z produced into the 3x3's LDS
+@pytest.mark.parametrize("version", [1, 2])
+def test_x3_dense_fused(imgs, H, K, version):
+    """K11x (v1: 8 waves, v2: 4 waves): the whole dense layer in one kernel (z produced into the 3x3's LDS
     ring, never written to HBM): one block's band prologue only, several tiles
     per block, ragged tails, every block width, and every K-step instantiation
     (K = 64..224, 2..7 steps).  Against fp64
@@ -196,10 +197,12 @@ def test_x3_dense_fused(imgs, H, K):
     w1h, w1l = _split(w1)
     w2p = _split(w2.permute(0, 2, 3, 1).reshape(32, -1))
     f1h, f1l = (hip.x3_w1_fragments(u) for u in (w1h, w1l))
-    f2h, f2l = (hip.x3_w3f_fragments(u) for u in w2p)
+    frag = hip.x3_w3f_fragments if version == 1 else hip.x3_w3_fragments
+    fused = hip.x3_dense_fused if version == 1 else hip.x3_dense_fused4
+    f2h, f2l = (frag(u) for u in w2p)
     xc = x.clone()
-    hip.x3_dense_fused(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), f1h.data_ptr(), f1l.data_ptr(),
-                       b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), x.data_ptr() + 4 * K, ldx, stream=_st())
+    fused(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), f1h.data_ptr(), f1l.data_ptr(),
+          b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), x.data_ptr() + 4 * K, ldx, stream=_st())
     torch.cuda.synchronize()
     a = torch.relu(xc[:, :K].double() * s.double() + t.double())
     z = torch.relu(a @ w1.double().t() + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--ks", default="", help="comma list of K: loop over them (overrides --k)")
     ap.add_argument("--fused-dbg", default="", help="comma list of K11x ablation masks (TCAMD_X3F_DBG) to time")
     ap.add_argument("--stamp", action="store_true", help="also run a TCAMD_X3F_STAMP=1 child (phase cycles)")
+    ap.add_argument("--both", action="store_true", help="also time K11x v1 (8 waves) in a child")
+    ap.add_argument("--stamp-dbg", default="", help="comma list of ablation masks to run as stamped children")
     a = ap.parse_args()
     for K in ([int(v) for v in a.ks.split(",")] if a.ks else [a.k]):
         a.k = K
@@ -78,12 +80,14 @@ def bench(a):
         print("hw=%d k=%d chunk=%d: %.1f us per %d images" % (a.hw, K, c, us, a.imgs), flush=True)
     # K11x: the same layer in one kernel, z kept in LDS
     f1h, f1l = hip.x3_w1_fragments(w1h), hip.x3_w1_fragments(w1l)
-    f3h, f3l = hip.x3_w3f_fragments(w3h), hip.x3_w3f_fragments(w3l)
+    v = int(os.environ.get("TCAMD_X3F_V", "2"))
+    frag = hip.x3_w3f_fragments if v == 1 else hip.x3_w3_fragments
+    fn = hip.x3_dense_fused if v == 1 else hip.x3_dense_fused4
+    f3h, f3l = frag(w3h), frag(w3l)
 
     def fused():
-        hip.x3_dense_fused(x.data_ptr(), a.ldx, a.imgs, a.hw, a.hw, K, s.data_ptr(), t.data_ptr(), f1h.data_ptr(),
-                           f1l.data_ptr(), b1.data_ptr(), f3h.data_ptr(), f3l.data_ptr(), x.data_ptr() + K * 4, a.ldx,
-                           stream=st)
+        fn(x.data_ptr(), a.ldx, a.imgs, a.hw, a.hw, K, s.data_ptr(), t.data_ptr(), f1h.data_ptr(), f1l.data_ptr(),
+           b1.data_ptr(), f3h.data_ptr(), f3l.data_ptr(), x.data_ptr() + K * 4, a.ldx, stream=st)
     for _ in range(3):
         fused()
     torch.cuda.synchronize()
@@ -92,7 +96,7 @@ def bench(a):
         fused()
     torch.cuda.synchronize()
     us = 1e6 * (time.perf_counter() - t0) / a.iters
-    print("hw=%d k=%d fused: %.1f us per %d images" % (a.hw, K, us, a.imgs), flush=True)
+    print("hw=%d k=%d fused v%d: %.1f us per %d images" % (a.hw, K, v, us, a.imgs), flush=True)
     st = hip.x3_fused_stamps() if os.environ.get("TCAMD_X3F_STAMP") else None
     if st is not None:
         tiles = st[:, 5].astype(float)
@@ -102,16 +106,21 @@ def bench(a):
         print("  stamps (cycles, %d blocks, %d tiles/block): prologue %.0f | per tile: %s | total %.0f" % (
             st.shape[0], tiles.max(), st[full, 0].mean(), ", ".join(per_tile), st[full, 6].mean()), flush=True)
     runs = [("TCAMD_X3F_DBG", d) for d in a.fused_dbg.split(",") if d] + ([("TCAMD_X3F_STAMP", "1")] if a.stamp else [])
+    runs = [(v, d, {}) for v, d in runs] + [("TCAMD_X3F_DBG", d, {"TCAMD_X3F_STAMP": "1"})
+                                            for d in a.stamp_dbg.split(",") if d]
+    if a.both and os.environ.get("TCAMD_X3F_V", "2") == "2":
+        runs.append(("TCAMD_X3F_V", "1", {}))
     if runs:
         import subprocess
-        for var, d in runs:
+        for var, d, extra in runs:
             # the knobs are read once per process: one child per setting
-            env = dict(os.environ, **{var: d})
+            env = dict(os.environ, **{var: d}, **extra)
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--hw", str(a.hw), "--k", str(K),
                                   "--imgs", str(a.imgs), "--ldx", str(a.ldx), "--chunks", "", "--iters",
                                   str(a.iters)], env=env, capture_output=True, text=True, timeout=300)
             line = [ln for ln in out.stdout.splitlines() if "fused" in ln or "stamps" in ln]
-            print("  %s=%s: %s" % (var, d, " / ".join(line) if line else out.stderr[-300:]), flush=True)
+            print("  %s=%s%s: %s" % (var, d, " +stamp" if extra else "", " / ".join(line) if line else out.stderr[-300:]),
+                  flush=True)
 
 
 if __name__ == "__main__":

@@ -19,6 +19,9 @@ Network walk (same as :class:`densenet_fused.FusedDenseNet`, fp32 activations):
                         K9x conv3x3 z -> block buffer ch[c_in : c_in+32] (fp32)
                         (one x3_dense_layer call; small-M layers run the 1x1
                         split-K and the 3x3 reduces its partials in-kernel)
+                        or, for big batches (>= 4 tiles per block, K <= 224,
+                        16 <= W <= 56): K11x, the whole layer in ONE kernel
+                        with z produced into the 3x3's LDS ring (never in HBM)
    -> per transition:   K8x conv1x1 with BN+ReLU+2x2 avg-pool prologue
                         -> next block buffer ch[0 : C/2] (fp32)
    -> K10x head: relu(BN5(x)) global average -> [b,1024] fp32
@@ -105,8 +108,10 @@ class FusedDenseNetFP32:
             self.bc = model.classifier.bias.float().to(dev).contiguous()
             self.num_features = c
         # K11x runs a layer when every block gets at least this many 64-pixel
-        # tiles (its per-block prologue recomputes a (2W+2)-row halo of z)
-        self.fuse_min_tiles = int(os.environ.get("TCAMD_X3_FUSE_MIN_TPB", "4"))
+        # tiles (its per-block prologue recomputes a (2W+2)-row halo of z, yet it
+        # still beats the two-launch pair at bs1); 0 disables it (A/B runs)
+        self.fuse_min_tiles = int(os.environ.get("TCAMD_X3_FUSE_MIN_TPB", "1"))
+        self.fuse_v2_min_k = int(os.environ.get("TCAMD_X3_FUSE_V2_MIN_K", "160"))
         self._alloc(max_batch)
 
     def _alloc(self, n):
@@ -170,9 +175,19 @@ class FusedDenseNetFP32:
             fused = self._fuse(M, hw)
             for L in layers:
                 if fused and L["cin"] <= FUSE_MAX_K:
-                    hip.x3_dense_fused(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
-                                       L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(),
-                                       L["w2fh"].data_ptr(), L["w2fl"].data_ptr(), fp + 4 * L["cin"], ctot, stream=st)
+                    # K11x v2 (4 waves) on the 56x56 block at big batches from K >=
+                    # fuse_v2_min_k, v1 (8 waves) elsewhere, bs1 included (per-K A/B:
+                    # profiles/r3_fused_dense_layer.md)
+                    if fused == 2 and L["cin"] >= self.fuse_v2_min_k:
+                        hip.x3_dense_fused4(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
+                                            L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(),
+                                            L["w2h"].data_ptr(), L["w2l"].data_ptr(), fp + 4 * L["cin"], ctot,
+                                            stream=st)
+                    else:
+                        hip.x3_dense_fused(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
+                                           L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(),
+                                           L["w2fh"].data_ptr(), L["w2fl"].data_ptr(), fp + 4 * L["cin"], ctot,
+                                           stream=st)
                     continue
                 hip.x3_dense_layer(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
                                    L["w1h"].data_ptr(), L["w1l"].data_ptr(), L["b1"].data_ptr(), zh, zl,
@@ -195,12 +210,15 @@ class FusedDenseNetFP32:
     __call__ = forward
 
     def _fuse(self, M, W):
-        """K11x (whole layer, z in LDS) for this block's layers?"""
+        """K11x (whole layer, z in LDS) for this block's layers: 0 = no (K8x + K9x
+        pair), 1 = v1 (8 waves), 2 = v2 allowed (4 waves, big-batch 56x56)."""
         if self.fuse_min_tiles <= 0 or W > 56 or W < 16:
-            return False
+            return 0
         tiles = (M + 63) // 64
         per_block = -(-tiles // min(tiles, _cu_count(self.device)))
-        return per_block >= self.fuse_min_tiles
+        if per_block < self.fuse_min_tiles:
+            return 0
+        return 2 if (W >= 56 and per_block >= 4) else 1
 
 
 _CU = {}

@@ -193,6 +193,14 @@ _SIGS = {
         ctypes.c_int,
     ),
     "tcamd_x3_fused_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
+    "tcamd_x3_dense_fused4": (
+        [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
     "tcamd_x3_stem": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
          ctypes.c_int, ctypes.c_void_p],
@@ -641,6 +649,13 @@ def x3_dense_fused(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo
     of 32 in 64..224."""
     _check(_load().tcamd_x3_dense_fused(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
                                         w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_fused")
+
+
+def x3_dense_fused4(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None):
+    """K11x v2 (4 waves, one per SIMD, 32x32x16 3x3): as :func:`x3_dense_fused`
+    but ``w2_*`` in the K9x x3_w3_fragments layout."""
+    _check(_load().tcamd_x3_dense_fused4(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
+                                         w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_fused4")
 
 
 def x3_fused_stamps():
