@@ -15,6 +15,10 @@
 //      loads, and every lane assembles two 16-B output chunks from LDS (owner
 //      element by binary search over the LDS starts) and writes each with one
 //      dwordx4 store (byte stores only on the two ragged edges of a part).
+//      A chunk is built branch-free from the elements overlapping it: element
+//      j's payload bytes are the staged stream shifted by 4(j+1), taken under
+//      a byte mask, and its length prefix is OR-ed in shifted into place (a
+//      per-byte walk made most chunks of short strings divergent).
 //   Fixed-width numpy 'S' arrays are packed without a host join: element i's
 //   payload is read at data + i * stride (tcamd_pack_bytes_strided).
 //
@@ -24,8 +28,10 @@
 // elements are shorter than kXR - 4 bytes, and chains started at every
 // candidate offset converge onto the true chain within a few hops:
 //   1. ix_walk: one WAVE per 4 KiB block, staged in LDS; each lane walks 4
-//      candidate chains interleaved (ILP hides the LDS latency of each hop)
-//      and records per candidate its exit offset into the next block (or
+//      candidate chains interleaved until they leave the first kXR bytes,
+//      then one wave-uniform walk per distinct exit (on the scalar unit, one
+//      broadcast LDS read per hop, 32-bit block-relative math) finishes them;
+//      it records per candidate its exit offset into the next block (or
 //      END / BAD / FAR) and its element count; a wave reduction marks the
 //      block "sync" when every live candidate leaves at the same offset;
 //   2. ix_resolve: per block, the entry = the sync exit of the nearest sync
@@ -36,9 +42,9 @@
 //   4. ix_status: ok / fewer / malformed, or "retry with a larger window",
 //      or "fall back to the general walk" (an element longer than kXR - 4
 //      bytes, or a long run of ambiguous blocks);
-//   5. ix_emit: one wave per block re-walks from its entry through LDS;
-//      lane 0 writes (offset, length) pairs into an LDS ring that the whole
-//      wave flushes with coalesced stores.
+//   5. ix_emit: one wave per block re-walks from its entry through LDS as a
+//      wave-uniform scalar chain; element i of each 64-group is written into
+//      lane i's registers (v_writelane) and stored with coalesced stores.
 //   The scan starts on a window sized from n_expected (a small tensor in a
 //   large region does not walk the whole region) and grows 8x per retry.
 //   Fallback: the round-2 general path (pointer doubling over every byte
@@ -169,7 +175,9 @@ __global__ void __launch_bounds__(kBlock) pk_emit(const uint8_t* __restrict__ da
                                                   uint8_t* __restrict__ out) {
   __shared__ uint32_t s_len[kSpan];
   __shared__ uint64_t s_os[kSpan + 1];  // local output start of every element (+ block end)
-  __shared__ __attribute__((aligned(16))) uint8_t s_pay[kPkTile + 32];
+  // staged payload: index i = absolute payload byte pay_lo - 16 + i (16-B
+  // front pad for the masked reads of a chunk's earlier elements)
+  __shared__ __attribute__((aligned(16))) uint8_t s_pay[kPkTile + 64];
   __shared__ uint64_t lds_warp[kBlock / 64 + 1];
   __shared__ uint64_t s_blk;
   const uint64_t nv = Vtop[(nb + kSpan - 1) / kSpan];  // total parts
@@ -247,9 +255,11 @@ __global__ void __launch_bounds__(kBlock) pk_emit(const uint8_t* __restrict__ da
         const bool a16 = (((uintptr_t)data) & 15) == 0;
         for (int i = threadIdx.x; i < (nbytes + 15) / 16; i += kBlock) {
           if (a16 && pay_lo + 16 * (uint64_t)(i + 1) <= pay_hi) {
-            *reinterpret_cast<uint4*>(s_pay + 16 * i) = *reinterpret_cast<const uint4*>(data + pay_lo + 16 * (uint64_t)i);
+            *reinterpret_cast<uint4*>(s_pay + 16 + 16 * i) =
+                *reinterpret_cast<const uint4*>(data + pay_lo + 16 * (uint64_t)i);
           } else {
-            for (int k = 0; k < 16 && 16 * i + k < nbytes; ++k) s_pay[16 * i + k] = data[pay_lo + 16 * (uint64_t)i + k];
+            for (int k = 0; k < 16 && 16 * i + k < nbytes; ++k)
+              s_pay[16 + 16 * i + k] = data[pay_lo + 16 * (uint64_t)i + k];
           }
         }
       }
@@ -271,17 +281,47 @@ __global__ void __launch_bounds__(kBlock) pk_emit(const uint8_t* __restrict__ da
             uint8_t b[16];
           } chunk;
           bool full = true;
-          const uint64_t e_end = e + 1 < cnt ? s_os[e + 1] : Lb;
-          if (!stride && l0 >= (int64_t)t0 && l0 + 16 <= (int64_t)t1 && (uint64_t)l0 >= s_os[e] + 4 &&
-              (uint64_t)l0 + 16 <= e_end) {
-            // fast path: the chunk lies inside one element's payload -> 16
-            // contiguous staged bytes, five dword LDS reads + funnel shifts
-            const uint64_t src = Db + s_os[e] - 4 * (uint64_t)e + ((uint64_t)l0 - s_os[e] - 4) - pay_lo;
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(s_pay) + (src >> 2);
-            const uint32_t sh = (uint32_t)(src & 3);
-            const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
-            chunk.v4 = make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
-                                  __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
+          if (!stride && l0 >= (int64_t)t0 && l0 + 16 <= (int64_t)t1) {
+            // the chunk lies inside the tile: assembled branch-free from the
+            // elements that overlap it.  Element j's payload bytes sit in the
+            // output at a fixed shift 4(j+1) from the payload stream, so its
+            // part of the chunk is the 16 staged bytes at (l0 - 4(j+1)) under
+            // a byte mask, and its length prefix is its len shifted into
+            // place; the byte-by-byte walk below (one divergent loop per byte)
+            // is left to the two ragged chunks at a part's edges.
+            uint32_t acc[4] = {0u, 0u, 0u, 0u};
+            const uint64_t ul0 = (uint64_t)l0;
+            for (int j = e; j < cnt && s_os[j] < ul0 + 16; ++j) {
+              const uint64_t oj = s_os[j], oj1 = s_os[j + 1];
+              // prefix: bytes of len_j at chunk positions r .. r+3
+              const int64_t r = (int64_t)oj - l0;
+              if (r > -4) {
+                const uint32_t L = s_len[j];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                  const int sh = (int)r - 4 * d;  // byte position of len's byte 0 in dword d
+                  if (sh > -4 && sh < 4) acc[d] |= sh >= 0 ? L << (8 * sh) : L >> (-8 * sh);
+                }
+              }
+              // payload: chunk positions [pa, pb)
+              const int64_t pa64 = (int64_t)oj + 4 - l0, pb64 = (int64_t)oj1 - l0;
+              const int pa = pa64 < 0 ? 0 : (int)pa64, pb = pb64 > 16 ? 16 : (int)pb64;
+              if (pa < pb) {
+                const uint64_t idx = Db + ul0 - 4 * (uint64_t)(j + 1) - pay_lo + 16;
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(s_pay) + (idx >> 2);
+                const uint32_t sh = (uint32_t)(idx & 3);
+                const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+                const uint32_t wv[4] = {__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                                        __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh)};
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                  const int lo = min(max(pa - 4 * d, 0), 4), hi = min(max(pb - 4 * d, 0), 4);
+                  const uint32_t mk = (uint32_t)((1ull << (8 * hi)) - 1) & ~(uint32_t)((1ull << (8 * lo)) - 1);
+                  acc[d] |= wv[d] & mk;
+                }
+              }
+            }
+            chunk.v4 = make_uint4(acc[0], acc[1], acc[2], acc[3]);
             if (out16) {
               *reinterpret_cast<uint4*>(out + c * 16) = chunk.v4;
             } else {
@@ -304,7 +344,7 @@ __global__ void __launch_bounds__(kBlock) pk_emit(const uint8_t* __restrict__ da
               } else if (stride) {
                 byte = data[(first + e) * stride + (rel - 4)];
               } else {
-                byte = s_pay[Db + s_os[e] - 4 * (uint64_t)e + (rel - 4) - pay_lo];
+                byte = s_pay[Db + s_os[e] - 4 * (uint64_t)e + (rel - 4) - pay_lo + 16];
               }
             }
             chunk.b[k] = byte;
@@ -649,11 +689,13 @@ __global__ void __launch_bounds__(kBlock) idx_emit(const uint8_t* __restrict__ b
 
 // ---- K3 v3: speculative multi-candidate block walk ----------------------------
 constexpr int kXB = 4096;                 // bytes per block (one wave)
-constexpr int kXR = 256;                  // candidate entry offsets per block
-constexpr int kXC = kXR / 64;             // candidates per lane
+// candidate entry offsets per block (XR): a first attempt with 64 (one per
+// lane: elements up to 60 bytes, the common short-string case, for a quarter
+// of the phase-1 work), 256 when an element crossing a block is longer
+constexpr int kXRMax = 256;
 constexpr int kXWaves = kBlock / 64;      // blocks per workgroup
 constexpr uint16_t kXBad = 0xFFFF;        // the chain meets a malformed element
-constexpr uint16_t kXFar = 0xFFFE;        // exit past the next block's first kXR bytes
+constexpr uint16_t kXFar = 0xFFFE;        // exit past the next block's first XR bytes
 constexpr uint16_t kXEnd = 0xFFFD;        // the chain ends exactly at the end of the data
 constexpr uint32_t kSyncAmbig = 0xFFFFFFFFu;
 constexpr uint32_t kSyncNone = 0xFFFFFFFEu;
@@ -700,44 +742,84 @@ __device__ __forceinline__ uint32_t lds_le32(const uint8_t* win, uint32_t off) {
   return __builtin_amdgcn_alignbyte(hi, lo, off & 3);
 }
 
-// One hop of a chain at block-relative position p (p < kXB): returns true while
-// the chain is still inside the block; otherwise *code is final.
-__device__ __forceinline__ bool ix_hop(const uint8_t* win, uint64_t b0, uint64_t nbytes, uint32_t* p, uint32_t* cnt,
-                                       uint32_t* code) {
-  const uint64_t abs = b0 + *p;
-  if (abs + 4 > nbytes) {
-    *code = kXBad;  // truncated length prefix
+// Bytes of data from block start b0, as a 32-bit limit for block-relative
+// hop math (clamped: then no chain can end or run out in this block, and a
+// length past the clamp only means "exit far away").
+struct IxLim {
+  uint32_t lim;
+  bool clamped;
+};
+__device__ __forceinline__ IxLim ix_lim(uint64_t nbytes, uint64_t b0) {
+  const uint64_t r = nbytes > b0 ? nbytes - b0 : 0;
+  return r > 0x7FFFFFF0ull ? IxLim{0x7FFFFFF0u, true} : IxLim{(uint32_t)r, false};
+}
+
+// One hop of a chain at block-relative position p (p < kXB), 32-bit: returns
+// true while the chain is still inside the block; otherwise code is final.
+// UNIFORM: p is wave-uniform and the length is broadcast (readfirstlane), so
+// the whole serial walk runs on the scalar unit beside one LDS read per hop
+// (as a lane-0 VALU walk every hop paid ~20 full-wave VALU issues).
+template <bool UNIFORM, int XR>
+__device__ __forceinline__ bool ix_hop(const uint8_t* win, IxLim l, uint32_t& p, uint32_t& cnt, uint32_t& code) {
+  const uint32_t p4 = p + 4;
+  if (p4 > l.lim) {
+    code = kXBad;  // truncated length prefix
     return false;
   }
-  const uint64_t nx = abs + 4 + (uint64_t)lds_le32(win, *p);
-  if (nx > nbytes) {
-    *code = kXBad;  // element runs past the data
+  uint32_t L = lds_le32(win, p);
+  if constexpr (UNIFORM) L = __builtin_amdgcn_readfirstlane(L);
+  if (L > l.lim - p4) {
+    code = l.clamped ? kXFar : kXBad;  // element runs past the data (or past the clamp)
     return false;
   }
-  ++*cnt;
-  if (nx == nbytes) {
-    *code = kXEnd;
+  const uint32_t nx = p4 + L;
+  ++cnt;
+  if (nx == l.lim && !l.clamped) {
+    code = kXEnd;
     return false;
   }
-  const uint64_t bend = b0 + kXB;
-  if (nx >= bend) {
-    *code = nx - bend < (uint64_t)kXR ? (uint32_t)(nx - bend) : kXFar;
+  if (nx >= (uint32_t)kXB) {
+    const uint32_t o = nx - kXB;
+    code = o < (uint32_t)XR ? o : kXFar;
     return false;
   }
-  *p = (uint32_t)(nx - b0);
+  p = nx;
   return true;
+}
+
+// The uniform walk of a block that ends at least XR + 8 bytes before the
+// data does: no hop can meet the end of the data inside it, so a hop is one
+// broadcast LDS read and a 64-bit scalar add (a length running past the data
+// shows up as an exit beyond the candidate window: FAR, which sends the call
+// to the general path that reports it).  About 12 instructions a hop instead
+// of 25.
+template <int XR>
+__device__ __forceinline__ void ix_walk_fast(const uint8_t* win, uint32_t q, uint32_t& n, uint32_t& code) {
+  for (;;) {
+    const uint32_t L = __builtin_amdgcn_readfirstlane(lds_le32(win, q));
+    const uint64_t nx = (uint64_t)q + 4 + L;
+    ++n;
+    if (nx >= (uint64_t)kXB) {
+      const uint64_t o = nx - kXB;
+      code = o < (uint64_t)XR ? (uint32_t)o : kXFar;
+      return;
+    }
+    q = (uint32_t)nx;
+  }
 }
 
 // Per block: every candidate entry c in [0, kXR) walks only until it leaves
 // the candidate window (phase 1, a few hops, all lanes busy).  Chains from
 // true element starts all leave it at the same position, so phase 2 walks
-// once per DISTINCT window-exit position (typically one: lane 0, serial) to
-// the block exit and hands the result to every candidate that left there.
+// once per DISTINCT window-exit position (typically one; wave-uniform, on the
+// scalar unit) to the block exit and hands the result to every candidate
+// that left there.
+template <int XR>
 __global__ void __launch_bounds__(kBlock) ix_walk(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t nblk,
                                                   uint16_t* __restrict__ tab, uint16_t* __restrict__ tcnt,
                                                   uint32_t* __restrict__ sync) {
   __shared__ __attribute__((aligned(16))) uint8_t win_all[kXWaves][kXB + 16];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint64_t b = (uint64_t)blockIdx.x * kXWaves + wave;
   if (b >= nblk) return;  // wave-uniform; no workgroup barrier below
   uint8_t* win = win_all[wave];
@@ -745,13 +827,16 @@ __global__ void __launch_bounds__(kBlock) ix_walk(const uint8_t* __restrict__ bu
   ix_stage(buf, nbytes, b0, win, lane);
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const IxLim l = ix_lim(nbytes, b0);
+  const bool fast = l.clamped || l.lim >= (uint32_t)(kXB + XR + 8);
+  constexpr int kXC = XR / 64;             // candidates per lane
   constexpr uint32_t kWalk = 0xFFFFFFFFu;  // code of a chain still walking (phase 2 pending)
   uint32_t p[kXC], cnt[kXC], code[kXC];
 #pragma unroll
   for (int j = 0; j < kXC; ++j) {
     p[j] = (uint32_t)(lane + 64 * j);
     cnt[j] = 0;
-    code[j] = b0 + p[j] >= nbytes ? (uint32_t)kXEnd : kWalk;  // no element starts at/after the data end
+    code[j] = p[j] >= l.lim && !l.clamped ? (uint32_t)kXEnd : kWalk;  // no element starts at/after the data end
   }
   // phase 1: walk while inside the candidate window
   bool any;
@@ -759,27 +844,24 @@ __global__ void __launch_bounds__(kBlock) ix_walk(const uint8_t* __restrict__ bu
     any = false;
 #pragma unroll
     for (int j = 0; j < kXC; ++j) {
-      if (code[j] == kWalk && p[j] < (uint32_t)kXR) {
-        if (ix_hop(win, b0, nbytes, &p[j], &cnt[j], &code[j])) any = any || p[j] < (uint32_t)kXR;
+      if (code[j] == kWalk && p[j] < (uint32_t)XR) {
+        if (ix_hop<false, XR>(win, l, p[j], cnt[j], code[j])) any = any || p[j] < (uint32_t)XR;
       }
     }
   } while (__any(any));
-  // phase 2: one serial walk per distinct window-exit position
+  // phase 2: one uniform walk per distinct window-exit position
   for (;;) {
     uint32_t m = 0xFFFFFFFFu;
 #pragma unroll
     for (int j = 0; j < kXC; ++j)
       if (code[j] == kWalk) m = min(m, p[j]);
-    m = wave_min_u32(m);
+    m = __builtin_amdgcn_readfirstlane(wave_min_u32(m));
     if (m == 0xFFFFFFFFu) break;
-    uint32_t c2 = 0, n2 = 0;
-    if (lane == 0) {
-      uint32_t q = m;
-      while (ix_hop(win, b0, nbytes, &q, &n2, &c2)) {
+    uint32_t q = m, c2 = 0, n2 = 0;
+    if (fast) ix_walk_fast<XR>(win, q, n2, c2);
+    else
+      while (ix_hop<true, XR>(win, l, q, n2, c2)) {
       }
-    }
-    c2 = (uint32_t)__shfl((int)c2, 0, 64);
-    n2 = (uint32_t)__shfl((int)n2, 0, 64);
 #pragma unroll
     for (int j = 0; j < kXC; ++j)
       if (code[j] == kWalk && p[j] == m) {
@@ -790,9 +872,9 @@ __global__ void __launch_bounds__(kBlock) ix_walk(const uint8_t* __restrict__ bu
   uint32_t lmin = 0xFFFFFFFFu, lmax = 0;
 #pragma unroll
   for (int j = 0; j < kXC; ++j) {
-    tab[b * kXR + lane + 64 * j] = (uint16_t)code[j];
-    tcnt[b * kXR + lane + 64 * j] = (uint16_t)cnt[j];
-    if (code[j] < (uint32_t)kXR) {
+    tab[b * XR + lane + 64 * j] = (uint16_t)code[j];
+    tcnt[b * XR + lane + 64 * j] = (uint16_t)cnt[j];
+    if (code[j] < (uint32_t)XR) {
       lmin = min(lmin, code[j]);
       lmax = max(lmax, code[j]);
     }
@@ -802,6 +884,7 @@ __global__ void __launch_bounds__(kBlock) ix_walk(const uint8_t* __restrict__ bu
   if (lane == 0) sync[b] = lmin == 0xFFFFFFFFu ? kSyncNone : (lmin == lmax ? lmin : kSyncAmbig);
 }
 
+template <int XR>
 __global__ void __launch_bounds__(kBlock) ix_resolve(const uint16_t* __restrict__ tab, const uint16_t* __restrict__ tcnt,
                                                      const uint32_t* __restrict__ sync, uint64_t nblk,
                                                      uint32_t* __restrict__ entry, uint64_t* __restrict__ count,
@@ -835,8 +918,8 @@ __global__ void __launch_bounds__(kBlock) ix_resolve(const uint16_t* __restrict_
       k = j + 1;
     }
     for (; k < b && e != kEntryNone; ++k) {
-      const uint16_t c = tab[k * kXR + e];
-      e = c < kXR ? c : kEntryNone;
+      const uint16_t c = tab[k * XR + e];
+      e = c < XR ? c : kEntryNone;
     }
   }
   entry[b] = e;
@@ -844,8 +927,8 @@ __global__ void __launch_bounds__(kBlock) ix_resolve(const uint16_t* __restrict_
     count[b] = 0;
     return;
   }
-  count[b] = tcnt[b * kXR + e];
-  const uint16_t c = tab[b * kXR + e];
+  count[b] = tcnt[b * XR + e];
+  const uint16_t c = tab[b * XR + e];
   int reason = -1;
   if (c == kXEnd) reason = kEndEnd;
   else if (c == kXBad) reason = kEndBad;
@@ -887,18 +970,16 @@ __global__ void __launch_bounds__(kBlock) ix_emit(const uint8_t* __restrict__ bu
                                                   const uint64_t* __restrict__ ctop, uint64_t n_expected,
                                                   uint64_t* __restrict__ offs, uint32_t* __restrict__ lens) {
   __shared__ __attribute__((aligned(16))) uint8_t win_all[kXWaves][kXB + 16];
-  __shared__ uint64_t ring_off[kXWaves][64];
-  __shared__ uint32_t ring_len[kXWaves][64];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint64_t b = (uint64_t)blockIdx.x * kXWaves + wave;
   if (b >= nblk) return;
   const uint32_t e = entry[b];
   if (e == kEntryNone) return;
   const uint64_t base = scan2_at(count, ctop, b);
   if (base >= n_expected) return;
-  uint64_t want = count[b];  // count[] holds the exclusive scan: the block's own count is the difference
+  // count[] holds the exclusive scan: the block's own count is the difference
   const uint64_t next = b + 1 < nblk ? scan2_at(count, ctop, b + 1) : ctop[(nblk + kSpan - 1) / kSpan];
-  want = next - base;
+  uint64_t want = next - base;
   if (base + want > n_expected) want = n_expected - base;
   if (want == 0) return;
   uint8_t* win = win_all[wave];
@@ -906,25 +987,31 @@ __global__ void __launch_bounds__(kBlock) ix_emit(const uint8_t* __restrict__ bu
   ix_stage(buf, nbytes, b0, win, lane);
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  uint64_t p = b0 + e;
+  // the chain is wave-uniform: the scalar unit walks it, one broadcast LDS
+  // read per element, and element i of each 64-group goes straight into
+  // lane i's registers (v_writelane) for one coalesced store per group
+  uint32_t p = __builtin_amdgcn_readfirstlane(e);
   for (uint64_t k0 = 0; k0 < want; k0 += 64) {
     const int m = (int)(want - k0 < 64 ? want - k0 : 64);
-    if (lane == 0) {
-      for (int i = 0; i < m; ++i) {
-        const uint32_t L = lds_le32(win, (uint32_t)(p - b0));
-        ring_off[wave][i] = p + 4;
-        ring_len[wave][i] = L;
-        p += 4 + (uint64_t)L;
-      }
+    int my_off = 0, my_len = 0;
+    for (int i = 0; i < m; ++i) {
+      const uint32_t L = __builtin_amdgcn_readfirstlane(lds_le32(win, p));
+      p += 4;
+      // v_writelane with the lane select in M0 (two SGPR operands break the
+      // constant-bus limit); M0 is saved and restored around it, since the
+      // compiler treats it as reserved and ignores a clobber
+      int m0save;
+      asm volatile(
+          "s_mov_b32 %1, m0\n\ts_mov_b32 m0, %4\n\tv_writelane_b32 %0, %2, m0\n\t"
+          "v_writelane_b32 %3, %5, m0\n\ts_mov_b32 m0, %1"
+          : "+v"(my_off), "=&s"(m0save), "+s"(p), "+v"(my_len)
+          : "s"(i), "s"(L));
+      p += L;  // only read again while the next element starts inside the block
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     if (lane < m) {
-      offs[base + k0 + lane] = ring_off[wave][lane];
-      lens[base + k0 + lane] = ring_len[wave][lane];
+      offs[base + k0 + lane] = b0 + (uint32_t)my_off;
+      lens[base + k0 + lane] = (uint32_t)my_len;
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   }
 }
 
@@ -1013,10 +1100,10 @@ static int index_general(const void* buf, uint64_t nbytes, uint64_t n_expected, 
 // 0 / 1 / -1, or 2 (retry larger window) / 3 (fall back), with the device
 // status written.  Synchronises the stream to read the status.
 static int index_v3(const uint8_t* buf, uint64_t nbytes, uint64_t window, uint64_t n_expected, uint64_t* offs,
-                    uint32_t* lens, int* status, hipStream_t s, int* host_status) {
+                    uint32_t* lens, int* status, hipStream_t s, int* host_status, int xr) {
   const uint64_t nblk = (window + kXB - 1) / kXB;
   const uint64_t nc = (nblk + kSpan - 1) / kSpan;
-  const size_t wsb = nblk * kXR * 4 + nblk * 4 + nblk * 4 + nblk * 8 + (nc + 1) * 8 + sizeof(IxCtl) + 256;
+  const size_t wsb = nblk * (size_t)xr * 4 + nblk * 4 + nblk * 4 + nblk * 8 + (nc + 1) * 8 + sizeof(IxCtl) + 256;
   void* ws = nullptr;
   hipError_t e = hipMallocAsync(&ws, wsb, s);
   if (e != hipSuccess) return e;
@@ -1026,13 +1113,18 @@ static int index_v3(const uint8_t* buf, uint64_t nbytes, uint64_t window, uint64
   uint32_t* sync = (uint32_t*)(ctl + 1);
   uint32_t* entry = sync + nblk;
   uint16_t* tab = (uint16_t*)(entry + nblk);
-  uint16_t* tcnt = tab + nblk * kXR;
+  uint16_t* tcnt = tab + nblk * xr;
   e = hipMemsetAsync(ctl, 0xFF, sizeof(IxCtl), s);
   const unsigned wg = (unsigned)((nblk + kXWaves - 1) / kXWaves);
   const unsigned tg = (unsigned)((nblk + kBlock - 1) / kBlock);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(ix_walk, dim3(wg), dim3(kBlock), 0, s, buf, nbytes, nblk, tab, tcnt, sync);
-    hipLaunchKernelGGL(ix_resolve, dim3(tg), dim3(kBlock), 0, s, tab, tcnt, sync, nblk, entry, count, ctl);
+    if (xr == 64) {
+      hipLaunchKernelGGL(ix_walk<64>, dim3(wg), dim3(kBlock), 0, s, buf, nbytes, nblk, tab, tcnt, sync);
+      hipLaunchKernelGGL(ix_resolve<64>, dim3(tg), dim3(kBlock), 0, s, tab, tcnt, sync, nblk, entry, count, ctl);
+    } else {
+      hipLaunchKernelGGL(ix_walk<kXRMax>, dim3(wg), dim3(kBlock), 0, s, buf, nbytes, nblk, tab, tcnt, sync);
+      hipLaunchKernelGGL(ix_resolve<kXRMax>, dim3(tg), dim3(kBlock), 0, s, tab, tcnt, sync, nblk, entry, count, ctl);
+    }
     hipLaunchKernelGGL(ix_mask, dim3(tg), dim3(kBlock), 0, s, count, nblk, ctl);
     hipLaunchKernelGGL(scan2_chunks, dim3((unsigned)nc), dim3(kBlock), 0, s, count, (uint64_t*)nullptr, nblk, ctop,
                        (uint64_t*)nullptr);
@@ -1057,7 +1149,7 @@ static int index_v3(const uint8_t* buf, uint64_t nbytes, uint64_t window, uint64
 // status: device int[4]: [0] = 0 ok / 1 fewer elements than expected / -1
 // malformed; [2..3] = u64 element count found.  Synchronous w.r.t. `stream`
 // (reads the status to size the scan window / pick the path).
-static thread_local int g_last_path = -1;  // 0 serial LDS walk, 1 v3 speculative walk, 2 general
+static thread_local int g_last_path = -1;  // 0 serial LDS walk, 1 v3 walk (64 candidates), 3 v3 (256), 2 general
 static thread_local uint64_t g_last_window = 0;
 
 // Which path the calling thread's last tcamd_index_bytes took (tests, kbench),
@@ -1082,18 +1174,23 @@ extern "C" int tcamd_index_bytes(const void* buf, uint64_t nbytes, uint64_t n_ex
     uint64_t need = 64 * n_expected;
     if (need < (1u << 20)) need = 1u << 20;
     uint64_t window = need < nbytes ? (need + kXB - 1) / kXB * kXB : nbytes;
+    int xr = 64;  // candidate window; 256 after a FAR / unresolved attempt
     for (;;) {
       if (window > nbytes) window = nbytes;
       int st = 0;
       g_last_window = window;
-      const int e = index_v3((const uint8_t*)buf, nbytes, window, n_expected, offs, lens, status, s, &st);
+      const int e = index_v3((const uint8_t*)buf, nbytes, window, n_expected, offs, lens, status, s, &st, xr);
       if (e != hipSuccess) return e;
       if (st == 0 || st == 1 || st == -1) {
-        g_last_path = 1;
+        g_last_path = xr == 64 ? 1 : 3;
         return hipSuccess;
       }
       if (st == 2 && window < nbytes) {
         window = window * 8 < nbytes ? window * 8 : nbytes;
+        continue;
+      }
+      if (st == 3 && xr == 64) {
+        xr = kXRMax;
         continue;
       }
       break;  // 3: fall back (or a window retry that cannot grow)

@@ -299,7 +299,7 @@ def _expect(elems):
 def test_index_bytes_v3_speculative_walk(env, kind):
     """K3 v3: candidate walks + resolve + emit on ~1.5 MB of BYTES with a
     tail of unrelated region bytes; must match the host walk and take the
-    v3 path (elements shorter than the 256-B candidate window)."""
+    v3 path with the 64-B candidate window (elements shorter than 60 B)."""
     torch, hip = env
     rng = np.random.default_rng({"ascii": 1, "zeros": 2, "binary": 3, "empty": 4}[kind])
     n = 60000
@@ -357,13 +357,14 @@ def test_index_bytes_window_grows_and_long_elements_fall_back(env):
     eo, el = _expect(elems)
     np.testing.assert_array_equal(offs, eo)
     np.testing.assert_array_equal(lens, el)
-    # short elements but a first window that is too small: v3 retries with 8x windows
+    # elements of 150-250 B and a first window that is too small: v3 retries
+    # with 8x windows, and with the 256-B candidate window (longer than 60 B)
     elems = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(150, 250, 12000)]
     wire = _wire(elems)
     buf = torch.from_numpy(np.concatenate([wire, np.zeros(1 << 22, np.uint8)])).cuda()
     st, found, offs, lens = _index(torch, hip, buf, buf.numel(), len(elems))
     path, window = hip.index_bytes_last_path()
-    assert st == 0 and found == len(elems) and path == 1 and window > (1 << 20)
+    assert st == 0 and found == len(elems) and path == 3 and window > (1 << 20)
     eo, el = _expect(elems)
     np.testing.assert_array_equal(offs, eo)
 

@@ -721,7 +721,9 @@ def pack_bytes_strided(data_ptr, stride, lens_ptr, n, out_ptr, workspace_ptr, st
 
 def index_bytes_last_path():
     """(path, window) of this thread's last index_bytes: 0 serial walk, 1 v3
-    speculative block walk, 2 general pointer-doubling fallback."""
+    speculative block walk (64-B candidate window), 3 v3 with the 256-B
+    window (an element of 60..252 B crossed a block), 2 general
+    pointer-doubling fallback."""
     w = ctypes.c_uint64(0)
     p = _load().tcamd_index_bytes_last_path(ctypes.byref(w))
     return p, w.value
