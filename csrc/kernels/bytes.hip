@@ -793,18 +793,38 @@ __device__ __forceinline__ bool ix_hop(const uint8_t* win, IxLim l, uint32_t& p,
 // shows up as an exit beyond the candidate window: FAR, which sends the call
 // to the general path that reports it).  About 12 instructions a hop instead
 // of 25.
-template <int XR>
-__device__ __forceinline__ void ix_walk_fast(const uint8_t* win, uint32_t q, uint32_t& n, uint32_t& code) {
+// REC: also record every element start the walk visits (u16, block-relative)
+// into rec[0..n): element i of each 64-group goes into lane i (v_writelane)
+// and each full group is stored with one 128-B store, so ix_emit can copy the
+// chain instead of walking it a second time.
+template <int XR, bool REC>
+__device__ __forceinline__ void ix_walk_fast(const uint8_t* win, uint32_t q, uint32_t& n, uint32_t& code,
+                                             uint16_t* __restrict__ rec, int lane) {
+  int grp = 0;
+  uint32_t k = 0;  // elements in the current group
   for (;;) {
     const uint32_t L = __builtin_amdgcn_readfirstlane(lds_le32(win, q));
+    if constexpr (REC) {
+      int m0save;
+      asm volatile("s_mov_b32 %1, m0\n\ts_mov_b32 m0, %3\n\tv_writelane_b32 %0, %2, m0\n\ts_mov_b32 m0, %1"
+                   : "+v"(grp), "=&s"(m0save)
+                   : "s"(q), "s"(k));
+      if (++k == 64) {
+        rec[n + 1 - 64 + lane] = (uint16_t)grp;
+        k = 0;
+      }
+    }
     const uint64_t nx = (uint64_t)q + 4 + L;
     ++n;
     if (nx >= (uint64_t)kXB) {
       const uint64_t o = nx - kXB;
       code = o < (uint64_t)XR ? (uint32_t)o : kXFar;
-      return;
+      break;
     }
     q = (uint32_t)nx;
+  }
+  if constexpr (REC) {
+    if (k && lane < (int)k) rec[n - k + lane] = (uint16_t)grp;
   }
 }
 
@@ -817,7 +837,8 @@ __device__ __forceinline__ void ix_walk_fast(const uint8_t* win, uint32_t q, uin
 template <int XR>
 __global__ void __launch_bounds__(kBlock) ix_walk(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t nblk,
                                                   uint16_t* __restrict__ tab, uint16_t* __restrict__ tcnt,
-                                                  uint32_t* __restrict__ sync) {
+                                                  uint32_t* __restrict__ sync, uint16_t* __restrict__ rec,
+                                                  uint32_t* __restrict__ rec_head) {
   __shared__ __attribute__((aligned(16))) uint8_t win_all[kXWaves][kXB + 16];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint64_t b = (uint64_t)blockIdx.x * kXWaves + wave;
@@ -849,19 +870,31 @@ __global__ void __launch_bounds__(kBlock) ix_walk(const uint8_t* __restrict__ bu
       }
     }
   } while (__any(any));
-  // phase 2: one uniform walk per distinct window-exit position
-  for (;;) {
-    uint32_t m = 0xFFFFFFFFu;
+  // phase 2: one uniform walk per distinct window-exit position.  With a
+  // single one (the common case), the walk records its element starts for
+  // ix_emit: rec_head[b] = (count << 16) | first position (0xFFFFFFFF: none)
+  uint32_t head = 0xFFFFFFFFu;
+  for (int pass = 0;; ++pass) {
+    uint32_t m = 0xFFFFFFFFu, mx = 0;
 #pragma unroll
     for (int j = 0; j < kXC; ++j)
-      if (code[j] == kWalk) m = min(m, p[j]);
+      if (code[j] == kWalk) {
+        m = min(m, p[j]);
+        mx = max(mx, p[j]);
+      }
     m = __builtin_amdgcn_readfirstlane(wave_min_u32(m));
     if (m == 0xFFFFFFFFu) break;
+    const bool single = pass == 0 && __builtin_amdgcn_readfirstlane(wave_max_u32(mx)) == m;
     uint32_t q = m, c2 = 0, n2 = 0;
-    if (fast) ix_walk_fast<XR>(win, q, n2, c2);
-    else
+    if (fast && single) {
+      ix_walk_fast<XR, true>(win, q, n2, c2, rec + b * (kXB / 4), lane);
+      head = (n2 << 16) | m;
+    } else if (fast) {
+      ix_walk_fast<XR, false>(win, q, n2, c2, nullptr, lane);
+    } else {
       while (ix_hop<true, XR>(win, l, q, n2, c2)) {
       }
+    }
 #pragma unroll
     for (int j = 0; j < kXC; ++j)
       if (code[j] == kWalk && p[j] == m) {
@@ -881,7 +914,10 @@ __global__ void __launch_bounds__(kBlock) ix_walk(const uint8_t* __restrict__ bu
   }
   lmin = wave_min_u32(lmin);
   lmax = wave_max_u32(lmax);
-  if (lane == 0) sync[b] = lmin == 0xFFFFFFFFu ? kSyncNone : (lmin == lmax ? lmin : kSyncAmbig);
+  if (lane == 0) {
+    sync[b] = lmin == 0xFFFFFFFFu ? kSyncNone : (lmin == lmax ? lmin : kSyncAmbig);
+    rec_head[b] = head;
+  }
 }
 
 template <int XR>
@@ -968,7 +1004,9 @@ __global__ void __launch_bounds__(kBlock) ix_emit(const uint8_t* __restrict__ bu
                                                   const uint32_t* __restrict__ entry,
                                                   const uint64_t* __restrict__ count,
                                                   const uint64_t* __restrict__ ctop, uint64_t n_expected,
-                                                  uint64_t* __restrict__ offs, uint32_t* __restrict__ lens) {
+                                                  uint64_t* __restrict__ offs, uint32_t* __restrict__ lens,
+                                                  const uint16_t* __restrict__ rec,
+                                                  const uint32_t* __restrict__ rec_head) {
   __shared__ __attribute__((aligned(16))) uint8_t win_all[kXWaves][kXB + 16];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint64_t b = (uint64_t)blockIdx.x * kXWaves + wave;
@@ -989,8 +1027,42 @@ __global__ void __launch_bounds__(kBlock) ix_emit(const uint8_t* __restrict__ bu
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   // the chain is wave-uniform: the scalar unit walks it, one broadcast LDS
   // read per element, and element i of each 64-group goes straight into
-  // lane i's registers (v_writelane) for one coalesced store per group
+  // lane i's registers (v_writelane) for one coalesced store per group.
+  // When ix_walk recorded the chain from its window exit (rec_head), only the
+  // elements before that position are walked; the rest are copied with every
+  // lane reading its own element's length.
   uint32_t p = __builtin_amdgcn_readfirstlane(e);
+  const uint32_t head = rec_head[b];
+  if (head != 0xFFFFFFFFu) {
+    const uint32_t m = head & 0xFFFFu, nrec = head >> 16;
+    int my_off = 0, my_len = 0;
+    uint32_t k = 0;
+    while (p < m && k < want && k < 64) {
+      const uint32_t L = __builtin_amdgcn_readfirstlane(lds_le32(win, p));
+      int m0save;
+      asm volatile(
+          "s_mov_b32 %1, m0\n\ts_mov_b32 m0, %4\n\tv_writelane_b32 %0, %2, m0\n\t"
+          "v_writelane_b32 %3, %5, m0\n\ts_mov_b32 m0, %1"
+          : "+v"(my_off), "=&s"(m0save), "+s"(p), "+v"(my_len)
+          : "s"(k), "s"(L));
+      p += 4 + L;
+      ++k;
+    }
+    if (p == m && (uint64_t)k + nrec >= want) {
+      if (lane < (int)k) {
+        offs[base + lane] = b0 + 4 + (uint32_t)my_off;
+        lens[base + lane] = (uint32_t)my_len;
+      }
+      const uint16_t* r = rec + b * (kXB / 4);
+      for (uint64_t i = lane; i < want - k; i += 64) {
+        const uint32_t q = r[i];
+        offs[base + k + i] = b0 + q + 4;
+        lens[base + k + i] = lds_le32(win, q);
+      }
+      return;
+    }
+    p = __builtin_amdgcn_readfirstlane(e);  // the chain left the window elsewhere: walk it all
+  }
   for (uint64_t k0 = 0; k0 < want; k0 += 64) {
     const int m = (int)(want - k0 < 64 ? want - k0 : 64);
     int my_off = 0, my_len = 0;
@@ -1103,7 +1175,9 @@ static int index_v3(const uint8_t* buf, uint64_t nbytes, uint64_t window, uint64
                     uint32_t* lens, int* status, hipStream_t s, int* host_status, int xr) {
   const uint64_t nblk = (window + kXB - 1) / kXB;
   const uint64_t nc = (nblk + kSpan - 1) / kSpan;
-  const size_t wsb = nblk * (size_t)xr * 4 + nblk * 4 + nblk * 4 + nblk * 8 + (nc + 1) * 8 + sizeof(IxCtl) + 256;
+  // + the walk's recorded chains: kXB / 4 u16 starts and a head word per block
+  const size_t wsb = nblk * (size_t)xr * 4 + nblk * 4 + nblk * 4 + nblk * 8 + (nc + 1) * 8 + sizeof(IxCtl) + 256 +
+                     nblk * (kXB / 4) * 2 + nblk * 4 + 256;
   void* ws = nullptr;
   hipError_t e = hipMallocAsync(&ws, wsb, s);
   if (e != hipSuccess) return e;
@@ -1114,15 +1188,18 @@ static int index_v3(const uint8_t* buf, uint64_t nbytes, uint64_t window, uint64
   uint32_t* entry = sync + nblk;
   uint16_t* tab = (uint16_t*)(entry + nblk);
   uint16_t* tcnt = tab + nblk * xr;
+  uint32_t* rec_head = (uint32_t*)(((uintptr_t)(tcnt + nblk * xr) + 255) & ~(uintptr_t)255);
+  uint16_t* rec = (uint16_t*)(((uintptr_t)(rec_head + nblk) + 255) & ~(uintptr_t)255);
   e = hipMemsetAsync(ctl, 0xFF, sizeof(IxCtl), s);
   const unsigned wg = (unsigned)((nblk + kXWaves - 1) / kXWaves);
   const unsigned tg = (unsigned)((nblk + kBlock - 1) / kBlock);
   if (e == hipSuccess) {
     if (xr == 64) {
-      hipLaunchKernelGGL(ix_walk<64>, dim3(wg), dim3(kBlock), 0, s, buf, nbytes, nblk, tab, tcnt, sync);
+      hipLaunchKernelGGL(ix_walk<64>, dim3(wg), dim3(kBlock), 0, s, buf, nbytes, nblk, tab, tcnt, sync, rec, rec_head);
       hipLaunchKernelGGL(ix_resolve<64>, dim3(tg), dim3(kBlock), 0, s, tab, tcnt, sync, nblk, entry, count, ctl);
     } else {
-      hipLaunchKernelGGL(ix_walk<kXRMax>, dim3(wg), dim3(kBlock), 0, s, buf, nbytes, nblk, tab, tcnt, sync);
+      hipLaunchKernelGGL(ix_walk<kXRMax>, dim3(wg), dim3(kBlock), 0, s, buf, nbytes, nblk, tab, tcnt, sync, rec,
+                         rec_head);
       hipLaunchKernelGGL(ix_resolve<kXRMax>, dim3(tg), dim3(kBlock), 0, s, tab, tcnt, sync, nblk, entry, count, ctl);
     }
     hipLaunchKernelGGL(ix_mask, dim3(tg), dim3(kBlock), 0, s, count, nblk, ctl);
@@ -1137,7 +1214,7 @@ static int index_v3(const uint8_t* buf, uint64_t nbytes, uint64_t window, uint64
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e == hipSuccess && (hs[0] == 0 || hs[0] == 1)) {
     hipLaunchKernelGGL(ix_emit, dim3(wg), dim3(kBlock), 0, s, buf, nbytes, nblk, entry, count, ctop, n_expected, offs,
-                       lens);
+                       lens, rec, rec_head);
     e = hipGetLastError();
   }
   hipError_t f = hipFreeAsync(ws, s);

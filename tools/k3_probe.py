@@ -51,7 +51,9 @@ def main():
             print("size %.3g n %d: status %d path %d window %d  %.1f us  %.1f GB/s" % (
                 size, ne, int(status[0]), path, window, dt * 1e6, total / dt / 1e9), flush=True)
         ok = np.array_equal(lns.cpu().numpy().view(np.uint32), lens)
-        print("lens match:", ok, flush=True)
+        exp_offs = np.concatenate([[0], np.cumsum(lens.astype(np.int64) + 4)[:-1]]) + 4
+        ok_o = np.array_equal(offs.cpu().numpy(), exp_offs)
+        print("lens match:", ok, "offsets match:", ok_o, flush=True)
 
 
 if __name__ == "__main__":
