@@ -1937,9 +1937,17 @@ X3Plan x3_plan(int M, int K, int N) {
     const char* e = getenv("TCAMD_X3_SPLITK_BELOW");
     return e ? atoi(e) : 192;
   }();
+  // split-K cap: the 3x3 that follows re-reads every split's partials of its
+  // band, so more splits trade 1x1 parallelism for 3x3 staging.  4 measured
+  // best (bs1 1.005 -> 0.975 ms, bs8 1.166 -> 1.082 ms vs uncapped, 8-16
+  // splits; profiles/r3_splitk_cap.log); TCAMD_X3_MAX_SPLITS overrides
+  static const int max_splits = [] {
+    const char* e = getenv("TCAMD_X3_MAX_SPLITS");
+    return e ? std::max(1, atoi(e)) : 4;
+  }();
   if (pl.tiles < splitk_below && K >= 4 * kBK) {
     const int steps = K / kBK;
-    int want = std::min(steps / 2, (384 + pl.tiles - 1) / pl.tiles);
+    int want = std::min(std::min(steps / 2, (384 + pl.tiles - 1) / pl.tiles), max_splits);
     if (want > 1) {
       pl.k_per_split = ((steps + want - 1) / want) * kBK;
       pl.splits = (K + pl.k_per_split - 1) / pl.k_per_split;
