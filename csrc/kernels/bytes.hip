@@ -365,6 +365,231 @@ __global__ void __launch_bounds__(kBlock) pk_emit(const uint8_t* __restrict__ da
   }
 }
 
+// Packed payload (stride 0), assembled a dword at a time (round 3b).  Every
+// element is >= 4 output bytes (its length prefix), so a 4-byte output dword
+// holds bytes of at most two elements j, j+1: the tail of j (prefix bytes
+// and/or payload) and the head of j+1's prefix.  Its owner j (the element
+// holding its byte 0) comes from a per-tile mark table: element j marks the
+// first dword starting inside it, and a block max-scan over the 2048 marks of
+// the tile hands every lane the owners of its 8 dwords (no binary search).
+// One 16-B LDS read of {start, len} for j and j+1 then gives the dword as
+//   (len_j >> 8 rel) | (payload under a byte mask) | (len_{j+1} << 8 s)
+// with rel = dword start - start_j and s = start_{j+1} - dword start, the
+// payload being the staged stream at a per-element shift of 4(j+1).  Local
+// offsets are 32-bit; a block whose output exceeds big_lim bytes goes through
+// a byte-granular 64-bit path instead.  Parts are dealt to workgroups in
+// contiguous runs, so the part -> block search runs once per workgroup.
+constexpr int kPkQ = kPkTile / 4;     // dwords per tile
+constexpr int kPkQT = kPkQ / kBlock;  // dwords per thread (8, contiguous)
+static_assert(kPkQT == 8, "pk_emit_packed assumes 8 dwords per thread");
+
+__global__ void __launch_bounds__(kBlock) pk_emit_packed(const uint8_t* __restrict__ data,
+                                                         const uint32_t* __restrict__ lens, uint64_t n, uint64_t nb,
+                                                         const uint64_t* __restrict__ P,
+                                                         const uint64_t* __restrict__ Ptop,
+                                                         const uint64_t* __restrict__ V,
+                                                         const uint64_t* __restrict__ Vtop, uint8_t* __restrict__ out,
+                                                         uint64_t big_lim) {
+  __shared__ uint2 s_ol[kSpan + 2];  // {local output start, len}; [cnt] = {Lb, 0}, [cnt+1] = sentinel
+  __shared__ __attribute__((aligned(16))) uint16_t s_mark[kPkQ];
+  // staged payload (index i = payload byte pay_lo - 16 + i); u64 starts on the big path
+  __shared__ __attribute__((aligned(16))) uint8_t s_pay[kPkTile + 64];
+  __shared__ uint64_t lds_warp[kBlock / 64 + 1];
+  __shared__ uint32_t s_wmax[kBlock / 64];
+  __shared__ int s_ez;
+  static_assert((kSpan + 1) * 8 <= kPkTile + 64, "u64 starts overlay the staging buffer");
+  uint64_t* s_os64 = reinterpret_cast<uint64_t*>(s_pay);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint64_t nv = Vtop[(nb + kSpan - 1) / kSpan];  // total parts
+  const uint64_t v0 = (uint64_t)blockIdx.x * nv / gridDim.x, v1 = (uint64_t)(blockIdx.x + 1) * nv / gridDim.x;
+  if (v0 >= v1) return;
+  const bool out16 = (((uintptr_t)out) & 15) == 0;
+  const bool a16 = (((uintptr_t)data) & 15) == 0;
+  uint64_t b;
+  {
+    uint64_t lo = 0, hi = nb;
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (scan2_at(V, Vtop, mid) <= v0) lo = mid;
+      else hi = mid;
+    }
+    b = lo;
+  }
+  uint64_t Vb = scan2_at(V, Vtop, b), Vn = b + 1 < nb ? scan2_at(V, Vtop, b + 1) : nv;
+  uint64_t cur = ~(uint64_t)0, Lb = 0;
+  int cnt = 0;
+  bool big = false;
+  for (uint64_t v = v0; v < v1; ++v) {
+    while (v >= Vn) {
+      ++b;
+      Vb = Vn;
+      Vn = b + 1 < nb ? scan2_at(V, Vtop, b + 1) : nv;
+    }
+    const uint64_t first = b * kSpan;
+    if (b != cur) {
+      cnt = (int)(n - first < (uint64_t)kSpan ? n - first : (uint64_t)kSpan);
+      uint32_t L[kPer];
+      uint64_t loc[kPer], sum = 0;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const int e = tid * kPer + k;
+        L[k] = e < cnt ? lens[first + e] : 0;
+        loc[k] = e < cnt ? (uint64_t)L[k] + 4 : 0;
+        sum += loc[k];
+      }
+      uint64_t excl = block_exclusive_scan(sum, lds_warp, &Lb);
+      big = Lb > big_lim;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const int e = tid * kPer + k;
+        s_ol[e] = make_uint2((uint32_t)excl, L[k]);
+        if (big) s_os64[e] = excl;
+        excl += loc[k];
+      }
+      if (tid == 0) {
+        s_ol[cnt] = make_uint2((uint32_t)Lb, 0u);
+        s_ol[cnt + 1] = make_uint2(0xFFFFFFFFu, 0u);
+        if (big) s_os64[cnt] = Lb;
+      }
+      cur = b;
+      __syncthreads();
+    }
+    const uint64_t Db = scan2_at(P, Ptop, b);  // block payload start in data
+    const uint64_t Ob = Db + 4 * first;        // block output start
+    const uint64_t q0 = (v - Vb) * kPkPart;
+    const uint64_t q1 = q0 + kPkPart < Lb ? q0 + kPkPart : Lb;
+    if (big) {
+      for (uint64_t pos = q0 + tid; pos < q1; pos += kBlock) {
+        int lo = 0, hi = cnt;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (s_os64[mid] <= pos) lo = mid;
+          else hi = mid;
+        }
+        const uint64_t rel = pos - s_os64[lo];
+        out[Ob + pos] = rel < 4 ? (uint8_t)(s_ol[lo].y >> (8 * rel))
+                                : data[Db + s_os64[lo] - 4 * (uint64_t)lo + (rel - 4)];
+      }
+      __syncthreads();
+      continue;
+    }
+    const int iq0 = (int)q0, iq1 = (int)q1;
+    // owner of the part's first byte (wave-uniform search over the starts)
+    int ea;
+    {
+      int lo = 0, hi = cnt;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if ((int)s_ol[mid].x <= iq0) lo = mid;
+        else hi = mid;
+      }
+      ea = lo;
+    }
+    const uint64_t c0 = (Ob + q0) / 16, c1 = (Ob + q1 + 15) / 16;
+    for (uint64_t ct = c0; ct < c1; ct += kPkTile / 16) {
+      const int base = (int)((int64_t)(ct * 16) - (int64_t)Ob);  // local byte of the tile's dword 0
+      const int tb0 = base > iq0 ? base : iq0, tb1 = base + kPkTile < iq1 ? base + kPkTile : iq1;
+      reinterpret_cast<uint4*>(s_mark)[tid] = make_uint4(0u, 0u, 0u, 0u);
+      __syncthreads();
+      // marks: element j -> the first tile dword starting inside it
+      for (int j = ea + tid; j < cnt; j += kBlock) {
+        const int oj = (int)s_ol[j].x;
+        if (oj >= tb1) break;
+        const int oj1 = (int)s_ol[j + 1].x;
+        int q = (oj - base + 3) >> 2;
+        q = q < 0 ? 0 : q;
+        if (q < kPkQ) s_mark[q] = (uint16_t)(j + 1);
+        if (oj <= tb1 - 1 && tb1 - 1 < oj1) s_ez = j;
+      }
+      __syncthreads();
+      const int ez = s_ez;
+      // payload bytes the tile needs: [payload pos of tb0's element, of tb1-1's]
+      const int oa = (int)s_ol[ea].x, oz = (int)s_ol[ez].x;
+      const uint64_t pa = (uint64_t)(oa - 4 * ea + (tb0 - oa > 4 ? tb0 - oa - 4 : 0));
+      const uint64_t pz = (uint64_t)(oz - 4 * ez + (tb1 - 1 - oz >= 4 ? tb1 - oz - 4 : 0));
+      const uint64_t pay_lo = (Db + pa) & ~(uint64_t)15;
+      const uint64_t pay_hi = Db + (pz > pa ? pz : pa);
+      const int nbytes = (int)(pay_hi - pay_lo);  // <= kPkTile + 15
+      const int nvec = (nbytes + 15) / 16;
+      auto ldv = [&](int i) {
+        return a16 && 16 * (i + 1) <= nbytes ? *reinterpret_cast<const uint4*>(data + pay_lo + 16 * (uint64_t)i)
+                                             : make_uint4(0u, 0u, 0u, 0u);
+      };
+      const uint4 st0 = ldv(tid), st1 = ldv(tid + kBlock), st2 = ldv(tid + 2 * kBlock);
+      // owners of this thread's 8 dwords: running max of the marks
+      const uint4 mk = reinterpret_cast<const uint4*>(s_mark)[tid];
+      uint32_t m[kPkQT];
+      m[0] = mk.x & 0xFFFFu;
+      m[1] = mk.x >> 16;
+      m[2] = mk.y & 0xFFFFu;
+      m[3] = mk.y >> 16;
+      m[4] = mk.z & 0xFFFFu;
+      m[5] = mk.z >> 16;
+      m[6] = mk.w & 0xFFFFu;
+      m[7] = mk.w >> 16;
+#pragma unroll
+      for (int d = 1; d < kPkQT; ++d) m[d] = m[d] > m[d - 1] ? m[d] : m[d - 1];
+      uint32_t x = m[kPkQT - 1];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x = x > y ? x : y;
+      }
+      if (lane == 63) s_wmax[wid] = x;
+      uint32_t carry = __shfl_up(x, 1, 64);
+      if (lane == 0) carry = 0;
+      auto stv = [&](int i, const uint4& v) {
+        if (a16 && 16 * (i + 1) <= nbytes) *reinterpret_cast<uint4*>(s_pay + 16 + 16 * i) = v;
+      };
+      stv(tid, st0);
+      stv(tid + kBlock, st1);
+      stv(tid + 2 * kBlock, st2);
+      for (int i = tid; i < nvec; i += kBlock) {
+        if (a16 && 16 * (i + 1) <= nbytes) continue;
+        for (int k = 0; k < 16 && 16 * i + k < nbytes; ++k) s_pay[16 + 16 * i + k] = data[pay_lo + 16 * (uint64_t)i + k];
+      }
+      __syncthreads();
+      if (carry < (uint32_t)(ea + 1)) carry = (uint32_t)(ea + 1);
+      for (int w = 0; w < wid; ++w) carry = carry > s_wmax[w] ? carry : s_wmax[w];
+      const int pbase = (int)((int64_t)Db - (int64_t)pay_lo) + 16;  // staged index of local payload pos 0
+      const int lb0 = base + 32 * tid;                             // local byte of this thread's dword 0
+      uint32_t wv[kPkQT];
+#pragma unroll
+      for (int d = 0; d < kPkQT; ++d) {
+        const int j = (int)(m[d] > carry ? m[d] : carry) - 1;
+        const int u = lb0 + 4 * d;
+        const uint2 ej = s_ol[j], ej1 = s_ol[j + 1];  // one ds_read2_b64
+        const int rel = u - (int)ej.x, s = (int)ej1.x - u;
+        // branch-free: all-ones masks from sign bits, byte ranges from clamped 64-bit shifts
+        uint32_t w = (ej.y >> (8 * (rel & 3))) & (uint32_t)((rel - 4) >> 31);
+        w |= (ej1.y << (8 * (s & 3))) & (uint32_t)((s - 4) >> 31);
+        int pix = pbase + u - 4 * (j + 1);
+        pix = min(max(pix, 0), kPkTile + 56);
+        const uint32_t* pw = reinterpret_cast<const uint32_t*>(s_pay) + (pix >> 2);
+        const uint32_t pv = __builtin_amdgcn_alignbyte(pw[1], pw[0], (uint32_t)(pix & 3));
+        // payload bytes of j in this dword: [4 - rel, s) when rel < 4, [0, s) after
+        const int rc = min(max(rel, 0), 4), sc = min(max(s, 0), 4);
+        const uint32_t lo_m = (uint32_t)(~0ull << (32 - 8 * rc));
+        const uint32_t hi_m = (uint32_t)(0xFFFFFFFFull >> (32 - 8 * sc));
+        wv[d] = w | (pv & lo_m & hi_m);
+      }
+      const uint64_t g = ct * 16 + 32 * (uint64_t)tid;
+      if (lb0 >= tb0 && lb0 + 32 <= tb1 && out16) {
+        *reinterpret_cast<uint4*>(out + g) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        *reinterpret_cast<uint4*>(out + g + 16) = make_uint4(wv[4], wv[5], wv[6], wv[7]);
+      } else if (lb0 < tb1 && lb0 + 32 > tb0) {
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+          const int pos = lb0 + k;
+          if (pos >= tb0 && pos < tb1) out[g + k] = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
+        }
+      }
+      // the next tile starts at tb1: owned by ez, or by ez + 1 when it starts there
+      ea = (int)s_ol[ez + 1].x <= tb1 ? ez + 1 : ez;
+    }
+  }
+}
+
 constexpr int kWin = 32768;  // LDS window (bytes)
 
 __global__ void __launch_bounds__(kBlock) index_bytes(const uint8_t* __restrict__ buf, uint64_t nbytes,
@@ -1110,8 +1335,17 @@ static int pack_impl(const void* data, uint64_t stride, const uint32_t* lens, ui
   hipLaunchKernelGGL(scan2_top, dim3(1), dim3(kBlock), 0, s, ta, tb, nc);
   // persistent grid over the parts (~20 KiB LDS per workgroup: 7 per CU)
   const uint64_t grid = nb < 1792 ? nb : 1792;
-  hipLaunchKernelGGL(pk_emit, dim3((unsigned)grid), dim3(kBlock), 0, s, (const uint8_t*)data, stride, lens, n, nb, S, ta,
-                     parts, tb, (uint8_t*)out);
+  static const bool legacy = getenv("TCAMD_PK_LEGACY") && atoi(getenv("TCAMD_PK_LEGACY"));
+  if (stride || legacy) {
+    hipLaunchKernelGGL(pk_emit, dim3((unsigned)grid), dim3(kBlock), 0, s, (const uint8_t*)data, stride, lens, n, nb, S,
+                       ta, parts, tb, (uint8_t*)out);
+  } else {
+    // blocks whose output passes big_lim take the 64-bit byte path (tests lower it)
+    static const uint64_t big_lim =
+        getenv("TCAMD_PK_BIG_LIM") ? strtoull(getenv("TCAMD_PK_BIG_LIM"), nullptr, 10) : ((1ull << 31) - (1ull << 20));
+    hipLaunchKernelGGL(pk_emit_packed, dim3((unsigned)grid), dim3(kBlock), 0, s, (const uint8_t*)data, lens, n, nb, S,
+                       ta, parts, tb, (uint8_t*)out, big_lim);
+  }
   return hipGetLastError();
 }
 

@@ -433,3 +433,83 @@ def test_image_preprocess_on_device_matches_host(env, scaling, fmt, dtype):
     assert got.shape == want.shape and got.dtype == want.dtype
     tol = 1e-5 if dtype == "FP32" else 2e-3
     np.testing.assert_allclose(got.astype(np.float32), want.astype(np.float32), rtol=tol, atol=tol * 128)
+
+
+def _pack_ref(payload, lens):
+    """Wire-format reference built with numpy (u32 LE length || bytes)."""
+    n = lens.size
+    out = np.empty(int(lens.sum()) + 4 * n, dtype=np.uint8)
+    o_starts = np.concatenate([[0], np.cumsum(lens.astype(np.int64) + 4)[:-1]])
+    pre = lens.astype("<u4").view(np.uint8).reshape(n, 4)
+    for k in range(4):
+        out[o_starts + k] = pre[:, k]
+    # payload bytes: output index = payload index + 4 * (element index + 1)
+    elem = np.repeat(np.arange(n), lens.astype(np.int64))
+    out[np.arange(payload.size) + 4 * (elem + 1)] = payload
+    return out
+
+
+@pytest.mark.parametrize("doff,ooff", [(0, 0), (5, 3), (1, 14)])
+def test_pack_bytes_dword_assembly_misaligned(env, doff, ooff):
+    """K2 dword-assembled emit (pk_emit_packed): empty, short, tile-spanning
+    and block-spanning elements, with data / output pointers off 16-B."""
+    torch, hip = env
+    rng = np.random.default_rng(doff * 7 + ooff)
+    n = 60000
+    lens = rng.integers(0, 40, n).astype(np.uint32)
+    lens[rng.integers(0, n, 40)] = 0
+    lens[rng.integers(0, n, 12)] = rng.integers(8000, 70000, 12).astype(np.uint32)  # > one tile / part
+    lens[1024:2048] = 0  # a whole block of prefixes only
+    payload = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    d_payload = torch.zeros(payload.size + 32, device="cuda", dtype=torch.uint8)
+    d_payload[doff:doff + payload.size] = torch.from_numpy(payload).cuda()
+    d_lens = torch.from_numpy(lens.view(np.int32).copy()).cuda()
+    total = int(lens.sum()) + 4 * n
+    out = torch.zeros(total + 64, device="cuda", dtype=torch.uint8)
+    ws = torch.empty(hip.pack_bytes_workspace(n), device="cuda", dtype=torch.uint8)
+    hip.pack_bytes(d_payload.data_ptr() + doff, d_lens.data_ptr(), n, out.data_ptr() + ooff, ws.data_ptr(),
+                   _stream(torch))
+    got = out.cpu().numpy()
+    ref = _pack_ref(payload, lens)
+    assert np.array_equal(got[ooff:ooff + total], ref)
+    assert not got[:ooff].any() and not got[ooff + total:].any()
+
+
+_BIG_PATH_SCRIPT = r"""
+import numpy as np, torch, sys
+sys.path.insert(0, %r)
+from triton_client_amd.ops import hip
+from tests.test_kernels_gpu import _pack_ref
+rng = np.random.default_rng(3)
+n = 5000
+lens = rng.integers(0, 60, n).astype(np.uint32)
+lens[7] = 100000
+payload = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+total = int(lens.sum()) + 4 * n
+out = torch.zeros(total + 16, device="cuda", dtype=torch.uint8)
+ws = torch.empty(hip.pack_bytes_workspace(n), device="cuda", dtype=torch.uint8)
+d_p = torch.from_numpy(payload).cuda()
+d_l = torch.from_numpy(lens.view(np.int32).copy()).cuda()
+hip.pack_bytes(d_p.data_ptr(), d_l.data_ptr(), n, out.data_ptr() + 1, ws.data_ptr(),
+               torch.cuda.current_stream().cuda_stream)
+got = out.cpu().numpy()
+assert np.array_equal(got[1:1 + total], _pack_ref(payload, lens)), "mismatch"
+assert got[0] == 0 and not got[1 + total:].any()
+print("BIG_OK")
+"""
+
+
+@pytest.mark.timeout(300)
+def test_pack_bytes_big_block_path():
+    """Blocks whose output passes the 32-bit local-offset limit take a 64-bit
+    byte path; TCAMD_PK_BIG_LIM=0 forces every block onto it (own process,
+    the limit is read once)."""
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TCAMD_PK_BIG_LIM="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-c", _BIG_PATH_SCRIPT % repo], capture_output=True, text=True,
+                       timeout=280, env=env, cwd=repo)
+    assert r.returncode == 0 and "BIG_OK" in r.stdout, r.stderr[-3000:]
