@@ -561,7 +561,9 @@ __global__ void __launch_bounds__(kBlock) pk_emit_packed(const uint8_t* __restri
         const uint2 ej = s_ol[j], ej1 = s_ol[j + 1];  // one ds_read2_b64
         const int rel = u - (int)ej.x, s = (int)ej1.x - u;
         // branch-free: all-ones masks from sign bits, byte ranges from clamped 64-bit shifts
-        uint32_t w = (ej.y >> (8 * (rel & 3))) & (uint32_t)((rel - 4) >> 31);
+        // (rel < 0 only on a block's or part's first dword: j starts inside it)
+        uint32_t w = rel < 0 ? (ej.y << (8 * (-rel & 3))) & (uint32_t)(-(rel > -4))
+                             : (ej.y >> (8 * (rel & 3))) & (uint32_t)((rel - 4) >> 31);
         w |= (ej1.y << (8 * (s & 3))) & (uint32_t)((s - 4) >> 31);
         int pix = pbase + u - 4 * (j + 1);
         pix = min(max(pix, 0), kPkTile + 56);
