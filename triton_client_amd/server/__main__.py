@@ -36,14 +36,17 @@ def main(argv=None):
     ap.add_argument("--native-grpc", default="auto", choices=["auto", "on", "off"],
                     help="serve the gRPC port with tcserve (C++ front end, csrc/cpp/server)")
     ap.add_argument("--hw-queues", type=int, default=8,
-                    help="HIP hardware queues for this process (GPU_MAX_HW_QUEUES, unless already set; 0 = HIP's "
-                         "default of 4).  Each model instance replays its graphs on its own stream; with 4 "
+                    help="HIP hardware queues for this process (sets GPU_MAX_HW_QUEUES, overriding an inherited "
+                         "value such as the pool's 4; 0 = leave the environment alone).  Each model instance replays its graphs on its own stream; with 4 "
                          "instances plus copy streams on 4 queues, ready batches waited for a queue: 1.6 ms of "
                          "every request's server time was outside queue and compute (profiles/r3_hw_queues.md)")
     args = ap.parse_args(argv)
     if args.hw_queues > 0:
-        # before anything initialises HIP in this process
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(min(args.hw_queues, 32)))
+        # before anything initialises HIP in this process.  The GPU boxes
+        # export GPU_MAX_HW_QUEUES=4 (HIP's own default) into every job, so a
+        # setdefault here never took effect under bench.py there: the r3
+        # 4 -> 8 A/B set it by hand
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
 
     from .app import default_models, serve
     from .core import InferenceServer
