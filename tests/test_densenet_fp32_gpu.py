@@ -175,6 +175,47 @@ def test_x3_dense_layer(imgs, H, K):
     assert torch.equal(x[:, :K], xc[:, :K]) and torch.equal(x[:, K + 32:], xc[:, K + 32:])
 
 
+@pytest.mark.parametrize("imgs,H,K", [(1, 14, 992), (1, 7, 992), (8, 14, 512), (8, 7, 1024), (1, 28, 480),
+                                      (2, 14, 256), (3, 9, 48), (1, 1, 128), (7, 5, 640)])
+def test_x3s_dense_layer(imgs, H, K):
+    """K13x small-M dense layer: the 1x1 adds into a zeroed fp32 accumulator
+    with float atomics over many workgroups, the 3x3 reads it (bias + ReLU +
+    split in registers) and zeroes the next layer's accumulator.  Against fp64
+    torch; run to run within float-atomic ordering noise (the 3x3 quarters add into y)."""
+    _need_gpu()
+    hip = _hip()
+    g = torch.Generator(device=DEV).manual_seed(imgs * 31 + H * 7 + K)
+    M, ldx = imgs * H * H, K + 64
+    x = torch.randn(M, ldx, device=DEV, generator=g)
+    s = torch.rand(K, device=DEV, generator=g) + 0.5
+    t = torch.randn(K, device=DEV, generator=g) * 0.2
+    w1 = torch.randn(128, K, device=DEV, generator=g) / K ** 0.5
+    b1 = torch.randn(128, device=DEV, generator=g) * 0.1
+    w2 = torch.randn(32, 128, 3, 3, device=DEV, generator=g) / (9 * 128) ** 0.5
+    f1h, f1l = (hip.x3_w1_fragments(u) for u in _split(w1))
+    f2h, f2l = (hip.x3_w3_fragments(u) for u in _split(w2.permute(0, 2, 3, 1).reshape(32, -1)))
+    xc = x.clone()
+    outs = []
+    for _ in range(2):
+        x.copy_(xc)
+        zacc = torch.zeros(M + 5, 128, device=DEV)
+        znext = torch.full((M + 5, 128), 3.0, device=DEV)
+        hip.x3s_dense_layer(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), f1h.data_ptr(),
+                            f1l.data_ptr(), b1.data_ptr(), zacc.data_ptr(), znext.data_ptr(), f2h.data_ptr(),
+                            f2l.data_ptr(), x.data_ptr() + 4 * K, ldx, stream=_st())
+        torch.cuda.synchronize()
+        assert (znext[:M] == 0).all() and (znext[M:] == 3.0).all()
+        outs.append(x[:, K:K + 32].clone())
+    a = torch.relu(xc[:, :K].double() * s.double() + t.double())
+    zraw = a @ w1.double().t()
+    assert _rel(zacc[:M], zraw) < 3e-5 and (zacc[M:] == 0).all()
+    z = torch.relu(zraw + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
+    ref = F.conv2d(z, w2.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 32)
+    assert _rel(x[:, K:K + 32], ref) < 3e-5
+    assert _rel(outs[0], outs[1]) < 1e-6
+    assert torch.equal(x[:, :K], xc[:, :K]) and torch.equal(x[:, K + 32:], xc[:, K + 32:])
+
+
 @pytest.mark.parametrize("imgs,H,K", [(1, 56, 64), (8, 56, 224), (32, 56, 128), (64, 28, 224), (5, 28, 96),
                                       (3, 28, 192), (2, 16, 160), (128, 28, 128), (40, 56, 192)])
 @pytest.mark.parametrize("version", [1, 2])
@@ -285,8 +326,8 @@ def test_fp32_engine_matches_fp32_module(fp32_engine, b):
 def test_fp32_engine_vs_fp64_and_graph_capture(fp32_engine):
     """Against an fp64 CPU reference the engine must stay fp32-class (rel-L2
     < 1e-4; measured 4.5e-5, torch's own fp32 forward 2.2e-6 on MI355X, the
-    bf16 engine 3e-2); and a captured HIP graph replays the same logits bit
-    for bit."""
+    bf16 engine 3e-2); and a captured HIP graph replays the same logits (to
+    float-atomic ordering noise: the small-M layers sum with atomics)."""
     eng, model = fp32_engine
     g = torch.Generator(device=DEV).manual_seed(7)
     x = torch.randn(2, 3, 224, 224, device=DEV, generator=g)
@@ -309,7 +350,7 @@ def test_fp32_engine_vs_fp64_and_graph_capture(fp32_engine):
         out.zero_()
         gr.replay()
     s.synchronize()
-    assert torch.equal(out[:2], got)
+    assert _rel(out[:2], got) < 1e-6
 
 
 def test_fp32_engine_workspace_covers_every_batch(fp32_engine):

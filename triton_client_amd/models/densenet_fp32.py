@@ -112,6 +112,9 @@ class FusedDenseNetFP32:
         # still beats the two-launch pair at bs1); 0 disables it (A/B runs)
         self.fuse_min_tiles = int(os.environ.get("TCAMD_X3_FUSE_MIN_TPB", "1"))
         self.fuse_v2_min_k = int(os.environ.get("TCAMD_X3_FUSE_V2_MIN_K", "160"))
+        # K13x (small-M dense layer, csrc/kernels/densenet_x3s.hip) for the
+        # unfused layers of a block with at most this many pixels; 0 disables it
+        self.small_m = int(os.environ.get("TCAMD_X3_SMALL_M", "1600"))
         self._alloc(max_batch)
 
     def _alloc(self, n):
@@ -138,6 +141,11 @@ class FusedDenseNetFP32:
                 need = max(need, max(hip.x3_conv1x1_ws_bytes(b * nhw * nhw, ctot, ctot // 2)
                                      for b in range(1, n + 1)))
         self.ws = torch.empty(max(need, 16), device=dev, dtype=torch.uint8)
+        # K13x ping-pong 1x1 accumulators: a layer adds into one (zero on
+        # entry) and its 3x3 zeroes the other for the next layer
+        rows = max([b * hw * hw for hw, _ in self.block_dims for b in range(1, n + 1)
+                    if b * hw * hw <= self.small_m] or [0])
+        self.zacc = torch.zeros(2, max(rows, 1), BN_SIZE * GROWTH, device=dev, dtype=torch.float32)
 
     def with_workspace(self, max_batch=None):
         """A second engine sharing these weights with its own activation buffers."""
@@ -168,11 +176,13 @@ class FusedDenseNetFP32:
                     self.feat[0].data_ptr(), b, c0, stream=st)
         ws, wsb = self.ws.data_ptr(), self.ws.numel()
         zh, zl = self.z_hi.data_ptr(), self.z_lo.data_ptr()
+        zacc = None  # K13x: index of the zeroed accumulator, None before the first small layer
         for bi, layers in enumerate(self.blocks):
             hw, ctot = self.block_dims[bi]
             fp = self.feat[bi].data_ptr()
             M = b * hw * hw
             fused = self._fuse(M, hw)
+            small = 0 < M <= self.small_m and M <= self.zacc.shape[1]
             for L in layers:
                 if fused and L["cin"] <= FUSE_MAX_K:
                     # K11x v2 (4 waves) on the 56x56 block at big batches from K >=
@@ -188,6 +198,18 @@ class FusedDenseNetFP32:
                                            L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(),
                                            L["w2fh"].data_ptr(), L["w2fl"].data_ptr(), fp + 4 * L["cin"], ctot,
                                            stream=st)
+                    continue
+                if small:
+                    # M only shrinks from here on, so the rows each 3x3 zeroes
+                    # cover every later layer's
+                    if zacc is None:
+                        zacc = 0
+                        self.zacc[0, :M].zero_()
+                    hip.x3s_dense_layer(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
+                                        L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(),
+                                        self.zacc[zacc].data_ptr(), self.zacc[zacc ^ 1].data_ptr(),
+                                        L["w2h"].data_ptr(), L["w2l"].data_ptr(), fp + 4 * L["cin"], ctot, stream=st)
+                    zacc ^= 1
                     continue
                 hip.x3_dense_layer(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
                                    L["w1h"].data_ptr(), L["w1l"].data_ptr(), L["b1"].data_ptr(), zh, zl,

@@ -184,6 +184,15 @@ _SIGS = {
         ],
         ctypes.c_int,
     ),
+    "tcamd_x3s_dense_layer": (
+        [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
+    "tcamd_x3s_steps_per_block": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "tcamd_x3_dense_fused": (
         [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -625,6 +634,24 @@ def x3_dense_layer(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, z_hi, z_lo, 
     _check(_load().tcamd_x3_dense_layer(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
                                         z_hi, z_lo, w2_hi, w2_lo, y, int(ldy), _vp(ws), int(ws_bytes), _vp(stream)),
            "x3_dense_layer")
+
+
+def x3s_dense_layer(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, zacc, zacc_next, w2_hi, w2_lo, y, ldy,
+                    stream=None):
+    """K13x small-M dense layer (csrc/kernels/densenet_x3s.hip): the 1x1 adds
+    into ``zacc`` ([M][128] fp32, ZERO on entry) with float atomics over many
+    workgroups, then the 3x3 reads it (bias ``b1`` + ReLU + split in registers)
+    into ``y`` rows of ``ldy``, zeroing rows [0, M) of ``zacc_next`` (may be
+    None) for the next layer.  ``w1_*`` in x3_w1_fragments, ``w2_*`` in
+    x3_w3_fragments."""
+    _check(_load().tcamd_x3s_dense_layer(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
+                                         zacc, _vp(zacc_next), w2_hi, w2_lo, y, int(ldy), _vp(stream)),
+           "x3s_dense_layer")
+
+
+def x3s_steps_per_block(M, K):
+    """k16 steps per workgroup the K13x 1x1 plans for an M x K layer."""
+    return int(_load().tcamd_x3s_steps_per_block(int(M), int(K)))
 
 
 def x3_w1_fragments(w):
