@@ -2242,23 +2242,19 @@ static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, 
   if (p.M >= (1 << 24) - 2 * kRingF) return hipErrorInvalidValue;  // fast_divmod range
   p.mag_hw = (uint32_t)((0x100000000ull + H * W - 1) / (uint64_t)(H * W));
   p.mag_w = (uint32_t)((0x100000000ull + W - 1) / (uint64_t)W);
-  // NST 2..7 (K 64..224): past that the fully unrolled chunk no longer fits
-  // the 8-wave kernel's 256-VGPR budget; those layers keep the K8x + K9x pair
-  static const void* const kFns[2][2][6] = {
-      {{(const void*)x3_dense_fused_kernel<2>, (const void*)x3_dense_fused_kernel<3>,
-        (const void*)x3_dense_fused_kernel<4>, (const void*)x3_dense_fused_kernel<5>,
-        (const void*)x3_dense_fused_kernel<6>, (const void*)x3_dense_fused_kernel<7>},
-       {(const void*)x3_dense_fused_kernel<2, true>, (const void*)x3_dense_fused_kernel<3, true>,
-        (const void*)x3_dense_fused_kernel<4, true>, (const void*)x3_dense_fused_kernel<5, true>,
-        (const void*)x3_dense_fused_kernel<6, true>, (const void*)x3_dense_fused_kernel<7, true>}},
-      {{(const void*)x3_dense_fused4_kernel<2>, (const void*)x3_dense_fused4_kernel<3>,
-        (const void*)x3_dense_fused4_kernel<4>, (const void*)x3_dense_fused4_kernel<5>,
-        (const void*)x3_dense_fused4_kernel<6>, (const void*)x3_dense_fused4_kernel<7>},
-       {(const void*)x3_dense_fused4_kernel<2, true>, (const void*)x3_dense_fused4_kernel<3, true>,
-        (const void*)x3_dense_fused4_kernel<4, true>, (const void*)x3_dense_fused4_kernel<5, true>,
-        (const void*)x3_dense_fused4_kernel<6, true>, (const void*)x3_dense_fused4_kernel<7, true>}}};
+  // NST 2..15 (K 64..480; the BN1 affine table in LDS holds K <= 480).  v1
+  // at NST 15 spills 12 B per lane; measured per K before the engine uses it
+#define X3F_ROW(KERN, ST)                                                                                        \
+  {(const void*)KERN<2, ST>,  (const void*)KERN<3, ST>,  (const void*)KERN<4, ST>,  (const void*)KERN<5, ST>,  \
+   (const void*)KERN<6, ST>,  (const void*)KERN<7, ST>,  (const void*)KERN<8, ST>,  (const void*)KERN<9, ST>,  \
+   (const void*)KERN<10, ST>, (const void*)KERN<11, ST>, (const void*)KERN<12, ST>, (const void*)KERN<13, ST>, \
+   (const void*)KERN<14, ST>, (const void*)KERN<15, ST>}
+  static const void* const kFns[2][2][14] = {
+      {X3F_ROW(x3_dense_fused_kernel, false), X3F_ROW(x3_dense_fused_kernel, true)},
+      {X3F_ROW(x3_dense_fused4_kernel, false), X3F_ROW(x3_dense_fused4_kernel, true)}};
+#undef X3F_ROW
   const int nst = K / 32;
-  if (nst < 2 || nst > 7 || (v != 1 && v != 2)) return hipErrorInvalidValue;
+  if (nst < 2 || nst > 15 || (v != 1 && v != 2)) return hipErrorInvalidValue;
   static const bool stamp = getenv("TCAMD_X3F_STAMP") && atoi(getenv("TCAMD_X3F_STAMP"));
   p.stamps = nullptr;
   if (stamp) {

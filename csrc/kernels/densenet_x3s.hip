@@ -267,6 +267,213 @@ __global__ void __launch_bounds__(64 * NKQ * TG) x3s_conv3x3_kernel(X3sConv3x3Pa
   }
 }
 
+
+// ============================================================================
+// K13x chain: one launch per small-M dense layer
+// ============================================================================
+// A layer's 1x1 is linear in its per-channel activated inputs, so the
+// contribution of each 32-channel chunk (one earlier layer's output) to each
+// later layer's bottleneck accumulator can be added as soon as that chunk
+// exists.  Over a run of small-M layers f..L-1 of one dense block:
+//   base launch: zacc_l = W1_l[:, 0:K_f] . act_l(x[:, 0:K_f]) for every l
+//                (plain stores), and the y slices of every layer zeroed;
+//   layer l:     part A (tiles x 4 input quarters): the 3x3 of layer l from
+//                zacc_l + the chunk of layer l-1 (computed here for the tile
+//                and its halo rows: 2 k16 steps), bias + ReLU + split into an
+//                LDS band, 9 taps, float atomics into y_l;
+//                part B (tiles x later layers, l > f): the chunk of layer l-1
+//                fanned out into zacc_l' for every l' > l (read-add-write: in
+//                one launch each element has exactly one writer).
+// So zacc_l = base + the chunks of layers f..l-2 (parts B of launches
+// f+1..l-1, in layer order: deterministic) + chunk l-1 (part A) when its 3x3
+// runs: one launch per layer instead of two, one more per run.
+struct X3cLayer {  // device table entry, one per layer of the run (72 B)
+  const uint16_t* w1_hi;  // x3_w1_fragments [K/16][q 4][lane 64][8]
+  const uint16_t* w1_lo;
+  const float* s1;  // [K] BN1 affine
+  const float* t1;
+  const float* b1;  // [128] BN2-folded bias
+  const uint16_t* w2_hi;  // x3_w3_fragments
+  const uint16_t* w2_lo;
+  float* zacc;  // [>= M][128] fp32
+  long long K;  // input channels of the layer
+};
+
+struct X3cParams {
+  const X3cLayer* layers;  // [L - f]: entry i = layer f + i
+  float* x;                // [M][ldx] the block's feature buffer (layer l's y = x + K_l)
+  int ldx, M, H, W;
+  int l, n;                // this layer (index into layers), layers in the run
+  int nA;                  // part-A blocks (tiles x 4)
+};
+
+constexpr int kBandPitch = 144;  // B per LDS band row: 64 B hi + 64 B lo + 16 B pad (b128 reads spread over banks)
+constexpr int kBandRows = 96;    // 32 + 2(W + 1) <= 96: W <= 31
+
+// acc += W1_l[32q.., 16 s.. +16] . act(x[row][16 s..]) over k16 steps [s0, s1)
+__device__ __forceinline__ f32x16 chunk_1x1(const X3cLayer& L, const float* xr, bool live, int q, int lane, int h,
+                                            int s0, int s1, f32x16 acc) {
+  for (int s = s0; s < s1; ++s) {
+    const size_t wo = ((size_t)(s * 4 + q) * 64 + lane) * 8;
+    const v4u ah = ld16(L.w1_hi + wo), al = ld16(L.w1_lo + wo);
+    const int k = 16 * s + 8 * h;
+    const f32x4 xa = ldf4(xr + 16 * s), xb = ldf4(xr + 16 * s + 4);
+    const f32x4 sa = ldf4(L.s1 + k), sb = ldf4(L.s1 + k + 4), ta = ldf4(L.t1 + k), tb = ldf4(L.t1 + k + 4);
+    f32x4 va, vb;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      va[e] = live ? fmaxf(xa[e] * sa[e] + ta[e], 0.f) : 0.f;
+      vb[e] = live ? fmaxf(xb[e] * sb[e] + tb[e], 0.f) : 0.f;
+    }
+    v4u bh, bl;
+    split8(va, vb, bh, bl);
+    acc = x3_32(ah, al, bh, bl, acc);
+  }
+  return acc;
+}
+
+// base: grid (tiles, n layers, 4 quarters); 4 waves split the k16 steps of
+// [0, K_f), sum through LDS, plain-store zacc_l[tile][quarter]; quarter 0
+// also zeroes the tile's rows of y_l
+__global__ void __launch_bounds__(256) x3c_base_kernel(X3cParams p) {
+  __shared__ __attribute__((aligned(16))) float red[4][kTile * kRedPitch];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 31, h = lane >> 5;
+  const int m0 = blockIdx.x * kTile, q = blockIdx.z;
+  const X3cLayer L = p.layers[blockIdx.y];
+  const int kf = (int)p.layers[0].K;
+  if (q == 0) {
+    const int px = threadIdx.x >> 3;
+    if (m0 + px < p.M)
+      *reinterpret_cast<f32x4*>(p.x + (size_t)(m0 + px) * p.ldx + L.K + 4 * (threadIdx.x & 7)) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int m = m0 + col;
+  const bool in = m < p.M;
+  const float* xr = p.x + (size_t)(in ? m : 0) * p.ldx + 8 * h;
+  const int nst = kf / 16, per = (nst + 3) / 4;
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  acc = chunk_1x1(L, xr, in, q, lane, h, wave * per, min(nst, wave * per + per), acc);
+  put_tile(red[wave], acc, col, h);
+  __syncthreads();
+  const int oc = threadIdx.x & 31;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int px = (threadIdx.x >> 5) + 8 * j;
+    const float v = red[0][px * kRedPitch + oc] + red[1][px * kRedPitch + oc] + red[2][px * kRedPitch + oc] +
+                    red[3][px * kRedPitch + oc];
+    if (m0 + px < p.M) L.zacc[(size_t)(m0 + px) * kZ + 32 * q + oc] = v;
+  }
+}
+
+__global__ void __launch_bounds__(256) x3c_layer_kernel(X3cParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t band[kBandRows * kBandPitch];
+  __shared__ __attribute__((aligned(16))) float red[4][kTile * kRedPitch];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 31, h = lane >> 5;
+  const X3cLayer L = p.layers[p.l];
+  const int c0 = (int)L.K - 32;  // the previous layer's chunk
+  if ((int)blockIdx.x >= p.nA) {
+    // ---- part B: chunk l-1 into zacc of layer l + 1 + j, quarter = wave ----
+    const int b = blockIdx.x - p.nA, ntl = p.n - p.l - 1;
+    const int m0 = (b / ntl) * kTile;
+    const X3cLayer T = p.layers[p.l + 1 + b % ntl];
+    const int m = m0 + col;
+    const bool in = m < p.M;
+    const float* xr = p.x + (size_t)(in ? m : 0) * p.ldx + c0 + 8 * h - 16 * (c0 / 16);
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    acc = chunk_1x1(T, xr, in, wave, lane, h, c0 / 16, c0 / 16 + 2, acc);
+    if (in) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4* zp = reinterpret_cast<f32x4*>(T.zacc + (size_t)m * kZ + 32 * wave + 8 * g + 4 * h);
+        *zp = *zp + f32x4{acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
+      }
+    }
+    return;
+  }
+  // ---- part A: the 3x3 of layer l over one tile and one input quarter ----
+  const int kq = blockIdx.x & 3, m0 = (blockIdx.x >> 2) * kTile;
+  const int W = p.W, band0 = m0 - W - 1, R = kTile + 2 * W + 2;
+  // this wave's taps tg, tg + 4, tg + 8: weight fragments in flight first
+  v4u wh[3][2], wl[3][2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int t = min(wave + 4 * i, 8);
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      const size_t wo = ((size_t)((t * 4 + kq) * 2 + kc) * 64 + lane) * 8;
+      wh[i][kc] = ld16(L.w2_hi + wo);
+      wl[i][kc] = ld16(L.w2_lo + wo);
+    }
+  }
+  // band rows [band0, band0 + R): z = zacc + chunk(l-1) + bias -> ReLU -> split
+  if (wave * kTile < R) {
+    const int row = band0 + wave * kTile + col;
+    const bool rin = row >= 0 && row < p.M;
+    const int rc = rin ? row : 0;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    if (p.l > 0) {
+      const float* xr = p.x + (size_t)rc * p.ldx + c0 + 8 * h - 16 * (c0 / 16);
+      acc = chunk_1x1(L, xr, rin, kq, lane, h, c0 / 16, c0 / 16 + 2, acc);
+    }
+    uint8_t* br = band + (wave * kTile + col) * kBandPitch;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = 8 * g + 4 * h;
+      const f32x4 zs = ldf4(L.zacc + (size_t)rc * kZ + 32 * kq + c);
+      const f32x4 bb = ldf4(L.b1 + 32 * kq + c);
+      const float v0 = fmaxf(acc[4 * g] + zs[0] + bb[0], 0.f), v1 = fmaxf(acc[4 * g + 1] + zs[1] + bb[1], 0.f);
+      const float v2 = fmaxf(acc[4 * g + 2] + zs[2] + bb[2], 0.f), v3 = fmaxf(acc[4 * g + 3] + zs[3] + bb[3], 0.f);
+      const uint32_t h0 = pk(v0, v1), h1 = pk(v2, v3);
+      const uint32_t l0 = pk(v0 - __uint_as_float(h0 << 16), v1 - __uint_as_float(h0 & 0xffff0000u));
+      const uint32_t l1 = pk(v2 - __uint_as_float(h1 << 16), v3 - __uint_as_float(h1 & 0xffff0000u));
+      typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<v2u*>(br + 2 * c) = v2u{h0, h1};
+      *reinterpret_cast<v2u*>(br + 64 + 2 * c) = v2u{l0, l1};
+    }
+  }
+  __syncthreads();
+  const int m = m0 + col;
+  const bool in = m < p.M;
+  const int HW = p.H * W;
+  const int r = in ? m % HW : 0;
+  const int yy = r / W, xx = r - yy * W;
+  f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int t = wave + 4 * i;
+    const int dy = t / 3 - 1, dx = t % 3 - 1;
+    const int y2 = yy + dy, x2 = xx + dx;
+    const bool ok = in && t < 9 && y2 >= 0 && y2 < p.H && x2 >= 0 && x2 < W;
+    const uint8_t* br = band + (ok ? col + (dy + 1) * W + dx + 1 : 0) * kBandPitch;
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      v4u bh = ld16(br + (2 * kc + h) * 16), bl = ld16(br + 64 + (2 * kc + h) * 16);
+      if (!ok) bh = bl = v4u{0u, 0u, 0u, 0u};
+      acc = x3_32(wh[i][kc], wl[i][kc], bh, bl, acc);
+    }
+  }
+  put_tile(red[wave], acc, col, h);
+  __syncthreads();
+  const int oc = threadIdx.x & 31;
+  float* y = p.x + L.K;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int px = (threadIdx.x >> 5) + 8 * j;
+    const float v = red[0][px * kRedPitch + oc] + red[1][px * kRedPitch + oc] + red[2][px * kRedPitch + oc] +
+                    red[3][px * kRedPitch + oc];
+    if (m0 + px < p.M) atomicAdd(y + (size_t)(m0 + px) * p.ldx + oc, v);
+  }
+}
+
 bool a16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
 }  // namespace
@@ -351,6 +558,47 @@ int tcamd_x3s_dense_layer(const float* x, int ldx, int imgs, int H, int W, int K
   c.zero_rows = M;
   if (split3) hipLaunchKernelGGL((x3s_conv3x3_kernel<1, 4>), dim3(tiles, 4), dim3(256), 0, s, c);
   else hipLaunchKernelGGL((x3s_conv3x3_kernel<4, 2>), dim3(tiles), dim3(512), 0, s, c);
+  return hipGetLastError();
+}
+
+// K13x chain over the small-M layers f..f+n-1 of one dense block (W <= 31):
+// `layers` is a device table of n X3cLayer entries (layer f first; every
+// zacc has >= M rows); x the block's feature buffer [M][ldx] (layer l's y =
+// x + K_l).  Call tcamd_x3c_base once, then tcamd_x3c_layer for l = 0..n-1 in
+// order on the same stream.
+static int x3c_check(const void* layers, const float* x, int ldx, int imgs, int H, int W, int l, int n, X3cParams& p) {
+  if (!layers || !x || !a16(layers) || !a16(x) || ldx % 4 || n < 1 || l < 0 || l >= n) return hipErrorInvalidValue;
+  if (H < 1 || W < 1 || W > (kBandRows - kTile - 2) / 2) return hipErrorInvalidValue;
+  const long long Ml = (long long)imgs * H * W;
+  if (Ml >= (1 << 24)) return hipErrorInvalidValue;
+  p.layers = (const X3cLayer*)layers;
+  p.x = (float*)x;
+  p.ldx = ldx;
+  p.M = (int)Ml;
+  p.H = H;
+  p.W = W;
+  p.l = l;
+  p.n = n;
+  p.nA = (p.M + kTile - 1) / kTile * 4;
+  return hipSuccess;
+}
+
+int tcamd_x3c_base(const void* layers, int n, float* x, int ldx, int imgs, int H, int W, void* stream) {
+  if (imgs <= 0) return hipSuccess;
+  X3cParams p;
+  int e = x3c_check(layers, x, ldx, imgs, H, W, 0, n, p);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(x3c_base_kernel, dim3((p.M + kTile - 1) / kTile, n, 4), dim3(256), 0, (hipStream_t)stream, p);
+  return hipGetLastError();
+}
+
+int tcamd_x3c_layer(const void* layers, int l, int n, float* x, int ldx, int imgs, int H, int W, void* stream) {
+  if (imgs <= 0) return hipSuccess;
+  X3cParams p;
+  int e = x3c_check(layers, x, ldx, imgs, H, W, l, n, p);
+  if (e != hipSuccess) return e;
+  const int nB = l > 0 ? (p.M + kTile - 1) / kTile * (n - l - 1) : 0;
+  hipLaunchKernelGGL(x3c_layer_kernel, dim3(p.nA + nB), dim3(256), 0, (hipStream_t)stream, p);
   return hipGetLastError();
 }
 

@@ -212,18 +212,66 @@ def test_x3s_dense_layer(imgs, H, K):
     z = torch.relu(zraw + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
     ref = F.conv2d(z, w2.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 32)
     assert _rel(x[:, K:K + 32], ref) < 3e-5
-    assert _rel(outs[0], outs[1]) < 1e-6
+    assert _rel(outs[0], outs[1]) < 2e-6
     assert torch.equal(x[:, :K], xc[:, :K]) and torch.equal(x[:, K + 32:], xc[:, K + 32:])
 
 
+@pytest.mark.parametrize("imgs,H,C0,n", [(1, 14, 256, 6), (8, 14, 256, 3), (1, 7, 512, 5), (32, 7, 512, 2),
+                                         (1, 28, 256, 4), (2, 28, 256, 1), (3, 9, 64, 4), (1, 31, 96, 3)])
+def test_x3c_chain(imgs, H, C0, n):
+    """K13x chain: a run of n dense layers as one base launch (every layer's
+    1x1 over the first C0 channels) plus one launch per layer (its 3x3, the
+    previous layer's 1x1 chunk for the tile + halo, and that chunk fanned out
+    to every later layer).  The whole block buffer against fp64 torch layer
+    by layer."""
+    _need_gpu()
+    hip = _hip()
+    g = torch.Generator(device=DEV).manual_seed(imgs * 131 + H * 17 + C0 + n)
+    M, ctot = imgs * H * H, C0 + 32 * n + 32  # 32 spare channels past the run
+    x = torch.randn(M, ctot, device=DEV, generator=g)
+    x[:, C0:] = 5.0  # the y slices must be zeroed by the base launch
+    x[:, C0 + 32 * n:] = 7.0
+    xc = x.clone()
+    zc = torch.full((n, M + 3, 128), 9.0, device=DEV)
+    keep, ent = [], []
+    for j in range(n):
+        K = C0 + 32 * j
+        s = torch.rand(K, device=DEV, generator=g) + 0.5
+        t = torch.randn(K, device=DEV, generator=g) * 0.2
+        w1 = torch.randn(128, K, device=DEV, generator=g) / K ** 0.5
+        b1 = torch.randn(128, device=DEV, generator=g) * 0.1
+        w2 = torch.randn(32, 128, 3, 3, device=DEV, generator=g) / (9 * 128) ** 0.5
+        f1h, f1l = (hip.x3_w1_fragments(u) for u in _split(w1))
+        f2h, f2l = (hip.x3_w3_fragments(u) for u in _split(w2.permute(0, 2, 3, 1).reshape(32, -1)))
+        keep.append((s, t, w1, b1, w2, f1h, f1l, f2h, f2l))
+        ent.append(hip.x3c_layer_entry(f1h.data_ptr(), f1l.data_ptr(), s.data_ptr(), t.data_ptr(), b1.data_ptr(),
+                                       f2h.data_ptr(), f2l.data_ptr(), zc[j].data_ptr(), K))
+    table = torch.tensor(ent, dtype=torch.int64, device=DEV)
+    hip.x3c_base(table.data_ptr(), n, x.data_ptr(), ctot, imgs, H, H, stream=_st())
+    for j in range(n):
+        hip.x3c_layer(table.data_ptr(), j, n, x.data_ptr(), ctot, imgs, H, H, stream=_st())
+    torch.cuda.synchronize()
+    ref = xc.double()
+    for j, (s, t, w1, b1, w2, *_) in enumerate(keep):
+        K = C0 + 32 * j
+        a = torch.relu(ref[:, :K] * s.double() + t.double())
+        z = torch.relu(a @ w1.double().t() + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
+        ref[:, K:K + 32] = F.conv2d(z, w2.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 32)
+    for j in range(n):
+        K = C0 + 32 * j
+        assert _rel(x[:, K:K + 32], ref[:, K:K + 32]) < 5e-5, "layer %d" % j
+    assert torch.equal(x[:, :C0], xc[:, :C0]) and (x[:, C0 + 32 * n:] == 7.0).all()
+
+
 @pytest.mark.parametrize("imgs,H,K", [(1, 56, 64), (8, 56, 224), (32, 56, 128), (64, 28, 224), (5, 28, 96),
-                                      (3, 28, 192), (2, 16, 160), (128, 28, 128), (40, 56, 192)])
+                                      (3, 28, 192), (2, 16, 160), (128, 28, 128), (40, 56, 192), (16, 28, 480),
+                                      (3, 28, 320), (24, 28, 256), (2, 20, 416)])
 @pytest.mark.parametrize("version", [1, 2])
 def test_x3_dense_fused(imgs, H, K, version):
     """K11x (v1: 8 waves, v2: 4 waves): the whole dense layer in one kernel (z produced into the 3x3's LDS
     ring, never written to HBM): one block's band prologue only, several tiles
     per block, ragged tails, every block width, and every K-step instantiation
-    (K = 64..224, 2..7 steps).  Against fp64
+    (K = 64..480, 2..15 steps).  Against fp64
     torch, and against the two-kernel path (same split products)."""
     _need_gpu()
     hip = _hip()
@@ -350,7 +398,7 @@ def test_fp32_engine_vs_fp64_and_graph_capture(fp32_engine):
         out.zero_()
         gr.replay()
     s.synchronize()
-    assert _rel(out[:2], got) < 1e-6
+    assert _rel(out[:2], got) < 2e-5  # measured run to run: 6e-6 (tools/engine_repeat.py)
 
 
 def test_fp32_engine_workspace_covers_every_batch(fp32_engine):

@@ -19,9 +19,11 @@ Network walk (same as :class:`densenet_fused.FusedDenseNet`, fp32 activations):
                         K9x conv3x3 z -> block buffer ch[c_in : c_in+32] (fp32)
                         (one x3_dense_layer call; small-M layers run the 1x1
                         split-K and the 3x3 reduces its partials in-kernel)
-                        or, for big batches (>= 4 tiles per block, K <= 224,
-                        16 <= W <= 56): K11x, the whole layer in ONE kernel
-                        with z produced into the 3x3's LDS ring (never in HBM)
+                        or (K <= 224, 16 <= W <= 56; K <= 480 at >= 4 tiles
+                        per block): K11x, the whole layer in ONE kernel with z
+                        produced into the 3x3's LDS ring (never in HBM)
+                        or, small M (<= 1600 pixels, W <= 31): the K13x chain,
+                        one launch per layer (csrc/kernels/densenet_x3s.hip)
    -> per transition:   K8x conv1x1 with BN+ReLU+2x2 avg-pool prologue
                         -> next block buffer ch[0 : C/2] (fp32)
    -> K10x head: relu(BN5(x)) global average -> [b,1024] fp32
@@ -42,7 +44,8 @@ from .densenet import BLOCKS, BN_SIZE, GROWTH, INIT_FEATURES  # noqa: F401
 from .densenet_fused import _bn_affine
 
 IMG_ELEMS = 3 * 224 * 224
-FUSE_MAX_K = 224  # K11x instantiations: K 64..224
+FUSE_MAX_K = 224  # K11x at every batch: K 64..224
+FUSE_MAX_K_BIG = 480  # ... and up to K 480 (the late block-2 layers) once every block walks >= 4 tiles
 
 
 def split_bf16(w):
@@ -112,9 +115,12 @@ class FusedDenseNetFP32:
         # still beats the two-launch pair at bs1); 0 disables it (A/B runs)
         self.fuse_min_tiles = int(os.environ.get("TCAMD_X3_FUSE_MIN_TPB", "1"))
         self.fuse_v2_min_k = int(os.environ.get("TCAMD_X3_FUSE_V2_MIN_K", "160"))
+        self.fuse_big_k_min_tiles = int(os.environ.get("TCAMD_X3_FUSE_BIGK_MIN_TPB", "4"))
         # K13x (small-M dense layer, csrc/kernels/densenet_x3s.hip) for the
         # unfused layers of a block with at most this many pixels; 0 disables it
         self.small_m = int(os.environ.get("TCAMD_X3_SMALL_M", "1600"))
+        # ... as the K13x chain (one launch per layer) where W <= 31; 0 = two launches per layer
+        self.use_chain = os.environ.get("TCAMD_X3_CHAIN", "1") != "0"
         self._alloc(max_batch)
 
     def _alloc(self, n):
@@ -146,6 +152,21 @@ class FusedDenseNetFP32:
         rows = max([b * hw * hw for hw, _ in self.block_dims for b in range(1, n + 1)
                     if b * hw * hw <= self.small_m] or [0])
         self.zacc = torch.zeros(2, max(rows, 1), BN_SIZE * GROWTH, device=dev, dtype=torch.float32)
+        # K13x chain (one launch per small-M layer, W <= 31): a zacc per layer of
+        # every block that can run small, and a device table of layer entries
+        self.chain = []
+        for bi, layers in enumerate(self.blocks):
+            hw = self.block_dims[bi][0]
+            rows = max([b * hw * hw for b in range(1, n + 1) if b * hw * hw <= self.small_m] or [0])
+            if not self.use_chain or rows == 0 or hw > 31:
+                self.chain.append(None)
+                continue
+            zc = torch.empty(len(layers), rows, BN_SIZE * GROWTH, device=dev, dtype=torch.float32)
+            ent = [hip.x3c_layer_entry(L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["s1"].data_ptr(),
+                                       L["t1"].data_ptr(), L["b1"].data_ptr(), L["w2h"].data_ptr(),
+                                       L["w2l"].data_ptr(), zc[j].data_ptr(), L["cin"]) for j, L in enumerate(layers)]
+            table = torch.tensor(ent, dtype=torch.int64).to(dev)
+            self.chain.append((zc, table, rows))
 
     def with_workspace(self, max_batch=None):
         """A second engine sharing these weights with its own activation buffers."""
@@ -182,22 +203,24 @@ class FusedDenseNetFP32:
             fp = self.feat[bi].data_ptr()
             M = b * hw * hw
             fused = self._fuse(M, hw)
+            fmax = self._fuse_max_k(M)
             small = 0 < M <= self.small_m and M <= self.zacc.shape[1]
+            ch = self.chain[bi] if small else None
+            if ch is not None and M <= ch[2]:
+                # the run of small layers: those K11x does not take
+                f = sum(1 for L in layers if fused and L["cin"] <= fmax)
+                for L in layers[:f]:
+                    self._fused_layer(fused, L, fp, ctot, b, hw, st)
+                tab, n = ch[1].data_ptr() + 8 * hip.X3C_LAYER_WORDS * f, len(layers) - f
+                if n:
+                    hip.x3c_base(tab, n, fp, ctot, b, hw, hw, stream=st)
+                for i in range(n):
+                    hip.x3c_layer(tab, i, n, fp, ctot, b, hw, hw, stream=st)
+                self._transition(bi, fp, ctot, b, hw, ws, wsb, st)
+                continue
             for L in layers:
-                if fused and L["cin"] <= FUSE_MAX_K:
-                    # K11x v2 (4 waves) on the 56x56 block at big batches from K >=
-                    # fuse_v2_min_k, v1 (8 waves) elsewhere, bs1 included (per-K A/B:
-                    # profiles/r3_fused_dense_layer.md)
-                    if fused == 2 and L["cin"] >= self.fuse_v2_min_k:
-                        hip.x3_dense_fused4(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
-                                            L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(),
-                                            L["w2h"].data_ptr(), L["w2l"].data_ptr(), fp + 4 * L["cin"], ctot,
-                                            stream=st)
-                    else:
-                        hip.x3_dense_fused(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
-                                           L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(),
-                                           L["w2fh"].data_ptr(), L["w2fl"].data_ptr(), fp + 4 * L["cin"], ctot,
-                                           stream=st)
+                if fused and L["cin"] <= fmax:
+                    self._fused_layer(fused, L, fp, ctot, b, hw, st)
                     continue
                 if small:
                     # M only shrinks from here on, so the rows each 3x3 zeroes
@@ -215,12 +238,7 @@ class FusedDenseNetFP32:
                                    L["w1h"].data_ptr(), L["w1l"].data_ptr(), L["b1"].data_ptr(), zh, zl,
                                    L["w2h"].data_ptr(), L["w2l"].data_ptr(), fp + 4 * L["cin"], ctot, ws=ws,
                                    ws_bytes=wsb, stream=st)
-            if bi < len(self.trans):
-                T = self.trans[bi]
-                nhw, nct = self.block_dims[bi + 1]
-                hip.x3_conv1x1(fp, ctot, b * nhw * nhw, ctot, T["s"].data_ptr(), T["t"].data_ptr(),
-                               T["wh"].data_ptr(), T["wl"].data_ptr(), y=self.feat[bi + 1].data_ptr(), ldy=nct,
-                               pool=1, H=hw, W=hw, ws=ws, ws_bytes=wsb, stream=st, N=ctot // 2)
+            self._transition(bi, fp, ctot, b, hw, ws, wsb, st)
         hw4, c4 = self.block_dims[-1]
         hip.x3_head_pool(self.feat[-1].data_ptr(), self.s5.data_ptr(), self.t5.data_ptr(), self.pooled.data_ptr(),
                          b, hw4 * hw4, c4, stream=st)
@@ -230,6 +248,35 @@ class FusedDenseNetFP32:
         return out[:b]
 
     __call__ = forward
+
+    def _fused_layer(self, fused, L, fp, ctot, b, hw, st):
+        """K11x: the whole dense layer in one kernel.  v2 (4 waves) on the 56x56
+        block at big batches from K >= fuse_v2_min_k, v1 (8 waves) elsewhere,
+        bs1 included (per-K A/B: profiles/r3_fused_dense_layer.md)."""
+        if fused == 2 and L["cin"] >= self.fuse_v2_min_k:
+            hip.x3_dense_fused4(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
+                                L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(), L["w2h"].data_ptr(),
+                                L["w2l"].data_ptr(), fp + 4 * L["cin"], ctot, stream=st)
+        else:
+            hip.x3_dense_fused(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
+                               L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(), L["w2fh"].data_ptr(),
+                               L["w2fl"].data_ptr(), fp + 4 * L["cin"], ctot, stream=st)
+
+    def _transition(self, bi, fp, ctot, b, hw, ws, wsb, st):
+        if bi < len(self.trans):
+            T = self.trans[bi]
+            nhw, nct = self.block_dims[bi + 1]
+            hip.x3_conv1x1(fp, ctot, b * nhw * nhw, ctot, T["s"].data_ptr(), T["t"].data_ptr(),
+                           T["wh"].data_ptr(), T["wl"].data_ptr(), y=self.feat[bi + 1].data_ptr(), ldy=nct,
+                           pool=1, H=hw, W=hw, ws=ws, ws_bytes=wsb, stream=st, N=ctot // 2)
+
+    def _fuse_max_k(self, M):
+        """Largest K that K11x takes: past 224 only at >= 4 tiles per block, where
+        v1 beats the pair by 8-15% per layer at 28x28 (K 256..480, bs128; at bs32
+        it loses at K >= 384: profiles/r3_fused_dense_layer.md)."""
+        tiles = (M + 63) // 64
+        per_block = -(-tiles // min(tiles, _cu_count(self.device)))
+        return FUSE_MAX_K_BIG if per_block >= self.fuse_big_k_min_tiles else FUSE_MAX_K
 
     def _fuse(self, M, W):
         """K11x (whole layer, z in LDS) for this block's layers: 0 = no (K8x + K9x

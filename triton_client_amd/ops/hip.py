@@ -193,6 +193,16 @@ _SIGS = {
         ctypes.c_int,
     ),
     "tcamd_x3s_steps_per_block": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "tcamd_x3c_base": (
+        [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+         ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "tcamd_x3c_layer": (
+        [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+         ctypes.c_int, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_x3_dense_fused": (
         [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -647,6 +657,31 @@ def x3s_dense_layer(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, zacc, zacc_
     _check(_load().tcamd_x3s_dense_layer(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
                                          zacc, _vp(zacc_next), w2_hi, w2_lo, y, int(ldy), _vp(stream)),
            "x3s_dense_layer")
+
+
+X3C_LAYER_WORDS = 9  # int64 words of one X3cLayer table entry
+
+
+def x3c_layer_entry(w1_hi, w1_lo, s1, t1, b1, w2_hi, w2_lo, zacc, K):
+    """One K13x chain table entry (9 int64: 8 device pointers + K); ``w1_*`` in
+    x3_w1_fragments, ``w2_*`` in x3_w3_fragments, ``zacc`` [>= M][128] fp32."""
+    return [int(w1_hi), int(w1_lo), int(s1), int(t1), int(b1), int(w2_hi), int(w2_lo), int(zacc), int(K)]
+
+
+def x3c_base(layers, n, x, ldx, imgs, H, W, stream=None):
+    """K13x chain, once per run of ``n`` small-M layers: every layer's 1x1 over
+    the run's first K_f input channels (plain stores into its zacc) and every
+    layer's y slice zeroed.  ``layers``: device table of chain entries."""
+    _check(_load().tcamd_x3c_base(_vp(layers), int(n), _vp(x), int(ldx), int(imgs), int(H), int(W), _vp(stream)),
+           "x3c_base")
+
+
+def x3c_layer(layers, l, n, x, ldx, imgs, H, W, stream=None):
+    """K13x chain, layer ``l`` of the run (one launch): its 3x3 (plus the
+    previous layer's chunk of its 1x1, computed for the tile and halo) and the
+    previous layer's chunk fanned out to every later layer's zacc."""
+    _check(_load().tcamd_x3c_layer(_vp(layers), int(l), int(n), _vp(x), int(ldx), int(imgs), int(H), int(W),
+                                   _vp(stream)), "x3c_layer")
 
 
 def x3s_steps_per_block(M, K):
