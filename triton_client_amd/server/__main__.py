@@ -27,7 +27,7 @@ def main(argv=None):
     ap.add_argument("--preferred-batch-sizes", default="",
                     help="override dynamic_batching.preferred_batch_size of the GPU models (comma-separated)")
     ap.add_argument("--max-batch-size", type=int, default=0,
-                    help="override densenet_onnx max_batch_size (power of two <= 256; HIP-graph buckets up to it)")
+                    help="override densenet_onnx max_batch_size (one of gpu_models.BUCKETS, <= 256; HIP-graph buckets up to it)")
     ap.add_argument("--no-graphs", action="store_true", help="disable HIP graph capture")
     ap.add_argument("--engine", default="fp32", choices=["fp32", "fused", "torch"],
                     help="densenet_onnx engine: fp32 = fp32-parity split-precision HIP/MFMA kernels (default), "

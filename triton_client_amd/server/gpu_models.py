@@ -34,7 +34,12 @@ from triton_client_amd.utils import roctx
 from .model_base import Model, TensorSpec
 from .types import DeviceView, OutputTensor, ServerError
 
-BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256)
+# HIP-graph batch buckets: powers of two up to 16, then every 8 rows to 128 and
+# every 16 to 256.  A batch runs the smallest bucket that holds it, and the
+# padding rows cost full compute: under the headline load (bs8 requests, 128-row
+# preferred batches) batches average 109-124 rows, which power-of-two buckets
+# padded to 128 (3-15% of the device time spent on padding)
+BUCKETS = (1, 2, 4, 8, 16) + tuple(range(24, 129, 8)) + tuple(range(144, 257, 16))
 
 
 class DensenetOnnx(Model):
@@ -63,8 +68,7 @@ class DensenetOnnx(Model):
         self.engine = engine
         self.device_id = int(kw.get("device", device_id))
         if max_batch_size:
-            # option max_batch_size: one HIP-graph bucket per power of two up to
-            # it.  The fused engine's device throughput keeps growing with the
+            # option max_batch_size: the HIP-graph buckets up to it (BUCKETS).  The fused engine's device throughput keeps growing with the
             # rows per forward: on MI355X (tools/engine_streams_bench.py) ~64k
             # img/s with 128-row forwards on 3-4 streams, ~70k with 256-row
             # forwards on 2 streams.
