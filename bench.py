@@ -74,7 +74,11 @@ def parse_args(argv=None):
     ap.add_argument("--engine", default="fp32", choices=["fp32", "fused", "torch"],
                     help="densenet_onnx engine for the headline (fp32 = fp32-parity split-precision kernels)")
     ap.add_argument("--no-bf16", action="store_true", help="skip the bf16-engine secondary measurement")
-    ap.add_argument("--instance-count", type=int, default=4)
+    # 2 instances (2 HIP streams): full 128-row batches on two overlapping
+    # streams beat 4 instances' ~110-row batches on four (one box: 42.1k infer/s
+    # p99 9.7 ms vs 40.5k p99 11.5 ms; the engine alone at bs128 makes 42.0k img/s
+    # on 2 streams, 40.9k on 4: profiles/r3_instances.md)
+    ap.add_argument("--instance-count", type=int, default=2)
     ap.add_argument("--max-queue-delay-us", type=int, default=2000)
     ap.add_argument("--max-batch-size", type=int, default=0)
     ap.add_argument("--preferred", default="128")
@@ -349,7 +353,10 @@ def main():
             breakdown["server_us_per_request"] - breakdown["queue_us_per_request"] - wc, 1)
 
         # ---- best throughput with p99 <= 10 ms (same server, lower concurrency) ---------
-        p99c = {"p99_target_us": 10000.0, "points": []}
+        p99c = {"p99_target_us": 10000.0, "points": [
+            {"concurrency": args.concurrency, "infer_per_sec": round(value, 1),
+             "p50_latency_us": round(percentile_us(all_lat, 50), 1),
+             "p99_latency_us": round(percentile_us(all_lat, 99), 1)}]}
         if not cpu:
             for c in (32, 24, 16):
                 pc = Point(srv, model, bs, c, "data_0_in", in_bytes, dev, cpu)
