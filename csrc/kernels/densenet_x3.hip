@@ -1879,24 +1879,45 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 // ============================================================================
 // K10x head: out[img][c] = mean_p relu(x[img][p][c]*s[c] + b[c])   (fp32)
 // ============================================================================
+// Head: relu(x * s + b) averaged over the HW pixels of each image.  Block =
+// (image, 256-channel group); the 4 waves take every 4th pixel (4 pixel loads
+// per lane in flight) and sum through LDS.  The first version (one block per
+// image, each thread a serial pixel loop) paid an L2 round trip per pixel:
+// 14 us at bs1, 1.4% of that forward.
 __global__ void __launch_bounds__(256) x3_head_pool_kernel(const float* __restrict__ x, const float* __restrict__ s,
                                                            const float* __restrict__ b, float* __restrict__ out, int HW,
                                                            int C) {
-  const int img = blockIdx.x;
-  for (int c4 = threadIdx.x; c4 < C / 4; c4 += blockDim.x) {
-    const f32x4 sc = ldf4(s + c4 * 4), bi = ldf4(b + c4 * 4);
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int q = 0; q < HW; ++q) {
-      const f32x4 f = ldf4(x + ((size_t)img * HW + q) * C + c4 * 4);
+  __shared__ f32x4 part[4][64];
+  const int img = blockIdx.x, lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c4 = blockIdx.y * 64 + lane;
+  const bool live = c4 < C / 4;
+  const int cc = live ? c4 : 0;
+  const f32x4 sc = ldf4(s + cc * 4), bi = ldf4(b + cc * 4);
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* xi = x + (size_t)img * HW * C + cc * 4;
+  int q = ph;
+  for (; q + 12 < HW; q += 16) {
+    f32x4 f[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[e] += fmaxf(f[e] * sc[e] + bi[e], 0.f);
-    }
-    const float inv = 1.0f / (float)HW;
-    *reinterpret_cast<f32x4*>(out + (size_t)img * C + c4 * 4) = acc * inv;
+    for (int u = 0; u < 4; ++u) f[u] = ldf4(xi + (size_t)(q + 4 * u) * C);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += fmaxf(f[u][e] * sc[e] + bi[e], 0.f);
+  }
+  for (; q < HW; q += 4) {
+    const f32x4 f = ldf4(xi + (size_t)q * C);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] += fmaxf(f[e] * sc[e] + bi[e], 0.f);
+  }
+  part[ph][lane] = acc;
+  __syncthreads();
+  if (ph == 0 && live) {
+    const f32x4 t = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    *reinterpret_cast<f32x4*>(out + (size_t)img * C + c4 * 4) = t * (1.0f / (float)HW);
   }
 }
 
-// weight hi/lo split on device (fp32 [n] -> two bf16 planes)
 __global__ void x3_split_kernel(const float* __restrict__ w, uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
                                 size_t n) {
   for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
@@ -2349,7 +2370,8 @@ int tcamd_x3_head_pool(const float* x, const float* s, const float* b, float* ou
                        void* stream) {
   if (imgs <= 0) return hipSuccess;
   if (C % 4 || !aligned16(x) || !aligned16(s) || !aligned16(b) || !aligned16(out)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(x3_head_pool_kernel, dim3(imgs), dim3(256), 0, (hipStream_t)stream, x, s, b, out, HW, C);
+  hipLaunchKernelGGL(x3_head_pool_kernel, dim3(imgs, (C / 4 + 63) / 64), dim3(256), 0, (hipStream_t)stream, x, s, b,
+                     out, HW, C);
   return hipGetLastError();
 }
 

@@ -333,17 +333,19 @@ def test_x3_stem(imgs):
     assert (y[:, 64:] == 7.0).all()
 
 
-def test_x3_head_pool():
+@pytest.mark.parametrize("imgs,HW,C", [(5, 49, 1024), (1, 49, 1024), (3, 7, 1000), (2, 1, 64), (4, 50, 512)])
+def test_x3_head_pool(imgs, HW, C):
     _need_gpu()
     hip = _hip()
-    x = torch.randn(5 * 49, 1024, device=DEV)
-    s = torch.rand(1024, device=DEV) + 0.5
-    b = torch.randn(1024, device=DEV)
-    out = torch.empty(5, 1024, device=DEV)
-    hip.x3_head_pool(x.data_ptr(), s.data_ptr(), b.data_ptr(), out.data_ptr(), 5, 49, 1024, stream=_st())
+    x = torch.randn(imgs * HW, C, device=DEV)
+    s = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV)
+    out = torch.full((imgs + 1, C), 7.0, device=DEV)
+    hip.x3_head_pool(x.data_ptr(), s.data_ptr(), b.data_ptr(), out.data_ptr(), imgs, HW, C, stream=_st())
     torch.cuda.synchronize()
-    ref = torch.relu(x.double() * s.double() + b.double()).reshape(5, 49, 1024).mean(1)
-    assert _rel(out, ref) < 1e-6
+    ref = torch.relu(x.double() * s.double() + b.double()).reshape(imgs, HW, C).mean(1)
+    assert _rel(out[:imgs], ref) < 1e-6
+    assert (out[imgs:] == 7.0).all()
 
 
 @pytest.fixture(scope="module")

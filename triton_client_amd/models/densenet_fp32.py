@@ -121,6 +121,7 @@ class FusedDenseNetFP32:
         self.small_m = int(os.environ.get("TCAMD_X3_SMALL_M", "1600"))
         # ... as the K13x chain (one launch per layer) where W <= 31; 0 = two launches per layer
         self.use_chain = os.environ.get("TCAMD_X3_CHAIN", "1") != "0"
+        self.chain_after_fused = os.environ.get("TCAMD_X3_CHAIN_AFTER_FUSED", "0") != "0"
         self._alloc(max_batch)
 
     def _alloc(self, n):
@@ -207,8 +208,10 @@ class FusedDenseNetFP32:
             small = 0 < M <= self.small_m and M <= self.zacc.shape[1]
             ch = self.chain[bi] if small else None
             if ch is not None and M <= ch[2]:
-                # the run of small layers: those K11x does not take
-                f = sum(1 for L in layers if fused and L["cin"] <= fmax)
+                # the whole block runs as one chain (at bs1-2 a 28x28 K11x layer
+                # takes 13-15 us, a chain layer ~5.5); TCAMD_X3_CHAIN_AFTER_FUSED=1
+                # starts the chain after the layers K11x would take
+                f = sum(1 for L in layers if fused and L["cin"] <= fmax) if self.chain_after_fused else 0
                 for L in layers[:f]:
                     self._fused_layer(fused, L, fp, ctot, b, hw, st)
                 tab, n = ch[1].data_ptr() + 8 * hip.X3C_LAYER_WORDS * f, len(layers) - f
