@@ -308,7 +308,7 @@ struct X3cParams {
 };
 
 constexpr int kBandPitch = 144;  // B per LDS band row: 64 B hi + 64 B lo + 16 B pad (b128 reads spread over banks)
-constexpr int kBandRows = 96;    // 32 + 2(W + 1) <= 96: W <= 31
+constexpr int kBandRows = 160;   // 32 + 2(W + 1) <= 160: W <= 63 (5 row tiles over 4 waves)
 
 // acc += W1_l[32q.., 16 s.. +16] . act(x[row][16 s..]) over k16 steps [s0, s1)
 __device__ __forceinline__ f32x16 chunk_1x1(const X3cLayer& L, const float* xr, bool live, int q, int lane, int h,
@@ -411,8 +411,8 @@ __global__ void __launch_bounds__(256) x3c_layer_kernel(X3cParams p) {
     }
   }
   // band rows [band0, band0 + R): z = zacc + chunk(l-1) + bias -> ReLU -> split
-  if (wave * kTile < R) {
-    const int row = band0 + wave * kTile + col;
+  for (int rt = wave; rt * kTile < R; rt += 4) {  // wave-uniform: the 56x56 band has 5 row tiles
+    const int row = band0 + rt * kTile + col;
     const bool rin = row >= 0 && row < p.M;
     const int rc = rin ? row : 0;
     f32x16 acc;
@@ -422,7 +422,7 @@ __global__ void __launch_bounds__(256) x3c_layer_kernel(X3cParams p) {
       const float* xr = p.x + (size_t)rc * p.ldx + c0 + 8 * h - 16 * (c0 / 16);
       acc = chunk_1x1(L, xr, rin, kq, lane, h, c0 / 16, c0 / 16 + 2, acc);
     }
-    uint8_t* br = band + (wave * kTile + col) * kBandPitch;
+    uint8_t* br = band + (rt * kTile + col) * kBandPitch;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int c = 8 * g + 4 * h;
@@ -561,7 +561,7 @@ int tcamd_x3s_dense_layer(const float* x, int ldx, int imgs, int H, int W, int K
   return hipGetLastError();
 }
 
-// K13x chain over the small-M layers f..f+n-1 of one dense block (W <= 31):
+// K13x chain over the small-M layers f..f+n-1 of one dense block (W <= 63):
 // `layers` is a device table of n X3cLayer entries (layer f first; every
 // zacc has >= M rows); x the block's feature buffer [M][ldx] (layer l's y =
 // x + K_l).  Call tcamd_x3c_base once, then tcamd_x3c_layer for l = 0..n-1 in

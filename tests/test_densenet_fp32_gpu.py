@@ -217,7 +217,8 @@ def test_x3s_dense_layer(imgs, H, K):
 
 
 @pytest.mark.parametrize("imgs,H,C0,n", [(1, 14, 256, 6), (8, 14, 256, 3), (1, 7, 512, 5), (32, 7, 512, 2),
-                                         (1, 28, 256, 4), (2, 28, 256, 1), (3, 9, 64, 4), (1, 31, 96, 3)])
+                                         (1, 28, 256, 4), (2, 28, 256, 1), (3, 9, 64, 4), (1, 31, 96, 3),
+                                         (1, 56, 64, 6), (1, 63, 64, 2), (2, 40, 128, 3)])
 def test_x3c_chain(imgs, H, C0, n):
     """K13x chain: a run of n dense layers as one base launch (every layer's
     1x1 over the first C0 channels) plus one launch per layer (its 3x3, the

@@ -22,7 +22,7 @@ Network walk (same as :class:`densenet_fused.FusedDenseNet`, fp32 activations):
                         or (K <= 224, 16 <= W <= 56; K <= 480 at >= 4 tiles
                         per block): K11x, the whole layer in ONE kernel with z
                         produced into the 3x3's LDS ring (never in HBM)
-                        or, small M (<= 1600 pixels, W <= 31): the K13x chain,
+                        or, small M (<= 3136 pixels, W <= 63): the K13x chain,
                         one launch per layer (csrc/kernels/densenet_x3s.hip)
    -> per transition:   K8x conv1x1 with BN+ReLU+2x2 avg-pool prologue
                         -> next block buffer ch[0 : C/2] (fp32)
@@ -119,8 +119,10 @@ class FusedDenseNetFP32:
         # K13x (small-M dense layer, csrc/kernels/densenet_x3s.hip) for the
         # unfused layers of a block with at most this many pixels; 0 disables it
         self.small_m = int(os.environ.get("TCAMD_X3_SMALL_M", "1600"))
-        # ... as the K13x chain (one launch per layer) where W <= 31; 0 = two launches per layer
+        # ... and, up to chain_m pixels (W <= 63), the K13x chain (one launch per
+        # layer); TCAMD_X3_CHAIN=0: two launches per layer up to small_m
         self.use_chain = os.environ.get("TCAMD_X3_CHAIN", "1") != "0"
+        self.chain_m = int(os.environ.get("TCAMD_X3_CHAIN_M", "3136"))
         self.chain_after_fused = os.environ.get("TCAMD_X3_CHAIN_AFTER_FUSED", "0") != "0"
         self._alloc(max_batch)
 
@@ -153,13 +155,13 @@ class FusedDenseNetFP32:
         rows = max([b * hw * hw for hw, _ in self.block_dims for b in range(1, n + 1)
                     if b * hw * hw <= self.small_m] or [0])
         self.zacc = torch.zeros(2, max(rows, 1), BN_SIZE * GROWTH, device=dev, dtype=torch.float32)
-        # K13x chain (one launch per small-M layer, W <= 31): a zacc per layer of
-        # every block that can run small, and a device table of layer entries
+        # K13x chain (one launch per small-M layer, W <= 63): a zacc per layer of
+        # every block that can run it, and a device table of layer entries
         self.chain = []
         for bi, layers in enumerate(self.blocks):
             hw = self.block_dims[bi][0]
-            rows = max([b * hw * hw for b in range(1, n + 1) if b * hw * hw <= self.small_m] or [0])
-            if not self.use_chain or rows == 0 or hw > 31:
+            rows = max([b * hw * hw for b in range(1, n + 1) if b * hw * hw <= self.chain_m] or [0])
+            if not self.use_chain or rows == 0 or hw > 63:
                 self.chain.append(None)
                 continue
             zc = torch.empty(len(layers), rows, BN_SIZE * GROWTH, device=dev, dtype=torch.float32)
@@ -206,8 +208,8 @@ class FusedDenseNetFP32:
             fused = self._fuse(M, hw)
             fmax = self._fuse_max_k(M)
             small = 0 < M <= self.small_m and M <= self.zacc.shape[1]
-            ch = self.chain[bi] if small else None
-            if ch is not None and M <= ch[2]:
+            ch = self.chain[bi]
+            if ch is not None and 0 < M <= ch[2]:
                 # the whole block runs as one chain (at bs1-2 a 28x28 K11x layer
                 # takes 13-15 us, a chain layer ~5.5); TCAMD_X3_CHAIN_AFTER_FUSED=1
                 # starts the chain after the layers K11x would take
