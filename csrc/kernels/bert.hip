@@ -119,9 +119,16 @@ constexpr int kAMaxS = 384;       // keys / queries per sequence (multiple of 64
 
 __device__ __forceinline__ bf16x8 as_bf8(v4u v) { return __builtin_bit_cast(bf16x8, v); }
 
+// qkv_bias (may be null): the QKV projection's bias [3 * heads * 64], applied
+// here so the projection runs as a plain GEMM (hipBLASLt's bias epilogue cost
+// ~20 us per layer at bs64 x 384): q + b_q feeds the scores; the key bias
+// adds (q + b_q) . b_k to every score of a query, a constant that softmax
+// removes, so it is dropped; the value bias passes through the normalised
+// weights unchanged and is added to the output.
 template <bool MASKED>
 __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __restrict__ qkv, const int* __restrict__ mask,
-                                                           uint16_t* __restrict__ out, int S, int heads, float scale) {
+                                                           uint16_t* __restrict__ out, int S, int heads, float scale,
+                                                           const uint16_t* __restrict__ qkv_bias) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_a[];
   const int ldv = S + 4;  // V^T row (elements)
   uint16_t* Ks = reinterpret_cast<uint16_t*>(lds_a);
@@ -160,6 +167,18 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
   v4u qf[4];
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) qf[kk] = *reinterpret_cast<const v4u*>(base + (size_t)q * ld + 16 * kk + 8 * h);
+  if (qkv_bias) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const v4u bq = *reinterpret_cast<const v4u*>(qkv_bias + head * kAD + 16 * kk + 8 * h);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a0 = __uint_as_float(qf[kk][j] << 16) + __uint_as_float(bq[j] << 16);
+        const float a1 = __uint_as_float(qf[kk][j] & 0xffff0000u) + __uint_as_float(bq[j] & 0xffff0000u);
+        qf[kk][j] = pack2(a0, a1);
+      }
+    }
+  }
   __syncthreads();
 
   const float sl2 = scale * kLog2e;
@@ -254,8 +273,16 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int d = 32 * rd + 8 * g + 4 * h;
-      *reinterpret_cast<v2u*>(orow + d) =
-          v2u{pack2(o[rd][4 * g] * inv, o[rd][4 * g + 1] * inv), pack2(o[rd][4 * g + 2] * inv, o[rd][4 * g + 3] * inv)};
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (qkv_bias) {
+        const v2u b2 = *reinterpret_cast<const v2u*>(qkv_bias + 2 * HD + head * kAD + d);
+        bv[0] = __uint_as_float(b2[0] << 16);
+        bv[1] = __uint_as_float(b2[0] & 0xffff0000u);
+        bv[2] = __uint_as_float(b2[1] << 16);
+        bv[3] = __uint_as_float(b2[1] & 0xffff0000u);
+      }
+      *reinterpret_cast<v2u*>(orow + d) = v2u{pack2(o[rd][4 * g] * inv + bv[0], o[rd][4 * g + 1] * inv + bv[1]),
+                                             pack2(o[rd][4 * g + 2] * inv + bv[2], o[rd][4 * g + 3] * inv + bv[3])};
     }
 }
 
@@ -291,10 +318,11 @@ int tcamd_add_layernorm(const void* x, const void* y, const void* gamma, const v
 // QKV projection's output: q | k | v, each [heads][64]) -> out [seqs * S][heads *
 // 64] bf16.  mask: int32 [seqs][S] key-padding mask (0 = padded) or null.
 // S % 64 == 0 and S <= 384; pointers 16-B aligned.
-int tcamd_attention(const void* qkv, const int* mask, void* out, int seqs, int S, int heads, float scale,
-                    void* stream) {
+int tcamd_attention_bias(const void* qkv, const void* qkv_bias, const int* mask, void* out, int seqs, int S, int heads,
+                         float scale, void* stream) {
   if (seqs <= 0) return hipSuccess;
-  if (S <= 0 || S % 64 || S > kAMaxS || heads <= 0 || ((uintptr_t)qkv | (uintptr_t)out) % 16 || (uintptr_t)mask % 16)
+  if (S <= 0 || S % 64 || S > kAMaxS || heads <= 0 || ((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)qkv_bias) % 16 ||
+      (uintptr_t)mask % 16)
     return hipErrorInvalidValue;
   const size_t lds = (size_t)S * kAD * 2 + (size_t)kAD * (S + 4) * 2 + (size_t)S * 4;
   static bool attr = false;
@@ -322,11 +350,17 @@ int tcamd_attention(const void* qkv, const int* mask, void* out, int seqs, int S
   const dim3 grid(seqs * heads, S / (32 * qw)), block(64 * qw);
   if (mask)
     hipLaunchKernelGGL(attention_kernel<true>, grid, block, lds, (hipStream_t)stream, (const uint16_t*)qkv, mask,
-                       (uint16_t*)out, S, heads, scale);
+                       (uint16_t*)out, S, heads, scale, (const uint16_t*)qkv_bias);
   else
     hipLaunchKernelGGL(attention_kernel<false>, grid, block, lds, (hipStream_t)stream, (const uint16_t*)qkv, mask,
-                       (uint16_t*)out, S, heads, scale);
+                       (uint16_t*)out, S, heads, scale, (const uint16_t*)qkv_bias);
   return hipGetLastError();
+}
+
+// K12 without a bias (the projection's output already holds it)
+int tcamd_attention(const void* qkv, const int* mask, void* out, int seqs, int S, int heads, float scale,
+                    void* stream) {
+  return tcamd_attention_bias(qkv, nullptr, mask, out, seqs, S, heads, scale, stream);
 }
 
 }  // extern "C"

@@ -50,6 +50,10 @@ def test_bert_fused_layers_match_torch_ops():
     from triton_client_amd.models import bert
 
     m = bert.build(device=DEV, layers=2)
+    with torch.no_grad():  # non-zero biases: the QKV bias is applied inside K12
+        for p in m.parameters():
+            if p.dim() == 1 and not torch.all(p == 1):
+                p.copy_(torch.randn_like(p.float()) * 0.05)
     ids = torch.randint(0, bert.VOCAB, (3, 128), device=DEV)
     mask = torch.ones(3, 128, device=DEV, dtype=torch.int64)
     mask[1, 100:] = 0
@@ -117,6 +121,30 @@ def test_attention_kernel_matches_fp32(seqs, S, masked):
     err = (out.float() - ref).norm() / ref.norm()
     assert err.item() < 1e-2, err.item()
     assert torch.isfinite(out.float()).all()
+
+
+@pytest.mark.parametrize("masked", [False, True])
+def test_attention_kernel_applies_qkv_bias(masked):
+    """K12 with the projection bias passed separately (q + b_q, b_k dropped:
+    softmax-invariant, b_v added to the output) vs the reference on qkv + b."""
+    _need_gpu()
+    from triton_client_amd.ops import hip
+
+    seqs, S = 2, 256
+    g = torch.Generator(device=DEV).manual_seed(11 + masked)
+    qkv = (torch.randn(seqs * S, 3 * 1024, device=DEV, generator=g) * 1.5).bfloat16()
+    bias = (torch.randn(3 * 1024, device=DEV, generator=g) * 0.5).bfloat16()
+    mask = None
+    if masked:
+        mask = torch.ones(seqs, S, device=DEV, dtype=torch.int32)
+        mask[1, S - 40:] = 0
+    out = torch.empty(seqs * S, 1024, device=DEV, dtype=torch.bfloat16)
+    hip.attention(qkv.data_ptr(), None if mask is None else mask.data_ptr(), out.data_ptr(), seqs, S, 16, 0.125,
+                  bias=bias.data_ptr())
+    torch.cuda.synchronize()
+    ref = _attn_ref((qkv.float() + bias.float()).bfloat16(), mask, seqs, S).reshape(seqs * S, 1024)
+    err = (out.float() - ref).norm() / ref.norm()
+    assert err.item() < 1e-2, err.item()
 
 
 def test_attention_rejects_unsupported_shapes():

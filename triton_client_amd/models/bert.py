@@ -9,8 +9,8 @@ on the box.
 Compute layout for MI355X: bf16 everywhere, fused QKV projection (one
 [3H, H] GEMM per layer instead of three), attention as ONE hand-written HIP
 kernel (K12, csrc/kernels/bert.hip) that reads Q/K/V straight from the QKV
-GEMM's output, applies the key-padding mask and writes the [tokens, hidden]
-layout the output projection reads (torch SDPA is the fallback for sequences
+GEMM's output (computed without its bias, which K12 applies), applies the
+key-padding mask and writes the [tokens, hidden] layout the output projection reads (torch SDPA is the fallback for sequences
 over 384 or off the GPU), plain GEMMs on hipBLASLt, the GELU
 in the FFN-up GEMM's epilogue (``torch._addmm_activation``) and every
 residual add + LayerNorm as ONE hand-written HIP kernel (K11,
@@ -59,18 +59,29 @@ def _linear_gelu(x, lin):
     return F.gelu(lin(x))
 
 
-def _attention(qkv, b, s, mask_i32, bias):
+def _k12_ok(x, s):
+    """K12 takes this activation: bf16 on the GPU, s % 64 == 0, s <= 384."""
+    if not (FUSED and x.is_cuda and x.dtype == torch.bfloat16 and s % 64 == 0 and x.is_contiguous()):
+        return False
+    from triton_client_amd.ops import hip
+
+    return s <= hip.ATTENTION_MAX_SEQ
+
+
+def _attention(qkv, b, s, mask_i32, bias, qkv_bias=None):
     """Multi-head attention over the QKV projection [b, s, 3H]: K12 on the GPU
-    (mask_i32: int32 [b, s] key-padding mask or None), SDPA elsewhere."""
-    if FUSED and qkv.is_cuda and qkv.dtype == torch.bfloat16 and s % 64 == 0 and qkv.is_contiguous():
+    (mask_i32: int32 [b, s] key-padding mask or None), SDPA elsewhere.
+    qkv_bias: the projection's bias when ``qkv`` was computed without it."""
+    if _k12_ok(qkv, s):
         from triton_client_amd.ops import hip
 
-        if s <= hip.ATTENTION_MAX_SEQ:
-            out = torch.empty(b, s, HIDDEN, device=qkv.device, dtype=qkv.dtype)
-            hip.attention(qkv.data_ptr(), None if mask_i32 is None else mask_i32.data_ptr(), out.data_ptr(), b, s,
-                          HEADS, 1.0 / math.sqrt(HIDDEN // HEADS),
-                          stream=torch.cuda.current_stream(qkv.device).cuda_stream)
-            return out
+        out = torch.empty(b, s, HIDDEN, device=qkv.device, dtype=qkv.dtype)
+        hip.attention(qkv.data_ptr(), None if mask_i32 is None else mask_i32.data_ptr(), out.data_ptr(), b, s,
+                      HEADS, 1.0 / math.sqrt(HIDDEN // HEADS), stream=torch.cuda.current_stream(qkv.device).cuda_stream,
+                      bias=None if qkv_bias is None else qkv_bias.data_ptr())
+        return out
+    if qkv_bias is not None:
+        qkv = qkv + qkv_bias
     q, k, v = qkv.view(b, s, 3, HEADS, HIDDEN // HEADS).permute(2, 0, 3, 1, 4)
     a = F.scaled_dot_product_attention(q, k, v, attn_mask=bias)
     return a.transpose(1, 2).reshape(b, s, HIDDEN)
@@ -88,7 +99,13 @@ class _Layer(nn.Module):
 
     def forward(self, x, bias, mask_i32=None):
         b, s, _ = x.shape
-        a = _attention(self.qkv(x), b, s, mask_i32, bias)
+        if _k12_ok(x, s):
+            # plain GEMM (no bias epilogue: 152 vs 171 us at bs64 x 384,
+            # profiles/r3_bert_gemm_layout.log); K12 applies the bias
+            qkv = torch.mm(x.view(-1, HIDDEN), self.qkv.weight.t()).view(b, s, 3 * HIDDEN)
+            a = _attention(qkv, b, s, mask_i32, bias, qkv_bias=self.qkv.bias)
+        else:
+            a = _attention(self.qkv(x), b, s, mask_i32, bias)
         x = _add_ln(x, self.out(a), self.ln1)
         return _add_ln(x, self.ffn2(_linear_gelu(x, self.ffn1)), self.ln2)
 

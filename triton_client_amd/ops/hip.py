@@ -239,6 +239,11 @@ _SIGS = {
          ctypes.c_int, ctypes.c_float, ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "tcamd_attention_bias": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+         ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_attention": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
          ctypes.c_void_p],
@@ -598,13 +603,16 @@ def add_layernorm(x, y, gamma, beta, out, rows, H, eps, stream=None):
 ATTENTION_MAX_SEQ = 384
 
 
-def attention(qkv, mask, out, seqs, S, heads, scale, stream=None):
+def attention(qkv, mask, out, seqs, S, heads, scale, stream=None, bias=None):
     """K12: multi-head attention (head dim 64, non-causal) over the fused QKV
     projection's output ``qkv`` [seqs*S][3*heads*64] bf16 into ``out``
     [seqs*S][heads*64] bf16; ``mask`` int32 [seqs][S] key-padding mask (0 =
-    padded key) or None.  S % 64 == 0 and S <= ATTENTION_MAX_SEQ."""
-    _check(_load().tcamd_attention(qkv, _vp(mask), out, int(seqs), int(S), int(heads), float(scale), _vp(stream)),
-           "attention")
+    padded key) or None.  S % 64 == 0 and S <= ATTENTION_MAX_SEQ.  ``bias``
+    (bf16 [3*heads*64] or None): the projection's bias, when ``qkv`` was
+    computed without it (q + b_q feeds the scores, b_v is added to the output;
+    b_k shifts every score of a query equally and cancels in the softmax)."""
+    _check(_load().tcamd_attention_bias(qkv, _vp(bias), _vp(mask), out, int(seqs), int(S), int(heads), float(scale),
+                                        _vp(stream)), "attention")
 
 
 def x3_conv1x1_ws_bytes(M, K, N=128):
