@@ -114,7 +114,11 @@ class FusedDenseNetFP32:
         # tiles (its per-block prologue recomputes a (2W+2)-row halo of z, yet it
         # still beats the two-launch pair at bs1); 0 disables it (A/B runs)
         self.fuse_min_tiles = int(os.environ.get("TCAMD_X3_FUSE_MIN_TPB", "1"))
-        self.fuse_v2_min_k = int(os.environ.get("TCAMD_X3_FUSE_V2_MIN_K", "160"))
+        # K11x v2 (4 waves) from this K on the 56x56 block at big batches.  In
+        # isolation v2 wins at K >= 160 (profiles/r3_fused_dense_layer.md), but in
+        # the whole forward v1 everywhere measured 1% faster on one stream and
+        # 0.7% on two (r3_fused/v1_everywhere.log): off by default
+        self.fuse_v2_min_k = int(os.environ.get("TCAMD_X3_FUSE_V2_MIN_K", "999"))
         self.fuse_big_k_min_tiles = int(os.environ.get("TCAMD_X3_FUSE_BIGK_MIN_TPB", "4"))
         # K13x (small-M dense layer, csrc/kernels/densenet_x3s.hip) for the
         # unfused layers of a block with at most this many pixels; 0 disables it
