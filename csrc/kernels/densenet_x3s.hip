@@ -1,14 +1,23 @@
-// K13x — the small-M fp32-parity dense layer (bs1 / bs8 at 28x28 and below).
+// K13x — the small-M fp32-parity dense layers (bs1-4 at every block width,
+// bs8-16 at 14x14 / 7x7; the engine's default limit is 3,136 pixels).
 //
 // At small M the K8x/K9x pair is latency-bound, not byte- or MFMA-bound: a
 // bs1 14x14 layer is 196 pixels, and its 3x3 (K9x with the split-K partials
 // summed while staging) ran on 4 CUs, each pulling the whole 147 KB of 3x3
 // weights plus 4 x 94 rows of fp32 partials before its first MFMA — 11 us per
 // layer for ~1 us of matrix work (profiles/r3_x3_forward_b1.md: the 48
-// small-M 3x3s were 52% of a 1.02 ms bs1 forward).  Here both convs spread
-// their operand bytes over many workgroups and keep every wave's load list
-// short and fully in flight:
+// small-M 3x3s were 52% of a 1.02 ms bs1 forward).  Two designs live here,
+// both spreading their operand bytes over many workgroups with short, fully
+// in-flight load lists (profiles/r3_x3s_small_m.md):
 //
+// The chain (default, x3c_* below): one launch per layer.  A layer's 1x1 is
+// linear in its per-channel activated inputs, so each layer's 32 new
+// channels are folded into every later layer's fp32 accumulator as soon as
+// they exist; a layer's launch adds the previous layer's chunk for its tile
+// and halo, runs its 3x3 (tiles x 4 input quarters) and fans that chunk out
+// to the later layers.  bs1 forward 0.978 -> 0.457 ms.
+//
+// Two launches per layer (x3s_*; TCAMD_X3_CHAIN=0, and the fallback):
 //   S1 (1x1, K -> 128): grid = 32-pixel tiles x 4 output quarters x K chunks;
 //      the 4 waves of a block take interleaved k16 steps of the block's chunk
 //      straight from global memory (A = BN2-folded W1 hi/lo in the K11x
@@ -16,19 +25,19 @@
 //      and the hi/lo split applied in registers), sum through LDS, and add
 //      the 32 x 32 fp32 tile into zacc with global float atomics (two whole
 //      128-B row segments per wave instruction).  zacc is zero on entry.
-//   S2 (3x3, 128 -> 32): grid = 32-pixel tiles; 8 waves = 4 input-channel
-//      quarters x 2 tap groups, each loading its taps' weight fragments (K9x
+//   S2 (3x3, 128 -> 32): grid = 32-pixel tiles x 4 input quarters (or all
+//      quarters per block), each wave loading its taps' weight fragments (K9x
 //      layout) and its pixels' zacc rows directly (bias + ReLU + split in
 //      registers, zero for taps outside the image), summed through LDS and
-//      stored as the layer's 32 new fp32 channels.  The same blocks zero the
-//      NEXT layer's zacc (a ping-pong pair): no memset launch per layer.
+//      added into (or stored as) the layer's 32 new fp32 channels.  The same
+//      blocks zero the NEXT layer's zacc (a ping-pong pair): no memset launch.
 //
-// Precision: the same bf16x3 products as K8x/K9x; the float atomics sum in
-// arrival order (last-bit run-to-run differences; see
-// tcamd_x3s_steps_per_block for the reproducible setting).
-// Float atomics run at memory side at ~1.3 TB/s chip-wide
-// (MI355X_MICROARCH.md, Global float atomics): the host sizes the K chunking
-// so a layer adds at most a few hundred KB.
+// Precision: the same bf16x3 products as K8x/K9x.  The float atomics sum in
+// arrival order (last-bit run-to-run differences, ~6e-6 rel-L2 on the
+// logits; see tcamd_x3s_steps_per_block for the reproducible setting of the
+// two-launch path).  Float atomics run at memory side at ~1.3 TB/s chip-wide
+// (MI355X_MICROARCH.md, Global float atomics); every launch here adds at
+// most a few hundred KB.
 
 #include <algorithm>
 #include <cstdlib>
