@@ -341,6 +341,41 @@ __device__ __forceinline__ f32x16 chunk_1x1(const X3cLayer& L, const float* xr, 
   return acc;
 }
 
+// the chain's per-chunk 1x1: exactly the 2 k16 steps of one 32-channel chunk,
+// every load issued before the first use (one memory round trip, not two)
+__device__ __forceinline__ f32x16 chunk2_1x1(const X3cLayer& L, const float* xr, bool live, int q, int lane, int h,
+                                             int s0, f32x16 acc) {
+  v4u ah[2], al[2];
+  f32x4 xa[2], xb[2], sa[2], sb[2], ta[2], tb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int s = s0 + i;
+    const size_t wo = ((size_t)(s * 4 + q) * 64 + lane) * 8;
+    ah[i] = ld16(L.w1_hi + wo);
+    al[i] = ld16(L.w1_lo + wo);
+    const int k = 16 * s + 8 * h;
+    xa[i] = ldf4(xr + 16 * s);
+    xb[i] = ldf4(xr + 16 * s + 4);
+    sa[i] = ldf4(L.s1 + k);
+    sb[i] = ldf4(L.s1 + k + 4);
+    ta[i] = ldf4(L.t1 + k);
+    tb[i] = ldf4(L.t1 + k + 4);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    f32x4 va, vb;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      va[e] = live ? fmaxf(xa[i][e] * sa[i][e] + ta[i][e], 0.f) : 0.f;
+      vb[e] = live ? fmaxf(xb[i][e] * sb[i][e] + tb[i][e], 0.f) : 0.f;
+    }
+    v4u bh, bl;
+    split8(va, vb, bh, bl);
+    acc = x3_32(ah[i], al[i], bh, bl, acc);
+  }
+  return acc;
+}
+
 // base: grid (tiles, n layers, 4 quarters); 4 waves split the k16 steps of
 // [0, K_f), sum through LDS, plain-store zacc_l[tile][quarter]; quarter 0
 // also zeroes the tile's rows of y_l
@@ -376,42 +411,50 @@ __global__ void __launch_bounds__(256) x3c_base_kernel(X3cParams p) {
   }
 }
 
-__global__ void __launch_bounds__(256) x3c_layer_kernel(X3cParams p) {
+// NW waves per block (4 or 8).  Part A: wave w takes taps w, w + NW, ... and
+// band row tiles w, w + NW, ...; part B: each group of 4 waves (one per
+// output quarter) takes one later layer, NW / 4 layers per block
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) x3c_layer_kernel(X3cParams p) {
+  constexpr int NL = NW / 4, NT = (9 + NW - 1) / NW;
   __shared__ __attribute__((aligned(16))) uint8_t band[kBandRows * kBandPitch];
-  __shared__ __attribute__((aligned(16))) float red[4][kTile * kRedPitch];
+  __shared__ __attribute__((aligned(16))) float red[NW][kTile * kRedPitch];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 31, h = lane >> 5;
   const X3cLayer L = p.layers[p.l];
   const int c0 = (int)L.K - 32;  // the previous layer's chunk
   if ((int)blockIdx.x >= p.nA) {
     // ---- part B: chunk l-1 into zacc of layer l + 1 + j, quarter = wave ----
-    const int b = blockIdx.x - p.nA, ntl = p.n - p.l - 1;
-    const int m0 = (b / ntl) * kTile;
-    const X3cLayer T = p.layers[p.l + 1 + b % ntl];
+    const int b = blockIdx.x - p.nA, ntl = p.n - p.l - 1, nbp = (ntl + NL - 1) / NL;
+    const int m0 = (b / nbp) * kTile, j = (b % nbp) * NL + (wave >> 2), q = wave & 3;
+    if (j >= ntl) return;  // wave-uniform
+    const X3cLayer T = p.layers[p.l + 1 + j];
     const int m = m0 + col;
     const bool in = m < p.M;
-    const float* xr = p.x + (size_t)(in ? m : 0) * p.ldx + c0 + 8 * h - 16 * (c0 / 16);
+    const float* xr = p.x + (size_t)(in ? m : 0) * p.ldx + 8 * h;
+    // the accumulator rows go out with the chunk's loads (one round trip)
+    f32x4* zp = reinterpret_cast<f32x4*>(T.zacc + (size_t)(in ? m : 0) * kZ + 32 * q + 4 * h);
+    f32x4 zv[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) zv[g] = zp[2 * g];
     f32x16 acc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-    acc = chunk_1x1(T, xr, in, wave, lane, h, c0 / 16, c0 / 16 + 2, acc);
+    acc = chunk2_1x1(T, xr, in, q, lane, h, c0 / 16, acc);
     if (in) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        f32x4* zp = reinterpret_cast<f32x4*>(T.zacc + (size_t)m * kZ + 32 * wave + 8 * g + 4 * h);
-        *zp = *zp + f32x4{acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
-      }
+      for (int g = 0; g < 4; ++g) zp[2 * g] = zv[g] + f32x4{acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
     }
     return;
   }
   // ---- part A: the 3x3 of layer l over one tile and one input quarter ----
   const int kq = blockIdx.x & 3, m0 = (blockIdx.x >> 2) * kTile;
   const int W = p.W, band0 = m0 - W - 1, R = kTile + 2 * W + 2;
-  // this wave's taps tg, tg + 4, tg + 8: weight fragments in flight first
-  v4u wh[3][2], wl[3][2];
+  // this wave's taps: weight fragments in flight first
+  v4u wh[NT][2], wl[NT][2];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int t = min(wave + 4 * i, 8);
+  for (int i = 0; i < NT; ++i) {
+    const int t = min(wave + NW * i, 8);
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
       const size_t wo = ((size_t)((t * 4 + kq) * 2 + kc) * 64 + lane) * 8;
@@ -420,23 +463,30 @@ __global__ void __launch_bounds__(256) x3c_layer_kernel(X3cParams p) {
     }
   }
   // band rows [band0, band0 + R): z = zacc + chunk(l-1) + bias -> ReLU -> split
-  for (int rt = wave; rt * kTile < R; rt += 4) {  // wave-uniform: the 56x56 band has 5 row tiles
+  for (int rt = wave; rt * kTile < R; rt += NW) {  // wave-uniform: the 56x56 band has 5 row tiles
     const int row = band0 + rt * kTile + col;
     const bool rin = row >= 0 && row < p.M;
     const int rc = rin ? row : 0;
+    // the accumulator rows and bias go out with the chunk's loads
+    f32x4 zsv[4], bbv[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      zsv[g] = ldf4(L.zacc + (size_t)rc * kZ + 32 * kq + 8 * g + 4 * h);
+      bbv[g] = ldf4(L.b1 + 32 * kq + 8 * g + 4 * h);
+    }
     f32x16 acc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
     if (p.l > 0) {
-      const float* xr = p.x + (size_t)rc * p.ldx + c0 + 8 * h - 16 * (c0 / 16);
-      acc = chunk_1x1(L, xr, rin, kq, lane, h, c0 / 16, c0 / 16 + 2, acc);
+      const float* xr = p.x + (size_t)rc * p.ldx + 8 * h;
+      acc = chunk2_1x1(L, xr, rin, kq, lane, h, c0 / 16, acc);
     }
     uint8_t* br = band + (rt * kTile + col) * kBandPitch;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int c = 8 * g + 4 * h;
-      const f32x4 zs = ldf4(L.zacc + (size_t)rc * kZ + 32 * kq + c);
-      const f32x4 bb = ldf4(L.b1 + 32 * kq + c);
+      const f32x4 zs = zsv[g];
+      const f32x4 bb = bbv[g];
       const float v0 = fmaxf(acc[4 * g] + zs[0] + bb[0], 0.f), v1 = fmaxf(acc[4 * g + 1] + zs[1] + bb[1], 0.f);
       const float v2 = fmaxf(acc[4 * g + 2] + zs[2] + bb[2], 0.f), v3 = fmaxf(acc[4 * g + 3] + zs[3] + bb[3], 0.f);
       const uint32_t h0 = pk(v0, v1), h1 = pk(v2, v3);
@@ -457,8 +507,8 @@ __global__ void __launch_bounds__(256) x3c_layer_kernel(X3cParams p) {
 #pragma unroll
   for (int e = 0; e < 16; ++e) acc[e] = 0.f;
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int t = wave + 4 * i;
+  for (int i = 0; i < NT; ++i) {
+    const int t = wave + NW * i;
     const int dy = t / 3 - 1, dx = t % 3 - 1;
     const int y2 = yy + dy, x2 = xx + dx;
     const bool ok = in && t < 9 && y2 >= 0 && y2 < p.H && x2 >= 0 && x2 < W;
@@ -475,10 +525,11 @@ __global__ void __launch_bounds__(256) x3c_layer_kernel(X3cParams p) {
   const int oc = threadIdx.x & 31;
   float* y = p.x + L.K;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int px = (threadIdx.x >> 5) + 8 * j;
-    const float v = red[0][px * kRedPitch + oc] + red[1][px * kRedPitch + oc] + red[2][px * kRedPitch + oc] +
-                    red[3][px * kRedPitch + oc];
+  for (int j = 0; j < 16 / NW; ++j) {
+    const int px = (threadIdx.x >> 5) + 2 * NW * j;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][px * kRedPitch + oc];
     if (m0 + px < p.M) atomicAdd(y + (size_t)(m0 + px) * p.ldx + oc, v);
   }
 }
@@ -606,8 +657,13 @@ int tcamd_x3c_layer(const void* layers, int l, int n, float* x, int ldx, int img
   X3cParams p;
   int e = x3c_check(layers, x, ldx, imgs, H, W, l, n, p);
   if (e != hipSuccess) return e;
-  const int nB = l > 0 ? (p.M + kTile - 1) / kTile * (n - l - 1) : 0;
-  hipLaunchKernelGGL(x3c_layer_kernel, dim3(p.nA + nB), dim3(256), 0, (hipStream_t)stream, p);
+  // 4 waves per block; TCAMD_X3C_WAVES=8 (taps and band tiles over 8 waves,
+  // two later layers per part-B block) measured slower: bs1 0.430 -> 0.455 ms
+  static const int nw = getenv("TCAMD_X3C_WAVES") && atoi(getenv("TCAMD_X3C_WAVES")) == 8 ? 8 : 4;
+  const int per = nw / 4;  // later layers per part-B block
+  const int nB = l > 0 ? (p.M + kTile - 1) / kTile * ((n - l - 1 + per - 1) / per) : 0;
+  if (nw == 4) hipLaunchKernelGGL(x3c_layer_kernel<4>, dim3(p.nA + nB), dim3(256), 0, (hipStream_t)stream, p);
+  else hipLaunchKernelGGL(x3c_layer_kernel<8>, dim3(p.nA + nB), dim3(512), 0, (hipStream_t)stream, p);
   return hipGetLastError();
 }
 
