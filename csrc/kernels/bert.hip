@@ -30,6 +30,40 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// LayerNorm of one row held as v[E] per lane (lane l owns the 16-B chunks
+// l, l + 64, ...) -> bf16 out row: exact two-pass mean / variance over the
+// register copy, wave butterflies through DPP-backed shuffles
+template <int E>
+__device__ __forceinline__ void ln_store_row(const float (&v)[E], const uint16_t* __restrict__ gamma,
+                                             const uint16_t* __restrict__ beta, uint16_t* orow, int lane, float eps) {
+  constexpr int H = 64 * E, C = E / 8;
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) s += v[e];
+  const float mean = wave_sum(s) * (1.0f / H);
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const float d = v[e] - mean;
+    ss += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(ss) * (1.0f / H) + eps);
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int off = (c * 64 + lane) * 8;
+    const v4u g = *reinterpret_cast<const v4u*>(gamma + off);
+    const v4u bt = *reinterpret_cast<const v4u*>(beta + off);
+    v4u o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float g0 = __uint_as_float(g[q] << 16), g1 = __uint_as_float(g[q] & 0xffff0000u);
+      const float b0 = __uint_as_float(bt[q] << 16), b1 = __uint_as_float(bt[q] & 0xffff0000u);
+      o[q] = pack2((v[c * 8 + 2 * q] - mean) * rstd * g0 + b0, (v[c * 8 + 2 * q + 1] - mean) * rstd * g1 + b1);
+    }
+    *reinterpret_cast<v4u*>(orow + off) = o;
+  }
+}
+
 // E = elements per lane (H = 64 * E), a multiple of 8.  Lane l owns the 16-B
 // chunks l, l + 64, ... of the row (coalesced: a wave instruction covers 1 KB).
 template <int E>
@@ -54,31 +88,46 @@ __global__ void __launch_bounds__(256) add_layernorm_kernel(const uint16_t* x, c
       v[c * 8 + 2 * q + 1] = __uint_as_float(a[q] & 0xffff0000u) + __uint_as_float(b[q] & 0xffff0000u);
     }
   }
-  float s = 0.f;
-#pragma unroll
-  for (int e = 0; e < E; ++e) s += v[e];
-  const float mean = wave_sum(s) * (1.0f / H);
-  float ss = 0.f;
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const float d = v[e] - mean;
-    ss += d * d;
-  }
-  const float rstd = rsqrtf(wave_sum(ss) * (1.0f / H) + eps);
+  ln_store_row<E>(v, gamma, beta, out + base, lane, eps);
+}
+
+// Embedding sum + LayerNorm: out[r] = LN(word[ids[r]] + pos[r % S] +
+// type[types[r]]) in one pass (torch: three gathers, two adds and a LayerNorm,
+// six launches and ~5 passes over [tokens, H]).  Ids outside the tables are
+// clamped (torch would raise).
+template <int E>
+__global__ void __launch_bounds__(256) embed_layernorm_kernel(const int64_t* __restrict__ ids,
+                                                              const int64_t* __restrict__ types,
+                                                              const uint16_t* __restrict__ word,
+                                                              const uint16_t* __restrict__ pos,
+                                                              const uint16_t* __restrict__ tok,
+                                                              const uint16_t* __restrict__ gamma,
+                                                              const uint16_t* __restrict__ beta, uint16_t* __restrict__ out,
+                                                              int rows, int S, int vocab, int ntypes, float eps) {
+  constexpr int H = 64 * E, C = E / 8;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const long long id = min(max(ids[row], (int64_t)0), (int64_t)vocab - 1);
+  const long long ty = min(max(types[row], (int64_t)0), (int64_t)ntypes - 1);
+  const uint16_t* rw = word + (size_t)id * H;
+  const uint16_t* rp = pos + (size_t)(row % S) * H;
+  const uint16_t* rt = tok + (size_t)ty * H;
+  float v[E];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     const int off = (c * 64 + lane) * 8;
-    const v4u g = *reinterpret_cast<const v4u*>(gamma + off);
-    const v4u bt = *reinterpret_cast<const v4u*>(beta + off);
-    v4u o;
+    const v4u a = *reinterpret_cast<const v4u*>(rw + off);
+    const v4u b = *reinterpret_cast<const v4u*>(rp + off);
+    const v4u t = *reinterpret_cast<const v4u*>(rt + off);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float g0 = __uint_as_float(g[q] << 16), g1 = __uint_as_float(g[q] & 0xffff0000u);
-      const float b0 = __uint_as_float(bt[q] << 16), b1 = __uint_as_float(bt[q] & 0xffff0000u);
-      o[q] = pack2((v[c * 8 + 2 * q] - mean) * rstd * g0 + b0, (v[c * 8 + 2 * q + 1] - mean) * rstd * g1 + b1);
+      v[c * 8 + 2 * q] = __uint_as_float(a[q] << 16) + __uint_as_float(b[q] << 16) + __uint_as_float(t[q] << 16);
+      v[c * 8 + 2 * q + 1] = __uint_as_float(a[q] & 0xffff0000u) + __uint_as_float(b[q] & 0xffff0000u) +
+                             __uint_as_float(t[q] & 0xffff0000u);
     }
-    *reinterpret_cast<v4u*>(out + base + off) = o;
   }
+  ln_store_row<E>(v, gamma, beta, out + (size_t)row * H, lane, eps);
 }
 
 }  // namespace
@@ -309,6 +358,30 @@ int tcamd_add_layernorm(const void* x, const void* y, const void* gamma, const v
     case 1024: hipLaunchKernelGGL(add_layernorm_kernel<16>, grid, block, 0, s, px, py, pg, pb, po, rows, eps); break;
     case 2048: hipLaunchKernelGGL(add_layernorm_kernel<32>, grid, block, 0, s, px, py, pg, pb, po, rows, eps); break;
     case 4096: hipLaunchKernelGGL(add_layernorm_kernel<64>, grid, block, 0, s, px, py, pg, pb, po, rows, eps); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// Embedding sum + LayerNorm (H in {512, 1024, 2048, 4096}): out [rows][H] bf16
+// = LN(word[ids] + pos[row % S] + type[types]); ids / types int64 [rows].
+int tcamd_embed_layernorm(const int64_t* ids, const int64_t* types, const void* word, const void* pos,
+                          const void* type, const void* gamma, const void* beta, void* out, int rows, int S, int H,
+                          int vocab, int ntypes, float eps, void* stream) {
+  if (rows <= 0) return hipSuccess;
+  if (!ids || !types || S <= 0 || vocab <= 0 || ntypes <= 0 ||
+      ((uintptr_t)word | (uintptr_t)pos | (uintptr_t)type | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)out) % 16)
+    return hipErrorInvalidValue;
+  const dim3 grid((rows + 3) / 4), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  const auto *w = (const uint16_t*)word, *p = (const uint16_t*)pos, *t = (const uint16_t*)type;
+  const auto *g = (const uint16_t*)gamma, *b = (const uint16_t*)beta;
+  auto* o = (uint16_t*)out;
+  switch (H) {
+    case 512: hipLaunchKernelGGL(embed_layernorm_kernel<8>, grid, block, 0, st, ids, types, w, p, t, g, b, o, rows, S, vocab, ntypes, eps); break;
+    case 1024: hipLaunchKernelGGL(embed_layernorm_kernel<16>, grid, block, 0, st, ids, types, w, p, t, g, b, o, rows, S, vocab, ntypes, eps); break;
+    case 2048: hipLaunchKernelGGL(embed_layernorm_kernel<32>, grid, block, 0, st, ids, types, w, p, t, g, b, o, rows, S, vocab, ntypes, eps); break;
+    case 4096: hipLaunchKernelGGL(embed_layernorm_kernel<64>, grid, block, 0, st, ids, types, w, p, t, g, b, o, rows, S, vocab, ntypes, eps); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

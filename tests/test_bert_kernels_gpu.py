@@ -35,6 +35,26 @@ def test_add_layernorm(rows, H, alias):
     assert (out.float() - ref).abs().max().item() < 0.1
 
 
+@pytest.mark.parametrize("b,s", [(1, 384), (3, 128), (2, 7)])
+def test_embed_layernorm_matches_torch(b, s):
+    """Embedding sum + LayerNorm in one launch vs the torch ops in fp32."""
+    _need_gpu()
+    from triton_client_amd.models import bert
+
+    m = bert.build(device=DEV, layers=1)
+    with torch.no_grad():
+        m.ln.weight.copy_(torch.rand_like(m.ln.weight.float()) + 0.5)
+        m.ln.bias.copy_(torch.randn_like(m.ln.bias.float()) * 0.1)
+        ids = torch.randint(0, bert.VOCAB, (b, s), device=DEV)
+        tt = torch.randint(0, bert.TYPES, (b, s), device=DEV)
+        got = m._embed(ids, tt).float()
+        pos = torch.arange(s, device=DEV)
+        e = m.word.weight.float()[ids] + m.pos.weight.float()[pos][None] + m.tok_type.weight.float()[tt]
+        ref = torch.nn.functional.layer_norm(e, (bert.HIDDEN,), m.ln.weight.float(), m.ln.bias.float(), m.ln.eps)
+    err = (got - ref).norm() / ref.norm()
+    assert err.item() < 1e-2, err.item()
+
+
 def test_add_layernorm_rejects_bad_width():
     _need_gpu()
     from triton_client_amd.ops import hip

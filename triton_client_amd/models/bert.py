@@ -14,7 +14,7 @@ key-padding mask and writes the [tokens, hidden] layout the output projection re
 over 384 or off the GPU), plain GEMMs on hipBLASLt, the GELU
 in the FFN-up GEMM's epilogue (``torch._addmm_activation``) and every
 residual add + LayerNorm as ONE hand-written HIP kernel (K11,
-csrc/kernels/bert.hip).  The serving wrapper captures one HIP graph per
+csrc/kernels/bert.hip), as is the embedding sum + LayerNorm.  The serving wrapper captures one HIP graph per
 batch bucket.
 """
 
@@ -120,13 +120,31 @@ class BertLargeQA(nn.Module):
         self.layers = nn.ModuleList(_Layer() for _ in range(layers))
         self.qa = nn.Linear(HIDDEN, 2)
 
+    def _embed(self, input_ids, token_type_ids):
+        """LayerNorm(word + position + token-type embeddings): one HIP launch on
+        the GPU (csrc/kernels/bert.hip embed_layernorm), torch ops elsewhere."""
+        b, s = input_ids.shape
+        w = self.word.weight
+        if FUSED and w.is_cuda and w.dtype == torch.bfloat16 and s <= MAX_POS:
+            from triton_client_amd.ops import hip
+
+            ids = input_ids.to(torch.int64).contiguous()
+            tt = token_type_ids.to(torch.int64).contiguous()
+            out = torch.empty(b, s, HIDDEN, device=w.device, dtype=w.dtype)
+            hip.embed_layernorm(ids.data_ptr(), tt.data_ptr(), w.data_ptr(), self.pos.weight.data_ptr(),
+                                self.tok_type.weight.data_ptr(), self.ln.weight.data_ptr(), self.ln.bias.data_ptr(),
+                                out.data_ptr(), b * s, s, HIDDEN, VOCAB, TYPES, self.ln.eps,
+                                stream=torch.cuda.current_stream(w.device).cuda_stream)
+            return out
+        pos = torch.arange(s, device=input_ids.device)
+        return self.ln(self.word(input_ids) + self.pos(pos)[None] + self.tok_type(token_type_ids))
+
     def forward(self, input_ids, attention_mask, token_type_ids, dense=False):
         """dense=True: the caller guarantees attention_mask is all ones, so
         attention runs without a bias (torch-ROCm's unmasked fused kernel is
         ~1.8x faster at bs64 x 384, tools/attn_probe.py)."""
         b, s = input_ids.shape
-        pos = torch.arange(s, device=input_ids.device)
-        x = self.ln(self.word(input_ids) + self.pos(pos)[None] + self.tok_type(token_type_ids))
+        x = self._embed(input_ids, token_type_ids)
         # additive key-padding mask [b, 1, 1, s] in the compute dtype
         bias = None if dense else ((1.0 - attention_mask[:, None, None, :].to(x.dtype)) * -10000.0).to(x.dtype)
         mask_i32 = None if dense else attention_mask.to(torch.int32).contiguous()

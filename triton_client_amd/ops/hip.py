@@ -239,6 +239,12 @@ _SIGS = {
          ctypes.c_int, ctypes.c_float, ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "tcamd_embed_layernorm": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+         ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_attention_bias": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
          ctypes.c_float, ctypes.c_void_p],
@@ -601,6 +607,13 @@ def add_layernorm(x, y, gamma, beta, out, rows, H, eps, stream=None):
 
 
 ATTENTION_MAX_SEQ = 384
+
+
+def embed_layernorm(ids, types, word, pos, type_, gamma, beta, out, rows, S, H, vocab, ntypes, eps, stream=None):
+    """BERT embeddings in one launch: out [rows][H] bf16 = LayerNorm(word[ids] +
+    pos[row % S] + type[types]) * gamma + beta; ids / types int64 [rows]."""
+    _check(_load().tcamd_embed_layernorm(_vp(ids), _vp(types), word, pos, type_, gamma, beta, out, int(rows), int(S),
+                                         int(H), int(vocab), int(ntypes), float(eps), _vp(stream)), "embed_layernorm")
 
 
 def attention(qkv, mask, out, seqs, S, heads, scale, stream=None, bias=None):
