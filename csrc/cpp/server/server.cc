@@ -1926,7 +1926,9 @@ void Server::Worker(std::shared_ptr<NativeModel> m, int instance)
         const char* e = getenv("TCSERVE_STAGGER");
         return !e || atoi(e) != 0;
       }();
-      if (stagger && m->instances > 1 && m->busy > 0 && m->ema_exec_ns > 0) {
+      // (only for full batches: under light load a partial batch goes out as
+      // before, so a second request never waits out half an execution)
+      if (stagger && m->instances > 1 && m->busy > 0 && m->ema_exec_ns > 0 && m->q_rows >= pref_max) {
         const uint64_t earliest = m->last_start_ns + static_cast<uint64_t>(m->ema_exec_ns / m->instances);
         while (!m->stopping && m->busy > 0) {
           const uint64_t now = NowNs();
