@@ -139,6 +139,7 @@ struct NativeModel {
   uint64_t delay_ns = 0;
   std::vector<int> preferred;  // ascending; dynamic_batching.preferred_batch_size
   bool idle_dispatch = true;   // no queue delay while every instance is idle
+  bool pipelined = false;      // a free instance takes the queue once it holds the last batch's rows
   int busy = 0;                // instances executing a batch (under mu)
   int instances = 1;
   uint64_t last_start_ns = 0;  // staggered dispatch (under mu): the last batch's start
@@ -1906,19 +1907,16 @@ void Server::Worker(std::shared_ptr<NativeModel> m, int instance)
       const int pref_max = m->preferred.empty() ? cap : std::min(cap, m->preferred.back());
       if (m->max_batch > 0 && m->delay_ns > 0) {
         const uint64_t deadline = m->q.front()->t_arrive + m->delay_ns;
-        // pipelined dispatch: with an instance free and as many rows queued as
-        // the last batch carried, waiting out the delay cannot build a bigger
-        // batch in a closed loop; go now.  bs1 at concurrency 64 on 2
-        // instances: 18.0-18.4k -> 19.9-22.1k infer/s, p50 3.3 -> 2.4 ms; the
-        // headline's full batches never reach this rule (profiles/r3_instances.md).
-        // TCSERVE_PIPELINED=0: off.
-        static const bool pipelined = [] {
-          const char* e = getenv("TCSERVE_PIPELINED");
-          return !e || atoi(e) != 0;
-        }();
+        // pipelined dispatch (per model, opt-in): with an instance free and as
+        // many rows queued as the last batch carried, waiting out the delay
+        // cannot build a bigger batch in a closed loop; go now.  densenet_onnx
+        // bs1 at concurrency 64 on 2 instances: 18.0-18.4k -> 19.9-22.1k
+        // infer/s, p50 3.3 -> 2.4 ms; its headline's full batches never reach
+        // this rule.  Off for bert_large, where it locked concurrency 16 into
+        // small batches (profiles/r3_instances.md).
         while (!m->stopping && m->q_rows < pref_max) {
           if (m->idle_dispatch && m->busy == 0) break;
-          if (pipelined && m->busy < m->instances && m->last_rows > 0 && m->q_rows >= m->last_rows) break;
+          if (m->pipelined && m->busy < m->instances && m->last_rows > 0 && m->q_rows >= m->last_rows) break;
           const uint64_t now = NowNs();
           if (now >= deadline) break;
           m->cv.wait_for(lk, std::chrono::nanoseconds(deadline - now));
@@ -2277,7 +2275,8 @@ int32_t tcserve_set_idle_dispatch(void* server, const char* name, int32_t on)
     m = it->second;
   }
   std::lock_guard<std::mutex> lk(m->mu);
-  m->idle_dispatch = on != 0;
+  m->idle_dispatch = (on & 1) != 0;  // bit 0: idle-aware dispatch
+  m->pipelined = (on & 2) != 0;      // bit 1: pipelined dispatch of partial batches
   return 0;
 }
 

@@ -49,7 +49,9 @@ class DensenetOnnx(Model):
     max_batch_size = 128
     inputs = (TensorSpec("data_0", "FP32", [3, 224, 224], fmt="NCHW"),)
     outputs = (TensorSpec("fc6_1", "FP32", [1000], label_filename="densenet_labels.txt"),)
-    dynamic_batching = {"preferred": [], "max_queue_delay_us": 500}
+    # pipelined: tcserve dispatches a partial batch to a free instance once the
+    # queue holds as many rows as the last batch (bs1 closed loops)
+    dynamic_batching = {"preferred": [], "max_queue_delay_us": 500, "pipelined": True}
     instance_kind = "KIND_GPU"
     instance_count = 2
     gpus = (0,)

@@ -214,14 +214,17 @@ class NativeFrontend:
         pref = [int(x) for x in (inst.dynamic_batching or {}).get("preferred", [])]
         if pref:
             self.set_preferred(name, pref)
-        self.set_idle_dispatch(name, bool((inst.dynamic_batching or {}).get("idle_dispatch", True)))
+        db = inst.dynamic_batching or {}
+        self.set_idle_dispatch(name, bool(db.get("idle_dispatch", True)), pipelined=bool(db.get("pipelined", False)))
         with self._lock:
             self._cbs[name] = cb
             self._versions[name] = str(inst.version)
 
-    def set_idle_dispatch(self, name, on):
-        """Skip the queue delay while every instance of the model is idle."""
-        if _load().tcserve_set_idle_dispatch(self._h, name.encode(), int(bool(on))) != 0:
+    def set_idle_dispatch(self, name, on, pipelined=False):
+        """Skip the queue delay while every instance of the model is idle;
+        ``pipelined``: a free instance also takes a partial batch once the queue
+        holds as many rows as the last batch did."""
+        if _load().tcserve_set_idle_dispatch(self._h, name.encode(), int(bool(on)) | (int(bool(pipelined)) << 1)) != 0:
             raise KeyError(name)
 
     def set_preferred(self, name, sizes):
