@@ -165,6 +165,14 @@ class ServerHandle:
                         native_grpc=self.native_grpc, tls=self.tls)
 
         loop.run_until_complete(main())
+        # batcher workers (and any other task still parked on a queue) end
+        # with the loop, as asyncio.run would do it
+        pending = asyncio.all_tasks(loop)
+        for t in pending:
+            t.cancel()
+        if pending:
+            loop.run_until_complete(asyncio.gather(*pending, return_exceptions=True))
+        loop.run_until_complete(loop.shutdown_asyncgens())
         loop.close()
 
     def start(self, timeout=30):
