@@ -58,7 +58,7 @@ for step in "$@"; do
     prof)
       tag=${args[0]}
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null || exit 1
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/prof_${tag}" -o run -- "${args[@]:1}" \
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/prof_${tag}" -o run_%pid% -- "${args[@]:1}" \
         > "gpurun_out/prof_${tag}.log" 2>&1
       rc=$?
       tail -2 "gpurun_out/prof_${tag}.log"
