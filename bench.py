@@ -71,6 +71,9 @@ def parse_args(argv=None):
     ap.add_argument("--window", type=int, default=16, help="requests per step = window x concurrency")
     ap.add_argument("--bs1-concurrency", type=int, default=64)
     ap.add_argument("--fanout", default="rccl", choices=["rccl", "p2p", "local"])
+    ap.add_argument("--fanout-fallback", default="none", choices=["none", "local"],
+                    help="none (default): a failed RCCL broadcast ends the run non-zero with the error; "
+                         "local: ranks agree over a gloo control group and refill locally (labelled)")
     ap.add_argument("--engine", default="fp32", choices=["fp32", "fused", "torch"],
                     help="densenet_onnx engine for the headline (fp32 = fp32-parity split-precision kernels)")
     ap.add_argument("--no-bf16", action="store_true", help="skip the bf16-engine secondary measurement")
@@ -246,6 +249,9 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        from triton_client_amd.parallel import fanout as _fo
+
+        _fo.cpu_group()  # the gloo control group (collective creation: every rank, now)
 
     import tritonclient.grpc as grpcclient
     from triton_client_amd.parallel import fanout
@@ -278,8 +284,8 @@ def main():
             r = shmod.create_shared_memory_region(name, nbytes, dev)
             regions.append(r)
             method = fanout.fill_and_fanout(r, "FP32", elems, seed=1234, mode="normal", lo=0.0, hi=1.0,
-                                            method=args.fanout)
-            if not fanout.verify_replicas(r, nbytes):
+                                            method=args.fanout, fallback=args.fanout_fallback)
+            if not fanout.verify_replicas(r, nbytes, over_cpu=method == fanout.LOCAL_FALLBACK):
                 raise RuntimeError("fan-out replicas differ across ranks")
             state["client"].register_cuda_shared_memory(name, shmod.get_raw_handle(r), dev, nbytes)
         return method, nbytes
@@ -287,7 +293,7 @@ def main():
     def measure(point, steps, per):
         """W warmup already done; EXACTLY `steps` windows between barrier + sync."""
         if world > 1:
-            dist.barrier()
+            fanout.barrier()
         if not cpu:
             torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -295,7 +301,7 @@ def main():
         if not cpu:
             torch.cuda.synchronize()
         if world > 1:
-            dist.barrier()
+            fanout.barrier()
         elapsed = time.perf_counter() - t0
         return lat, end, fanout.max_over_ranks(elapsed)
 
@@ -313,8 +319,11 @@ def main():
         if not cpu and world > 1:
             # X1 (RCCL broadcast) vs X2 (xGMI one-hop star), once, on the headline input
             # region; a rehearsal on one GPU times p2p and host staging
-            fan["timings"] = fanout.time_fanout(regions[0], in_bytes, ["p2p", "host"] if rehearse else ["rccl", "p2p"])
-            if not fanout.verify_replicas(regions[0], in_bytes):
+            fan["timings"] = fanout.time_fanout(
+                regions[0], in_bytes, ["p2p", "host"] if rehearse else
+                (["p2p"] if method == fanout.LOCAL_FALLBACK else ["rccl", "p2p"]))
+            fan["errors"] = fanout.fanout_errors(fan["timings"])
+            if not fanout.verify_replicas(regions[0], in_bytes, over_cpu=method == fanout.LOCAL_FALLBACK):
                 raise RuntimeError("fan-out replicas differ across ranks after the fan-out timing")
             t_used = fan["timings"].get(method, {})
             if "us" in t_used:
@@ -443,6 +452,7 @@ def main():
             "p99_constrained": p99c,
             "bs1": bs1,
             "fanout": fan,
+            "fanout_errors": fan.get("errors", {}),
             "world_size_reported_by_process_group": dist.get_world_size() if world > 1 else 1,
         }
         for p in points:
@@ -531,8 +541,8 @@ def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout
             r = shmod.create_shared_memory_region(reg, nbytes, local_rank)
             regions.append(r)
             method = fanout.fill_and_fanout(r, "INT32", BERT_SEQ, seed=1234, mode=mode, lo=lo, hi=hi,
-                                            method=args.fanout)
-            if not fanout.verify_replicas(r, nbytes):
+                                            method=args.fanout, fallback=args.fanout_fallback)
+            if not fanout.verify_replicas(r, nbytes, over_cpu=method == fanout.LOCAL_FALLBACK):
                 raise RuntimeError("fan-out replicas differ across ranks")
             client.register_cuda_shared_memory(reg, shmod.get_raw_handle(r), local_rank, nbytes)
         inputs[name] = reg

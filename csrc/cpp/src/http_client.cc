@@ -963,7 +963,7 @@ InferenceServerHttpClient::LoadModel(
   if (!config.empty() || !files.empty()) {
     Value p = Value::Object();
     if (!config.empty()) p.Set("config", Value(config));
-    for (const auto& kv : files) p.Set(kv.first, Value(Base64Encode(kv.second.data(), kv.second.size())));
+    for (const auto& kv : files) p.Set(kv.first, Value(Base64EncodeLibb64(kv.second.data(), kv.second.size())));
     req.Set("parameters", std::move(p));
   }
   return Post(uri, req.Serialize(), headers, q, nullptr);
@@ -1085,7 +1085,7 @@ InferenceServerHttpClient::RegisterCudaSharedMemory(
   std::string uri = "v2/cudasharedmemory/region/" + UrlEncode(name) + "/register";
   Value req = Value::Object();
   Value h = Value::Object();
-  h.Set("b64", Value(Base64Encode(&cuda_shm_handle, sizeof(cuda_shm_handle))));
+  h.Set("b64", Value(Base64EncodeLibb64(&cuda_shm_handle, sizeof(cuda_shm_handle))));
   req.Set("raw_handle", std::move(h));
   req.Set("device_id", Value(static_cast<uint64_t>(device_id)));
   req.Set("byte_size", Value(static_cast<uint64_t>(byte_size)));

@@ -492,6 +492,21 @@ Base64Encode(const void* data, size_t n)
   return out;
 }
 
+std::string
+Base64EncodeLibb64(const void* data, size_t n)
+{
+  const std::string flat = Base64Encode(data, n);
+  const size_t full = (n / 3) * 4;  // characters of complete 3-byte groups
+  std::string out;
+  out.reserve(flat.size() + full / 72 + 1);
+  for (size_t i = 0; i < flat.size(); ++i) {
+    out.push_back(flat[i]);
+    if (i < full && (i + 1) % 72 == 0) out.push_back('\n');
+  }
+  out.push_back('\n');
+  return out;
+}
+
 bool
 Base64Decode(const std::string& in, std::string* out)
 {

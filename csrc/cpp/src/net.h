@@ -95,6 +95,12 @@ bool Compress(const std::vector<std::pair<const char*, size_t>>& parts, bool gzi
 bool Decompress(const std::string& in, std::string* out);
 
 std::string Base64Encode(const void* data, size_t n);
+/// Base64 with the reference's libb64 framing (src/c++/library/cencode.c:
+/// 78-81,106): a '\n' after every 72 output characters of full 3-byte groups,
+/// then the padding, then a terminating '\n'.  The reference HTTP client sends
+/// exactly these bytes in the LoadModel file-override values and the CUDA-shm
+/// register "b64" handle, so ours does too (byte-compatible request bodies).
+std::string Base64EncodeLibb64(const void* data, size_t n);
 bool Base64Decode(const std::string& in, std::string* out);
 std::string UrlEncode(const std::string& s);
 

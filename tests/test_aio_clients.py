@@ -199,3 +199,52 @@ def test_http_aio_stays_on_native_path_and_scales(cpu_server):
     assert after["proxied_calls"] == before["proxied_calls"]
     assert one > 800, "one aio task: %.0f infer/s (the relayed/gzip path ran ~400)" % one
     assert many > 800, "64 aio tasks: %.0f infer/s (the relayed/gzip path ran ~970-1300)" % many
+
+
+def test_http_aio_transport_retries_only_idempotent_requests():
+    """A keep-alive connection the server drops before answering: GET is retried
+    once on a fresh connection, POST is not (it may already have run on the
+    server)."""
+    from tritonclient.http.aio._transport import HttpTransportError, Pool
+
+    async def body():
+        seen = []
+
+        async def handle(reader, writer):
+            n = 0
+            while True:
+                head = await reader.readuntil(b"\r\n\r\n")
+                line = head.split(b"\r\n", 1)[0].decode()
+                clen = [int(h.split(b":")[1]) for h in head.split(b"\r\n") if h.lower().startswith(b"content-length")]
+                if clen:
+                    await reader.readexactly(clen[0])
+                seen.append(line)
+                n += 1
+                if n == 2:  # the second request on a connection: drop it unanswered
+                    writer.close()
+                    return
+                writer.write(b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\n\r\nok")
+                await writer.drain()
+
+        srv = await asyncio.start_server(handle, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        pool = Pool("127.0.0.1", port, limit=1)
+        try:
+            # every second request on a connection is dropped and retried on a new one
+            for _ in range(3):
+                assert (await pool.request("GET", "/v2", {})).body == b"ok"
+        finally:
+            pool.close()
+        assert sum(s.startswith("GET") for s in seen) == 5
+        pool = Pool("127.0.0.1", port, limit=1)
+        try:
+            assert (await pool.request("POST", "/v2/models/m/infer", {}, b"{}")).status == 200
+            with pytest.raises(HttpTransportError):
+                await pool.request("POST", "/v2/models/m/infer", {}, b"{}")
+        finally:
+            pool.close()
+            srv.close()
+        posts = [s for s in seen if s.startswith("POST")]
+        assert len(posts) == 2, seen  # the dropped POST was not re-sent
+
+    run(body())

@@ -68,3 +68,77 @@ def test_every_reference_cpp_example_is_ported():
            "simple_http_infer_client", "simple_http_model_control", "simple_http_sequence_sync_infer_client",
            "simple_http_shm_client", "simple_http_string_infer_client"}
     assert ref <= set(os.listdir(BIN)), sorted(ref - set(os.listdir(BIN)))
+
+
+def _libb64(data):
+    """The reference's libb64 framing, written from its documented behaviour
+    (src/c++/library/cencode.c:78-81,106): '\\n' after each 72 characters of
+    complete 3-byte groups, then the padding, then a terminating '\\n'."""
+    import base64
+
+    flat = base64.b64encode(bytes(data)).decode()
+    full = len(data) // 3 * 4
+    out = []
+    for i, ch in enumerate(flat):
+        out.append(ch)
+        if i < full and (i + 1) % 72 == 0:
+            out.append("\n")
+    return "".join(out) + "\n"
+
+
+def _capture_bodies(args, n_requests=2):
+    """Run http_body_test against a raw socket that records each request's
+    (request line, body) and answers 200 "{}"."""
+    import json
+    import socket
+    import threading
+
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(4)
+    port = srv.getsockname()[1]
+    got = []
+
+    def serve():
+        conn, _ = srv.accept()
+        buf = b""
+        while len(got) < n_requests:
+            while b"\r\n\r\n" not in buf:
+                d = conn.recv(65536)
+                if not d:
+                    return
+                buf += d
+            head, buf = buf.split(b"\r\n\r\n", 1)
+            n = [int(h.split(b":")[1]) for h in head.split(b"\r\n") if h.lower().startswith(b"content-length")][0]
+            while len(buf) < n:
+                buf += conn.recv(65536)
+            body, buf = buf[:n], buf[n:]
+            got.append((head.split(b"\r\n")[0].decode(), json.loads(body)))
+            conn.sendall(b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\nContent-Type: application/json\r\n\r\n{}")
+        conn.close()
+
+    t = threading.Thread(target=serve, daemon=True)
+    t.start()
+    r = subprocess.run([os.path.join(BIN, "http_body_test"), "127.0.0.1:%d" % port] + args, capture_output=True,
+                       text=True, timeout=60)
+    t.join(10)
+    srv.close()
+    assert r.returncode == 0, r.stderr
+    return got
+
+
+@pytest.mark.parametrize("nbytes", [0, 1, 2, 53, 54, 55, 200])
+def test_cpp_http_base64_is_libb64_framed(nbytes):
+    """C7: LoadModel file overrides and the CUDA-shm register handle carry
+    base64 with the reference's libb64 line framing, byte for byte."""
+    got = _capture_bodies([str(nbytes)])
+    (load_line, load), (reg_line, reg) = got
+    assert load_line.startswith("POST /v2/repository/models/b64_model/load")
+    content = bytes(i % 251 for i in range(nbytes))
+    assert load["parameters"]["file:1/model.onnx"] == _libb64(content)
+    assert reg_line.startswith("POST /v2/cudasharedmemory/region/b64_region/register")
+    assert reg["raw_handle"]["b64"] == _libb64(bytes(range(64)))
+    # pinned literal for the 64-byte handle: wrapped after 72 characters, trailing newline
+    assert reg["raw_handle"]["b64"] == (
+        "AAECAwQFBgcICQoLDA0ODxAREhMUFRYXGBkaGxwdHh8gISIjJCUmJygpKissLS4vMDEyMzQ1\n"
+        "Njc4OTo7PD0+Pw==\n")

@@ -81,3 +81,104 @@ def test_two_rank_fanout_and_perf(tmp_path):
     if "elapsed" in results[0]:
         assert results[0]["elapsed_max"] == results[1]["elapsed_max"] == max(r["elapsed"] for r in results)
         assert results[0]["n_lat_all"] == 400
+
+
+def _fanout_fault_worker(rank, world, port, out_dir, fallback):
+    """fill_and_fanout with an injected broadcast failure on rank 1 (the region
+    is a CPU tensor and the fill a deterministic CPU write, so the RCCL code
+    path runs over gloo here)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      TCAMD_FANOUT_FAULT="broadcast:1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from triton_client_amd.parallel import fanout
+
+    n = 256
+    region = torch.zeros(n * 4, dtype=torch.uint8)
+    fanout.region_tensor = lambda r, nbytes: r[:nbytes]
+
+    def fill(r, datatype, n_elems, mode, lo, hi, seed):
+        r.view(torch.int32)[:n_elems] = torch.arange(n_elems, dtype=torch.int32) * 3 + seed
+
+    fanout._fill = fill
+    res = {"rank": rank}
+    try:
+        res["method"] = fanout.fill_and_fanout(region, "INT32", n, seed=5, method="rccl", fallback=fallback)
+        res["verified"] = fanout.verify_replicas(region, n * 4, over_cpu=res["method"] == fanout.LOCAL_FALLBACK)
+        res["data_ok"] = bool(torch.equal(region.view(torch.int32), torch.arange(n, dtype=torch.int32) * 3 + 5))
+    except Exception as e:  # noqa: BLE001 - recorded, then re-raised: the rank must exit non-zero
+        res["error"] = str(e)
+        with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
+            json.dump(res, f)
+        raise
+    finally:
+        if "error" not in res:
+            with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
+                json.dump(res, f)
+    dist.destroy_process_group()
+
+
+def test_fanout_rccl_failure_is_loud_by_default(tmp_path):
+    """A failed broadcast ends the run non-zero with the error (verdict r3 #5)."""
+    with pytest.raises(mp.ProcessRaisedException, match="RCCL broadcast of the synthetic batch failed"):
+        mp.start_processes(_fanout_fault_worker, args=(2, _free_port(), str(tmp_path), None), nprocs=2, join=True,
+                           start_method="spawn")
+    with open(os.path.join(tmp_path, "rank1.json")) as f:
+        r1 = json.load(f)
+    assert "injected broadcast fault on rank 1" in r1["error"]
+
+
+def test_fanout_rccl_failure_labelled_local_fallback(tmp_path):
+    """--fanout-fallback local: every rank agrees over the control group, refills
+    locally, labels the method and verifies the replicas over gloo."""
+    mp.start_processes(_fanout_fault_worker, args=(2, _free_port(), str(tmp_path), "local"), nprocs=2, join=True,
+                       start_method="spawn")
+    from triton_client_amd.parallel import fanout
+
+    for r in range(2):
+        with open(os.path.join(tmp_path, "rank%d.json" % r)) as f:
+            res = json.load(f)
+        assert res["method"] == fanout.LOCAL_FALLBACK
+        assert res["verified"] and res["data_ok"]
+
+
+def _p2p_error_worker(rank, world, port, out_dir):
+    """time_fanout with a p2p failure on rank 0 only: every rank reports the same
+    agreed error and the collective sequence stays aligned (the next collective
+    completes on every rank)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      TCAMD_FANOUT_FAULT="p2p:0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from triton_client_amd.parallel import fanout
+
+    calls = []
+
+    def fake_copy(region, nbytes, d):
+        calls.append(1)
+        err = None
+        try:
+            fanout._fault("p2p")
+        except RuntimeError as e:
+            err = e
+        d.barrier()
+        return err
+
+    fanout._p2p_copy = fake_copy
+    t = fanout.time_fanout(object(), 64, ["p2p"], reps=2)
+    after = fanout.max_over_ranks(float(rank))
+    with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
+        json.dump({"timings": t, "errors": fanout.fanout_errors(t), "after": after, "calls": len(calls)}, f)
+    dist.destroy_process_group()
+
+
+def test_time_fanout_agrees_on_a_one_rank_failure(tmp_path):
+    mp.start_processes(_p2p_error_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    res = []
+    for r in range(2):
+        with open(os.path.join(tmp_path, "rank%d.json" % r)) as f:
+            res.append(json.load(f))
+    for r in res:
+        assert "p2p" in r["errors"], r
+        assert r["after"] == 1.0 and r["calls"] == 3
+    assert "injected p2p fault on rank 0" in res[0]["errors"]["p2p"]
+    assert res[1]["errors"]["p2p"] == "failed on another rank"

@@ -17,6 +17,9 @@ For a few-MB batch the broadcast is latency-bound (densenet bs=8: 4.8 MB is
 ~31 us at ~153 GB/s per link), so the star pays one hop where a ring pays 7.
 """
 
+import os
+import sys
+
 import numpy as np
 
 from triton_client_amd.utils import roctx
@@ -38,60 +41,148 @@ def region_tensor(region, nbytes):
     return torch.from_dlpack(view)
 
 
-def fill_and_fanout(region, datatype, n_elems, seed=0, mode="random", lo=0.0, hi=1.0, method="rccl"):
-    """Fill ``region`` on rank 0 and replicate to every rank. Returns method used."""
+def _fill(region, datatype, n_elems, mode, lo, hi, seed):
     from tritonclient.utils import hip_shared_memory as hipshm
+
+    hipshm.fill_synthetic_data(region, datatype, n_elems, mode, lo, hi, seed)
+
+
+def _device_sync():
+    import torch
+
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+_CPU_GROUP = []
+
+
+def cpu_group(timeout_s=300):
+    """A gloo group over the same ranks, for control-plane agreement.  An RCCL
+    failure must not be voted on over the communicator that just failed: a
+    poisoned communicator hangs or pairs the vote with the wrong collective on
+    the other ranks.  Creating a group is itself collective, so every rank calls
+    this once right after init_process_group (bench.py does).  Returns None
+    (= the default group) when the default group already is gloo."""
+    dist = _dist()
+    if dist is None or dist.get_backend() == "gloo":
+        return None
+    if not _CPU_GROUP:
+        import datetime
+
+        _CPU_GROUP.append(dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s)))
+    return _CPU_GROUP[0]
+
+
+def all_ok(ok):
+    """True on every rank iff ``ok`` is true on every rank (MIN over the gloo
+    control group; also a barrier)."""
+    dist = _dist()
+    if dist is None or dist.get_world_size() == 1:
+        return bool(ok)
+    import torch
+
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=cpu_group())
+    return bool(t.item())
+
+
+def _fault(point):
+    """Test hook: TCAMD_FANOUT_FAULT=<point>:<rank,rank..> raises after the
+    collective at ``point`` on the listed ranks (an NCCL error surfaces at the
+    next synchronize, after the call was issued on every rank)."""
+    spec = os.environ.get("TCAMD_FANOUT_FAULT", "")
+    if not spec or ":" not in spec:
+        return
+    where, ranks = spec.split(":", 1)
+    dist = _dist()
+    if where == point and dist is not None and str(dist.get_rank()) in ranks.split(","):
+        raise RuntimeError("injected %s fault on rank %d" % (point, dist.get_rank()))
+
+
+def fill_and_fanout(region, datatype, n_elems, seed=0, mode="random", lo=0.0, hi=1.0, method="rccl",
+                    fallback=None):
+    """Fill ``region`` on rank 0 and replicate to every rank.  Returns the
+    method used.
+
+    A failed RCCL broadcast raises (the caller exits non-zero with the error):
+    the north star's fan-out must not be skipped quietly.  ``fallback="local"``
+    (bench.py ``--fanout-fallback local``) instead has every rank agree on the
+    broadcast's outcome over the gloo control group and, if any rank failed,
+    refill locally (K1 is a pure function of (seed, offset)); the method is then
+    labelled ``"local (fallback: rccl broadcast failed)"`` and the replicas must
+    be verified over the control group (``verify_replicas(..., over_cpu=True)``)."""
     from triton_client_amd.ops import dtypes
 
     dist = _dist()
     nbytes = n_elems * dtypes.SIZES[datatype]
     if dist is None or dist.get_world_size() == 1:
-        hipshm.fill_synthetic_data(region, datatype, n_elems, mode, lo, hi, seed)
+        _fill(region, datatype, n_elems, mode, lo, hi, seed)
         return "local"
     rank = dist.get_rank()
     if method == "local":
-        hipshm.fill_synthetic_data(region, datatype, n_elems, mode, lo, hi, seed)
+        _fill(region, datatype, n_elems, mode, lo, hi, seed)
         dist.barrier()
         return "local"
+    if fallback not in (None, "none", "local"):
+        raise ValueError("unknown fan-out fallback %s" % fallback)
     if rank == 0:
-        hipshm.fill_synthetic_data(region, datatype, n_elems, mode, lo, hi, seed)
+        _fill(region, datatype, n_elems, mode, lo, hi, seed)
     if method == "rccl":
-        import torch
-
         t = region_tensor(region, nbytes)
+        err = None
         try:
             with roctx.range("fanout.rccl_broadcast bytes=%d" % t.numel()):
                 dist.broadcast(t, src=0)
-            torch.cuda.synchronize()
+            _fault("broadcast")
+            _device_sync()
+        except Exception as e:  # noqa: BLE001 - re-raised below unless the fallback is asked for
+            err = e
+        if fallback != "local":
+            if err is not None:
+                raise RuntimeError("RCCL broadcast of the synthetic batch failed on rank %d: %s"
+                                   % (rank, err)) from err
             return "rccl"
-        except Exception as e:  # noqa: BLE001
-            # the Philox fill is deterministic: every rank can produce the
-            # same replica itself (the caller still verifies the replicas)
-            import sys
-
-            print("[fanout] rccl broadcast failed (%s); filling locally" % str(e)[:200], file=sys.stderr)
-            hipshm.fill_synthetic_data(region, datatype, n_elems, mode, lo, hi, seed)
-            torch.cuda.synchronize()
-            return "local (rccl broadcast failed)"
+        if all_ok(err is None):
+            return "rccl"
+        if err is not None:
+            print("[fanout] rank %d: rccl broadcast failed (%s)" % (rank, str(err)[:200]), file=sys.stderr)
+        _fill(region, datatype, n_elems, mode, lo, hi, seed)
+        _device_sync()
+        return LOCAL_FALLBACK
     if method == "p2p":
         with roctx.range("fanout.p2p_star bytes=%d" % nbytes):
             return _p2p_star(region, nbytes, dist)
     raise ValueError("unknown fan-out method %s" % method)
 
 
+LOCAL_FALLBACK = "local (fallback: rccl broadcast failed)"
+
+
 def _sync_all(dist):
-    import torch
-
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
-    dist.barrier()
+    _device_sync()
+    dist.barrier(group=cpu_group())
 
 
-def replicate(region, nbytes, method):
+def barrier():
+    """Barrier over the gloo control group (no-op without a process group):
+    the bench's control plane never rides on the RCCL communicator, so an RCCL
+    fallback run can still bracket, aggregate and report."""
+    dist = _dist()
+    if dist is not None:
+        dist.barrier(group=cpu_group())
+
+
+def replicate(region, nbytes, method, errors=None):
     """Copy rank 0's first ``nbytes`` of ``region`` into every rank's region
     (no refill).  rccl: one broadcast collective (X1); p2p: the xGMI one-hop
     star from rank 0 (X2); host: staged through host memory and a gloo/CPU
-    broadcast (the rehearsal path when several ranks share one GPU)."""
+    broadcast (the rehearsal path when several ranks share one GPU).
+
+    A p2p copy failure on rank 0 is caught there (every rank still reaches the
+    star's closing barrier): with an ``errors`` list it is appended for the
+    caller to agree on later, otherwise the ranks agree now over the gloo control
+    group and all raise together."""
     dist = _dist()
     if dist is None or dist.get_world_size() == 1:
         return "local"
@@ -99,10 +190,17 @@ def replicate(region, nbytes, method):
         t = region_tensor(region, nbytes)
         with roctx.range("fanout.rccl_broadcast bytes=%d" % nbytes):
             dist.broadcast(t, src=0)
+        _fault("broadcast")
         return "rccl"
     if method == "p2p":
         with roctx.range("fanout.p2p_star bytes=%d" % nbytes):
-            return _p2p_star(region, nbytes, dist)
+            err = _p2p_copy(region, nbytes, dist)
+        if errors is not None:
+            if err is not None:
+                errors.append(err)
+        elif not all_ok(err is None):
+            raise RuntimeError("p2p fan-out failed: %s" % (err if err is not None else "on another rank"))
+        return "p2p"
     if method == "host":
         import torch
 
@@ -117,8 +215,12 @@ def replicate(region, nbytes, method):
 def time_fanout(region, nbytes, methods, reps=5):
     """Time each fan-out method replicating the (already filled) region:
     median over ``reps`` of barrier -> replicate -> device sync -> barrier,
-    MAX over ranks.  Returns {method: {"us", "GBps_per_peer", "bytes"}} or an
-    {"error": ...} entry for a method this process group cannot run."""
+    MAX over ranks.  Returns {method: {"us", "GBps_per_peer", "bytes"}}; a p2p
+    method whose copies failed on any rank gets an agreed {"error": ...} entry
+    on every rank (the ranks never leave the common collective sequence: the
+    failure is caught where it happens and voted on over the gloo control
+    group).  A collective that raises (RCCL) propagates: the communicator is
+    unusable after it, and the run must fail loudly."""
     import time
 
     dist = _dist()
@@ -126,20 +228,15 @@ def time_fanout(region, nbytes, methods, reps=5):
     if dist is None or dist.get_world_size() == 1:
         return out
     for m in methods:
-        ts = []
-        try:
-            for _ in range(reps + 1):
-                _sync_all(dist)
-                t0 = time.perf_counter()
-                replicate(region, nbytes, m)
-                _sync_all(dist)
-                ts.append(time.perf_counter() - t0)
-        except Exception as e:  # noqa: BLE001 - reported in the JSON, the run goes on
-            out[m] = {"error": str(e)[:200]}
-            try:
-                dist.barrier()
-            except Exception:
-                pass
+        ts, errors = [], []
+        for _ in range(reps + 1):
+            _sync_all(dist)
+            t0 = time.perf_counter()
+            replicate(region, nbytes, m, errors=errors)
+            _sync_all(dist)
+            ts.append(time.perf_counter() - t0)
+        if not all_ok(not errors):
+            out[m] = {"error": str(errors[0])[:200] if errors else "failed on another rank"}
             continue
         med = float(np.median(ts[1:]))
         med = max_over_ranks(med)
@@ -147,7 +244,16 @@ def time_fanout(region, nbytes, methods, reps=5):
     return out
 
 
-def _p2p_star(region, nbytes, dist):
+def fanout_errors(timings):
+    """{method: error} of a time_fanout result (surfaced at the top level of
+    the bench JSON)."""
+    return {m: v["error"] for m, v in (timings or {}).items() if "error" in v}
+
+
+def _p2p_copy(region, nbytes, dist):
+    """The X2 star: rank 0 opens every peer's region and copies into it on one
+    stream per peer.  Returns rank 0's exception (None elsewhere / on success);
+    every rank reaches the closing barrier either way."""
     from tritonclient.utils import hip_shared_memory as hipshm  # noqa: F401
     from triton_client_amd.ops import hip
 
@@ -155,6 +261,7 @@ def _p2p_star(region, nbytes, dist):
     world = dist.get_world_size()
     handles = [None] * world
     dist.all_gather_object(handles, (region._device_id, region._hip_shm_handle))
+    err = None
     if rank == 0:
         src_dev = region._device_id
         streams = []
@@ -173,12 +280,22 @@ def _p2p_star(region, nbytes, dist):
                 hip.memcpy_async(ptr, region._base_addr, nbytes, s.handle)
             for s in streams:
                 s.synchronize()
+        except Exception as e:  # noqa: BLE001 - agreed on by the caller
+            err = e
         finally:
             for s in streams:
                 s.close()
             for p in opened:
                 hip.ipc_close(p, src_dev)
+    _fault("p2p")  # test hook (raises on the listed ranks after the copies)
     dist.barrier()
+    return err
+
+
+def _p2p_star(region, nbytes, dist):
+    err = _p2p_copy(region, nbytes, dist)
+    if not all_ok(err is None):
+        raise RuntimeError("p2p fan-out failed: %s" % (err if err is not None else "on another rank"))
     return "p2p"
 
 
@@ -221,8 +338,9 @@ def verify_host_replicas(buf, sample=4096):
     return bool(flag.item())
 
 
-def verify_replicas(region, nbytes, sample=4096):
-    """Every rank checks a strided sample of its region against rank 0's."""
+def verify_replicas(region, nbytes, sample=4096, over_cpu=False):
+    """Every rank checks a strided sample of its region against rank 0's
+    (``over_cpu``: over the gloo control group, after an RCCL fallback)."""
     import torch
 
     dist = _dist()
@@ -231,13 +349,17 @@ def verify_replicas(region, nbytes, sample=4096):
     s = t[idx].to(torch.int64)
     if dist is None:
         return True
-    if dist.get_backend() == "gloo":  # rehearsal: collectives on host copies
+    group = None
+    if over_cpu:
+        group = cpu_group()
+        s = s.cpu()
+    elif dist.get_backend() == "gloo":  # rehearsal: collectives on host copies
         s = s.cpu()
     ref = s.clone()
-    dist.broadcast(ref, src=0)
+    dist.broadcast(ref, src=0, group=group)
     ok = torch.equal(s, ref)
     flag = torch.tensor([1 if ok else 0], device=s.device)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
     return bool(flag.item())
 
 
@@ -248,11 +370,8 @@ def max_over_ranks(value):
         return value
     import torch
 
-    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
-    if dist.get_backend() == "gloo":
-        dev = "cpu"
-    t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = torch.tensor([float(value)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=cpu_group())
     return float(t.item())
 
 
@@ -262,5 +381,5 @@ def gather_arrays(arr):
     if dist is None:
         return arr
     out = [None] * dist.get_world_size()
-    dist.all_gather_object(out, np.asarray(arr))
+    dist.all_gather_object(out, np.asarray(arr), group=cpu_group())
     return np.concatenate(out) if out else arr

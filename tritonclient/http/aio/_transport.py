@@ -218,6 +218,7 @@ class Pool:
             head.append(b"Content-Length: %d\r\n" % n)
         head.append(b"\r\n")
         buffers = [b"".join(head)] + [b for b in bufs if memoryview(b).nbytes]
+        idempotent = method in ("GET", "HEAD")
         async with self._sem:
             for attempt in (0, 1):
                 conn = None
@@ -234,7 +235,12 @@ class Pool:
                 except HttpTransportError as e:
                     conn.close()
                     self._all.discard(conn)
-                    if attempt == 0 and conn.reused and getattr(e, "retryable", False):
+                    # a reused keep-alive connection the server closed before
+                    # any response byte: retried once, for GET/HEAD only.  A
+                    # POST (infer, load, shm register) may already have run on
+                    # the server; re-sending it could duplicate a sequence step,
+                    # so it surfaces as the reference's aiohttp client does.
+                    if attempt == 0 and conn.reused and getattr(e, "retryable", False) and idempotent:
                         continue
                     raise
                 except BaseException:

@@ -42,11 +42,12 @@ class DeviceContext:
         nbytes = int(nbytes)
         if nbytes > self._bytes:
             hip = _hip()
+            old = self._bytes  # doubling is against the size being replaced
             if self._scratch:
                 self.stream.synchronize()
                 hip.free(self.dev, self._scratch)
                 self._scratch, self._bytes = 0, 0
-            size = max(nbytes, 2 * self._bytes, 1 << 20)
+            size = max(nbytes, 2 * old, 1 << 20)
             size = (size + (2 << 20) - 1) & ~((2 << 20) - 1)
             self._scratch = hip.malloc(self.dev, size)
             self._bytes = size
