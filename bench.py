@@ -77,6 +77,9 @@ def parse_args(argv=None):
     ap.add_argument("--engine", default="fp32", choices=["fp32", "fused", "torch"],
                     help="densenet_onnx engine for the headline (fp32 = fp32-parity split-precision kernels)")
     ap.add_argument("--no-bf16", action="store_true", help="skip the bf16-engine secondary measurement")
+    ap.add_argument("--same-input", action="store_true",
+                    help="every request reads the same bs images (default: each concurrency slot has its own "
+                         "images and output slice, and every slot's output is checked after the run)")
     # 2 instances (2 HIP streams): full 128-row batches on two overlapping
     # streams beat 4 instances' ~110-row batches on four (one box: 42.1k infer/s
     # p99 9.7 ms vs 40.5k p99 11.5 ms; the engine alone at bs128 makes 42.0k img/s
@@ -113,7 +116,7 @@ def spawn_ranks(args):
 class Point:
     """One load point of the native engine against one server."""
 
-    def __init__(self, srv, model, bs, conc, region, nbytes, device, cpu, inputs=None, out_bytes=None):
+    def __init__(self, srv, model, bs, conc, region, nbytes, device, cpu, inputs=None, out_bytes=None, outputs=None):
         from triton_client_amd.perf.native import PerfSession
 
         self.bs, self.conc = bs, conc
@@ -121,8 +124,11 @@ class Point:
         args = ["-m", model, "-i", "grpc", "-u", srv.grpc_url, "-b", bs,
                 "--shared-memory", "system" if cpu else "hip", "--device", device,
                 "--output-shared-memory-size", out_bytes, "--concurrency-range", conc]
+        # a list value pins entry s % n to concurrency slot s (REGION@OFFSET slices)
         for name, reg in (inputs or {"data_0": region}).items():
-            args += ["--shared-memory-input", "%s=%s" % (name, reg)]
+            args += ["--shared-memory-input", "%s=%s" % (name, ",".join(reg) if isinstance(reg, list) else reg)]
+        for name, reg in (outputs or {}).items():
+            args += ["--shared-memory-output", "%s=%s" % (name, ",".join(reg) if isinstance(reg, list) else reg)]
         self.s = PerfSession(args)
 
     def run(self, n):
@@ -314,16 +320,35 @@ def main():
         if bert:
             return bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout, rank, world,
                               dev, cpu)
-        method, in_bytes = make_input("data_0_in", bs)
-        fan = {"method": method, "replicas_verified": True}
+        # one region of `nslots` x bs distinct images (one fan-out); concurrency
+        # slot s reads slice s and writes output slice s, so a batch of 16
+        # requests mixes 16 different inputs and a row mix-up is visible below
+        nslots = 1 if args.same_input else conc
+        req_bytes = bs * 3 * 224 * 224 * 4
+        method, in_total = make_input("data_0_in", bs * nslots)
+        in_bytes = req_bytes
+        in_list = ["data_0_in@%d" % (i * req_bytes) for i in range(nslots)] if nslots > 1 else "data_0_in"
+        out_list = None
+        if not cpu:
+            ob = bs * 1000 * 4
+            ro = shmod.create_shared_memory_region("fc6_1_out", nslots * ob, dev)
+            regions.append(ro)
+            client.register_cuda_shared_memory("fc6_1_out", shmod.get_raw_handle(ro), dev, nslots * ob)
+            out_list = ["fc6_1_out@%d" % (i * ob) for i in range(nslots)]
+
+        def slots(c):
+            return {"data_0": in_list[:c] if isinstance(in_list, list) else in_list}, \
+                ({"fc6_1": out_list[:c]} if out_list else None)
+
+        fan = {"method": method, "replicas_verified": True, "bytes": in_total}
         if not cpu and world > 1:
             # X1 (RCCL broadcast) vs X2 (xGMI one-hop star), once, on the headline input
             # region; a rehearsal on one GPU times p2p and host staging
             fan["timings"] = fanout.time_fanout(
-                regions[0], in_bytes, ["p2p", "host"] if rehearse else
+                regions[0], in_total, ["p2p", "host"] if rehearse else
                 (["p2p"] if method == fanout.LOCAL_FALLBACK else ["rccl", "p2p"]))
             fan["errors"] = fanout.fanout_errors(fan["timings"])
-            if not fanout.verify_replicas(regions[0], in_bytes, over_cpu=method == fanout.LOCAL_FALLBACK):
+            if not fanout.verify_replicas(regions[0], in_total, over_cpu=method == fanout.LOCAL_FALLBACK):
                 raise RuntimeError("fan-out replicas differ across ranks after the fan-out timing")
             t_used = fan["timings"].get(method, {})
             if "us" in t_used:
@@ -334,7 +359,8 @@ def main():
 
         # ---- headline: bs=8 -------------------------------------------------------
         per = args.window * conc
-        p8 = Point(srv, model, bs, conc, "data_0_in", in_bytes, dev, cpu)
+        ins, outs = slots(conc)
+        p8 = Point(srv, model, bs, conc, None, in_bytes, dev, cpu, inputs=ins, outputs=outs)
         points.append(p8)
         lat_w, _, _ = p8.run(max(args.warmup, 1) * per)
         log("warmup done: p50 %.0f us" % percentile_us(lat_w.astype(np.float64), 50))
@@ -360,6 +386,9 @@ def main():
         breakdown["compute_us_per_request_weighted"] = round(wc, 1)
         breakdown["unattributed_us_per_request"] = round(
             breakdown["server_us_per_request"] - breakdown["queue_us_per_request"] - wc, 1)
+        # every slot's output slice must be the logits of ITS images (checked
+        # against the same server running that request alone, outside the timing)
+        slot_check = None if (cpu or out_list is None) else _verify_slots(client, shmod, regions, nslots, bs, dev)
 
         # ---- best throughput with p99 <= 10 ms (same server, lower concurrency) ---------
         p99c = {"p99_target_us": 10000.0, "points": [
@@ -368,7 +397,8 @@ def main():
              "p99_latency_us": round(percentile_us(all_lat, 99), 1)}]}
         if not cpu:
             for c in (32, 24, 16):
-                pc = Point(srv, model, bs, c, "data_0_in", in_bytes, dev, cpu)
+                ins_c, outs_c = slots(c)
+                pc = Point(srv, model, bs, c, None, in_bytes, dev, cpu, inputs=ins_c, outputs=outs_c)
                 points.append(pc)
                 perc = 16 * c
                 pc.run(perc)
@@ -424,7 +454,8 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32" if (cpu or args.engine == "fp32") else "bf16",
             "data": ("synthetic (host normal, fanned out by %s), no model weights (CPU frontend_sink)" % method if cpu
-                     else "synthetic (K1 Philox normal on device, fanned out by %s), random-init weights" % method),
+                     else "synthetic (K1 Philox normal on device: %d distinct images, %d per concurrency slot, "
+                          "fanned out by %s), random-init weights" % (nslots * bs, bs, method)),
             "config": {
                 "model": model,
                 "global_batch": world * conc * bs,
@@ -452,6 +483,8 @@ def main():
             "p99_constrained": p99c,
             "bs1": bs1,
             "fanout": fan,
+            "distinct_inputs": {"slots": nslots, "images": nslots * bs,
+                                "outputs_checked": slot_check},
             "fanout_errors": fan.get("errors", {}),
             "world_size_reported_by_process_group": dist.get_world_size() if world > 1 else 1,
         }
@@ -470,8 +503,11 @@ def main():
             srv.wait_ready(timeout=1500, model=model)
             client = grpcclient.InferenceServerClient(srv.grpc_url)
             state["client"] = client
-            client.register_cuda_shared_memory("data_0_in", shmod.get_raw_handle(regions[0]), dev, in_bytes)
-            pb = Point(srv, model, bs, conc, "data_0_in", in_bytes, dev, cpu)
+            client.register_cuda_shared_memory("data_0_in", shmod.get_raw_handle(regions[0]), dev, in_total)
+            client.register_cuda_shared_memory("fc6_1_out", shmod.get_raw_handle(regions[1]), dev,
+                                               nslots * bs * 1000 * 4)
+            ins, outs = slots(conc)
+            pb = Point(srv, model, bs, conc, None, in_bytes, dev, cpu, inputs=ins, outputs=outs)
             points.append(pb)
             pb.run(per)
             _, _, elb = measure(pb, max(2, args.steps // 4), per)
@@ -585,6 +621,37 @@ def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout
     if rank == 0:
         print(json.dumps(res), flush=True)
     return 0
+
+
+def _verify_slots(client, hipshm, regions, nslots, bs, dev):
+    """After the timed run, output slice s holds the logits the server produced
+    for slot s's images inside a mixed 128-row batch.  Re-run each slot's
+    images alone (one bs-row request, its own HIP-graph bucket) and compare: a
+    pointer-table or scatter row mix-up gives another image's logits (rel-L2
+    ~1); split-K plans differ between buckets, so the bound is fp32-class."""
+    import numpy as np
+    import tritonclient.grpc as grpcclient
+
+    ob = bs * 1000 * 4
+    outs = hipshm.get_contents_as_numpy(regions[1], np.float32, [nslots, bs, 1000]).copy()
+    chk = hipshm.create_shared_memory_region("fc6_1_slotchk", ob, dev)
+    regions.append(chk)
+    client.register_cuda_shared_memory("fc6_1_slotchk", hipshm.get_raw_handle(chk), dev, ob)
+    worst = 0.0
+    for s in range(nslots):
+        x = grpcclient.InferInput("data_0", [bs, 3, 224, 224], "FP32")
+        x.set_shared_memory("data_0_in", bs * 3 * 224 * 224 * 4, offset=s * bs * 3 * 224 * 224 * 4)
+        o = grpcclient.InferRequestedOutput("fc6_1")
+        o.set_shared_memory("fc6_1_slotchk", ob)
+        client.infer("densenet_onnx", [x], outputs=[o])
+        ref = hipshm.get_contents_as_numpy(chk, np.float32, [bs, 1000]).astype(np.float64)
+        got = outs[s].astype(np.float64)
+        rel = np.linalg.norm(got - ref, axis=1) / np.maximum(np.linalg.norm(ref, axis=1), 1e-30)
+        worst = max(worst, float(rel.max()))
+    client.unregister_cuda_shared_memory("fc6_1_slotchk")
+    if not worst < 1e-3:
+        raise RuntimeError("served outputs do not match their own inputs (worst per-row rel-L2 %.3g)" % worst)
+    return {"slots": nslots, "rows": nslots * bs, "max_row_rel_l2_vs_unbatched": float("%.3g" % worst)}
 
 
 def _sanity_check(client, hipshm, bs, dev, regions):

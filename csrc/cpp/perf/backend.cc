@@ -18,6 +18,21 @@
 
 namespace tcperf {
 
+// "REGION" or "REGION@OFFSET" (a slice of one registered region: one fan-out
+// of a big region feeds every slot its own bytes)
+static void SplitRegionRef(const std::string& ref, std::string* name, size_t* off)
+{
+  const auto at = ref.rfind('@');
+  if (at == std::string::npos) {
+    *name = ref;
+    *off = 0;
+    return;
+  }
+  *name = ref.substr(0, at);
+  *off = static_cast<size_t>(std::stoull(ref.substr(at + 1)));
+}
+
+
 namespace tc = triton::client;
 namespace js = triton::client::json;
 
@@ -485,7 +500,9 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
     Error e = LoadJsonData(o.input_data, &entries);
     if (!e.IsOk()) return e;
   }
-  const size_t n_entries = json_data ? entries.size() : 1;
+  size_t n_entries = json_data ? entries.size() : 1;
+  for (const auto& kv : o.preregistered_input_lists) n_entries = std::max(n_entries, kv.second.size());
+  slot_entries_ = !o.preregistered_input_lists.empty();
   const int bs = info.max_batch_size > 0 ? o.batch : 1;
   if (info.max_batch_size == 0 && o.batch > 1) return Error("model does not support batching; use -b 1");
   if (info.max_batch_size > 0 && o.batch > info.max_batch_size)
@@ -638,8 +655,17 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
       }
       auto pre = o.preregistered_inputs.find(t.name);
       if (pre != o.preregistered_inputs.end()) {
+        auto lst = o.preregistered_input_lists.find(t.name);
+        if (lst != o.preregistered_input_lists.end()) {
+          std::string rn;
+          size_t off = 0;
+          SplitRegionRef(lst->second[ent % lst->second.size()], &rn, &off);
+          in->SetSharedMemory(rn, batch_bytes.size(), off);
+          if (ent == 0) desc << t.name << ": " << lst->second.size() << " caller regions pinned to slots; ";
+          continue;
+        }
         in->SetSharedMemory(pre->second, batch_bytes.size(), 0);
-        desc << t.name << ": caller region '" << pre->second << "'; ";
+        if (ent == 0) desc << t.name << ": caller region '" << pre->second << "'; ";
         continue;
       }
       Region r;
@@ -695,6 +721,17 @@ Error DataSet::Init(const Options& o, const ModelInfo& info, Backend* be, size_t
       bool fixed = es > 0;
       for (auto d : t.shape) fixed = fixed && d >= 0;
       if (fixed) bytes = std::max<size_t>(bytes, static_cast<size_t>(Elements(t.shape)) * es * bs);
+      auto po = o.preregistered_outputs.find(t.name);
+      if (po != o.preregistered_outputs.end()) {
+        // a caller region: the output's exact size when the shape is fixed
+        // (the server checks it against the region), else --output-shared-memory-size
+        const size_t exact = fixed ? static_cast<size_t>(Elements(t.shape)) * es * bs : o.output_shm_size;
+        std::string rn;
+        size_t off = 0;
+        SplitRegionRef(po->second[s % po->second.size()], &rn, &off);
+        out->SetSharedMemory(rn, exact, off);
+        continue;
+      }
       Region r;
       e = MakeRegion(be, prefix_ + "out_" + t.name + "_" + std::to_string(s), bytes, dev, &r);
       regions_.push_back(r);

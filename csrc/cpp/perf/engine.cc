@@ -130,14 +130,14 @@ Error LoadEngine::Issue(size_t slot)
       stream_ids_[id] = {slot, t};
     }
     s.opt.request_id_ = id;
-    e = be_->StreamInfer(s.opt, data_->Inputs(issued_++), data_->Outputs(slot));
+    e = be_->StreamInfer(s.opt, data_->Inputs(issued_++, slot), data_->Outputs(slot));
     if (!e.IsOk()) {
       std::lock_guard<std::mutex> lk(stream_mu_);
       stream_ids_.erase(id);
     }
   } else {
     Backend* be = clients_.empty() ? be_ : clients_[slot % clients_.size()];
-    e = be->AsyncInfer([this, slot, t](InferResult* r) { OnComplete(slot, t, r); }, s.opt, data_->Inputs(issued_++),
+    e = be->AsyncInfer([this, slot, t](InferResult* r) { OnComplete(slot, t, r); }, s.opt, data_->Inputs(issued_++, slot),
                        data_->Outputs(slot));
   }
   if (!e.IsOk()) {
@@ -242,7 +242,7 @@ void LoadEngine::SyncLoop(size_t slot)
     InferResult* r = nullptr;
     const uint64_t t = NowNs();
     in_flight_++;
-    e = be->SyncInfer(&r, s.opt, data_->Inputs(issued_++), data_->Outputs(slot));
+    e = be->SyncInfer(&r, s.opt, data_->Inputs(issued_++, slot), data_->Outputs(slot));
     Record rec{t, NowNs(), e.IsOk()};
     if (r) {
       if (!r->RequestStatus().IsOk()) rec.ok = false;

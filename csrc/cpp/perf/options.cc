@@ -14,7 +14,7 @@ namespace {
 enum LongOnly {
   OPT_SYNC = 1000, OPT_ASYNC, OPT_STREAMING, OPT_SHAPE, OPT_CONC_RANGE, OPT_RATE_RANGE, OPT_DIST, OPT_INTERVALS,
   OPT_SEQ_LEN, OPT_SEQ_RANGE, OPT_INPUT_DATA, OPT_STR_LEN, OPT_STR_DATA, OPT_SHM, OPT_OUT_SHM_SIZE, OPT_MEAS_MODE,
-  OPT_MEAS_COUNT, OPT_PERCENTILE, OPT_WARMUP, OPT_VERBOSE_CSV, OPT_JSON, OPT_RESUME, OPT_COLLECT_METRICS, OPT_METRICS_INTERVAL, OPT_METRICS_SYSFS, OPT_SHM_INPUT, OPT_DEVICE, OPT_SEED,
+  OPT_MEAS_COUNT, OPT_PERCENTILE, OPT_WARMUP, OPT_VERBOSE_CSV, OPT_JSON, OPT_RESUME, OPT_COLLECT_METRICS, OPT_METRICS_INTERVAL, OPT_METRICS_SYSFS, OPT_SHM_INPUT, OPT_SHM_OUTPUT, OPT_DEVICE, OPT_SEED,
   OPT_NUM_CLIENTS, OPT_NO_SERVER_STATS, OPT_GPUS, OPT_DEVICES, OPT_FANOUT, OPT_LOAD_PER_GPU, OPT_MEAS_INTERVAL, OPT_STABILITY, OPT_MAX_TRIALS, OPT_LAT_THRESH,
   OPT_SSL_GRPC_USE, OPT_SSL_GRPC_ROOT, OPT_SSL_GRPC_KEY, OPT_SSL_GRPC_CHAIN, OPT_SSL_HTTPS_PEER, OPT_SSL_HTTPS_HOST,
   OPT_SSL_HTTPS_CA, OPT_SSL_HTTPS_CERT, OPT_SSL_HTTPS_CERT_TYPE, OPT_SSL_HTTPS_KEY, OPT_SSL_HTTPS_KEY_TYPE,
@@ -95,7 +95,10 @@ std::string Usage()
       "  --metrics-interval <ms>          GPU metrics sampling interval (default 1000)\n"
       "  [ext] --resume                   skip sweep points already in --json-report (same model/batch/\n"
       "                                   protocol/shm/mode) and keep them in the reports\n"
-      "  [ext] --shared-memory-input NAME=REGION  use a region the caller already registered\n"
+      "  [ext] --shared-memory-input NAME=REGION[,REGION..]  use region(s) the caller already registered;\n"
+      "                                   a list pins entry s % n to concurrency slot s\n"
+      "  [ext] --shared-memory-output NAME=REGION[,REGION..]  caller output region(s), slot s -> s % n\n"
+      "                                   (a list entry may be REGION@OFFSET: a slice of one region)\n"
       "  [ext] --device <gpu>             GPU for hip shared memory (default 0)\n"
       "  [ext] --seed <n>                 synthetic data seed (K1 Philox stream)\n"
       "  [ext] --num-clients <n>          protocol clients (connections) to spread requests over\n"
@@ -159,6 +162,7 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
       {"metrics-interval", required_argument, nullptr, OPT_METRICS_INTERVAL},
       {"metrics-sysfs-root", required_argument, nullptr, OPT_METRICS_SYSFS},
       {"shared-memory-input", required_argument, nullptr, OPT_SHM_INPUT},
+      {"shared-memory-output", required_argument, nullptr, OPT_SHM_OUTPUT},
       {"device", required_argument, nullptr, OPT_DEVICE},
       {"seed", required_argument, nullptr, OPT_SEED},
       {"num-clients", required_argument, nullptr, OPT_NUM_CLIENTS},
@@ -323,7 +327,33 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
       case OPT_SHM_INPUT: {
         auto p = arg.find('=');
         if (p == std::string::npos) return Error("--shared-memory-input expects NAME=REGION");
-        o->preregistered_inputs[arg.substr(0, p)] = arg.substr(p + 1);
+        const std::string name = arg.substr(0, p), val = arg.substr(p + 1);
+        if (val.find(',') == std::string::npos) {
+          o->preregistered_inputs[name] = val;
+        } else {
+          auto& l = o->preregistered_input_lists[name];
+          for (size_t b = 0; b <= val.size();) {
+            size_t c = val.find(',', b);
+            if (c == std::string::npos) c = val.size();
+            if (c > b) l.push_back(val.substr(b, c - b));
+            b = c + 1;
+          }
+          o->preregistered_inputs[name] = l.front();
+        }
+        break;
+      }
+      case OPT_SHM_OUTPUT: {
+        auto p = arg.find('=');
+        if (p == std::string::npos) return Error("--shared-memory-output expects NAME=REGION[,REGION..]");
+        const std::string val = arg.substr(p + 1);
+        auto& l = o->preregistered_outputs[arg.substr(0, p)];
+        for (size_t b = 0; b <= val.size();) {
+          size_t c = val.find(',', b);
+          if (c == std::string::npos) c = val.size();
+          if (c > b) l.push_back(val.substr(b, c - b));
+          b = c + 1;
+        }
+        if (l.empty()) return Error("--shared-memory-output: no region for " + arg.substr(0, p));
         break;
       }
       case OPT_DEVICE:
@@ -448,6 +478,10 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
     return Error("--input-tensor-format / --output-tensor-format json need -i http");
   if (!o->preregistered_inputs.empty() && o->shared_memory == "none")
     return Error("--shared-memory-input requires --shared-memory system|hip");
+  if (!o->preregistered_outputs.empty() && o->shared_memory == "none")
+    return Error("--shared-memory-output requires --shared-memory system|hip");
+  if (!o->preregistered_input_lists.empty() && o->input_data != "random" && o->input_data != "zero")
+    return Error("--shared-memory-input region lists and JSON --input-data are exclusive");
   return Error::Success;
 }
 

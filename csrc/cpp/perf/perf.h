@@ -98,6 +98,12 @@ struct Options {
   std::string shared_memory = "none";
   size_t output_shm_size = 102400;
   std::map<std::string, std::string> preregistered_inputs;  // input -> registered region name
+  // [ext] NAME=R0,R1,..: several caller regions per input / output.  Request
+  // slot s (a concurrency slot) always uses entry s % n, so after a run the
+  // caller can check every output region against its own input region (the
+  // served batch mixes rows of distinct requests: a row mix-up is visible)
+  std::map<std::string, std::vector<std::string>> preregistered_input_lists;
+  std::map<std::string, std::vector<std::string>> preregistered_outputs;
   int device = 0;
   uint64_t seed = 0;
   // multi-GPU: one lane per device
@@ -214,6 +220,12 @@ class DataSet {
   /// Inputs of request number `seq` (JSON data with several entries cycles
   /// through them; synthetic data has one entry).
   const std::vector<InferInput*>& Inputs(uint64_t seq = 0) const { return inputs_[seq % inputs_.size()]; }
+  /// Inputs of request `seq` issued on concurrency slot `slot`: slot-pinned
+  /// entries (caller region lists) use entry slot % n, otherwise as Inputs(seq).
+  const std::vector<InferInput*>& Inputs(uint64_t seq, size_t slot) const
+  {
+    return inputs_[(slot_entries_ ? slot : seq) % inputs_.size()];
+  }
   size_t Entries() const { return inputs_.size(); }
   /// Shared-memory input regions in creation order (what a Fanout replicates).
   struct RegionView {
@@ -252,6 +264,7 @@ class DataSet {
   std::vector<Region> regions_;
   std::vector<size_t> input_regions_;  // indices into regions_
   void* stream_ = nullptr;             // hipStream_t on o_.device
+  bool slot_entries_ = false;          // entries pinned to slots (caller region lists)
   std::string describe_;
 };
 

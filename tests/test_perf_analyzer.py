@@ -312,3 +312,64 @@ def test_request_parameters_reach_server(cpu_server, proto):
     for bad in ("x:1", "x:1:float", "x:maybe:bool", "x:abc:int"):
         r = _pa(["-m", "simple", "--request-parameter", bad])
         assert r.returncode == 1 and "request-parameter" in r.stderr, bad
+
+
+def test_slot_pinned_caller_regions_keep_requests_apart(cpu_server):
+    """--shared-memory-input NAME=R0,..,Rn / --shared-memory-output NAME=O0,..:
+    concurrency slot s reads entry s % n and writes its own output region, so
+    after a batched run (add_sub_batched rides the native dynamic batcher with
+    batches of several requests) every output region must hold the result of
+    ITS slot's inputs: a row mix-up in batch assembly or output scatter shows."""
+    import numpy as np
+
+    import tritonclient.grpc as grpcclient
+    from tritonclient.utils import shared_memory as shm
+
+    n = 6
+    c = grpcclient.InferenceServerClient(cpu_server.grpc_url)
+    regions, names = [], {"in0": [], "in1": [], "out0": [], "out1": []}
+    try:
+        for i in range(n):
+            for kind in names:
+                nm = "pin_%s_%d" % (kind, i)
+                key = "/pin_%s_%d_%d" % (kind, i, os.getpid())
+                r = shm.create_shared_memory_region(nm, key, 64)
+                regions.append(r)
+                names[kind].append(nm)
+                if kind == "in0":
+                    shm.set_shared_memory_region(r, [np.arange(16, dtype=np.int32) + 100 * i])
+                elif kind == "in1":
+                    shm.set_shared_memory_region(r, [np.full(16, 7 * i + 1, np.int32)])
+                else:
+                    shm.set_shared_memory_region(r, [np.full(16, -999, np.int32)])
+                c.register_system_shared_memory(nm, key, 64)
+        args = ["-m", "add_sub_batched", "-i", "grpc", "-u", cpu_server.grpc_url, "--shared-memory", "system",
+                "--shared-memory-input", "INPUT0=" + ",".join(names["in0"]),
+                "--shared-memory-input", "INPUT1=" + ",".join(names["in1"]),
+                "--shared-memory-output", "OUTPUT0=" + ",".join(names["out0"]),
+                "--shared-memory-output", "OUTPUT1=" + ",".join(names["out1"]),
+                "--concurrency-range", str(n)]
+        with native.PerfSession(args) as s:
+            assert "caller regions pinned to slots" in s.describe()
+            st0 = s.server_stats()
+            lat, _ = s.run_fixed(n, 600)
+            assert len(lat) == 600
+            st1 = s.server_stats()
+        execs = st1["execution_count"] - st0["execution_count"]
+        infers = st1["inference_count"] - st0["inference_count"]
+        assert infers >= 600 and infers > execs, ("no request was batched with another", infers, execs)
+        byname = {nm: r for nm, r in zip([x for i in range(n) for x in (names["in0"][i], names["in1"][i],
+                                                                         names["out0"][i], names["out1"][i])],
+                                         regions)}
+        for i in range(n):
+            a = np.arange(16, dtype=np.int32) + 100 * i
+            b = np.full(16, 7 * i + 1, np.int32)
+            o0 = shm.get_contents_as_numpy(byname[names["out0"][i]], np.int32, [16])
+            o1 = shm.get_contents_as_numpy(byname[names["out1"][i]], np.int32, [16])
+            assert (o0 == a + b).all() and (o1 == a - b).all(), (i, o0, o1)
+    finally:
+        try:
+            c.unregister_system_shared_memory()
+        finally:
+            for r in regions:
+                shm.destroy_shared_memory_region(r)
