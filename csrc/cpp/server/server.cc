@@ -33,6 +33,7 @@
 #include "json.h"
 #include "net.h"
 #include "tcserve.h"
+#include "batch_policy.h"
 #include "trace.h"
 
 namespace tcserve {
@@ -1896,65 +1897,49 @@ void Server::Worker(std::shared_ptr<NativeModel> m, int instance)
       std::unique_lock<std::mutex> lk(m->mu);
       m->cv.wait(lk, [&] { return m->stopping || !m->q.empty(); });
       if (m->stopping) return;
-      const int cap = m->max_batch > 0 ? m->max_batch : 1;
-      // Triton dynamic-batcher semantics: a batch of the largest preferred
-      // size dispatches at once; otherwise wait up to the queue delay for a
-      // full batch.  Whatever is queued then goes out, capped at the largest
-      // preferred size that fits (so pipelined instances keep alternating).
-      // Idle-aware: the delay only buys batching while another instance
-      // keeps the GPU busy; with every instance idle the queue goes out now
-      // (a lone request never waits out the delay on an idle GPU).
-      const int pref_max = m->preferred.empty() ? cap : std::min(cap, m->preferred.back());
-      if (m->max_batch > 0 && m->delay_ns > 0) {
-        const uint64_t deadline = m->q.front()->t_arrive + m->delay_ns;
-        // pipelined dispatch (per model, opt-in): with an instance free and as
-        // many rows queued as the last batch carried, waiting out the delay
-        // cannot build a bigger batch in a closed loop; go now.  densenet_onnx
-        // bs1 at concurrency 64 on 2 instances: 18.0-18.4k -> 19.9-22.1k
-        // infer/s, p50 3.3 -> 2.4 ms; its headline's full batches never reach
-        // this rule.  Off for bert_large, where it locked concurrency 16 into
-        // small batches (profiles/r3_instances.md).
-        while (!m->stopping && m->q_rows < pref_max) {
-          if (m->idle_dispatch && m->busy == 0) break;
-          if (m->pipelined && m->busy < m->instances && m->last_rows > 0 && m->q_rows >= m->last_rows) break;
-          const uint64_t now = NowNs();
-          if (now >= deadline) break;
-          m->cv.wait_for(lk, std::chrono::nanoseconds(deadline - now));
-          if (m->q.empty()) break;
-        }
-        if (m->stopping) return;
-        if (m->q.empty()) continue;
-      }
-      // Staggered dispatch: with another instance busy, a batch starts no
-      // sooner than 1/instances of a batch's execution time after the previous
-      // start, so closed-loop load settles into instances offset by a fraction
-      // of a batch instead of starting together (which leaves the next batch
-      // waiting a whole execution: bimodal latency).  densenet_onnx headline,
-      // 2 instances: p99 9.1-12.2 ms -> 9.1-9.2 ms on three runs each, same or
-      // higher throughput (profiles/r3_instances.md).  TCSERVE_STAGGER=0: off.
+      // dispatch policy (batch_policy.h): re-evaluated after every wake-up
+      // until it says go.  The rules and their measured effects:
+      //   * pipelined dispatch (per model, opt-in): densenet_onnx bs1 at
+      //     concurrency 64 on 2 instances: 18.0-18.4k -> 19.9-22.1k infer/s, p50
+      //     3.3 -> 2.4 ms; its headline's full batches never reach this rule.
+      //     Off for bert_large, where it locked concurrency 16 into small
+      //     batches (profiles/r3_instances.md);
+      //   * staggered dispatch of full batches (TCSERVE_STAGGER=0: off):
+      //     densenet_onnx headline, 2 instances: p99 9.1-12.2 ms -> 9.1-9.2 ms
+      //     on three runs each, same or higher throughput (r3_instances.md).
       static const bool stagger = [] {
         const char* e = getenv("TCSERVE_STAGGER");
         return !e || atoi(e) != 0;
       }();
-      // (only for full batches: under light load a partial batch goes out as
-      // before, so a second request never waits out half an execution)
-      if (stagger && m->instances > 1 && m->busy > 0 && m->ema_exec_ns > 0 && m->q_rows >= pref_max) {
-        const uint64_t earliest = m->last_start_ns + static_cast<uint64_t>(m->ema_exec_ns / m->instances);
-        while (!m->stopping && m->busy > 0) {
-          const uint64_t now = NowNs();
-          if (now >= earliest) break;
-          m->cv.wait_for(lk, std::chrono::nanoseconds(earliest - now));
-        }
-        if (m->stopping) return;
-        if (m->q.empty()) continue;
-      }
-      m->last_start_ns = NowNs();
-      int limit = cap;
-      for (auto it = m->preferred.rbegin(); it != m->preferred.rend(); ++it)
-        if (*it <= m->q_rows && *it <= cap) {
-          limit = *it;
+      tcserve::BatchPolicyConfig pc;
+      pc.max_batch = m->max_batch;
+      pc.delay_ns = m->delay_ns;
+      pc.preferred = m->preferred;
+      pc.idle_dispatch = m->idle_dispatch;
+      pc.pipelined = m->pipelined;
+      pc.stagger = stagger;
+      pc.instances = m->instances;
+      bool go = false;
+      while (!m->stopping && !m->q.empty()) {
+        tcserve::BatchPolicyState st;
+        st.now_ns = NowNs();
+        st.front_arrive_ns = m->q.front()->t_arrive;
+        st.q_rows = m->q_rows;
+        st.busy = m->busy;
+        st.last_rows = m->last_rows;
+        st.ema_exec_ns = m->ema_exec_ns;
+        st.last_start_ns = m->last_start_ns;
+        const uint64_t until = tcserve::WaitUntil(pc, st);
+        if (!until) {
+          go = true;
           break;
         }
+        m->cv.wait_for(lk, std::chrono::nanoseconds(until - st.now_ns));
+      }
+      if (m->stopping) return;
+      if (!go) continue;  // another worker emptied the queue
+      m->last_start_ns = NowNs();
+      const int limit = tcserve::TakeLimit(pc, m->q_rows);
       int rows = 0;
       while (!m->q.empty() && (rows == 0 || rows + m->q.front()->rows <= limit)) {
         rows += m->q.front()->rows;
@@ -2278,6 +2263,96 @@ int32_t tcserve_set_idle_dispatch(void* server, const char* name, int32_t on)
   m->idle_dispatch = (on & 1) != 0;  // bit 0: idle-aware dispatch
   m->pipelined = (on & 2) != 0;      // bit 1: pipelined dispatch of partial batches
   return 0;
+}
+
+int32_t tcserve_batch_policy_sim(int32_t max_batch, uint64_t delay_ns, const int32_t* preferred, int32_t n_pref,
+                                 int32_t instances, int32_t flags, const uint64_t* arrive_ns, const int32_t* rows,
+                                 int32_t n, uint64_t exec_base_ns, uint64_t exec_per_row_ns, uint64_t* out_start_ns,
+                                 int32_t* out_rows, int32_t* out_first, int32_t* out_instance, int32_t max_batches)
+{
+  if (instances < 1 || n < 0 || n_pref < 0 || (n && (!arrive_ns || !rows)) || (n_pref && !preferred)) return -1;
+  tcserve::BatchPolicyConfig pc;
+  pc.max_batch = max_batch;
+  pc.delay_ns = delay_ns;
+  for (int32_t i = 0; i < n_pref; ++i)
+    if (preferred[i] > 0) pc.preferred.push_back(preferred[i]);
+  std::sort(pc.preferred.begin(), pc.preferred.end());
+  pc.idle_dispatch = flags & 1;
+  pc.pipelined = (flags & 2) != 0;
+  pc.stagger = (flags & 4) != 0;
+  pc.instances = instances;
+  const int cap = pc.Cap();
+  for (int32_t i = 0; i < n; ++i)
+    if (rows[i] < 1 || rows[i] > cap || (i && arrive_ns[i] < arrive_ns[i - 1])) return -1;
+  std::deque<int32_t> q;
+  int q_rows = 0, busy = 0, last_rows = 0, nb = 0;
+  double ema = 0;
+  uint64_t last_start = 0, t = n ? arrive_ns[0] : 0;
+  std::vector<uint64_t> free_at(instances, 0);  // 0 = idle
+  std::vector<uint64_t> started(instances, 0);
+  int32_t next = 0, done = 0;
+  while (done < n) {
+    // completions at or before t, then arrivals at or before t
+    for (int i = 0; i < instances; ++i)
+      if (free_at[i] && free_at[i] <= t) {
+        const double d = static_cast<double>(free_at[i] - started[i]);
+        ema = ema > 0 ? 0.9 * ema + 0.1 * d : d;
+        free_at[i] = 0;
+        busy--;
+      }
+    while (next < n && arrive_ns[next] <= t) {
+      q.push_back(next);
+      q_rows += rows[next++];
+    }
+    uint64_t timer = UINT64_MAX;
+    while (!q.empty()) {
+      int idle = -1;
+      for (int i = 0; i < instances && idle < 0; ++i)
+        if (!free_at[i]) idle = i;
+      if (idle < 0) break;
+      tcserve::BatchPolicyState st;
+      st.now_ns = t;
+      st.front_arrive_ns = arrive_ns[q.front()];
+      st.q_rows = q_rows;
+      st.busy = busy;
+      st.last_rows = last_rows;
+      st.ema_exec_ns = ema;
+      st.last_start_ns = last_start;
+      const uint64_t until = tcserve::WaitUntil(pc, st);
+      if (until) {
+        timer = until;
+        break;
+      }
+      const int limit = tcserve::TakeLimit(pc, q_rows);
+      int r = 0;
+      const int32_t first = q.front();
+      while (!q.empty() && (r == 0 || r + rows[q.front()] <= limit)) {
+        r += rows[q.front()];
+        q_rows -= rows[q.front()];
+        q.pop_front();
+        done++;
+      }
+      if (nb >= max_batches) return -2;
+      out_start_ns[nb] = t;
+      out_rows[nb] = r;
+      out_first[nb] = first;
+      out_instance[nb] = idle;
+      nb++;
+      last_rows = r;
+      last_start = t;
+      started[idle] = t;
+      free_at[idle] = t + exec_base_ns + exec_per_row_ns * static_cast<uint64_t>(r);
+      busy++;
+    }
+    if (done >= n) break;
+    uint64_t nt = timer;
+    if (next < n) nt = std::min(nt, arrive_ns[next]);
+    for (int i = 0; i < instances; ++i)
+      if (free_at[i]) nt = std::min(nt, free_at[i]);
+    if (nt == UINT64_MAX) return -1;  // cannot happen: a queued request always has a deadline or a free instance
+    t = std::max(t, nt);
+  }
+  return nb;
 }
 
 int32_t tcserve_set_preferred(void* server, const char* name, const int32_t* sizes, int32_t n)

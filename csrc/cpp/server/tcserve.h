@@ -64,6 +64,18 @@ int32_t tcserve_remove_model(void* server, const char* name);
 int32_t tcserve_set_idle_dispatch(void* server, const char* name, int32_t on);
 /// dynamic_batching.preferred_batch_size for a registered model (n = 0 clears).
 int32_t tcserve_set_preferred(void* server, const char* name, const int32_t* sizes, int32_t n);
+/// Discrete-event simulation of the native batcher's dispatch policy
+/// (batch_policy.h, the functions Server::Worker runs) over scripted
+/// arrivals: request i arrives at arrive_ns[i] (non-decreasing) with rows[i]
+/// rows; a batch of r rows executes for exec_base_ns + r * exec_per_row_ns on
+/// one of `instances` instances.  flags: bit 0 idle-aware, bit 1 pipelined,
+/// bit 2 staggered.  Writes per batch its start time, rows, first request and
+/// instance; returns the batch count (-1 on bad arguments, -2 if max_batches
+/// was too small).
+int32_t tcserve_batch_policy_sim(int32_t max_batch, uint64_t delay_ns, const int32_t* preferred, int32_t n_pref,
+                                 int32_t instances, int32_t flags, const uint64_t* arrive_ns, const int32_t* rows,
+                                 int32_t n, uint64_t exec_base_ns, uint64_t exec_per_row_ns, uint64_t* out_start_ns,
+                                 int32_t* out_rows, int32_t* out_first, int32_t* out_instance, int32_t max_batches);
 /// Mirror of the Python shared-memory registries; kind 0 = system (ptr = host mapping), 1 = device.
 int32_t tcserve_shm_add(void* server, const char* name, int32_t kind, uint64_t ptr, uint64_t bytes, int32_t device);
 /// Unregister (name "" = all of kind).  Never blocks: returns how many of the removed regions

@@ -1609,6 +1609,320 @@ x3_dense_fused4_kernel(X3FusedParams p) {
 }
 
 // ============================================================================
+// K14x: the whole dense layer in one kernel for the 14x14 and 7x7 blocks
+// ============================================================================
+// K11x's ring needs W >= 16; at 14x14 / 7x7 the K8x + K9x pair ran every
+// layer as two launches with z (hi|lo, 512 B a pixel) written to HBM and read
+// back (40 of the 58 dense layers, 36% of a bs128 forward).  Here one block
+// owns one TILE of whole image rows and keeps z on chip:
+//
+//   14x14: tile = half an image (output rows 0-6 or 7-13) plus the one halo
+//          row the 3x3 needs from the other half: z over 8 rows = 112 pixels,
+//          98 outputs.  Both halves of an image go to blocks b and b+8, which
+//          the dispatcher places on one XCD (blockIdx % 8 labels the XCD), so
+//          the halo rows' second read is an L2 hit.
+//    7x7:  tile = one whole image (49 pixels; no halo).
+//
+//   1x1 (K -> 128, BN1+ReLU prologue, BN2-folded bias+ReLU epilogue): the K8x
+//   ws pipeline on ONE tile of <= 128 rows: producer waves 4-7 keep PF K steps
+//   of X in flight in registers and stage each step split hi/lo into LDS, W
+//   slices go by LDS-DMA, consumer waves 0-3 run the 32x32x16 MFMAs (2 x 2
+//   blocks of the 128 x 128 tile each); one raw s_barrier per K step.
+//   The epilogue writes z into a zero-PADDED image of the tile in LDS
+//   ([rows+2][W+2] pixels x 512 B, 16-B chunks XOR-swizzled by pixel) that
+//   aliases the drained K-step stages, so every 3x3 tap is one constant
+//   offset from the output pixel: no bounds tests in the tap loop.
+//   3x3 (128 -> 32): all 8 waves as K11x v1 (input-channel quarter x output
+//   half, 16x16x32 MFMAs, weights resident: x3_w3f_fragments), the 4 partials
+//   summed through an LDS scratch, fp32 stores of the layer's 32 channels.
+//
+// HBM per layer: the input X once (+ the halo rows through L2) and 32 output
+// channels; one launch.  LDS: 4 K-step stages (128 KB), then z + scratch.
+constexpr int kSmS = 4;
+constexpr int kLdsSm = kSmS * kWsStage;  // 128 KB (z and the 3x3 scratch alias it once the 1x1 drained)
+
+struct X3SmallParams {
+  const float* x;  // block buffer rows of ldx (the layer's first K channels)
+  const float* s1;  // [K] BN1 affine
+  const float* t1;
+  const uint16_t* w1_hi;  // [128][K] bf16 (BN2 folded, K8x layout)
+  const uint16_t* w1_lo;
+  const float* b1;        // [128] BN2 shift
+  const uint16_t* w2_hi;  // [tap 9][kq 4][oh 2][lane 64][8] bf16 (x3_w3f_fragments)
+  const uint16_t* w2_lo;
+  float* y;               // [pixels][ldy] fp32, offset to the layer's 32-channel slice
+  int ldx, K, ldy, imgs;
+  int dbg;                // ablation (TCAMD_X3_SMALLF_DBG): 1 = no 3x3 phase
+};
+
+// W = image side (14: half-image tiles, 7: whole images); PF = X K-steps in
+// the producers' registers
+template <int W, int PF>
+__global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p) {
+  constexpr int kHalves = W == 14 ? 2 : 1;
+  constexpr int kRowsOut = W / kHalves;              // 7
+  constexpr int kPW = W + 2, kPR = kRowsOut + 2;     // padded tile image
+  constexpr int kNPad = kPR * kPW;
+  constexpr int kPOut = kRowsOut * W;                // 98 / 49 outputs
+  constexpr int kNPG = (kPOut + 15) / 16;            // 16-pixel groups of the 3x3
+  constexpr int kTRMax = (kRowsOut + kHalves) * W;   // z pixels: 112 / 49
+  constexpr int kNRI = (kTRMax + 31) / 32;           // producer row passes (32 rows each)
+  constexpr int kOps = 4 + 2 + kNRI;                 // vm ops per producer iteration
+  static_assert(kTRMax <= 128, "one 1x1 tile");
+  static_assert(kNPad * kRowB + 2 * 4 * 3 * kNPG * 64 * 4 <= kLdsSm, "K14x LDS budget");
+  extern __shared__ __attribute__((aligned(16))) uint8_t ldss[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  // tile: the two halves of image 8g+j are blocks 16g+j and 16g+8+j (one XCD)
+  int img, half;
+  if constexpr (kHalves == 2) {
+    const int g = blockIdx.x >> 4, r = blockIdx.x & 15;
+    half = r >> 3;
+    img = 8 * g + (r & 7);
+  } else {
+    img = blockIdx.x;
+    half = 0;
+  }
+  if (img >= p.imgs) return;  // block-uniform, before any barrier
+  const int r0 = half * kRowsOut;
+  const int zr0 = max(r0 - 1, 0), zr1 = min(r0 + kRowsOut + 1, W);
+  const int TR = (zr1 - zr0) * W;  // z rows of the tile
+  const int mz0 = img * W * W + zr0 * W;
+  const int nst = p.K / kBK;
+  const int Q = nst, Qp = (Q + PF - 1) / PF * PF;
+  f32x16 acc[2][2];  // consumers: [channel block][pixel block] of the 128 x 128 1x1 tile
+  const int wm = wave & 1, wn = (wave >> 1) & 1;
+  const int col = lane & 31, h = lane >> 5;
+
+  if (wave >= 4) {
+    // ------------------------------ producer (K8x ws) ------------------------------
+    const int pt = tid - 256, pw = wave - 4;
+    const int pj = pt & 7, prow = pt >> 3;
+    const ptrdiff_t lo_off = p.w1_lo - p.w1_hi;
+    f32x4 xr[PF][kNRI], xs[PF], xt[PF];
+    const int rot = (int)(blockIdx.x % (unsigned)nst);  // blocks read different K offsets at a time
+    auto kofs = [&](int ks) { ks += rot; return (ks >= nst ? ks - nst : ks) * kBK; };
+    auto issue_x = [&](int q, int slot) {
+      q = min(q, Q - 1);
+      const int k0 = kofs(q);
+      xs[slot] = ldf4(p.s1 + k0 + 4 * pj);
+      xt[slot] = ldf4(p.t1 + k0 + 4 * pj);
+#pragma unroll
+      for (int i = 0; i < kNRI; ++i) {
+        const int m = mz0 + min(prow + 32 * i, TR - 1);
+        xr[slot][i] = ldf4(p.x + (size_t)m * p.ldx + k0 + 4 * pj);
+      }
+    };
+    auto issue_w = [&](int q) {
+      q = min(q, Q - 1);
+      const int k0 = kofs(q);
+      uint8_t* st = ldss + (q % kSmS) * kWsStage + 2 * kWsPlane;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ii = 4 * pw + i, plane = ii >> 3, rb = ii & 7;
+        const int row = 16 * rb + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 3);
+        const uint16_t* src = p.w1_hi + (plane ? lo_off : 0) + (size_t)row * p.K + k0 + 8 * c;
+        __builtin_amdgcn_global_load_lds((const void*)src, (void*)(st + plane * kWsPlane + rb * 1024), 16, 0, 0);
+      }
+    };
+    auto write_x = [&](int q, int slot) {
+      uint8_t* st = ldss + (q % kSmS) * kWsStage;
+      const f32x4 sc = xs[slot], sb = xt[slot];
+#pragma unroll
+      for (int i = 0; i < kNRI; ++i) {
+        const int row = prow + 32 * i;
+        const bool ok = row < TR;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = ok ? fmaxf(xr[slot][i][e] * sc[e] + sb[e], 0.f) : 0.f;
+        v2u h, l;
+        split4(v, h, l);
+        const int off = ws_chunk(row, pj >> 1) + (pj & 1) * 8;
+        *reinterpret_cast<v2u*>(st + off) = h;
+        *reinterpret_cast<v2u*>(st + kWsPlane + off) = l;
+      }
+    };
+#pragma unroll
+    for (int s = 0; s < PF; ++s) issue_x(s, s);
+    for (int s = 0; s <= kSmS - 3; ++s) issue_w(s);
+    __builtin_amdgcn_s_waitcnt(ws_vmcnt(0));
+    write_x(0, 0);
+    issue_w(kSmS - 2);
+    __builtin_amdgcn_sched_barrier(0);
+    issue_x(PF, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ws_barrier();  // B0
+    for (int q0 = 0; q0 < Qp; q0 += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int q = q0 + u;
+        const int slot = (u + 1) % PF;
+        __builtin_amdgcn_s_waitcnt(ws_vmcnt(kOps * (PF - 1)));  // X of step q+1
+        __builtin_amdgcn_sched_barrier(0);
+        write_x(q + 1, slot);
+        issue_w(q + kSmS - 1);
+        __builtin_amdgcn_sched_barrier(0);  // W copies ahead of the X loads (vmcnt retires in order)
+        issue_x(q + 1 + PF, slot);
+        __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0((2 + kNRI) + kOps * (kSmS - 2)));  // W of step q+1
+        ws_barrier();  // B(q+1)
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stages are z's memory next
+  } else {
+    // ------------------------------- consumer -------------------------------
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+    const int rv = TR - 64 * wm;  // valid z rows from this wave's first
+    ws_barrier();  // B0
+    for (int q = 0; q < Qp; ++q) {
+      if (q >= Q) {
+        ws_barrier();
+        continue;
+      }
+      const uint8_t* st = ldss + (q % kSmS) * kWsStage;
+      if (rv > 0) {
+        v4u ah[2][2], al[2][2], bh[2][2], bl[2][2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int xo = ws_chunk(64 * wm + 32 * b + col, 2 * kk + h);
+            const int wo = ws_chunk(64 * wn + 32 * b + col, 2 * kk + h);
+            bh[kk][b] = ld16(st + xo);
+            bl[kk][b] = ld16(st + kWsPlane + xo);
+            ah[kk][b] = ld16(st + 2 * kWsPlane + wo);
+            al[kk][b] = ld16(st + 3 * kWsPlane + wo);
+          }
+        if (rv > 32) {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+              for (int b = 0; b < 2; ++b) acc[a][b] = x3_32(ah[kk][a], al[kk][a], bh[kk][b], bl[kk][b], acc[a][b]);
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int a = 0; a < 2; ++a) acc[a][0] = x3_32(ah[kk][a], al[kk][a], bh[kk][0], bl[kk][0], acc[a][0]);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      ws_barrier();  // B(q+1): stage q is free
+    }
+  }
+  // 3x3 weights: in flight while the LDS changes hands and z is written
+  const int kq = wave & 3, oh = wave >> 2;
+  v4u w2h[kTaps], w2l[kTaps];
+#pragma unroll
+  for (int t = 0; t < kTaps; ++t) {
+    const size_t off = ((size_t)((t * 4 + kq) * 2 + oh) * 64 + lane) * 8;
+    w2h[t] = ld16(p.w2_hi + off);
+    w2l[t] = ld16(p.w2_lo + off);
+  }
+  __syncthreads();  // Bz: every DMA and stage read retired; the LDS holds z from here
+  // zero the padding of the tile image (columns 0 and W+1, rows outside the image)
+  for (int i = tid; i < kNPad * 32; i += 512) {
+    const int pos = i >> 5, piece = i & 31;
+    const int prr = pos / kPW, pc = pos - prr * kPW;
+    const int ir = r0 - 1 + prr;
+    if (pc == 0 || pc == kPW - 1 || ir < zr0 || ir >= zr1)
+      *reinterpret_cast<v4u*>(ldss + pos * kRowB + piece * 16) = v4u{0, 0, 0, 0};
+  }
+  if (wave < 4) {
+    // 1x1 epilogue: + bias, ReLU, hi/lo split into the padded tile image.
+    // C (32x32): lane col = pixel, reg 4g+e -> channel 64wn + 32a + 8g + 4h + e
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int pz = 64 * wm + 32 * b + col;  // z pixel of the tile
+      if (pz < TR) {
+        const int zy = pz / W, zx = pz - zy * W;
+        const int pos = (zr0 + zy - r0 + 1) * kPW + zx + 1;
+        uint8_t* rp = ldss + pos * kRowB + 8 * h;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 bb = ldf4(p.b1 + 64 * wn + 32 * a + 8 * g + 4 * h);
+            f32x4 r;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) r[e] = fmaxf(acc[a][b][4 * g + e] + bb[e], 0.f);
+            v2u hh, ll;
+            split4(r, hh, ll);
+            uint8_t* q = rp + (((8 * wn + 4 * a + g) ^ (pos & 15)) << 4);
+            *reinterpret_cast<v2u*>(q) = hh;
+            *reinterpret_cast<v2u*>(q + 256) = ll;
+          }
+      }
+    }
+  }
+
+  // ---- 3x3 phase: 8 waves = input-channel quarter kq x output half oh ----
+  __syncthreads();  // z and its padding complete
+  if (p.dbg & 1) return;
+  int base[kNPG];
+#pragma unroll
+  for (int pg = 0; pg < kNPG; ++pg) {
+    const int o = 16 * pg + (lane & 15);
+    const int yy = o / W, xx = o - (o / W) * W;
+    // padded (yy, xx) is tap (0, 0) of output (yy, xx); lanes past the tile
+    // read from pixel 0 (in bounds; their columns are never stored)
+    base[pg] = o < kPOut ? yy * kPW + xx : 0;
+  }
+  f32x4 acc3[kNPG];
+#pragma unroll
+  for (int pg = 0; pg < kNPG; ++pg) acc3[pg] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int chunk16 = 4 * kq + (lane >> 4);
+  constexpr int kSteps = kTaps * kNPG;
+  constexpr int kLead = 3;
+  v4u bq[kLead + 1][2];
+  auto rd = [&](int step) {
+    const int t = step / kNPG, pg = step - (step / kNPG) * kNPG;
+    const int pos = base[pg] + (t / 3) * kPW + (t % 3);
+    const uint8_t* q = ldss + pos * kRowB + (((chunk16 ^ (pos & 15))) << 4);
+    bq[step % (kLead + 1)][0] = ld16(q);
+    bq[step % (kLead + 1)][1] = ld16(q + 256);
+  };
+#pragma unroll
+  for (int step = 0; step < kLead; ++step) rd(step);
+#pragma unroll
+  for (int step = 0; step < kSteps; ++step) {
+    if (step + kLead < kSteps) rd(step + kLead);
+    __builtin_amdgcn_sched_barrier(0);
+    const int t = step / kNPG, pg = step - (step / kNPG) * kNPG;
+    acc3[pg] = x3_16(w2h[t], w2l[t], bq[step % (kLead + 1)][0], bq[step % (kLead + 1)][1], acc3[pg]);
+  }
+  // C (16x16): lane (lane&15) = pixel of group pg, reg e -> channel 16oh + 4c + e
+  // (c = lane>>4); wave (kq = c, oh) owns those 4 channels and adds the other
+  // three waves' partials
+  float* scr = reinterpret_cast<float*>(ldss + kNPad * kRowB);
+  const int c4 = lane >> 4;
+  constexpr int kSlot = kNPG * 64;
+  if (c4 != kq) {
+    float* sw = scr + ((oh * 4 + c4) * 3 + (kq - c4 + 3) % 4) * kSlot + (lane & 15) * 4;
+#pragma unroll
+    for (int pg = 0; pg < kNPG; ++pg) *reinterpret_cast<f32x4*>(sw + pg * 64) = acc3[pg];
+  }
+  __syncthreads();
+  if (c4 == kq) {
+    const float* sr = scr + (oh * 4 + kq) * 3 * kSlot + (lane & 15) * 4;
+    const int m0 = img * W * W + r0 * W;
+#pragma unroll
+    for (int pg = 0; pg < kNPG; ++pg) {
+      f32x4 v = acc3[pg];
+#pragma unroll
+      for (int src = 0; src < 3; ++src) v += *reinterpret_cast<const f32x4*>(sr + src * kSlot + pg * 64);
+      const int o = 16 * pg + (lane & 15);
+      if (o < kPOut) *reinterpret_cast<f32x4*>(p.y + (size_t)(m0 + o) * p.ldy + 16 * oh + 4 * kq) = v;
+    }
+  }
+}
+
+// ============================================================================
 // K10x stem: y = relu(maxpool3x3/2(conv7x7/2(x)) + b), 3 -> 64 channels, fp32
 // ============================================================================
 // As K10s in densenet.hip (patch staged once per block, conv as an implicit
@@ -2318,6 +2632,59 @@ int tcamd_x3_dense_fused4(const float* x, int ldx, int imgs, int H, int W, int K
                           const void* w1_hi, const void* w1_lo, const float* b1, const void* w2_hi,
                           const void* w2_lo, float* y, int ldy, void* stream) {
   return x3_dense_fused_impl(2, x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream);
+}
+
+
+// K14x: one dense layer of the 14x14 (half-image tiles) or 7x7 (whole-image
+// tiles) block in one kernel; w1 in the K8x [128][K] layout, w2 in
+// x3_w3f_fragments.  K a multiple of 32 (>= 64).
+int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K, const float* s1, const float* t1,
+                         const void* w1_hi, const void* w1_lo, const float* b1, const void* w2_hi, const void* w2_lo,
+                         float* y, int ldy, void* stream) {
+  if (imgs <= 0) return hipSuccess;
+  if ((W != 14 && W != 7) || H != W || K < 64 || K % 32 || ldx < K || ldx % 4 || ldy % 4)
+    return hipErrorInvalidValue;
+  if (!x || !s1 || !t1 || !w1_hi || !w1_lo || !b1 || !w2_hi || !w2_lo || !y) return hipErrorInvalidValue;
+  if (!aligned16(x) || !aligned16(s1) || !aligned16(t1) || !aligned16(w1_hi) || !aligned16(w1_lo) ||
+      !aligned16(b1) || !aligned16(w2_hi) || !aligned16(w2_lo) || !aligned16(y))
+    return hipErrorInvalidValue;
+  if ((size_t)imgs * H * W >= (1u << 30) / 4) return hipErrorInvalidValue;
+  X3SmallParams p;
+  p.x = x;
+  p.s1 = s1;
+  p.t1 = t1;
+  p.w1_hi = (const uint16_t*)w1_hi;
+  p.w1_lo = (const uint16_t*)w1_lo;
+  p.b1 = b1;
+  p.w2_hi = (const uint16_t*)w2_hi;
+  p.w2_lo = (const uint16_t*)w2_lo;
+  p.y = y;
+  p.ldx = ldx;
+  p.K = K;
+  p.ldy = ldy;
+  p.imgs = imgs;
+  static const int dbg = getenv("TCAMD_X3_SMALLF_DBG") ? atoi(getenv("TCAMD_X3_SMALLF_DBG")) : 0;
+  p.dbg = dbg;
+  // X steps in flight in the producers' registers (TCAMD_X3_SMALLF_PF 3 or 6, A/B runs)
+  static const int pf = getenv("TCAMD_X3_SMALLF_PF") ? atoi(getenv("TCAMD_X3_SMALLF_PF")) : 3;
+  const void* const fns[2][2] = {{(const void*)x3_dense_small_kernel<14, 3>, (const void*)x3_dense_small_kernel<14, 6>},
+                                 {(const void*)x3_dense_small_kernel<7, 3>, (const void*)x3_dense_small_kernel<7, 6>}};
+  static std::atomic<bool> attr_set[kMaxDevices];
+  const int dev_slot = device_slot();
+  if (!attr_set[dev_slot].load(std::memory_order_acquire)) {
+    for (const auto& r : fns)
+      for (const void* f : r) {
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsSm);
+        if (e != hipSuccess) return e;
+      }
+    attr_set[dev_slot].store(true, std::memory_order_release);
+  }
+  const int blocks = W == 14 ? (imgs + 7) / 8 * 16 : imgs;
+  void* args[] = {&p};
+  const hipError_t e = hipLaunchKernel(fns[W == 14 ? 0 : 1][pf == 6 ? 1 : 0], dim3(blocks), dim3(512), args, kLdsSm,
+                                       (hipStream_t)stream);
+  if (e != hipSuccess) return e;
+  return hipGetLastError();
 }
 
 static int cu_count() {

@@ -311,6 +311,65 @@ def test_x3_dense_fused(imgs, H, K, version):
     assert _rel(x[:, K:K + 32], y2[:, K:K + 32]) < 2e-5
 
 
+@pytest.mark.parametrize("imgs,H,K", [(1, 14, 64), (3, 14, 256), (8, 14, 288), (9, 14, 992), (17, 14, 640),
+                                      (128, 14, 512), (16, 14, 96), (1, 7, 512), (5, 7, 992), (64, 7, 768),
+                                      (130, 7, 544), (2, 7, 64), (40, 14, 416)])
+def test_x3_dense_small(imgs, H, K):
+    """K14x: the whole dense layer of a 14x14 (half-image tiles with a halo
+    row) or 7x7 (whole-image tiles) block in one kernel, z in a zero-padded
+    LDS image of the tile.  Ragged image counts (not multiples of 8: the 14x14
+    grid pairs the halves of images 8g+j), K from 64 to 992 (2..31 K steps,
+    every padding-round count of both producer depths) and a layer slice in
+    the middle of a wider block buffer.  Against fp64 torch (< 3e-5), and
+    against the two-kernel path on the same split products."""
+    _need_gpu()
+    hip = _hip()
+    g = torch.Generator(device=DEV).manual_seed(imgs * 131 + H * 7 + K)
+    M, ldx = imgs * H * H, K + 96
+    x = torch.randn(M, ldx, device=DEV, generator=g)
+    s = torch.rand(K, device=DEV, generator=g) + 0.5
+    t = torch.randn(K, device=DEV, generator=g) * 0.2
+    w1 = torch.randn(128, K, device=DEV, generator=g) / K ** 0.5
+    b1 = torch.randn(128, device=DEV, generator=g) * 0.1
+    w2 = torch.randn(32, 128, 3, 3, device=DEV, generator=g) / (9 * 128) ** 0.5
+    w1h, w1l = _split(w1)
+    w2p = _split(w2.permute(0, 2, 3, 1).reshape(32, -1))
+    f2h, f2l = (hip.x3_w3f_fragments(u) for u in w2p)
+    xc = x.clone()
+    hip.x3_dense_small(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), w1h.data_ptr(), w1l.data_ptr(),
+                       b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), x.data_ptr() + 4 * K, ldx, stream=_st())
+    torch.cuda.synchronize()
+    a = torch.relu(xc[:, :K].double() * s.double() + t.double())
+    z = torch.relu(a @ w1.double().t() + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
+    ref = F.conv2d(z, w2.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 32)
+    err = _rel(x[:, K:K + 32], ref)
+    # per image too: a tile written to the wrong image / half shows even when the total is close
+    per_img = ((x[:, K:K + 32].double() - ref).reshape(imgs, -1).norm(dim=1) / ref.reshape(imgs, -1).norm(dim=1))
+    print("K14x imgs %d H %d K %d: rel %.3g, worst image %.3g" % (imgs, H, K, err, per_img.max().item()))
+    assert err < 3e-5 and per_img.max().item() < 1e-4
+    assert torch.equal(x[:, :K], xc[:, :K]) and torch.equal(x[:, K + 32:], xc[:, K + 32:])
+    y2 = xc.clone()
+    w2h, w2l = (hip.x3_w3_fragments(u) for u in w2p)
+    zh = torch.empty(M, 128, device=DEV, dtype=torch.bfloat16)
+    zl = torch.empty_like(zh)
+    hip.x3_dense_layer(y2.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), w1h.data_ptr(),
+                       w1l.data_ptr(), b1.data_ptr(), zh.data_ptr(), zl.data_ptr(), w2h.data_ptr(), w2l.data_ptr(),
+                       y2.data_ptr() + 4 * K, ldx, stream=_st())
+    torch.cuda.synchronize()
+    assert _rel(x[:, K:K + 32], y2[:, K:K + 32]) < 2e-5
+
+
+def test_x3_dense_small_rejects_bad_shapes():
+    _need_gpu()
+    hip = _hip()
+    x = torch.zeros(2 * 196, 320, device=DEV)
+    w = torch.zeros(128 * 256, device=DEV)
+    for H, W, K in [(28, 28, 256), (14, 7, 256), (14, 14, 250), (14, 14, 32)]:
+        with pytest.raises(Exception):
+            hip.x3_dense_small(x.data_ptr(), 320, 2, H, W, K, w.data_ptr(), w.data_ptr(), w.data_ptr(), w.data_ptr(),
+                               w.data_ptr(), w.data_ptr(), w.data_ptr(), x.data_ptr() + 4 * K, 320, stream=_st())
+
+
 @pytest.mark.parametrize("imgs", [3, 20])  # 20: more tiles than the persistent grid (several per block)
 def test_x3_stem(imgs):
     _need_gpu()

@@ -123,6 +123,16 @@ def main():
                              "-r", "3", "-s", "80"]),
         ("perf gRPC sync x4 clients", [pa, "-m", "simple", "-i", "grpc", "-u", grpc, "--sync", "--concurrency-range",
                                        "4", "-p", "300", "-r", "3", "-s", "80"]),
+        # the threaded batcher's rules (2 instances, dynamic batching, preferred
+        # 8, staggered full batches, idle-aware and pipelined partial batches)
+        ("perf batcher rules gRPC c64", [pa, "-m", "add_sub_pipelined", "-i", "grpc", "-u", grpc,
+                                         "--concurrency-range", "64", "-p", "500", "-r", "3", "-s", "80"]),
+        ("perf batcher rules gRPC c1..8", [pa, "-m", "add_sub_pipelined", "-i", "grpc", "-u", grpc,
+                                           "--concurrency-range", "1:8:3", "-p", "300", "-r", "3", "-s", "80"]),
+        ("perf batcher rules HTTP c64", [pa, "-m", "add_sub_pipelined", "-i", "http", "-u", http,
+                                         "--concurrency-range", "64", "-p", "500", "-r", "3", "-s", "80"]),
+        ("perf batcher rules shm c32", [pa, "-m", "add_sub_pipelined", "-i", "grpc", "-u", grpc, "--shared-memory",
+                                        "system", "--concurrency-range", "32", "-p", "400", "-r", "3", "-s", "80"]),
     ]
     for ex in ("simple_http_infer_client", "simple_grpc_infer_client", "simple_http_shm_client",
                "simple_grpc_shm_client", "simple_grpc_async_infer_client", "simple_http_async_infer_client",
@@ -170,7 +180,7 @@ def main():
                 reports.append((os.path.basename(f), blk[:3000]))
             else:
                 foreign += 1
-    lines = ["# tcserve under %s (round 2)" % a.preset.upper(), "",
+    lines = ["# tcserve under %s" % a.preset.upper(), "",
              "`tools/sanitize_tcserve.py --preset %s`: the instrumented `libtcserve.so` (`make -C csrc/cpp %s`) "
              "loaded by the Python test server (runtime preloaded, leak checker off: Python is not instrumented), "
              "driven by the native clients and hostile HTTP inputs." % (a.preset, a.preset), "",

@@ -24,6 +24,9 @@ Network walk (same as :class:`densenet_fused.FusedDenseNet`, fp32 activations):
                         produced into the 3x3's LDS ring (never in HBM)
                         or, small M (<= 3136 pixels, W <= 63): the K13x chain,
                         one launch per layer (csrc/kernels/densenet_x3s.hip)
+                        or (14x14 / 7x7 blocks at big batches): K14x, one
+                        launch per layer over half-image / whole-image tiles,
+                        z in a zero-padded LDS image of the tile
    -> per transition:   K8x conv1x1 with BN+ReLU+2x2 avg-pool prologue
                         -> next block buffer ch[0 : C/2] (fp32)
    -> K10x head: relu(BN5(x)) global average -> [b,1024] fp32
@@ -128,6 +131,10 @@ class FusedDenseNetFP32:
         self.use_chain = os.environ.get("TCAMD_X3_CHAIN", "1") != "0"
         self.chain_m = int(os.environ.get("TCAMD_X3_CHAIN_M", "3136"))
         self.chain_after_fused = os.environ.get("TCAMD_X3_CHAIN_AFTER_FUSED", "0") != "0"
+        # K14x (whole dense layer in one kernel at 14x14 / 7x7) once it has at
+        # least this many blocks (a 14x14 image is two blocks, a 7x7 image one);
+        # 0 disables it
+        self.smallf_min_blocks = int(os.environ.get("TCAMD_X3_SMALLF_MIN_BLOCKS", "128"))
         self._alloc(max_batch)
 
     def _alloc(self, n):
@@ -212,6 +219,14 @@ class FusedDenseNetFP32:
             fused = self._fuse(M, hw)
             fmax = self._fuse_max_k(M)
             small = 0 < M <= self.small_m and M <= self.zacc.shape[1]
+            if self._small_fused(b, hw):
+                # K14x: the 14x14 / 7x7 blocks, one launch per layer, z on chip
+                for L in layers:
+                    hip.x3_dense_small(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
+                                       L["w1h"].data_ptr(), L["w1l"].data_ptr(), L["b1"].data_ptr(),
+                                       L["w2fh"].data_ptr(), L["w2fl"].data_ptr(), fp + 4 * L["cin"], ctot, stream=st)
+                self._transition(bi, fp, ctot, b, hw, ws, wsb, st)
+                continue
             ch = self.chain[bi]
             if ch is not None and 0 < M <= ch[2]:
                 # the whole block runs as one chain (at bs1-2 a 28x28 K11x layer
@@ -278,6 +293,11 @@ class FusedDenseNetFP32:
             hip.x3_conv1x1(fp, ctot, b * nhw * nhw, ctot, T["s"].data_ptr(), T["t"].data_ptr(),
                            T["wh"].data_ptr(), T["wl"].data_ptr(), y=self.feat[bi + 1].data_ptr(), ldy=nct,
                            pool=1, H=hw, W=hw, ws=ws, ws_bytes=wsb, stream=st, N=ctot // 2)
+
+    def _small_fused(self, b, hw):
+        if self.smallf_min_blocks <= 0 or hw not in (7, 14):
+            return False
+        return b * (2 if hw == 14 else 1) >= self.smallf_min_blocks
 
     def _fuse_max_k(self, M):
         """Largest K that K11x takes: past 224 only at >= 4 tiles per block, where

@@ -211,6 +211,14 @@ _SIGS = {
         ],
         ctypes.c_int,
     ),
+    "tcamd_x3_dense_small": (
+        [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
     "tcamd_x3_fused_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "tcamd_x3_dense_fused4": (
         [
@@ -732,6 +740,15 @@ def x3_dense_fused(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo
     of 32 in 64..224."""
     _check(_load().tcamd_x3_dense_fused(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
                                         w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_fused")
+
+
+def x3_dense_small(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None):
+    """K14x: one fp32-parity dense layer of the 14x14 (half-image tiles + one
+    halo row) or 7x7 (whole-image tiles) block in ONE kernel, z kept in a
+    zero-padded LDS image of the tile.  ``w1_*`` in the K8x [128][K] layout,
+    ``w2_*`` in x3_w3f_fragments; K a multiple of 32, >= 64."""
+    _check(_load().tcamd_x3_dense_small(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
+                                        w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_small")
 
 
 def x3_dense_fused4(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None):

@@ -310,6 +310,20 @@ class AddSubBatched(Model):
         b.timing_ns[2] = 0
 
 
+class AddSubPipelined(AddSubBatched):
+    """add_sub_batched with every tcserve batcher rule engaged: 2 instances,
+    a preferred batch of 8 rows (full batches -> staggered starts), idle-aware
+    and pipelined dispatch of partial batches.  Exists so the threaded
+    batcher's rules run under the sanitizers (tools/sanitize_tcserve.py) and
+    the CPU tests; the rules themselves are unit-tested on scripted arrivals
+    (tests/test_batch_policy.py)."""
+
+    name = "add_sub_pipelined"
+    dynamic_batching = {"preferred": [8], "max_queue_delay_us": 300, "pipelined": True}
+    instance_count = 2
+    native_delay_s = 0.0002  # each batch holds its instance ~0.2 ms: queues build, rules fire
+
+
 class FrontendSink(Model):
     """densenet_onnx-shaped model that does no compute: FP32 [3,224,224] in,
     FP32 [1000] out (first input value broadcast).  Served natively, it
@@ -408,4 +422,5 @@ CPU_MODELS = [
     RepeatInt32,
     PreprocessInception,
     AddSubBatched,
+    AddSubPipelined,
 ]
