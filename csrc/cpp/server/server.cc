@@ -223,6 +223,63 @@ class Loop {
   std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns_;
 };
 
+// Response compression for the native REST path (Accept-Encoding gzip /
+// deflate).  Deflating a batch's responses inline would hold the batcher
+// thread (the next batch waits behind zlib) and a loop thread would stall
+// every connection on it, so the work goes to this small pool: two threads,
+// started on first use, drained and joined when the server stops.
+class CodecPool {
+ public:
+  ~CodecPool() { Stop(); }
+  void Submit(std::function<void()> f)
+  {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (th_.empty() && !stop_)
+        for (int i = 0; i < 2; ++i)
+          th_.emplace_back([this, i] {
+            pthread_setname_np(pthread_self(), ("tcs-codec" + std::to_string(i)).c_str());
+            Run();
+          });
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+  // runs what is queued, then joins
+  void Stop()
+  {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_)
+      if (t.joinable()) t.join();
+    th_.clear();
+  }
+
+ private:
+  void Run()
+  {
+    while (true) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;  // stopping and drained
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  std::vector<std::thread> th_;
+  bool stop_ = false;
+};
+
 class Server {
  public:
   ~Server();
@@ -265,20 +322,22 @@ class Server {
 
  private:
   bool TryNative(Conn* c, Stream* st, const char* msg, size_t len, std::string* owner);
-  bool TryNativeHttp(Conn* c, uint64_t seq, bool close, const std::string& name, const std::string& version,
-                     std::string* body, size_t json_len, int resp_enc);
-  void ProxyHttp(Conn* c, uint64_t seq, bool close, std::string&& raw);
+  // (any thread: the connection is named by its loop and id)
+  bool TryNativeHttp(Loop* loop, uint64_t conn_id, uint64_t seq, bool close, const std::string& name,
+                     const std::string& version, std::string* body, size_t json_len, int resp_enc);
+  void ProxyHttp(Loop* loop, uint64_t conn_id, uint64_t seq, bool close, std::string&& raw);
   void FailPending(PendingReq* pr, int grpc_status, int http_status, const std::string& msg);
   void Proxy(Conn* c, Stream* st, bool streaming);
   std::shared_ptr<tc::H2Channel> Upstream();
   void Worker(std::shared_ptr<NativeModel> m, int instance);
-  void Execute(NativeModel* m, int instance, std::vector<std::unique_ptr<PendingReq>>& batch);
+  void Execute(const std::shared_ptr<NativeModel>& ms, int instance, std::vector<std::unique_ptr<PendingReq>>& batch);
   static std::string HttpInferResponse(NativeModel* m, PendingReq* pr);
 
   int port_ = 0, http_port_ = 0;
   std::string up_host_, up_http_host_;
   int up_port_ = 0, up_http_port_ = 0;
   std::atomic<int> proxies_{0};  // in-flight HTTP proxy threads
+  CodecPool codec_;              // REST response compression (off the batcher threads)
   std::mutex up_mu_;
   std::vector<std::shared_ptr<tc::H2Channel>> up_;
   std::atomic<uint32_t> up_rr_{0};
@@ -750,6 +809,7 @@ Server::~Server()
     for (auto& t : m->workers)
       if (t.joinable()) t.join();
   }
+  codec_.Stop();  // queued compressed responses still post to the loops
   for (int i = 0; i < 3000 && proxies_.load() > 0; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(1));
   for (auto& l : loops) l->Stop();
   if (!loops.empty() && loops[0]->listen_fd >= 0) close(loops[0]->listen_fd);
@@ -899,6 +959,8 @@ int ParseHead(const std::string& in, HttpHead* h)
 // requests get 413 and the connection is closed.  KServe gRPC messages are
 // capped at INT32_MAX too (reference src/c++/library/common.h:53).
 constexpr uint64_t kMaxHttpBody = 0x7fffffffull;
+// compressed REST bodies at least this large are inflated on the codec pool, not the loop thread
+constexpr size_t kInflateOnLoopMax = 64 * 1024;
 
 // returns bytes consumed, 0 = need more input, -1 = malformed, -2 = too large
 long DecodeChunked(const std::string& in, size_t from, std::string* body)
@@ -1126,16 +1188,45 @@ void Server::OnHttpData(Conn* c)
       // counts the uncompressed JSON header in both directions.
       const int req_enc = ContentCoding(ce);
       const int resp_enc = AcceptCoding(ae);
-      std::string plain;
-      bool ok = req_enc >= 0;
-      if (ok && req_enc > 0) {
-        ok = InflateBounded(body, kMaxHttpBody, &plain);
-        if (ok) n_inflated++;
-      }
-      if (ok) {
-        std::string& b = req_enc > 0 ? plain : body;
-        const size_t jl = strtoull(ihcl->c_str(), nullptr, 10);
-        if (jl <= b.size()) handled = TryNativeHttp(c, seq, close, model, version, &b, jl, resp_enc);
+      const size_t jl = strtoull(ihcl->c_str(), nullptr, 10);
+      if (req_enc > 0 && body.size() >= kInflateOnLoopMax) {
+        // a large compressed body is inflated on the codec pool, not here (a
+        // gzip client would stall every connection of this loop); the pool
+        // thread then takes the native path, or relays the original request
+        std::string head;
+        if (rebuilt) {
+          head = h.method + " " + h.target + " HTTP/1.1\r\n";
+          for (const auto& kv : h.headers)
+            if (kv.first != "transfer-encoding" && kv.first != "content-length")
+              head += kv.first + ": " + kv.second + "\r\n";
+          head += "Content-Length: " + std::to_string(body.size()) + "\r\n\r\n";
+        } else {
+          head.assign(c->hin, 0, h.head_len);
+        }
+        Loop* loop = c->loop;
+        const uint64_t conn_id = c->id;
+        auto zbody = std::make_shared<std::string>(std::move(body));
+        codec_.Submit([this, loop, conn_id, seq, close, model, version, jl, resp_enc, head, zbody] {
+          std::string plain;
+          bool done = false;
+          if (InflateBounded(*zbody, kMaxHttpBody, &plain)) {
+            n_inflated++;
+            if (jl <= plain.size()) done = TryNativeHttp(loop, conn_id, seq, close, model, version, &plain, jl, resp_enc);
+          }
+          if (!done) ProxyHttp(loop, conn_id, seq, close, head + *zbody);
+        });
+        handled = true;
+      } else {
+        std::string plain;
+        bool ok = req_enc >= 0;
+        if (ok && req_enc > 0) {
+          ok = InflateBounded(body, kMaxHttpBody, &plain);
+          if (ok) n_inflated++;
+        }
+        if (ok) {
+          std::string& b = req_enc > 0 ? plain : body;
+          if (jl <= b.size()) handled = TryNativeHttp(c->loop, c->id, seq, close, model, version, &b, jl, resp_enc);
+        }
       }
     }
     if (!handled) {
@@ -1150,13 +1241,13 @@ void Server::OnHttpData(Conn* c)
       } else {
         raw.assign(c->hin, 0, consumed);
       }
-      ProxyHttp(c, seq, close, std::move(raw));
+      ProxyHttp(c->loop, c->id, seq, close, std::move(raw));
     }
     c->hin.erase(0, consumed);
   }
 }
 
-bool Server::TryNativeHttp(Conn* c, uint64_t seq, bool close, const std::string& name, const std::string& version,
+bool Server::TryNativeHttp(Loop* loop, uint64_t conn_id, uint64_t seq, bool close, const std::string& name, const std::string& version,
                            std::string* body, size_t json_len, int resp_enc)
 {
   std::shared_ptr<NativeModel> m;
@@ -1185,8 +1276,8 @@ bool Server::TryNativeHttp(Conn* c, uint64_t seq, bool close, const std::string&
   pr->http_seq = seq;
   pr->http_close = close;
   pr->http_resp_enc = resp_enc;
-  pr->conn_id = c->id;
-  pr->loop = c->loop;
+  pr->conn_id = conn_id;
+  pr->loop = loop;
   pr->stream_id = 0;
   if (const js::Value* id = root.Find("id")) pr->id = id->AsString();
   pr->t_arrive = NowNs();
@@ -1194,7 +1285,7 @@ bool Server::TryNativeHttp(Conn* c, uint64_t seq, bool close, const std::string&
   pr->rows = -1;
   size_t data_off = json_len;
   auto fail = [&](const std::string& msg) {
-    PostHttp(c->loop, c->id, seq, HttpError(400, msg, close), close);
+    PostHttp(loop, conn_id, seq, HttpError(400, msg, close), close);
     std::lock_guard<std::mutex> lk(m->smu);
     m->fail.count++;
     m->fail.ns += NowNs() - pr->t_arrive;
@@ -1459,12 +1550,10 @@ void Server::PostHttp(Loop* loop, uint64_t conn_id, uint64_t seq, std::string&& 
   });
 }
 
-void Server::ProxyHttp(Conn* c, uint64_t seq, bool close, std::string&& raw)
+void Server::ProxyHttp(Loop* loop, uint64_t conn_id, uint64_t seq, bool close, std::string&& raw)
 {
   n_proxied++;
   proxies_++;
-  Loop* loop = c->loop;
-  const uint64_t conn_id = c->id;
   auto req = std::make_shared<std::string>(std::move(raw));
   std::thread([this, loop, conn_id, seq, close, req] {
     std::string resp;
@@ -1952,7 +2041,7 @@ void Server::Worker(std::shared_ptr<NativeModel> m, int instance)
       m->busy++;
     }
     const uint64_t t_exec = NowNs();
-    Execute(m.get(), instance, batch);
+    Execute(m, instance, batch);
     const double d_exec = static_cast<double>(NowNs() - t_exec);
     {
       std::lock_guard<std::mutex> lk(m->mu);
@@ -1963,8 +2052,10 @@ void Server::Worker(std::shared_ptr<NativeModel> m, int instance)
   }
 }
 
-void Server::Execute(NativeModel* m, int instance, std::vector<std::unique_ptr<PendingReq>>& batch)
+void Server::Execute(const std::shared_ptr<NativeModel>& ms, int instance,
+                     std::vector<std::unique_ptr<PendingReq>>& batch)
 {
+  NativeModel* m = ms.get();
   const int n = static_cast<int>(batch.size());
   const size_t ni = m->inputs.size(), no = m->outputs.size();
   std::vector<int32_t> rows(n);
@@ -2032,7 +2123,17 @@ void Server::Execute(NativeModel* m, int instance, std::vector<std::unique_ptr<P
       continue;
     }
     if (pr->http) {
-      if (pr->http_resp_enc) n_deflated++;
+      if (pr->http_resp_enc) {
+        // compressed response: built and deflated on the codec pool (the
+        // request, its host outputs and the model stay alive with the task)
+        n_deflated++;
+        std::shared_ptr<PendingReq> own(pr.release());
+        std::shared_ptr<NativeModel> keep = ms;
+        codec_.Submit([this, own, keep] {
+          PostHttp(own->loop, own->conn_id, own->http_seq, HttpInferResponse(keep.get(), own.get()), own->http_close);
+        });
+        continue;
+      }
       PostHttp(pr->loop, pr->conn_id, pr->http_seq, HttpInferResponse(m, pr.get()), pr->http_close);
       continue;
     }

@@ -60,4 +60,25 @@ int64_t tcamd_host_scan_bytes(const uint8_t* buf, uint64_t nbytes, uint64_t* off
   return (int64_t)n;
 }
 
+// As tcamd_host_scan_bytes over a buffer that may end mid-element (a prefix
+// of a region copied to the host in chunks): stops at the first element that
+// does not fit, returns the complete elements (up to cap) and, in *consumed,
+// the bytes they span.
+int64_t tcamd_host_scan_bytes_prefix(const uint8_t* buf, uint64_t nbytes, uint64_t* offs, uint32_t* lens,
+                                     uint64_t cap, uint64_t* consumed) {
+  uint64_t p = 0;
+  uint64_t n = 0;
+  while (n < cap && p + 4 <= nbytes) {
+    uint32_t L;
+    std::memcpy(&L, buf + p, 4);
+    if (p + 4 + (uint64_t)L > nbytes) break;
+    offs[n] = p + 4;
+    lens[n] = L;
+    p += 4 + (uint64_t)L;
+    ++n;
+  }
+  *consumed = p;
+  return (int64_t)n;
+}
+
 }  // extern "C"

@@ -293,3 +293,27 @@ def test_infer_input_from_device_tensor(hipshm, dt):
     xb = x.to(torch.bfloat16)
     c = httpclient.InferInput("x", [4, 1000], "BF16").set_data_from_dlpack(xb)
     assert c._get_binary_data() == xb.view(torch.int16).cpu().numpy().tobytes()
+
+
+@pytest.mark.parametrize("n,maxlen", [(16, 30), (4000, 40), (5000, 20), (12, 9000)])
+@pytest.mark.parametrize("path", ["host", "device", "auto"])
+def test_bytes_host_and_device_paths_agree(hipshm, n, maxlen, path):
+    """Small BYTES tensors go through the host codec (one copy of the span),
+    large ones through K2 / K3; both directions, both paths, byte-identical
+    region contents and round trips (the crossover: tools/bytes_crossover.py)."""
+    from tritonclient.utils import serialize_byte_tensor
+
+    rng = np.random.default_rng(n + maxlen)
+    data = np.array([bytes(rng.integers(0, 256, int(rng.integers(0, maxlen)), dtype=np.uint8)) for _ in range(n)],
+                    dtype=np.object_)
+    want = serialize_byte_tensor(data).item()
+    h = hipshm.create_shared_memory_region("bp_%s_%d" % (path, n), len(want) + 64, 0)
+    try:
+        hipshm.set_shared_memory_region(h, [data], serialize_bytes=True, bytes_path=path)
+        assert hipshm.get_contents_as_numpy(h, np.uint8, [len(want)]).tobytes() == want
+        back = hipshm.get_contents_as_numpy(h, np.object_, [n], bytes_path=path)
+        assert list(back) == list(data)
+        with pytest.raises(hipshm.CudaSharedMemoryException):
+            hipshm.get_contents_as_numpy(h, np.object_, [n + 17], bytes_path=path)
+    finally:
+        hipshm.destroy_shared_memory_region(h)

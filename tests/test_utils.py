@@ -121,3 +121,46 @@ def test_dlpack_host_view_zero_copy():
     nc = _dlpack.consume(torch.ones(4, 4).t())
     assert not nc.is_contiguous()
     nc.release()
+
+
+@pytest.mark.parametrize("lens", [[0] * 50, [3, 0, 70000, 5], [20] * 5000, [40000, 40000, 1], [1] * 3])
+def test_hip_shm_host_bytes_walk_grows_its_prefix(lens):
+    """The HIP-shm BYTES host path (small tensors) walks the length-prefixed
+    chain over a prefix copied D2H in growing chunks; on CPU the 'device' is a
+    numpy buffer (a fake memcpy_d2h), so every growth case runs here: empty
+    elements, an element longer than the first chunk, exactly n elements."""
+    from tritonclient.utils import hip_shared_memory as hipshm
+    from tritonclient.utils import serialize_byte_tensor
+
+    rng = np.random.default_rng(len(lens))
+    data = np.array([bytes(rng.integers(0, 256, n, dtype=np.uint8)) for n in lens], dtype=np.object_)
+    ser = np.frombuffer(serialize_byte_tensor(data).item(), dtype=np.uint8)
+    dev = np.zeros(ser.size + 300, dtype=np.uint8)  # a region larger than the stream (zeros = empty elements)
+    dev[:ser.size] = ser
+    copies = []
+
+    class FakeHip:
+        @staticmethod
+        def memcpy_d2h(dst, src, nbytes, d):
+            copies.append(nbytes)
+            dst[:nbytes] = dev[src:src + nbytes]
+
+    host, offs, lens_out = hipshm._index_bytes_host(FakeHip, 0, dev.size, len(lens), 0)
+    got = [bytes(host[o:o + n]) for o, n in zip(offs.tolist(), lens_out.tolist())]
+    assert got == list(data)
+    assert sum(copies) <= dev.size  # each byte copied at most once
+    # more elements than the stream holds: the zero tail parses as empty
+    # elements up to the region end, then it is an error
+    with pytest.raises(hipshm.CudaSharedMemoryException):
+        hipshm._index_bytes_host(FakeHip, 0, dev.size, len(lens) + 76, 0)
+    # an element that runs past the region end
+    bad = dev[:ser.size].copy()
+    bad[:4] = np.frombuffer(np.uint32(10 ** 6).tobytes(), np.uint8)
+
+    class BadHip:
+        @staticmethod
+        def memcpy_d2h(dst, src, nbytes, d):
+            dst[:nbytes] = bad[src:src + nbytes]
+
+    with pytest.raises(hipshm.CudaSharedMemoryException, match="past the end"):
+        hipshm._index_bytes_host(BadHip, 0, bad.size, len(lens), 0)

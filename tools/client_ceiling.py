@@ -28,12 +28,13 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def perf(url, proto, model, conc, extra=()):
+def perf(url, proto, model, conc, extra=(), count=None):
     from triton_client_amd.perf import native
 
     j = "/tmp/ceiling_%s_%s_%d.json" % (proto, model, conc)
     cmd = [native.BIN_PATH, "-m", model, "-i", proto, "-u", url, "--concurrency-range", str(conc),
-           "--measurement-mode", "count_windows", "--measurement-request-count", str(max(2000, 40 * conc)),
+           "--measurement-mode", "count_windows", "--measurement-request-count",
+           str(count or max(2000, 40 * conc)),
            "-s", "15", "-r", "6", "--json-report", j, *extra]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     if r.returncode:
@@ -114,6 +115,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default="")
     ap.add_argument("--md", default="")
+    ap.add_argument("--compression-only", action="store_true", help="only the gzip REST points")
     ap.add_argument("--target-req-per-gpu", type=float, default=34455.0 / 8,
                     help="headline request rate one GPU's load generator must sustain (infer/s / bs)")
     a = ap.parse_args()
@@ -124,6 +126,24 @@ def main():
     rows = {"perf_analyzer": {}, "python": {}}
     try:
         srv.wait_ready(timeout=120, model="add_sub_batched")
+        # compressed native REST (gzip both ways, in-band bs8 zero tensors, so
+        # the client's own deflate of 4.8 MB bodies stays cheap): the
+        # responses are deflated on tcserve's codec pool, off the batcher threads
+        for conc in (16, 64):
+            k = "http frontend_sink bs8 in-band gzip c%d" % conc
+            rows["perf_analyzer"][k] = perf(srv.http_url, "http", "frontend_sink", conc,
+                                            ("-b", "8", "--compression-algorithm", "gzip", "--input-data", "zero"),
+                                            count=400)
+            print(k, rows["perf_analyzer"][k], flush=True)
+        for conc in (16, 64):
+            k = "http add_sub_batched gzip c%d" % conc
+            rows["perf_analyzer"][k] = perf(srv.http_url, "http", "add_sub_batched", conc,
+                                            ("--compression-algorithm", "gzip"))
+            print(k, rows["perf_analyzer"][k], flush=True)
+        if a.compression_only:
+            for k, v in rows["perf_analyzer"].items():
+                print(json.dumps({k: v}))
+            return
         for proto, url in (("grpc", srv.grpc_url), ("http", srv.http_url)):
             for conc in (1, 16, 64, 256):
                 k = "%s add_sub_batched c%d" % (proto, conc)

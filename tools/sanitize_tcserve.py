@@ -143,6 +143,19 @@ def main():
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
         rows.append((name, r.returncode))
         print("%-32s rc=%d" % (name, r.returncode), flush=True)
+    # evidence that the batcher-rule drivers formed full (staggered) and
+    # partial (idle / pipelined) batches on both instances
+    batch_hist = {}
+    try:
+        import tritonclient.grpc as grpcclient
+
+        st = grpcclient.InferenceServerClient(grpc).get_inference_statistics("add_sub_pipelined", as_json=True)
+        for m in st.get("model_stats", []):
+            for b in m.get("batch_stats", []):
+                batch_hist[int(b["batch_size"])] = int(b.get("compute_infer", {}).get("count", 0))
+    except Exception as e:  # noqa: BLE001 - reported
+        batch_hist = {"error": str(e)[:200]}
+    print("add_sub_pipelined executions by batch size:", batch_hist, flush=True)
     # malformed / hostile input on the native HTTP port
     probes = [
         ("negative shm byte size", b"POST /v2/models/simple/infer HTTP/1.1\r\nHost: x\r\nContent-Length: 160\r\n\r\n"
@@ -190,6 +203,10 @@ def main():
     lines += ["", "Mapped into the server process (/proc/PID/maps): sanitizer runtime **%s**, instrumented "
               "`%s` **%s**." % (mapped["runtime"], os.path.relpath(lib, REPO), mapped["instrumented libtcserve"]),
               "", "Server alive after all drivers and probes: **%s**." % alive, "",
+              "`add_sub_pipelined` (2 instances, preferred 8, idle-aware + pipelined + staggered dispatch) "
+              "executions by batch rows during the batcher-rule drivers: `%s` (8 = full batches, the staggered "
+              "rule; smaller = partial batches sent by the idle or pipelined rule or the queue delay)." % (
+                  batch_hist,), "",
               "Sanitizer reports with a frame in the instrumented `libtcserve.so`: **%d**." % len(reports),
               "", "Reports entirely inside uninstrumented third-party code (grpcio cygrpc / CPython threads; "
               "their synchronisation is invisible to the sanitizer): %d." % foreign]

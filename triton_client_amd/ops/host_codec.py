@@ -18,6 +18,10 @@ class HostCodec:
             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
         ]
         lib.tcamd_host_scan_bytes.restype = ctypes.c_int64
+        lib.tcamd_host_scan_bytes_prefix.argtypes = [
+            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+        ]
+        lib.tcamd_host_scan_bytes_prefix.restype = ctypes.c_int64
 
     def pack_bytes(self, elems, lens):
         payload = b"".join(elems)
@@ -36,6 +40,16 @@ class HostCodec:
         lens = np.empty(n, dtype=np.uint32)
         self._lib.tcamd_host_scan_bytes(ptr, arr.size, offs.ctypes.data, lens.ctypes.data, n)
         return offs, lens
+
+
+    def scan_prefix(self, arr, offs, lens, cap):
+        """Index up to ``cap`` complete elements of the uint8 array ``arr`` (a
+        prefix of a BYTES stream) into ``offs`` / ``lens``; returns (count,
+        bytes consumed)."""
+        consumed = ctypes.c_uint64(0)
+        n = self._lib.tcamd_host_scan_bytes_prefix(arr.ctypes.data, arr.size, offs.ctypes.data, lens.ctypes.data,
+                                                   cap, ctypes.byref(consumed))
+        return int(n), int(consumed.value)
 
 
 _INSTANCE = None

@@ -37,6 +37,7 @@ multi-element object array is concatenated, like the system-shm module) and an
 """
 
 import base64
+import os
 
 import numpy as np
 
@@ -135,6 +136,58 @@ def _as_bytes(v):
     return v.reshape(-1).view(np.uint8)  # np.bytes_ too: size * itemsize raw bytes
 
 
+# BYTES tensors of at most this many elements are packed / indexed on the
+# host (C++ codec, one H2D or D2H of the span) instead of by K2 / K3 on the
+# device: below the crossover the device path's fixed cost (scratch, three
+# stream syncs, the offsets/lengths copies) dominates.  Measured with
+# tools/bytes_crossover.py (profiles/r4_bytes_crossover.md);
+# TCAMD_BYTES_HOST_MAX overrides, 0 = always the device kernels.
+_BYTES_HOST_MAX = int(os.environ.get("TCAMD_BYTES_HOST_MAX", "4096"))
+
+
+def _bytes_on_host(n, path):
+    if path not in ("auto", "host", "device"):
+        raise CudaSharedMemoryException("bytes_path must be auto, host or device")
+    return path == "host" or (path == "auto" and n <= _BYTES_HOST_MAX)
+
+
+def _index_bytes_host(hip, src, nbytes, n, dev):
+    """Host walk of the ``<u32 len>||bytes`` chain at device ``src`` (the
+    reference's path, tc/utils/cuda_shared_memory/__init__.py:242-325, but on
+    a prefix copied D2H in growing chunks, indexed by the C++ host codec).
+    Returns (host bytes, offsets, lengths)."""
+    from triton_client_amd.ops import host_codec
+
+    codec = host_codec.load()
+    offs = np.empty(n, dtype=np.uint64)
+    lens = np.empty(n, dtype=np.uint32)
+    span = min(nbytes, max(1 << 14, 32 * n))
+    host = np.empty(span, dtype=np.uint8)
+    have = got = pos = 0
+    while True:
+        if have < span:
+            hip.memcpy_d2h(host[have:span], src + have, span - have, dev)
+            have = span
+        k, used = codec.scan_prefix(host[pos:span], offs[got:], lens[got:], n - got)
+        if k:
+            offs[got:got + k] += pos
+        got += k
+        pos += used
+        if got == n:
+            return host, offs, lens
+        if span == nbytes:
+            if pos == nbytes:
+                raise CudaSharedMemoryException("the region holds %d BYTES elements, %d requested" % (got, n))
+            raise CudaSharedMemoryException("BYTES element runs past the end of the region")
+        want = 2 * span
+        if pos + 4 <= span:  # the next element's length is known: fetch at least through it
+            want = max(want, pos + 4 + int(host[pos:pos + 4].view("<u4")[0]))
+        span = min(nbytes, want)
+        grown = np.empty(span, dtype=np.uint8)
+        grown[:have] = host[:have]
+        host = grown
+
+
 _NARROW = {"BF16": None, "FP16": np.float16, "FP8_E4M3": None, "FP8_E5M2": None}
 
 
@@ -203,7 +256,8 @@ def _convert_into(hip, ctx, dst, arr, datatype):
     return out_bytes
 
 
-def set_shared_memory_region(cuda_shm_handle, input_values, offset=0, serialize_bytes=False, datatype=None):
+def set_shared_memory_region(cuda_shm_handle, input_values, offset=0, serialize_bytes=False, datatype=None,
+                             bytes_path="auto"):
     """Copy numpy arrays back-to-back into the region starting at ``offset``.
 
     Reference behaviour (tc/utils/cuda_shared_memory/__init__.py:173-239):
@@ -211,7 +265,9 @@ def set_shared_memory_region(cuda_shm_handle, input_values, offset=0, serialize_
     output of ``serialize_byte_tensor``.  Opt-in device work (MI355X):
 
     * ``serialize_bytes=True``: object / ``np.bytes_`` arrays are UNserialised
-      BYTES tensors; K2 writes the ``<u32 len>||bytes`` stream into the region;
+      BYTES tensors; K2 writes the ``<u32 len>||bytes`` stream into the region
+      (up to ``_BYTES_HOST_MAX`` elements, ``bytes_path="auto"``, the host
+      codec packs them and one H2D copies the stream);
     * ``datatype`` in BF16 / FP16 / FP8_E4M3 / FP8_E5M2: float arrays are
       converted on the GPU (K4/K5; BF16 truncates like serialize_bf16_tensor).
     """
@@ -226,6 +282,7 @@ def set_shared_memory_region(cuda_shm_handle, input_values, offset=0, serialize_
     hip = _hip()
     from triton_client_amd.ops import dtypes
 
+    _bytes_on_host(0, bytes_path)  # validates the argument
     plan = []  # (kind, value, nbytes)
     for v in input_values:
         is_bytes = v.dtype == np.object_ or v.dtype.type == np.bytes_
@@ -253,7 +310,15 @@ def set_shared_memory_region(cuda_shm_handle, input_values, offset=0, serialize_
         with ctx.lock:
             cur = cuda_shm_handle._base_addr + offset
             for kind, b, nb in plan:
-                if kind == "k2":
+                if kind == "k2" and _bytes_on_host(b.size, bytes_path):
+                    from tritonclient.utils import _element_bytes
+                    from triton_client_amd.ops import host_codec
+
+                    el = _element_bytes(np.ascontiguousarray(b))
+                    packed = np.frombuffer(host_codec.load().pack_bytes(el, [len(e) for e in el]), dtype=np.uint8)
+                    hip.memcpy_async(cur, packed.ctypes.data, packed.size, ctx.stream.handle)
+                    ctx.stream.synchronize()  # `packed` must outlive the copy
+                elif kind == "k2":
                     _pack_bytes_on_device(hip, ctx, cur, b)
                 elif kind == "cvt":
                     _convert_into(hip, ctx, cur, b, datatype)
@@ -265,13 +330,16 @@ def set_shared_memory_region(cuda_shm_handle, input_values, offset=0, serialize_
         raise CudaSharedMemoryException("unable to set values in cuda shared memory") from ex
 
 
-def get_contents_as_numpy(cuda_shm_handle, datatype, shape, offset=0, region_datatype=None):
+def get_contents_as_numpy(cuda_shm_handle, datatype, shape, offset=0, region_datatype=None, bytes_path="auto"):
     """Copy region contents back to the host as a numpy array.
 
     Only the requested bytes are copied (the reference copies the whole
     region every call, tc/utils/cuda_shared_memory/__init__.py:266-276).
     BYTES: K3 indexes the ``<u32 len>||bytes`` chain on the device, then only
-    the bytes the elements span come back.  ``region_datatype`` (BF16 / FP16 /
+    the bytes the elements span come back; up to ``_BYTES_HOST_MAX`` elements
+    (``bytes_path="auto"``; or ``"host"`` / ``"device"``) the chain is walked
+    on the host instead, over a prefix copied in growing chunks.
+    ``region_datatype`` (BF16 / FP16 /
     FP8_E4M3 / FP8_E5M2) with a float32 ``datatype``: the region holds that
     narrow type and is widened to float32 on the GPU before the copy.
     """
@@ -325,6 +393,16 @@ def get_contents_as_numpy(cuda_shm_handle, datatype, shape, offset=0, region_dat
     nbytes = size - offset
     out = np.empty(n, dtype=np.object_)
     if n == 0:
+        return out.reshape(shape)
+    if _bytes_on_host(n, bytes_path):
+        try:
+            host, offs, lens = _index_bytes_host(hip, src, nbytes, n, dev)
+        except CudaSharedMemoryException:
+            raise
+        except Exception as ex:
+            raise CudaSharedMemoryException("failed to read cuda shared memory results") from ex
+        mv = memoryview(host)
+        out[:] = [bytes(mv[o:o + ln]) for o, ln in zip(offs.tolist(), lens.tolist())]
         return out.reshape(shape)
     ctx = _ctx(cuda_shm_handle)
     try:
