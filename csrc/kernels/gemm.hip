@@ -1,0 +1,218 @@
+// K15: bf16 projection GEMM with fused epilogues for bert_large (gfx950).
+//
+//   Y[m][n] = epi( sum_k X[m][k] * W[n][k] )      X [M][K], W [N][K] (nn.Linear
+//                                                  layout), Y [M][N], all bf16
+//   epi: 0 plain | 1 + bias[n] | 2 GELU(. + bias[n]) (erf form) |
+//        3 + bias[n] + R[m][n] (residual)
+//
+// The four BERT-large projections per layer (M = tokens): QKV (N 3072, K 1024,
+// plain: K12 applies the bias), attention out (1024, 1024, + bias), FFN up
+// (4096, 1024, bias + GELU), FFN down (1024, 4096, + bias).
+//
+// Block tile 256 x 256 x 64, 8 waves (2 along M x 4 along N), each wave a
+// 128 (m) x 64 (n) sub-tile on 16x16x32 bf16 MFMAs with W as operand A (rows =
+// output channels) and X as operand B (columns = tokens), so a lane's four
+// accumulators are four consecutive output channels of one token: the
+// epilogue stores 8 bytes per lane and reads bias / residual the same way.
+// Operands are staged global -> LDS by LDS-DMA (global_load_lds, 16 B a lane,
+// 8 per thread per K step) into two buffers: the next K step's copies are
+// issued before the current step's LDS reads and MFMAs and retired at the one
+// barrier per step.  The LDS image is lane-linear (the DMA writes base +
+// 16 * lane); rows are 128 B and the 16-B chunk c of row r sits at physical
+// chunk c ^ ((r >> 1) & 7), applied on the global SOURCE address, so the 16
+// lanes of a ds_read_b128 group (16 consecutive rows, one chunk) hit 16
+// distinct slots of the bank rows (conflict-free).
+// Blocks are remapped so each XCD (blockIdx % 8 group) walks a contiguous
+// range of tiles, N fastest: the X row-panel of consecutive tiles stays in
+// that XCD's L2.
+
+#include <atomic>
+#include <cmath>
+
+#include "kernels/common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
+constexpr int kBM = 256, kBN = 256, kBK = 64;
+constexpr int kTileB = kBM * kBK * 2;        // 32 KB: one operand tile
+constexpr int kBufB = 2 * kTileB;            // W tile | X tile
+constexpr int kLdsG = 2 * kBufB;             // two buffers: 128 KB
+
+struct GemmParams {
+  const uint16_t* x;  // [M][ldx]
+  const uint16_t* w;  // [N][ldw]
+  const uint16_t* bias;  // [N] (epi >= 1)
+  const uint16_t* r;  // [M][ldr] (epi 3)
+  uint16_t* y;        // [M][ldy]
+  int M, N, K, ldx, ldw, ldr, ldy;
+  int mt, nt;         // tiles along M, N
+};
+
+__device__ __forceinline__ bf16x8 fr(v4u v) { return __builtin_bit_cast(bf16x8, v); }
+
+__device__ __forceinline__ uint32_t pk(float a, float b) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+// byte offset of 16-B chunk c of row r in a [rows][64 bf16] tile image
+__device__ __forceinline__ int chunk_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+template <int EPI>
+__global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // XCD-contiguous tile order (bijective for any tile count)
+  const int nwg = p.mt * p.nt;
+  const int b = blockIdx.x, xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
+  const int wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  const int tm = wg / p.nt, tn = wg - tm * p.nt;
+  const int m0 = tm * kBM, n0 = tn * kBN;
+
+  // LDS-DMA sources: instruction i of wave w covers tile rows 8(8i + w) ..+8;
+  // lane L -> row (8i + w) * 8 + L / 8, physical chunk L % 8
+  const uint16_t* srcw[4];
+  const uint16_t* srcx[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (8 * i + wave) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    srcw[i] = p.w + (size_t)(n0 + row) * p.ldw + 8 * c;
+    srcx[i] = p.x + (size_t)min(m0 + row, p.M - 1) * p.ldx + 8 * c;
+  }
+  auto stage = [&](int kt, int buf) {
+    uint8_t* dw = lds + buf * kBufB;
+    uint8_t* dx = dw + kTileB;
+    const int k0 = kt * kBK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_global_load_lds((const void*)(srcw[i] + k0), (void*)(dw + (8 * i + wave) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(srcx[i] + k0), (void*)(dx + (8 * i + wave) * 1024), 16, 0, 0);
+    }
+  };
+
+  const int wm = wave >> 2, wn = wave & 3;  // wave sub-tile: tokens 128 wm.., channels 64 wn..
+  const int fr16 = lane & 15, fq = lane >> 4;
+  f32x4 acc[4][8];  // [channel frag][token frag]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / kBK;
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
+    const uint8_t* tw = lds + buf * kBufB;
+    const uint8_t* tx = tw + kTileB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      v4u a[4], bq[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const v4u*>(tw + chunk_off(64 * wn + 16 * i + fr16, 4 * kk + fq));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bq[j] = *reinterpret_cast<const v4u*>(tx + chunk_off(128 * wm + 16 * j + fr16, 4 * kk + fq));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr(a[i]), fr(bq[j]), acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();  // the next step's DMA landed; this buffer's reads are done
+  }
+
+  // epilogue: C (16x16): lane column = token m, rows 4 fq + e = channels
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + 64 * wn + 16 * i + 4 * fq;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI >= 1) {
+      const v2u bb = *reinterpret_cast<const v2u*>(p.bias + n);
+      bv[0] = __uint_as_float(bb[0] << 16);
+      bv[1] = __uint_as_float(bb[0] & 0xffff0000u);
+      bv[2] = __uint_as_float(bb[1] << 16);
+      bv[3] = __uint_as_float(bb[1] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = m0 + 128 * wm + 16 * j + fr16;
+      if (m >= p.M) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
+      if constexpr (EPI == 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+      }
+      if constexpr (EPI == 3) {
+        const v2u rr = *reinterpret_cast<const v2u*>(p.r + (size_t)m * p.ldr + n);
+        v[0] += __uint_as_float(rr[0] << 16);
+        v[1] += __uint_as_float(rr[0] & 0xffff0000u);
+        v[2] += __uint_as_float(rr[1] << 16);
+        v[3] += __uint_as_float(rr[1] & 0xffff0000u);
+      }
+      *reinterpret_cast<v2u*>(p.y + (size_t)m * p.ldy + n) = v2u{pk(v[0], v[1]), pk(v[2], v[3])};
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Y = epi(X W^T): bf16 X [M][ldx], W [N][ldw], Y [M][ldy]; N % 256 == 0,
+// K % 64 == 0, leading dimensions multiples of 8 elements, 16-B aligned bases.
+int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* r, void* y, int M, int N, int K,
+                    int ldx, int ldw, int ldr, int ldy, int epi, void* stream) {
+  if (M <= 0) return hipSuccess;
+  if (N <= 0 || N % kBN || K <= 0 || K % kBK || epi < 0 || epi > 3) return hipErrorInvalidValue;
+  if (!x || !w || !y || ldx < K || ldw < K || ldy < N || ldx % 8 || ldw % 8 || ldy % 8) return hipErrorInvalidValue;
+  if (epi >= 1 && !bias) return hipErrorInvalidValue;
+  if (epi == 3 && (!r || ldr < N || ldr % 8)) return hipErrorInvalidValue;
+  auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  if (!al(x) || !al(w) || !al(y) || (bias && ((uintptr_t)bias & 7)) || (r && !al(r))) return hipErrorInvalidValue;
+  GemmParams p;
+  p.x = (const uint16_t*)x;
+  p.w = (const uint16_t*)w;
+  p.bias = (const uint16_t*)bias;
+  p.r = (const uint16_t*)r;
+  p.y = (uint16_t*)y;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.ldx = ldx;
+  p.ldw = ldw;
+  p.ldr = ldr;
+  p.ldy = ldy;
+  p.mt = (M + kBM - 1) / kBM;
+  p.nt = N / kBN;
+  const void* fns[4] = {(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
+                        (const void*)gemm_bf16_kernel<2>, (const void*)gemm_bf16_kernel<3>};
+  // dynamic-LDS opt-in once per device (cached only after every call succeeded)
+  static std::atomic<bool> attr_set[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (!attr_set[dev].load(std::memory_order_acquire)) {
+    for (const void* f : fns) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsG);
+      if (e != hipSuccess) return e;
+    }
+    attr_set[dev].store(true, std::memory_order_release);
+  }
+  void* args[] = {&p};
+  const hipError_t e =
+      hipLaunchKernel(fns[epi], dim3(p.mt * p.nt), dim3(512), args, kLdsG, (hipStream_t)stream);
+  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -211,6 +211,11 @@ _SIGS = {
         ],
         ctypes.c_int,
     ),
+    "tcamd_gemm_bf16": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_x3_dense_small": (
         [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -740,6 +745,20 @@ def x3_dense_fused(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo
     of 32 in 64..224."""
     _check(_load().tcamd_x3_dense_fused(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
                                         w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_fused")
+
+
+GEMM_EPI = {"none": 0, "bias": 1, "bias_gelu": 2, "bias_residual": 3}
+
+
+def gemm_bf16(x, w, y, M, N, K, bias=None, residual=None, epilogue="none", ldx=None, ldw=None, ldr=None, ldy=None,
+              stream=None):
+    """K15: ``y = epi(x @ w.T)`` in bf16 (fp32 accumulate) on the hand-written
+    gfx950 GEMM (csrc/kernels/gemm.hip).  x [M][ldx], w [N][ldw] (nn.Linear
+    layout), y [M][ldy] device pointers; epilogue none | bias | bias_gelu (erf)
+    | bias_residual (+ residual[M][ldr]).  N % 256 == 0, K % 64 == 0."""
+    _check(_load().tcamd_gemm_bf16(x, w, _vp(bias), _vp(residual), y, int(M), int(N), int(K), int(ldx or K),
+                                   int(ldw or K), int(ldr or N), int(ldy or N), GEMM_EPI[epilogue], _vp(stream)),
+           "gemm_bf16")
 
 
 def x3_dense_small(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None):
