@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[64])
     ap.add_argument("--seq", type=int, default=384)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--k15-ab", type=int, default=0,
+                    help="also time the forward with K15 GEMMs from this many tokens (interleaved A/B rounds)")
+    ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     model = bert.build(device=dev)
@@ -28,17 +31,30 @@ def main():
         ids = torch.randint(0, bert.VOCAB, (b, a.seq), device=dev)
         mask = torch.ones(b, a.seq, device=dev, dtype=torch.int64)
         tt = torch.zeros(b, a.seq, device=dev, dtype=torch.int64)
+        variants = {"default": bert.K15_MIN_TOKENS}
+        if a.k15_ab:
+            variants = {"hipblaslt": 0, "k15": a.k15_ab}
+        ts = {k: [] for k in variants}
         with torch.no_grad():
-            for _ in range(2):
-                model(ids, mask, tt)
+            for name, thr in variants.items():
+                bert.K15_MIN_TOKENS = thr
+                for _ in range(2):
+                    model(ids, mask, tt)
             torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(a.iters):
-                model(ids, mask, tt)
-            torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / a.iters
-        tf = bert.flops_per_sequence(a.seq) * b / dt / 1e12
-        print({"batch": b, "ms": round(dt * 1e3, 3), "seq_per_s": round(b / dt, 1), "tflops": round(tf, 1)}, flush=True)
+            for _ in range(a.rounds):
+                for name, thr in variants.items():
+                    bert.K15_MIN_TOKENS = thr
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    for _ in range(a.iters):
+                        model(ids, mask, tt)
+                    torch.cuda.synchronize()
+                    ts[name].append((time.perf_counter() - t0) / a.iters)
+        for name, v in ts.items():
+            dt = sorted(v)[len(v) // 2]
+            tf = bert.flops_per_sequence(a.seq) * b / dt / 1e12
+            print({"batch": b, "variant": name, "ms": round(dt * 1e3, 3), "seq_per_s": round(b / dt, 1),
+                   "tflops": round(tf, 1)}, flush=True)
 
 
 if __name__ == "__main__":

@@ -36,6 +36,34 @@ TYPES = 2
 
 # fused paths on the GPU (bf16 CUDA tensors); TC_BERT_FUSED=0 runs plain torch ops
 FUSED = os.environ.get("TC_BERT_FUSED", "1") != "0"
+# K15 (csrc/kernels/gemm.hip) for the four projections from this many tokens
+# up (0 = never: hipBLASLt); small batches stay on the library (few tiles)
+K15_MIN_TOKENS = int(os.environ.get("TC_BERT_K15_MIN_TOKENS", "0"))
+
+
+def _k15_ok(x2d, n):
+    return (FUSED and K15_MIN_TOKENS > 0 and x2d.is_cuda and x2d.dtype == torch.bfloat16 and x2d.is_contiguous()
+            and x2d.shape[0] >= K15_MIN_TOKENS and n % 256 == 0 and x2d.shape[1] % 64 == 0)
+
+
+def _proj(x, lin, epilogue="bias"):
+    """lin(x) (epilogue "bias"), gelu(lin(x)) ("bias_gelu") or x @ W^T ("none"):
+    K15 with the epilogue fused at big token counts, torch / hipBLASLt otherwise."""
+    x2 = x.reshape(-1, x.shape[-1])
+    n = lin.weight.shape[0]
+    if _k15_ok(x2, n):
+        from triton_client_amd.ops import hip
+
+        y = torch.empty(x2.shape[0], n, device=x.device, dtype=x.dtype)
+        hip.gemm_bf16(x2.data_ptr(), lin.weight.data_ptr(), y.data_ptr(), x2.shape[0], n, x2.shape[1],
+                      bias=None if epilogue == "none" else lin.bias.data_ptr(), epilogue=epilogue,
+                      stream=torch.cuda.current_stream(x.device).cuda_stream)
+        return y.view(*x.shape[:-1], n)
+    if epilogue == "none":
+        return torch.mm(x2, lin.weight.t()).view(*x.shape[:-1], n)
+    if epilogue == "bias_gelu":
+        return _linear_gelu(x, lin)
+    return lin(x)
 
 
 def _add_ln(x, y, ln):
@@ -102,12 +130,12 @@ class _Layer(nn.Module):
         if _k12_ok(x, s):
             # plain GEMM (no bias epilogue: 152 vs 171 us at bs64 x 384,
             # profiles/r3_bert_gemm_layout.log); K12 applies the bias
-            qkv = torch.mm(x.view(-1, HIDDEN), self.qkv.weight.t()).view(b, s, 3 * HIDDEN)
+            qkv = _proj(x, self.qkv, "none")
             a = _attention(qkv, b, s, mask_i32, bias, qkv_bias=self.qkv.bias)
         else:
             a = _attention(self.qkv(x), b, s, mask_i32, bias)
-        x = _add_ln(x, self.out(a), self.ln1)
-        return _add_ln(x, self.ffn2(_linear_gelu(x, self.ffn1)), self.ln2)
+        x = _add_ln(x, _proj(a, self.out), self.ln1)
+        return _add_ln(x, _proj(_proj(x, self.ffn1, "bias_gelu"), self.ffn2), self.ln2)
 
 
 class BertLargeQA(nn.Module):
