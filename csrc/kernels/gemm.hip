@@ -28,6 +28,7 @@
 
 #include <atomic>
 #include <cmath>
+#include <cstdlib>
 
 #include "kernels/common.h"
 
@@ -63,6 +64,45 @@ __device__ __forceinline__ uint32_t pk(float a, float b) {
 
 // byte offset of 16-B chunk c of row r in a [rows][64 bf16] tile image
 __device__ __forceinline__ int chunk_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+// C (16x16) of a wave's 128 (m) x 64 (n) sub-tile: lane column = token m,
+// rows 4 fq + e = four consecutive output channels -> 8-B stores
+template <int EPI>
+__device__ __forceinline__ void epilogue(const GemmParams& p, f32x4 (&acc)[4][8], int m0, int n0, int wm, int wn,
+                                         int fr16, int fq) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + 64 * wn + 16 * i + 4 * fq;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI >= 1) {
+      const v2u bb = *reinterpret_cast<const v2u*>(p.bias + n);
+      bv[0] = __uint_as_float(bb[0] << 16);
+      bv[1] = __uint_as_float(bb[0] & 0xffff0000u);
+      bv[2] = __uint_as_float(bb[1] << 16);
+      bv[3] = __uint_as_float(bb[1] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = m0 + 128 * wm + 16 * j + fr16;
+      if (m >= p.M) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
+      if constexpr (EPI == 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+      }
+      if constexpr (EPI == 3) {
+        const v2u rr = *reinterpret_cast<const v2u*>(p.r + (size_t)m * p.ldr + n);
+        v[0] += __uint_as_float(rr[0] << 16);
+        v[1] += __uint_as_float(rr[0] & 0xffff0000u);
+        v[2] += __uint_as_float(rr[1] << 16);
+        v[3] += __uint_as_float(rr[1] & 0xffff0000u);
+      }
+      *reinterpret_cast<v2u*>(p.y + (size_t)m * p.ldy + n) = v2u{pk(v[0], v[1]), pk(v[2], v[3])};
+    }
+  }
+}
 
 template <int EPI>
 __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
@@ -130,39 +170,125 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
     __syncthreads();  // the next step's DMA landed; this buffer's reads are done
   }
 
-  // epilogue: C (16x16): lane column = token m, rows 4 fq + e = channels
+  epilogue<EPI>(p, acc, m0, n0, wm, wn, fr16, fq);
+}
+
+// ---- phased variant: 4 phases per K step, counted vmcnt across barriers ----
+// A K step's 64 MFMAs per wave run as four 16-MFMA quadrant clusters (64
+// tokens x 32 channels of the wave's 128 x 64 sub-tile), ordered (qm, qn) =
+// (0,0) (0,1) (1,1) (1,0) so each phase reads only the operand that changed
+// (12, 4, 8, 4 ds_read_b128).  The next K step is staged by quarter-tiles in
+// the order the phases need them, one per phase:
+//   S0 X rows of qm 0 (tokens 0-63, 128-191), S1 W rows of qn 0 (channel rows
+//   r % 64 < 32), S2 W rows of qn 1, S3 X rows of qm 1,
+// each 16 KB = 2 LDS-DMA per thread.  Phase = counted vmcnt (the quarter this
+// phase reads landed; the two younger quarters stay in flight) -> raw
+// barrier -> stage the next step's quarter into the other buffer (every read
+// of that buffer retired before this barrier) -> LDS reads -> MFMA cluster.
+// One barrier per phase; no vmcnt(0) in steady state.
+constexpr int kSubRows = 128;  // rows per quarter-tile
+
+__device__ __forceinline__ int sub_rowbase(int s, int g) {  // 8-row group g (0..15) of quarter s
+  switch (s) {
+    case 0: return g < 8 ? 8 * g : 128 + 8 * (g - 8);
+    case 1: return 64 * (g >> 2) + 8 * (g & 3);
+    case 2: return 64 * (g >> 2) + 32 + 8 * (g & 3);
+    default: return g < 8 ? 64 + 8 * g : 192 + 8 * (g - 8);
+  }
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(512, 1) gemm_bf16_ph_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwg = p.mt * p.nt;
+  const int b = blockIdx.x, xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
+  const int wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  const int tm = wg / p.nt, tn = wg - tm * p.nt;
+  const int m0 = tm * kBM, n0 = tn * kBN;
+
+  // per quarter s and instruction i: the lane's source row and the group's LDS row base
+  const uint16_t* src[4][2];
+  int dbase[4][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int n = n0 + 64 * wn + 16 * i + 4 * fq;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPI >= 1) {
-      const v2u bb = *reinterpret_cast<const v2u*>(p.bias + n);
-      bv[0] = __uint_as_float(bb[0] << 16);
-      bv[1] = __uint_as_float(bb[0] & 0xffff0000u);
-      bv[2] = __uint_as_float(bb[1] << 16);
-      bv[3] = __uint_as_float(bb[1] & 0xffff0000u);
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rb = sub_rowbase(s, 8 * i + wave);
+      const int row = rb + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      const bool isx = s == 0 || s == 3;
+      src[s][i] = isx ? p.x + (size_t)min(m0 + row, p.M - 1) * p.ldx + 8 * c : p.w + (size_t)(n0 + row) * p.ldw + 8 * c;
+      dbase[s][i] = (isx ? kTileB : 0) + rb * 128;
     }
+  auto stage = [&](int kt, int buf, int s) {
+    const int k0 = kt * kBK;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int m = m0 + 128 * wm + 16 * j + fr16;
-      if (m >= p.M) continue;
-      float v[4];
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src[s][i] + k0), (void*)(lds + buf * kBufB + dbase[s][i]), 16, 0,
+                                       0);
+  };
+
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr16 = lane & 15, fq = lane >> 4;
+  f32x4 acc[4][8];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
-      if constexpr (EPI == 2) {
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / kBK;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) stage(0, 0, s);
+  __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): step 0 landed
+  __builtin_amdgcn_s_barrier();
+  v4u xa[4][2], wa[2][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    const bool last = kt + 1 == nk;
+    const uint8_t* tw = lds + buf * kBufB;
+    const uint8_t* tx = tw + kTileB;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int qm = ph >> 1, qn = (ph == 1 || ph == 2) ? 1 : 0;
+      // the quarter this phase reads landed (issue order: S0..S3 per step)
+      if (last) {
+        if (ph == 0) __builtin_amdgcn_s_waitcnt(0x0F74);       // vmcnt(4)
+        else if (ph == 1) __builtin_amdgcn_s_waitcnt(0x0F72);  // vmcnt(2)
+        else __builtin_amdgcn_s_waitcnt(0x0F70);               // vmcnt(0)
+      } else {
+        if (ph == 3) __builtin_amdgcn_s_waitcnt(0x0F76);       // vmcnt(6)
+        else __builtin_amdgcn_s_waitcnt(0x0F74);               // vmcnt(4)
       }
-      if constexpr (EPI == 3) {
-        const v2u rr = *reinterpret_cast<const v2u*>(p.r + (size_t)m * p.ldr + n);
-        v[0] += __uint_as_float(rr[0] << 16);
-        v[1] += __uint_as_float(rr[0] & 0xffff0000u);
-        v[2] += __uint_as_float(rr[1] << 16);
-        v[3] += __uint_as_float(rr[1] & 0xffff0000u);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (!last) stage(kt + 1, buf ^ 1, ph);
+      if (ph == 0 || ph == 2) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            xa[j][kk] = *reinterpret_cast<const v4u*>(tx + chunk_off(128 * wm + 64 * qm + 16 * j + fr16, 4 * kk + fq));
       }
-      *reinterpret_cast<v2u*>(p.y + (size_t)m * p.ldy + n) = v2u{pk(v[0], v[1]), pk(v[2], v[3])};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          wa[i][kk] = *reinterpret_cast<const v4u*>(tw + chunk_off(64 * wn + 32 * qn + 16 * i + fr16, 4 * kk + fq));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[2 * qn + i][4 * qm + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr(wa[i][kk]), fr(xa[j][kk]), acc[2 * qn + i][4 * qm + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
   }
+  epilogue<EPI>(p, acc, m0, n0, wm, wn, fr16, fq);
 }
 
 }  // namespace
@@ -195,17 +321,23 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
   p.ldy = ldy;
   p.mt = (M + kBM - 1) / kBM;
   p.nt = N / kBN;
-  const void* fns[4] = {(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
-                        (const void*)gemm_bf16_kernel<2>, (const void*)gemm_bf16_kernel<3>};
+  // TCAMD_GEMM_V: 1 = one barrier per K step (default), 2 = the phased kernel
+  static const int ver = getenv("TCAMD_GEMM_V") ? atoi(getenv("TCAMD_GEMM_V")) : 1;
+  const void* all[2][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
+                            (const void*)gemm_bf16_kernel<2>, (const void*)gemm_bf16_kernel<3>},
+                           {(const void*)gemm_bf16_ph_kernel<0>, (const void*)gemm_bf16_ph_kernel<1>,
+                            (const void*)gemm_bf16_ph_kernel<2>, (const void*)gemm_bf16_ph_kernel<3>}};
+  const void* const* fns = all[ver == 2 ? 1 : 0];
   // dynamic-LDS opt-in once per device (cached only after every call succeeded)
   static std::atomic<bool> attr_set[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
   if (!attr_set[dev].load(std::memory_order_acquire)) {
-    for (const void* f : fns) {
-      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsG);
-      if (e != hipSuccess) return e;
-    }
+    for (const auto& row : all)
+      for (const void* f : row) {
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsG);
+        if (e != hipSuccess) return e;
+      }
     attr_set[dev].store(true, std::memory_order_release);
   }
   void* args[] = {&p};

@@ -88,3 +88,44 @@ def test_gemm_bf16_rejects_bad_shapes():
             hip.gemm_bf16(t.data_ptr(), t.data_ptr(), t.data_ptr(), M, N, K)
     with pytest.raises(Exception):  # bias epilogue without a bias
         hip.gemm_bf16(t.data_ptr(), t.data_ptr(), t.data_ptr(), 16, 256, 64, epilogue="bias")
+
+
+def test_gemm_bf16_phased_variant_matches(tmp_path):
+    """TCAMD_GEMM_V=2 (4 phases per K step, counted vmcnt across barriers) in a
+    child process (the variant is chosen once per process): same results as
+    the fp32 reference on every epilogue, including K = 64 (one step: the last
+    step's wait counts) and K = 4096."""
+    _need_gpu()
+    import os
+    import subprocess
+    import sys
+
+    code = r'''
+import torch, torch.nn.functional as F
+from triton_client_amd.ops import hip
+for (M, N, K) in [(512, 256, 64), (1000, 1024, 1024), (768, 1024, 4096), (384, 3072, 1024)]:
+    for epi in ["none", "bias", "bias_gelu", "bias_residual"]:
+        g = torch.Generator(device="cuda").manual_seed(M + N + K)
+        x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(torch.bfloat16)
+        b = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
+        r = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+        y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        hip.gemm_bf16(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, N, K, bias=b.data_ptr(), residual=r.data_ptr(),
+                      epilogue=epi)
+        torch.cuda.synchronize()
+        ref = x.float() @ w.float().t()
+        if epi != "none":
+            ref = ref + b.float()
+        if epi == "bias_gelu":
+            ref = F.gelu(ref)
+        if epi == "bias_residual":
+            ref = ref + r.float()
+        err = ((y.float() - ref).norm() / ref.norm()).item()
+        assert err < 4e-3, (M, N, K, epi, err)
+print("PHASED_OK")
+'''
+    env = dict(os.environ, TCAMD_GEMM_V="2")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "PHASED_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

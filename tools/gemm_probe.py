@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--tokens", default="24576,3072")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--variant", default="", help="run this TCAMD_GEMM_V in a child (1, 2) and print its rows")
     a = ap.parse_args()
     import torch
     import torch.nn.functional as F
