@@ -186,8 +186,6 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
 // barrier -> stage the next step's quarter into the other buffer (every read
 // of that buffer retired before this barrier) -> LDS reads -> MFMA cluster.
 // One barrier per phase; no vmcnt(0) in steady state.
-constexpr int kSubRows = 128;  // rows per quarter-tile
-
 __device__ __forceinline__ int sub_rowbase(int s, int g) {  // 8-row group g (0..15) of quarter s
   switch (s) {
     case 0: return g < 8 ? 8 * g : 128 + 8 * (g - 8);

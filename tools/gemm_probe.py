@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--variant", default="", help="run this TCAMD_GEMM_V in a child (1, 2) and print its rows")
     a = ap.parse_args()
+    if a.variant:
+        os.environ["TCAMD_GEMM_V"] = a.variant  # read by the library at its first GEMM
     import torch
     import torch.nn.functional as F
 
@@ -66,7 +68,7 @@ def main():
             tl.sort()
             fl = 2.0 * M * N * K
             mo, ml = to[len(to) // 2], tl[len(tl) // 2]
-            print(json.dumps({"tokens": M, "gemm": name, "N": N, "K": K, "epilogue": epi, "k15_us": round(mo, 1),
+            print(json.dumps({"variant": os.environ.get("TCAMD_GEMM_V", "1"), "tokens": M, "gemm": name, "N": N, "K": K, "epilogue": epi, "k15_us": round(mo, 1),
                               "hipblaslt_us": round(ml, 1), "k15_PFps": round(fl / mo / 1e9, 3),
                               "hipblaslt_PFps": round(fl / ml / 1e9, 3)}), flush=True)
 
