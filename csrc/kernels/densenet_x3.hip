@@ -1668,6 +1668,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   constexpr int kTRMax = (kRowsOut + kHalves) * W;   // z pixels: 112 / 49
   constexpr int kNRI = (kTRMax + 31) / 32;           // producer row passes (32 rows each)
   constexpr int kOps = 4 + 2 + kNRI;                 // vm ops per producer iteration
+  constexpr bool kQ4 = kTRMax <= 64;                 // 1x1 consumers split channels, not pixels
   static_assert(kTRMax <= 128, "one 1x1 tile");
   static_assert(kNPad * kRowB + 2 * 4 * 3 * kNPG * 64 * 4 <= kLdsSm, "K14x LDS budget");
   extern __shared__ __attribute__((aligned(16))) uint8_t ldss[];
@@ -1784,7 +1785,28 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
         continue;
       }
       const uint8_t* st = ldss + (q % kSmS) * kWsStage;
-      if (rv > 0) {
+      if constexpr (kQ4) {
+        // 7x7: the tile is <= 64 rows, so the 4 waves split the 128 channels
+        // instead (wave = 32-channel quarter x both 32-pixel blocks)
+        v4u ah[2], al[2], bh[2][2], bl[2][2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int wo = ws_chunk(32 * wave + col, 2 * kk + h);
+          ah[kk] = ld16(st + 2 * kWsPlane + wo);
+          al[kk] = ld16(st + 3 * kWsPlane + wo);
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int xo = ws_chunk(32 * b + col, 2 * kk + h);
+            bh[kk][b] = ld16(st + xo);
+            bl[kk][b] = ld16(st + kWsPlane + xo);
+          }
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            if (b == 0 || TR > 32) acc[0][b] = x3_32(ah[kk], al[kk], bh[kk][b], bl[kk][b], acc[0][b]);
+      } else if (rv > 0) {
         v4u ah[2][2], al[2][2], bh[2][2], bl[2][2];
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
@@ -1838,22 +1860,23 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
     // C (32x32): lane col = pixel, reg 4g+e -> channel 64wn + 32a + 8g + 4h + e
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
-      const int pz = 64 * wm + 32 * b + col;  // z pixel of the tile
+      const int pz = (kQ4 ? 0 : 64 * wm) + 32 * b + col;  // z pixel of the tile
       if (pz < TR) {
         const int zy = pz / W, zx = pz - zy * W;
         const int pos = (zr0 + zy - r0 + 1) * kPW + zx + 1;
         uint8_t* rp = ldss + pos * kRowB + 8 * h;
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < (kQ4 ? 1 : 2); ++a)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const f32x4 bb = ldf4(p.b1 + 64 * wn + 32 * a + 8 * g + 4 * h);
+            const int cb = kQ4 ? 32 * wave : 64 * wn + 32 * a;  // the channel block's first channel
+            const f32x4 bb = ldf4(p.b1 + cb + 8 * g + 4 * h);
             f32x4 r;
 #pragma unroll
             for (int e = 0; e < 4; ++e) r[e] = fmaxf(acc[a][b][4 * g + e] + bb[e], 0.f);
             v2u hh, ll;
             split4(r, hh, ll);
-            uint8_t* q = rp + (((8 * wn + 4 * a + g) ^ (pos & 15)) << 4);
+            uint8_t* q = rp + ((((cb >> 3) + g) ^ (pos & 15)) << 4);
             *reinterpret_cast<v2u*>(q) = hh;
             *reinterpret_cast<v2u*>(q + 256) = ll;
           }
