@@ -433,6 +433,31 @@ def test_fp32_engine_matches_fp32_module(fp32_engine, b):
     assert err < 1e-3
 
 
+@pytest.mark.parametrize("b", [3, 9, 24])
+def test_fp32_engine_k14x_blocks_match_fp32_module(fp32_engine, b):
+    """The engine with K14x forced on for the 14x14 and 7x7 blocks at every
+    batch (ragged image counts: the 14x14 grid pairs images 8g+j), against the
+    fp32 module, and against the same engine with K14x off."""
+    eng, model = fp32_engine
+    g = torch.Generator(device=DEV).manual_seed(300 + b)
+    x = torch.randn(b, 3, 224, 224, device=DEV, generator=g)
+    keep = eng.smallf_min_blocks
+    try:
+        eng.smallf_min_blocks = 1
+        with torch.no_grad():
+            got = eng(x).clone()
+        eng.smallf_min_blocks = 0
+        with torch.no_grad():
+            base = eng(x).clone()
+            ref = model.to(DEV).float()(x)
+    finally:
+        eng.smallf_min_blocks = keep
+    torch.cuda.synchronize()
+    e_ref, e_base = _rel(got, ref), _rel(got, base)
+    print("K14x engine b=%d: rel vs fp32 module %.3g, vs the pair path %.3g" % (b, e_ref, e_base))
+    assert e_ref < 1e-3 and e_base < 1e-4
+
+
 def test_fp32_engine_vs_fp64_and_graph_capture(fp32_engine):
     """Against an fp64 CPU reference the engine must stay fp32-class (rel-L2
     < 1e-4; measured 4.5e-5, torch's own fp32 forward 2.2e-6 on MI355X, the
