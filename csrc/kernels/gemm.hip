@@ -195,7 +195,15 @@ __device__ __forceinline__ int sub_rowbase(int s, int g) {  // 8-row group g (0.
   }
 }
 
-template <int EPI>
+// STAG: the two wave groups (waves 0-3 = token half 0, waves 4-7 = half 1)
+// run one phase apart (waves 4-7 pass one extra barrier first, waves 0-3 one
+// extra at the end), so on every SIMD one wave's MFMA cluster overlaps the
+// other wave's LDS reads.  A quarter staged by the late group lands one
+// barrier later, so that group retires its copies one phase earlier (the
+// counts below); the buffer a group restages was last read by the late
+// group in the early group's staging interval only for rows the early group
+// does not write then (phase 3 reads W rows qn 0, phase 0 stages X rows qm 0).
+template <int EPI, bool STAG>
 __global__ void __launch_bounds__(512, 1) gemm_bf16_ph_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -236,10 +244,12 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_ph_kernel(GemmParams p) {
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.K / kBK;
+  const int grp = __builtin_amdgcn_readfirstlane(wave >> 2);  // scalar: a wave-uniform branch
 #pragma unroll
   for (int s = 0; s < 4; ++s) stage(0, 0, s);
   __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): step 0 landed
   __builtin_amdgcn_s_barrier();
+  if (STAG && grp) __builtin_amdgcn_s_barrier();  // the late group starts one phase behind
   v4u xa[4][2], wa[2][2];
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
@@ -249,8 +259,17 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_ph_kernel(GemmParams p) {
 #pragma unroll
     for (int ph = 0; ph < 4; ++ph) {
       const int qm = ph >> 1, qn = (ph == 1 || ph == 2) ? 1 : 0;
-      // the quarter this phase reads landed (issue order: S0..S3 per step)
-      if (last) {
+      // the quarter this phase reads landed (issue order: S0..S3 per step);
+      // the late group retires the quarter the NEXT phase reads
+      if (STAG && grp) {
+        if (last) {
+          if (ph == 0) __builtin_amdgcn_s_waitcnt(0x0F72);  // vmcnt(2)
+          else __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
+        } else {
+          if (ph == 2) __builtin_amdgcn_s_waitcnt(0x0F74);  // vmcnt(4)
+          else __builtin_amdgcn_s_waitcnt(0x0F72);          // vmcnt(2)
+        }
+      } else if (last) {
         if (ph == 0) __builtin_amdgcn_s_waitcnt(0x0F74);       // vmcnt(4)
         else if (ph == 1) __builtin_amdgcn_s_waitcnt(0x0F72);  // vmcnt(2)
         else __builtin_amdgcn_s_waitcnt(0x0F70);               // vmcnt(0)
@@ -286,6 +305,7 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_ph_kernel(GemmParams p) {
       __builtin_amdgcn_s_setprio(0);
     }
   }
+  if (STAG && !grp) __builtin_amdgcn_s_barrier();  // matches the late group's extra barrier
   epilogue<EPI>(p, acc, m0, n0, wm, wn, fr16, fq);
 }
 
@@ -319,13 +339,16 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
   p.ldy = ldy;
   p.mt = (M + kBM - 1) / kBM;
   p.nt = N / kBN;
-  // TCAMD_GEMM_V: 1 = one barrier per K step (default), 2 = the phased kernel
+  // TCAMD_GEMM_V: 1 = one barrier per K step (default), 2 = the phased
+  // kernel, 3 = phased with the two wave groups one phase apart
   static const int ver = getenv("TCAMD_GEMM_V") ? atoi(getenv("TCAMD_GEMM_V")) : 1;
-  const void* all[2][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
+  const void* all[3][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
                             (const void*)gemm_bf16_kernel<2>, (const void*)gemm_bf16_kernel<3>},
-                           {(const void*)gemm_bf16_ph_kernel<0>, (const void*)gemm_bf16_ph_kernel<1>,
-                            (const void*)gemm_bf16_ph_kernel<2>, (const void*)gemm_bf16_ph_kernel<3>}};
-  const void* const* fns = all[ver == 2 ? 1 : 0];
+                           {(const void*)gemm_bf16_ph_kernel<0, false>, (const void*)gemm_bf16_ph_kernel<1, false>,
+                            (const void*)gemm_bf16_ph_kernel<2, false>, (const void*)gemm_bf16_ph_kernel<3, false>},
+                           {(const void*)gemm_bf16_ph_kernel<0, true>, (const void*)gemm_bf16_ph_kernel<1, true>,
+                            (const void*)gemm_bf16_ph_kernel<2, true>, (const void*)gemm_bf16_ph_kernel<3, true>}};
+  const void* const* fns = all[ver == 2 ? 1 : (ver == 3 ? 2 : 0)];
   // dynamic-LDS opt-in once per device (cached only after every call succeeded)
   static std::atomic<bool> attr_set[64];
   int dev = 0;

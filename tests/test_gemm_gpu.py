@@ -90,9 +90,10 @@ def test_gemm_bf16_rejects_bad_shapes():
         hip.gemm_bf16(t.data_ptr(), t.data_ptr(), t.data_ptr(), 16, 256, 64, epilogue="bias")
 
 
-def test_gemm_bf16_phased_variant_matches(tmp_path):
-    """TCAMD_GEMM_V=2 (4 phases per K step, counted vmcnt across barriers) in a
-    child process (the variant is chosen once per process): same results as
+@pytest.mark.parametrize("variant", ["2", "3"])
+def test_gemm_bf16_phased_variant_matches(tmp_path, variant):
+    """TCAMD_GEMM_V=2 (4 phases per K step, counted vmcnt across barriers) and 3
+    (the same with the two wave groups one phase apart) in a child process (the variant is chosen once per process): same results as
     the fp32 reference on every epilogue, including K = 64 (one step: the last
     step's wait counts) and K = 4096."""
     _need_gpu()
@@ -125,7 +126,7 @@ for (M, N, K) in [(512, 256, 64), (1000, 1024, 1024), (768, 1024, 4096), (384, 3
         assert err < 4e-3, (M, N, K, epi, err)
 print("PHASED_OK")
 '''
-    env = dict(os.environ, TCAMD_GEMM_V="2")
+    env = dict(os.environ, TCAMD_GEMM_V=variant)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "PHASED_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
