@@ -182,3 +182,16 @@ def test_time_fanout_agrees_on_a_one_rank_failure(tmp_path):
         assert r["after"] == 1.0 and r["calls"] == 3
     assert "injected p2p fault on rank 0" in res[0]["errors"]["p2p"]
     assert res[1]["errors"]["p2p"] == "failed on another rank"
+
+
+@pytest.mark.parametrize("nbytes", [1, 2, 4096, 4097, 4816896, 231211008, 2 ** 31 + 12345])
+def test_replica_sample_positions_stay_in_bounds(nbytes):
+    """verify_replicas samples the region at int64 positions: for the 48-slot
+    bench region (231 MB) a float32 linspace put its last index one past the
+    end (an out-of-bounds read that faulted the GPU on the round-4 box)."""
+    from triton_client_amd.parallel import fanout
+
+    idx = fanout.sample_positions(nbytes)
+    assert int(idx.min()) == 0 and int(idx.max()) == nbytes - 1
+    assert idx.numel() == min(4096, nbytes)
+    assert bool((idx[1:] >= idx[:-1]).all())

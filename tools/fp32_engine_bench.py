@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--engines", default="fp32,bf16")
     ap.add_argument("--json", default="")
+    ap.add_argument("--k14x-ab", action="store_true",
+                    help="fp32 engine: also capture graphs with K14x off and interleave the two (rounds)")
+    ap.add_argument("--rounds", type=int, default=1)
     args = ap.parse_args()
     import torch
 
@@ -44,34 +47,50 @@ def main():
             e.ptrs[:maxb] = torch.arange(maxb, device=dev, dtype=torch.int64) * (3 * 224 * 224 * 4) + imgs.data_ptr()
         outs = [torch.zeros(maxb, 1000, device=dev) for _ in engines]
         sts = [torch.cuda.Stream(device=dev) for _ in engines]
+        variants = [("default", None)]
+        if args.k14x_ab and name == "fp32":
+            variants = [("k14x", eng.smallf_min_blocks), ("pair", 0)]
         for b in batches:
-            graphs = []
-            for e, o, s in zip(engines, outs, sts):
-                with torch.cuda.stream(s), torch.no_grad():
-                    e.forward_ptrs(b, out=o)
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, stream=s):
+            gv = {}
+            for vname, mb in variants:
+                graphs = []
+                for e, o, s in zip(engines, outs, sts):
+                    if mb is not None:
+                        e.smallf_min_blocks = mb
+                    with torch.cuda.stream(s), torch.no_grad():
                         e.forward_ptrs(b, out=o)
-                graphs.append(g)
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, stream=s):
+                            e.forward_ptrs(b, out=o)
+                    graphs.append(g)
+                gv[vname] = graphs
             torch.cuda.synchronize()
             for ns in streams:
-                for _ in range(2):
-                    for i in range(ns):
-                        with torch.cuda.stream(sts[i]):
-                            graphs[i].replay()
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                for _ in range(args.iters):
-                    for i in range(ns):
-                        with torch.cuda.stream(sts[i]):
-                            graphs[i].replay()
-                torch.cuda.synchronize()
-                dt = time.perf_counter() - t0
-                ms = 1000 * dt / args.iters
-                r = {"engine": name, "batch": b, "streams": ns, "ms_per_round": round(ms, 3),
-                     "img_per_s": round(ns * b * args.iters / dt, 1)}
-                rows.append(r)
-                print(json.dumps(r), flush=True)
+                ts = {v: [] for v, _ in variants}
+                for _ in range(args.rounds):
+                    for vname, _ in variants:
+                        graphs = gv[vname]
+                        for _ in range(2):
+                            for i in range(ns):
+                                with torch.cuda.stream(sts[i]):
+                                    graphs[i].replay()
+                        torch.cuda.synchronize()
+                        t0 = time.perf_counter()
+                        for _ in range(args.iters):
+                            for i in range(ns):
+                                with torch.cuda.stream(sts[i]):
+                                    graphs[i].replay()
+                        torch.cuda.synchronize()
+                        ts[vname].append(time.perf_counter() - t0)
+                for vname, _ in variants:
+                    dt = sorted(ts[vname])[len(ts[vname]) // 2]
+                    ms = 1000 * dt / args.iters
+                    r = {"engine": name, "variant": vname, "batch": b, "streams": ns, "ms_per_round": round(ms, 3),
+                         "img_per_s": round(ns * b * args.iters / dt, 1)}
+                    rows.append(r)
+                    print(json.dumps(r), flush=True)
+            graphs = None
+            gv = None
         del engines, graphs
         torch.cuda.empty_cache()
     if args.json:

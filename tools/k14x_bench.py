@@ -120,7 +120,10 @@ def main():
     ap.add_argument("--fwd-iters", type=int, default=5)
     ap.add_argument("--min-blocks", type=int, default=1)
     ap.add_argument("--no-layers", action="store_true")
+    ap.add_argument("--pf", default="", help="TCAMD_X3_SMALLF_PF for this process (3 or 6)")
     a = ap.parse_args()
+    if a.pf:
+        os.environ["TCAMD_X3_SMALLF_PF"] = a.pf  # read by the library at its first K14x launch
     import torch
 
     from triton_client_amd.ops import hip

@@ -338,17 +338,28 @@ def verify_host_replicas(buf, sample=4096):
     return bool(flag.item())
 
 
+def sample_positions(nbytes, sample=4096, device="cpu"):
+    """``min(sample, nbytes)`` evenly spread byte positions in [0, nbytes),
+    first and last included, in int64 arithmetic (a float32 linspace rounds
+    the last position of a > 16 MiB region past its end: an out-of-bounds
+    device read)."""
+    import torch
+
+    n = min(sample, nbytes)
+    return torch.arange(n, device=device, dtype=torch.int64) * (nbytes - 1) // max(n - 1, 1)
+
+
 def verify_replicas(region, nbytes, sample=4096, over_cpu=False):
     """Every rank checks a strided sample of its region against rank 0's
     (``over_cpu``: over the gloo control group, after an RCCL fallback)."""
     import torch
 
     dist = _dist()
-    t = region_tensor(region, nbytes)
-    idx = torch.linspace(0, nbytes - 1, min(sample, nbytes), device=t.device).long()
-    s = t[idx].to(torch.int64)
     if dist is None:
         return True
+    t = region_tensor(region, nbytes)
+    idx = sample_positions(nbytes, sample, t.device)
+    s = t[idx].to(torch.int64)
     group = None
     if over_cpu:
         group = cpu_group()
