@@ -1768,7 +1768,6 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
         ws_barrier();  // B(q+1)
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stages are z's memory next
   } else {
     // ------------------------------- consumer -------------------------------
 #pragma unroll
@@ -1837,6 +1836,15 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
       ws_barrier();  // B(q+1): stage q is free
     }
   }
+  // BN2 bias of this consumer lane's channels, loaded BEFORE the 3x3
+  // weights: a later load would make its wait drain the weight loads too
+  f32x4 ob[2][4];
+  if (wave < 4) {
+#pragma unroll
+    for (int a = 0; a < (kQ4 ? 1 : 2); ++a)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) ob[a][g] = ldf4(p.b1 + (kQ4 ? 32 * wave : 64 * wn + 32 * a) + 8 * g + 4 * h);
+  }
   // 3x3 weights: in flight while the LDS changes hands and z is written
   const int kq = wave & 3, oh = wave >> 2;
   v4u w2h[kTaps], w2l[kTaps];
@@ -1846,7 +1854,13 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
     w2h[t] = ld16(p.w2_hi + off);
     w2l[t] = ld16(p.w2_lo + off);
   }
-  __syncthreads();  // Bz: every DMA and stage read retired; the LDS holds z from here
+  // Bz: every DMA and stage read retired (vmcnt retires in order: the 18
+  // weight loads just issued are younger than the producers' last DMA and X
+  // loads), the LDS holds z from here; raw barrier, so the weight loads stay
+  // in flight across it (a __syncthreads would drain them)
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0(2 * kTaps));
+  ws_barrier();
   // zero the padding of the tile image (columns 0 and W+1, rows outside the image)
   for (int i = tid; i < kNPad * 32; i += 512) {
     const int pos = i >> 5, piece = i & 31;
@@ -1870,7 +1884,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const int cb = kQ4 ? 32 * wave : 64 * wn + 32 * a;  // the channel block's first channel
-            const f32x4 bb = ldf4(p.b1 + cb + 8 * g + 4 * h);
+            const f32x4 bb = ob[a][g];
             f32x4 r;
 #pragma unroll
             for (int e = 0; e < 4; ++e) r[e] = fmaxf(acc[a][b][4 * g + e] + bb[e], 0.f);
