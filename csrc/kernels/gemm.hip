@@ -104,7 +104,11 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, f32x4 (&acc)[4][8]
   }
 }
 
-template <int EPI>
+// SPREAD: the next step's 8 LDS-DMA copies are issued one per 8-MFMA group
+// instead of all before the step's LDS reads (an LDS-DMA piece costs ~60-185
+// issue cycles; issued in a burst by every wave at once they stall the
+// matrix pipe at the top of each step)
+template <int EPI, bool SPREAD = false>
 __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -126,15 +130,18 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
     srcw[i] = p.w + (size_t)(n0 + row) * p.ldw + 8 * c;
     srcx[i] = p.x + (size_t)min(m0 + row, p.M - 1) * p.ldx + 8 * c;
   }
-  auto stage = [&](int kt, int buf) {
+  auto stage1 = [&](int kt, int buf, int piece) {  // piece 0..7: W rows 8(8i + w).., then X
     uint8_t* dw = lds + buf * kBufB;
-    uint8_t* dx = dw + kTileB;
-    const int k0 = kt * kBK;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    const int k0 = kt * kBK, i = piece & 3;
+    if (piece < 4)
       __builtin_amdgcn_global_load_lds((const void*)(srcw[i] + k0), (void*)(dw + (8 * i + wave) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(srcx[i] + k0), (void*)(dx + (8 * i + wave) * 1024), 16, 0, 0);
-    }
+    else
+      __builtin_amdgcn_global_load_lds((const void*)(srcx[i] + k0), (void*)(dw + kTileB + (8 * i + wave) * 1024), 16,
+                                       0, 0);
+  };
+  auto stage = [&](int kt, int buf) {
+#pragma unroll
+    for (int piece = 0; piece < 8; ++piece) stage1(kt, buf, piece);
   };
 
   const int wm = wave >> 2, wn = wave & 3;  // wave sub-tile: tokens 128 wm.., channels 64 wn..
@@ -150,7 +157,8 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
+    const bool more = kt + 1 < nk;
+    if (!SPREAD && more) stage(kt + 1, buf ^ 1);
     const uint8_t* tw = lds + buf * kBufB;
     const uint8_t* tx = tw + kTileB;
 #pragma unroll
@@ -162,9 +170,14 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
       for (int j = 0; j < 8; ++j) bq[j] = *reinterpret_cast<const v4u*>(tx + chunk_off(128 * wm + 16 * j + fr16, 4 * kk + fq));
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr(a[i]), fr(bq[j]), acc[i][j], 0, 0, 0);
+        if constexpr (SPREAD) {
+          if (more) stage1(kt + 1, buf ^ 1, 4 * kk + i);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
       __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();  // the next step's DMA landed; this buffer's reads are done
@@ -340,15 +353,18 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
   p.mt = (M + kBM - 1) / kBM;
   p.nt = N / kBN;
   // TCAMD_GEMM_V: 1 = one barrier per K step (default), 2 = the phased
-  // kernel, 3 = phased with the two wave groups one phase apart
+  // kernel, 3 = phased with the two wave groups one phase apart, 4 = one
+  // barrier per step with the DMA spread over the MFMA groups
   static const int ver = getenv("TCAMD_GEMM_V") ? atoi(getenv("TCAMD_GEMM_V")) : 1;
-  const void* all[3][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
+  const void* all[4][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
                             (const void*)gemm_bf16_kernel<2>, (const void*)gemm_bf16_kernel<3>},
                            {(const void*)gemm_bf16_ph_kernel<0, false>, (const void*)gemm_bf16_ph_kernel<1, false>,
                             (const void*)gemm_bf16_ph_kernel<2, false>, (const void*)gemm_bf16_ph_kernel<3, false>},
                            {(const void*)gemm_bf16_ph_kernel<0, true>, (const void*)gemm_bf16_ph_kernel<1, true>,
-                            (const void*)gemm_bf16_ph_kernel<2, true>, (const void*)gemm_bf16_ph_kernel<3, true>}};
-  const void* const* fns = all[ver == 2 ? 1 : (ver == 3 ? 2 : 0)];
+                            (const void*)gemm_bf16_ph_kernel<2, true>, (const void*)gemm_bf16_ph_kernel<3, true>},
+                           {(const void*)gemm_bf16_kernel<0, true>, (const void*)gemm_bf16_kernel<1, true>,
+                            (const void*)gemm_bf16_kernel<2, true>, (const void*)gemm_bf16_kernel<3, true>}};
+  const void* const* fns = all[(ver >= 2 && ver <= 4) ? ver - 1 : 0];
   // dynamic-LDS opt-in once per device (cached only after every call succeeded)
   static std::atomic<bool> attr_set[64];
   int dev = 0;
