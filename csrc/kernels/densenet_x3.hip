@@ -1653,6 +1653,7 @@ struct X3SmallParams {
   float* y;               // [pixels][ldy] fp32, offset to the layer's 32-channel slice
   int ldx, K, ldy, imgs;
   int dbg;                // ablation (TCAMD_X3_SMALLF_DBG): 1 = no 3x3 phase
+  unsigned long long* stamps;  // TCAMD_X3_SMALLF_STAMP: per block [8] s_memrealtime (100 MHz) marks
 };
 
 // W = image side (14: half-image tiles, 7: whole images); PF = X K-steps in
@@ -1685,6 +1686,13 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
     half = 0;
   }
   if (img >= p.imgs) return;  // block-uniform, before any barrier
+  // diagnostic marks (wave 0): [0] entry [1] after B0 [2] 1x1 done [3] z
+  // handover [4] z complete [5] 3x3 MFMAs done [6] partials summed [7] exit
+  unsigned long long mk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto mark = [&](int i) {
+    if (p.stamps) mk[i] = __builtin_amdgcn_s_memrealtime();
+  };
+  mark(0);
   const int r0 = half * kRowsOut;
   const int zr0 = max(r0 - 1, 0), zr1 = min(r0 + kRowsOut + 1, W);
   const int TR = (zr1 - zr0) * W;  // z rows of the tile
@@ -1778,6 +1786,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
         for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
     const int rv = TR - 64 * wm;  // valid z rows from this wave's first
     ws_barrier();  // B0
+    mark(1);
     for (int q = 0; q < Qp; ++q) {
       if (q >= Q) {
         ws_barrier();
@@ -1836,6 +1845,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
       ws_barrier();  // B(q+1): stage q is free
     }
   }
+  mark(2);
   // BN2 bias of this consumer lane's channels, loaded BEFORE the 3x3
   // weights: a later load would make its wait drain the weight loads too
   f32x4 ob[2][4];
@@ -1861,6 +1871,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0(2 * kTaps));
   ws_barrier();
+  mark(3);
   // zero the padding of the tile image (columns 0 and W+1, rows outside the image)
   for (int i = tid; i < kNPad * 32; i += 512) {
     const int pos = i >> 5, piece = i & 31;
@@ -1900,6 +1911,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
 
   // ---- 3x3 phase: 8 waves = input-channel quarter kq x output half oh ----
   __syncthreads();  // z and its padding complete
+  mark(4);
   if (p.dbg & 1) return;
   int base[kNPG];
 #pragma unroll
@@ -1936,6 +1948,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   // C (16x16): lane (lane&15) = pixel of group pg, reg e -> channel 16oh + 4c + e
   // (c = lane>>4); wave (kq = c, oh) owns those 4 channels and adds the other
   // three waves' partials
+  mark(5);
   float* scr = reinterpret_cast<float*>(ldss + kNPad * kRowB);
   const int c4 = lane >> 4;
   constexpr int kSlot = kNPG * 64;
@@ -1955,6 +1968,17 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
       for (int src = 0; src < 3; ++src) v += *reinterpret_cast<const f32x4*>(sr + src * kSlot + pg * 64);
       const int o = 16 * pg + (lane & 15);
       if (o < kPOut) *reinterpret_cast<f32x4*>(p.y + (size_t)(m0 + o) * p.ldy + 16 * oh + 4 * kq) = v;
+    }
+  }
+  mark(6);
+  if (p.stamps && wave == 0) {
+    mark(7);
+    if (lane < 8) {
+      unsigned long long v = mk[0];
+#pragma unroll
+      for (int i = 1; i < 8; ++i)
+        if (lane == i) v = mk[i];
+      p.stamps[blockIdx.x * 8 + lane] = v;  // a vector store (lane-indexed)
     }
   }
 }
@@ -2672,6 +2696,20 @@ int tcamd_x3_dense_fused4(const float* x, int ldx, int imgs, int H, int W, int K
 }
 
 
+static unsigned long long* g_x3s_stamps = nullptr;  // TCAMD_X3_SMALLF_STAMP builds
+static int g_x3s_stamp_blocks = 0;
+
+// Copies the last stamped K14x launch's per-block marks ([blocks][8],
+// s_memrealtime ticks of 10 ns; blocks past the image count stay 0).
+int tcamd_x3_small_stamps(unsigned long long* out, int n) {
+  if (!g_x3s_stamps || !out) return 0;
+  const int m = std::min(n, 8 * g_x3s_stamp_blocks);
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(out, g_x3s_stamps, m * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return g_x3s_stamp_blocks;
+}
+
 // K14x: one dense layer of the 14x14 (half-image tiles) or 7x7 (whole-image
 // tiles) block in one kernel; w1 in the K8x [128][K] layout, w2 in
 // x3_w3f_fragments.  K a multiple of 32 (>= 64).
@@ -2702,6 +2740,13 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
   p.imgs = imgs;
   static const int dbg = getenv("TCAMD_X3_SMALLF_DBG") ? atoi(getenv("TCAMD_X3_SMALLF_DBG")) : 0;
   p.dbg = dbg;
+  static const bool stamp = getenv("TCAMD_X3_SMALLF_STAMP") && atoi(getenv("TCAMD_X3_SMALLF_STAMP"));
+  p.stamps = nullptr;
+  if (stamp) {
+    if (!g_x3s_stamps && hipMalloc((void**)&g_x3s_stamps, 8 * 4096 * sizeof(unsigned long long)) != hipSuccess)
+      return hipErrorOutOfMemory;
+    p.stamps = g_x3s_stamps;
+  }
   // X steps in flight in the producers' registers (TCAMD_X3_SMALLF_PF 3 or 6, A/B runs)
   static const int pf = getenv("TCAMD_X3_SMALLF_PF") ? atoi(getenv("TCAMD_X3_SMALLF_PF")) : 3;
   const void* const fns[2][2] = {{(const void*)x3_dense_small_kernel<14, 3>, (const void*)x3_dense_small_kernel<14, 6>},
@@ -2717,6 +2762,8 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
     attr_set[dev_slot].store(true, std::memory_order_release);
   }
   const int blocks = W == 14 ? (imgs + 7) / 8 * 16 : imgs;
+  if (stamp && blocks > 4096) return hipErrorInvalidValue;
+  g_x3s_stamp_blocks = blocks;
   void* args[] = {&p};
   const hipError_t e = hipLaunchKernel(fns[W == 14 ? 0 : 1][pf == 6 ? 1 : 0], dim3(blocks), dim3(512), args, kLdsSm,
                                        (hipStream_t)stream);

@@ -11,6 +11,8 @@ import json
 import os
 import sys
 
+import numpy as np
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
@@ -73,6 +75,20 @@ def layers(a, torch, hip):
             row = {"hw": hw, "imgs": a.imgs, "K": K, "pair_us": round(tp[len(tp) // 2], 2),
                    "k14x_us": round(tk[len(tk) // 2], 2), "k14x_min_us": round(tk[0], 2),
                    "x_TBps_k14x": round(gb / (tk[len(tk) // 2] * 1e-6) / 1e3, 2)}
+            if a.stamp:
+                k14()
+                torch.cuda.synchronize()
+                st = hip.x3_small_stamps()
+                st = st[st[:, 0] > 0]
+                t0 = st[:, 0].min()
+                rel = (st - t0) / 100.0  # us
+                ph = {"prologue": (1, 0), "1x1": (2, 1), "z_handover": (3, 2), "z_write": (4, 3), "3x3": (5, 4),
+                      "exchange_store": (6, 5)}
+                med = {k: round(float(np.median(rel[:, b] - rel[:, e])), 2) for k, (b, e) in ph.items()}
+                row["stamps"] = {"blocks": int(len(st)), "start_spread_us": round(float(rel[:, 0].max()), 2),
+                                 "span_us": round(float(rel[:, 7].max()), 2),
+                                 "end_spread_us": round(float(rel[:, 7].max() - rel[:, 7].min()), 2),
+                                 "median_phase_us": med}
             print(json.dumps(row), flush=True)
             out.append(row)
     return out
@@ -121,9 +137,12 @@ def main():
     ap.add_argument("--min-blocks", type=int, default=1)
     ap.add_argument("--no-layers", action="store_true")
     ap.add_argument("--pf", default="", help="TCAMD_X3_SMALLF_PF for this process (3 or 6)")
+    ap.add_argument("--stamp", action="store_true", help="in-kernel timeline marks of one launch per layer")
     a = ap.parse_args()
     if a.pf:
         os.environ["TCAMD_X3_SMALLF_PF"] = a.pf  # read by the library at its first K14x launch
+    if a.stamp:
+        os.environ["TCAMD_X3_SMALLF_STAMP"] = "1"
     import torch
 
     from triton_client_amd.ops import hip

@@ -225,6 +225,7 @@ _SIGS = {
         ctypes.c_int,
     ),
     "tcamd_x3_fused_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
+    "tcamd_x3_small_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "tcamd_x3_dense_fused4": (
         [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -768,6 +769,16 @@ def x3_dense_small(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo
     ``w2_*`` in x3_w3f_fragments; K a multiple of 32, >= 64."""
     _check(_load().tcamd_x3_dense_small(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
                                         w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_small")
+
+
+def x3_small_stamps(max_blocks=4096):
+    """Per-block timeline marks of the last K14x launch (TCAMD_X3_SMALLF_STAMP=1
+    processes): int64 array [blocks][8] of s_memrealtime ticks (10 ns)."""
+    out = np.zeros(8 * max_blocks, dtype=np.uint64)
+    n = _load().tcamd_x3_small_stamps(out.ctypes.data, out.size)
+    if n < 0:
+        raise HipError(n, "x3_small_stamps")
+    return out[:8 * n].reshape(n, 8).astype(np.int64)
 
 
 def x3_dense_fused4(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None):
