@@ -22,7 +22,12 @@ def main():
     ap.add_argument("--n", default="256,1024,4096")
     ap.add_argument("--mean-len", type=int, default=20)
     ap.add_argument("--reps", type=int, default=300)
+    ap.add_argument("--crossover-seq", action="store_true",
+                    help="replay tools/bytes_crossover.py's exact sequence (sizes 16,64,256,1024, host then device "
+                         "paths, same data), printing every step")
     a = ap.parse_args()
+    if a.crossover_seq:
+        return crossover_seq(a)
     from tritonclient.utils import hip_shared_memory as hipshm
     from tritonclient.utils import serialize_byte_tensor
 
@@ -55,6 +60,33 @@ def main():
         hipshm.destroy_shared_memory_region(h)
         print(json.dumps({"n": n, "bytes": len(want), "reps": a.reps, "k2_mismatch": bad_set, "k3_mismatch": bad_get,
                           "k3_errors": errs, "first": first}), flush=True)
+
+
+def crossover_seq(a):
+    from tritonclient.utils import hip_shared_memory as hipshm
+    from tritonclient.utils import serialize_byte_tensor
+
+    rng = np.random.default_rng(0)
+    for n in (16, 64, 256, 1024, 4096):
+        lens = rng.integers(0, 2 * a.mean_len + 1, n)
+        pool = rng.integers(97, 123, int(lens.sum()) + 1, dtype=np.uint8).tobytes()
+        offs = np.concatenate([[0], np.cumsum(lens)])
+        data = np.array([pool[offs[i]:offs[i + 1]] for i in range(n)], dtype=np.object_)
+        want = serialize_byte_tensor(data).item()
+        h = hipshm.create_shared_memory_region("xs_%d" % n, len(want) + 256, 0)
+        for path in ("host", "device"):
+            for r in range(a.reps):
+                print("n %d path %s rep %d set" % (n, path, r), flush=True)
+                hipshm.set_shared_memory_region(h, [data], serialize_bytes=True, bytes_path=path)
+                raw = hipshm.get_contents_as_numpy(h, np.uint8, [len(want)]).tobytes()
+                if raw != want:
+                    print("SET MISMATCH", n, path, r, flush=True)
+                print("n %d path %s rep %d get" % (n, path, r), flush=True)
+                out = hipshm.get_contents_as_numpy(h, np.object_, [n], bytes_path=path)
+                if list(out) != list(data):
+                    print("GET MISMATCH", n, path, r, flush=True)
+        hipshm.destroy_shared_memory_region(h)
+    print("CROSSOVER_SEQ_DONE", flush=True)
 
 
 if __name__ == "__main__":

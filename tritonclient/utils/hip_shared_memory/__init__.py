@@ -435,6 +435,19 @@ def get_contents_as_numpy(cuda_shm_handle, datatype, shape, offset=0, region_dat
         hip.memcpy_d2h(host, src, end, dev)
     except Exception as ex:
         raise CudaSharedMemoryException("failed to read cuda shared memory results") from ex
+    # the span K3 indexed is on the host now: re-walking it with the host
+    # codec costs a pass at memory speed and catches an index that does not
+    # match the chain (then the host walk's result is returned)
+    from triton_client_amd.ops import host_codec
+
+    ho = np.empty(n, dtype=np.uint64)
+    hl = np.empty(n, dtype=np.uint32)
+    k, _ = host_codec.load().scan_prefix(host, ho, hl, n)
+    if k != n or not (np.array_equal(ho, offs) and np.array_equal(hl, lens)):
+        import warnings
+
+        warnings.warn("hip_shared_memory: the device BYTES index disagreed with the host walk; using the host walk")
+        host, offs, lens = _index_bytes_host(hip, src, nbytes, n, dev)
     mv = memoryview(host)
     out[:] = [bytes(mv[o:o + ln]) for o, ln in zip(offs.tolist(), lens.tolist())]
     return out.reshape(shape)
