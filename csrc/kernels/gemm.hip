@@ -42,7 +42,7 @@ typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 constexpr int kBM = 256, kBN = 256, kBK = 64;
 constexpr int kTileB = kBM * kBK * 2;        // 32 KB: one operand tile
 constexpr int kBufB = 2 * kTileB;            // W tile | X tile
-constexpr int kLdsG = 2 * kBufB;             // two buffers: 128 KB
+constexpr int kLdsG = 2 * kBufB + 8192;      // two buffers: 128 KB (+ 8 KB L2 warm-up trash)
 
 struct GemmParams {
   const uint16_t* x;  // [M][ldx]
@@ -108,7 +108,12 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, f32x4 (&acc)[4][8]
 // instead of all before the step's LDS reads (an LDS-DMA piece costs ~60-185
 // issue cycles; issued in a burst by every wave at once they stall the
 // matrix pipe at the top of each step)
-template <int EPI, bool SPREAD = false>
+// L2PF: one more LDS-DMA per thread per step warms L2 with the operand lines
+// of the step after next (one 128-B line = one tile row's 64 k; the bytes land
+// in a 8 KB trash area of LDS), so the next step's real copies are L2 hits;
+// the step barrier is then raw with a counted vmcnt(1) (the warm-up copy may
+// stay in flight across it)
+template <int EPI, bool SPREAD = false, bool L2PF = false>
 __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -153,12 +158,25 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.K / kBK;
+  // L2 warm-up source: thread t -> W row t (t < 256) or X row t - 256
+  const uint16_t* srcl2 = tid < 256 ? p.w + (size_t)(n0 + tid) * p.ldw
+                                    : p.x + (size_t)min(m0 + tid - 256, p.M - 1) * p.ldx;
+  auto warm = [&](int kt) {
+    __builtin_amdgcn_global_load_lds((const void*)(srcl2 + (size_t)kt * kBK), (void*)(lds + 2 * kBufB + wave * 1024),
+                                     16, 0, 0);
+  };
   stage(0, 0);
+  if constexpr (L2PF) {
+    if (nk > 1) warm(1);
+  }
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     const bool more = kt + 1 < nk;
     if (!SPREAD && more) stage(kt + 1, buf ^ 1);
+    if constexpr (L2PF) {
+      if (kt + 2 < nk) warm(kt + 2);  // issued after the copies: it may stay in flight past the barrier
+    }
     const uint8_t* tw = lds + buf * kBufB;
     const uint8_t* tx = tw + kTileB;
 #pragma unroll
@@ -180,7 +198,16 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
       }
       __builtin_amdgcn_s_setprio(0);
     }
-    __syncthreads();  // the next step's DMA landed; this buffer's reads are done
+    if constexpr (L2PF) {
+      // the next step's 8 copies landed; the warm-up issued after them may not
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 2 < nk) __builtin_amdgcn_s_waitcnt(0x0071);  // vmcnt(1) lgkmcnt(0)
+      else __builtin_amdgcn_s_waitcnt(0x0070);            // vmcnt(0) lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      __syncthreads();  // the next step's DMA landed; this buffer's reads are done
+    }
   }
 
   epilogue<EPI>(p, acc, m0, n0, wm, wn, fr16, fq);
@@ -354,17 +381,20 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
   p.nt = N / kBN;
   // TCAMD_GEMM_V: 1 = one barrier per K step (default), 2 = the phased
   // kernel, 3 = phased with the two wave groups one phase apart, 4 = one
-  // barrier per step with the DMA spread over the MFMA groups
+  // barrier per step with the DMA spread over the MFMA groups, 5 = 1 with the
+  // L2 warm-up of the step after next
   static const int ver = getenv("TCAMD_GEMM_V") ? atoi(getenv("TCAMD_GEMM_V")) : 1;
-  const void* all[4][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
+  const void* all[5][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
                             (const void*)gemm_bf16_kernel<2>, (const void*)gemm_bf16_kernel<3>},
                            {(const void*)gemm_bf16_ph_kernel<0, false>, (const void*)gemm_bf16_ph_kernel<1, false>,
                             (const void*)gemm_bf16_ph_kernel<2, false>, (const void*)gemm_bf16_ph_kernel<3, false>},
                            {(const void*)gemm_bf16_ph_kernel<0, true>, (const void*)gemm_bf16_ph_kernel<1, true>,
                             (const void*)gemm_bf16_ph_kernel<2, true>, (const void*)gemm_bf16_ph_kernel<3, true>},
                            {(const void*)gemm_bf16_kernel<0, true>, (const void*)gemm_bf16_kernel<1, true>,
-                            (const void*)gemm_bf16_kernel<2, true>, (const void*)gemm_bf16_kernel<3, true>}};
-  const void* const* fns = all[(ver >= 2 && ver <= 4) ? ver - 1 : 0];
+                            (const void*)gemm_bf16_kernel<2, true>, (const void*)gemm_bf16_kernel<3, true>},
+                           {(const void*)gemm_bf16_kernel<0, false, true>, (const void*)gemm_bf16_kernel<1, false, true>,
+                            (const void*)gemm_bf16_kernel<2, false, true>, (const void*)gemm_bf16_kernel<3, false, true>}};
+  const void* const* fns = all[(ver >= 2 && ver <= 5) ? ver - 1 : 0];
   // dynamic-LDS opt-in once per device (cached only after every call succeeded)
   static std::atomic<bool> attr_set[64];
   int dev = 0;
