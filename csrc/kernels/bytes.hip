@@ -56,6 +56,8 @@
 
 #include <stdlib.h>
 
+#include <mutex>
+
 #include "kernels/common.h"
 
 using namespace tcamd;
@@ -1364,6 +1366,61 @@ extern "C" int tcamd_pack_bytes_strided(const void* data, uint64_t stride, const
   return pack_impl(data, stride, lens, n, out, workspace, stream);
 }
 
+// K3 workspace: one grow-only hipMalloc per device, owned by the call that
+// holds g_ix_mu (tcamd_index_bytes holds it from start to end and
+// synchronises its stream before returning, so no launch can still read the
+// buffer when the next call, on any stream, reuses or replaces it).  The
+// stream-ordered pool (hipMallocAsync / hipFreeAsync per call) was dropped in
+// round 4: unserialised runs of many back-to-back calls saw wrong element
+// counts and an illegal-address error that never showed with kernels and
+// copies serialised (AMD_SERIALIZE_KERNEL=3), and a fixed buffer takes the
+// pool's map / trim out of the picture.
+constexpr int kIxMaxDev = 64;
+static std::mutex g_ix_mu;
+static void* g_ix_ws[kIxMaxDev] = {};
+static size_t g_ix_bytes[kIxMaxDev] = {};
+constexpr size_t kIxKeepMax = 256ull << 20;  // larger one-off workspaces are freed after the call
+
+static hipError_t ix_workspace(hipStream_t s, size_t need, void** out) {
+  int dev = 0;
+  hipError_t e = hipStreamGetDevice(s, &dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= kIxMaxDev) return hipErrorInvalidDevice;
+  if (need > g_ix_bytes[dev]) {
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != dev) (void)hipSetDevice(dev);
+    if (g_ix_ws[dev]) {
+      (void)hipFree(g_ix_ws[dev]);  // synchronising; earlier calls already drained their streams
+      g_ix_ws[dev] = nullptr;
+      g_ix_bytes[dev] = 0;
+    }
+    size_t sz = need < (4ull << 20) ? (4ull << 20) : need;
+    sz = (sz + (2ull << 20) - 1) & ~((2ull << 20) - 1);
+    e = hipMalloc(&g_ix_ws[dev], sz);
+    if (e == hipSuccess) g_ix_bytes[dev] = sz;
+    else g_ix_ws[dev] = nullptr;
+    if (prev != dev) (void)hipSetDevice(prev);
+    if (e != hipSuccess) return e;
+  }
+  *out = g_ix_ws[dev];
+  return hipSuccess;
+}
+
+// Drops an oversized workspace once the call that needed it is done.
+static void ix_workspace_trim(hipStream_t s) {
+  int dev = 0;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess || dev < 0 || dev >= kIxMaxDev) return;
+  if (g_ix_bytes[dev] <= kIxKeepMax) return;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  if (prev != dev) (void)hipSetDevice(dev);
+  (void)hipFree(g_ix_ws[dev]);
+  g_ix_ws[dev] = nullptr;
+  g_ix_bytes[dev] = 0;
+  if (prev != dev) (void)hipSetDevice(prev);
+}
+
 // Round-2 general path (every byte position a candidate; 10 B of tables per
 // input byte): only for chains the v3 walk cannot resolve.
 static int index_general(const void* buf, uint64_t nbytes, uint64_t n_expected, uint64_t* offs, uint32_t* lens,
@@ -1372,9 +1429,9 @@ static int index_general(const void* buf, uint64_t nbytes, uint64_t n_expected, 
   // parallel path: stream-ordered scratch (exit u64 + count u16 per byte, entry/base per block)
   const uint64_t nblk = (nbytes + kIdxB - 1) / kIdxB;
   const uint64_t nsb = (nblk + kS - 1) / kS;
-  void* ws = nullptr;
   const size_t wsb = nbytes * 8 + nbytes * 2 + 16 + nblk * 16 + nblk * kR * 6 + nsb * kR * 8 + nsb * 12 + 64;
-  hipError_t e = hipMallocAsync(&ws, wsb, s);
+  void* ws = nullptr;
+  hipError_t e = ix_workspace(s, wsb, &ws);
   if (e != hipSuccess) return e;
   uint64_t* exit_pos = (uint64_t*)ws;
   uint16_t* count = (uint16_t*)(exit_pos + nbytes);
@@ -1399,9 +1456,7 @@ static int index_general(const void* buf, uint64_t nbytes, uint64_t n_expected, 
                      status, fast);
   hipLaunchKernelGGL(idx_emit, dim3((unsigned)nblk), dim3(kBlock), 0, s, (const uint8_t*)buf, nbytes, entry, base,
                      n_expected, offs, lens);
-  e = hipGetLastError();
-  hipError_t f = hipFreeAsync(ws, s);
-  return e != hipSuccess ? e : f;
+  return hipGetLastError();
 }
 
 // v3 speculative walk over a window of the data; returns the (host) status
@@ -1415,7 +1470,7 @@ static int index_v3(const uint8_t* buf, uint64_t nbytes, uint64_t window, uint64
   const size_t wsb = nblk * (size_t)xr * 4 + nblk * 4 + nblk * 4 + nblk * 8 + (nc + 1) * 8 + sizeof(IxCtl) + 256 +
                      nblk * (kXB / 4) * 2 + nblk * 4 + 256;
   void* ws = nullptr;
-  hipError_t e = hipMallocAsync(&ws, wsb, s);
+  hipError_t e = ix_workspace(s, wsb, &ws);
   if (e != hipSuccess) return e;
   uint64_t* count = (uint64_t*)ws;
   uint64_t* ctop = count + nblk;
@@ -1453,10 +1508,9 @@ static int index_v3(const uint8_t* buf, uint64_t nbytes, uint64_t window, uint64
                        lens, rec, rec_head);
     e = hipGetLastError();
   }
-  hipError_t f = hipFreeAsync(ws, s);
   if (e != hipSuccess) return e;
   *host_status = hs[0];
-  return f;
+  return hipSuccess;
 }
 
 // status: device int[4]: [0] = 0 ok / 1 fewer elements than expected / -1
@@ -1472,16 +1526,29 @@ extern "C" int tcamd_index_bytes_last_path(uint64_t* window) {
   return g_last_path;
 }
 
+static int index_locked(const void* buf, uint64_t nbytes, uint64_t n_expected, uint64_t* offs, uint32_t* lens,
+                        int* status, hipStream_t s);
+
 extern "C" int tcamd_index_bytes(const void* buf, uint64_t nbytes, uint64_t n_expected, uint64_t* offs,
                                  uint32_t* lens, int* status, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   g_last_window = 0;
-  if (nbytes <= 8192 || n_expected <= 256) {
+  if (nbytes <= 8192 || n_expected <= 256) {  // one workgroup, no workspace
     g_last_path = 0;
     hipLaunchKernelGGL(index_bytes, dim3(1), dim3(kBlock), 0, s, (const uint8_t*)buf, nbytes, n_expected, offs,
                        lens, status);
     return hipGetLastError();
   }
+  std::lock_guard<std::mutex> lk(g_ix_mu);
+  const int rc = index_locked(buf, nbytes, n_expected, offs, lens, status, s);
+  // the workspace is free for the next call once this stream drained
+  const hipError_t f = hipStreamSynchronize(s);
+  ix_workspace_trim(s);
+  return rc != hipSuccess ? rc : f;
+}
+
+static int index_locked(const void* buf, uint64_t nbytes, uint64_t n_expected, uint64_t* offs, uint32_t* lens,
+                        int* status, hipStream_t s) {
   static const int mode = getenv("TCAMD_K3_MODE") ? atoi(getenv("TCAMD_K3_MODE")) : 0;  // 1: general path only
   if (mode != 1) {
     uint64_t need = 64 * n_expected;
@@ -1510,5 +1577,5 @@ extern "C" int tcamd_index_bytes(const void* buf, uint64_t nbytes, uint64_t n_ex
     }
   }
   g_last_path = 2;
-  return index_general(buf, nbytes, n_expected, offs, lens, status, stream);
+  return index_general(buf, nbytes, n_expected, offs, lens, status, s);
 }

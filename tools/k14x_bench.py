@@ -78,14 +78,14 @@ def layers(a, torch, hip):
             if a.stamp:
                 k14()
                 torch.cuda.synchronize()
-                st = hip.x3_small_stamps()
-                st = st[st[:, 0] > 0]
-                t0 = st[:, 0].min()
-                rel = (st - t0) / 100.0  # us
+                sm = hip.x3_small_stamps()
+                sm = sm[sm[:, 0] > 0]
+                t0 = sm[:, 0].min()
+                rel = (sm - t0) / 100.0  # us
                 ph = {"prologue": (1, 0), "1x1": (2, 1), "z_handover": (3, 2), "z_write": (4, 3), "3x3": (5, 4),
                       "exchange_store": (6, 5)}
                 med = {k: round(float(np.median(rel[:, b] - rel[:, e])), 2) for k, (b, e) in ph.items()}
-                row["stamps"] = {"blocks": int(len(st)), "start_spread_us": round(float(rel[:, 0].max()), 2),
+                row["stamps"] = {"blocks": int(len(sm)), "start_spread_us": round(float(rel[:, 0].max()), 2),
                                  "span_us": round(float(rel[:, 7].max()), 2),
                                  "end_spread_us": round(float(rel[:, 7].max() - rel[:, 7].min()), 2),
                                  "median_phase_us": med}
