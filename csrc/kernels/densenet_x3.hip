@@ -1638,8 +1638,9 @@ x3_dense_fused4_kernel(X3FusedParams p) {
 //
 // HBM per layer: the input X once (+ the halo rows through L2) and 32 output
 // channels; one launch.  LDS: 4 K-step stages (128 KB), then z + scratch.
-constexpr int kSmS = 4;
-constexpr int kLdsSm = kSmS * kWsStage;  // 128 KB (z and the 3x3 scratch alias it once the 1x1 drained)
+// K-step stages (kSmS below): 4 (128 KB) or 5 (160 KB: the W copies one more
+// step ahead; TCAMD_X3_SMALLF_STAGES); z and the 3x3 scratch alias them once
+// the 1x1 drained
 
 struct X3SmallParams {
   const float* x;  // block buffer rows of ldx (the layer's first K channels)
@@ -1658,8 +1659,9 @@ struct X3SmallParams {
 
 // W = image side (14: half-image tiles, 7: whole images); PF = X K-steps in
 // the producers' registers
-template <int W, int PF>
+template <int W, int PF, int kSmS>
 __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p) {
+  constexpr int kLdsSm = kSmS * kWsStage;
   constexpr int kHalves = W == 14 ? 2 : 1;
   constexpr int kRowsOut = W / kHalves;              // 7
   constexpr int kPW = W + 2, kPR = kRowsOut + 2;     // padded tile image
@@ -2747,26 +2749,34 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
       return hipErrorOutOfMemory;
     p.stamps = g_x3s_stamps;
   }
-  // X steps in flight in the producers' registers (TCAMD_X3_SMALLF_PF 3 or 6, A/B runs)
+  // X steps in flight in the producers' registers (TCAMD_X3_SMALLF_PF 3 or 6)
+  // and K-step stages (TCAMD_X3_SMALLF_STAGES 4 or 5), for A/B runs
   static const int pf = getenv("TCAMD_X3_SMALLF_PF") ? atoi(getenv("TCAMD_X3_SMALLF_PF")) : 3;
-  const void* const fns[2][2] = {{(const void*)x3_dense_small_kernel<14, 3>, (const void*)x3_dense_small_kernel<14, 6>},
-                                 {(const void*)x3_dense_small_kernel<7, 3>, (const void*)x3_dense_small_kernel<7, 6>}};
+  static const int ns = getenv("TCAMD_X3_SMALLF_STAGES") ? atoi(getenv("TCAMD_X3_SMALLF_STAGES")) : 4;
+  const void* const fns[2][2][2] = {
+      {{(const void*)x3_dense_small_kernel<14, 3, 4>, (const void*)x3_dense_small_kernel<14, 3, 5>},
+       {(const void*)x3_dense_small_kernel<14, 6, 4>, (const void*)x3_dense_small_kernel<14, 6, 5>}},
+      {{(const void*)x3_dense_small_kernel<7, 3, 4>, (const void*)x3_dense_small_kernel<7, 3, 5>},
+       {(const void*)x3_dense_small_kernel<7, 6, 4>, (const void*)x3_dense_small_kernel<7, 6, 5>}}};
   static std::atomic<bool> attr_set[kMaxDevices];
   const int dev_slot = device_slot();
   if (!attr_set[dev_slot].load(std::memory_order_acquire)) {
-    for (const auto& r : fns)
-      for (const void* f : r) {
-        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsSm);
-        if (e != hipSuccess) return e;
-      }
+    for (int w = 0; w < 2; ++w)
+      for (int f = 0; f < 2; ++f)
+        for (int n = 0; n < 2; ++n) {
+          const hipError_t e =
+              hipFuncSetAttribute(fns[w][f][n], hipFuncAttributeMaxDynamicSharedMemorySize, (4 + n) * kWsStage);
+          if (e != hipSuccess) return e;
+        }
     attr_set[dev_slot].store(true, std::memory_order_release);
   }
   const int blocks = W == 14 ? (imgs + 7) / 8 * 16 : imgs;
   if (stamp && blocks > 4096) return hipErrorInvalidValue;
   g_x3s_stamp_blocks = blocks;
   void* args[] = {&p};
-  const hipError_t e = hipLaunchKernel(fns[W == 14 ? 0 : 1][pf == 6 ? 1 : 0], dim3(blocks), dim3(512), args, kLdsSm,
-                                       (hipStream_t)stream);
+  const int n5 = ns == 5 ? 1 : 0;
+  const hipError_t e = hipLaunchKernel(fns[W == 14 ? 0 : 1][pf == 6 ? 1 : 0][n5], dim3(blocks), dim3(512), args,
+                                       (4 + n5) * kWsStage, (hipStream_t)stream);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }

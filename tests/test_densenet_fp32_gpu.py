@@ -359,6 +359,53 @@ def test_x3_dense_small(imgs, H, K):
     assert _rel(x[:, K:K + 32], y2[:, K:K + 32]) < 2e-5
 
 
+@pytest.mark.parametrize("pf,stages", [("6", "4"), ("3", "5"), ("6", "5")])
+def test_x3_dense_small_variants(pf, stages):
+    """K14x's A/B variants (TCAMD_X3_SMALLF_PF: X steps in the producers'
+    registers; TCAMD_X3_SMALLF_STAGES: K-step stages, 5 = 160 KB of LDS), chosen
+    once per process, so in a child process: the same fp64 comparison as
+    test_x3_dense_small on shapes that cover every padding-round count."""
+    _need_gpu()
+    import os
+    import subprocess
+    import sys
+
+    code = r'''
+import torch, torch.nn.functional as F
+from triton_client_amd.ops import hip
+st = torch.cuda.current_stream().cuda_stream
+def split(t):
+    h = t.to(torch.bfloat16)
+    return h.contiguous(), (t - h.float()).to(torch.bfloat16).contiguous()
+for imgs, H, K in [(3, 14, 256), (9, 14, 992), (17, 14, 640), (16, 14, 96), (5, 7, 992), (2, 7, 64), (40, 14, 416)]:
+    g = torch.Generator(device="cuda").manual_seed(imgs * 131 + H * 7 + K)
+    M, ldx = imgs * H * H, K + 96
+    x = torch.randn(M, ldx, device="cuda", generator=g)
+    s = torch.rand(K, device="cuda", generator=g) + 0.5
+    t = torch.randn(K, device="cuda", generator=g) * 0.2
+    w1 = torch.randn(128, K, device="cuda", generator=g) / K ** 0.5
+    b1 = torch.randn(128, device="cuda", generator=g) * 0.1
+    w2 = torch.randn(32, 128, 3, 3, device="cuda", generator=g) / (9 * 128) ** 0.5
+    w1h, w1l = split(w1)
+    f2h, f2l = (hip.x3_w3f_fragments(u) for u in split(w2.permute(0, 2, 3, 1).reshape(32, -1)))
+    xc = x.clone()
+    hip.x3_dense_small(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), w1h.data_ptr(), w1l.data_ptr(),
+                       b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), x.data_ptr() + 4 * K, ldx, stream=st)
+    torch.cuda.synchronize()
+    a = torch.relu(xc[:, :K].double() * s.double() + t.double())
+    z = torch.relu(a @ w1.double().t() + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
+    ref = F.conv2d(z, w2.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 32)
+    err = ((x[:, K:K + 32].double() - ref).norm() / ref.norm()).item()
+    assert err < 3e-5, (imgs, H, K, err)
+    assert torch.equal(x[:, :K], xc[:, :K]) and torch.equal(x[:, K + 32:], xc[:, K + 32:])
+print("K14X_VARIANT_OK")
+'''
+    env = dict(os.environ, TCAMD_X3_SMALLF_PF=pf, TCAMD_X3_SMALLF_STAGES=stages)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "K14X_VARIANT_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_x3_dense_small_rejects_bad_shapes():
     _need_gpu()
     hip = _hip()
