@@ -1653,7 +1653,8 @@ struct X3SmallParams {
   const uint16_t* w2_lo;
   float* y;               // [pixels][ldy] fp32, offset to the layer's 32-channel slice
   int ldx, K, ldy, imgs;
-  int dbg;                // ablation (TCAMD_X3_SMALLF_DBG): 1 = no 3x3 phase
+  int dbg;                // ablation (TCAMD_X3_SMALLF_DBG): 1 = no 3x3 phase, 2 = X rows of image 0 only,
+                          // 4 = no 1x1 MFMAs, 8 = no W copies (results invalid with 4 / 8)
   unsigned long long* stamps;  // TCAMD_X3_SMALLF_STAMP: per block [8] s_memrealtime (100 MHz) marks
 };
 
@@ -1720,11 +1721,13 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
       xt[slot] = ldf4(p.t1 + k0 + 4 * pj);
 #pragma unroll
       for (int i = 0; i < kNRI; ++i) {
-        const int m = mz0 + min(prow + 32 * i, TR - 1);
+        // ablation 2: every block reads image 0's rows (X L2-resident)
+        const int m = ((p.dbg & 2) ? zr0 * W : mz0) + min(prow + 32 * i, TR - 1);
         xr[slot][i] = ldf4(p.x + (size_t)m * p.ldx + k0 + 4 * pj);
       }
     };
     auto issue_w = [&](int q) {
+      if (p.dbg & 8) return;  // ablation 8: no W copies (the stages keep stale W)
       q = min(q, Q - 1);
       const int k0 = kofs(q);
       uint8_t* st = ldss + (q % kSmS) * kWsStage + 2 * kWsPlane;
@@ -1795,6 +1798,10 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
         continue;
       }
       const uint8_t* st = ldss + (q % kSmS) * kWsStage;
+      if (p.dbg & 4) {  // ablation 4: no MFMAs / stage reads
+        ws_barrier();
+        continue;
+      }
       if constexpr (kQ4) {
         // 7x7: the tile is <= 64 rows, so the 4 waves split the 128 channels
         // instead (wave = 32-channel quarter x both 32-pixel blocks)

@@ -64,13 +64,15 @@ def test_unserialized_bytes_packed_by_k2_and_indexed_by_k3(hipshm):
     hipshm.set_shared_memory_region(h, [head, data], serialize_bytes=True)  # int32 head, then K2 at offset 32
     raw = hipshm.get_contents_as_numpy(h, np.uint8, [32 + len(ser)])
     assert raw[32:].tobytes() == ser
-    out = hipshm.get_contents_as_numpy(h, np.object_, [100, 200], offset=32)
-    assert out.shape == (100, 200) and list(out.ravel()) == list(data.ravel())
+    for path in ("device", "auto"):  # K3 / the host walk ("auto" always walks on the host)
+        out = hipshm.get_contents_as_numpy(h, np.object_, [100, 200], offset=32, bytes_path=path)
+        assert out.shape == (100, 200) and list(out.ravel()) == list(data.ravel())
     # asking for more elements than the region holds is an error, not garbage
     small = hipshm.create_shared_memory_region("rk3", len(serialize_byte_tensor(data[:1]).item()), 0)
     hipshm.set_shared_memory_region(small, [data[:1]], serialize_bytes=True)
-    with pytest.raises(hipshm.CudaSharedMemoryException):
-        hipshm.get_contents_as_numpy(small, np.object_, [400])
+    for path in ("device", "auto"):
+        with pytest.raises(hipshm.CudaSharedMemoryException):
+            hipshm.get_contents_as_numpy(small, np.object_, [400], bytes_path=path)
     hipshm.destroy_shared_memory_region(small)
     hipshm.destroy_shared_memory_region(h)
 

@@ -136,19 +136,31 @@ def _as_bytes(v):
     return v.reshape(-1).view(np.uint8)  # np.bytes_ too: size * itemsize raw bytes
 
 
-# BYTES tensors of at most this many elements are packed / indexed on the
-# host (C++ codec, one H2D or D2H of the span) instead of by K2 / K3 on the
-# device: below the crossover the device path's fixed cost (scratch, three
-# stream syncs, the offsets/lengths copies) dominates.  Measured with
-# tools/bytes_crossover.py (profiles/r4_bytes_crossover.md);
-# TCAMD_BYTES_HOST_MAX overrides, 0 = always the device kernels.
-_BYTES_HOST_MAX = int(os.environ.get("TCAMD_BYTES_HOST_MAX", "4096"))
+# bytes_path="auto" for BYTES tensors (measured with tools/bytes_crossover.py
+# on MI355X, mean string length 20: profiles/r4_bytes_crossover.md):
+# * set: up to _BYTES_HOST_MAX elements the C++ host codec packs the stream
+#   and one H2D copies it; above it K2 packs on the device.  The host wins up
+#   to 4096 elements (413 vs 442 us), K2 from 16384 on (1.67 vs 1.78 ms) and by
+#   ~12% at 1e6.
+# * get: the host walk over a prefix copied D2H won at every size measured
+#   (16 .. 1e6 elements: the K3 path needs the same D2H of the span plus three
+#   stream syncs and the offsets / lengths copies), so "auto" always walks on
+#   the host unless _BYTES_GET_DEVICE_MIN is set; "device" still runs K3.
+# TCAMD_BYTES_HOST_MAX / TCAMD_BYTES_GET_DEVICE_MIN override (0 = always K2 /
+# K3 above 0 elements).
+_BYTES_HOST_MAX = int(os.environ.get("TCAMD_BYTES_HOST_MAX", "8192"))
+_BYTES_GET_DEVICE_MIN = (int(os.environ["TCAMD_BYTES_GET_DEVICE_MIN"])
+                         if os.environ.get("TCAMD_BYTES_GET_DEVICE_MIN") else None)
 
 
-def _bytes_on_host(n, path):
+def _bytes_on_host(n, path, get=False):
     if path not in ("auto", "host", "device"):
         raise CudaSharedMemoryException("bytes_path must be auto, host or device")
-    return path == "host" or (path == "auto" and n <= _BYTES_HOST_MAX)
+    if path != "auto":
+        return path == "host"
+    if get:
+        return _BYTES_GET_DEVICE_MIN is None or n < _BYTES_GET_DEVICE_MIN
+    return n <= _BYTES_HOST_MAX
 
 
 def _index_bytes_host(hip, src, nbytes, n, dev):
@@ -335,10 +347,11 @@ def get_contents_as_numpy(cuda_shm_handle, datatype, shape, offset=0, region_dat
 
     Only the requested bytes are copied (the reference copies the whole
     region every call, tc/utils/cuda_shared_memory/__init__.py:266-276).
-    BYTES: K3 indexes the ``<u32 len>||bytes`` chain on the device, then only
-    the bytes the elements span come back; up to ``_BYTES_HOST_MAX`` elements
-    (``bytes_path="auto"``; or ``"host"`` / ``"device"``) the chain is walked
-    on the host instead, over a prefix copied in growing chunks.
+    BYTES: the ``<u32 len>||bytes`` chain is walked on the host over a prefix
+    copied in growing chunks (``bytes_path="auto"`` / ``"host"``; measured
+    faster than the device index at every size), or indexed by K3 on the
+    device (``"device"``), after which only the bytes the elements span come
+    back.
     ``region_datatype`` (BF16 / FP16 /
     FP8_E4M3 / FP8_E5M2) with a float32 ``datatype``: the region holds that
     narrow type and is widened to float32 on the GPU before the copy.
@@ -394,7 +407,7 @@ def get_contents_as_numpy(cuda_shm_handle, datatype, shape, offset=0, region_dat
     out = np.empty(n, dtype=np.object_)
     if n == 0:
         return out.reshape(shape)
-    if _bytes_on_host(n, bytes_path):
+    if _bytes_on_host(n, bytes_path, get=True):
         try:
             host, offs, lens = _index_bytes_host(hip, src, nbytes, n, dev)
         except CudaSharedMemoryException:
