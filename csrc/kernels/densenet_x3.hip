@@ -1654,7 +1654,8 @@ struct X3SmallParams {
   float* y;               // [pixels][ldy] fp32, offset to the layer's 32-channel slice
   int ldx, K, ldy, imgs;
   int dbg;                // ablation (TCAMD_X3_SMALLF_DBG): 1 = no 3x3 phase, 2 = X rows of image 0 only,
-                          // 4 = no 1x1 MFMAs, 8 = no W copies (results invalid with 4 / 8)
+                          // 4 = no 1x1 MFMAs, 8 = no W copies, 16 = no X conversion (results
+                          // invalid with 4 / 8 / 16)
   unsigned long long* stamps;  // TCAMD_X3_SMALLF_STAMP: per block [8] s_memrealtime (100 MHz) marks
 };
 
@@ -1740,6 +1741,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
       }
     };
     auto write_x = [&](int q, int slot) {
+      if (p.dbg & 16) return;  // ablation 16: no X conversion / stage writes
       uint8_t* st = ldss + (q % kSmS) * kWsStage;
       const f32x4 sc = xs[slot], sb = xt[slot];
 #pragma unroll
