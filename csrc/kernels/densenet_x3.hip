@@ -1661,8 +1661,14 @@ struct X3SmallParams {
 
 // W = image side (14: half-image tiles, 7: whole images); PF = X K-steps in
 // the producers' registers
-template <int W, int PF, int kSmS>
+// LEAD = K steps between a stage's fill and its MFMAs: 1 (the consumer reads
+// each stage after the barrier that publishes it) or 2 (the producer fills
+// stage q+2 while the consumer runs step q from registers and reads stage q+1
+// into a second operand set: the stage reads overlap the MFMAs;
+// TCAMD_X3_SMALLF_LEAD)
+template <int W, int PF, int kSmS, int LEAD>
 __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p) {
+  static_assert(LEAD == 1 || LEAD == 2, "K14x lead");
   constexpr int kLdsSm = kSmS * kWsStage;
   constexpr int kHalves = W == 14 ? 2 : 1;
   constexpr int kRowsOut = W / kHalves;              // 7
@@ -1760,27 +1766,60 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
     };
 #pragma unroll
     for (int s = 0; s < PF; ++s) issue_x(s, s);
-    for (int s = 0; s <= kSmS - 3; ++s) issue_w(s);
-    __builtin_amdgcn_s_waitcnt(ws_vmcnt(0));
-    write_x(0, 0);
-    issue_w(kSmS - 2);
-    __builtin_amdgcn_sched_barrier(0);
-    issue_x(PF, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    ws_barrier();  // B0
-    for (int q0 = 0; q0 < Qp; q0 += PF) {
+    if constexpr (LEAD == 1) {
+      for (int s = 0; s <= kSmS - 3; ++s) issue_w(s);
+      __builtin_amdgcn_s_waitcnt(ws_vmcnt(0));
+      write_x(0, 0);
+      issue_w(kSmS - 2);
+      __builtin_amdgcn_sched_barrier(0);
+      issue_x(PF, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      ws_barrier();  // B0
+      for (int q0 = 0; q0 < Qp; q0 += PF) {
 #pragma unroll
-      for (int u = 0; u < PF; ++u) {
-        const int q = q0 + u;
-        const int slot = (u + 1) % PF;
-        __builtin_amdgcn_s_waitcnt(ws_vmcnt(kOps * (PF - 1)));  // X of step q+1
-        __builtin_amdgcn_sched_barrier(0);
-        write_x(q + 1, slot);
-        issue_w(q + kSmS - 1);
-        __builtin_amdgcn_sched_barrier(0);  // W copies ahead of the X loads (vmcnt retires in order)
-        issue_x(q + 1 + PF, slot);
-        __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0((2 + kNRI) + kOps * (kSmS - 2)));  // W of step q+1
-        ws_barrier();  // B(q+1)
+        for (int u = 0; u < PF; ++u) {
+          const int q = q0 + u;
+          const int slot = (u + 1) % PF;
+          __builtin_amdgcn_s_waitcnt(ws_vmcnt(kOps * (PF - 1)));  // X of step q+1
+          __builtin_amdgcn_sched_barrier(0);
+          write_x(q + 1, slot);
+          issue_w(q + kSmS - 1);
+          __builtin_amdgcn_sched_barrier(0);  // W copies ahead of the X loads (vmcnt retires in order)
+          issue_x(q + 1 + PF, slot);
+          __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0((2 + kNRI) + kOps * (kSmS - 2)));  // W of step q+1
+          ws_barrier();  // B(q+1)
+        }
+      }
+    } else {
+      // stages 0 and 1 complete before B0; then interval q (B(q) .. B(q+1))
+      // fills stage q+2: X(q+2) from the registers, W(q+kSmS-1) by DMA, and
+      // waits for W(q+2).  The prologue's "iterations" -2 (X only) and -1
+      // (W + X) keep every later iteration's counted waits exact.
+      for (int s = 0; s <= kSmS - 3; ++s) issue_w(s);
+      __builtin_amdgcn_s_waitcnt(ws_vmcnt(0));
+      write_x(0, 0);
+      write_x(1, 1 % PF);
+      __builtin_amdgcn_sched_barrier(0);
+      issue_x(PF, 0);
+      issue_w(kSmS - 2);
+      __builtin_amdgcn_sched_barrier(0);
+      issue_x(PF + 1, 1 % PF);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      ws_barrier();  // B0
+      for (int q0 = 0; q0 < Qp; q0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+          const int q = q0 + u;
+          const int slot = (u + 2) % PF;
+          __builtin_amdgcn_s_waitcnt(ws_vmcnt(kOps * (PF - 1)));  // X of step q+2
+          __builtin_amdgcn_sched_barrier(0);
+          write_x(q + 2, slot);
+          issue_w(q + kSmS - 1);
+          __builtin_amdgcn_sched_barrier(0);
+          issue_x(q + 2 + PF, slot);
+          __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0((2 + kNRI) + kOps * (kSmS - 3)));  // W of step q+2
+          ws_barrier();  // B(q+1)
+        }
       }
     }
   } else {
@@ -1792,68 +1831,95 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
     const int rv = TR - 64 * wm;  // valid z rows from this wave's first
-    ws_barrier();  // B0
-    mark(1);
-    for (int q = 0; q < Qp; ++q) {
-      if (q >= Q) {
-        ws_barrier();
-        continue;
-      }
+    // one K step's operands: [kk][channel block] W hi/lo, [kk][pixel block] X hi/lo
+    // (7x7: W of this wave's channel quarter in [kk][0])
+    struct Ops {
+      v4u ah[2][2], al[2][2], bh[2][2], bl[2][2];
+    };
+    auto rd = [&](int q, Ops& o) {
       const uint8_t* st = ldss + (q % kSmS) * kWsStage;
-      if (p.dbg & 4) {  // ablation 4: no MFMAs / stage reads
-        ws_barrier();
-        continue;
-      }
       if constexpr (kQ4) {
-        // 7x7: the tile is <= 64 rows, so the 4 waves split the 128 channels
-        // instead (wave = 32-channel quarter x both 32-pixel blocks)
-        v4u ah[2], al[2], bh[2][2], bl[2][2];
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           const int wo = ws_chunk(32 * wave + col, 2 * kk + h);
-          ah[kk] = ld16(st + 2 * kWsPlane + wo);
-          al[kk] = ld16(st + 3 * kWsPlane + wo);
+          o.ah[kk][0] = ld16(st + 2 * kWsPlane + wo);
+          o.al[kk][0] = ld16(st + 3 * kWsPlane + wo);
 #pragma unroll
           for (int b = 0; b < 2; ++b) {
             const int xo = ws_chunk(32 * b + col, 2 * kk + h);
-            bh[kk][b] = ld16(st + xo);
-            bl[kk][b] = ld16(st + kWsPlane + xo);
+            o.bh[kk][b] = ld16(st + xo);
+            o.bl[kk][b] = ld16(st + kWsPlane + xo);
           }
         }
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int b = 0; b < 2; ++b)
-            if (b == 0 || TR > 32) acc[0][b] = x3_32(ah[kk], al[kk], bh[kk][b], bl[kk][b], acc[0][b]);
-      } else if (rv > 0) {
-        v4u ah[2][2], al[2][2], bh[2][2], bl[2][2];
+      } else {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
           for (int b = 0; b < 2; ++b) {
             const int xo = ws_chunk(64 * wm + 32 * b + col, 2 * kk + h);
             const int wo = ws_chunk(64 * wn + 32 * b + col, 2 * kk + h);
-            bh[kk][b] = ld16(st + xo);
-            bl[kk][b] = ld16(st + kWsPlane + xo);
-            ah[kk][b] = ld16(st + 2 * kWsPlane + wo);
-            al[kk][b] = ld16(st + 3 * kWsPlane + wo);
+            o.bh[kk][b] = ld16(st + xo);
+            o.bl[kk][b] = ld16(st + kWsPlane + xo);
+            o.ah[kk][b] = ld16(st + 2 * kWsPlane + wo);
+            o.al[kk][b] = ld16(st + 3 * kWsPlane + wo);
           }
-        if (rv > 32) {
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int a = 0; a < 2; ++a)
-#pragma unroll
-              for (int b = 0; b < 2; ++b) acc[a][b] = x3_32(ah[kk][a], al[kk][a], bh[kk][b], bl[kk][b], acc[a][b]);
-        } else {
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int a = 0; a < 2; ++a) acc[a][0] = x3_32(ah[kk][a], al[kk][a], bh[kk][0], bl[kk][0], acc[a][0]);
-        }
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      ws_barrier();  // B(q+1): stage q is free
+    };
+    auto mma = [&](const Ops& o) {
+      if constexpr (kQ4) {
+        // 7x7: the tile is <= 64 rows, so the 4 waves split the 128 channels
+        // instead (wave = 32-channel quarter x both 32-pixel blocks)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            if (b == 0 || TR > 32) acc[0][b] = x3_32(o.ah[kk][0], o.al[kk][0], o.bh[kk][b], o.bl[kk][b], acc[0][b]);
+      } else if (rv > 32) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) acc[a][b] = x3_32(o.ah[kk][a], o.al[kk][a], o.bh[kk][b], o.bl[kk][b], acc[a][b]);
+      } else if (rv > 0) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int a = 0; a < 2; ++a) acc[a][0] = x3_32(o.ah[kk][a], o.al[kk][a], o.bh[kk][0], o.bl[kk][0], acc[a][0]);
+      }
+    };
+    const bool live = !(p.dbg & 4) && (kQ4 || rv > 0);  // ablation 4: no MFMAs / stage reads
+    ws_barrier();  // B0
+    mark(1);
+    if constexpr (LEAD == 1) {
+      for (int q = 0; q < Qp; ++q) {
+        if (q < Q && live) {
+          Ops o;
+          rd(q, o);
+          mma(o);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        ws_barrier();  // B(q+1): stage q is free
+      }
+    } else {
+      // step q runs from registers read in interval q-1 while stage q+1 is read
+      Ops oa, ob;
+      if (live) rd(0, oa);
+      // both loop entries (this one and the back edge) then hold no pending
+      // LDS reads, so the MFMAs of a step need no wait for the reads issued
+      // just before them
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      for (int q = 0; q < Qp; q += 2) {
+        if (q + 1 < Q && live) rd(q + 1, ob);
+        if (q < Q && live) mma(oa);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        ws_barrier();  // B(q+1)
+        if (q + 1 >= Qp) break;
+        if (q + 2 < Q && live) rd(q + 2, oa);
+        if (q + 1 < Q && live) mma(ob);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        ws_barrier();  // B(q+2)
+      }
     }
   }
   mark(2);
@@ -2762,21 +2828,24 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
   // and K-step stages (TCAMD_X3_SMALLF_STAGES 4 or 5), for A/B runs
   static const int pf = getenv("TCAMD_X3_SMALLF_PF") ? atoi(getenv("TCAMD_X3_SMALLF_PF")) : 3;
   static const int ns = getenv("TCAMD_X3_SMALLF_STAGES") ? atoi(getenv("TCAMD_X3_SMALLF_STAGES")) : 4;
-  const void* const fns[2][2][2] = {
-      {{(const void*)x3_dense_small_kernel<14, 3, 4>, (const void*)x3_dense_small_kernel<14, 3, 5>},
-       {(const void*)x3_dense_small_kernel<14, 6, 4>, (const void*)x3_dense_small_kernel<14, 6, 5>}},
-      {{(const void*)x3_dense_small_kernel<7, 3, 4>, (const void*)x3_dense_small_kernel<7, 3, 5>},
-       {(const void*)x3_dense_small_kernel<7, 6, 4>, (const void*)x3_dense_small_kernel<7, 6, 5>}}};
+  static const int lead = getenv("TCAMD_X3_SMALLF_LEAD") ? atoi(getenv("TCAMD_X3_SMALLF_LEAD")) : 1;
+#define X3S_FN(HW, PF_, NS_)                                                                    \
+  {(const void*)x3_dense_small_kernel<HW, PF_, NS_, 1>, (const void*)x3_dense_small_kernel<HW, PF_, NS_, 2>}
+  // [14x14 / 7x7][PF 3 / 6][4 / 5 stages][lead 1 / 2]
+  const void* const fns[2][2][2][2] = {{{X3S_FN(14, 3, 4), X3S_FN(14, 3, 5)}, {X3S_FN(14, 6, 4), X3S_FN(14, 6, 5)}},
+                                       {{X3S_FN(7, 3, 4), X3S_FN(7, 3, 5)}, {X3S_FN(7, 6, 4), X3S_FN(7, 6, 5)}}};
+#undef X3S_FN
   static std::atomic<bool> attr_set[kMaxDevices];
   const int dev_slot = device_slot();
   if (!attr_set[dev_slot].load(std::memory_order_acquire)) {
     for (int w = 0; w < 2; ++w)
       for (int f = 0; f < 2; ++f)
-        for (int n = 0; n < 2; ++n) {
-          const hipError_t e =
-              hipFuncSetAttribute(fns[w][f][n], hipFuncAttributeMaxDynamicSharedMemorySize, (4 + n) * kWsStage);
-          if (e != hipSuccess) return e;
-        }
+        for (int n = 0; n < 2; ++n)
+          for (int l = 0; l < 2; ++l) {
+            const hipError_t e =
+                hipFuncSetAttribute(fns[w][f][n][l], hipFuncAttributeMaxDynamicSharedMemorySize, (4 + n) * kWsStage);
+            if (e != hipSuccess) return e;
+          }
     attr_set[dev_slot].store(true, std::memory_order_release);
   }
   const int blocks = W == 14 ? (imgs + 7) / 8 * 16 : imgs;
@@ -2784,7 +2853,8 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
   g_x3s_stamp_blocks = blocks;
   void* args[] = {&p};
   const int n5 = ns == 5 ? 1 : 0;
-  const hipError_t e = hipLaunchKernel(fns[W == 14 ? 0 : 1][pf == 6 ? 1 : 0][n5], dim3(blocks), dim3(512), args,
+  const hipError_t e = hipLaunchKernel(fns[W == 14 ? 0 : 1][pf == 6 ? 1 : 0][n5][lead == 2 ? 1 : 0], dim3(blocks),
+                                       dim3(512), args,
                                        (4 + n5) * kWsStage, (hipStream_t)stream);
   if (e != hipSuccess) return e;
   return hipGetLastError();

@@ -359,10 +359,13 @@ def test_x3_dense_small(imgs, H, K):
     assert _rel(x[:, K:K + 32], y2[:, K:K + 32]) < 2e-5
 
 
-@pytest.mark.parametrize("pf,stages", [("6", "4"), ("3", "5"), ("6", "5")])
-def test_x3_dense_small_variants(pf, stages):
+@pytest.mark.parametrize("pf,stages,lead", [("6", "4", "1"), ("3", "5", "1"), ("6", "5", "1"), ("3", "4", "2"),
+                                            ("6", "4", "2"), ("3", "5", "2"), ("6", "5", "2")])
+def test_x3_dense_small_variants(pf, stages, lead):
     """K14x's A/B variants (TCAMD_X3_SMALLF_PF: X steps in the producers'
-    registers; TCAMD_X3_SMALLF_STAGES: K-step stages, 5 = 160 KB of LDS), chosen
+    registers; TCAMD_X3_SMALLF_STAGES: K-step stages, 5 = 160 KB of LDS;
+    TCAMD_X3_SMALLF_LEAD 2: stages filled two steps ahead, operands read one
+    step ahead of the MFMAs), chosen
     once per process, so in a child process: the same fp64 comparison as
     test_x3_dense_small on shapes that cover every padding-round count."""
     _need_gpu()
@@ -400,7 +403,7 @@ for imgs, H, K in [(3, 14, 256), (9, 14, 992), (17, 14, 640), (16, 14, 96), (5, 
     assert torch.equal(x[:, :K], xc[:, :K]) and torch.equal(x[:, K + 32:], xc[:, K + 32:])
 print("K14X_VARIANT_OK")
 '''
-    env = dict(os.environ, TCAMD_X3_SMALLF_PF=pf, TCAMD_X3_SMALLF_STAGES=stages)
+    env = dict(os.environ, TCAMD_X3_SMALLF_PF=pf, TCAMD_X3_SMALLF_STAGES=stages, TCAMD_X3_SMALLF_LEAD=lead)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "K14X_VARIANT_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

@@ -138,6 +138,7 @@ def main():
     ap.add_argument("--no-layers", action="store_true")
     ap.add_argument("--pf", default="", help="TCAMD_X3_SMALLF_PF for this process (3 or 6)")
     ap.add_argument("--dbg", default="", help="TCAMD_X3_SMALLF_DBG ablation flags (1 no 3x3, 2 X of image 0)")
+    ap.add_argument("--lead", default="", help="TCAMD_X3_SMALLF_LEAD for this process (1 or 2)")
     ap.add_argument("--stages", default="", help="TCAMD_X3_SMALLF_STAGES for this process (4 or 5)")
     ap.add_argument("--stamp", action="store_true", help="in-kernel timeline marks of one launch per layer")
     a = ap.parse_args()
@@ -145,6 +146,8 @@ def main():
         os.environ["TCAMD_X3_SMALLF_PF"] = a.pf  # read by the library at its first K14x launch
     if a.dbg:
         os.environ["TCAMD_X3_SMALLF_DBG"] = a.dbg
+    if a.lead:
+        os.environ["TCAMD_X3_SMALLF_LEAD"] = a.lead
     if a.stages:
         os.environ["TCAMD_X3_SMALLF_STAGES"] = a.stages
     if a.stamp:
