@@ -71,10 +71,20 @@ __device__ __forceinline__ uint32_t pk(float a, float b) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
-// hi/lo split of two fp32: a ~= hi + lo to 2^-17 relative (a - hi is exact)
+// hi/lo split of two fp32: a ~= hi + lo to 2^-17 relative (a - hi is exact).
+// (A v_pk_fma_f32 / v_pk_add_f32 form of this and of the BN affine issues
+// fewer instructions but measured 3-8% slower in K14x / K8x / K11x: round 4.)
 __device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
   hi = pk(a, b);
   lo = pk(a - __uint_as_float(hi << 16), b - __uint_as_float(hi & 0xffff0000u));
+}
+
+// relu(x * s + t), per element (as scalar v_fma_f32)
+__device__ __forceinline__ f32x4 bn_relu4(f32x4 x, f32x4 s, f32x4 t) {
+  f32x4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = fmaxf(__builtin_fmaf(x[e], s[e], t[e]), 0.f);
+  return v;
 }
 
 __device__ __forceinline__ void split4(f32x4 v, v2u& hi, v2u& lo) {
@@ -926,7 +936,8 @@ constexpr int kCvtF = 64 * 64;     // one plane of a converted X step: 64 px x 3
 constexpr int kPfF = 4;             // X steps in flight (registers)
 constexpr int kMaxKF = 480;         // BN1 affine staged in LDS: K <= 480 (blocks 1-2)
 constexpr int kScrF = 2 * 4 * 3 * 64 * 4;  // floats: [oh][owner][3 sources][px][4]
-constexpr int kLdsF = kRingRowsF * kRowB + kScrF * 4 + 4 * kCvtF + 2 * kMaxKF * 4;
+constexpr int kYsF = 2 * 4 * 4 * 64;  // floats: v1 owners' y sums [oh][owner][pg][px 16][4]
+constexpr int kLdsF = kRingRowsF * kRowB + kScrF * 4 + 4 * kCvtF + 2 * kMaxKF * 4 + kYsF * 4;
 static_assert(kLdsF <= 160 * 1024, "K11x LDS budget");
 constexpr uint32_t kMagRingF = (uint32_t)((0x100000000ull + kRingF - 1) / kRingF);
 
@@ -972,6 +983,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
   float* const scr = reinterpret_cast<float*>(ldsf + kRingRowsF * kRowB);
   uint8_t* const cvt = ldsf + kRingRowsF * kRowB + kScrF * 4;             // [buf 2][plane 2][64 px][64 B]
   float* const bn = reinterpret_cast<float*>(cvt + 4 * kCvtF);            // s1 [kMaxKF] | t1 [kMaxKF]
+  float* const ysum = bn + 2 * kMaxKF;                                     // [oh][owner][pg][16 px][4]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int W = p.W, HW = p.H * p.W;
 
@@ -1022,9 +1034,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
   auto convert = [&](int slot, int buf, int st) {
     const f32x4 sv = *reinterpret_cast<const f32x4*>(bn + st * 32 + 4 * cj);
     const f32x4 tv = *reinterpret_cast<const f32x4*>(bn + kMaxKF + st * 32 + 4 * cj);
-    f32x4 v = xr[slot] * sv + tv;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    const f32x4 v = bn_relu4(xr[slot], sv, tv);
     v2u h, l;
     split4(v, h, l);
     uint8_t* q = cvt + buf * 2 * kCvtF + cw_off;
@@ -1114,24 +1124,11 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
   }
   stamp(0);
 
-  // y of the previous tile: stored at the start of the next 3x3 phase, which
-  // consumes no global loads, so the store never sits in front of a W1 wait
-  f32x4 yo[4];
-  int ym0 = -1;
   const int c4 = lane >> 4;
-  auto store_y = [&]() {
-    if (ym0 < 0 || c4 != kq) return;
-#pragma unroll
-    for (int pg = 0; pg < 4; ++pg) {
-      const int m = ym0 + 16 * pg + (lane & 15);
-      if (m < p.M) *reinterpret_cast<f32x4*>(p.y + (size_t)m * p.ldy + 16 * oh + 4 * kq) = yo[pg];
-    }
-  };
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int m0 = tile * kT2;
     __syncthreads();  // B0: the ring holds band(tile); the scratch is free
     stamp(1);
-    store_y();
     // this iteration's chunk: its first X steps and W(0) go out now and land
     // while the 3x3 runs (issued and consumed in one tile iteration: a load
     // carried round the loop is one the compiler's waits cannot follow)
@@ -1210,33 +1207,46 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
     // C (16x16): lane (lane&15) = pixel of group pg, reg e -> channel 16oh + 4c + e,
     // c = lane>>4; owner of channels 16oh + 4c .. +4 is wave (kq = c, oh), whose
     // lanes 16c .. 16c+15 hold their own share and add the other three
+    // C (16x16) lanes of another wave's 4 channels go to that owner's
+    // scratch slots, the owner's own share to its y-sum slot: no 3x3 result
+    // stays in registers through the 1x1 chunk
     if (c4 != kq) {
       float* sw = scr + ((oh * 4 + c4) * 3 + (kq - c4 + 3) % 4) * 256 + (lane & 15) * 4;
 #pragma unroll
       for (int pg = 0; pg < 4; ++pg) *reinterpret_cast<f32x4*>(sw + pg * 64) = acc[pg];
-    }
-    __syncthreads();  // B1
-    if (c4 == kq) {
-      const float* sr = scr + (oh * 4 + kq) * 3 * 256 + (lane & 15) * 4;
+    } else {
+      float* yw = ysum + (oh * 4 + kq) * 256 + (lane & 15) * 4;
 #pragma unroll
-      for (int pg = 0; pg < 4; ++pg) {
-        yo[pg] = acc[pg];
-#pragma unroll
-        for (int src = 0; src < 3; ++src) yo[pg] += *reinterpret_cast<const f32x4*>(sr + src * 256 + pg * 64);
-      }
+      for (int pg = 0; pg < 4; ++pg) *reinterpret_cast<f32x4*>(yw + pg * 64) = acc[pg];
     }
-    ym0 = m0;
     }
     stamp(3);
 
-    // ---- 1x1 phase: the 64 rows band(tile+1) adds ----
+    // ---- 1x1 phase: the 64 rows band(tile+1) adds; its first barrier
+    // publishes the partials (no exchange barrier of its own), its last one
+    // makes them readable by the owners below ----
     if (tile + 1 < t_end && !(p.dbg & 2)) {
       const int g0 = m0 + kT2 + W + 1;
       z_chunk(g0, kT2);
+    } else {
+      __syncthreads();
+    }
+    // owners: own share + the three partials -> y (the stores are issued
+    // after the chunk's last W1 / X wait and long retired by the next one)
+    if (!(p.dbg & 1) && c4 == kq) {
+      const float* sr = scr + (oh * 4 + kq) * 3 * 256 + (lane & 15) * 4;
+      const float* yr = ysum + (oh * 4 + kq) * 256 + (lane & 15) * 4;
+#pragma unroll
+      for (int pg = 0; pg < 4; ++pg) {
+        f32x4 v = *reinterpret_cast<const f32x4*>(yr + pg * 64);
+#pragma unroll
+        for (int src = 0; src < 3; ++src) v += *reinterpret_cast<const f32x4*>(sr + src * 256 + pg * 64);
+        const int m = m0 + 16 * pg + (lane & 15);
+        if (m < p.M) *reinterpret_cast<f32x4*>(p.y + (size_t)m * p.ldy + 16 * oh + 4 * kq) = v;
+      }
     }
     stamp(4);
   }
-  store_y();
   if constexpr (STAMP) {
     st_acc[5] = t_end - t_begin;
     st_acc[6] = __builtin_amdgcn_s_memtime() - st_t0;
@@ -1340,12 +1350,7 @@ x3_dense_fused4_kernel(X3FusedParams p) {
     const float* sb = bn + st * 32 + 8 * cc;
     const f32x4 s0 = *reinterpret_cast<const f32x4*>(sb), s1 = *reinterpret_cast<const f32x4*>(sb + 4);
     const f32x4 t0 = *reinterpret_cast<const f32x4*>(sb + kMaxKF), t1 = *reinterpret_cast<const f32x4*>(sb + kMaxKF + 4);
-    f32x4 v0 = xr[slot][0] * s0 + t0, v1 = xr[slot][1] * s1 + t1;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v0[e] = fmaxf(v0[e], 0.f);
-      v1[e] = fmaxf(v1[e], 0.f);
-    }
+    const f32x4 v0 = bn_relu4(xr[slot][0], s0, t0), v1 = bn_relu4(xr[slot][1], s1, t1);
     v2u h0, l0, h1, l1;
     split4(v0, h0, l0);
     split4(v1, h1, l1);
@@ -1752,11 +1757,10 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
       const f32x4 sc = xs[slot], sb = xt[slot];
 #pragma unroll
       for (int i = 0; i < kNRI; ++i) {
+        // rows >= TR hold row TR-1's data (clamped loads): their z columns
+        // are never written to the tile image, so they need no zeroing
         const int row = prow + 32 * i;
-        const bool ok = row < TR;
-        f32x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = ok ? fmaxf(xr[slot][i][e] * sc[e] + sb[e], 0.f) : 0.f;
+        const f32x4 v = bn_relu4(xr[slot][i], sc, sb);
         v2u h, l;
         split4(v, h, l);
         const int off = ws_chunk(row, pj >> 1) + (pj & 1) * 8;

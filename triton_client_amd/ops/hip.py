@@ -23,7 +23,10 @@ import numpy as np
 
 from . import dtypes
 
-_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libtcamd_hip.so")
+# TCAMD_HIP_LIB: load another build of the library (A/B timing of two kernel
+# builds in one tree, tools only)
+_PATH = os.environ.get("TCAMD_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                        "libtcamd_hip.so")
 IPC_HANDLE_SIZE = 64
 
 MEMORY_UNREGISTERED = 0
