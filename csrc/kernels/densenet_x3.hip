@@ -1714,6 +1714,12 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   const int mz0 = img * W * W + zr0 * W;
   const int nst = p.K / kBK;
   const int Q = nst, Qp = (Q + PF - 1) / PF * PF;
+  // timeline diagnostic (dbg 64, 4 stages, block 0, LEAD 1): shader-clock time
+  // of producer wave 4 and consumer wave 0 reaching each step barrier, kept in
+  // LDS past the stages (no memory op inside the counted-wait loop)
+  const bool tl = (p.dbg & 64) && kSmS == 4 && blockIdx.x == 0;
+  unsigned long long* const tls = reinterpret_cast<unsigned long long*>(ldss + kSmS * kWsStage);
+  const unsigned long long tl0 = __builtin_amdgcn_s_memtime();
   f32x16 acc[2][2];  // consumers: [channel block][pixel block] of the 128 x 128 1x1 tile
   const int wm = wave & 1, wn = (wave >> 1) & 1;
   const int col = lane & 31, h = lane >> 5;
@@ -1791,6 +1797,8 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
           __builtin_amdgcn_sched_barrier(0);  // W copies ahead of the X loads (vmcnt retires in order)
           issue_x(q + 1 + PF, slot);
           __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0((2 + kNRI) + kOps * (kSmS - 2)));  // W of step q+1
+          if (tl && pw == 0 && lane == 0 && q < 32)  // timeline: producer wave 4 at the barrier (LDS, no vm op)
+            tls[2 * q] = __builtin_amdgcn_s_memtime();
           ws_barrier();  // B(q+1)
         }
       }
@@ -1903,6 +1911,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
           mma(o);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (tl && wave == 0 && lane == 0 && q < 32) tls[2 * q + 1] = __builtin_amdgcn_s_memtime();
         ws_barrier();  // B(q+1): stage q is free
       }
     } else {
@@ -2052,6 +2061,11 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
     }
   }
   mark(6);
+  if (tl && p.stamps) {
+    __syncthreads();
+    // [16384 + 2q + side]: cycles since kernel entry (side 0 producer, 1 consumer)
+    if (tid < 64) p.stamps[16384 + tid] = tls[tid] > tl0 ? tls[tid] - tl0 : 0;
+  }
   if (p.stamps && wave == 0) {
     mark(7);
     if (lane < 8) {
@@ -2780,6 +2794,19 @@ int tcamd_x3_dense_fused4(const float* x, int ldx, int imgs, int H, int W, int K
 static unsigned long long* g_x3s_stamps = nullptr;  // TCAMD_X3_SMALLF_STAMP builds
 static int g_x3s_stamp_blocks = 0;
 
+// Copies the last K14x launch's step timeline (TCAMD_X3_SMALLF_STAMP=1 and
+// TCAMD_X3_SMALLF_DBG & 64): [2q + side] shader-clock cycles since block 0's
+// entry at which producer wave 4 (side 0) / consumer wave 0 (side 1) reached
+// the barrier after K step q (q < 32).
+int tcamd_x3_small_timeline(unsigned long long* out, int n) {
+  if (!g_x3s_stamps || !out) return 0;
+  const int m = std::min(n, 64);
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(out, g_x3s_stamps + 16384, m * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return m;
+}
+
 // Copies the last stamped K14x launch's per-block marks ([blocks][8],
 // s_memrealtime ticks of 10 ns; blocks past the image count stay 0).
 int tcamd_x3_small_stamps(unsigned long long* out, int n) {
@@ -2847,7 +2874,8 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
         for (int n = 0; n < 2; ++n)
           for (int l = 0; l < 2; ++l) {
             const hipError_t e =
-                hipFuncSetAttribute(fns[w][f][n][l], hipFuncAttributeMaxDynamicSharedMemorySize, (4 + n) * kWsStage);
+                hipFuncSetAttribute(fns[w][f][n][l], hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (4 + n) * kWsStage + (n ? 0 : 512));
             if (e != hipSuccess) return e;
           }
     attr_set[dev_slot].store(true, std::memory_order_release);
@@ -2859,7 +2887,7 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
   const int n5 = ns == 5 ? 1 : 0;
   const hipError_t e = hipLaunchKernel(fns[W == 14 ? 0 : 1][pf == 6 ? 1 : 0][n5][lead == 2 ? 1 : 0], dim3(blocks),
                                        dim3(512), args,
-                                       (4 + n5) * kWsStage, (hipStream_t)stream);
+                                       (4 + n5) * kWsStage + ((dbg & 64) && !n5 ? 512 : 0), (hipStream_t)stream);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }

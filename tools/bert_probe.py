@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--k15-ab", type=int, default=0,
                     help="also time the forward with K15 GEMMs from this many tokens (interleaved A/B rounds)")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--tunable", default="",
+                    help="A/B against PyTorch TunableOp (hipBLASLt / rocBLAS solution search per GEMM shape); "
+                         "the tuned results go to this CSV path")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     model = bert.build(device=dev)
@@ -34,16 +37,33 @@ def main():
         variants = {"default": bert.K15_MIN_TOKENS}
         if a.k15_ab:
             variants = {"hipblaslt": 0, "k15": a.k15_ab}
+        tun = None
+        if a.tunable:
+            import torch.cuda.tunable as tun
+
+            tun.set_filename(a.tunable)
+            variants = {"default": bert.K15_MIN_TOKENS, "tunableop": bert.K15_MIN_TOKENS}
+            with torch.no_grad():  # tune every GEMM shape of this batch once, outside the timed rounds
+                tun.enable(True)
+                tun.tuning_enable(True)
+                model(ids, mask, tt)
+                torch.cuda.synchronize()
+                tun.tuning_enable(False)
+                tun.enable(False)
         ts = {k: [] for k in variants}
         with torch.no_grad():
             for name, thr in variants.items():
                 bert.K15_MIN_TOKENS = thr
+                if tun is not None:
+                    tun.enable(name == "tunableop")
                 for _ in range(2):
                     model(ids, mask, tt)
             torch.cuda.synchronize()
             for _ in range(a.rounds):
                 for name, thr in variants.items():
                     bert.K15_MIN_TOKENS = thr
+                    if tun is not None:
+                        tun.enable(name == "tunableop")
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
                     for _ in range(a.iters):

@@ -89,6 +89,12 @@ def layers(a, torch, hip):
                                  "span_us": round(float(rel[:, 7].max()), 2),
                                  "end_spread_us": round(float(rel[:, 7].max() - rel[:, 7].min()), 2),
                                  "median_phase_us": med}
+            if a.stamp and a.dbg and int(a.dbg) & 64:
+                tlv = hip.x3_small_timeline()
+                n = int((tlv[:, 0] > 0).sum())
+                d = tlv[:n]
+                row["timeline_cycles"] = {"producer_arrive": d[:, 0].tolist(), "consumer_arrive": d[:, 1].tolist(),
+                                          "step": np.diff(np.maximum(d[:, 0], d[:, 1])).tolist()}
             print(json.dumps(row), flush=True)
             out.append(row)
     return out

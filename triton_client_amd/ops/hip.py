@@ -229,6 +229,7 @@ _SIGS = {
     ),
     "tcamd_x3_fused_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "tcamd_x3_small_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
+    "tcamd_x3_small_timeline": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "tcamd_x3_dense_fused4": (
         [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -772,6 +773,17 @@ def x3_dense_small(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo
     ``w2_*`` in x3_w3f_fragments; K a multiple of 32, >= 64."""
     _check(_load().tcamd_x3_dense_small(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
                                         w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_small")
+
+
+def x3_small_timeline():
+    """Step timeline of the last K14x launch (STAMP process with TCAMD_X3_SMALLF_DBG
+    bit 64): int64 [32][2] cycles since block 0's entry at which producer wave 4
+    / consumer wave 0 reached the barrier after each K step (0 = not reached)."""
+    out = np.zeros(64, dtype=np.uint64)
+    n = _load().tcamd_x3_small_timeline(out.ctypes.data, out.size)
+    if n < 0:
+        raise HipError(n, "x3_small_timeline")
+    return out.reshape(32, 2).astype(np.int64)
 
 
 def x3_small_stamps(max_blocks=4096):
