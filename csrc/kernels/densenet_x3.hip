@@ -1660,7 +1660,8 @@ struct X3SmallParams {
   int ldx, K, ldy, imgs;
   int dbg;                // ablation (TCAMD_X3_SMALLF_DBG): 1 = no 3x3 phase, 2 = X rows of image 0 only,
                           // 4 = no 1x1 MFMAs, 8 = no W copies, 16 = no X conversion (results
-                          // invalid with 4 / 8 / 16)
+                          // invalid with 4 / 8 / 16), 64 = step timeline (block 0),
+                          // 128 = producer waves at s_setprio 1
   unsigned long long* stamps;  // TCAMD_X3_SMALLF_STAMP: per block [8] s_memrealtime (100 MHz) marks
 };
 
@@ -1774,6 +1775,9 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
         *reinterpret_cast<v2u*>(st + kWsPlane + off) = l;
       }
     };
+    // A/B (dbg 128): the producer waves (the younger half: they lose VALU
+    // issue arbitration to the consumers' MFMA stream) at s_setprio 1
+    if (p.dbg & 128) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < PF; ++s) issue_x(s, s);
     if constexpr (LEAD == 1) {

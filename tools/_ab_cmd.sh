@@ -15,3 +15,5 @@ TCAMD_X3F_V=1 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUS
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/ab/pmc3 -- python3 tools/k14x_bench.py --ks 992 --hw 14 --rounds 1 --iters 5 > gpurun_out/ab/pmc3.log 2>&1 || exit 1
 timeout -k 10 300 python -u tools/bert_probe.py --batch 64 --iters 5 --rounds 3 --tunable gpurun_out/ab/tunableop_b64.csv > gpurun_out/ab/bert_tun.log 2>&1 || exit 1
 timeout -k 10 120 python -u tools/k14x_bench.py --ks 256,992 --hw 14 --stamp --dbg 64 --rounds 1 > gpurun_out/ab/timeline.log 2>&1 || exit 1
+timeout -k 10 120 python -u tools/k14x_bench.py --ks 256,992 --hw 14,7 --stamp --dbg 192 --rounds 3 > gpurun_out/ab/prio.log 2>&1 || exit 1
+timeout -k 10 120 python -u tools/k14x_bench.py --ks 256,992 --hw 14,7 --stamp --dbg 64 --rounds 3 > gpurun_out/ab/noprio.log 2>&1 || exit 1
