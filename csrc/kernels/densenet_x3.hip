@@ -962,7 +962,10 @@ struct X3FusedParams {
 // NST = K / 32 (2..7): the k loop of a chunk is straight-line code, so the
 // compiler's waits for the W1 fragments are exact (through a loop back edge
 // it fell back to draining the whole counter every step).
-template <int NST, bool STAMP = false>
+// STG: stagger the two waves of each SIMD in the 1x1 chunk (waves 4-7 run a
+// step's MFMAs before converting the next step's X, waves 0-3 after), so one
+// wave's conversion VALU sits beside its partner's MFMAs (TCAMD_X3F_STAGGER=1)
+template <int NST, bool STAMP = false, bool STG = false>
 __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p) {
   // STAMP (diagnostic builds, TCAMD_X3F_STAMP=1): shader-clock cycles per
   // phase, summed over the block's tiles by wave 0: [0] prologue, [1] B0 wait,
@@ -1075,15 +1078,28 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
 #pragma unroll
     for (int st = 0; st < nst; ++st) {
       wload((st + 1) & 1, st + 1);
-      if (st + 1 < nst) {
-        convert((st + 1) % kPfF, (st + 1) & 1, st + 1);
-        xload((st + 1) % kPfF, st + 1 + kPfF);
-      }
-      const uint8_t* cb = cvt + (st & 1) * 2 * kCvtF;
+      auto next = [&]() {
+        if (st + 1 < nst) {
+          convert((st + 1) % kPfF, (st + 1) & 1, st + 1);
+          xload((st + 1) % kPfF, st + 1 + kPfF);
+        }
+      };
+      auto mma = [&]() {
+        const uint8_t* cb = cvt + (st & 1) * 2 * kCvtF;
 #pragma unroll
-      for (int kc = 0; kc < 2; ++kc) {
-        const uint8_t* q = cb + br_off[kc];
-        acc = x3_32(a1[st & 1][kc][0], a1[st & 1][kc][1], ld16(q), ld16(q + kCvtF), acc);
+        for (int kc = 0; kc < 2; ++kc) {
+          const uint8_t* q = cb + br_off[kc];
+          acc = x3_32(a1[st & 1][kc][0], a1[st & 1][kc][1], ld16(q), ld16(q + kCvtF), acc);
+        }
+      };
+      if (STG && ph) {
+        mma();
+        __builtin_amdgcn_sched_barrier(0);
+        next();
+      } else {
+        next();
+        if constexpr (STG) __builtin_amdgcn_sched_barrier(0);
+        mma();
       }
       __syncthreads();
     }
@@ -2739,14 +2755,18 @@ static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, 
   p.mag_w = (uint32_t)((0x100000000ull + W - 1) / (uint64_t)W);
   // NST 2..15 (K 64..480; the BN1 affine table in LDS holds K <= 480).  v1
   // at NST 15 spills 12 B per lane; measured per K before the engine uses it
-#define X3F_ROW(KERN, ST)                                                                                        \
-  {(const void*)KERN<2, ST>,  (const void*)KERN<3, ST>,  (const void*)KERN<4, ST>,  (const void*)KERN<5, ST>,  \
-   (const void*)KERN<6, ST>,  (const void*)KERN<7, ST>,  (const void*)KERN<8, ST>,  (const void*)KERN<9, ST>,  \
-   (const void*)KERN<10, ST>, (const void*)KERN<11, ST>, (const void*)KERN<12, ST>, (const void*)KERN<13, ST>, \
-   (const void*)KERN<14, ST>, (const void*)KERN<15, ST>}
-  static const void* const kFns[2][2][14] = {
-      {X3F_ROW(x3_dense_fused_kernel, false), X3F_ROW(x3_dense_fused_kernel, true)},
-      {X3F_ROW(x3_dense_fused4_kernel, false), X3F_ROW(x3_dense_fused4_kernel, true)}};
+#define X3F_ROW(KERN, ...)                                                                                   \
+  {(const void*)KERN<2, __VA_ARGS__>,  (const void*)KERN<3, __VA_ARGS__>,  (const void*)KERN<4, __VA_ARGS__>,  \
+   (const void*)KERN<5, __VA_ARGS__>,  (const void*)KERN<6, __VA_ARGS__>,  (const void*)KERN<7, __VA_ARGS__>,  \
+   (const void*)KERN<8, __VA_ARGS__>,  (const void*)KERN<9, __VA_ARGS__>,  (const void*)KERN<10, __VA_ARGS__>, \
+   (const void*)KERN<11, __VA_ARGS__>, (const void*)KERN<12, __VA_ARGS__>, (const void*)KERN<13, __VA_ARGS__>, \
+   (const void*)KERN<14, __VA_ARGS__>, (const void*)KERN<15, __VA_ARGS__>}
+  // [version][0 plain / 1 stamped / 2 staggered (v1 only)][NST - 2]
+  static const void* const kFns[2][3][14] = {
+      {X3F_ROW(x3_dense_fused_kernel, false), X3F_ROW(x3_dense_fused_kernel, true),
+       X3F_ROW(x3_dense_fused_kernel, false, true)},
+      {X3F_ROW(x3_dense_fused4_kernel, false), X3F_ROW(x3_dense_fused4_kernel, true),
+       X3F_ROW(x3_dense_fused4_kernel, false)}};
 #undef X3F_ROW
   const int nst = K / 32;
   if (nst < 2 || nst > 15 || (v != 1 && v != 2)) return hipErrorInvalidValue;
@@ -2775,7 +2795,9 @@ static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, 
   p.tiles_per_block = (p.tiles + grid - 1) / grid;
   const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
   void* args[] = {&p};
-  const hipError_t e = hipLaunchKernel(kFns[v - 1][stamp ? 1 : 0][nst - 2], dim3(blocks), dim3(v == 2 ? 256 : 512),
+  static const bool stg = getenv("TCAMD_X3F_STAGGER") && atoi(getenv("TCAMD_X3F_STAGGER"));
+  const hipError_t e = hipLaunchKernel(kFns[v - 1][stamp ? 1 : (stg ? 2 : 0)][nst - 2], dim3(blocks),
+                                       dim3(v == 2 ? 256 : 512),
                                        args, kLdsF, (hipStream_t)stream);
   if (e != hipSuccess) return e;
   g_x3f_stamp_blocks = blocks;

@@ -17,3 +17,8 @@ timeout -k 10 300 python -u tools/bert_probe.py --batch 64 --iters 5 --rounds 3 
 timeout -k 10 120 python -u tools/k14x_bench.py --ks 256,992 --hw 14 --stamp --dbg 64 --rounds 1 > gpurun_out/ab/timeline.log 2>&1 || exit 1
 timeout -k 10 120 python -u tools/k14x_bench.py --ks 256,992 --hw 14,7 --stamp --dbg 192 --rounds 3 > gpurun_out/ab/prio.log 2>&1 || exit 1
 timeout -k 10 120 python -u tools/k14x_bench.py --ks 256,992 --hw 14,7 --stamp --dbg 64 --rounds 3 > gpurun_out/ab/noprio.log 2>&1 || exit 1
+for r in 1 2; do for sg in 0 1; do
+  TCAMD_X3F_V=1 TCAMD_X3F_STAGGER=$sg timeout -k 10 120 python -u tools/x3_pair_bench.py --hw 56 --ks 64,128,224 --ldx 256 --chunks "" --iters 20 >> gpurun_out/ab/stg56_$sg.log 2>&1 || exit 1
+  TCAMD_X3F_V=1 TCAMD_X3F_STAGGER=$sg timeout -k 10 120 python -u tools/x3_pair_bench.py --hw 28 --ks 128,256,480 --ldx 512 --chunks "" --iters 20 >> gpurun_out/ab/stg28_$sg.log 2>&1 || exit 1
+done; done
+for sg in 0 1; do TCAMD_X3F_STAGGER=$sg timeout -k 10 120 python -u tools/fp32_engine_bench.py --batches 128 --streams 1,2,3 --engines fp32 --iters 20 >> gpurun_out/ab/eng_stg$sg.log 2>&1 || exit 1; done
