@@ -1,5 +1,4 @@
 mkdir -p gpurun_out/ab
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_densenet_fp32_gpu.py -k "x3_dense_small or x3_dense_fused or engine or stagger" > gpurun_out/ab/tests.log 2>&1 || exit 1
 for r in 1 2; do
   for lib in base new; do
     if [ $lib = base ]; then export TCAMD_HIP_LIB=$PWD/ab/libtcamd_hip_base.so; else unset TCAMD_HIP_LIB; fi

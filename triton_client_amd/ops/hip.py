@@ -322,6 +322,8 @@ def _load():
     # SONAME, so whichever copy is loaded first is shared by both.
     lib = ctypes.CDLL(_PATH, mode=ctypes.RTLD_GLOBAL)
     for name, (argtypes, restype) in _SIGS.items():
+        if os.environ.get("TCAMD_HIP_LIB") and not hasattr(lib, name):
+            continue  # an older A/B build: entry points it predates stay unbound
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = restype
