@@ -962,10 +962,10 @@ struct X3FusedParams {
 // NST = K / 32 (2..7): the k loop of a chunk is straight-line code, so the
 // compiler's waits for the W1 fragments are exact (through a loop back edge
 // it fell back to draining the whole counter every step).
-// STG: stagger the two waves of each SIMD in the 1x1 chunk (waves 4-7 run a
-// step's MFMAs before converting the next step's X, waves 0-3 after), so one
-// wave's conversion VALU sits beside its partner's MFMAs (TCAMD_X3F_STAGGER=1)
-template <int NST, bool STAMP = false, bool STG = false>
+// (A stagger of the two waves of each SIMD in the 1x1 chunk -- waves 4-7
+// running a step's MFMAs before converting the next X step -- measured 5-20%
+// slower at 56x56 and 28x28 in round 4 and was dropped.)
+template <int NST, bool STAMP = false>
 __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p) {
   // STAMP (diagnostic builds, TCAMD_X3F_STAMP=1): shader-clock cycles per
   // phase, summed over the block's tiles by wave 0: [0] prologue, [1] B0 wait,
@@ -1092,15 +1092,8 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
           acc = x3_32(a1[st & 1][kc][0], a1[st & 1][kc][1], ld16(q), ld16(q + kCvtF), acc);
         }
       };
-      if (STG && ph) {
-        mma();
-        __builtin_amdgcn_sched_barrier(0);
-        next();
-      } else {
-        next();
-        if constexpr (STG) __builtin_amdgcn_sched_barrier(0);
-        mma();
-      }
+      next();
+      mma();
       __syncthreads();
     }
     // C (32x32): lane col = pixel, reg 4g+e -> channel 32q1 + 8g + 4hh + e
@@ -1812,13 +1805,18 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
           const int slot = (u + 1) % PF;
           __builtin_amdgcn_s_waitcnt(ws_vmcnt(kOps * (PF - 1)));  // X of step q+1
           __builtin_amdgcn_sched_barrier(0);
+          if (tl && pw == 0 && lane == 0 && q < 32) tls[4 * q] = __builtin_amdgcn_s_memtime();
           write_x(q + 1, slot);
+          if (tl && pw == 0 && lane == 0 && q < 32) {
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // the conversion's LDS writes done
+            tls[4 * q + 1] = __builtin_amdgcn_s_memtime();
+          }
           issue_w(q + kSmS - 1);
           __builtin_amdgcn_sched_barrier(0);  // W copies ahead of the X loads (vmcnt retires in order)
           issue_x(q + 1 + PF, slot);
           __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0((2 + kNRI) + kOps * (kSmS - 2)));  // W of step q+1
           if (tl && pw == 0 && lane == 0 && q < 32)  // timeline: producer wave 4 at the barrier (LDS, no vm op)
-            tls[2 * q] = __builtin_amdgcn_s_memtime();
+            tls[4 * q + 2] = __builtin_amdgcn_s_memtime();
           ws_barrier();  // B(q+1)
         }
       }
@@ -1931,7 +1929,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
           mma(o);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (tl && wave == 0 && lane == 0 && q < 32) tls[2 * q + 1] = __builtin_amdgcn_s_memtime();
+        if (tl && wave == 0 && lane == 0 && q < 32) tls[4 * q + 3] = __builtin_amdgcn_s_memtime();
         ws_barrier();  // B(q+1): stage q is free
       }
     } else {
@@ -2083,8 +2081,9 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   mark(6);
   if (tl && p.stamps) {
     __syncthreads();
-    // [16384 + 2q + side]: cycles since kernel entry (side 0 producer, 1 consumer)
-    if (tid < 64) p.stamps[16384 + tid] = tls[tid] > tl0 ? tls[tid] - tl0 : 0;
+    // [16384 + 4q + e]: cycles since kernel entry of: e 0 producer past its X
+    // wait, 1 producer after the conversion, 2 producer at the barrier, 3 consumer at the barrier
+    if (tid < 128) p.stamps[16384 + tid] = tls[tid] > tl0 ? tls[tid] - tl0 : 0;
   }
   if (p.stamps && wave == 0) {
     mark(7);
@@ -2761,12 +2760,10 @@ static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, 
    (const void*)KERN<8, __VA_ARGS__>,  (const void*)KERN<9, __VA_ARGS__>,  (const void*)KERN<10, __VA_ARGS__>, \
    (const void*)KERN<11, __VA_ARGS__>, (const void*)KERN<12, __VA_ARGS__>, (const void*)KERN<13, __VA_ARGS__>, \
    (const void*)KERN<14, __VA_ARGS__>, (const void*)KERN<15, __VA_ARGS__>}
-  // [version][0 plain / 1 stamped / 2 staggered (v1 only)][NST - 2]
-  static const void* const kFns[2][3][14] = {
-      {X3F_ROW(x3_dense_fused_kernel, false), X3F_ROW(x3_dense_fused_kernel, true),
-       X3F_ROW(x3_dense_fused_kernel, false, true)},
-      {X3F_ROW(x3_dense_fused4_kernel, false), X3F_ROW(x3_dense_fused4_kernel, true),
-       X3F_ROW(x3_dense_fused4_kernel, false)}};
+  // [version][0 plain / 1 stamped][NST - 2]
+  static const void* const kFns[2][2][14] = {
+      {X3F_ROW(x3_dense_fused_kernel, false), X3F_ROW(x3_dense_fused_kernel, true)},
+      {X3F_ROW(x3_dense_fused4_kernel, false), X3F_ROW(x3_dense_fused4_kernel, true)}};
 #undef X3F_ROW
   const int nst = K / 32;
   if (nst < 2 || nst > 15 || (v != 1 && v != 2)) return hipErrorInvalidValue;
@@ -2795,9 +2792,7 @@ static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, 
   p.tiles_per_block = (p.tiles + grid - 1) / grid;
   const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
   void* args[] = {&p};
-  static const bool stg = getenv("TCAMD_X3F_STAGGER") && atoi(getenv("TCAMD_X3F_STAGGER"));
-  const hipError_t e = hipLaunchKernel(kFns[v - 1][stamp ? 1 : (stg ? 2 : 0)][nst - 2], dim3(blocks),
-                                       dim3(v == 2 ? 256 : 512),
+  const hipError_t e = hipLaunchKernel(kFns[v - 1][stamp ? 1 : 0][nst - 2], dim3(blocks), dim3(v == 2 ? 256 : 512),
                                        args, kLdsF, (hipStream_t)stream);
   if (e != hipSuccess) return e;
   g_x3f_stamp_blocks = blocks;
@@ -2821,12 +2816,12 @@ static unsigned long long* g_x3s_stamps = nullptr;  // TCAMD_X3_SMALLF_STAMP bui
 static int g_x3s_stamp_blocks = 0;
 
 // Copies the last K14x launch's step timeline (TCAMD_X3_SMALLF_STAMP=1 and
-// TCAMD_X3_SMALLF_DBG & 64): [2q + side] shader-clock cycles since block 0's
-// entry at which producer wave 4 (side 0) / consumer wave 0 (side 1) reached
-// the barrier after K step q (q < 32).
+// TCAMD_X3_SMALLF_DBG & 64): [4q + e] shader-clock cycles since block 0's
+// entry: producer wave 4 past its X wait (e 0), after the conversion (1), at
+// the barrier after K step q (2); consumer wave 0 at that barrier (3).
 int tcamd_x3_small_timeline(unsigned long long* out, int n) {
   if (!g_x3s_stamps || !out) return 0;
-  const int m = std::min(n, 64);
+  const int m = std::min(n, 128);
   if (hipDeviceSynchronize() != hipSuccess ||
       hipMemcpy(out, g_x3s_stamps + 16384, m * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
@@ -2901,7 +2896,7 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
           for (int l = 0; l < 2; ++l) {
             const hipError_t e =
                 hipFuncSetAttribute(fns[w][f][n][l], hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (4 + n) * kWsStage + (n ? 0 : 512));
+                                    (4 + n) * kWsStage + (n ? 0 : 1024));
             if (e != hipSuccess) return e;
           }
     attr_set[dev_slot].store(true, std::memory_order_release);
@@ -2913,7 +2908,7 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
   const int n5 = ns == 5 ? 1 : 0;
   const hipError_t e = hipLaunchKernel(fns[W == 14 ? 0 : 1][pf == 6 ? 1 : 0][n5][lead == 2 ? 1 : 0], dim3(blocks),
                                        dim3(512), args,
-                                       (4 + n5) * kWsStage + ((dbg & 64) && !n5 ? 512 : 0), (hipStream_t)stream);
+                                       (4 + n5) * kWsStage + ((dbg & 64) && !n5 ? 1024 : 0), (hipStream_t)stream);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }

@@ -311,52 +311,6 @@ def test_x3_dense_fused(imgs, H, K, version):
     assert _rel(x[:, K:K + 32], y2[:, K:K + 32]) < 2e-5
 
 
-def test_x3_dense_fused_stagger_variant():
-    """K11x v1 with the two waves of each SIMD staggered in the 1x1 chunk
-    (TCAMD_X3F_STAGGER=1, chosen once per process, so in a child process):
-    against fp64 torch on shapes covering the band prologue, ragged tails and
-    NST 2..15."""
-    _need_gpu()
-    import os
-    import subprocess
-    import sys
-
-    code = r'''
-import torch, torch.nn.functional as F
-from triton_client_amd.ops import hip
-st = torch.cuda.current_stream().cuda_stream
-def split(t):
-    h = t.to(torch.bfloat16)
-    return h.contiguous(), (t - h.float()).to(torch.bfloat16).contiguous()
-for imgs, H, K in [(1, 56, 64), (8, 56, 224), (5, 28, 96), (2, 16, 160), (16, 28, 480), (3, 28, 320)]:
-    g = torch.Generator(device="cuda").manual_seed(imgs * 7919 + H + K)
-    M, ldx = imgs * H * H, K + 64
-    x = torch.randn(M, ldx, device="cuda", generator=g)
-    s = torch.rand(K, device="cuda", generator=g) + 0.5
-    t = torch.randn(K, device="cuda", generator=g) * 0.2
-    w1 = torch.randn(128, K, device="cuda", generator=g) / K ** 0.5
-    b1 = torch.randn(128, device="cuda", generator=g) * 0.1
-    w2 = torch.randn(32, 128, 3, 3, device="cuda", generator=g) / (9 * 128) ** 0.5
-    f1h, f1l = (hip.x3_w1_fragments(u) for u in split(w1))
-    f2h, f2l = (hip.x3_w3f_fragments(u) for u in split(w2.permute(0, 2, 3, 1).reshape(32, -1)))
-    xc = x.clone()
-    hip.x3_dense_fused(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), f1h.data_ptr(), f1l.data_ptr(),
-                       b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), x.data_ptr() + 4 * K, ldx, stream=st)
-    torch.cuda.synchronize()
-    a = torch.relu(xc[:, :K].double() * s.double() + t.double())
-    z = torch.relu(a @ w1.double().t() + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
-    ref = F.conv2d(z, w2.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 32)
-    err = ((x[:, K:K + 32].double() - ref).norm() / ref.norm()).item()
-    assert err < 3e-5, (imgs, H, K, err)
-    assert torch.equal(x[:, :K], xc[:, :K]) and torch.equal(x[:, K + 32:], xc[:, K + 32:])
-print("K11X_STAGGER_OK")
-'''
-    env = dict(os.environ, TCAMD_X3F_STAGGER="1")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=110)
-    assert r.returncode == 0 and "K11X_STAGGER_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
-
-
 @pytest.mark.parametrize("imgs,H,K", [(1, 14, 64), (3, 14, 256), (8, 14, 288), (9, 14, 992), (17, 14, 640),
                                       (128, 14, 512), (16, 14, 96), (1, 7, 512), (5, 7, 992), (64, 7, 768),
                                       (130, 7, 544), (2, 7, 64), (40, 14, 416)])

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--k15-ab", type=int, default=0,
                     help="also time the forward with K15 GEMMs from this many tokens (interleaved A/B rounds)")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--tuned-table", default="",
+                    help="A/B against TunableOp reading this solution table (tuning off), e.g. "
+                         "triton_client_amd/models/tuned/bert_large_gfx950.csv")
     ap.add_argument("--tunable", default="",
                     help="A/B against PyTorch TunableOp (hipBLASLt / rocBLAS solution search per GEMM shape); "
                          "the tuned results go to this CSV path")
@@ -38,7 +41,12 @@ def main():
         if a.k15_ab:
             variants = {"hipblaslt": 0, "k15": a.k15_ab}
         tun = None
-        if a.tunable:
+        if a.tuned_table:
+            import torch.cuda.tunable as tun
+
+            assert bert.use_tuned_gemms(a.tuned_table), "the table does not load in this process"
+            variants = {"default": bert.K15_MIN_TOKENS, "tunableop": bert.K15_MIN_TOKENS}
+        elif a.tunable:
             import torch.cuda.tunable as tun
 
             tun.set_filename(a.tunable)

@@ -91,10 +91,15 @@ def layers(a, torch, hip):
                                  "median_phase_us": med}
             if a.stamp and a.dbg and int(a.dbg) & 64:
                 tlv = hip.x3_small_timeline()
-                n = int((tlv[:, 0] > 0).sum())
+                n = min(int((tlv[:, 2] > 0).sum()), K // 32 - 1)
                 d = tlv[:n]
-                row["timeline_cycles"] = {"producer_arrive": d[:, 0].tolist(), "consumer_arrive": d[:, 1].tolist(),
-                                          "step": np.diff(np.maximum(d[:, 0], d[:, 1])).tolist()}
+                rel = np.concatenate([[0], np.maximum(d[:-1, 2], d[:-1, 3])])  # previous barrier (approx. release)
+                row["timeline_cycles"] = {
+                    "x_wait": np.median(d[1:, 0] - rel[1:]).item(), "convert": np.median(d[1:, 1] - d[1:, 0]).item(),
+                    "w_issue_and_wait": np.median(d[1:, 2] - d[1:, 1]).item(),
+                    "producer_step": np.median(d[1:, 2] - rel[1:]).item(),
+                    "consumer_step": np.median(d[1:, 3] - rel[1:]).item(),
+                    "producer_last": int((d[1:, 2] > d[1:, 3]).sum()), "steps": n - 1}
             print(json.dumps(row), flush=True)
             out.append(row)
     return out

@@ -195,6 +195,31 @@ def init_weights(model, seed=0):
                 m.bias.zero_()
 
 
+# GEMM solutions measured on MI355X for the bert_large bucket shapes (every
+# projection at batch 1..64 x seq 384) by PyTorch TunableOp over hipBLASLt and
+# rocBLAS (tools/bert_probe.py --tunable); see use_tuned_gemms.
+TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "bert_large_gfx950.csv")
+
+
+def use_tuned_gemms(path=TUNED_GEMMS):
+    """Route torch's GEMMs through TunableOp with the measured solution table
+    (tuning itself stays off: a shape missing from the table runs the
+    library's default solution).  The table's validators (PyTorch, HIP,
+    hipBLASLt, rocBLAS, gfx arch) must match this process, else TunableOp stays
+    off.  TC_BERT_TUNED_GEMMS=0 disables it.  Returns True when it is on."""
+    if os.environ.get("TC_BERT_TUNED_GEMMS", "1") == "0" or not os.path.exists(path) or not torch.cuda.is_available():
+        return False
+    import torch.cuda.tunable as tun
+
+    tun.tuning_enable(False)
+    tun.record_untuned_enable(False)
+    tun.enable(True)
+    if not tun.read_file(path):
+        tun.enable(False)
+        return False
+    return True
+
+
 def build(device="cuda", dtype=torch.bfloat16, seed=0, layers=LAYERS):
     model = BertLargeQA(layers)
     init_weights(model, seed)

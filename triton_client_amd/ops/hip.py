@@ -779,13 +779,14 @@ def x3_dense_small(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo
 
 def x3_small_timeline():
     """Step timeline of the last K14x launch (STAMP process with TCAMD_X3_SMALLF_DBG
-    bit 64): int64 [32][2] cycles since block 0's entry at which producer wave 4
-    / consumer wave 0 reached the barrier after each K step (0 = not reached)."""
-    out = np.zeros(64, dtype=np.uint64)
+    bit 64): int64 [32][4] cycles since block 0's entry: producer wave 4 past
+    its X wait, after the conversion, at the step barrier; consumer wave 0 at
+    the step barrier (0 = not reached)."""
+    out = np.zeros(128, dtype=np.uint64)
     n = _load().tcamd_x3_small_timeline(out.ctypes.data, out.size)
     if n < 0:
         raise HipError(n, "x3_small_timeline")
-    return out.reshape(32, 2).astype(np.int64)
+    return out.reshape(32, 4).astype(np.int64)
 
 
 def x3_small_stamps(max_blocks=4096):

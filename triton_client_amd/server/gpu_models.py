@@ -540,6 +540,8 @@ class BertLarge(Model):
         self.torch = torch
         dev = torch.device("cuda", self.device_id)
         self.model = bert.build(device=dev, layers=self.layers)
+        # before the warm-up runs and graph captures below pick their GEMM solutions
+        self.tuned_gemms = bert.use_tuned_gemms()
         for _ in range(max(1, self.instance_count)):
             self._slots.append(self._make_slot(dev))
         self._free = list(range(len(self._slots)))
