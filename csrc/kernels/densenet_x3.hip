@@ -1660,8 +1660,10 @@ struct X3SmallParams {
   const float* x;  // block buffer rows of ldx (the layer's first K channels)
   const float* s1;  // [K] BN1 affine
   const float* t1;
-  const uint16_t* w1_hi;  // [128][K] bf16 (BN2 folded, K8x layout)
+  const uint16_t* w1_hi;  // [128][K] bf16 (BN2 folded, K8x layout): WR 0
   const uint16_t* w1_lo;
+  const uint16_t* w1f_hi;  // [K/16][q 4][lane 64][8] bf16 (x3_w1_fragments): WR 1
+  const uint16_t* w1f_lo;
   const float* b1;        // [128] BN2 shift
   const uint16_t* w2_hi;  // [tap 9][kq 4][oh 2][lane 64][8] bf16 (x3_w3f_fragments)
   const uint16_t* w2_lo;
@@ -1675,15 +1677,17 @@ struct X3SmallParams {
 };
 
 // W = image side (14: half-image tiles, 7: whole images); PF = X K-steps in
-// the producers' registers
-// LEAD = K steps between a stage's fill and its MFMAs: 1 (the consumer reads
-// each stage after the barrier that publishes it) or 2 (the producer fills
-// stage q+2 while the consumer runs step q from registers and reads stage q+1
-// into a second operand set: the stage reads overlap the MFMAs;
-// TCAMD_X3_SMALLF_LEAD)
-template <int W, int PF, int kSmS, int LEAD>
+// the producers' registers.
+// WR = where the consumers' W1 operand comes from: 0 = LDS-DMA copies issued
+// by the producers into each K-step stage; 1 = the consumers load their own
+// fragments (x3_w1_fragments: 1 KB per wave load) from L2 into registers one K
+// step ahead.  The step timeline showed the producer last at every barrier,
+// ~40% of its step in issuing and waiting for the W copies, and those copies
+// plus the consumers' W reads are half the stage's LDS traffic
+// (TCAMD_X3_SMALLF_WREG).  (A variant with the stage filled two steps ahead
+// and the operands read one step ahead of the MFMAs measured no faster.)
+template <int W, int PF, int kSmS, int WR>
 __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p) {
-  static_assert(LEAD == 1 || LEAD == 2, "K14x lead");
   constexpr int kLdsSm = kSmS * kWsStage;
   constexpr int kHalves = W == 14 ? 2 : 1;
   constexpr int kRowsOut = W / kHalves;              // 7
@@ -1693,7 +1697,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   constexpr int kNPG = (kPOut + 15) / 16;            // 16-pixel groups of the 3x3
   constexpr int kTRMax = (kRowsOut + kHalves) * W;   // z pixels: 112 / 49
   constexpr int kNRI = (kTRMax + 31) / 32;           // producer row passes (32 rows each)
-  constexpr int kOps = 4 + 2 + kNRI;                 // vm ops per producer iteration
+  constexpr int kOps = (WR ? 0 : 4) + 2 + kNRI;      // vm ops per producer iteration
   constexpr bool kQ4 = kTRMax <= 64;                 // 1x1 consumers split channels, not pixels
   static_assert(kTRMax <= 128, "one 1x1 tile");
   static_assert(kNPad * kRowB + 2 * 4 * 3 * kNPG * 64 * 4 <= kLdsSm, "K14x LDS budget");
@@ -1724,7 +1728,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   const int mz0 = img * W * W + zr0 * W;
   const int nst = p.K / kBK;
   const int Q = nst, Qp = (Q + PF - 1) / PF * PF;
-  // timeline diagnostic (dbg 64, 4 stages, block 0, LEAD 1): shader-clock time
+  // timeline diagnostic (dbg 64, 4 stages, block 0): shader-clock time
   // of producer wave 4 and consumer wave 0 reaching each step barrier, kept in
   // LDS past the stages (no memory op inside the counted-wait loop)
   const bool tl = (p.dbg & 64) && kSmS == 4 && blockIdx.x == 0;
@@ -1733,6 +1737,8 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   f32x16 acc[2][2];  // consumers: [channel block][pixel block] of the 128 x 128 1x1 tile
   const int wm = wave & 1, wn = (wave >> 1) & 1;
   const int col = lane & 31, h = lane >> 5;
+  const int rot = (int)(blockIdx.x % (unsigned)nst);  // blocks read different K offsets at a time
+  auto kofs = [&](int ks) { ks += rot; return (ks >= nst ? ks - nst : ks) * kBK; };
 
   if (wave >= 4) {
     // ------------------------------ producer (K8x ws) ------------------------------
@@ -1740,8 +1746,6 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
     const int pj = pt & 7, prow = pt >> 3;
     const ptrdiff_t lo_off = p.w1_lo - p.w1_hi;
     f32x4 xr[PF][kNRI], xs[PF], xt[PF];
-    const int rot = (int)(blockIdx.x % (unsigned)nst);  // blocks read different K offsets at a time
-    auto kofs = [&](int ks) { ks += rot; return (ks >= nst ? ks - nst : ks) * kBK; };
     auto issue_x = [&](int q, int slot) {
       q = min(q, Q - 1);
       const int k0 = kofs(q);
@@ -1755,7 +1759,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
       }
     };
     auto issue_w = [&](int q) {
-      if (p.dbg & 8) return;  // ablation 8: no W copies (the stages keep stale W)
+      if (WR || (p.dbg & 8)) return;  // WR 1: the consumers load W; ablation 8: no W copies
       q = min(q, Q - 1);
       const int k0 = kofs(q);
       uint8_t* st = ldss + (q % kSmS) * kWsStage + 2 * kWsPlane;
@@ -1789,67 +1793,37 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
     if (p.dbg & 128) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < PF; ++s) issue_x(s, s);
-    if constexpr (LEAD == 1) {
-      for (int s = 0; s <= kSmS - 3; ++s) issue_w(s);
-      __builtin_amdgcn_s_waitcnt(ws_vmcnt(0));
-      write_x(0, 0);
-      issue_w(kSmS - 2);
-      __builtin_amdgcn_sched_barrier(0);
-      issue_x(PF, 0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      ws_barrier();  // B0
-      for (int q0 = 0; q0 < Qp; q0 += PF) {
+    for (int s = 0; s <= kSmS - 3; ++s) issue_w(s);
+    __builtin_amdgcn_s_waitcnt(ws_vmcnt(0));
+    write_x(0, 0);
+    issue_w(kSmS - 2);
+    __builtin_amdgcn_sched_barrier(0);
+    issue_x(PF, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ws_barrier();  // B0
+    for (int q0 = 0; q0 < Qp; q0 += PF) {
 #pragma unroll
-        for (int u = 0; u < PF; ++u) {
-          const int q = q0 + u;
-          const int slot = (u + 1) % PF;
-          __builtin_amdgcn_s_waitcnt(ws_vmcnt(kOps * (PF - 1)));  // X of step q+1
-          __builtin_amdgcn_sched_barrier(0);
-          if (tl && pw == 0 && lane == 0 && q < 32) tls[4 * q] = __builtin_amdgcn_s_memtime();
-          write_x(q + 1, slot);
-          if (tl && pw == 0 && lane == 0 && q < 32) {
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // the conversion's LDS writes done
-            tls[4 * q + 1] = __builtin_amdgcn_s_memtime();
-          }
-          issue_w(q + kSmS - 1);
-          __builtin_amdgcn_sched_barrier(0);  // W copies ahead of the X loads (vmcnt retires in order)
-          issue_x(q + 1 + PF, slot);
-          __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0((2 + kNRI) + kOps * (kSmS - 2)));  // W of step q+1
-          if (tl && pw == 0 && lane == 0 && q < 32)  // timeline: producer wave 4 at the barrier (LDS, no vm op)
-            tls[4 * q + 2] = __builtin_amdgcn_s_memtime();
-          ws_barrier();  // B(q+1)
+      for (int u = 0; u < PF; ++u) {
+        const int q = q0 + u;
+        const int slot = (u + 1) % PF;
+        __builtin_amdgcn_s_waitcnt(ws_vmcnt(kOps * (PF - 1)));  // X of step q+1
+        __builtin_amdgcn_sched_barrier(0);
+        if (tl && pw == 0 && lane == 0 && q < 32) tls[4 * q] = __builtin_amdgcn_s_memtime();
+        write_x(q + 1, slot);
+        if (tl && pw == 0 && lane == 0 && q < 32) {
+          __builtin_amdgcn_s_waitcnt(0xc07f);  // the conversion's LDS writes done
+          tls[4 * q + 1] = __builtin_amdgcn_s_memtime();
         }
-      }
-    } else {
-      // stages 0 and 1 complete before B0; then interval q (B(q) .. B(q+1))
-      // fills stage q+2: X(q+2) from the registers, W(q+kSmS-1) by DMA, and
-      // waits for W(q+2).  The prologue's "iterations" -2 (X only) and -1
-      // (W + X) keep every later iteration's counted waits exact.
-      for (int s = 0; s <= kSmS - 3; ++s) issue_w(s);
-      __builtin_amdgcn_s_waitcnt(ws_vmcnt(0));
-      write_x(0, 0);
-      write_x(1, 1 % PF);
-      __builtin_amdgcn_sched_barrier(0);
-      issue_x(PF, 0);
-      issue_w(kSmS - 2);
-      __builtin_amdgcn_sched_barrier(0);
-      issue_x(PF + 1, 1 % PF);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      ws_barrier();  // B0
-      for (int q0 = 0; q0 < Qp; q0 += PF) {
-#pragma unroll
-        for (int u = 0; u < PF; ++u) {
-          const int q = q0 + u;
-          const int slot = (u + 2) % PF;
-          __builtin_amdgcn_s_waitcnt(ws_vmcnt(kOps * (PF - 1)));  // X of step q+2
-          __builtin_amdgcn_sched_barrier(0);
-          write_x(q + 2, slot);
-          issue_w(q + kSmS - 1);
-          __builtin_amdgcn_sched_barrier(0);
-          issue_x(q + 2 + PF, slot);
-          __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0((2 + kNRI) + kOps * (kSmS - 3)));  // W of step q+2
-          ws_barrier();  // B(q+1)
-        }
+        issue_w(q + kSmS - 1);
+        __builtin_amdgcn_sched_barrier(0);  // W copies ahead of the X loads (vmcnt retires in order)
+        issue_x(q + 1 + PF, slot);
+        if constexpr (WR)
+          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this step's stage writes
+        else
+          __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0((2 + kNRI) + kOps * (kSmS - 2)));  // + W of step q+1
+        if (tl && pw == 0 && lane == 0 && q < 32)  // timeline: producer wave 4 at the barrier (LDS, no vm op)
+          tls[4 * q + 2] = __builtin_amdgcn_s_memtime();
+        ws_barrier();  // B(q+1)
       }
     }
   } else {
@@ -1861,41 +1835,53 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
     const int rv = TR - 64 * wm;  // valid z rows from this wave's first
-    // one K step's operands: [kk][channel block] W hi/lo, [kk][pixel block] X hi/lo
-    // (7x7: W of this wave's channel quarter in [kk][0])
-    struct Ops {
-      v4u ah[2][2], al[2][2], bh[2][2], bl[2][2];
+    // one K step's operands: W hi/lo [kk][channel block], X hi/lo [kk][pixel
+    // block] (7x7: W of this wave's channel quarter in [kk][0])
+    struct AOps {
+      v4u h[2][2], l[2][2];
     };
-    auto rd = [&](int q, Ops& o) {
+    struct BOps {
+      v4u h[2][2], l[2][2];
+    };
+    auto rd_b = [&](int q, BOps& o) {
       const uint8_t* st = ldss + (q % kSmS) * kWsStage;
-      if constexpr (kQ4) {
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const int wo = ws_chunk(32 * wave + col, 2 * kk + h);
-          o.ah[kk][0] = ld16(st + 2 * kWsPlane + wo);
-          o.al[kk][0] = ld16(st + 3 * kWsPlane + wo);
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            const int xo = ws_chunk(32 * b + col, 2 * kk + h);
-            o.bh[kk][b] = ld16(st + xo);
-            o.bl[kk][b] = ld16(st + kWsPlane + xo);
-          }
+        for (int b = 0; b < 2; ++b) {
+          const int xo = ws_chunk((kQ4 ? 0 : 64 * wm) + 32 * b + col, 2 * kk + h);
+          o.h[kk][b] = ld16(st + xo);
+          o.l[kk][b] = ld16(st + kWsPlane + xo);
         }
-      } else {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            const int xo = ws_chunk(64 * wm + 32 * b + col, 2 * kk + h);
-            const int wo = ws_chunk(64 * wn + 32 * b + col, 2 * kk + h);
-            o.bh[kk][b] = ld16(st + xo);
-            o.bl[kk][b] = ld16(st + kWsPlane + xo);
-            o.ah[kk][b] = ld16(st + 2 * kWsPlane + wo);
-            o.al[kk][b] = ld16(st + 3 * kWsPlane + wo);
-          }
-      }
     };
-    auto mma = [&](const Ops& o) {
+    constexpr int kNA = kQ4 ? 1 : 2;  // channel blocks per consumer wave
+    auto rd_a = [&](int q, AOps& o) {  // WR 0: from the stage
+      const uint8_t* st = ldss + (q % kSmS) * kWsStage;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int a = 0; a < kNA; ++a) {
+          const int wo = ws_chunk(kQ4 ? 32 * wave + col : 64 * wn + 32 * a + col, 2 * kk + h);
+          o.h[kk][a] = ld16(st + 2 * kWsPlane + wo);
+          o.l[kk][a] = ld16(st + 3 * kWsPlane + wo);
+        }
+    };
+    // WR 1: this wave's fragments from L2 (1 KB per wave load) as buffer
+    // loads: a lane-constant VGPR offset and the step's offset in an SGPR
+    const auto w1h = __builtin_amdgcn_make_buffer_rsrc((void*)p.w1f_hi, (short)0, p.K * 256, 0x00020000);
+    const auto w1l = __builtin_amdgcn_make_buffer_rsrc((void*)p.w1f_lo, (short)0, p.K * 256, 0x00020000);
+    auto ld_a = [&](int q, AOps& o) {
+      const int k16 = kofs(min(q, Q - 1)) / 16;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int a = 0; a < kNA; ++a) {
+          const int vo = ((kQ4 ? wave : 2 * wn + a) * 64 + lane) * 16;
+          o.h[kk][a] = __builtin_amdgcn_raw_buffer_load_b128(w1h, vo, (k16 + kk) * 4096, 0);
+          o.l[kk][a] = __builtin_amdgcn_raw_buffer_load_b128(w1l, vo, (k16 + kk) * 4096, 0);
+        }
+    };
+    auto mma = [&](const AOps& A, const BOps& B) {
       if constexpr (kQ4) {
         // 7x7: the tile is <= 64 rows, so the 4 waves split the 128 channels
         // instead (wave = 32-channel quarter x both 32-pixel blocks)
@@ -1903,53 +1889,70 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
           for (int b = 0; b < 2; ++b)
-            if (b == 0 || TR > 32) acc[0][b] = x3_32(o.ah[kk][0], o.al[kk][0], o.bh[kk][b], o.bl[kk][b], acc[0][b]);
+            if (b == 0 || TR > 32) acc[0][b] = x3_32(A.h[kk][0], A.l[kk][0], B.h[kk][b], B.l[kk][b], acc[0][b]);
       } else if (rv > 32) {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
           for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int b = 0; b < 2; ++b) acc[a][b] = x3_32(o.ah[kk][a], o.al[kk][a], o.bh[kk][b], o.bl[kk][b], acc[a][b]);
+            for (int b = 0; b < 2; ++b) acc[a][b] = x3_32(A.h[kk][a], A.l[kk][a], B.h[kk][b], B.l[kk][b], acc[a][b]);
       } else if (rv > 0) {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-          for (int a = 0; a < 2; ++a) acc[a][0] = x3_32(o.ah[kk][a], o.al[kk][a], o.bh[kk][0], o.bl[kk][0], acc[a][0]);
+          for (int a = 0; a < 2; ++a) acc[a][0] = x3_32(A.h[kk][a], A.l[kk][a], B.h[kk][0], B.l[kk][0], acc[a][0]);
       }
     };
     const bool live = !(p.dbg & 4) && (kQ4 || rv > 0);  // ablation 4: no MFMAs / stage reads
-    ws_barrier();  // B0
-    mark(1);
-    if constexpr (LEAD == 1) {
+    auto stamp_c = [&](int q) {
+      if (tl && wave == 0 && lane == 0 && q < 32) tls[4 * q + 3] = __builtin_amdgcn_s_memtime();
+    };
+    if constexpr (!WR) {
+      ws_barrier();  // B0
+      mark(1);
       for (int q = 0; q < Qp; ++q) {
         if (q < Q && live) {
-          Ops o;
-          rd(q, o);
-          mma(o);
+          AOps A;
+          BOps B;
+          rd_b(q, B);
+          rd_a(q, A);
+          mma(A, B);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (tl && wave == 0 && lane == 0 && q < 32) tls[4 * q + 3] = __builtin_amdgcn_s_memtime();
+        stamp_c(q);
         ws_barrier();  // B(q+1): stage q is free
       }
     } else {
-      // step q runs from registers read in interval q-1 while stage q+1 is read
-      Ops oa, ob;
-      if (live) rd(0, oa);
-      // both loop entries (this one and the back edge) then hold no pending
-      // LDS reads, so the MFMAs of a step need no wait for the reads issued
-      // just before them
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-      for (int q = 0; q < Qp; q += 2) {
-        if (q + 1 < Q && live) rd(q + 1, ob);
-        if (q < Q && live) mma(oa);
+      // W of step q is loaded during step q-1 (two register sets, the loop
+      // unrolled by 2 so each has a fixed name); the step's counted wait
+      // leaves the next step's kNA x 4 fragment loads in flight
+      // The prefetch is unconditional (past the last step it reloads that
+      // step's fragments): with a conditional one the compiler's own waits
+      // before the MFMAs assume the no-prefetch path and drain it.  Every
+      // consumer wave is live here (14x14: >= 48 z rows per pixel block;
+      // 7x7: channel quarters), so the dbg 4 ablation does not apply.
+      constexpr int kAOps = 4 * kNA;
+      AOps fa, fb;
+      ld_a(0, fa);  // lands during the producers' prologue
+      ws_barrier();  // B0
+      mark(1);
+      auto step = [&](int q, const AOps& cur, AOps& nxt) {
+        ld_a(q + 1, nxt);
+        if (q < Q) {
+          BOps B;
+          rd_b(q, B);
+          __builtin_amdgcn_s_waitcnt(ws_vmcnt(kAOps));  // this step's fragments
+          mma(cur, B);
+        }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        stamp_c(q);
         ws_barrier();  // B(q+1)
+      };
+      for (int q = 0; q < Qp; q += 2) {
+        step(q, fa, fb);
         if (q + 1 >= Qp) break;
-        if (q + 2 < Q && live) rd(q + 2, oa);
-        if (q + 1 < Q && live) mma(ob);
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-        ws_barrier();  // B(q+2)
+        step(q + 1, fb, fa);
       }
     }
   }
@@ -2843,8 +2846,8 @@ int tcamd_x3_small_stamps(unsigned long long* out, int n) {
 // tiles) block in one kernel; w1 in the K8x [128][K] layout, w2 in
 // x3_w3f_fragments.  K a multiple of 32 (>= 64).
 int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K, const float* s1, const float* t1,
-                         const void* w1_hi, const void* w1_lo, const float* b1, const void* w2_hi, const void* w2_lo,
-                         float* y, int ldy, void* stream) {
+                         const void* w1_hi, const void* w1_lo, const void* w1f_hi, const void* w1f_lo,
+                         const float* b1, const void* w2_hi, const void* w2_lo, float* y, int ldy, void* stream) {
   if (imgs <= 0) return hipSuccess;
   if ((W != 14 && W != 7) || H != W || K < 64 || K % 32 || ldx < K || ldx % 4 || ldy % 4)
     return hipErrorInvalidValue;
@@ -2853,12 +2856,15 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
       !aligned16(b1) || !aligned16(w2_hi) || !aligned16(w2_lo) || !aligned16(y))
     return hipErrorInvalidValue;
   if ((size_t)imgs * H * W >= (1u << 30) / 4) return hipErrorInvalidValue;
+  if ((!w1f_hi) != (!w1f_lo) || (w1f_hi && (!aligned16(w1f_hi) || !aligned16(w1f_lo)))) return hipErrorInvalidValue;
   X3SmallParams p;
   p.x = x;
   p.s1 = s1;
   p.t1 = t1;
   p.w1_hi = (const uint16_t*)w1_hi;
   p.w1_lo = (const uint16_t*)w1_lo;
+  p.w1f_hi = (const uint16_t*)w1f_hi;
+  p.w1f_lo = (const uint16_t*)w1f_lo;
   p.b1 = b1;
   p.w2_hi = (const uint16_t*)w2_hi;
   p.w2_lo = (const uint16_t*)w2_lo;
@@ -2880,10 +2886,14 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
   // and K-step stages (TCAMD_X3_SMALLF_STAGES 4 or 5), for A/B runs
   static const int pf = getenv("TCAMD_X3_SMALLF_PF") ? atoi(getenv("TCAMD_X3_SMALLF_PF")) : 3;
   static const int ns = getenv("TCAMD_X3_SMALLF_STAGES") ? atoi(getenv("TCAMD_X3_SMALLF_STAGES")) : 4;
-  static const int lead = getenv("TCAMD_X3_SMALLF_LEAD") ? atoi(getenv("TCAMD_X3_SMALLF_LEAD")) : 1;
+  // W1 for the consumers (TCAMD_X3_SMALLF_WREG, default 1): from their own
+  // register loads of the fragments when the caller passed them, else by the
+  // producers' LDS-DMA copies
+  static const int wreg = getenv("TCAMD_X3_SMALLF_WREG") ? atoi(getenv("TCAMD_X3_SMALLF_WREG")) : 1;
+  const int wr = wreg && w1f_hi ? 1 : 0;
 #define X3S_FN(HW, PF_, NS_)                                                                    \
-  {(const void*)x3_dense_small_kernel<HW, PF_, NS_, 1>, (const void*)x3_dense_small_kernel<HW, PF_, NS_, 2>}
-  // [14x14 / 7x7][PF 3 / 6][4 / 5 stages][lead 1 / 2]
+  {(const void*)x3_dense_small_kernel<HW, PF_, NS_, 0>, (const void*)x3_dense_small_kernel<HW, PF_, NS_, 1>}
+  // [14x14 / 7x7][PF 3 / 6][4 / 5 stages][W1 by DMA / by consumer loads]
   const void* const fns[2][2][2][2] = {{{X3S_FN(14, 3, 4), X3S_FN(14, 3, 5)}, {X3S_FN(14, 6, 4), X3S_FN(14, 6, 5)}},
                                        {{X3S_FN(7, 3, 4), X3S_FN(7, 3, 5)}, {X3S_FN(7, 6, 4), X3S_FN(7, 6, 5)}}};
 #undef X3S_FN
@@ -2906,7 +2916,7 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
   g_x3s_stamp_blocks = blocks;
   void* args[] = {&p};
   const int n5 = ns == 5 ? 1 : 0;
-  const hipError_t e = hipLaunchKernel(fns[W == 14 ? 0 : 1][pf == 6 ? 1 : 0][n5][lead == 2 ? 1 : 0], dim3(blocks),
+  const hipError_t e = hipLaunchKernel(fns[W == 14 ? 0 : 1][pf == 6 ? 1 : 0][n5][wr], dim3(blocks),
                                        dim3(512), args,
                                        (4 + n5) * kWsStage + ((dbg & 64) && !n5 ? 1024 : 0), (hipStream_t)stream);
   if (e != hipSuccess) return e;

@@ -314,14 +314,17 @@ def test_x3_dense_fused(imgs, H, K, version):
 @pytest.mark.parametrize("imgs,H,K", [(1, 14, 64), (3, 14, 256), (8, 14, 288), (9, 14, 992), (17, 14, 640),
                                       (128, 14, 512), (16, 14, 96), (1, 7, 512), (5, 7, 992), (64, 7, 768),
                                       (130, 7, 544), (2, 7, 64), (40, 14, 416)])
-def test_x3_dense_small(imgs, H, K):
+@pytest.mark.parametrize("wfrag", [True, False])
+def test_x3_dense_small(imgs, H, K, wfrag):
     """K14x: the whole dense layer of a 14x14 (half-image tiles with a halo
     row) or 7x7 (whole-image tiles) block in one kernel, z in a zero-padded
     LDS image of the tile.  Ragged image counts (not multiples of 8: the 14x14
     grid pairs the halves of images 8g+j), K from 64 to 992 (2..31 K steps,
     every padding-round count of both producer depths) and a layer slice in
     the middle of a wider block buffer.  Against fp64 torch (< 3e-5), and
-    against the two-kernel path on the same split products."""
+    against the two-kernel path on the same split products.  wfrag: the 1x1
+    consumers load their W1 fragments themselves (default engine path) or
+    read the producers' LDS copies."""
     _need_gpu()
     hip = _hip()
     g = torch.Generator(device=DEV).manual_seed(imgs * 131 + H * 7 + K)
@@ -335,9 +338,11 @@ def test_x3_dense_small(imgs, H, K):
     w1h, w1l = _split(w1)
     w2p = _split(w2.permute(0, 2, 3, 1).reshape(32, -1))
     f2h, f2l = (hip.x3_w3f_fragments(u) for u in w2p)
+    f1 = [hip.x3_w1_fragments(u) for u in (w1h, w1l)] if wfrag else None
     xc = x.clone()
     hip.x3_dense_small(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), w1h.data_ptr(), w1l.data_ptr(),
-                       b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), x.data_ptr() + 4 * K, ldx, stream=_st())
+                       b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), x.data_ptr() + 4 * K, ldx, stream=_st(),
+                       w1f_hi=f1[0].data_ptr() if f1 else None, w1f_lo=f1[1].data_ptr() if f1 else None)
     torch.cuda.synchronize()
     a = torch.relu(xc[:, :K].double() * s.double() + t.double())
     z = torch.relu(a @ w1.double().t() + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
@@ -359,13 +364,13 @@ def test_x3_dense_small(imgs, H, K):
     assert _rel(x[:, K:K + 32], y2[:, K:K + 32]) < 2e-5
 
 
-@pytest.mark.parametrize("pf,stages,lead", [("6", "4", "1"), ("3", "5", "1"), ("6", "5", "1"), ("3", "4", "2"),
-                                            ("6", "4", "2"), ("3", "5", "2"), ("6", "5", "2")])
-def test_x3_dense_small_variants(pf, stages, lead):
+@pytest.mark.parametrize("pf,stages,wreg", [("6", "4", "1"), ("3", "5", "1"), ("6", "5", "1"), ("6", "4", "0"),
+                                            ("3", "5", "0"), ("6", "5", "0")])
+def test_x3_dense_small_variants(pf, stages, wreg):
     """K14x's A/B variants (TCAMD_X3_SMALLF_PF: X steps in the producers'
     registers; TCAMD_X3_SMALLF_STAGES: K-step stages, 5 = 160 KB of LDS;
-    TCAMD_X3_SMALLF_LEAD 2: stages filled two steps ahead, operands read one
-    step ahead of the MFMAs), chosen
+    TCAMD_X3_SMALLF_WREG: W1 by consumer fragment loads or producer LDS
+    copies), chosen
     once per process, so in a child process: the same fp64 comparison as
     test_x3_dense_small on shapes that cover every padding-round count."""
     _need_gpu()
@@ -391,9 +396,11 @@ for imgs, H, K in [(3, 14, 256), (9, 14, 992), (17, 14, 640), (16, 14, 96), (5, 
     w2 = torch.randn(32, 128, 3, 3, device="cuda", generator=g) / (9 * 128) ** 0.5
     w1h, w1l = split(w1)
     f2h, f2l = (hip.x3_w3f_fragments(u) for u in split(w2.permute(0, 2, 3, 1).reshape(32, -1)))
+    f1h, f1l = hip.x3_w1_fragments(w1h), hip.x3_w1_fragments(w1l)
     xc = x.clone()
     hip.x3_dense_small(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), w1h.data_ptr(), w1l.data_ptr(),
-                       b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), x.data_ptr() + 4 * K, ldx, stream=st)
+                       b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), x.data_ptr() + 4 * K, ldx, stream=st,
+                       w1f_hi=f1h.data_ptr(), w1f_lo=f1l.data_ptr())
     torch.cuda.synchronize()
     a = torch.relu(xc[:, :K].double() * s.double() + t.double())
     z = torch.relu(a @ w1.double().t() + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
@@ -403,7 +410,7 @@ for imgs, H, K in [(3, 14, 256), (9, 14, 992), (17, 14, 640), (16, 14, 96), (5, 
     assert torch.equal(x[:, :K], xc[:, :K]) and torch.equal(x[:, K + 32:], xc[:, K + 32:])
 print("K14X_VARIANT_OK")
 '''
-    env = dict(os.environ, TCAMD_X3_SMALLF_PF=pf, TCAMD_X3_SMALLF_STAGES=stages, TCAMD_X3_SMALLF_LEAD=lead)
+    env = dict(os.environ, TCAMD_X3_SMALLF_PF=pf, TCAMD_X3_SMALLF_STAGES=stages, TCAMD_X3_SMALLF_WREG=wreg)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "K14X_VARIANT_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

@@ -57,10 +57,12 @@ def layers(a, torch, hip):
                                    w1l.data_ptr(), b1.data_ptr(), zh.data_ptr(), zl.data_ptr(), w3[0].data_ptr(),
                                    w3[1].data_ptr(), y, ldx, ws=ws.data_ptr(), ws_bytes=ws.numel(), stream=st)
 
+            f1 = [hip.x3_w1_fragments(u) for u in (w1h, w1l)]
+
             def k14():
                 hip.x3_dense_small(x.data_ptr(), ldx, a.imgs, hw, hw, K, s.data_ptr(), t.data_ptr(), w1h.data_ptr(),
                                    w1l.data_ptr(), b1.data_ptr(), f2[0].data_ptr(), f2[1].data_ptr(), y, ldx,
-                                   stream=st)
+                                   stream=st, w1f_hi=f1[0].data_ptr(), w1f_lo=f1[1].data_ptr())
 
             for f in (pair, k14):
                 f()
@@ -149,7 +151,8 @@ def main():
     ap.add_argument("--no-layers", action="store_true")
     ap.add_argument("--pf", default="", help="TCAMD_X3_SMALLF_PF for this process (3 or 6)")
     ap.add_argument("--dbg", default="", help="TCAMD_X3_SMALLF_DBG ablation flags (1 no 3x3, 2 X of image 0)")
-    ap.add_argument("--lead", default="", help="TCAMD_X3_SMALLF_LEAD for this process (1 or 2)")
+    ap.add_argument("--wreg", default="", help="TCAMD_X3_SMALLF_WREG for this process (0: W1 by producer "
+                                               "LDS copies, 1: consumer fragment loads)")
     ap.add_argument("--stages", default="", help="TCAMD_X3_SMALLF_STAGES for this process (4 or 5)")
     ap.add_argument("--stamp", action="store_true", help="in-kernel timeline marks of one launch per layer")
     a = ap.parse_args()
@@ -157,8 +160,8 @@ def main():
         os.environ["TCAMD_X3_SMALLF_PF"] = a.pf  # read by the library at its first K14x launch
     if a.dbg:
         os.environ["TCAMD_X3_SMALLF_DBG"] = a.dbg
-    if a.lead:
-        os.environ["TCAMD_X3_SMALLF_LEAD"] = a.lead
+    if a.wreg:
+        os.environ["TCAMD_X3_SMALLF_WREG"] = a.wreg
     if a.stages:
         os.environ["TCAMD_X3_SMALLF_STAGES"] = a.stages
     if a.stamp:

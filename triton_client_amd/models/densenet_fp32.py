@@ -224,7 +224,8 @@ class FusedDenseNetFP32:
                 for L in layers:
                     hip.x3_dense_small(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
                                        L["w1h"].data_ptr(), L["w1l"].data_ptr(), L["b1"].data_ptr(),
-                                       L["w2fh"].data_ptr(), L["w2fl"].data_ptr(), fp + 4 * L["cin"], ctot, stream=st)
+                                       L["w2fh"].data_ptr(), L["w2fl"].data_ptr(), fp + 4 * L["cin"], ctot, stream=st,
+                                       w1f_hi=L["w1fh"].data_ptr(), w1f_lo=L["w1fl"].data_ptr())
                 self._transition(bi, fp, ctot, b, hw, ws, wsb, st)
                 continue
             ch = self.chain[bi]

@@ -223,7 +223,7 @@ _SIGS = {
         [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
         ],
         ctypes.c_int,
     ),
@@ -768,13 +768,17 @@ def gemm_bf16(x, w, y, M, N, K, bias=None, residual=None, epilogue="none", ldx=N
            "gemm_bf16")
 
 
-def x3_dense_small(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None):
+def x3_dense_small(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None,
+                   w1f_hi=None, w1f_lo=None):
     """K14x: one fp32-parity dense layer of the 14x14 (half-image tiles + one
     halo row) or 7x7 (whole-image tiles) block in ONE kernel, z kept in a
     zero-padded LDS image of the tile.  ``w1_*`` in the K8x [128][K] layout,
-    ``w2_*`` in x3_w3f_fragments; K a multiple of 32, >= 64."""
-    _check(_load().tcamd_x3_dense_small(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
-                                        w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_small")
+    ``w2_*`` in x3_w3f_fragments; K a multiple of 32, >= 64.  With
+    ``w1f_*`` (x3_w1_fragments of the same W1) the 1x1 consumers load their
+    W1 operand themselves instead of from the producers' LDS copies."""
+    _check(_load().tcamd_x3_dense_small(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo,
+                                        _vp(w1f_hi), _vp(w1f_lo), b1, w2_hi, w2_lo, y, int(ldy), _vp(stream)),
+           "x3_dense_small")
 
 
 def x3_small_timeline():
