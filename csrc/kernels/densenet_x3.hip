@@ -1697,7 +1697,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   constexpr int kNPG = (kPOut + 15) / 16;            // 16-pixel groups of the 3x3
   constexpr int kTRMax = (kRowsOut + kHalves) * W;   // z pixels: 112 / 49
   constexpr int kNRI = (kTRMax + 31) / 32;           // producer row passes (32 rows each)
-  constexpr int kOps = (WR ? 0 : 4) + 2 + kNRI;      // vm ops per producer iteration
+  constexpr int kOps = (WR ? 0 : 4 + 2) + kNRI;      // vm ops per producer iteration
   constexpr bool kQ4 = kTRMax <= 64;                 // 1x1 consumers split channels, not pixels
   static_assert(kTRMax <= 128, "one 1x1 tile");
   static_assert(kNPad * kRowB + 2 * 4 * 3 * kNPG * 64 * 4 <= kLdsSm, "K14x LDS budget");
@@ -1739,6 +1739,8 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   const int col = lane & 31, h = lane >> 5;
   const int rot = (int)(blockIdx.x % (unsigned)nst);  // blocks read different K offsets at a time
   auto kofs = [&](int ks) { ks += rot; return (ks >= nst ? ks - nst : ks) * kBK; };
+  // WR 1: BN1 affine s1 | t1 (2 x K floats) in stage 0's unused W planes
+  float* const bnl = reinterpret_cast<float*>(ldss + 2 * kWsPlane);
 
   if (wave >= 4) {
     // ------------------------------ producer (K8x ws) ------------------------------
@@ -1746,11 +1748,17 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
     const int pj = pt & 7, prow = pt >> 3;
     const ptrdiff_t lo_off = p.w1_lo - p.w1_hi;
     f32x4 xr[PF][kNRI], xs[PF], xt[PF];
+    // WR 1: the BN1 affine of every step after the first comes from the LDS
+    // copy the consumers make before B0 (two fewer 1 KB wave loads per step
+    // on the vector-memory path the consumers' fragment loads share)
     auto issue_x = [&](int q, int slot) {
+      const bool st_ld = !WR || q == 0;
       q = min(q, Q - 1);
       const int k0 = kofs(q);
-      xs[slot] = ldf4(p.s1 + k0 + 4 * pj);
-      xt[slot] = ldf4(p.t1 + k0 + 4 * pj);
+      if (st_ld) {
+        xs[slot] = ldf4(p.s1 + k0 + 4 * pj);
+        xt[slot] = ldf4(p.t1 + k0 + 4 * pj);
+      }
 #pragma unroll
       for (int i = 0; i < kNRI; ++i) {
         // ablation 2: every block reads image 0's rows (X L2-resident)
@@ -1774,7 +1782,12 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
     auto write_x = [&](int q, int slot) {
       if (p.dbg & 16) return;  // ablation 16: no X conversion / stage writes
       uint8_t* st = ldss + (q % kSmS) * kWsStage;
-      const f32x4 sc = xs[slot], sb = xt[slot];
+      f32x4 sc = xs[slot], sb = xt[slot];
+      if (WR && q > 0) {
+        const int k0 = kofs(min(q, Q - 1)) + 4 * pj;
+        sc = *reinterpret_cast<const f32x4*>(bnl + k0);
+        sb = *reinterpret_cast<const f32x4*>(bnl + p.K + k0);
+      }
 #pragma unroll
       for (int i = 0; i < kNRI; ++i) {
         // rows >= TR hold row TR-1's data (clamped loads): their z columns
@@ -1933,8 +1946,14 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
       // consumer wave is live here (14x14: >= 48 z rows per pixel block;
       // 7x7: channel quarters), so the dbg 4 ablation does not apply.
       constexpr int kAOps = 4 * kNA;
+      // the producers' BN1 affine for steps >= 1 (published by B0)
+      for (int i = tid; i < p.K / 4; i += 256) {
+        *reinterpret_cast<f32x4*>(bnl + 4 * i) = ldf4(p.s1 + 4 * i);
+        *reinterpret_cast<f32x4*>(bnl + p.K + 4 * i) = ldf4(p.t1 + 4 * i);
+      }
       AOps fa, fb;
       ld_a(0, fa);  // lands during the producers' prologue
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the copy is in LDS
       ws_barrier();  // B0
       mark(1);
       auto step = [&](int q, const AOps& cur, AOps& nxt) {
@@ -2890,7 +2909,7 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
   // register loads of the fragments when the caller passed them, else by the
   // producers' LDS-DMA copies
   static const int wreg = getenv("TCAMD_X3_SMALLF_WREG") ? atoi(getenv("TCAMD_X3_SMALLF_WREG")) : 1;
-  const int wr = wreg && w1f_hi ? 1 : 0;
+  const int wr = wreg && w1f_hi && K <= 2048 ? 1 : 0;  // WR 1 keeps the BN1 affine (8 K bytes) in 16 KB of LDS
 #define X3S_FN(HW, PF_, NS_)                                                                    \
   {(const void*)x3_dense_small_kernel<HW, PF_, NS_, 0>, (const void*)x3_dense_small_kernel<HW, PF_, NS_, 1>}
   // [14x14 / 7x7][PF 3 / 6][4 / 5 stages][W1 by DMA / by consumer loads]
