@@ -1640,8 +1640,9 @@ x3_dense_fused4_kernel(X3FusedParams p) {
 //   1x1 (K -> 128, BN1+ReLU prologue, BN2-folded bias+ReLU epilogue): the K8x
 //   ws pipeline on ONE tile of <= 128 rows: producer waves 4-7 keep PF K steps
 //   of X in flight in registers and stage each step split hi/lo into LDS, W
-//   slices go by LDS-DMA, consumer waves 0-3 run the 32x32x16 MFMAs (2 x 2
-//   blocks of the 128 x 128 tile each); one raw s_barrier per K step.
+//   slices go by LDS-DMA (or the consumers load their own W1 fragments: WR),
+//   consumer waves 0-3 run the 32x32x16 MFMAs (wave = 32-channel quarter x
+//   every 32-pixel block of the tile); one raw s_barrier per K step.
 //   The epilogue writes z into a zero-PADDED image of the tile in LDS
 //   ([rows+2][W+2] pixels x 512 B, 16-B chunks XOR-swizzled by pixel) that
 //   aliases the drained K-step stages, so every 3x3 tap is one constant
@@ -1698,7 +1699,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   constexpr int kTRMax = (kRowsOut + kHalves) * W;   // z pixels: 112 / 49
   constexpr int kNRI = (kTRMax + 31) / 32;           // producer row passes (32 rows each)
   constexpr int kOps = (WR ? 0 : 4 + 2) + kNRI;      // vm ops per producer iteration
-  constexpr bool kQ4 = kTRMax <= 64;                 // 1x1 consumers split channels, not pixels
+  constexpr int kNB = (kTRMax + 31) / 32;            // 32-pixel blocks of the 1x1 tile: 4 / 2
   static_assert(kTRMax <= 128, "one 1x1 tile");
   static_assert(kNPad * kRowB + 2 * 4 * 3 * kNPG * 64 * 4 <= kLdsSm, "K14x LDS budget");
   extern __shared__ __attribute__((aligned(16))) uint8_t ldss[];
@@ -1734,8 +1735,11 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   const bool tl = (p.dbg & 64) && kSmS == 4 && blockIdx.x == 0;
   unsigned long long* const tls = reinterpret_cast<unsigned long long*>(ldss + kSmS * kWsStage);
   const unsigned long long tl0 = __builtin_amdgcn_s_memtime();
-  f32x16 acc[2][2];  // consumers: [channel block][pixel block] of the 128 x 128 1x1 tile
-  const int wm = wave & 1, wn = (wave >> 1) & 1;
+  // consumer wave = 32-channel quarter of the 1x1 output x every 32-pixel
+  // block: each W1 fragment is loaded by one wave only (a 2 x 2 split of the
+  // 128 x 128 tile loaded every fragment twice), for twice the X operand
+  // reads, which go to LDS (256 B/clk) instead of the vector-memory path
+  f32x16 acc[kNB];
   const int col = lane & 31, h = lane >> 5;
   const int rot = (int)(blockIdx.x % (unsigned)nst);  // blocks read different K offsets at a time
   auto kofs = [&](int ks) { ks += rot; return (ks >= nst ? ks - nst : ks) * kBK; };
@@ -1842,42 +1846,35 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   } else {
     // ------------------------------- consumer -------------------------------
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < kNB; ++b)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
-    const int rv = TR - 64 * wm;  // valid z rows from this wave's first
-    // one K step's operands: W hi/lo [kk][channel block], X hi/lo [kk][pixel
-    // block] (7x7: W of this wave's channel quarter in [kk][0])
+      for (int e = 0; e < 16; ++e) acc[b][e] = 0.f;
+    // one K step's operands: W hi/lo [kk] of this wave's channel quarter, X hi/lo [kk][pixel block]
     struct AOps {
-      v4u h[2][2], l[2][2];
+      v4u h[2], l[2];
     };
     struct BOps {
-      v4u h[2][2], l[2][2];
+      v4u h[2][kNB], l[2][kNB];
     };
     auto rd_b = [&](int q, BOps& o) {
       const uint8_t* st = ldss + (q % kSmS) * kWsStage;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int xo = ws_chunk((kQ4 ? 0 : 64 * wm) + 32 * b + col, 2 * kk + h);
+        for (int b = 0; b < kNB; ++b) {
+          const int xo = ws_chunk(32 * b + col, 2 * kk + h);
           o.h[kk][b] = ld16(st + xo);
           o.l[kk][b] = ld16(st + kWsPlane + xo);
         }
     };
-    constexpr int kNA = kQ4 ? 1 : 2;  // channel blocks per consumer wave
     auto rd_a = [&](int q, AOps& o) {  // WR 0: from the stage
       const uint8_t* st = ldss + (q % kSmS) * kWsStage;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int a = 0; a < kNA; ++a) {
-          const int wo = ws_chunk(kQ4 ? 32 * wave + col : 64 * wn + 32 * a + col, 2 * kk + h);
-          o.h[kk][a] = ld16(st + 2 * kWsPlane + wo);
-          o.l[kk][a] = ld16(st + 3 * kWsPlane + wo);
-        }
+      for (int kk = 0; kk < 2; ++kk) {
+        const int wo = ws_chunk(32 * wave + col, 2 * kk + h);
+        o.h[kk] = ld16(st + 2 * kWsPlane + wo);
+        o.l[kk] = ld16(st + 3 * kWsPlane + wo);
+      }
     };
     // WR 1: this wave's fragments from L2 (1 KB per wave load) as buffer
     // loads: a lane-constant VGPR offset and the step's offset in an SGPR
@@ -1885,39 +1882,21 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
     const auto w1l = __builtin_amdgcn_make_buffer_rsrc((void*)p.w1f_lo, (short)0, p.K * 256, 0x00020000);
     auto ld_a = [&](int q, AOps& o) {
       const int k16 = kofs(min(q, Q - 1)) / 16;
+      const int vo = (wave * 64 + lane) * 16;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        o.h[kk] = __builtin_amdgcn_raw_buffer_load_b128(w1h, vo, (k16 + kk) * 4096, 0);
+        o.l[kk] = __builtin_amdgcn_raw_buffer_load_b128(w1l, vo, (k16 + kk) * 4096, 0);
+      }
+    };
+    auto mma = [&](const AOps& A, const BOps& B) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int a = 0; a < kNA; ++a) {
-          const int vo = ((kQ4 ? wave : 2 * wn + a) * 64 + lane) * 16;
-          o.h[kk][a] = __builtin_amdgcn_raw_buffer_load_b128(w1h, vo, (k16 + kk) * 4096, 0);
-          o.l[kk][a] = __builtin_amdgcn_raw_buffer_load_b128(w1l, vo, (k16 + kk) * 4096, 0);
-        }
+        for (int b = 0; b < kNB; ++b)
+          if (32 * b < TR) acc[b] = x3_32(A.h[kk], A.l[kk], B.h[kk][b], B.l[kk][b], acc[b]);
     };
-    auto mma = [&](const AOps& A, const BOps& B) {
-      if constexpr (kQ4) {
-        // 7x7: the tile is <= 64 rows, so the 4 waves split the 128 channels
-        // instead (wave = 32-channel quarter x both 32-pixel blocks)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int b = 0; b < 2; ++b)
-            if (b == 0 || TR > 32) acc[0][b] = x3_32(A.h[kk][0], A.l[kk][0], B.h[kk][b], B.l[kk][b], acc[0][b]);
-      } else if (rv > 32) {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 2; ++b) acc[a][b] = x3_32(A.h[kk][a], A.l[kk][a], B.h[kk][b], B.l[kk][b], acc[a][b]);
-      } else if (rv > 0) {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int a = 0; a < 2; ++a) acc[a][0] = x3_32(A.h[kk][a], A.l[kk][a], B.h[kk][0], B.l[kk][0], acc[a][0]);
-      }
-    };
-    const bool live = !(p.dbg & 4) && (kQ4 || rv > 0);  // ablation 4: no MFMAs / stage reads
+    const bool live = !(p.dbg & 4);  // ablation 4: no MFMAs / stage reads
     auto stamp_c = [&](int q) {
       if (tl && wave == 0 && lane == 0 && q < 32) tls[4 * q + 3] = __builtin_amdgcn_s_memtime();
     };
@@ -1942,10 +1921,9 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
       // leaves the next step's kNA x 4 fragment loads in flight
       // The prefetch is unconditional (past the last step it reloads that
       // step's fragments): with a conditional one the compiler's own waits
-      // before the MFMAs assume the no-prefetch path and drain it.  Every
-      // consumer wave is live here (14x14: >= 48 z rows per pixel block;
-      // 7x7: channel quarters), so the dbg 4 ablation does not apply.
-      constexpr int kAOps = 4 * kNA;
+      // before the MFMAs assume the no-prefetch path and drain it (so the
+      // dbg 4 ablation does not apply here).
+      constexpr int kAOps = 4;
       // the producers' BN1 affine for steps >= 1 (published by B0)
       for (int i = tid; i < p.K / 4; i += 256) {
         *reinterpret_cast<f32x4*>(bnl + 4 * i) = ldf4(p.s1 + 4 * i);
@@ -1978,12 +1956,10 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   mark(2);
   // BN2 bias of this consumer lane's channels, loaded BEFORE the 3x3
   // weights: a later load would make its wait drain the weight loads too
-  f32x4 ob[2][4];
+  f32x4 ob[4];
   if (wave < 4) {
 #pragma unroll
-    for (int a = 0; a < (kQ4 ? 1 : 2); ++a)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) ob[a][g] = ldf4(p.b1 + (kQ4 ? 32 * wave : 64 * wn + 32 * a) + 8 * g + 4 * h);
+    for (int g = 0; g < 4; ++g) ob[g] = ldf4(p.b1 + 32 * wave + 8 * g + 4 * h);
   }
   // 3x3 weights: in flight while the LDS changes hands and z is written
   const int kq = wave & 3, oh = wave >> 2;
@@ -2012,29 +1988,25 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
   }
   if (wave < 4) {
     // 1x1 epilogue: + bias, ReLU, hi/lo split into the padded tile image.
-    // C (32x32): lane col = pixel, reg 4g+e -> channel 64wn + 32a + 8g + 4h + e
+    // C (32x32): lane col = pixel, reg 4g+e -> channel 32wave + 8g + 4h + e
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int pz = (kQ4 ? 0 : 64 * wm) + 32 * b + col;  // z pixel of the tile
+    for (int b = 0; b < kNB; ++b) {
+      const int pz = 32 * b + col;  // z pixel of the tile
       if (pz < TR) {
         const int zy = pz / W, zx = pz - zy * W;
         const int pos = (zr0 + zy - r0 + 1) * kPW + zx + 1;
         uint8_t* rp = ldss + pos * kRowB + 8 * h;
 #pragma unroll
-        for (int a = 0; a < (kQ4 ? 1 : 2); ++a)
+        for (int g = 0; g < 4; ++g) {
+          f32x4 r;
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int cb = kQ4 ? 32 * wave : 64 * wn + 32 * a;  // the channel block's first channel
-            const f32x4 bb = ob[a][g];
-            f32x4 r;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) r[e] = fmaxf(acc[a][b][4 * g + e] + bb[e], 0.f);
-            v2u hh, ll;
-            split4(r, hh, ll);
-            uint8_t* q = rp + ((((cb >> 3) + g) ^ (pos & 15)) << 4);
-            *reinterpret_cast<v2u*>(q) = hh;
-            *reinterpret_cast<v2u*>(q + 256) = ll;
-          }
+          for (int e = 0; e < 4; ++e) r[e] = fmaxf(acc[b][4 * g + e] + ob[g][e], 0.f);
+          v2u hh, ll;
+          split4(r, hh, ll);
+          uint8_t* q = rp + ((((4 * wave) + g) ^ (pos & 15)) << 4);
+          *reinterpret_cast<v2u*>(q) = hh;
+          *reinterpret_cast<v2u*>(q + 256) = ll;
+        }
       }
     }
   }
