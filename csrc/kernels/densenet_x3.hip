@@ -919,17 +919,19 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p
 //   * A operand: BN2-folded W1 hi/lo fragments straight from L2 in a
 //     fragment-major copy (1 KB per wave load), one step ahead.
 //   * one barrier per step; epilogue: + bias, ReLU, hi/lo split, into the
-//     ring rows (16-B chunks XOR-swizzled by ring row, as K9x).
+//     ring rows (544-B row stride: each row's banks rotated two chunks from
+//     the previous row's, see kRowF1).
 //
 // 3x3 phase: wave (kq, oh) = input-channel quarter x output half on 16x16x32
 // MFMAs, so a wave's resident weights are 9 taps x 16 outputs x 32 inputs x
 // hi/lo = 72 VGPRs (K9x's 32-output waves hold 144, which leaves no room for
 // the 1x1 phase).  Operand reads roll two (tap, pixel-group) steps ahead.
 // The 4 kq partials: lanes holding another wave's 4 channels write them to
-// the owner's scratch slots, barrier, the owner lanes add and store y.
+// the owner's scratch slots (the owner its own share to a y-sum slot); the
+// owners add and store y after the next 1x1 chunk's barriers.
 //
-// LDS: ring 193 x 512 B + scratch 24 KB + X stages 4 x 8 KB + BN1 affine
-// 2 x 480 floats = 160,000 B.
+// LDS: ring 197 x 544 B + scratch 24 KB + X stages 2 x 2 x 4 KB + BN1 affine
+// 2 x 480 floats + y sums 8 KB = 160,160 B.
 constexpr int kRingF = 192;
 // physical ring row = logical + 1: [guard = logical -1 (mirrors 191)]
 // [logical 0..191] [guard = logical 192 (mirrors 0)] [logical 193..195: zero]
@@ -940,7 +942,15 @@ constexpr int kPfF = 4;             // X steps in flight (registers)
 constexpr int kMaxKF = 480;         // BN1 affine staged in LDS: K <= 480 (blocks 1-2)
 constexpr int kScrF = 2 * 4 * 3 * 64 * 4;  // floats: [oh][owner][3 sources][px][4]
 constexpr int kYsF = 2 * 4 * 4 * 64;  // floats: v1 owners' y sums [oh][owner][pg][px 16][4]
-constexpr int kLdsF = kRingRowsF * kRowB + kScrF * 4 + 4 * kCvtF + 2 * kMaxKF * 4 + kYsF * 4;
+// v1 ring row stride: 512 B of z (hi | lo) + 32 B of padding, so row r's banks
+// start 8 banks (two 16-B chunks) after row r-1's.  With that rotation the
+// 3x3's ds_read_b128 lane groups ({0-3,12-15 | chunk c} + {20-27 | chunk c+1}
+// over 16 consecutive rows) land on 16 distinct chunk slots for ANY first
+// row; the XOR swizzle by (row & 15) it replaces cannot do that (a 2-way
+// conflict whenever the group's first row is odd, ~10% of the 3x3's LDS time
+// by SQ_LDS_BANK_CONFLICT).
+constexpr int kRowF1 = kRowB + 32;
+constexpr int kLdsF = kRingRowsF * kRowF1 + kScrF * 4 + 4 * kCvtF + 2 * kMaxKF * 4 + kYsF * 4;
 static_assert(kLdsF <= 160 * 1024, "K11x LDS budget");
 constexpr uint32_t kMagRingF = (uint32_t)((0x100000000ull + kRingF - 1) / kRingF);
 
@@ -986,8 +996,8 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
   };
   extern __shared__ __attribute__((aligned(16))) uint8_t ldsf[];
   uint8_t* const ring = ldsf;
-  float* const scr = reinterpret_cast<float*>(ldsf + kRingRowsF * kRowB);
-  uint8_t* const cvt = ldsf + kRingRowsF * kRowB + kScrF * 4;             // [buf 2][plane 2][64 px][64 B]
+  float* const scr = reinterpret_cast<float*>(ldsf + kRingRowsF * kRowF1);
+  uint8_t* const cvt = ldsf + kRingRowsF * kRowF1 + kScrF * 4;             // [buf 2][plane 2][64 px][64 B]
   float* const bn = reinterpret_cast<float*>(cvt + 4 * kCvtF);            // s1 [kMaxKF] | t1 [kMaxKF]
   float* const ysum = bn + 2 * kMaxKF;                                     // [oh][owner][pg][16 px][4]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1011,7 +1021,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
     bn[i] = p.s1[i];
     bn[kMaxKF + i] = p.t1[i];
   }
-  if (tid < 3 * kRowB / 16) *reinterpret_cast<v4u*>(ring + kZeroF * kRowB + tid * 16) = v4u{0, 0, 0, 0};
+  if (tid < 3 * kRowF1 / 16) *reinterpret_cast<v4u*>(ring + kZeroF * kRowF1 + tid * 16) = v4u{0, 0, 0, 0};
   __syncthreads();
 
   // ---- 1x1 phase -----------------------------------------------------------
@@ -1104,9 +1114,9 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
       int pos;
       (void)fast_divmod(g0 + bpx + W + 1, kRingF, kMagRingF, pos);
       // physical row pos + 1; logical rows 0 and 191 also go to the guard
-      // rows 193 / 0 (same swizzle key: 192 is a multiple of 16)
-      uint8_t* rp = ring + (pos + 1) * kRowB + 8 * hh;
-      const int mirror = pos == 0 ? kRingF * kRowB : (pos == kRingF - 1 ? -kRingF * kRowB : 0);
+      // rows 193 / 0 (same bank rotation: 192 rows x 8 banks is a multiple of 64)
+      uint8_t* rp = ring + (pos + 1) * kRowF1 + 8 * hh;
+      const int mirror = pos == 0 ? kRingF * kRowF1 : (pos == kRingF - 1 ? -kRingF * kRowF1 : 0);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         f32x4 r;
@@ -1114,7 +1124,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
         for (int e = 0; e < 4; ++e) r[e] = fmaxf(acc[4 * g + e], 0.f);
         v2u h, l;
         split4(r, h, l);
-        uint8_t* q = rp + (((4 * q1 + g) ^ (pos & 15)) << 4);
+        uint8_t* q = rp + ((4 * q1 + g) << 4);
         *reinterpret_cast<v2u*>(q) = h;
         *reinterpret_cast<v2u*>(q + 256) = l;
         if (mirror) {
@@ -1199,10 +1209,10 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
       const int t = step >> 2, pg = step & 3;
       const int dy = t / 3, dx = t % 3 - 1;
       const int a = R[pg][dy] + dx;  // logical row, -1 .. 192 (or a zero row)
-      int off = (a << 9) + ((((a << 4) & 0xF0)) ^ chunk16);
-      if (dx < 0 && !lfm[pg]) off = kZeroF << 9;
-      if (dx > 0 && !rtm[pg]) off = kZeroF << 9;
-      const uint8_t* q = ring + kRowB + off;  // physical row = logical + 1
+      int off = a * kRowF1 + chunk16;
+      if (dx < 0 && !lfm[pg]) off = kZeroF * kRowF1;
+      if (dx > 0 && !rtm[pg]) off = kZeroF * kRowF1;
+      const uint8_t* q = ring + kRowF1 + off;  // physical row = logical + 1
       bq[step % (kLead + 1)][0] = ld16(q);
       bq[step % (kLead + 1)][1] = ld16(q + 256);
     };
