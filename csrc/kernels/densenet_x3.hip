@@ -74,12 +74,12 @@ __device__ __forceinline__ uint32_t pk(float a, float b) {
 // hi/lo split of two fp32: a ~= hi + lo to 2^-17 relative (a - hi is exact).
 // (A v_pk_fma_f32 / v_pk_add_f32 form of this and of the BN affine issues
 // fewer instructions but measured 3-8% slower in K14x / K8x / K11x: round 4.)
+// (hipcc turns the hi << 16 below into a second v_cvt_pk_bf16_f32 of (a, 0)
+// plus a shift; a v_perm_b32 instead issued fewer instructions but measured
+// 1-5% slower in K14x, round 4.)
 __device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
   hi = pk(a, b);
-  // a's bf16 back as fp32 by one v_perm_b32 (hi[15:0] << 16): written as a
-  // shift, hipcc re-derived it as a second v_cvt_pk_bf16_f32 of (a, 0) + shift
-  const uint32_t ha = __builtin_amdgcn_perm(0u, hi, 0x01000c0cu);
-  lo = pk(a - __uint_as_float(ha), b - __uint_as_float(hi & 0xffff0000u));
+  lo = pk(a - __uint_as_float(hi << 16), b - __uint_as_float(hi & 0xffff0000u));
 }
 
 // relu(x * s + t), per element (as scalar v_fma_f32)
