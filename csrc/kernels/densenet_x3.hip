@@ -1701,7 +1701,7 @@ struct X3SmallParams {
 // (TCAMD_X3_SMALLF_WREG).  (A variant with the stage filled two steps ahead
 // and the operands read one step ahead of the MFMAs measured no faster.)
 template <int W, int PF, int kSmS, int WR>
-__global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p) {
+__device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
   constexpr int kLdsSm = kSmS * kWsStage;
   constexpr int kHalves = W == 14 ? 2 : 1;
   constexpr int kRowsOut = W / kHalves;              // 7
@@ -2101,6 +2101,52 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
         if (lane == i) v = mk[i];
       p.stamps[blockIdx.x * 8 + lane] = v;  // a vector store (lane-indexed)
     }
+  }
+}
+
+template <int W, int PF, int kSmS, int WR>
+__global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p) {
+  x3_small_body<W, PF, kSmS, WR>(p);
+}
+
+// K16x: every layer of the 7x7 dense block in ONE launch.  A block owns one
+// image through all its layers (at 7x7 a K14x tile is the whole image, so
+// layer l+1 reads only what this block wrote in layer l: no cross-block
+// dependency); between layers the block's y stores complete and the LDS is
+// reused.  Saves per layer the launch, the wait for the slowest of the 128
+// blocks and its idle CUs.  Layer l+1's input channels [K_l, K_l + 32) were
+// never read by this CU before layer l wrote them (they sit in their own
+// 128-B lines), so no L1 line can be stale.
+struct X3SmallLayer {
+  const float* s1;
+  const float* t1;
+  const uint16_t* w1_hi;   // K8x layout (unused by WR 1, kept for the params)
+  const uint16_t* w1_lo;
+  const uint16_t* w1f_hi;  // x3_w1_fragments
+  const uint16_t* w1f_lo;
+  const float* b1;
+  const uint16_t* w2_hi;   // x3_w3f_fragments
+  const uint16_t* w2_lo;
+  int K, pad;
+};
+
+__global__ void __launch_bounds__(512, 1) x3_dense_block7_kernel(X3SmallParams p, const X3SmallLayer* __restrict__ L,
+                                                               int nl) {
+  for (int l = 0; l < nl; ++l) {
+    X3SmallParams q = p;
+    q.s1 = L[l].s1;
+    q.t1 = L[l].t1;
+    q.w1_hi = L[l].w1_hi;
+    q.w1_lo = L[l].w1_lo;
+    q.w1f_hi = L[l].w1f_hi;
+    q.w1f_lo = L[l].w1f_lo;
+    q.b1 = L[l].b1;
+    q.w2_hi = L[l].w2_hi;
+    q.w2_lo = L[l].w2_lo;
+    q.K = L[l].K;
+    q.y = const_cast<float*>(p.x) + L[l].K;
+    x3_small_body<7, 3, 4, 1>(q);
+    __syncthreads();  // this layer's y stores done (release) before the next layer reads them
   }
 }
 
@@ -2926,6 +2972,39 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }
+
+// K16x: nl layers of the 7x7 block in one launch.  layers: device array of
+// X3SmallLayer (K, BN1 affine, W1 fragments, BN2 shift, W2 fragments per
+// layer; K multiple of 32, 64 <= K <= 2048, growing by 32 per layer so layer
+// l writes channels [K_l, K_l + 32) of the block buffer x).
+int tcamd_x3_dense_block7(float* x, int ldx, int imgs, const void* layers, int nl, void* stream) {
+  if (imgs <= 0 || nl <= 0) return hipSuccess;
+  if (!x || !layers || ldx % 4 || !aligned16(x) || !aligned16(layers)) return hipErrorInvalidValue;
+  if ((size_t)imgs * 49 >= (1u << 30) / 4) return hipErrorInvalidValue;
+  X3SmallParams p = {};
+  p.x = x;
+  p.ldx = ldx;
+  p.ldy = ldx;
+  p.imgs = imgs;
+  p.dbg = 0;
+  p.stamps = nullptr;
+  static std::atomic<bool> attr_set[kMaxDevices];
+  const int dev_slot = device_slot();
+  if (!attr_set[dev_slot].load(std::memory_order_acquire)) {
+    const hipError_t e = hipFuncSetAttribute((const void*)x3_dense_block7_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kWsStage);
+    if (e != hipSuccess) return e;
+    attr_set[dev_slot].store(true, std::memory_order_release);
+  }
+  const X3SmallLayer* L = (const X3SmallLayer*)layers;
+  void* args[] = {&p, &L, &nl};
+  const hipError_t e = hipLaunchKernel((const void*)x3_dense_block7_kernel, dim3(imgs), dim3(512), args, 4 * kWsStage,
+                                       (hipStream_t)stream);
+  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+int tcamd_x3_small_layer_bytes() { return (int)sizeof(X3SmallLayer); }
 
 static int cu_count() {
   static std::atomic<int> ncu_dev[kMaxDevices];

@@ -364,6 +364,53 @@ def test_x3_dense_small(imgs, H, K, wfrag):
     assert _rel(x[:, K:K + 32], y2[:, K:K + 32]) < 2e-5
 
 
+@pytest.mark.parametrize("imgs,K0,nl", [(1, 64, 3), (37, 512, 16), (130, 96, 5)])
+def test_x3_dense_block7(imgs, K0, nl):
+    """K16x: ``nl`` 7x7 dense layers in ONE persistent launch (each workgroup
+    takes an image through every layer, each layer reading the channels the
+    previous ones wrote) against ``nl`` K14x launches on the same weights
+    (bit-equal: the same body), and the last layer against fp64 torch."""
+    _need_gpu()
+    hip = _hip()
+    g = torch.Generator(device=DEV).manual_seed(imgs * 17 + K0 + nl)
+    H, M, ldx = 7, imgs * 49, K0 + 32 * nl
+    x = torch.zeros(M, ldx, device=DEV)
+    x[:, :K0] = torch.randn(M, K0, device=DEV, generator=g)
+    layers, P = [], []
+    for j in range(nl):
+        K = K0 + 32 * j
+        s = torch.rand(K, device=DEV, generator=g) + 0.5
+        t = torch.randn(K, device=DEV, generator=g) * 0.2
+        w1 = torch.randn(128, K, device=DEV, generator=g) / K ** 0.5
+        b1 = torch.randn(128, device=DEV, generator=g) * 0.1
+        w2 = torch.randn(32, 128, 3, 3, device=DEV, generator=g) / (9 * 128) ** 0.5
+        w1h, w1l = _split(w1)
+        f1h, f1l = (hip.x3_w1_fragments(u) for u in (w1h, w1l))
+        f2h, f2l = (hip.x3_w3f_fragments(u) for u in _split(w2.permute(0, 2, 3, 1).reshape(32, -1)))
+        P.append((K, s, t, w1, b1, w2, w1h, w1l, f1h, f1l, f2h, f2l))
+        layers.append({"s1": s.data_ptr(), "t1": t.data_ptr(), "w1_hi": w1h.data_ptr(), "w1_lo": w1l.data_ptr(),
+                       "w1f_hi": f1h.data_ptr(), "w1f_lo": f1l.data_ptr(), "b1": b1.data_ptr(),
+                       "w2_hi": f2h.data_ptr(), "w2_lo": f2l.data_ptr(), "K": K})
+    tab = torch.from_numpy(hip.x3_small_layer_table(layers)).to(DEV)
+    y = x.clone()
+    hip.x3_dense_block7(y.data_ptr(), ldx, imgs, tab.data_ptr(), nl, stream=_st())
+    ref = x.clone()
+    for K, s, t, w1, b1, w2, w1h, w1l, f1h, f1l, f2h, f2l in P:
+        hip.x3_dense_small(ref.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), w1h.data_ptr(),
+                           w1l.data_ptr(), b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), ref.data_ptr() + 4 * K, ldx,
+                           stream=_st(), w1f_hi=f1h.data_ptr(), w1f_lo=f1l.data_ptr())
+    torch.cuda.synchronize()
+    K, s, t, w1, b1, w2 = P[-1][:6]
+    a = torch.relu(y[:, :K].double() * s.double() + t.double())
+    z = torch.relu(a @ w1.double().t() + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
+    r64 = F.conv2d(z, w2.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 32)
+    err = _rel(y[:, K:], r64)
+    print("K16x imgs %d K0 %d layers %d: last layer rel %.3g, equal to K14x %s" % (
+        imgs, K0, nl, err, torch.equal(y, ref)))
+    assert err < 3e-5
+    assert torch.equal(y, ref)
+
+
 @pytest.mark.parametrize("pf,stages,wreg", [("6", "4", "1"), ("3", "5", "1"), ("6", "5", "1"), ("6", "4", "0"),
                                             ("3", "5", "0"), ("6", "5", "0")])
 def test_x3_dense_small_variants(pf, stages, wreg):

@@ -135,6 +135,19 @@ class FusedDenseNetFP32:
         # least this many blocks (a 14x14 image is two blocks, a 7x7 image one);
         # 0 disables it
         self.smallf_min_blocks = int(os.environ.get("TCAMD_X3_SMALLF_MIN_BLOCKS", "128"))
+        # K16x: the K14x 7x7 block as ONE persistent launch (every layer of an
+        # image in one workgroup), TCAMD_X3_BLOCK7=1; off by default: measured no
+        # faster than 16 launches (profiles/r4_k16x_block7.md)
+        self.block7_tab = None
+        if os.environ.get("TCAMD_X3_BLOCK7", "0") != "0":
+            for bi, layers in enumerate(self.blocks):
+                if self.block_dims[bi][0] == 7 and all(L["cin"] <= 2048 for L in layers):
+                    tab = hip.x3_small_layer_table([{
+                        "s1": L["s1"].data_ptr(), "t1": L["t1"].data_ptr(), "w1_hi": L["w1h"].data_ptr(),
+                        "w1_lo": L["w1l"].data_ptr(), "w1f_hi": L["w1fh"].data_ptr(), "w1f_lo": L["w1fl"].data_ptr(),
+                        "b1": L["b1"].data_ptr(), "w2_hi": L["w2fh"].data_ptr(), "w2_lo": L["w2fl"].data_ptr(),
+                        "K": L["cin"]} for L in layers])
+                    self.block7_tab = (bi, torch.from_numpy(tab).to(dev))
         self._alloc(max_batch)
 
     def _alloc(self, n):
@@ -221,6 +234,9 @@ class FusedDenseNetFP32:
             small = 0 < M <= self.small_m and M <= self.zacc.shape[1]
             if self._small_fused(b, hw):
                 # K14x: the 14x14 / 7x7 blocks, one launch per layer, z on chip
+                if self.block7_tab is not None and self.block7_tab[0] == bi:
+                    hip.x3_dense_block7(fp, ctot, b, self.block7_tab[1].data_ptr(), len(layers), stream=st)
+                    layers = ()
                 for L in layers:
                     hip.x3_dense_small(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
                                        L["w1h"].data_ptr(), L["w1l"].data_ptr(), L["b1"].data_ptr(),

@@ -228,6 +228,9 @@ _SIGS = {
         ctypes.c_int,
     ),
     "tcamd_x3_fused_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
+    "tcamd_x3_dense_block7": (
+        [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
+    "tcamd_x3_small_layer_bytes": ([], ctypes.c_int),
     "tcamd_x3_small_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "tcamd_x3_small_timeline": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "tcamd_x3_dense_fused4": (
@@ -779,6 +782,35 @@ def x3_dense_small(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo
     _check(_load().tcamd_x3_dense_small(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo,
                                         _vp(w1f_hi), _vp(w1f_lo), b1, w2_hi, w2_lo, y, int(ldy), _vp(stream)),
            "x3_dense_small")
+
+
+_X3_LAYER_DTYPE = np.dtype([("s1", "<u8"), ("t1", "<u8"), ("w1_hi", "<u8"), ("w1_lo", "<u8"), ("w1f_hi", "<u8"),
+                             ("w1f_lo", "<u8"), ("b1", "<u8"), ("w2_hi", "<u8"), ("w2_lo", "<u8"), ("K", "<i4"),
+                             ("pad", "<i4")])
+
+
+def x3_small_layer_table(layers):
+    """Host bytes of the K16x layer table: one X3SmallLayer per dict with
+    device pointers s1, t1, w1_hi, w1_lo, w1f_hi, w1f_lo, b1, w2_hi, w2_lo
+    (x3_w3f_fragments) and K.  Copy it to the device and pass its address to
+    :func:`x3_dense_block7`."""
+    if _X3_LAYER_DTYPE.itemsize != int(_load().tcamd_x3_small_layer_bytes()):
+        raise HipError(-1, "X3SmallLayer size mismatch")
+    t = np.zeros(len(layers), dtype=_X3_LAYER_DTYPE)
+    for i, L in enumerate(layers):
+        for k in _X3_LAYER_DTYPE.names:
+            if k != "pad":
+                t[k][i] = int(L[k])
+    return t.view(np.uint8)
+
+
+def x3_dense_block7(x, ldx, imgs, table, nl, stream=None):
+    """K16x: ``nl`` dense layers of the 7x7 block in ONE launch (one block per
+    image through every layer); ``table`` = device copy of
+    :func:`x3_small_layer_table`.  Same results as ``nl`` K14x launches
+    (W1 by consumer loads, PF 3, 4 stages)."""
+    _check(_load().tcamd_x3_dense_block7(_vp(x), int(ldx), int(imgs), _vp(table), int(nl), _vp(stream)),
+           "x3_dense_block7")
 
 
 def x3_small_timeline():
