@@ -27,6 +27,7 @@
 // that XCD's L2.
 
 #include <atomic>
+#include <type_traits>
 #include <cmath>
 #include <cstdlib>
 
@@ -65,32 +66,59 @@ __device__ __forceinline__ uint32_t pk(float a, float b) {
 // byte offset of 16-B chunk c of row r in a [rows][64 bf16] tile image
 __device__ __forceinline__ int chunk_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
+// GELU, erf form, with erf from Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7,
+// far below the bf16 output's half ulp): one v_rcp, one v_exp and 8 FMAs
+// instead of the device library's branchy erff, which took ~30% of the FFN-up
+// tile time in the epilogue (PMC: MFMA busy 35% with erff against 49% with
+// no epilogue, profiles/r4_gemm_k15.md)
+__device__ __forceinline__ float gelu_erf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
+  float q = fmaf(1.061405429f, t, -1.453152027f);
+  q = fmaf(q, t, 1.421413741f);
+  q = fmaf(q, t, -0.284496736f);
+  q = fmaf(q, t, 0.254829592f);
+  q *= t;
+  const float e = __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);
+  const float erf_abs = fmaf(-q, e, 1.f);
+  const float erf_x = __builtin_copysignf(erf_abs, x);
+  return 0.5f * x * (1.f + erf_x);
+}
+
 // C (16x16) of a wave's 128 (m) x 64 (n) sub-tile: lane column = token m,
 // rows 4 fq + e = four consecutive output channels -> 8-B stores
 template <int EPI>
-__device__ __forceinline__ void epilogue(const GemmParams& p, f32x4 (&acc)[4][8], int m0, int n0, int wm, int wn,
-                                         int fr16, int fq) {
+__device__ __forceinline__ void load_bias(const GemmParams& p, float (&bv)[4][4], int n0, int wn, int fq) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int n = n0 + 64 * wn + 16 * i + 4 * fq;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    bv[i][0] = bv[i][1] = bv[i][2] = bv[i][3] = 0.f;
     if constexpr (EPI >= 1) {
       const v2u bb = *reinterpret_cast<const v2u*>(p.bias + n);
-      bv[0] = __uint_as_float(bb[0] << 16);
-      bv[1] = __uint_as_float(bb[0] & 0xffff0000u);
-      bv[2] = __uint_as_float(bb[1] << 16);
-      bv[3] = __uint_as_float(bb[1] & 0xffff0000u);
+      bv[i][0] = __uint_as_float(bb[0] << 16);
+      bv[i][1] = __uint_as_float(bb[0] & 0xffff0000u);
+      bv[i][2] = __uint_as_float(bb[1] << 16);
+      bv[i][3] = __uint_as_float(bb[1] & 0xffff0000u);
     }
+  }
+}
+
+template <int EPI, int NJ = 8>
+__device__ __forceinline__ void epilogue_b(const GemmParams& p, f32x4 (&acc)[4][NJ], const float (&bv)[4][4], int m0,
+                                           int n0, int wm, int wn, int fr16, int fq) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int m = m0 + 128 * wm + 16 * j + fr16;
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + 64 * wn + 16 * i + 4 * fq;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int m = m0 + NJ * 16 * wm + 16 * j + fr16;
       if (m >= p.M) continue;
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[i][e];
       if constexpr (EPI == 2) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
       }
       if constexpr (EPI == 3) {
         const v2u rr = *reinterpret_cast<const v2u*>(p.r + (size_t)m * p.ldr + n);
@@ -102,6 +130,14 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, f32x4 (&acc)[4][8]
       *reinterpret_cast<v2u*>(p.y + (size_t)m * p.ldy + n) = v2u{pk(v[0], v[1]), pk(v[2], v[3])};
     }
   }
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue(const GemmParams& p, f32x4 (&acc)[4][8], int m0, int n0, int wm, int wn,
+                                         int fr16, int fq) {
+  float bv[4][4];
+  load_bias<EPI>(p, bv, n0, wn, fq);
+  epilogue_b<EPI>(p, acc, bv, m0, n0, wm, wn, fr16, fq);
 }
 
 // SPREAD: the next step's 8 LDS-DMA copies are issued one per 8-MFMA group
@@ -210,6 +246,262 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
     }
   }
 
+  epilogue<EPI>(p, acc, m0, n0, wm, wn, fr16, fq);
+}
+
+// ---- pipelined persistent variant (TCAMD_GEMM_V=6) ----
+// The one-barrier kernel reads a half step's 12 operand fragments and then
+// waits for them before its first MFMA; both waves of a SIMD do so at the same
+// moment (the step barrier lines them up), so every half step starts with the
+// LDS latency exposed.  Here the fragments are double-buffered in registers:
+// a half step's MFMAs run on fragments read during the previous half step.
+//   top of step:   DMA of step + 1 -> other buffer; read kk 1 of this step
+//   MFMAs kk 0;    barrier (DMA landed, kk 1 reads retired everywhere)
+//   read kk 0 of step + 1 (other buffer); MFMAs kk 1
+// The other buffer's last reads (kk 1 of the previous step) retired before the
+// previous barrier, so its DMA may start at the top of the step.
+// Persistent (one workgroup per CU walks its tiles): the next tile's first
+// step is staged before this tile's epilogue, so its latency hides there.
+// BMT: token rows per tile, 256 or 128 (128: twice the tiles, for N = 1024
+// where 256 x 256 tiles leave the last round half empty)
+template <int EPI, int BMT = 256>
+__global__ void __launch_bounds__(512, 1) gemm_bf16_pipe_kernel(GemmParams p) {
+  constexpr int NJ = BMT / 32;             // token fragments per wave
+  constexpr int NXP = BMT / 64;            // X copies per thread per step
+  constexpr int kXB = BMT * kBK * 2;       // X tile bytes
+  constexpr int kBuf = kTileB + kXB;       // W tile | X tile
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwg = p.mt * p.nt, q = nwg >> 3, rem = nwg & 7;
+  // persistent: workgroup b takes virtual tiles b, b + G, ... (G % 8 == 0
+  // keeps each on the XCD of b); virtual tile -> XCD-contiguous tile order
+  auto tile_of = [&](int v, int& m0, int& n0) {
+    const int xcd = v & 7;
+    const int wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (v >> 3);
+    const int tm = wg / p.nt;
+    m0 = tm * BMT;
+    n0 = (wg - tm * p.nt) * kBN;
+  };
+  const uint16_t* srcw[4];
+  const uint16_t* srcx[NXP];
+  auto set_src = [&](int m0, int n0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (8 * i + wave) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      srcw[i] = p.w + (size_t)(n0 + row) * p.ldw + 8 * c;
+      if (i < NXP) srcx[i] = p.x + (size_t)min(m0 + row, p.M - 1) * p.ldx + 8 * c;
+    }
+  };
+  auto stage1 = [&](int kt, int buf, int piece) {  // piece 0-3: W rows, 4..: X rows
+    uint8_t* dw = lds + buf * kBuf;
+    const int k0 = kt * kBK, i = piece & 3;
+    if (piece < 4)
+      __builtin_amdgcn_global_load_lds((const void*)(srcw[i] + k0), (void*)(dw + (8 * i + wave) * 1024), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds((const void*)(srcx[i] + k0), (void*)(dw + kTileB + (8 * i + wave) * 1024), 16,
+                                       0, 0);
+  };
+  auto stage = [&](int kt, int buf) {
+#pragma unroll
+    for (int piece = 0; piece < 4 + NXP; ++piece) stage1(kt, buf, piece);
+  };
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr16 = lane & 15, fq = lane >> 4;
+  // per-lane byte offsets of fragment 0 of half step kk; fragment i sits
+  // 16 rows (2048 B) further: the swizzle term (r >> 1) & 7 does not change
+  // by 16 rows, so the other fragments are immediate offsets
+  int oa[2], ob[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    oa[kk] = chunk_off(64 * wn + fr16, 4 * kk + fq);
+    ob[kk] = kTileB + chunk_off(NJ * 16 * wm + fr16, 4 * kk + fq);
+  }
+  v4u fa[2][4], fb[2][NJ];
+  auto rd = [&](int buf, int kk) {
+    const uint8_t* ta = lds + buf * kBuf + oa[kk];
+    const uint8_t* tb = lds + buf * kBuf + ob[kk];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[kk][i] = *reinterpret_cast<const v4u*>(ta + 2048 * i);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) fb[kk][j] = *reinterpret_cast<const v4u*>(tb + 2048 * j);
+  };
+  f32x4 acc[4][NJ];
+  auto mma = [&](int kk) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr(fa[kk][i]), fr(fb[kk][j]), acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = p.K / kBK, G = gridDim.x;
+  int vb = blockIdx.x, m0, n0;
+  tile_of(vb, m0, n0);
+  set_src(m0, n0);
+  stage(0, 0);
+  for (;;) {
+    __syncthreads();  // this tile's step 0 landed
+    rd(0, 0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      const bool more = kt + 1 < nk;
+      if (more) stage(kt + 1, buf ^ 1);
+      rd(buf, 1);
+      mma(0);
+      __syncthreads();
+      rd(buf ^ 1, 0);  // unconditional (stale on the last step, unused)
+      mma(1);
+      // those reads retired during mma(1); retiring them explicitly here keeps
+      // the compiler from draining the kk 1 reads before mma(0) (it loses the
+      // count of reads pending across the back edge)
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    }
+    // the next tile's first step is in flight during this tile's epilogue;
+    // the bias is loaded first (the in-order vmcnt would make its wait a wait
+    // for those copies too)
+    float bv[4][4];
+    load_bias<EPI>(p, bv, n0, wn, fq);
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the bias, before the copies queue behind it
+    const int nvb = vb + G;
+    int nm0 = 0, nn0 = 0;
+    if (nvb < nwg) {
+      tile_of(nvb, nm0, nn0);
+      set_src(nm0, nn0);
+      __syncthreads();  // every wave's last reads of buffer 0 retired (and the bias landed)
+      stage(0, 0);
+    }
+    epilogue_b<EPI, NJ>(p, acc, bv, m0, n0, wm, wn, fr16, fq);
+    if (nvb >= nwg) break;
+    vb = nvb;
+    m0 = nm0;
+    n0 = nn0;
+  }
+}
+
+// ---- deep variant (TCAMD_GEMM_V=7): five 32-k stages, 3 stages of DMA lead ----
+// At 2 stages of 64 k the next step's copies must land within half a step of
+// their issue (v6) -- far less than an L2 miss under load.  Here a stage is
+// 32 k (W 256 x 32 | X 256 x 32 bf16 = 32 KB, 2 + 2 LDS-DMA per thread) and
+// five stages fill the 160 KB of LDS: the copies of stage s + 4 are issued in
+// iteration s and read in iteration s + 3.  Iteration s:
+//   counted vmcnt (stage s + 1 landed: stages s + 2, s + 3 may stay in
+//   flight) -> raw barrier -> DMA of stage s + 4 into stage s - 1's slot ->
+//   read stage s + 1's fragments -> MFMAs on stage s's (read one iteration
+//   earlier) -> retire the reads.
+// Past the last stage the DMA is re-issued for the last stage into the free
+// slot, so every iteration issues four copies and the counts hold.
+// Rows are 64 B (4 chunks); chunk c of row r sits at c ^ g((r >> 2) & 3),
+// g = (0, 2, 3, 1): the 16 lanes of each ds_read_b128 group (rows 0-3 and
+// 12-15 of one chunk, rows 4-11 of the next, or the mirror) hit 16 distinct
+// 16-B slots of the 256-B bank row.
+constexpr int kBK32 = 32;
+constexpr int kStB = 2 * kBM * kBK32 * 2;  // 32 KB: W | X of one 32-k stage
+constexpr int kNSt = 5;
+constexpr int kLdsD = kNSt * kStB;  // 160 KB
+static_assert(kLdsD <= 160 * 1024, "LDS");
+__device__ __forceinline__ int g32(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
+__device__ __forceinline__ int off32(int r, int c) { return r * 64 + ((c ^ g32(r)) << 4); }
+constexpr int gvm(int n) { return (((n >> 4) & 3) << 14) | (0xF << 8) | (7 << 4) | (n & 15); }
+
+template <int EPI>
+__global__ void __launch_bounds__(512, 1) gemm_bf16_deep_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwg = p.mt * p.nt;
+  const int b = blockIdx.x, xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
+  const int wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  const int tm = wg / p.nt, tn = wg - tm * p.nt;
+  const int m0 = tm * kBM, n0 = tn * kBN;
+  // DMA instruction i of wave w writes tile rows 16 (8 i + w) ..+16 (1 KB):
+  // lane L -> row 16 (8 i + w) + L / 4, physical chunk L % 4
+  const uint16_t* srcw[2];
+  const uint16_t* srcx[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * (8 * i + wave) + (lane >> 2);
+    const int c = (lane & 3) ^ g32(row);
+    srcw[i] = p.w + (size_t)(n0 + row) * p.ldw + 8 * c;
+    srcx[i] = p.x + (size_t)min(m0 + row, p.M - 1) * p.ldx + 8 * c;
+  }
+  const int ns = p.K / kBK32;
+  auto stage = [&](int st, int slot) {
+    uint8_t* d = lds + slot * kStB;
+    const int k0 = min(st, ns - 1) * kBK32;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(srcw[i] + k0), (void*)(d + (8 * i + wave) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(srcx[i] + k0), (void*)(d + kStB / 2 + (8 * i + wave) * 1024),
+                                       16, 0, 0);
+  };
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr16 = lane & 15, fq = lane >> 4;
+  // fragment 0's offset; fragment i sits 16 rows = 1 KB further (g32 is
+  // periodic in 16 rows)
+  const int oa = off32(64 * wn + fr16, fq), ob = kStB / 2 + off32(128 * wm + fr16, fq);
+  v4u fa[2][4], fb[2][8];
+  auto rd = [&](int slot, int set) {
+    const uint8_t* ta = lds + slot * kStB + oa;
+    const uint8_t* tb = lds + slot * kStB + ob;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[set][i] = *reinterpret_cast<const v4u*>(ta + 1024 * i);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fb[set][j] = *reinterpret_cast<const v4u*>(tb + 1024 * j);
+  };
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](int set) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr(fa[set][i]), fr(fb[set][j]), acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+#pragma unroll
+  for (int st = 0; st < kNSt - 1; ++st) stage(st, st);
+  __builtin_amdgcn_s_waitcnt(gvm(12));  // stage 0 landed (this wave's copies)
+  __builtin_amdgcn_s_barrier();
+  rd(0, 0);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  int slot = 0;  // stage s's slot
+  // the fragment set must be a compile-time index (a runtime one turns the
+  // register arrays into scratch): two iterations per loop trip (ns is even)
+  auto step = [&](int s, auto cur_c) {
+    constexpr int C = decltype(cur_c)::value;
+    const int nx = slot == kNSt - 1 ? 0 : slot + 1;   // stage s + 1
+    const int fr = slot == 0 ? kNSt - 1 : slot - 1;   // stage s - 1 = s + 4
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(gvm(8));  // stage s + 1 landed
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    stage(s + kNSt - 1, fr);
+    rd(nx, C ^ 1);
+    mma(C);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the stage s + 1 reads retired
+    slot = nx;
+  };
+  for (int s = 0; s < ns; s += 2) {
+    step(s, std::integral_constant<int, 0>{});
+    step(s + 1, std::integral_constant<int, 1>{});
+  }
+  __builtin_amdgcn_s_waitcnt(gvm(0));  // the trailing re-issued copies
   epilogue<EPI>(p, acc, m0, n0, wm, wn, fr16, fq);
 }
 
@@ -379,12 +671,14 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
   p.ldy = ldy;
   p.mt = (M + kBM - 1) / kBM;
   p.nt = N / kBN;
-  // TCAMD_GEMM_V: 1 = one barrier per K step (default), 2 = the phased
+  // TCAMD_GEMM_V: 1 = one barrier per K step, 2 = the phased
   // kernel, 3 = phased with the two wave groups one phase apart, 4 = one
   // barrier per step with the DMA spread over the MFMA groups, 5 = 1 with the
-  // L2 warm-up of the step after next
-  static const int ver = getenv("TCAMD_GEMM_V") ? atoi(getenv("TCAMD_GEMM_V")) : 1;
-  const void* all[5][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
+  // L2 warm-up of the step after next, 6 = fragments double-buffered in
+  // registers, persistent (the pipelined kernel; default), 7 = five 32-k
+  // stages (the deep kernel)
+  static const int ver = getenv("TCAMD_GEMM_V") ? atoi(getenv("TCAMD_GEMM_V")) : 6;
+  const void* all[7][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
                             (const void*)gemm_bf16_kernel<2>, (const void*)gemm_bf16_kernel<3>},
                            {(const void*)gemm_bf16_ph_kernel<0, false>, (const void*)gemm_bf16_ph_kernel<1, false>,
                             (const void*)gemm_bf16_ph_kernel<2, false>, (const void*)gemm_bf16_ph_kernel<3, false>},
@@ -393,8 +687,25 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
                            {(const void*)gemm_bf16_kernel<0, true>, (const void*)gemm_bf16_kernel<1, true>,
                             (const void*)gemm_bf16_kernel<2, true>, (const void*)gemm_bf16_kernel<3, true>},
                            {(const void*)gemm_bf16_kernel<0, false, true>, (const void*)gemm_bf16_kernel<1, false, true>,
-                            (const void*)gemm_bf16_kernel<2, false, true>, (const void*)gemm_bf16_kernel<3, false, true>}};
-  const void* const* fns = all[(ver >= 2 && ver <= 5) ? ver - 1 : 0];
+                            (const void*)gemm_bf16_kernel<2, false, true>, (const void*)gemm_bf16_kernel<3, false, true>},
+                           {(const void*)gemm_bf16_pipe_kernel<0>, (const void*)gemm_bf16_pipe_kernel<1>,
+                            (const void*)gemm_bf16_pipe_kernel<2>, (const void*)gemm_bf16_pipe_kernel<3>},
+                           {(const void*)gemm_bf16_deep_kernel<0>, (const void*)gemm_bf16_deep_kernel<1>,
+                            (const void*)gemm_bf16_deep_kernel<2>, (const void*)gemm_bf16_deep_kernel<3>}};
+  const void* half[4] = {(const void*)gemm_bf16_pipe_kernel<0, 128>, (const void*)gemm_bf16_pipe_kernel<1, 128>,
+                         (const void*)gemm_bf16_pipe_kernel<2, 128>, (const void*)gemm_bf16_pipe_kernel<3, 128>};
+  const void* const* fns = all[(ver >= 2 && ver <= 7) ? ver - 1 : 0];
+  // v6: 128-token tiles (TCAMD_GEMM_HALF: 0 never, 1 (default) when N <= 1024
+  // and 256-token tiles would fill at most half the CUs, 2 always).  Measured
+  // (profiles/r4_gemm_k15.md): 3072 tokens x N 1024 +33-61%; at 24,576 tokens
+  // or N >= 3072 the smaller tiles lose more per tile than the fuller last
+  // round gains
+  static const int half_mode = getenv("TCAMD_GEMM_HALF") ? atoi(getenv("TCAMD_GEMM_HALF")) : 1;
+  const bool use_half = ver == 6 && (half_mode == 2 || (half_mode == 1 && N <= 1024 && p.mt * p.nt <= 128));
+  if (use_half) {
+    fns = half;
+    p.mt = (M + 127) / 128;
+  }
   // dynamic-LDS opt-in once per device (cached only after every call succeeded)
   static std::atomic<bool> attr_set[64];
   int dev = 0;
@@ -402,14 +713,29 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
   if (!attr_set[dev].load(std::memory_order_acquire)) {
     for (const auto& row : all)
       for (const void* f : row) {
-        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsG);
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsD);
         if (e != hipSuccess) return e;
       }
+    for (const void* f : half) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsD);
+      if (e != hipSuccess) return e;
+    }
     attr_set[dev].store(true, std::memory_order_release);
   }
   void* args[] = {&p};
-  const hipError_t e =
-      hipLaunchKernel(fns[epi], dim3(p.mt * p.nt), dim3(512), args, kLdsG, (hipStream_t)stream);
+  int grid = p.mt * p.nt;
+  if (ver == 6) {  // persistent: one workgroup per CU (a multiple of 8: XCD-stable)
+    static std::atomic<int> ncu_cache[64];
+    int ncu = ncu_cache[dev].load(std::memory_order_relaxed);
+    if (ncu <= 0) {
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8) ncu = 256;
+      ncu &= ~7;
+      ncu_cache[dev].store(ncu, std::memory_order_relaxed);
+    }
+    grid = grid < ncu ? grid : ncu;
+  }
+  const int lds_b = ver == 7 ? kLdsD : use_half ? 2 * (kTileB + 128 * kBK * 2) : kLdsG;
+  const hipError_t e = hipLaunchKernel(fns[epi], dim3(grid), dim3(512), args, lds_b, (hipStream_t)stream);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }

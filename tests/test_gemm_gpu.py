@@ -31,7 +31,8 @@ def _ref(x, w, bias, r, epi):
 
 
 @pytest.mark.parametrize("M,N,K", [(384, 3072, 1024), (1000, 1024, 1024), (3072, 4096, 1024), (768, 1024, 4096),
-                                   (24576, 1024, 1024), (256, 256, 64), (130, 512, 128)])
+                                   (24576, 1024, 1024), (256, 256, 64), (130, 512, 128),
+                                   (8200, 2048, 128)])
 @pytest.mark.parametrize("epi", ["none", "bias", "bias_gelu", "bias_residual"])
 def test_gemm_bf16_matches_fp32_reference(M, N, K, epi):
     _need_gpu()
@@ -90,7 +91,7 @@ def test_gemm_bf16_rejects_bad_shapes():
         hip.gemm_bf16(t.data_ptr(), t.data_ptr(), t.data_ptr(), 16, 256, 64, epilogue="bias")
 
 
-@pytest.mark.parametrize("variant", ["2", "3", "4", "5"])
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "7"])
 def test_gemm_bf16_phased_variant_matches(tmp_path, variant):
     """TCAMD_GEMM_V=2 (4 phases per K step, counted vmcnt across barriers) and 3
     (the same with the two wave groups one phase apart) in a child process (the variant is chosen once per process): same results as
