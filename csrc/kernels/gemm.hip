@@ -264,7 +264,12 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
 // step is staged before this tile's epilogue, so its latency hides there.
 // BMT: token rows per tile, 256 or 128 (128: twice the tiles, for N = 1024
 // where 256 x 256 tiles leave the last round half empty)
-template <int EPI, int BMT = 256>
+// STAG (TCAMD_GEMM_V=8): waves w and w + 4 share a SIMD and both issued
+// their copies at the top of the step, so the SIMD's MFMA pipe idled while
+// both were issuing.  With STAG, waves 4-7 issue step kt + 2's copies right
+// after step kt's middle barrier (that buffer's reads all retired there), a
+// half step before waves 0-3 issue theirs at the top of step kt + 1.
+template <int EPI, int BMT = 256, bool STAG = false>
 __global__ void __launch_bounds__(512, 1) gemm_bf16_pipe_kernel(GemmParams p) {
   constexpr int NJ = BMT / 32;             // token fragments per wave
   constexpr int NXP = BMT / 64;            // X copies per thread per step
@@ -340,8 +345,10 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_pipe_kernel(GemmParams p) {
   const int nk = p.K / kBK, G = gridDim.x;
   int vb = blockIdx.x, m0, n0;
   tile_of(vb, m0, n0);
+  const bool grp_b = STAG && wave >= 4;
   set_src(m0, n0);
   stage(0, 0);
+  if (grp_b && nk > 1) stage(1, 1);
   for (;;) {
     __syncthreads();  // this tile's step 0 landed
     rd(0, 0);
@@ -353,10 +360,11 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_pipe_kernel(GemmParams p) {
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = kt & 1;
       const bool more = kt + 1 < nk;
-      if (more) stage(kt + 1, buf ^ 1);
+      if (more && !grp_b) stage(kt + 1, buf ^ 1);
       rd(buf, 1);
       mma(0);
       __syncthreads();
+      if (grp_b && kt + 2 < nk) stage(kt + 2, buf);
       rd(buf ^ 1, 0);  // unconditional (stale on the last step, unused)
       mma(1);
       // those reads retired during mma(1); retiring them explicitly here keeps
@@ -376,8 +384,9 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_pipe_kernel(GemmParams p) {
     if (nvb < nwg) {
       tile_of(nvb, nm0, nn0);
       set_src(nm0, nn0);
-      __syncthreads();  // every wave's last reads of buffer 0 retired (and the bias landed)
+      __syncthreads();  // every wave's last reads of both buffers retired (and the bias landed)
       stage(0, 0);
+      if (grp_b && nk > 1) stage(1, 1);
     }
     epilogue_b<EPI, NJ>(p, acc, bv, m0, n0, wm, wn, fr16, fq);
     if (nvb >= nwg) break;
@@ -676,9 +685,10 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
   // barrier per step with the DMA spread over the MFMA groups, 5 = 1 with the
   // L2 warm-up of the step after next, 6 = fragments double-buffered in
   // registers, persistent (the pipelined kernel; default), 7 = five 32-k
-  // stages (the deep kernel)
+  // stages (the deep kernel), 8 = 6 with the SIMD-partner waves' copies half a
+  // step apart
   static const int ver = getenv("TCAMD_GEMM_V") ? atoi(getenv("TCAMD_GEMM_V")) : 6;
-  const void* all[7][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
+  const void* all[8][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
                             (const void*)gemm_bf16_kernel<2>, (const void*)gemm_bf16_kernel<3>},
                            {(const void*)gemm_bf16_ph_kernel<0, false>, (const void*)gemm_bf16_ph_kernel<1, false>,
                             (const void*)gemm_bf16_ph_kernel<2, false>, (const void*)gemm_bf16_ph_kernel<3, false>},
@@ -691,10 +701,14 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
                            {(const void*)gemm_bf16_pipe_kernel<0>, (const void*)gemm_bf16_pipe_kernel<1>,
                             (const void*)gemm_bf16_pipe_kernel<2>, (const void*)gemm_bf16_pipe_kernel<3>},
                            {(const void*)gemm_bf16_deep_kernel<0>, (const void*)gemm_bf16_deep_kernel<1>,
-                            (const void*)gemm_bf16_deep_kernel<2>, (const void*)gemm_bf16_deep_kernel<3>}};
+                            (const void*)gemm_bf16_deep_kernel<2>, (const void*)gemm_bf16_deep_kernel<3>},
+                           {(const void*)gemm_bf16_pipe_kernel<0, 256, true>,
+                            (const void*)gemm_bf16_pipe_kernel<1, 256, true>,
+                            (const void*)gemm_bf16_pipe_kernel<2, 256, true>,
+                            (const void*)gemm_bf16_pipe_kernel<3, 256, true>}};
   const void* half[4] = {(const void*)gemm_bf16_pipe_kernel<0, 128>, (const void*)gemm_bf16_pipe_kernel<1, 128>,
                          (const void*)gemm_bf16_pipe_kernel<2, 128>, (const void*)gemm_bf16_pipe_kernel<3, 128>};
-  const void* const* fns = all[(ver >= 2 && ver <= 7) ? ver - 1 : 0];
+  const void* const* fns = all[(ver >= 2 && ver <= 8) ? ver - 1 : 0];
   // v6: 128-token tiles (TCAMD_GEMM_HALF: 0 never, 1 (default) when N <= 1024
   // and 256-token tiles would fill at most half the CUs, 2 always).  Measured
   // (profiles/r4_gemm_k15.md): 3072 tokens x N 1024 +33-61%; at 24,576 tokens
@@ -724,7 +738,7 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
   }
   void* args[] = {&p};
   int grid = p.mt * p.nt;
-  if (ver == 6) {  // persistent: one workgroup per CU (a multiple of 8: XCD-stable)
+  if (ver == 6 || ver == 8) {  // persistent: one workgroup per CU (a multiple of 8: XCD-stable)
     static std::atomic<int> ncu_cache[64];
     int ncu = ncu_cache[dev].load(std::memory_order_relaxed);
     if (ncu <= 0) {
