@@ -269,7 +269,9 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmParams p) {
 // both were issuing.  With STAG, waves 4-7 issue step kt + 2's copies right
 // after step kt's middle barrier (that buffer's reads all retired there), a
 // half step before waves 0-3 issue theirs at the top of step kt + 1.
-template <int EPI, int BMT = 256, bool STAG = false>
+// STAG 2 (TCAMD_GEMM_V=9): every wave issues step kt + 2's copies after step
+// kt's middle barrier: a full step of lead for every copy (v6: half a step)
+template <int EPI, int BMT = 256, int STAG = 0>
 __global__ void __launch_bounds__(512, 1) gemm_bf16_pipe_kernel(GemmParams p) {
   constexpr int NJ = BMT / 32;             // token fragments per wave
   constexpr int NXP = BMT / 64;            // X copies per thread per step
@@ -345,7 +347,7 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_pipe_kernel(GemmParams p) {
   const int nk = p.K / kBK, G = gridDim.x;
   int vb = blockIdx.x, m0, n0;
   tile_of(vb, m0, n0);
-  const bool grp_b = STAG && wave >= 4;
+  const bool grp_b = (STAG == 1 && wave >= 4) || STAG == 2;
   set_src(m0, n0);
   stage(0, 0);
   if (grp_b && nk > 1) stage(1, 1);
@@ -363,6 +365,10 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_pipe_kernel(GemmParams p) {
       if (more && !grp_b) stage(kt + 1, buf ^ 1);
       rd(buf, 1);
       mma(0);
+      // step kt + 1's copies landed (explicit: with STAG 2 they were issued in
+      // the previous iteration and the compiler does not see them here)
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
       __syncthreads();
       if (grp_b && kt + 2 < nk) stage(kt + 2, buf);
       rd(buf ^ 1, 0);  // unconditional (stale on the last step, unused)
@@ -686,9 +692,9 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
   // L2 warm-up of the step after next, 6 = fragments double-buffered in
   // registers, persistent (the pipelined kernel; default), 7 = five 32-k
   // stages (the deep kernel), 8 = 6 with the SIMD-partner waves' copies half a
-  // step apart
+  // step apart, 9 = 6 with every copy issued a full step ahead
   static const int ver = getenv("TCAMD_GEMM_V") ? atoi(getenv("TCAMD_GEMM_V")) : 6;
-  const void* all[8][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
+  const void* all[9][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
                             (const void*)gemm_bf16_kernel<2>, (const void*)gemm_bf16_kernel<3>},
                            {(const void*)gemm_bf16_ph_kernel<0, false>, (const void*)gemm_bf16_ph_kernel<1, false>,
                             (const void*)gemm_bf16_ph_kernel<2, false>, (const void*)gemm_bf16_ph_kernel<3, false>},
@@ -702,13 +708,17 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
                             (const void*)gemm_bf16_pipe_kernel<2>, (const void*)gemm_bf16_pipe_kernel<3>},
                            {(const void*)gemm_bf16_deep_kernel<0>, (const void*)gemm_bf16_deep_kernel<1>,
                             (const void*)gemm_bf16_deep_kernel<2>, (const void*)gemm_bf16_deep_kernel<3>},
-                           {(const void*)gemm_bf16_pipe_kernel<0, 256, true>,
-                            (const void*)gemm_bf16_pipe_kernel<1, 256, true>,
-                            (const void*)gemm_bf16_pipe_kernel<2, 256, true>,
-                            (const void*)gemm_bf16_pipe_kernel<3, 256, true>}};
+                           {(const void*)gemm_bf16_pipe_kernel<0, 256, 1>,
+                            (const void*)gemm_bf16_pipe_kernel<1, 256, 1>,
+                            (const void*)gemm_bf16_pipe_kernel<2, 256, 1>,
+                            (const void*)gemm_bf16_pipe_kernel<3, 256, 1>},
+                           {(const void*)gemm_bf16_pipe_kernel<0, 256, 2>,
+                            (const void*)gemm_bf16_pipe_kernel<1, 256, 2>,
+                            (const void*)gemm_bf16_pipe_kernel<2, 256, 2>,
+                            (const void*)gemm_bf16_pipe_kernel<3, 256, 2>}};
   const void* half[4] = {(const void*)gemm_bf16_pipe_kernel<0, 128>, (const void*)gemm_bf16_pipe_kernel<1, 128>,
                          (const void*)gemm_bf16_pipe_kernel<2, 128>, (const void*)gemm_bf16_pipe_kernel<3, 128>};
-  const void* const* fns = all[(ver >= 2 && ver <= 8) ? ver - 1 : 0];
+  const void* const* fns = all[(ver >= 2 && ver <= 9) ? ver - 1 : 0];
   // v6: 128-token tiles (TCAMD_GEMM_HALF: 0 never, 1 (default) when N <= 1024
   // and 256-token tiles would fill at most half the CUs, 2 always).  Measured
   // (profiles/r4_gemm_k15.md): 3072 tokens x N 1024 +33-61%; at 24,576 tokens
@@ -738,7 +748,7 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
   }
   void* args[] = {&p};
   int grid = p.mt * p.nt;
-  if (ver == 6 || ver == 8) {  // persistent: one workgroup per CU (a multiple of 8: XCD-stable)
+  if (ver == 6 || ver == 8 || ver == 9) {  // persistent: one workgroup per CU (a multiple of 8: XCD-stable)
     static std::atomic<int> ncu_cache[64];
     int ncu = ncu_cache[dev].load(std::memory_order_relaxed);
     if (ncu <= 0) {
