@@ -402,6 +402,136 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_pipe_kernel(GemmParams p) {
   }
 }
 
+// ---- one wave per SIMD (TCAMD_GEMM_V=10) ----
+// 4 waves of 128 x 128 (2 x 2 over the 256 x 256 tile), 64 accumulators per
+// lane (256 registers, AGPR half of the 512-entry file): per 64-k step each
+// wave reads 32 fragments for 128 MFMAs (v6: 24 for 64), and the step barrier
+// joins 4 waves instead of 8.  With one wave per SIMD nothing hides a stall,
+// so the next step's 16 copies per thread are issued one per 4 MFMAs of the
+// first half step, and the fragments are double-buffered as in v6.
+template <int EPI>
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+gemm_bf16_w4_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwg = p.mt * p.nt;
+  const int b = blockIdx.x, xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
+  const int wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  const int tm = wg / p.nt, tn = wg - tm * p.nt;
+  const int m0 = tm * kBM, n0 = tn * kBN;
+  // copy piece i (0-7) of wave w: tile rows 8 (4 i + w) ..+8 (1 KB); row
+  // (4 i + w) 8 + lane / 8 = row0 + 32 i keeps the swizzle of row0, so one
+  // 32-bit element offset per operand (the X row clamped per piece) instead
+  // of 16 pointers
+  const int row0 = wave * 8 + (lane >> 3);
+  const int c0 = (lane & 7) ^ ((row0 >> 1) & 7);
+  const int offw = (n0 + row0) * p.ldw + 8 * c0;
+  auto stage1 = [&](int kt, int buf, int piece) {  // piece 0-7 W, 8-15 X
+    uint8_t* dw = lds + buf * kBufB;
+    const int k0 = kt * kBK, i = piece & 7;
+    if (piece < 8) {
+      const uint16_t* src = p.w + offw + (32 * i * p.ldw + k0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dw + (4 * i + wave) * 1024), 16, 0, 0);
+    } else {
+      const uint16_t* src = p.x + (min(m0 + row0 + 32 * i, p.M - 1) * p.ldx + 8 * c0 + k0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dw + kTileB + (4 * i + wave) * 1024), 16, 0, 0);
+    }
+  };
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr16 = lane & 15, fq = lane >> 4;
+  int oa[2], ob[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    oa[kk] = chunk_off(128 * wn + fr16, 4 * kk + fq);
+    ob[kk] = kTileB + chunk_off(128 * wm + fr16, 4 * kk + fq);
+  }
+  v4u fa[2][8], fb[2][8];
+  auto rd = [&](int buf, int kk) {
+    const uint8_t* ta = lds + buf * kBufB + oa[kk];
+    const uint8_t* tb = lds + buf * kBufB + ob[kk];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[kk][i] = *reinterpret_cast<const v4u*>(ta + 2048 * i);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fb[kk][j] = *reinterpret_cast<const v4u*>(tb + 2048 * j);
+  };
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // COPY: step kt_next's 16 copies go out one per 4 MFMAs (unconditional:
+  // branches between the MFMA groups make the compiler shuffle accumulators)
+  auto mma = [&](int kk, auto copy_c, int kt_next, int buf_next) {
+    constexpr bool COPY = decltype(copy_c)::value;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int j = 4 * h; j < 4 * h + 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr(fa[kk][i]), fr(fb[kk][j]), acc[i][j], 0, 0, 0);
+        if constexpr (COPY) {
+          stage1(kt_next, buf_next, 2 * i + h);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+  };
+
+  const int nk = p.K / kBK;
+#pragma unroll
+  for (int piece = 0; piece < 16; ++piece) stage1(0, 0, piece);
+  __syncthreads();
+  rd(0, 0);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    rd(buf, 1);
+    // the last step re-copies itself into the other buffer (read by nothing)
+    mma(0, std::true_type{}, kt + 1 < nk ? kt + 1 : nk - 1, buf ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): step kt + 1 landed
+    __syncthreads();
+    rd(buf ^ 1, 0);  // unconditional (stale on the last step, unused)
+    mma(1, std::false_type{}, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  }
+  // epilogue: lane column = token, four consecutive channels -> 8-B stores
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int n = n0 + 128 * wn + 16 * i + 4 * fq;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI >= 1) {
+      const v2u bb = *reinterpret_cast<const v2u*>(p.bias + n);
+      bv[0] = __uint_as_float(bb[0] << 16);
+      bv[1] = __uint_as_float(bb[0] & 0xffff0000u);
+      bv[2] = __uint_as_float(bb[1] << 16);
+      bv[3] = __uint_as_float(bb[1] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = m0 + 128 * wm + 16 * j + fr16;
+      if (m >= p.M) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
+      if constexpr (EPI == 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+      }
+      if constexpr (EPI == 3) {
+        const v2u rr = *reinterpret_cast<const v2u*>(p.r + (size_t)m * p.ldr + n);
+        v[0] += __uint_as_float(rr[0] << 16);
+        v[1] += __uint_as_float(rr[0] & 0xffff0000u);
+        v[2] += __uint_as_float(rr[1] << 16);
+        v[3] += __uint_as_float(rr[1] & 0xffff0000u);
+      }
+      *reinterpret_cast<v2u*>(p.y + (size_t)m * p.ldy + n) = v2u{pk(v[0], v[1]), pk(v[2], v[3])};
+    }
+  }
+}
+
 // ---- deep variant (TCAMD_GEMM_V=7): five 32-k stages, 3 stages of DMA lead ----
 // At 2 stages of 64 k the next step's copies must land within half a step of
 // their issue (v6) -- far less than an L2 miss under load.  Here a stage is
@@ -692,9 +822,10 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
   // L2 warm-up of the step after next, 6 = fragments double-buffered in
   // registers, persistent (the pipelined kernel; default), 7 = five 32-k
   // stages (the deep kernel), 8 = 6 with the SIMD-partner waves' copies half a
-  // step apart, 9 = 6 with every copy issued a full step ahead
+  // step apart, 9 = 6 with every copy issued a full step ahead, 10 = one
+  // wave per SIMD (4 waves of 128 x 128)
   static const int ver = getenv("TCAMD_GEMM_V") ? atoi(getenv("TCAMD_GEMM_V")) : 6;
-  const void* all[9][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
+  const void* all[10][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
                             (const void*)gemm_bf16_kernel<2>, (const void*)gemm_bf16_kernel<3>},
                            {(const void*)gemm_bf16_ph_kernel<0, false>, (const void*)gemm_bf16_ph_kernel<1, false>,
                             (const void*)gemm_bf16_ph_kernel<2, false>, (const void*)gemm_bf16_ph_kernel<3, false>},
@@ -715,10 +846,12 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
                            {(const void*)gemm_bf16_pipe_kernel<0, 256, 2>,
                             (const void*)gemm_bf16_pipe_kernel<1, 256, 2>,
                             (const void*)gemm_bf16_pipe_kernel<2, 256, 2>,
-                            (const void*)gemm_bf16_pipe_kernel<3, 256, 2>}};
+                            (const void*)gemm_bf16_pipe_kernel<3, 256, 2>},
+                           {(const void*)gemm_bf16_w4_kernel<0>, (const void*)gemm_bf16_w4_kernel<1>,
+                            (const void*)gemm_bf16_w4_kernel<2>, (const void*)gemm_bf16_w4_kernel<3>}};
   const void* half[4] = {(const void*)gemm_bf16_pipe_kernel<0, 128>, (const void*)gemm_bf16_pipe_kernel<1, 128>,
                          (const void*)gemm_bf16_pipe_kernel<2, 128>, (const void*)gemm_bf16_pipe_kernel<3, 128>};
-  const void* const* fns = all[(ver >= 2 && ver <= 9) ? ver - 1 : 0];
+  const void* const* fns = all[(ver >= 2 && ver <= 10) ? ver - 1 : 0];
   // v6: 128-token tiles (TCAMD_GEMM_HALF: 0 never, 1 (default) when N <= 1024
   // and 256-token tiles would fill at most half the CUs, 2 always).  Measured
   // (profiles/r4_gemm_k15.md): 3072 tokens x N 1024 +33-61%; at 24,576 tokens
@@ -759,7 +892,8 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
     grid = grid < ncu ? grid : ncu;
   }
   const int lds_b = ver == 7 ? kLdsD : use_half ? 2 * (kTileB + 128 * kBK * 2) : kLdsG;
-  const hipError_t e = hipLaunchKernel(fns[epi], dim3(grid), dim3(512), args, lds_b, (hipStream_t)stream);
+  const hipError_t e =
+      hipLaunchKernel(fns[epi], dim3(grid), dim3(ver == 10 ? 256 : 512), args, lds_b, (hipStream_t)stream);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }
