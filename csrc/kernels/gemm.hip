@@ -343,11 +343,25 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_pipe_kernel(GemmParams p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr(fa[kk][i]), fr(fb[kk][j]), acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
+  // STAG 3: mma(1) with step kt_c's copies (clamped, unconditional: no branch
+  // between the MFMA groups) into buffer bufc, one per NJ / 2 MFMAs
+  auto mma_copy = [&](int kk, int kt_c, int bufc) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int j = h * NJ / 2; j < (h + 1) * NJ / 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr(fa[kk][i]), fr(fb[kk][j]), acc[i][j], 0, 0, 0);
+        if (2 * i + h < 4 + NXP) stage1(kt_c, bufc, 2 * i + h);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  };
 
   const int nk = p.K / kBK, G = gridDim.x;
   int vb = blockIdx.x, m0, n0;
   tile_of(vb, m0, n0);
-  const bool grp_b = (STAG == 1 && wave >= 4) || STAG == 2;
+  const bool grp_b = (STAG == 1 && wave >= 4) || STAG >= 2;
   set_src(m0, n0);
   stage(0, 0);
   if (grp_b && nk > 1) stage(1, 1);
@@ -370,9 +384,12 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_pipe_kernel(GemmParams p) {
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
       __syncthreads();
-      if (grp_b && kt + 2 < nk) stage(kt + 2, buf);
+      if (STAG != 3 && grp_b && kt + 2 < nk) stage(kt + 2, buf);
       rd(buf ^ 1, 0);  // unconditional (stale on the last step, unused)
-      mma(1);
+      if constexpr (STAG == 3)
+        mma_copy(1, kt + 2 < nk ? kt + 2 : nk - 1, buf);  // past the end: a re-copy nothing reads
+      else
+        mma(1);
       // those reads retired during mma(1); retiring them explicitly here keeps
       // the compiler from draining the kk 1 reads before mma(0) (it loses the
       // count of reads pending across the back edge)
@@ -823,9 +840,10 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
   // registers, persistent (the pipelined kernel; default), 7 = five 32-k
   // stages (the deep kernel), 8 = 6 with the SIMD-partner waves' copies half a
   // step apart, 9 = 6 with every copy issued a full step ahead, 10 = one
-  // wave per SIMD (4 waves of 128 x 128)
+  // wave per SIMD (4 waves of 128 x 128), 11 = 9 with the copies spread
+  // over the second MFMA half
   static const int ver = getenv("TCAMD_GEMM_V") ? atoi(getenv("TCAMD_GEMM_V")) : 6;
-  const void* all[10][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
+  const void* all[11][4] = {{(const void*)gemm_bf16_kernel<0>, (const void*)gemm_bf16_kernel<1>,
                             (const void*)gemm_bf16_kernel<2>, (const void*)gemm_bf16_kernel<3>},
                            {(const void*)gemm_bf16_ph_kernel<0, false>, (const void*)gemm_bf16_ph_kernel<1, false>,
                             (const void*)gemm_bf16_ph_kernel<2, false>, (const void*)gemm_bf16_ph_kernel<3, false>},
@@ -848,10 +866,14 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
                             (const void*)gemm_bf16_pipe_kernel<2, 256, 2>,
                             (const void*)gemm_bf16_pipe_kernel<3, 256, 2>},
                            {(const void*)gemm_bf16_w4_kernel<0>, (const void*)gemm_bf16_w4_kernel<1>,
-                            (const void*)gemm_bf16_w4_kernel<2>, (const void*)gemm_bf16_w4_kernel<3>}};
+                            (const void*)gemm_bf16_w4_kernel<2>, (const void*)gemm_bf16_w4_kernel<3>},
+                           {(const void*)gemm_bf16_pipe_kernel<0, 256, 3>,
+                            (const void*)gemm_bf16_pipe_kernel<1, 256, 3>,
+                            (const void*)gemm_bf16_pipe_kernel<2, 256, 3>,
+                            (const void*)gemm_bf16_pipe_kernel<3, 256, 3>}};
   const void* half[4] = {(const void*)gemm_bf16_pipe_kernel<0, 128>, (const void*)gemm_bf16_pipe_kernel<1, 128>,
                          (const void*)gemm_bf16_pipe_kernel<2, 128>, (const void*)gemm_bf16_pipe_kernel<3, 128>};
-  const void* const* fns = all[(ver >= 2 && ver <= 10) ? ver - 1 : 0];
+  const void* const* fns = all[(ver >= 2 && ver <= 11) ? ver - 1 : 0];
   // v6: 128-token tiles (TCAMD_GEMM_HALF: 0 never, 1 (default) when N <= 1024
   // and 256-token tiles would fill at most half the CUs, 2 always).  Measured
   // (profiles/r4_gemm_k15.md): 3072 tokens x N 1024 +33-61%; at 24,576 tokens
@@ -881,7 +903,7 @@ int tcamd_gemm_bf16(const void* x, const void* w, const void* bias, const void* 
   }
   void* args[] = {&p};
   int grid = p.mt * p.nt;
-  if (ver == 6 || ver == 8 || ver == 9) {  // persistent: one workgroup per CU (a multiple of 8: XCD-stable)
+  if (ver == 6 || (ver >= 8 && ver != 10)) {  // persistent: one workgroup per CU (a multiple of 8: XCD-stable)
     static std::atomic<int> ncu_cache[64];
     int ncu = ncu_cache[dev].load(std::memory_order_relaxed);
     if (ncu <= 0) {

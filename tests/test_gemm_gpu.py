@@ -91,7 +91,7 @@ def test_gemm_bf16_rejects_bad_shapes():
         hip.gemm_bf16(t.data_ptr(), t.data_ptr(), t.data_ptr(), 16, 256, 64, epilogue="bias")
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "7", "8", "9", "10"])
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "7", "8", "9", "10", "11"])
 def test_gemm_bf16_phased_variant_matches(tmp_path, variant):
     """TCAMD_GEMM_V=2 (4 phases per K step, counted vmcnt across barriers) and 3
     (the same with the two wave groups one phase apart) in a child process (the variant is chosen once per process): same results as
