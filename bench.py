@@ -93,6 +93,9 @@ def parse_args(argv=None):
     ap.add_argument("--rehearse", action="store_true",
                     help="one-GPU rehearsal of the N-GPU launch: every rank (and its server) on GPU 0, gloo "
                          "process group, p2p/host fan-out (RCCL cannot put two ranks on one device)")
+    ap.add_argument("--pin", default="auto", choices=["auto", "on", "off"],
+                    help="pin each rank (server child + load generator threads) to CPUs of its GPU's NUMA node "
+                         "(auto: when more than one rank runs on this host)")
     ap.add_argument("--server-log", default="")
     ap.add_argument("--model", default="densenet_onnx", choices=["densenet_onnx", "bert_large"])
     ap.add_argument("--sweep", default="1,4,16,64,256", help="bert_large: concurrencies per GPU")
@@ -149,6 +152,25 @@ def windows(end_ns, per, k):
         out.append(per / max((t - t_prev) * 1e-9, 1e-9))
         t_prev = t
     return out
+
+
+def window_percentiles(lat_ns, end_ns, per, k):
+    """p50 and p99 (us) of the requests that completed in each of the k
+    windows of `per` requests (completion order, as :func:`windows`)."""
+    import numpy as np
+
+    from triton_client_amd.perf.loadgen import percentile_us
+
+    order = np.argsort(end_ns, kind="stable")
+    lat = lat_ns.astype(np.float64)[order]
+    p50, p99 = [], []
+    for i in range(k):
+        w = lat[i * per:(i + 1) * per]
+        if len(w) == 0:
+            break
+        p50.append(round(percentile_us(w, 50), 1))
+        p99.append(round(percentile_us(w, 99), 1))
+    return p50, p99
 
 
 def stats_delta(a, b):
@@ -225,6 +247,19 @@ def main():
     log_dir = os.path.join(REPO, "gpurun_out")
     os.makedirs(log_dir, exist_ok=True)
 
+    # host placement BEFORE the server is spawned (the child inherits it): the
+    # CPUs of this rank's GPU's NUMA node, split among the ranks sharing it
+    from triton_client_amd.parallel import placement
+
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    place = placement.plan(dev if args.rehearse else local_rank, 1 if args.rehearse else local_world)
+    if args.pin == "on" or (args.pin == "auto" and local_world > 1 and not args.rehearse):
+        place = placement.apply(place)
+    else:
+        place["applied"] = False
+    place.pop("cpus", None)
+    log("placement: %s" % place)
+
     def start_server(engine, tag):
         if bert:
             extra = ["--instance-count", str(args.bert_instance_count), "--max-queue-delay-us",
@@ -244,6 +279,7 @@ def main():
                              port_stripe=local_rank if world > 1 else None), path
 
     srv, srv_log = start_server(args.engine, "bert" if bert else args.engine)
+    place["grpc_port"] = srv.grpc_port
 
     import torch
     import torch.distributed as dist
@@ -376,6 +412,10 @@ def main():
         mean3 = sum(last3) / len(last3)
         stable = all(abs(w - mean3) <= 0.10 * mean3 for w in last3)
         all_lat = fanout.gather_arrays(lat.astype(np.int64)).astype(np.float64)
+        # per-window p50 / p99 (rank 0, requests binned by completion time into
+        # the same windows as the throughputs): a wide tail is then visible as
+        # one bad window or as the whole run
+        win_p = window_percentiles(lat, end, per, args.steps)
         value = world * args.steps * per * bs / elapsed
         breakdown = stats_delta(st0, st1)
         breakdown["client_overhead_us_per_request"] = round(
@@ -479,6 +519,9 @@ def main():
             "p99_latency_us": round(percentile_us(all_lat, 99), 1),
             "stable": bool(fanout.max_over_ranks(0.0 if stable else 1.0) == 0.0),
             "window_infer_per_sec_rank0": [round(w * bs, 1) for w in wins],
+            "window_p50_latency_us_rank0": win_p[0],
+            "window_p99_latency_us_rank0": win_p[1],
+            "placement": fanout.gather_objects(place),
             "server_breakdown_rank0": breakdown,
             "p99_constrained": p99c,
             "bs1": bs1,

@@ -338,6 +338,7 @@ Error ParseOptions(int argc, char** argv, Options* o, bool* help)
             if (c > b) l.push_back(val.substr(b, c - b));
             b = c + 1;
           }
+          if (l.empty()) return Error("--shared-memory-input: no region for " + name);
           o->preregistered_inputs[name] = l.front();
         }
         break;

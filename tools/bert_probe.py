@@ -21,8 +21,6 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[64])
     ap.add_argument("--seq", type=int, default=384)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--k15-ab", type=int, default=0,
-                    help="also time the forward with K15 GEMMs from this many tokens (interleaved A/B rounds)")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--tuned-table", default="",
                     help="A/B against TunableOp reading this solution table (tuning off), e.g. "
@@ -37,20 +35,18 @@ def main():
         ids = torch.randint(0, bert.VOCAB, (b, a.seq), device=dev)
         mask = torch.ones(b, a.seq, device=dev, dtype=torch.int64)
         tt = torch.zeros(b, a.seq, device=dev, dtype=torch.int64)
-        variants = {"default": bert.K15_MIN_TOKENS}
-        if a.k15_ab:
-            variants = {"hipblaslt": 0, "k15": a.k15_ab}
+        variants = {"default": 0}
         tun = None
         if a.tuned_table:
             import torch.cuda.tunable as tun
 
             assert bert.use_tuned_gemms(a.tuned_table), "the table does not load in this process"
-            variants = {"default": bert.K15_MIN_TOKENS, "tunableop": bert.K15_MIN_TOKENS}
+            variants = {"default": 0, "tunableop": 0}
         elif a.tunable:
             import torch.cuda.tunable as tun
 
             tun.set_filename(a.tunable)
-            variants = {"default": bert.K15_MIN_TOKENS, "tunableop": bert.K15_MIN_TOKENS}
+            variants = {"default": 0, "tunableop": 0}
             with torch.no_grad():  # tune every GEMM shape of this batch once, outside the timed rounds
                 tun.enable(True)
                 tun.tuning_enable(True)
@@ -60,16 +56,14 @@ def main():
                 tun.enable(False)
         ts = {k: [] for k in variants}
         with torch.no_grad():
-            for name, thr in variants.items():
-                bert.K15_MIN_TOKENS = thr
+            for name in variants:
                 if tun is not None:
                     tun.enable(name == "tunableop")
                 for _ in range(2):
                     model(ids, mask, tt)
             torch.cuda.synchronize()
             for _ in range(a.rounds):
-                for name, thr in variants.items():
-                    bert.K15_MIN_TOKENS = thr
+                for name in variants:
                     if tun is not None:
                         tun.enable(name == "tunableop")
                     torch.cuda.synchronize()

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--k14x-ab", action="store_true",
                     help="fp32 engine: also capture graphs with K14x off and interleave the two (rounds)")
+    ap.add_argument("--ab", default="",
+                    help="fp32 engine A/B of one engine attribute, interleaved per round: ATTR=V1,V2 "
+                         "(e.g. fuse_v3=0,56; integer values)")
     ap.add_argument("--rounds", type=int, default=1)
     args = ap.parse_args()
     import torch
@@ -48,15 +51,19 @@ def main():
         outs = [torch.zeros(maxb, 1000, device=dev) for _ in engines]
         sts = [torch.cuda.Stream(device=dev) for _ in engines]
         variants = [("default", None)]
+        attr = "smallf_min_blocks"
         if args.k14x_ab and name == "fp32":
             variants = [("k14x", eng.smallf_min_blocks), ("pair", 0)]
+        if args.ab and name == "fp32":
+            attr, vals = args.ab.split("=")
+            variants = [("%s=%s" % (attr, v), int(v)) for v in vals.split(",")]
         for b in batches:
             gv = {}
             for vname, mb in variants:
                 graphs = []
                 for e, o, s in zip(engines, outs, sts):
                     if mb is not None:
-                        e.smallf_min_blocks = mb
+                        setattr(e, attr, mb)
                     with torch.cuda.stream(s), torch.no_grad():
                         e.forward_ptrs(b, out=o)
                         g = torch.cuda.CUDAGraph()

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--ks", default="", help="comma list of K: loop over them (overrides --k)")
     ap.add_argument("--fused-dbg", default="", help="comma list of K11x ablation masks (TCAMD_X3F_DBG) to time")
     ap.add_argument("--stamp", action="store_true", help="also run a TCAMD_X3F_STAMP=1 child (phase cycles)")
-    ap.add_argument("--both", action="store_true", help="also time K11x v1 (8 waves) in a child")
+    ap.add_argument("--both", action="store_true", help="also time K11x v1 in a child (default v3)")
     ap.add_argument("--stamp-dbg", default="", help="comma list of ablation masks to run as stamped children")
     a = ap.parse_args()
     for K in ([int(v) for v in a.ks.split(",")] if a.ks else [a.k]):
@@ -80,9 +80,9 @@ def bench(a):
         print("hw=%d k=%d chunk=%d: %.1f us per %d images" % (a.hw, K, c, us, a.imgs), flush=True)
     # K11x: the same layer in one kernel, z kept in LDS
     f1h, f1l = hip.x3_w1_fragments(w1h), hip.x3_w1_fragments(w1l)
-    v = int(os.environ.get("TCAMD_X3F_V", "2"))
-    frag = hip.x3_w3f_fragments if v == 1 else hip.x3_w3_fragments
-    fn = hip.x3_dense_fused if v == 1 else hip.x3_dense_fused4
+    v = int(os.environ.get("TCAMD_X3F_V", "3"))
+    frag = hip.x3_w3f_fragments
+    fn = hip.x3_dense_fused if v == 1 else hip.x3_dense_fused3
     f3h, f3l = frag(w3h), frag(w3l)
 
     def fused():
@@ -108,7 +108,7 @@ def bench(a):
     runs = [("TCAMD_X3F_DBG", d) for d in a.fused_dbg.split(",") if d] + ([("TCAMD_X3F_STAMP", "1")] if a.stamp else [])
     runs = [(v, d, {}) for v, d in runs] + [("TCAMD_X3F_DBG", d, {"TCAMD_X3F_STAMP": "1"})
                                             for d in a.stamp_dbg.split(",") if d]
-    if a.both and os.environ.get("TCAMD_X3F_V", "2") == "2":
+    if a.both and os.environ.get("TCAMD_X3F_V", "3") == "3":
         runs.append(("TCAMD_X3F_V", "1", {}))
     if runs:
         import subprocess

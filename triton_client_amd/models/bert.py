@@ -36,29 +36,14 @@ TYPES = 2
 
 # fused paths on the GPU (bf16 CUDA tensors); TC_BERT_FUSED=0 runs plain torch ops
 FUSED = os.environ.get("TC_BERT_FUSED", "1") != "0"
-# K15 (csrc/kernels/gemm.hip) for the four projections from this many tokens
-# up (0 = never: hipBLASLt); small batches stay on the library (few tiles)
-K15_MIN_TOKENS = int(os.environ.get("TC_BERT_K15_MIN_TOKENS", "0"))
-
-
-def _k15_ok(x2d, n):
-    return (FUSED and K15_MIN_TOKENS > 0 and x2d.is_cuda and x2d.dtype == torch.bfloat16 and x2d.is_contiguous()
-            and x2d.shape[0] >= K15_MIN_TOKENS and n % 256 == 0 and x2d.shape[1] % 64 == 0)
-
-
 def _proj(x, lin, epilogue="bias"):
-    """lin(x) (epilogue "bias"), gelu(lin(x)) ("bias_gelu") or x @ W^T ("none"):
-    K15 with the epilogue fused at big token counts, torch / hipBLASLt otherwise."""
+    """lin(x) (epilogue "bias"), gelu(lin(x)) ("bias_gelu") or x @ W^T ("none")
+    on hipBLASLt.  The four projections are plain library GEMMs: a hand-written
+    gfx950 GEMM (K15, rounds 3-4) reached 0.80-0.93x of hipBLASLt at 24,576
+    tokens and made the served forward slower, so it was retired
+    (profiles/r4_gemm_k15.md); config 4 is library-bound on these GEMMs."""
     x2 = x.reshape(-1, x.shape[-1])
     n = lin.weight.shape[0]
-    if _k15_ok(x2, n):
-        from triton_client_amd.ops import hip
-
-        y = torch.empty(x2.shape[0], n, device=x.device, dtype=x.dtype)
-        hip.gemm_bf16(x2.data_ptr(), lin.weight.data_ptr(), y.data_ptr(), x2.shape[0], n, x2.shape[1],
-                      bias=None if epilogue == "none" else lin.bias.data_ptr(), epilogue=epilogue,
-                      stream=torch.cuda.current_stream(x.device).cuda_stream)
-        return y.view(*x.shape[:-1], n)
     if epilogue == "none":
         return torch.mm(x2, lin.weight.t()).view(*x.shape[:-1], n)
     if epilogue == "bias_gelu":
@@ -206,8 +191,12 @@ def use_tuned_gemms(path=TUNED_GEMMS):
     (tuning itself stays off: a shape missing from the table runs the
     library's default solution).  The table's validators (PyTorch, HIP,
     hipBLASLt, rocBLAS, gfx arch) must match this process, else TunableOp stays
-    off.  TC_BERT_TUNED_GEMMS=0 disables it.  Returns True when it is on."""
-    if os.environ.get("TC_BERT_TUNED_GEMMS", "1") == "0" or not os.path.exists(path) or not torch.cuda.is_available():
+    off.  Off by default: TunableOp is process-wide (every torch GEMM of every
+    model in the server process would go through it) and the table measured
+    neutral within noise in served runs (profiles/r4_bench_bert_tunable_on.json
+    vs _off.json).  TC_BERT_TUNED_GEMMS=1 turns it on (bert-only server
+    processes).  Returns True when it is on."""
+    if os.environ.get("TC_BERT_TUNED_GEMMS", "0") != "1" or not os.path.exists(path) or not torch.cuda.is_available():
         return False
     import torch.cuda.tunable as tun
 

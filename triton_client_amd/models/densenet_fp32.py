@@ -117,12 +117,12 @@ class FusedDenseNetFP32:
         # tiles (its per-block prologue recomputes a (2W+2)-row halo of z, yet it
         # still beats the two-launch pair at bs1); 0 disables it (A/B runs)
         self.fuse_min_tiles = int(os.environ.get("TCAMD_X3_FUSE_MIN_TPB", "1"))
-        # K11x v2 (4 waves) from this K on the 56x56 block at big batches.  In
-        # isolation v2 wins at K >= 160 (profiles/r3_fused_dense_layer.md), but in
-        # the whole forward v1 everywhere measured 1% faster on one stream and
-        # 0.7% on two (r3_fused/v1_everywhere.log): off by default
-        self.fuse_v2_min_k = int(os.environ.get("TCAMD_X3_FUSE_V2_MIN_K", "999"))
         self.fuse_big_k_min_tiles = int(os.environ.get("TCAMD_X3_FUSE_BIGK_MIN_TPB", "4"))
+        # K11x v3 (the next chunk's 1x1 interleaved into the 3x3) on blocks of
+        # width >= fuse_v3 at >= 2 tiles per block; 0 = v1 everywhere.  Engine
+        # bs128 x 2 streams 47.1k -> 47.6k img/s with v3 on both K11x blocks
+        # (profiles/r5_k11x_v3.md)
+        self.fuse_v3 = int(os.environ.get("TCAMD_X3_FUSE_V3", "28"))
         # K13x (small-M dense layer, csrc/kernels/densenet_x3s.hip) for the
         # unfused layers of a block with at most this many pixels; 0 disables it
         self.small_m = int(os.environ.get("TCAMD_X3_SMALL_M", "1600"))
@@ -291,17 +291,18 @@ class FusedDenseNetFP32:
     __call__ = forward
 
     def _fused_layer(self, fused, L, fp, ctot, b, hw, st):
-        """K11x: the whole dense layer in one kernel.  v2 (4 waves) on the 56x56
-        block at big batches from K >= fuse_v2_min_k, v1 (8 waves) elsewhere,
-        bs1 included (per-K A/B: profiles/r3_fused_dense_layer.md)."""
-        if fused == 2 and L["cin"] >= self.fuse_v2_min_k:
-            hip.x3_dense_fused4(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
-                                L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(), L["w2h"].data_ptr(),
-                                L["w2l"].data_ptr(), fp + 4 * L["cin"], ctot, stream=st)
+        """K11x: the whole dense layer in one kernel.  v3 (the next chunk's 1x1
+        interleaved into each tile's 3x3) on blocks of width >= fuse_v3 once every
+        block walks >= 2 tiles; v1 elsewhere (bs1 included: one tile per block
+        has no next chunk to interleave).  The 4-wave v2 of rounds 3-4 lost in
+        the whole forward and was removed (profiles/r5_k11x_v3.md)."""
+        args = (fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(), L["w1fh"].data_ptr(),
+                L["w1fl"].data_ptr(), L["b1"].data_ptr(), L["w2fh"].data_ptr(), L["w2fl"].data_ptr(),
+                fp + 4 * L["cin"], ctot)
+        if self.fuse_v3 and hw >= self.fuse_v3 and b * hw * hw >= 2 * 64 * _cu_count(self.device):
+            hip.x3_dense_fused3(*args, stream=st)
         else:
-            hip.x3_dense_fused(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
-                               L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(), L["w2fh"].data_ptr(),
-                               L["w2fl"].data_ptr(), fp + 4 * L["cin"], ctot, stream=st)
+            hip.x3_dense_fused(*args, stream=st)
 
     def _transition(self, bi, fp, ctot, b, hw, ws, wsb, st):
         if bi < len(self.trans):
@@ -326,7 +327,7 @@ class FusedDenseNetFP32:
 
     def _fuse(self, M, W):
         """K11x (whole layer, z in LDS) for this block's layers: 0 = no (K8x + K9x
-        pair), 1 = v1 (8 waves), 2 = v2 allowed (4 waves, big-batch 56x56)."""
+        pair), otherwise yes (1 / 2: small / big batch)."""
         if self.fuse_min_tiles <= 0 or W > 56 or W < 16:
             return 0
         tiles = (M + 63) // 64

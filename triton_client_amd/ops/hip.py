@@ -214,11 +214,6 @@ _SIGS = {
         ],
         ctypes.c_int,
     ),
-    "tcamd_gemm_bf16": (
-        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p],
-        ctypes.c_int,
-    ),
     "tcamd_x3_dense_small": (
         [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -233,7 +228,7 @@ _SIGS = {
     "tcamd_x3_small_layer_bytes": ([], ctypes.c_int),
     "tcamd_x3_small_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "tcamd_x3_small_timeline": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
-    "tcamd_x3_dense_fused4": (
+    "tcamd_x3_dense_fused3": (
         [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -757,20 +752,6 @@ def x3_dense_fused(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo
                                         w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_fused")
 
 
-GEMM_EPI = {"none": 0, "bias": 1, "bias_gelu": 2, "bias_residual": 3}
-
-
-def gemm_bf16(x, w, y, M, N, K, bias=None, residual=None, epilogue="none", ldx=None, ldw=None, ldr=None, ldy=None,
-              stream=None):
-    """K15: ``y = epi(x @ w.T)`` in bf16 (fp32 accumulate) on the hand-written
-    gfx950 GEMM (csrc/kernels/gemm.hip).  x [M][ldx], w [N][ldw] (nn.Linear
-    layout), y [M][ldy] device pointers; epilogue none | bias | bias_gelu (erf)
-    | bias_residual (+ residual[M][ldr]).  N % 256 == 0, K % 64 == 0."""
-    _check(_load().tcamd_gemm_bf16(x, w, _vp(bias), _vp(residual), y, int(M), int(N), int(K), int(ldx or K),
-                                   int(ldw or K), int(ldr or N), int(ldy or N), GEMM_EPI[epilogue], _vp(stream)),
-           "gemm_bf16")
-
-
 def x3_dense_small(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None,
                    w1f_hi=None, w1f_lo=None):
     """K14x: one fp32-parity dense layer of the 14x14 (half-image tiles + one
@@ -835,11 +816,11 @@ def x3_small_stamps(max_blocks=4096):
     return out[:8 * n].reshape(n, 8).astype(np.int64)
 
 
-def x3_dense_fused4(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None):
-    """K11x v2 (4 waves, one per SIMD, 32x32x16 3x3): as :func:`x3_dense_fused`
-    but ``w2_*`` in the K9x x3_w3_fragments layout."""
-    _check(_load().tcamd_x3_dense_fused4(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
-                                         w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_fused4")
+def x3_dense_fused3(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None):
+    """K11x v3: v1's roles and fragment layouts (``w2_*`` in x3_w3f_fragments),
+    with the next chunk's 1x1 K steps interleaved into each tile's 3x3."""
+    _check(_load().tcamd_x3_dense_fused3(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
+                                         w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_fused3")
 
 
 def x3_fused_stamps():
@@ -853,6 +834,17 @@ def x3_fused_stamps():
     if n <= 0:
         return None
     return buf[: 8 * n].reshape(n, 8)
+
+
+def x3_fused_timeline():
+    """K11x v3 STAMP builds: block 0's barrier timeline of two steady-state
+    tiles, [wave 8][tile 2][barrier 32][arrive, release] shader-clock stamps."""
+    import numpy as np
+
+    buf = np.zeros(8 * 1024, dtype=np.uint64)
+    if _load().tcamd_x3_fused_stamps(buf.ctypes.data, buf.size) <= 0:
+        return None
+    return buf[4096:5120].reshape(8, 2, 32, 2)
 
 
 def x3_stem_fragments(w):

@@ -241,6 +241,14 @@ def time_fanout(region, nbytes, methods, reps=5):
         med = float(np.median(ts[1:]))
         med = max_over_ranks(med)
         out[m] = {"us": round(med * 1e6, 1), "GBps_per_peer": round(nbytes / med / 1e9, 2), "bytes": int(nbytes)}
+        if m == "p2p":
+            # rank 0 knows whether every peer had direct access; MIN over ranks
+            # hands its answer to all of them
+            ok = all_ok(all(_PEER_ACCESS.values()) if dist.get_rank() == 0 else True)
+            out[m]["peer_access"] = ok
+            if not ok:
+                out[m]["note"] = ("hipDeviceEnablePeerAccess failed for a peer: the copies ran over the "
+                                  "runtime's staging path, not the xGMI star")
     return out
 
 
@@ -250,44 +258,67 @@ def fanout_errors(timings):
     return {m: v["error"] for m, v in (timings or {}).items() if "error" in v}
 
 
-def _p2p_copy(region, nbytes, dist):
-    """The X2 star: rank 0 opens every peer's region and copies into it on one
-    stream per peer.  Returns rank 0's exception (None elsewhere / on success);
-    every rank reaches the closing barrier either way."""
+# rank 0's last X2 star: {peer rank: hipDeviceEnablePeerAccess succeeded}
+_PEER_ACCESS = {}
+
+
+def _star_copies(region, handles, nbytes):
+    """Rank 0's half of the X2 star: open every peer's region and copy into it
+    on one stream per peer.  Returns {peer rank: peer access enabled}; a peer
+    whose ``hipDeviceEnablePeerAccess`` failed is still copied to (the runtime
+    stages such copies), but the timing is then not the xGMI star and
+    :func:`time_fanout` labels it ``peer_access: false``.  Raises on a copy
+    failure."""
     from tritonclient.utils import hip_shared_memory as hipshm  # noqa: F401
     from triton_client_amd.ops import hip
 
+    src_dev = region._device_id
+    streams, opened, access = [], [], {}
+    try:
+        for peer in range(1, len(handles)):
+            dev, h = handles[peer]
+            try:
+                hip.enable_peer(src_dev, dev)
+                access[peer] = True
+            except Exception as e:  # noqa: BLE001 - recorded and reported, never swallowed
+                access[peer] = False
+                print("[fanout] hipDeviceEnablePeerAccess(%d -> %d) failed: %s" % (src_dev, dev, str(e)[:200]),
+                      file=sys.stderr)
+            ptr = hip.ipc_open(h, src_dev)
+            opened.append(ptr)
+            s = hip.Stream(src_dev)
+            streams.append(s)
+            hip.memcpy_async(ptr, region._base_addr, nbytes, s.handle)
+        for s in streams:
+            s.synchronize()
+    finally:
+        for s in streams:
+            s.close()
+        for p in opened:
+            hip.ipc_close(p, src_dev)
+    return access
+
+
+def _p2p_copy(region, nbytes, dist):
+    """The X2 star.  Returns this rank's exception (rank 0's copy failure, or
+    an injected fault) or None; every rank reaches the closing barrier either
+    way, so the collective sequence stays aligned and the caller can agree on
+    the outcome."""
     rank = dist.get_rank()
-    world = dist.get_world_size()
-    handles = [None] * world
+    handles = [None] * dist.get_world_size()
     dist.all_gather_object(handles, (region._device_id, region._hip_shm_handle))
     err = None
     if rank == 0:
-        src_dev = region._device_id
-        streams = []
-        opened = []
         try:
-            for peer in range(1, world):
-                dev, h = handles[peer]
-                try:
-                    hip.enable_peer(src_dev, dev)
-                except Exception:
-                    pass  # copies still work through the runtime's staging path
-                ptr = hip.ipc_open(h, src_dev)
-                opened.append(ptr)
-                s = hip.Stream(src_dev)
-                streams.append(s)
-                hip.memcpy_async(ptr, region._base_addr, nbytes, s.handle)
-            for s in streams:
-                s.synchronize()
+            access = _star_copies(region, handles, nbytes)
+            _PEER_ACCESS.clear()
+            _PEER_ACCESS.update(access)
         except Exception as e:  # noqa: BLE001 - agreed on by the caller
             err = e
-        finally:
-            for s in streams:
-                s.close()
-            for p in opened:
-                hip.ipc_close(p, src_dev)
-    _fault("p2p")  # test hook (raises on the listed ranks after the copies)
+    try:
+        _fault("p2p")  # test hook: recorded like a real copy error, before the barrier
+    except RuntimeError as e:
+        err = err or e
     dist.barrier()
     return err
 
@@ -394,3 +425,13 @@ def gather_arrays(arr):
     out = [None] * dist.get_world_size()
     dist.all_gather_object(out, np.asarray(arr), group=cpu_group())
     return np.concatenate(out) if out else arr
+
+
+def gather_objects(obj):
+    """[obj of rank 0, obj of rank 1, ...] on every rank ([obj] without a process group)."""
+    dist = _dist()
+    if dist is None:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj, group=cpu_group())
+    return out
