@@ -12,6 +12,8 @@
 // Reference analog: none (the reference client runs no model; this serves the
 // `bert_large` perf_analyzer config of BASELINE.json).
 
+#include <algorithm>
+
 #include "kernels/common.h"
 
 namespace {
@@ -335,9 +337,41 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
     }
 }
 
+// bf16x3 operand of the fp32-parity bert mode: x fp32 [rows][K] -> out bf16
+// [rows][3K] = [hi | hi | lo] (hi = bf16_rne(x), lo = bf16_rne(x - hi)), so
+// ONE bf16 GEMM against W' = [W_hi | W_lo | W_hi] (K' = 3K) accumulates
+// x_hi W_hi + x_hi W_lo + x_lo W_hi in fp32: ~1e-5 of an fp32 GEMM at 3x the
+// bf16 MFMA work (gfx950 has no xf32, and its f32-input MFMA runs at 1/16 of
+// the bf16 rate).  One thread per 4 elements: a 16-B load, three 8-B stores.
+__global__ void __launch_bounds__(256) x3_cat_kernel(const float* __restrict__ x, uint16_t* __restrict__ out,
+                                                     long n4, int k4) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const long r = i / k4, c = i - r * k4;
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    const uint32_t h0 = pack2(v.x, v.y), h1 = pack2(v.z, v.w);
+    const uint32_t l0 = pack2(v.x - __uint_as_float(h0 << 16), v.y - __uint_as_float(h0 & 0xffff0000u));
+    const uint32_t l1 = pack2(v.z - __uint_as_float(h1 << 16), v.w - __uint_as_float(h1 & 0xffff0000u));
+    uint2* row = reinterpret_cast<uint2*>(out) + r * 3 * k4;  // 3 segments of k4 x 8 B
+    row[c] = make_uint2(h0, h1);
+    row[k4 + c] = make_uint2(h0, h1);
+    row[2 * k4 + c] = make_uint2(l0, l1);
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// fp32-parity bert: out bf16 [rows][3K] = [hi | hi | lo] of x fp32 [rows][K]
+// (K % 4 == 0, 16-B aligned x, 8-B aligned out)
+int tcamd_x3_cat(const float* x, void* out, int rows, int K, void* stream) {
+  if (rows <= 0) return hipSuccess;
+  if (!x || !out || K <= 0 || K % 4 || (uintptr_t)x % 16 || (uintptr_t)out % 8) return hipErrorInvalidValue;
+  const long n4 = (long)rows * (K / 4);
+  const int grid = (int)std::min<long>((n4 + 255) / 256, 256L * 16);
+  hipLaunchKernelGGL(x3_cat_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, (uint16_t*)out, n4, K / 4);
+  return hipGetLastError();
+}
 
 // out = LayerNorm(x + y) * gamma + beta over rows of H bf16 elements
 // (H in {512, 1024, 2048, 4096}); x, y, out, gamma, beta 16-B aligned; out may alias x or y.

@@ -44,11 +44,48 @@ def _proj(x, lin, epilogue="bias"):
     (profiles/r4_gemm_k15.md); config 4 is library-bound on these GEMMs."""
     x2 = x.reshape(-1, x.shape[-1])
     n = lin.weight.shape[0]
+    if getattr(lin, "w3", None) is not None and x2.is_cuda and x2.dtype == torch.float32:
+        y = _mm_x3(x2, lin.w3)
+        if epilogue != "none":
+            y += lin.bias
+        if epilogue == "bias_gelu":
+            y = F.gelu(y)
+        return y.view(*x.shape[:-1], n)
     if epilogue == "none":
         return torch.mm(x2, lin.weight.t()).view(*x.shape[:-1], n)
     if epilogue == "bias_gelu":
         return _linear_gelu(x, lin)
     return lin(x)
+
+
+def _mm_x3(x2, w3):
+    """fp32-parity GEMM: x2 fp32 [M, K] against w3 = [W_hi | W_lo | W_hi] bf16
+    [N, 3K] as ONE bf16 GEMM with fp32 output over [x_hi | x_hi | x_lo]
+    (csrc/kernels/bert.hip x3_cat): x_hi W_hi + x_hi W_lo + x_lo W_hi, ~1e-5
+    of an fp32 GEMM."""
+    from triton_client_amd.ops import hip
+
+    M, K = x2.shape
+    xc = torch.empty(M, 3 * K, device=x2.device, dtype=torch.bfloat16)
+    hip.x3_cat(x2.contiguous().data_ptr(), xc.data_ptr(), M, K, stream=torch.cuda.current_stream(x2.device).cuda_stream)
+    return torch.mm(xc, w3.t(), out_dtype=torch.float32)
+
+
+def prepare_x3(model):
+    """fp32-parity mode of an fp32 model: every projection of every layer gets
+    its bf16x3 weight w3 = [W_hi | W_lo | W_hi] (the fp32 weights stay for the
+    reference path); forward() on fp32 CUDA activations then runs those GEMMs
+    on the bf16 MFMA (3x the bf16 work instead of the 16x of f32-input MFMA)
+    and everything else (LayerNorm, GELU, softmax attention) in fp32."""
+    with torch.no_grad():
+        for layer in model.layers:
+            for lin in (layer.qkv, layer.out, layer.ffn1, layer.ffn2):
+                w = lin.weight.float()
+                hi = w.to(torch.bfloat16)
+                lo = (w - hi.float()).to(torch.bfloat16)
+                lin.w3 = torch.cat([hi, lo, hi], dim=1).contiguous()
+    model.precision = "fp32"
+    return model
 
 
 def _add_ln(x, y, ln):
@@ -118,7 +155,7 @@ class _Layer(nn.Module):
             qkv = _proj(x, self.qkv, "none")
             a = _attention(qkv, b, s, mask_i32, bias, qkv_bias=self.qkv.bias)
         else:
-            a = _attention(self.qkv(x), b, s, mask_i32, bias)
+            a = _attention(_proj(x, self.qkv), b, s, mask_i32, bias)
         x = _add_ln(x, _proj(a, self.out), self.ln1)
         return _add_ln(x, _proj(_proj(x, self.ffn1, "bias_gelu"), self.ffn2), self.ln2)
 

@@ -236,6 +236,7 @@ _SIGS = {
         ],
         ctypes.c_int,
     ),
+    "tcamd_x3_cat": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "tcamd_x3_stem": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
          ctypes.c_int, ctypes.c_void_p],
@@ -821,6 +822,13 @@ def x3_dense_fused3(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_l
     with the next chunk's 1x1 K steps interleaved into each tile's 3x3."""
     _check(_load().tcamd_x3_dense_fused3(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
                                          w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_fused3")
+
+
+def x3_cat(x, out, rows, K, stream=None):
+    """fp32-parity bert operand: x fp32 [rows][K] -> out bf16 [rows][3K] =
+    [hi | hi | lo] (csrc/kernels/bert.hip), for one bf16 GEMM against
+    [W_hi | W_lo | W_hi] that accumulates the three split products."""
+    _check(_load().tcamd_x3_cat(x, out, int(rows), int(K), _vp(stream)), "x3_cat")
 
 
 def x3_fused_stamps():

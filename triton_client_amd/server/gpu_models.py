@@ -539,12 +539,15 @@ class BertLarge(Model):
         torch.cuda.set_device(self.device_id)
         self.torch = torch
         dev = torch.device("cuda", self.device_id)
-        self.model = bert.build(device=dev, layers=self.layers)
+        self.model = self._build_model(bert, dev)
         # before the warm-up runs and graph captures below pick their GEMM solutions
         self.tuned_gemms = bert.use_tuned_gemms()
         for _ in range(max(1, self.instance_count)):
             self._slots.append(self._make_slot(dev))
         self._free = list(range(len(self._slots)))
+
+    def _build_model(self, bert, dev):
+        return bert.build(device=dev, layers=self.layers)
 
     def _make_slot(self, dev):
         torch = self.torch
@@ -757,4 +760,22 @@ class BertLarge(Model):
     reports_batch_stats = True
 
 
-GPU_MODELS = [DensenetOnnx, PreprocessInceptionEnsemble, BertLarge]
+class BertLargeFP32(BertLarge):
+    """``bert_large_fp32`` — the same BERT-large QA model (same seed, same
+    inputs and outputs) with fp32-parity compute, the way densenet_onnx has
+    one: fp32 weights and activations, every projection one bf16x3 GEMM on
+    the bf16 MFMA (models/bert.py prepare_x3: x_hi W_hi + x_hi W_lo + x_lo W_hi,
+    fp32 accumulate), LayerNorm / GELU / softmax attention in fp32.  Served
+    logits match an fp32 forward of the fp32 weights to ~1e-5
+    (tests/test_bert_accuracy_gpu.py); ~3x the bf16 model's GEMM work.  The
+    bf16 ``bert_large`` stays the config-4 serving default."""
+
+    name = "bert_large_fp32"
+
+    def _build_model(self, bert, dev):
+        import torch
+
+        return bert.prepare_x3(bert.build(device=dev, dtype=torch.float32, layers=self.layers))
+
+
+GPU_MODELS = [DensenetOnnx, PreprocessInceptionEnsemble, BertLarge, BertLargeFP32]
