@@ -235,27 +235,35 @@ class CodecPool {
   {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      if (th_.empty() && !stop_)
-        for (int i = 0; i < 2; ++i)
-          th_.emplace_back([this, i] {
-            pthread_setname_np(pthread_self(), ("tcs-codec" + std::to_string(i)).c_str());
-            Run();
-          });
-      q_.push_back(std::move(f));
+      if (!stop_) {
+        if (th_.empty())
+          for (int i = 0; i < 2; ++i)
+            th_.emplace_back([this, i] {
+              pthread_setname_np(pthread_self(), ("tcs-codec" + std::to_string(i)).c_str());
+              Run();
+            });
+        q_.push_back(std::move(f));
+        f = nullptr;
+      }
+    }
+    if (f) {
+      f();  // stopping: the pool no longer takes work, so the caller runs it (the connection still gets its reply)
+      return;
     }
     cv_.notify_one();
   }
-  // runs what is queued, then joins
+  // runs what is queued, then joins; later Submit()s run on their caller
   void Stop()
   {
+    std::vector<std::thread> th;
     {
       std::lock_guard<std::mutex> lk(mu_);
       stop_ = true;
+      th.swap(th_);  // under mu_: a concurrent Submit() sees either the running pool or stop_
     }
     cv_.notify_all();
-    for (auto& t : th_)
+    for (auto& t : th)
       if (t.joinable()) t.join();
-    th_.clear();
   }
 
  private:

@@ -58,6 +58,9 @@
 
 #include <mutex>
 
+#include <atomic>
+#include <cstdio>
+
 #include "kernels/common.h"
 
 using namespace tcamd;
@@ -1375,17 +1378,50 @@ extern "C" int tcamd_pack_bytes_strided(const void* data, uint64_t stride, const
 // counts and an illegal-address error that never showed with kernels and
 // copies serialised (AMD_SERIALIZE_KERNEL=3), and a fixed buffer takes the
 // pool's map / trim out of the picture.
+//
+// Overrun check (tcamd_k3_set_check(1), tests/test_bytes_k3_gpu.py): every
+// call allocates its workspace at EXACTLY the size it asks for, followed by a
+// 4 KiB canary filled with 0xA5 on the call's stream; after the call's final
+// sync the canary is read back, and a changed byte fails the call
+// (hipErrorUnknown + a message on stderr) instead of being absorbed by the
+// grow-only buffer's slack.
 constexpr int kIxMaxDev = 64;
 static std::mutex g_ix_mu;
 static void* g_ix_ws[kIxMaxDev] = {};
 static size_t g_ix_bytes[kIxMaxDev] = {};
 constexpr size_t kIxKeepMax = 256ull << 20;  // larger one-off workspaces are freed after the call
+constexpr size_t kIxCanary = 4096;
+static std::atomic<int> g_ix_check{0};
+static size_t g_ix_need[kIxMaxDev] = {};  // check mode: the exact size of the current workspace
 
 static hipError_t ix_workspace(hipStream_t s, size_t need, void** out) {
   int dev = 0;
   hipError_t e = hipStreamGetDevice(s, &dev);
   if (e != hipSuccess) return e;
   if (dev < 0 || dev >= kIxMaxDev) return hipErrorInvalidDevice;
+  if (g_ix_check.load(std::memory_order_relaxed)) {
+    // exact size + canary, re-allocated whenever the size changes
+    if (need != g_ix_need[dev] || !g_ix_ws[dev]) {
+      int prev = 0;
+      (void)hipGetDevice(&prev);
+      if (prev != dev) (void)hipSetDevice(dev);
+      if (g_ix_ws[dev]) (void)hipFree(g_ix_ws[dev]);
+      g_ix_ws[dev] = nullptr;
+      g_ix_bytes[dev] = 0;
+      e = hipMalloc(&g_ix_ws[dev], need + kIxCanary);
+      if (prev != dev) (void)hipSetDevice(prev);
+      if (e != hipSuccess) {
+        g_ix_ws[dev] = nullptr;
+        return e;
+      }
+      g_ix_bytes[dev] = need;
+      g_ix_need[dev] = need;
+    }
+    e = hipMemsetAsync((uint8_t*)g_ix_ws[dev] + need, 0xA5, kIxCanary, s);
+    if (e != hipSuccess) return e;
+    *out = g_ix_ws[dev];
+    return hipSuccess;
+  }
   if (need > g_ix_bytes[dev]) {
     int prev = 0;
     (void)hipGetDevice(&prev);
@@ -1412,6 +1448,7 @@ static void ix_workspace_trim(hipStream_t s) {
   int dev = 0;
   if (hipStreamGetDevice(s, &dev) != hipSuccess || dev < 0 || dev >= kIxMaxDev) return;
   if (g_ix_bytes[dev] <= kIxKeepMax) return;
+  g_ix_need[dev] = 0;
   int prev = 0;
   (void)hipGetDevice(&prev);
   if (prev != dev) (void)hipSetDevice(dev);
@@ -1420,6 +1457,8 @@ static void ix_workspace_trim(hipStream_t s) {
   g_ix_bytes[dev] = 0;
   if (prev != dev) (void)hipSetDevice(prev);
 }
+
+static hipError_t ix_canary_check(hipStream_t s);
 
 // Round-2 general path (every byte position a candidate; 10 B of tables per
 // input byte): only for chains the v3 walk cannot resolve.
@@ -1503,6 +1542,7 @@ static int index_v3(const uint8_t* buf, uint64_t nbytes, uint64_t window, uint64
   int hs[4] = {0, 0, 0, 0};
   if (e == hipSuccess) e = hipMemcpyAsync(hs, status, sizeof(hs), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess && g_ix_check.load(std::memory_order_relaxed)) e = ix_canary_check(s);  // walk + resolve + scan
   if (e == hipSuccess && (hs[0] == 0 || hs[0] == 1)) {
     hipLaunchKernelGGL(ix_emit, dim3(wg), dim3(kBlock), 0, s, buf, nbytes, nblk, entry, count, ctop, n_expected, offs,
                        lens, rec, rec_head);
@@ -1542,10 +1582,30 @@ extern "C" int tcamd_index_bytes(const void* buf, uint64_t nbytes, uint64_t n_ex
   std::lock_guard<std::mutex> lk(g_ix_mu);
   const int rc = index_locked(buf, nbytes, n_expected, offs, lens, status, s);
   // the workspace is free for the next call once this stream drained
-  const hipError_t f = hipStreamSynchronize(s);
+  hipError_t f = hipStreamSynchronize(s);
+  if (f == hipSuccess && rc == hipSuccess && g_ix_check.load(std::memory_order_relaxed)) f = ix_canary_check(s);
   ix_workspace_trim(s);
   return rc != hipSuccess ? rc : f;
 }
+
+// Check mode: the canary after the exact-size workspace must be intact.
+static hipError_t ix_canary_check(hipStream_t s) {
+  int dev = 0;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess || dev < 0 || dev >= kIxMaxDev || !g_ix_ws[dev]) return hipSuccess;
+  static thread_local uint8_t host[kIxCanary];
+  hipError_t e = hipMemcpy(host, (uint8_t*)g_ix_ws[dev] + g_ix_need[dev], kIxCanary, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  for (size_t i = 0; i < kIxCanary; ++i)
+    if (host[i] != 0xA5) {
+      fprintf(stderr, "tcamd_index_bytes: workspace overrun: byte %zu past the %zu-byte workspace was written\n", i,
+              g_ix_need[dev]);
+      return hipErrorUnknown;
+    }
+  return hipSuccess;
+}
+
+// Overrun check mode on / off (tests); returns the previous setting.
+extern "C" int tcamd_k3_set_check(int on) { return g_ix_check.exchange(on ? 1 : 0); }
 
 static int index_locked(const void* buf, uint64_t nbytes, uint64_t n_expected, uint64_t* offs, uint32_t* lens,
                         int* status, hipStream_t s) {

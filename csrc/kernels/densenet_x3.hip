@@ -1701,60 +1701,57 @@ struct X3SmallParams {
   const float* x;  // block buffer rows of ldx (the layer's first K channels)
   const float* s1;  // [K] BN1 affine
   const float* t1;
-  const uint16_t* w1_hi;  // [128][K] bf16 (BN2 folded, K8x layout): WR 0
-  const uint16_t* w1_lo;
-  const uint16_t* w1f_hi;  // [K/16][q 4][lane 64][8] bf16 (x3_w1_fragments): WR 1
+  const uint16_t* w1f_hi;  // [K/16][q 4][lane 64][8] bf16 (x3_w1_fragments, BN2 folded)
   const uint16_t* w1f_lo;
   const float* b1;        // [128] BN2 shift
   const uint16_t* w2_hi;  // [tap 9][kq 4][oh 2][lane 64][8] bf16 (x3_w3f_fragments)
   const uint16_t* w2_lo;
   float* y;               // [pixels][ldy] fp32, offset to the layer's 32-channel slice
   int ldx, K, ldy, imgs;
-  int dbg;                // ablation (TCAMD_X3_SMALLF_DBG): 1 = no 3x3 phase, 2 = X rows of image 0 only,
-                          // 4 = no 1x1 MFMAs, 8 = no W copies, 16 = no X conversion (results
-                          // invalid with 4 / 8 / 16), 64 = step timeline (block 0),
-                          // 128 = producer waves at s_setprio 1
+  int dbg;                // 1 = no 3x3 phase (timing ablation), 64 = step timeline (block 0)
   unsigned long long* stamps;  // TCAMD_X3_SMALLF_STAMP: per block [8] s_memrealtime (100 MHz) marks
 };
 
-// W = image side (14: half-image tiles, 7: whole images); PF = X K-steps in
-// the producers' registers.
-// WR = where the consumers' W1 operand comes from: 0 = LDS-DMA copies issued
-// by the producers into each K-step stage; 1 = the consumers load their own
-// fragments (x3_w1_fragments: 1 KB per wave load) from L2 into registers one K
-// step ahead.  The step timeline showed the producer last at every barrier,
-// ~40% of its step in issuing and waiting for the W copies, and those copies
-// plus the consumers' W reads are half the stage's LDS traffic
-// (TCAMD_X3_SMALLF_WREG).  (A variant with the stage filled two steps ahead
-// and the operands read one step ahead of the MFMAs measured no faster.)
-template <int W, int PF, int kSmS, int WR>
+// Tile geometry of T tiles per W x W image: tile t owns output rows
+// [tW/T, (t+1)W/T) and computes z over those rows plus one halo row on each
+// side that exists (the halo's 1x1 is recomputed by the neighbour tile).
+constexpr int x3s_zrows_max(int W, int T) {
+  int m = 0;
+  for (int t = 0; t < T; ++t) {
+    const int r0 = t * W / T, r1 = (t + 1) * W / T;
+    const int z0 = r0 > 0 ? r0 - 1 : 0, z1 = r1 < W ? r1 + 1 : W;
+    m = z1 - z0 > m ? z1 - z0 : m;
+  }
+  return m;
+}
+
+// W = image side (14 or 7); T = tiles per image.  More tiles per image give a
+// small batch more workgroups (bs64 at 14x14: 128 half-image tiles on 256
+// CUs) for the price of the recomputed halo rows.  PF = 3 X K-steps in the
+// producers' registers, 4 K-step stages, W1 loaded by the consumers.
+template <int W, int T>
 __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
+  constexpr int PF = 3, kSmS = 4;
   constexpr int kLdsSm = kSmS * kWsStage;
-  constexpr int kHalves = W == 14 ? 2 : 1;
-  constexpr int kRowsOut = W / kHalves;              // 7
+  constexpr int kRowsOut = (W + T - 1) / T;          // most output rows of a tile
   constexpr int kPW = W + 2, kPR = kRowsOut + 2;     // padded tile image
   constexpr int kNPad = kPR * kPW;
-  constexpr int kPOut = kRowsOut * W;                // 98 / 49 outputs
+  constexpr int kPOut = kRowsOut * W;                // most outputs of a tile
   constexpr int kNPG = (kPOut + 15) / 16;            // 16-pixel groups of the 3x3
-  constexpr int kTRMax = (kRowsOut + kHalves) * W;   // z pixels: 112 / 49
+  constexpr int kTRMax = x3s_zrows_max(W, T) * W;    // most z pixels of a tile
   constexpr int kNRI = (kTRMax + 31) / 32;           // producer row passes (32 rows each)
-  constexpr int kOps = (WR ? 0 : 4 + 2) + kNRI;      // vm ops per producer iteration
-  constexpr int kNB = (kTRMax + 31) / 32;            // 32-pixel blocks of the 1x1 tile: 4 / 2
+  constexpr int kOps = kNRI;                         // vm ops per producer iteration
+  constexpr int kNB = (kTRMax + 31) / 32;            // 32-pixel blocks of the 1x1 tile
   static_assert(kTRMax <= 128, "one 1x1 tile");
   static_assert(kNPad * kRowB + 2 * 4 * 3 * kNPG * 64 * 4 <= kLdsSm, "K14x LDS budget");
   extern __shared__ __attribute__((aligned(16))) uint8_t ldss[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-  // tile: the two halves of image 8g+j are blocks 16g+j and 16g+8+j (one XCD)
-  int img, half;
-  if constexpr (kHalves == 2) {
-    const int g = blockIdx.x >> 4, r = blockIdx.x & 15;
-    half = r >> 3;
-    img = 8 * g + (r & 7);
-  } else {
-    img = blockIdx.x;
-    half = 0;
-  }
+  // tile t of image 8g+j is block 8Tg + 8t + j: an image's tiles share
+  // blockIdx % 8, which the dispatcher maps to one XCD, so the halo rows'
+  // second read is an L2 hit (speed only, never correctness)
+  const int g8 = blockIdx.x / (8 * T), rr = blockIdx.x % (8 * T);
+  const int tile = rr >> 3, img = 8 * g8 + (rr & 7);
   if (img >= p.imgs) return;  // block-uniform, before any barrier
   // diagnostic marks (wave 0): [0] entry [1] after B0 [2] 1x1 done [3] z
   // handover [4] z complete [5] 3x3 MFMAs done [6] partials summed [7] exit
@@ -1763,71 +1760,48 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
     if (p.stamps) mk[i] = __builtin_amdgcn_s_memrealtime();
   };
   mark(0);
-  const int r0 = half * kRowsOut;
-  const int zr0 = max(r0 - 1, 0), zr1 = min(r0 + kRowsOut + 1, W);
+  const int r0 = tile * W / T, r1 = (tile + 1) * W / T;
+  const int zr0 = max(r0 - 1, 0), zr1 = min(r1 + 1, W);
   const int TR = (zr1 - zr0) * W;  // z rows of the tile
   const int mz0 = img * W * W + zr0 * W;
   const int nst = p.K / kBK;
   const int Q = nst, Qp = (Q + PF - 1) / PF * PF;
-  // timeline diagnostic (dbg 64, 4 stages, block 0): shader-clock time
-  // of producer wave 4 and consumer wave 0 reaching each step barrier, kept in
-  // LDS past the stages (no memory op inside the counted-wait loop)
-  const bool tl = (p.dbg & 64) && kSmS == 4 && blockIdx.x == 0;
+  // timeline diagnostic (dbg 64, block 0): shader-clock time of producer wave
+  // 4 and consumer wave 0 reaching each step barrier, kept in LDS past the
+  // stages (no memory op inside the counted-wait loop)
+  const bool tl = (p.dbg & 64) && blockIdx.x == 0;
   unsigned long long* const tls = reinterpret_cast<unsigned long long*>(ldss + kSmS * kWsStage);
   const unsigned long long tl0 = __builtin_amdgcn_s_memtime();
   // consumer wave = 32-channel quarter of the 1x1 output x every 32-pixel
-  // block: each W1 fragment is loaded by one wave only (a 2 x 2 split of the
-  // 128 x 128 tile loaded every fragment twice), for twice the X operand
-  // reads, which go to LDS (256 B/clk) instead of the vector-memory path
+  // block: each W1 fragment is loaded by one wave only, for twice the X
+  // operand reads, which go to LDS (256 B/clk) instead of the vector-memory path
   f32x16 acc[kNB];
   const int col = lane & 31, h = lane >> 5;
   const int rot = (int)(blockIdx.x % (unsigned)nst);  // blocks read different K offsets at a time
   auto kofs = [&](int ks) { ks += rot; return (ks >= nst ? ks - nst : ks) * kBK; };
-  // WR 1: BN1 affine s1 | t1 (2 x K floats) in stage 0's unused W planes
+  // BN1 affine s1 | t1 (2 x K floats) in stage 0's W planes (no W copies there)
   float* const bnl = reinterpret_cast<float*>(ldss + 2 * kWsPlane);
 
   if (wave >= 4) {
     // ------------------------------ producer (K8x ws) ------------------------------
-    const int pt = tid - 256, pw = wave - 4;
+    const int pt = tid - 256;
     const int pj = pt & 7, prow = pt >> 3;
-    const ptrdiff_t lo_off = p.w1_lo - p.w1_hi;
-    f32x4 xr[PF][kNRI], xs[PF], xt[PF];
-    // WR 1: the BN1 affine of every step after the first comes from the LDS
-    // copy the consumers make before B0 (two fewer 1 KB wave loads per step
-    // on the vector-memory path the consumers' fragment loads share)
+    f32x4 xr[PF][kNRI], xs, xt;
+    // the BN1 affine of step 0 from global memory, of every later step from the
+    // LDS copy the consumers make before B0
     auto issue_x = [&](int q, int slot) {
-      const bool st_ld = !WR || q == 0;
       q = min(q, Q - 1);
       const int k0 = kofs(q);
-      if (st_ld) {
-        xs[slot] = ldf4(p.s1 + k0 + 4 * pj);
-        xt[slot] = ldf4(p.t1 + k0 + 4 * pj);
-      }
 #pragma unroll
       for (int i = 0; i < kNRI; ++i) {
-        // ablation 2: every block reads image 0's rows (X L2-resident)
-        const int m = ((p.dbg & 2) ? zr0 * W : mz0) + min(prow + 32 * i, TR - 1);
+        const int m = mz0 + min(prow + 32 * i, TR - 1);
         xr[slot][i] = ldf4(p.x + (size_t)m * p.ldx + k0 + 4 * pj);
       }
     };
-    auto issue_w = [&](int q) {
-      if (WR || (p.dbg & 8)) return;  // WR 1: the consumers load W; ablation 8: no W copies
-      q = min(q, Q - 1);
-      const int k0 = kofs(q);
-      uint8_t* st = ldss + (q % kSmS) * kWsStage + 2 * kWsPlane;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ii = 4 * pw + i, plane = ii >> 3, rb = ii & 7;
-        const int row = 16 * rb + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 3);
-        const uint16_t* src = p.w1_hi + (plane ? lo_off : 0) + (size_t)row * p.K + k0 + 8 * c;
-        __builtin_amdgcn_global_load_lds((const void*)src, (void*)(st + plane * kWsPlane + rb * 1024), 16, 0, 0);
-      }
-    };
     auto write_x = [&](int q, int slot) {
-      if (p.dbg & 16) return;  // ablation 16: no X conversion / stage writes
       uint8_t* st = ldss + (q % kSmS) * kWsStage;
-      f32x4 sc = xs[slot], sb = xt[slot];
-      if (WR && q > 0) {
+      f32x4 sc = xs, sb = xt;
+      if (q > 0) {
         const int k0 = kofs(min(q, Q - 1)) + 4 * pj;
         sc = *reinterpret_cast<const f32x4*>(bnl + k0);
         sb = *reinterpret_cast<const f32x4*>(bnl + p.K + k0);
@@ -1838,22 +1812,19 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
         // are never written to the tile image, so they need no zeroing
         const int row = prow + 32 * i;
         const f32x4 v = bn_relu4(xr[slot][i], sc, sb);
-        v2u h, l;
-        split4(v, h, l);
+        v2u hh, ll;
+        split4(v, hh, ll);
         const int off = ws_chunk(row, pj >> 1) + (pj & 1) * 8;
-        *reinterpret_cast<v2u*>(st + off) = h;
-        *reinterpret_cast<v2u*>(st + kWsPlane + off) = l;
+        *reinterpret_cast<v2u*>(st + off) = hh;
+        *reinterpret_cast<v2u*>(st + kWsPlane + off) = ll;
       }
     };
-    // A/B (dbg 128): the producer waves (the younger half: they lose VALU
-    // issue arbitration to the consumers' MFMA stream) at s_setprio 1
-    if (p.dbg & 128) __builtin_amdgcn_s_setprio(1);
+    xs = ldf4(p.s1 + kofs(0) + 4 * pj);
+    xt = ldf4(p.t1 + kofs(0) + 4 * pj);
 #pragma unroll
     for (int s = 0; s < PF; ++s) issue_x(s, s);
-    for (int s = 0; s <= kSmS - 3; ++s) issue_w(s);
     __builtin_amdgcn_s_waitcnt(ws_vmcnt(0));
     write_x(0, 0);
-    issue_w(kSmS - 2);
     __builtin_amdgcn_sched_barrier(0);
     issue_x(PF, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1865,20 +1836,16 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
         const int slot = (u + 1) % PF;
         __builtin_amdgcn_s_waitcnt(ws_vmcnt(kOps * (PF - 1)));  // X of step q+1
         __builtin_amdgcn_sched_barrier(0);
-        if (tl && pw == 0 && lane == 0 && q < 32) tls[4 * q] = __builtin_amdgcn_s_memtime();
+        if (tl && wave == 4 && lane == 0 && q < 32) tls[4 * q] = __builtin_amdgcn_s_memtime();
         write_x(q + 1, slot);
-        if (tl && pw == 0 && lane == 0 && q < 32) {
+        if (tl && wave == 4 && lane == 0 && q < 32) {
           __builtin_amdgcn_s_waitcnt(0xc07f);  // the conversion's LDS writes done
           tls[4 * q + 1] = __builtin_amdgcn_s_memtime();
         }
-        issue_w(q + kSmS - 1);
-        __builtin_amdgcn_sched_barrier(0);  // W copies ahead of the X loads (vmcnt retires in order)
+        __builtin_amdgcn_sched_barrier(0);
         issue_x(q + 1 + PF, slot);
-        if constexpr (WR)
-          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this step's stage writes
-        else
-          __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0((2 + kNRI) + kOps * (kSmS - 2)));  // + W of step q+1
-        if (tl && pw == 0 && lane == 0 && q < 32)  // timeline: producer wave 4 at the barrier (LDS, no vm op)
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this step's stage writes
+        if (tl && wave == 4 && lane == 0 && q < 32)  // producer wave 4 at the barrier (LDS, no vm op)
           tls[4 * q + 2] = __builtin_amdgcn_s_memtime();
         ws_barrier();  // B(q+1)
       }
@@ -1907,17 +1874,8 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
           o.l[kk][b] = ld16(st + kWsPlane + xo);
         }
     };
-    auto rd_a = [&](int q, AOps& o) {  // WR 0: from the stage
-      const uint8_t* st = ldss + (q % kSmS) * kWsStage;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int wo = ws_chunk(32 * wave + col, 2 * kk + h);
-        o.h[kk] = ld16(st + 2 * kWsPlane + wo);
-        o.l[kk] = ld16(st + 3 * kWsPlane + wo);
-      }
-    };
-    // WR 1: this wave's fragments from L2 (1 KB per wave load) as buffer
-    // loads: a lane-constant VGPR offset and the step's offset in an SGPR
+    // this wave's W1 fragments from L2 (1 KB per wave load) as buffer loads: a
+    // lane-constant VGPR offset and the step's offset in an SGPR
     const auto w1h = __builtin_amdgcn_make_buffer_rsrc((void*)p.w1f_hi, (short)0, p.K * 256, 0x00020000);
     const auto w1l = __builtin_amdgcn_make_buffer_rsrc((void*)p.w1f_lo, (short)0, p.K * 256, 0x00020000);
     auto ld_a = [&](int q, AOps& o) {
@@ -1936,61 +1894,42 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
         for (int b = 0; b < kNB; ++b)
           if (32 * b < TR) acc[b] = x3_32(A.h[kk], A.l[kk], B.h[kk][b], B.l[kk][b], acc[b]);
     };
-    const bool live = !(p.dbg & 4);  // ablation 4: no MFMAs / stage reads
     auto stamp_c = [&](int q) {
       if (tl && wave == 0 && lane == 0 && q < 32) tls[4 * q + 3] = __builtin_amdgcn_s_memtime();
     };
-    if constexpr (!WR) {
-      ws_barrier();  // B0
-      mark(1);
-      for (int q = 0; q < Qp; ++q) {
-        if (q < Q && live) {
-          AOps A;
-          BOps B;
-          rd_b(q, B);
-          rd_a(q, A);
-          mma(A, B);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        stamp_c(q);
-        ws_barrier();  // B(q+1): stage q is free
+    // W of step q is loaded during step q-1 (two register sets, the loop
+    // unrolled by 2 so each has a fixed name); the step's counted wait leaves
+    // the next step's 4 fragment loads in flight.  The prefetch is
+    // unconditional (past the last step it reloads that step's fragments):
+    // with a conditional one the compiler's own waits before the MFMAs assume
+    // the no-prefetch path and drain it.
+    constexpr int kAOps = 4;
+    // the producers' BN1 affine for steps >= 1 (published by B0)
+    for (int i = tid; i < p.K / 4; i += 256) {
+      *reinterpret_cast<f32x4*>(bnl + 4 * i) = ldf4(p.s1 + 4 * i);
+      *reinterpret_cast<f32x4*>(bnl + p.K + 4 * i) = ldf4(p.t1 + 4 * i);
+    }
+    AOps fa, fb;
+    ld_a(0, fa);  // lands during the producers' prologue
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the copy is in LDS
+    ws_barrier();  // B0
+    mark(1);
+    auto step = [&](int q, const AOps& cur, AOps& nxt) {
+      ld_a(q + 1, nxt);
+      if (q < Q) {
+        BOps B;
+        rd_b(q, B);
+        __builtin_amdgcn_s_waitcnt(ws_vmcnt(kAOps));  // this step's fragments
+        mma(cur, B);
       }
-    } else {
-      // W of step q is loaded during step q-1 (two register sets, the loop
-      // unrolled by 2 so each has a fixed name); the step's counted wait
-      // leaves the next step's kNA x 4 fragment loads in flight
-      // The prefetch is unconditional (past the last step it reloads that
-      // step's fragments): with a conditional one the compiler's own waits
-      // before the MFMAs assume the no-prefetch path and drain it (so the
-      // dbg 4 ablation does not apply here).
-      constexpr int kAOps = 4;
-      // the producers' BN1 affine for steps >= 1 (published by B0)
-      for (int i = tid; i < p.K / 4; i += 256) {
-        *reinterpret_cast<f32x4*>(bnl + 4 * i) = ldf4(p.s1 + 4 * i);
-        *reinterpret_cast<f32x4*>(bnl + p.K + 4 * i) = ldf4(p.t1 + 4 * i);
-      }
-      AOps fa, fb;
-      ld_a(0, fa);  // lands during the producers' prologue
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the copy is in LDS
-      ws_barrier();  // B0
-      mark(1);
-      auto step = [&](int q, const AOps& cur, AOps& nxt) {
-        ld_a(q + 1, nxt);
-        if (q < Q) {
-          BOps B;
-          rd_b(q, B);
-          __builtin_amdgcn_s_waitcnt(ws_vmcnt(kAOps));  // this step's fragments
-          mma(cur, B);
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-        stamp_c(q);
-        ws_barrier();  // B(q+1)
-      };
-      for (int q = 0; q < Qp; q += 2) {
-        step(q, fa, fb);
-        if (q + 1 >= Qp) break;
-        step(q + 1, fb, fa);
-      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      stamp_c(q);
+      ws_barrier();  // B(q+1)
+    };
+    for (int q = 0; q < Qp; q += 2) {
+      step(q, fa, fb);
+      if (q + 1 >= Qp) break;
+      step(q + 1, fb, fa);
     }
   }
   mark(2);
@@ -2010,10 +1949,8 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
     w2h[t] = ld16(p.w2_hi + off);
     w2l[t] = ld16(p.w2_lo + off);
   }
-  // Bz: every DMA and stage read retired (vmcnt retires in order: the 18
-  // weight loads just issued are younger than the producers' last DMA and X
-  // loads), the LDS holds z from here; raw barrier, so the weight loads stay
-  // in flight across it (a __syncthreads would drain them)
+  // Bz: every stage read retired, the LDS holds z from here; raw barrier, so
+  // the weight loads stay in flight across it (a __syncthreads would drain them)
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0(2 * kTaps));
   ws_barrier();
@@ -2055,6 +1992,7 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
   __syncthreads();  // z and its padding complete
   mark(4);
   if (p.dbg & 1) return;
+  const int nout = (r1 - r0) * W;  // this tile's outputs (the last tile may have fewer rows)
   int base[kNPG];
 #pragma unroll
   for (int pg = 0; pg < kNPG; ++pg) {
@@ -2062,7 +2000,7 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
     const int yy = o / W, xx = o - (o / W) * W;
     // padded (yy, xx) is tap (0, 0) of output (yy, xx); lanes past the tile
     // read from pixel 0 (in bounds; their columns are never stored)
-    base[pg] = o < kPOut ? yy * kPW + xx : 0;
+    base[pg] = o < nout ? yy * kPW + xx : 0;
   }
   f32x4 acc3[kNPG];
 #pragma unroll
@@ -2109,7 +2047,7 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
 #pragma unroll
       for (int src = 0; src < 3; ++src) v += *reinterpret_cast<const f32x4*>(sr + src * kSlot + pg * 64);
       const int o = 16 * pg + (lane & 15);
-      if (o < kPOut) *reinterpret_cast<f32x4*>(p.y + (size_t)(m0 + o) * p.ldy + 16 * oh + 4 * kq) = v;
+      if (o < nout) *reinterpret_cast<f32x4*>(p.y + (size_t)(m0 + o) * p.ldy + 16 * oh + 4 * kq) = v;
     }
   }
   mark(6);
@@ -2131,50 +2069,9 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
   }
 }
 
-template <int W, int PF, int kSmS, int WR>
+template <int W, int T>
 __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p) {
-  x3_small_body<W, PF, kSmS, WR>(p);
-}
-
-// K16x: every layer of the 7x7 dense block in ONE launch.  A block owns one
-// image through all its layers (at 7x7 a K14x tile is the whole image, so
-// layer l+1 reads only what this block wrote in layer l: no cross-block
-// dependency); between layers the block's y stores complete and the LDS is
-// reused.  Saves per layer the launch, the wait for the slowest of the 128
-// blocks and its idle CUs.  Layer l+1's input channels [K_l, K_l + 32) were
-// never read by this CU before layer l wrote them (they sit in their own
-// 128-B lines), so no L1 line can be stale.
-struct X3SmallLayer {
-  const float* s1;
-  const float* t1;
-  const uint16_t* w1_hi;   // K8x layout (unused by WR 1, kept for the params)
-  const uint16_t* w1_lo;
-  const uint16_t* w1f_hi;  // x3_w1_fragments
-  const uint16_t* w1f_lo;
-  const float* b1;
-  const uint16_t* w2_hi;   // x3_w3f_fragments
-  const uint16_t* w2_lo;
-  int K, pad;
-};
-
-__global__ void __launch_bounds__(512, 1) x3_dense_block7_kernel(X3SmallParams p, const X3SmallLayer* __restrict__ L,
-                                                               int nl) {
-  for (int l = 0; l < nl; ++l) {
-    X3SmallParams q = p;
-    q.s1 = L[l].s1;
-    q.t1 = L[l].t1;
-    q.w1_hi = L[l].w1_hi;
-    q.w1_lo = L[l].w1_lo;
-    q.w1f_hi = L[l].w1f_hi;
-    q.w1f_lo = L[l].w1f_lo;
-    q.b1 = L[l].b1;
-    q.w2_hi = L[l].w2_hi;
-    q.w2_lo = L[l].w2_lo;
-    q.K = L[l].K;
-    q.y = const_cast<float*>(p.x) + L[l].K;
-    x3_small_body<7, 3, 4, 1>(q);
-    __syncthreads();  // this layer's y stores done (release) before the next layer reads them
-  }
+  x3_small_body<W, T>(p);
 }
 
 // ============================================================================
@@ -2921,27 +2818,43 @@ int tcamd_x3_small_stamps(unsigned long long* out, int n) {
   return g_x3s_stamp_blocks;
 }
 
-// K14x: one dense layer of the 14x14 (half-image tiles) or 7x7 (whole-image
-// tiles) block in one kernel; w1 in the K8x [128][K] layout, w2 in
-// x3_w3f_fragments.  K a multiple of 32 (>= 64).
+static int cu_count();
+
+// Tiles per image K14x uses for imgs images of side W when the caller passes
+// tiles <= 0: the fewest (least halo recompute) that give every CU a
+// workgroup; 14x14: 2 (half images) or 4, 7x7: 1 (whole images), 2 or 4.
+int tcamd_x3_small_tiles(int imgs, int W) {
+  const int ncu = cu_count();
+  const int opts14[2] = {2, 4}, opts7[3] = {1, 2, 4};
+  const int* o = W == 14 ? opts14 : opts7;
+  const int n = W == 14 ? 2 : 3;
+  for (int i = 0; i < n; ++i)
+    if ((imgs + 7) / 8 * 8 * o[i] >= ncu) return o[i];
+  return o[n - 1];
+}
+
+// K14x: one dense layer of the 14x14 or 7x7 block in one kernel, `tiles`
+// tiles per image (14x14: 2 or 4, 7x7: 1, 2 or 4; <= 0: the chip-filling
+// default above); w1 in x3_w1_fragments, w2 in x3_w3f_fragments.  K a
+// multiple of 32 in 64..2048.
 int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K, const float* s1, const float* t1,
-                         const void* w1_hi, const void* w1_lo, const void* w1f_hi, const void* w1f_lo,
-                         const float* b1, const void* w2_hi, const void* w2_lo, float* y, int ldy, void* stream) {
+                         const void* w1f_hi, const void* w1f_lo, const float* b1, const void* w2_hi,
+                         const void* w2_lo, float* y, int ldy, int tiles, void* stream) {
   if (imgs <= 0) return hipSuccess;
-  if ((W != 14 && W != 7) || H != W || K < 64 || K % 32 || ldx < K || ldx % 4 || ldy % 4)
+  if ((W != 14 && W != 7) || H != W || K < 64 || K > 2048 || K % 32 || ldx < K || ldx % 4 || ldy % 4)
     return hipErrorInvalidValue;
-  if (!x || !s1 || !t1 || !w1_hi || !w1_lo || !b1 || !w2_hi || !w2_lo || !y) return hipErrorInvalidValue;
-  if (!aligned16(x) || !aligned16(s1) || !aligned16(t1) || !aligned16(w1_hi) || !aligned16(w1_lo) ||
+  if (!x || !s1 || !t1 || !w1f_hi || !w1f_lo || !b1 || !w2_hi || !w2_lo || !y) return hipErrorInvalidValue;
+  if (!aligned16(x) || !aligned16(s1) || !aligned16(t1) || !aligned16(w1f_hi) || !aligned16(w1f_lo) ||
       !aligned16(b1) || !aligned16(w2_hi) || !aligned16(w2_lo) || !aligned16(y))
     return hipErrorInvalidValue;
   if ((size_t)imgs * H * W >= (1u << 30) / 4) return hipErrorInvalidValue;
-  if ((!w1f_hi) != (!w1f_lo) || (w1f_hi && (!aligned16(w1f_hi) || !aligned16(w1f_lo)))) return hipErrorInvalidValue;
+  if (tiles <= 0) tiles = tcamd_x3_small_tiles(imgs, W);
+  const int ti = tiles == 1 ? 0 : tiles == 2 ? 1 : tiles == 4 ? 2 : -1;
+  if (ti < 0 || (W == 14 && ti == 0)) return hipErrorInvalidValue;
   X3SmallParams p;
   p.x = x;
   p.s1 = s1;
   p.t1 = t1;
-  p.w1_hi = (const uint16_t*)w1_hi;
-  p.w1_lo = (const uint16_t*)w1_lo;
   p.w1f_hi = (const uint16_t*)w1f_hi;
   p.w1f_lo = (const uint16_t*)w1f_lo;
   p.b1 = b1;
@@ -2961,79 +2874,33 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
       return hipErrorOutOfMemory;
     p.stamps = g_x3s_stamps;
   }
-  // X steps in flight in the producers' registers (TCAMD_X3_SMALLF_PF 3 or 6)
-  // and K-step stages (TCAMD_X3_SMALLF_STAGES 4 or 5), for A/B runs
-  static const int pf = getenv("TCAMD_X3_SMALLF_PF") ? atoi(getenv("TCAMD_X3_SMALLF_PF")) : 3;
-  static const int ns = getenv("TCAMD_X3_SMALLF_STAGES") ? atoi(getenv("TCAMD_X3_SMALLF_STAGES")) : 4;
-  // W1 for the consumers (TCAMD_X3_SMALLF_WREG, default 1): from their own
-  // register loads of the fragments when the caller passed them, else by the
-  // producers' LDS-DMA copies
-  static const int wreg = getenv("TCAMD_X3_SMALLF_WREG") ? atoi(getenv("TCAMD_X3_SMALLF_WREG")) : 1;
-  const int wr = wreg && w1f_hi && K <= 2048 ? 1 : 0;  // WR 1 keeps the BN1 affine (8 K bytes) in 16 KB of LDS
-#define X3S_FN(HW, PF_, NS_)                                                                    \
-  {(const void*)x3_dense_small_kernel<HW, PF_, NS_, 0>, (const void*)x3_dense_small_kernel<HW, PF_, NS_, 1>}
-  // [14x14 / 7x7][PF 3 / 6][4 / 5 stages][W1 by DMA / by consumer loads]
-  const void* const fns[2][2][2][2] = {{{X3S_FN(14, 3, 4), X3S_FN(14, 3, 5)}, {X3S_FN(14, 6, 4), X3S_FN(14, 6, 5)}},
-                                       {{X3S_FN(7, 3, 4), X3S_FN(7, 3, 5)}, {X3S_FN(7, 6, 4), X3S_FN(7, 6, 5)}}};
-#undef X3S_FN
+  // [14x14 / 7x7][1 / 2 / 4 tiles per image]
+  const void* const fns[2][3] = {
+      {nullptr, (const void*)x3_dense_small_kernel<14, 2>, (const void*)x3_dense_small_kernel<14, 4>},
+      {(const void*)x3_dense_small_kernel<7, 1>, (const void*)x3_dense_small_kernel<7, 2>,
+       (const void*)x3_dense_small_kernel<7, 4>}};
+  constexpr int kLds = 4 * kWsStage + 1024;  // 4 K-step stages + the dbg-64 timeline
   static std::atomic<bool> attr_set[kMaxDevices];
   const int dev_slot = device_slot();
   if (!attr_set[dev_slot].load(std::memory_order_acquire)) {
-    for (int w = 0; w < 2; ++w)
-      for (int f = 0; f < 2; ++f)
-        for (int n = 0; n < 2; ++n)
-          for (int l = 0; l < 2; ++l) {
-            const hipError_t e =
-                hipFuncSetAttribute(fns[w][f][n][l], hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (4 + n) * kWsStage + (n ? 0 : 1024));
-            if (e != hipSuccess) return e;
-          }
+    for (const auto& row : fns)
+      for (const void* f : row) {
+        if (!f) continue;
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+        if (e != hipSuccess) return e;
+      }
     attr_set[dev_slot].store(true, std::memory_order_release);
   }
-  const int blocks = W == 14 ? (imgs + 7) / 8 * 16 : imgs;
+  const int blocks = (imgs + 7) / 8 * 8 * tiles;
   if (stamp && blocks > 4096) return hipErrorInvalidValue;
   g_x3s_stamp_blocks = blocks;
   void* args[] = {&p};
-  const int n5 = ns == 5 ? 1 : 0;
-  const hipError_t e = hipLaunchKernel(fns[W == 14 ? 0 : 1][pf == 6 ? 1 : 0][n5][wr], dim3(blocks),
-                                       dim3(512), args,
-                                       (4 + n5) * kWsStage + ((dbg & 64) && !n5 ? 1024 : 0), (hipStream_t)stream);
-  if (e != hipSuccess) return e;
-  return hipGetLastError();
-}
-
-// K16x: nl layers of the 7x7 block in one launch.  layers: device array of
-// X3SmallLayer (K, BN1 affine, W1 fragments, BN2 shift, W2 fragments per
-// layer; K multiple of 32, 64 <= K <= 2048, growing by 32 per layer so layer
-// l writes channels [K_l, K_l + 32) of the block buffer x).
-int tcamd_x3_dense_block7(float* x, int ldx, int imgs, const void* layers, int nl, void* stream) {
-  if (imgs <= 0 || nl <= 0) return hipSuccess;
-  if (!x || !layers || ldx % 4 || !aligned16(x) || !aligned16(layers)) return hipErrorInvalidValue;
-  if ((size_t)imgs * 49 >= (1u << 30) / 4) return hipErrorInvalidValue;
-  X3SmallParams p = {};
-  p.x = x;
-  p.ldx = ldx;
-  p.ldy = ldx;
-  p.imgs = imgs;
-  p.dbg = 0;
-  p.stamps = nullptr;
-  static std::atomic<bool> attr_set[kMaxDevices];
-  const int dev_slot = device_slot();
-  if (!attr_set[dev_slot].load(std::memory_order_acquire)) {
-    const hipError_t e = hipFuncSetAttribute((const void*)x3_dense_block7_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kWsStage);
-    if (e != hipSuccess) return e;
-    attr_set[dev_slot].store(true, std::memory_order_release);
-  }
-  const X3SmallLayer* L = (const X3SmallLayer*)layers;
-  void* args[] = {&p, &L, &nl};
-  const hipError_t e = hipLaunchKernel((const void*)x3_dense_block7_kernel, dim3(imgs), dim3(512), args, 4 * kWsStage,
+  const hipError_t e = hipLaunchKernel(fns[W == 14 ? 0 : 1][ti], dim3(blocks), dim3(512), args, kLds,
                                        (hipStream_t)stream);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 
-int tcamd_x3_small_layer_bytes() { return (int)sizeof(X3SmallLayer); }
 
 static int cu_count() {
   static std::atomic<int> ncu_dev[kMaxDevices];

@@ -314,18 +314,19 @@ def test_x3_dense_fused(imgs, H, K, version):
 @pytest.mark.parametrize("imgs,H,K", [(1, 14, 64), (3, 14, 256), (8, 14, 288), (9, 14, 992), (17, 14, 640),
                                       (128, 14, 512), (16, 14, 96), (1, 7, 512), (5, 7, 992), (64, 7, 768),
                                       (130, 7, 544), (2, 7, 64), (40, 14, 416)])
-@pytest.mark.parametrize("wfrag", [True, False])
-def test_x3_dense_small(imgs, H, K, wfrag):
-    """K14x: the whole dense layer of a 14x14 (half-image tiles with a halo
-    row) or 7x7 (whole-image tiles) block in one kernel, z in a zero-padded
-    LDS image of the tile.  Ragged image counts (not multiples of 8: the 14x14
-    grid pairs the halves of images 8g+j), K from 64 to 992 (2..31 K steps,
-    every padding-round count of both producer depths) and a layer slice in
-    the middle of a wider block buffer.  Against fp64 torch (< 3e-5), and
-    against the two-kernel path on the same split products.  wfrag: the 1x1
-    consumers load their W1 fragments themselves (default engine path) or
-    read the producers' LDS copies."""
+@pytest.mark.parametrize("tiles", [1, 2, 4])
+def test_x3_dense_small(imgs, H, K, tiles):
+    """K14x: the whole dense layer of a 14x14 or 7x7 block in one kernel over
+    row tiles of the images (tiles per image: 14x14 2 or 4, 7x7 1, 2 or 4;
+    every tile recomputes the 1x1 of its halo rows), z in a zero-padded LDS
+    image of the tile.  Ragged image counts (not multiples of 8: the grid
+    groups the tiles of images 8g+j), uneven tiles (14 rows in 4 tiles, 7 in 2
+    or 4), K from 64 to 992 (2..31 K steps) and a layer slice in the middle of
+    a wider block buffer.  Against fp64 torch (< 3e-5, and per image), and
+    against the two-kernel path on the same split products."""
     _need_gpu()
+    if H == 14 and tiles == 1:
+        pytest.skip("14x14 takes 2 or 4 tiles per image")
     hip = _hip()
     g = torch.Generator(device=DEV).manual_seed(imgs * 131 + H * 7 + K)
     M, ldx = imgs * H * H, K + 96
@@ -338,19 +339,20 @@ def test_x3_dense_small(imgs, H, K, wfrag):
     w1h, w1l = _split(w1)
     w2p = _split(w2.permute(0, 2, 3, 1).reshape(32, -1))
     f2h, f2l = (hip.x3_w3f_fragments(u) for u in w2p)
-    f1 = [hip.x3_w1_fragments(u) for u in (w1h, w1l)] if wfrag else None
+    f1h, f1l = (hip.x3_w1_fragments(u) for u in (w1h, w1l))
     xc = x.clone()
-    hip.x3_dense_small(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), w1h.data_ptr(), w1l.data_ptr(),
+    hip.x3_dense_small(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), f1h.data_ptr(), f1l.data_ptr(),
                        b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), x.data_ptr() + 4 * K, ldx, stream=_st(),
-                       w1f_hi=f1[0].data_ptr() if f1 else None, w1f_lo=f1[1].data_ptr() if f1 else None)
+                       tiles=tiles)
     torch.cuda.synchronize()
     a = torch.relu(xc[:, :K].double() * s.double() + t.double())
     z = torch.relu(a @ w1.double().t() + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
     ref = F.conv2d(z, w2.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 32)
     err = _rel(x[:, K:K + 32], ref)
-    # per image too: a tile written to the wrong image / half shows even when the total is close
+    # per image too: a tile written to the wrong image / rows shows even when the total is close
     per_img = ((x[:, K:K + 32].double() - ref).reshape(imgs, -1).norm(dim=1) / ref.reshape(imgs, -1).norm(dim=1))
-    print("K14x imgs %d H %d K %d: rel %.3g, worst image %.3g" % (imgs, H, K, err, per_img.max().item()))
+    print("K14x imgs %d H %d K %d tiles %d: rel %.3g, worst image %.3g" % (imgs, H, K, tiles, err,
+                                                                         per_img.max().item()))
     assert err < 3e-5 and per_img.max().item() < 1e-4
     assert torch.equal(x[:, :K], xc[:, :K]) and torch.equal(x[:, K + 32:], xc[:, K + 32:])
     y2 = xc.clone()
@@ -364,103 +366,17 @@ def test_x3_dense_small(imgs, H, K, wfrag):
     assert _rel(x[:, K:K + 32], y2[:, K:K + 32]) < 2e-5
 
 
-@pytest.mark.parametrize("imgs,K0,nl", [(1, 64, 3), (37, 512, 16), (130, 96, 5)])
-def test_x3_dense_block7(imgs, K0, nl):
-    """K16x: ``nl`` 7x7 dense layers in ONE persistent launch (each workgroup
-    takes an image through every layer, each layer reading the channels the
-    previous ones wrote) against ``nl`` K14x launches on the same weights
-    (bit-equal: the same body), and the last layer against fp64 torch."""
+def test_x3_small_tiles_fill_the_chip():
+    """The default tiling: the fewest tiles per image that give every CU a workgroup."""
     _need_gpu()
     hip = _hip()
-    g = torch.Generator(device=DEV).manual_seed(imgs * 17 + K0 + nl)
-    H, M, ldx = 7, imgs * 49, K0 + 32 * nl
-    x = torch.zeros(M, ldx, device=DEV)
-    x[:, :K0] = torch.randn(M, K0, device=DEV, generator=g)
-    layers, P = [], []
-    for j in range(nl):
-        K = K0 + 32 * j
-        s = torch.rand(K, device=DEV, generator=g) + 0.5
-        t = torch.randn(K, device=DEV, generator=g) * 0.2
-        w1 = torch.randn(128, K, device=DEV, generator=g) / K ** 0.5
-        b1 = torch.randn(128, device=DEV, generator=g) * 0.1
-        w2 = torch.randn(32, 128, 3, 3, device=DEV, generator=g) / (9 * 128) ** 0.5
-        w1h, w1l = _split(w1)
-        f1h, f1l = (hip.x3_w1_fragments(u) for u in (w1h, w1l))
-        f2h, f2l = (hip.x3_w3f_fragments(u) for u in _split(w2.permute(0, 2, 3, 1).reshape(32, -1)))
-        P.append((K, s, t, w1, b1, w2, w1h, w1l, f1h, f1l, f2h, f2l))
-        layers.append({"s1": s.data_ptr(), "t1": t.data_ptr(), "w1_hi": w1h.data_ptr(), "w1_lo": w1l.data_ptr(),
-                       "w1f_hi": f1h.data_ptr(), "w1f_lo": f1l.data_ptr(), "b1": b1.data_ptr(),
-                       "w2_hi": f2h.data_ptr(), "w2_lo": f2l.data_ptr(), "K": K})
-    tab = torch.from_numpy(hip.x3_small_layer_table(layers)).to(DEV)
-    y = x.clone()
-    hip.x3_dense_block7(y.data_ptr(), ldx, imgs, tab.data_ptr(), nl, stream=_st())
-    ref = x.clone()
-    for K, s, t, w1, b1, w2, w1h, w1l, f1h, f1l, f2h, f2l in P:
-        hip.x3_dense_small(ref.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), w1h.data_ptr(),
-                           w1l.data_ptr(), b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), ref.data_ptr() + 4 * K, ldx,
-                           stream=_st(), w1f_hi=f1h.data_ptr(), w1f_lo=f1l.data_ptr())
-    torch.cuda.synchronize()
-    K, s, t, w1, b1, w2 = P[-1][:6]
-    a = torch.relu(y[:, :K].double() * s.double() + t.double())
-    z = torch.relu(a @ w1.double().t() + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
-    r64 = F.conv2d(z, w2.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 32)
-    err = _rel(y[:, K:], r64)
-    print("K16x imgs %d K0 %d layers %d: last layer rel %.3g, equal to K14x %s" % (
-        imgs, K0, nl, err, torch.equal(y, ref)))
-    assert err < 3e-5
-    assert torch.equal(y, ref)
-
-
-@pytest.mark.parametrize("pf,stages,wreg", [("6", "4", "1"), ("3", "5", "1"), ("6", "5", "1"), ("6", "4", "0"),
-                                            ("3", "5", "0"), ("6", "5", "0")])
-def test_x3_dense_small_variants(pf, stages, wreg):
-    """K14x's A/B variants (TCAMD_X3_SMALLF_PF: X steps in the producers'
-    registers; TCAMD_X3_SMALLF_STAGES: K-step stages, 5 = 160 KB of LDS;
-    TCAMD_X3_SMALLF_WREG: W1 by consumer fragment loads or producer LDS
-    copies), chosen
-    once per process, so in a child process: the same fp64 comparison as
-    test_x3_dense_small on shapes that cover every padding-round count."""
-    _need_gpu()
-    import os
-    import subprocess
-    import sys
-
-    code = r'''
-import torch, torch.nn.functional as F
-from triton_client_amd.ops import hip
-st = torch.cuda.current_stream().cuda_stream
-def split(t):
-    h = t.to(torch.bfloat16)
-    return h.contiguous(), (t - h.float()).to(torch.bfloat16).contiguous()
-for imgs, H, K in [(3, 14, 256), (9, 14, 992), (17, 14, 640), (16, 14, 96), (5, 7, 992), (2, 7, 64), (40, 14, 416)]:
-    g = torch.Generator(device="cuda").manual_seed(imgs * 131 + H * 7 + K)
-    M, ldx = imgs * H * H, K + 96
-    x = torch.randn(M, ldx, device="cuda", generator=g)
-    s = torch.rand(K, device="cuda", generator=g) + 0.5
-    t = torch.randn(K, device="cuda", generator=g) * 0.2
-    w1 = torch.randn(128, K, device="cuda", generator=g) / K ** 0.5
-    b1 = torch.randn(128, device="cuda", generator=g) * 0.1
-    w2 = torch.randn(32, 128, 3, 3, device="cuda", generator=g) / (9 * 128) ** 0.5
-    w1h, w1l = split(w1)
-    f2h, f2l = (hip.x3_w3f_fragments(u) for u in split(w2.permute(0, 2, 3, 1).reshape(32, -1)))
-    f1h, f1l = hip.x3_w1_fragments(w1h), hip.x3_w1_fragments(w1l)
-    xc = x.clone()
-    hip.x3_dense_small(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), w1h.data_ptr(), w1l.data_ptr(),
-                       b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), x.data_ptr() + 4 * K, ldx, stream=st,
-                       w1f_hi=f1h.data_ptr(), w1f_lo=f1l.data_ptr())
-    torch.cuda.synchronize()
-    a = torch.relu(xc[:, :K].double() * s.double() + t.double())
-    z = torch.relu(a @ w1.double().t() + b1.double()).reshape(imgs, H, H, 128).permute(0, 3, 1, 2)
-    ref = F.conv2d(z, w2.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 32)
-    err = ((x[:, K:K + 32].double() - ref).norm() / ref.norm()).item()
-    assert err < 3e-5, (imgs, H, K, err)
-    assert torch.equal(x[:, :K], xc[:, :K]) and torch.equal(x[:, K + 32:], xc[:, K + 32:])
-print("K14X_VARIANT_OK")
-'''
-    env = dict(os.environ, TCAMD_X3_SMALLF_PF=pf, TCAMD_X3_SMALLF_STAGES=stages, TCAMD_X3_SMALLF_WREG=wreg)
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=110)
-    assert r.returncode == 0 and "K14X_VARIANT_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    for imgs in (1, 8, 32, 64, 128, 256):
+        for W, opts in ((14, (2, 4)), (7, (1, 2, 4))):
+            t = hip.x3_small_tiles(imgs, W)
+            assert t in opts
+            fill = [o for o in opts if (imgs + 7) // 8 * 8 * o >= ncu]
+            assert t == (fill[0] if fill else opts[-1]), (imgs, W, t)
 
 
 def test_x3_dense_small_rejects_bad_shapes():
@@ -468,10 +384,12 @@ def test_x3_dense_small_rejects_bad_shapes():
     hip = _hip()
     x = torch.zeros(2 * 196, 320, device=DEV)
     w = torch.zeros(128 * 256, device=DEV)
-    for H, W, K in [(28, 28, 256), (14, 7, 256), (14, 14, 250), (14, 14, 32)]:
+    for H, W, K, tiles in [(28, 28, 256, 0), (14, 7, 256, 0), (14, 14, 250, 0), (14, 14, 32, 0), (14, 14, 256, 1),
+                           (7, 7, 256, 3), (14, 14, 256, 8), (7, 7, 2080, 0)]:
         with pytest.raises(Exception):
             hip.x3_dense_small(x.data_ptr(), 320, 2, H, W, K, w.data_ptr(), w.data_ptr(), w.data_ptr(), w.data_ptr(),
-                               w.data_ptr(), w.data_ptr(), w.data_ptr(), x.data_ptr() + 4 * K, 320, stream=_st())
+                               w.data_ptr(), w.data_ptr(), w.data_ptr(), x.data_ptr() + 4 * K, 320, stream=_st(),
+                               tiles=tiles)
 
 
 @pytest.mark.parametrize("imgs", [3, 20])  # 20: more tiles than the persistent grid (several per block)
@@ -540,8 +458,9 @@ def test_fp32_engine_matches_fp32_module(fp32_engine, b):
 @pytest.mark.parametrize("b", [3, 9, 24])
 def test_fp32_engine_k14x_blocks_match_fp32_module(fp32_engine, b):
     """The engine with K14x forced on for the 14x14 and 7x7 blocks at every
-    batch (ragged image counts: the 14x14 grid pairs images 8g+j), against the
-    fp32 module, and against the same engine with K14x off."""
+    batch (ragged image counts: the grid groups the tiles of images 8g+j; at
+    these batches the default tiling is 4 tiles per image), against the fp32
+    module, and against the same engine with K14x off."""
     eng, model = fp32_engine
     g = torch.Generator(device=DEV).manual_seed(300 + b)
     x = torch.randn(b, 3, 224, 224, device=DEV, generator=g)

@@ -477,3 +477,92 @@ def test_oversized_content_length_gets_413(cpu_server):
             data += chunk
         s.close()
         assert data.startswith(b"HTTP/1.1 413"), data[:200]
+
+
+def _read_http_responses(s, n):
+    """n HTTP/1.1 responses (Content-Length framed) from socket s, in arrival order."""
+    data, out = b"", []
+    while len(out) < n:
+        while b"\r\n\r\n" not in data:
+            chunk = s.recv(65536)
+            assert chunk, "connection closed after %d responses" % len(out)
+            data += chunk
+        head, rest = data.split(b"\r\n\r\n", 1)
+        hdrs = {ln.split(b":", 1)[0].strip().lower(): ln.split(b":", 1)[1].strip()
+                for ln in head.split(b"\r\n")[1:] if b":" in ln}
+        clen = int(hdrs.get(b"content-length", b"0"))
+        while len(rest) < clen:
+            chunk = s.recv(65536)
+            assert chunk
+            rest += chunk
+        out.append((head.split(b"\r\n")[0], hdrs, rest[:clen]))
+        data = rest[clen:]
+    return out
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_http_large_gzip_infer_on_codec_pool_keeps_pipeline_order(cpu_server, native):
+    """A compressed KServe REST infer body >= 64 KiB is inflated on tcserve's
+    codec pool (not the loop thread), then served natively (binary tensor) or
+    relayed to the Python server as the original compressed request (JSON
+    tensor: the relay-fallback path).  A small identity-encoded infer and a
+    /live GET pipelined behind it on the same keep-alive connection must come
+    back after it, in order, and the inflated / native / proxied counters move
+    accordingly."""
+    import gzip
+
+    nf = cpu_server.server.native_frontend
+    host, port = cpu_server.http_url.split(":")
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((1, 3, 224, 224)).astype(np.float32)
+    if native:
+        hdr = json.dumps({"inputs": [{"name": "data_0", "shape": [1, 3, 224, 224], "datatype": "FP32",
+                                      "parameters": {"binary_data_size": x.nbytes}}],
+                          "parameters": {"binary_data_output": True}}).encode()
+        plain = hdr + x.tobytes()
+    else:
+        hdr = json.dumps({"inputs": [{"name": "data_0", "shape": [1, 3, 224, 224], "datatype": "FP32",
+                                      "data": [round(float(v), 3) for v in x.ravel()]}],
+                          "outputs": [{"name": "fc6_1", "parameters": {"binary_data": False}}]}).encode()
+        plain = hdr
+    z = gzip.compress(plain)
+    assert len(z) >= 64 * 1024
+    big = (b"POST /v2/models/frontend_sink/infer HTTP/1.1\r\nHost: x\r\nContent-Encoding: gzip\r\n"
+           b"Inference-Header-Content-Length: %d\r\nContent-Length: %d\r\n\r\n" % (len(hdr), len(z))) + z
+    a = np.arange(16, dtype=np.int32)
+    shdr = json.dumps({"inputs": [{"name": n, "shape": [1, 16], "datatype": "INT32",
+                                   "parameters": {"binary_data_size": 64}} for n in ("INPUT0", "INPUT1")],
+                       "parameters": {"binary_data_output": True}}).encode()
+    sbody = shdr + a.tobytes() + (3 * a).tobytes()
+    small = (b"POST /v2/models/add_sub_batched/infer HTTP/1.1\r\nHost: x\r\nInference-Header-Content-Length: %d\r\n"
+             b"Content-Length: %d\r\n\r\n" % (len(shdr), len(sbody))) + sbody
+    live = b"GET /v2/health/live HTTP/1.1\r\nHost: x\r\n\r\n"
+    before = nf.counters()
+    s = socket.create_connection((host, int(port)))
+    try:
+        s.sendall(big + small + live)
+        (st1, h1, b1), (st2, h2, b2), (st3, _, _) = _read_http_responses(s, 3)
+        # the connection stays open for another request (keep-alive)
+        s.sendall(live)
+        (st4, _, _), = _read_http_responses(s, 1)
+    finally:
+        s.close()
+    assert st1.startswith(b"HTTP/1.1 200") and st2.startswith(b"HTTP/1.1 200"), (st1, b1[:200], st2)
+    assert st3.startswith(b"HTTP/1.1 200") and st4.startswith(b"HTTP/1.1 200")
+    # response 1: frontend_sink broadcasts the first input value
+    if native:
+        jl = int(h1[b"inference-header-content-length"])
+        out = np.frombuffer(b1[jl:], dtype=np.float32)
+        np.testing.assert_array_equal(out, np.full(1000, x.ravel()[0], np.float32))
+    else:
+        out = json.loads(b1)["outputs"][0]["data"]
+        np.testing.assert_allclose(out, np.full(1000, round(float(x.ravel()[0]), 3)), rtol=1e-6)
+    # response 2: the pipelined add_sub infer, after the big one
+    jl2 = int(h2[b"inference-header-content-length"])
+    meta = json.loads(b2[:jl2])
+    assert meta["model_name"] == "add_sub_batched"
+    np.testing.assert_array_equal(np.frombuffer(b2[jl2:jl2 + 64], dtype=np.int32), 4 * a)
+    after = nf.counters()
+    assert after["inflated_requests"] == before["inflated_requests"] + 1
+    assert after["native_requests"] == before["native_requests"] + (2 if native else 1)
+    assert after["proxied_calls"] >= before["proxied_calls"] + (2 if native else 3)

@@ -133,6 +133,15 @@ def main():
                                          "--concurrency-range", "64", "-p", "500", "-r", "3", "-s", "80"]),
         ("perf batcher rules shm c32", [pa, "-m", "add_sub_pipelined", "-i", "grpc", "-u", grpc, "--shared-memory",
                                         "system", "--concurrency-range", "32", "-p", "400", "-r", "3", "-s", "80"]),
+        # compressed REST: 600 KB frontend_sink bodies gzip to > 64 KiB, so every
+        # request is inflated on the codec pool and its response deflated there,
+        # 8 connections at once (the pool's Submit / Run / Stop paths)
+        ("perf HTTP gzip >64KiB codec pool c8", [pa, "-m", "frontend_sink", "-i", "http", "-u", http,
+                                                 "--compression-algorithm", "gzip", "--concurrency-range", "8", "-p",
+                                                 "400", "-r", "3", "-s", "80"]),
+        ("perf HTTP deflate >64KiB codec pool c4", [pa, "-m", "frontend_sink", "-i", "http", "-u", http,
+                                                    "--compression-algorithm", "deflate", "--concurrency-range", "4",
+                                                    "-p", "300", "-r", "3", "-s", "80"]),
     ]
     for ex in ("simple_http_infer_client", "simple_grpc_infer_client", "simple_http_shm_client",
                "simple_grpc_shm_client", "simple_grpc_async_infer_client", "simple_http_async_infer_client",

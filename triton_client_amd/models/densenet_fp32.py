@@ -24,9 +24,10 @@ Network walk (same as :class:`densenet_fused.FusedDenseNet`, fp32 activations):
                         produced into the 3x3's LDS ring (never in HBM)
                         or, small M (<= 3136 pixels, W <= 63): the K13x chain,
                         one launch per layer (csrc/kernels/densenet_x3s.hip)
-                        or (14x14 / 7x7 blocks at big batches): K14x, one
-                        launch per layer over half-image / whole-image tiles,
-                        z in a zero-padded LDS image of the tile
+                        or (14x14 / 7x7 blocks from ~16-32 images): K14x, one
+                        launch per layer over row tiles of the images (2-4
+                        per image, halo rows recomputed), z in a zero-padded
+                        LDS image of the tile
    -> per transition:   K8x conv1x1 with BN+ReLU+2x2 avg-pool prologue
                         -> next block buffer ch[0 : C/2] (fp32)
    -> K10x head: relu(BN5(x)) global average -> [b,1024] fp32
@@ -132,22 +133,11 @@ class FusedDenseNetFP32:
         self.chain_m = int(os.environ.get("TCAMD_X3_CHAIN_M", "3136"))
         self.chain_after_fused = os.environ.get("TCAMD_X3_CHAIN_AFTER_FUSED", "0") != "0"
         # K14x (whole dense layer in one kernel at 14x14 / 7x7) once it has at
-        # least this many blocks (a 14x14 image is two blocks, a 7x7 image one);
-        # 0 disables it
+        # least this many workgroups (row tiles of the images, 2-4 per 14x14
+        # image, 1-4 per 7x7 image: x3_small_tiles); 0 disables it
         self.smallf_min_blocks = int(os.environ.get("TCAMD_X3_SMALLF_MIN_BLOCKS", "128"))
-        # K16x: the K14x 7x7 block as ONE persistent launch (every layer of an
-        # image in one workgroup), TCAMD_X3_BLOCK7=1; off by default: measured no
-        # faster than 16 launches (profiles/r4_k16x_block7.md)
-        self.block7_tab = None
-        if os.environ.get("TCAMD_X3_BLOCK7", "0") != "0":
-            for bi, layers in enumerate(self.blocks):
-                if self.block_dims[bi][0] == 7 and all(L["cin"] <= 2048 for L in layers):
-                    tab = hip.x3_small_layer_table([{
-                        "s1": L["s1"].data_ptr(), "t1": L["t1"].data_ptr(), "w1_hi": L["w1h"].data_ptr(),
-                        "w1_lo": L["w1l"].data_ptr(), "w1f_hi": L["w1fh"].data_ptr(), "w1f_lo": L["w1fl"].data_ptr(),
-                        "b1": L["b1"].data_ptr(), "w2_hi": L["w2fh"].data_ptr(), "w2_lo": L["w2fl"].data_ptr(),
-                        "K": L["cin"]} for L in layers])
-                    self.block7_tab = (bi, torch.from_numpy(tab).to(dev))
+        # tiles per image for K14x: 0 = the library's chip-filling choice
+        self.smallf_tiles = int(os.environ.get("TCAMD_X3_SMALLF_TILES", "0"))
         self._alloc(max_batch)
 
     def _alloc(self, n):
@@ -234,14 +224,11 @@ class FusedDenseNetFP32:
             small = 0 < M <= self.small_m and M <= self.zacc.shape[1]
             if self._small_fused(b, hw):
                 # K14x: the 14x14 / 7x7 blocks, one launch per layer, z on chip
-                if self.block7_tab is not None and self.block7_tab[0] == bi:
-                    hip.x3_dense_block7(fp, ctot, b, self.block7_tab[1].data_ptr(), len(layers), stream=st)
-                    layers = ()
                 for L in layers:
                     hip.x3_dense_small(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
-                                       L["w1h"].data_ptr(), L["w1l"].data_ptr(), L["b1"].data_ptr(),
+                                       L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(),
                                        L["w2fh"].data_ptr(), L["w2fl"].data_ptr(), fp + 4 * L["cin"], ctot, stream=st,
-                                       w1f_hi=L["w1fh"].data_ptr(), w1f_lo=L["w1fl"].data_ptr())
+                                       tiles=self.smallf_tiles)
                 self._transition(bi, fp, ctot, b, hw, ws, wsb, st)
                 continue
             ch = self.chain[bi]
@@ -315,7 +302,8 @@ class FusedDenseNetFP32:
     def _small_fused(self, b, hw):
         if self.smallf_min_blocks <= 0 or hw not in (7, 14):
             return False
-        return b * (2 if hw == 14 else 1) >= self.smallf_min_blocks
+        tiles = self.smallf_tiles or hip.x3_small_tiles(b, hw)
+        return (b + 7) // 8 * 8 * tiles >= self.smallf_min_blocks
 
     def _fuse_max_k(self, M):
         """Largest K that K11x takes: past 224 only at >= 4 tiles per block, where

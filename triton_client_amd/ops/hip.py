@@ -218,14 +218,12 @@ _SIGS = {
         [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
         ],
         ctypes.c_int,
     ),
+    "tcamd_x3_small_tiles": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "tcamd_x3_fused_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
-    "tcamd_x3_dense_block7": (
-        [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
-    "tcamd_x3_small_layer_bytes": ([], ctypes.c_int),
     "tcamd_x3_small_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "tcamd_x3_small_timeline": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "tcamd_x3_dense_fused3": (
@@ -236,6 +234,7 @@ _SIGS = {
         ],
         ctypes.c_int,
     ),
+    "tcamd_k3_set_check": ([ctypes.c_int], ctypes.c_int),
     "tcamd_x3_cat": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "tcamd_x3_stem": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
@@ -753,46 +752,20 @@ def x3_dense_fused(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo
                                         w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_fused")
 
 
-def x3_dense_small(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None,
-                   w1f_hi=None, w1f_lo=None):
-    """K14x: one fp32-parity dense layer of the 14x14 (half-image tiles + one
-    halo row) or 7x7 (whole-image tiles) block in ONE kernel, z kept in a
-    zero-padded LDS image of the tile.  ``w1_*`` in the K8x [128][K] layout,
-    ``w2_*`` in x3_w3f_fragments; K a multiple of 32, >= 64.  With
-    ``w1f_*`` (x3_w1_fragments of the same W1) the 1x1 consumers load their
-    W1 operand themselves instead of from the producers' LDS copies."""
-    _check(_load().tcamd_x3_dense_small(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo,
-                                        _vp(w1f_hi), _vp(w1f_lo), b1, w2_hi, w2_lo, y, int(ldy), _vp(stream)),
-           "x3_dense_small")
+def x3_dense_small(x, ldx, imgs, H, W, K, s1, t1, w1f_hi, w1f_lo, b1, w2_hi, w2_lo, y, ldy, stream=None, tiles=0):
+    """K14x: one fp32-parity dense layer of the 14x14 or 7x7 block in ONE
+    kernel, ``tiles`` row tiles per image (each with the halo rows its 3x3
+    needs, recomputed; 14x14: 2 or 4, 7x7: 1, 2 or 4; 0 = the fewest that give
+    every CU a workgroup, :func:`x3_small_tiles`), z kept in a zero-padded LDS
+    image of the tile.  ``w1f_*`` in x3_w1_fragments, ``w2_*`` in
+    x3_w3f_fragments; K a multiple of 32 in 64..2048."""
+    _check(_load().tcamd_x3_dense_small(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1f_hi, w1f_lo, b1,
+                                        w2_hi, w2_lo, y, int(ldy), int(tiles), _vp(stream)), "x3_dense_small")
 
 
-_X3_LAYER_DTYPE = np.dtype([("s1", "<u8"), ("t1", "<u8"), ("w1_hi", "<u8"), ("w1_lo", "<u8"), ("w1f_hi", "<u8"),
-                             ("w1f_lo", "<u8"), ("b1", "<u8"), ("w2_hi", "<u8"), ("w2_lo", "<u8"), ("K", "<i4"),
-                             ("pad", "<i4")])
-
-
-def x3_small_layer_table(layers):
-    """Host bytes of the K16x layer table: one X3SmallLayer per dict with
-    device pointers s1, t1, w1_hi, w1_lo, w1f_hi, w1f_lo, b1, w2_hi, w2_lo
-    (x3_w3f_fragments) and K.  Copy it to the device and pass its address to
-    :func:`x3_dense_block7`."""
-    if _X3_LAYER_DTYPE.itemsize != int(_load().tcamd_x3_small_layer_bytes()):
-        raise HipError(-1, "X3SmallLayer size mismatch")
-    t = np.zeros(len(layers), dtype=_X3_LAYER_DTYPE)
-    for i, L in enumerate(layers):
-        for k in _X3_LAYER_DTYPE.names:
-            if k != "pad":
-                t[k][i] = int(L[k])
-    return t.view(np.uint8)
-
-
-def x3_dense_block7(x, ldx, imgs, table, nl, stream=None):
-    """K16x: ``nl`` dense layers of the 7x7 block in ONE launch (one block per
-    image through every layer); ``table`` = device copy of
-    :func:`x3_small_layer_table`.  Same results as ``nl`` K14x launches
-    (W1 by consumer loads, PF 3, 4 stages)."""
-    _check(_load().tcamd_x3_dense_block7(_vp(x), int(ldx), int(imgs), _vp(table), int(nl), _vp(stream)),
-           "x3_dense_block7")
+def x3_small_tiles(imgs, W):
+    """The tiles per image K14x picks for ``imgs`` images of side ``W``."""
+    return int(_load().tcamd_x3_small_tiles(int(imgs), int(W)))
 
 
 def x3_small_timeline():
@@ -911,6 +884,13 @@ def index_bytes_last_path():
     w = ctypes.c_uint64(0)
     p = _load().tcamd_index_bytes_last_path(ctypes.byref(w))
     return p, w.value
+
+
+def k3_set_check(on):
+    """K3 overrun check mode (process-wide): each index_bytes call allocates its
+    workspace at exactly the size it needs with a 4 KiB canary behind it and
+    fails if the canary changed.  Returns the previous setting."""
+    return bool(_load().tcamd_k3_set_check(1 if on else 0))
 
 
 def index_bytes(buf_ptr, nbytes, n_expected, offs_ptr, lens_ptr, status_ptr, stream=None):
