@@ -462,8 +462,19 @@ def main():
         points.append(p1)
         n1 = 16 * args.bs1_concurrency
         p1.run(n1 // 4)
+        s10, b10 = p1.s.server_stats(), batch_stats(client, model)
         l1, e1, el1 = measure(p1, 4, n1 // 4)
+        s11, b11 = p1.s.server_stats(), batch_stats(client, model)
         bs1 = {"concurrency": args.bs1_concurrency, "infer_per_sec": round(world * n1 / el1, 1)}
+        # where a bs=1 request's latency goes at this concurrency: rows per
+        # batch, queueing, and the request-weighted device time of its batch
+        bd64 = stats_delta(s10, s11)
+        bd64["client_overhead_us_per_request"] = round(float(np.mean(l1)) / 1e3 - bd64["server_us_per_request"], 1)
+        wc1 = weighted_compute_us(b10, b11, 1)
+        bd64["compute_us_per_request_weighted"] = round(wc1, 1)
+        bd64["unattributed_us_per_request"] = round(
+            bd64["server_us_per_request"] - bd64["queue_us_per_request"] - wc1, 1)
+        bs1["breakdown_rank0"] = bd64
         l1g = fanout.gather_arrays(l1.astype(np.int64)).astype(np.float64)
         bs1.update({"p50_latency_us": round(percentile_us(l1g, 50), 1),
                     "p99_latency_us": round(percentile_us(l1g, 99), 1)})

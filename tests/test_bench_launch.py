@@ -48,6 +48,7 @@ def test_bench_spawns_ranks_and_aggregates(gpus):
                                                    res["window_p99_latency_us_rank0"]))
     assert len(res["placement"]) == gpus and all(p["applied"] is (gpus > 1) for p in res["placement"])
     assert res["bs1"]["infer_per_sec"] > 0
+    assert res["bs1"]["breakdown_rank0"]["avg_rows_per_batch"] >= 1
     if gpus > 1:
         assert "spawning %d ranks" % gpus in err
         assert "fanned out by gloo" in res["data"]
