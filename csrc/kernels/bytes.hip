@@ -62,6 +62,7 @@
 #include <cstdio>
 
 #include "kernels/common.h"
+#include "kernels/knobs.h"
 
 using namespace tcamd;
 
@@ -1342,14 +1343,12 @@ static int pack_impl(const void* data, uint64_t stride, const uint32_t* lens, ui
   hipLaunchKernelGGL(scan2_top, dim3(1), dim3(kBlock), 0, s, ta, tb, nc);
   // persistent grid over the parts (~20 KiB LDS per workgroup: 7 per CU)
   const uint64_t grid = nb < 1792 ? nb : 1792;
-  static const bool legacy = getenv("TCAMD_PK_LEGACY") && atoi(getenv("TCAMD_PK_LEGACY"));
-  if (stride || legacy) {
+  if (stride) {
     hipLaunchKernelGGL(pk_emit, dim3((unsigned)grid), dim3(kBlock), 0, s, (const uint8_t*)data, stride, lens, n, nb, S,
                        ta, parts, tb, (uint8_t*)out);
   } else {
     // blocks whose output passes big_lim take the 64-bit byte path (tests lower it)
-    static const uint64_t big_lim =
-        getenv("TCAMD_PK_BIG_LIM") ? strtoull(getenv("TCAMD_PK_BIG_LIM"), nullptr, 10) : ((1ull << 31) - (1ull << 20));
+    const uint64_t big_lim = (uint64_t)tcamd::knob(tcamd::Knob::PkBigLim);
     hipLaunchKernelGGL(pk_emit_packed, dim3((unsigned)grid), dim3(kBlock), 0, s, (const uint8_t*)data, lens, n, nb, S,
                        ta, parts, tb, (uint8_t*)out, big_lim);
   }
@@ -1609,7 +1608,7 @@ extern "C" int tcamd_k3_set_check(int on) { return g_ix_check.exchange(on ? 1 : 
 
 static int index_locked(const void* buf, uint64_t nbytes, uint64_t n_expected, uint64_t* offs, uint32_t* lens,
                         int* status, hipStream_t s) {
-  static const int mode = getenv("TCAMD_K3_MODE") ? atoi(getenv("TCAMD_K3_MODE")) : 0;  // 1: general path only
+  const int mode = (int)tcamd::knob(tcamd::Knob::K3Mode);  // 1: general path only
   if (mode != 1) {
     uint64_t need = 64 * n_expected;
     if (need < (1u << 20)) need = 1u << 20;

@@ -43,6 +43,7 @@
 #include <cstdlib>
 
 #include "kernels/common.h"
+#include "kernels/knobs.h"
 
 // Host-side per-device caches (CU count, dynamic-LDS opt-ins): indexed by the
 // current HIP device, clamped into the table.
@@ -1692,10 +1693,8 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused3_kernel(X3FusedParams p
 //   summed through an LDS scratch, fp32 stores of the layer's 32 channels.
 //
 // HBM per layer: the input X once (+ the halo rows through L2) and 32 output
-// channels; one launch.  LDS: 4 K-step stages (128 KB), then z + scratch.
-// K-step stages (kSmS below): 4 (128 KB) or 5 (160 KB: the W copies one more
-// step ahead; TCAMD_X3_SMALLF_STAGES); z and the 3x3 scratch alias them once
-// the 1x1 drained
+// channels; one launch.  LDS: 4 K-step stages (128 KB); z and the 3x3
+// scratch alias them once the 1x1 drained.
 
 struct X3SmallParams {
   const float* x;  // block buffer rows of ldx (the layer's first K channels)
@@ -2079,15 +2078,15 @@ __global__ void __launch_bounds__(512, 1) x3_dense_small_kernel(X3SmallParams p)
 // ============================================================================
 // As K10s in densenet.hip (patch staged once per block, conv as an implicit
 // GEMM on v_mfma_f32_32x32x16 with weights [64][kh 7][kw 8][ch 4] as operand
-// A), with the patch split into hi/lo planes, the weights' hi/lo fragments in
-// registers, and the conv tile kept in fp32 for the max-pool.
+// A), with the patch split into hi/lo planes and the weights' hi/lo fragments
+// in registers; the 3x3/2 max-pool runs on the conv rows in registers.
+// (A conv tile in LDS and a one-block-per-tile grid were the v1 / v2 of
+// round 2: both slower than the persistent kernel below, removed in round 5.)
 constexpr int kSPR = 4, kSPC = 14;       // pooled outputs per block
 constexpr int kSCR = 2 * kSPR + 1;       // 9 conv rows
-constexpr int kSCC = 32;                 // conv cols computed (2*PC+1 = 29 used)
 constexpr int kSIR = 2 * kSCR + 5;       // 23 input rows
 constexpr int kSIC = 72;                 // input cols
 constexpr int kSK = 7 * 32;              // (kh, kw[8], ch[4])
-constexpr int kSOS = 64 + 4;             // conv-tile pixel stride (fp32)
 constexpr int kSHin = 224, kSHo = 56;
 
 struct X3StemParams {
@@ -2248,65 +2247,6 @@ __device__ __forceinline__ void x3_stem_pool_tile(const X3StemParams& p, const u
   }
 }
 
-template <bool V2>
-__global__ void __launch_bounds__(256) x3_stem_kernel(X3StemParams p) {
-  __shared__ __attribute__((aligned(16))) uint16_t Ih[kSIR * kSIC * 4];  // 13.2 KB
-  __shared__ __attribute__((aligned(16))) uint16_t Il[kSIR * kSIC * 4];
-  __shared__ __attribute__((aligned(16))) float Cv[V2 ? 4 : kSCR * kSCC * kSOS];   // v1: 78 KB conv tile
-  __shared__ __attribute__((aligned(16))) float sb[64];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int img = blockIdx.z, pr0 = blockIdx.y * kSPR, pc0 = blockIdx.x * kSPC;
-  if (tid < 16) *reinterpret_cast<f32x4*>(sb + 4 * tid) = ldf4(p.bias + 4 * tid);
-  {
-    float v[kStage][3];
-    x3_stem_load(p.srcs[img], pr0, pc0, tid, v);
-    x3_stem_stage(Ih, Il, tid, v);
-  }
-  // wave = (channel half nh) x (conv-row group mg)
-  const int nh = wave & 1, mg = wave >> 1;
-  v4u wh[kSK / 16], wl[kSK / 16];
-  x3_stem_weights(p, lane, nh, wh, wl);
-  __syncthreads();
-  if constexpr (V2) {
-    // v2: no conv tile in LDS (26 KB per block: several blocks per CU, so
-    // one block's staging overlaps another's MFMAs)
-    x3_stem_pool_tile(p, Ih, Il, sb, wh, wl, img, pr0, pc0, lane, wave);
-    return;
-  }
-  const int jj = lane & 31, hh = lane >> 5;
-  const int r_lo = mg ? 5 : 0, r_hi = mg ? kSCR : 5;
-  for (int cr = r_lo; cr < r_hi; ++cr) {
-    const f32x16 acc = x3_stem_conv_row(Ih, Il, wh, wl, cr, lane);
-    float* cp = &Cv[(cr * kSCC + jj) * kSOS + nh * 32 + 4 * hh];
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-      *reinterpret_cast<f32x4*>(cp + 8 * g) = f32x4{acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
-  }
-  __syncthreads();
-  for (int t = tid; t < kSPR * kSPC * 16; t += 256) {
-    const int cc = t & 15, px = t >> 4;  // 4-channel chunk, pooled pixel
-    const int a = px / kSPC, b = px - a * kSPC;
-    const int pr = pr0 + a, pc = pc0 + b;
-    f32x4 mx = f32x4{-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy) {
-      if (2 * pr - 1 + dy < 0) continue;
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        if (2 * pc - 1 + dx < 0) continue;
-        const f32x4 f = *reinterpret_cast<const f32x4*>(&Cv[((2 * a + dy) * kSCC + 2 * b + dx) * kSOS + cc * 4]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) mx[e] = fmaxf(mx[e], f[e]);
-      }
-    }
-    const f32x4 bb = ldf4(p.bias + cc * 4);
-    f32x4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = fmaxf(mx[e] + bb[e], 0.f);
-    *reinterpret_cast<f32x4*>(p.y + (((size_t)img * kSHo + pr) * kSHo + pc) * p.ldy + cc * 4) = o;
-  }
-}
-
 // K10x stem v3: persistent.  A block loads its waves' weight fragments once
 // and walks tiles t = blockIdx.x, +gridDim.x, ...; the next tile's input
 // patch is loaded into registers while the current tile's conv rows run on
@@ -2412,26 +2352,18 @@ X3Plan x3_plan(int M, int K, int N) {
   const int big = ((M + 127) / 128) * nt;
   const int mid = ((M + 63) / 64) * nt;
   pl.bm = big >= 384 ? 128 : (mid >= 256 ? 64 : 32);
-  static const int force_bm = [] {  // A/B knob for tools/x3_kbench.py
-    const char* e = getenv("TCAMD_X3_BM");
-    return e ? atoi(e) : 0;
-  }();
+  const int force_bm = (int)tcamd::knob(tcamd::Knob::X3Bm);  // A/B knob for tools/x3_kbench.py
   if (force_bm == 32 || force_bm == 64 || force_bm == 128) pl.bm = force_bm;
   pl.tiles = ((M + pl.bm - 1) / pl.bm) * nt;
   pl.splits = 1;
   pl.k_per_split = K;
-  static const int splitk_below = [] {  // A/B knob: split-K when fewer tiles than this
-    const char* e = getenv("TCAMD_X3_SPLITK_BELOW");
-    return e ? atoi(e) : 192;
-  }();
-  // split-K cap: the 3x3 that follows re-reads every split's partials of its
-  // band, so more splits trade 1x1 parallelism for 3x3 staging.  4 measured
-  // best (bs1 1.005 -> 0.975 ms, bs8 1.166 -> 1.082 ms vs uncapped, 8-16
-  // splits; profiles/r3_splitk_cap.log); TCAMD_X3_MAX_SPLITS overrides
-  static const int max_splits = [] {
-    const char* e = getenv("TCAMD_X3_MAX_SPLITS");
-    return e ? std::max(1, atoi(e)) : 4;
-  }();
+  // split-K when fewer tiles than TCAMD_X3_SPLITK_BELOW (192).  The cap: the
+  // 3x3 that follows re-reads every split's partials of its band, so more
+  // splits trade 1x1 parallelism for 3x3 staging.  4 measured best (bs1
+  // 1.005 -> 0.975 ms, bs8 1.166 -> 1.082 ms vs uncapped, 8-16 splits;
+  // profiles/r3_splitk_cap.log); TCAMD_X3_MAX_SPLITS overrides
+  const int splitk_below = (int)tcamd::knob(tcamd::Knob::X3SplitkBelow);
+  const int max_splits = std::max(1, (int)tcamd::knob(tcamd::Knob::X3MaxSplits));
   if (pl.tiles < splitk_below && K >= 4 * kBK) {
     const int steps = K / kBK;
     int want = std::min(std::min(steps / 2, (384 + pl.tiles - 1) / pl.tiles), max_splits);
@@ -2501,8 +2433,7 @@ static int x3_conv3x3_launch(const void* z_hi, const void* z_lo, const float* pa
     if (e != hipSuccess) return e;
     attr_set[dev_slot].store(true, std::memory_order_release);
   }
-  static const int k9dbg = getenv("TCAMD_X3_K9_DBG") ? atoi(getenv("TCAMD_X3_K9_DBG")) : 0;
-  p.dbg = k9dbg;
+  p.dbg = (int)tcamd::knob(tcamd::Knob::X3K9Dbg);
   p.tiles = (p.M + kT2 - 1) / kT2;
   const int grid = std::min(p.tiles, 256);
   p.tiles_per_block = (p.tiles + grid - 1) / grid;
@@ -2583,11 +2514,8 @@ static int x3_conv1x1_impl(const float* x, int ldx, int M, int K, int N, const f
   }
   hipStream_t s = (hipStream_t)stream;
   // warp-specialised persistent kernel for the big dense-layer 1x1s
-  // (TCAMD_X3_WS=0 turns it off for A/B runs)
-  static const int ws_mode = getenv("TCAMD_X3_WS") ? atoi(getenv("TCAMD_X3_WS")) : 1;
-  // (M floor: TCAMD_X3_WS_MIN, A/B runs)
-  static const int ws_min = getenv("TCAMD_X3_WS_MIN") ? atoi(getenv("TCAMD_X3_WS_MIN")) : 16384;
-  if (ws_mode && !pool && split_out && N == kBN && M >= ws_min) {
+  // (TCAMD_X3_WS=0 turns it off, TCAMD_X3_WS_MIN moves its M floor: A/B runs)
+  if (tcamd::knob(tcamd::Knob::X3Ws) && !pool && split_out && N == kBN && M >= tcamd::knob(tcamd::Knob::X3WsMin)) {
     // per device: the CU count and the dynamic-LDS opt-in, cached only after
     // every attribute call succeeded (a failed setup is retried, never launched)
     static std::atomic<int> ncu_dev[kMaxDevices];
@@ -2598,9 +2526,7 @@ static int x3_conv1x1_impl(const float* x, int ldx, int M, int K, int N, const f
       hipError_t e = hipGetDevice(&dev);
       if (e == hipSuccess) e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
       if (e == hipSuccess && n <= 0) e = hipErrorInvalidDevice;
-      for (const void* f : {(const void*)x3_conv1x1_ws_kernel<3, 0>, (const void*)x3_conv1x1_ws_kernel<5, 0>,
-                            (const void*)x3_conv1x1_ws_kernel<6, 0>, (const void*)x3_conv1x1_ws_kernel<3, -1>,
-                            (const void*)x3_conv1x1_ws_kernel<5, -1>, (const void*)x3_conv1x1_ws_kernel<6, -1>})
+      for (const void* f : {(const void*)x3_conv1x1_ws_kernel<3, 0>, (const void*)x3_conv1x1_ws_kernel<3, -1>})
         if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsWs);
       if (e != hipSuccess) return e;
       ncu = n;
@@ -2608,8 +2534,7 @@ static int x3_conv1x1_impl(const float* x, int ldx, int M, int K, int N, const f
     }
     X3WsParams wp;
     wp.c = p;
-    static const int dbg = getenv("TCAMD_X3_WS_DBG") ? atoi(getenv("TCAMD_X3_WS_DBG")) : 0;
-    wp.dbg = dbg;
+    wp.dbg = (int)tcamd::knob(tcamd::Knob::X3WsDbg);
     const int units = (M + 15) / 16;
     wp.units_per_block = (units + ncu - 1) / ncu;
     // equal tiles: 392 rows -> 4 x 98 instead of 3 x 128 + 8 (every tile
@@ -2618,23 +2543,12 @@ static int x3_conv1x1_impl(const float* x, int ldx, int M, int K, int N, const f
     const int nt = (rpb + 127) / 128;
     wp.tile_rows = (rpb + nt - 1) / nt;
     const int blocks = (units + wp.units_per_block - 1) / wp.units_per_block;
-    static const int ws_pf = getenv("TCAMD_X3_WS_PF") ? atoi(getenv("TCAMD_X3_WS_PF")) : 3;
-    if (wp.dbg) {
-      if (ws_pf == 5) hipLaunchKernelGGL((x3_conv1x1_ws_kernel<5, -1>), dim3(blocks), dim3(512), kLdsWs, s, wp);
-      else if (ws_pf == 6) hipLaunchKernelGGL((x3_conv1x1_ws_kernel<6, -1>), dim3(blocks), dim3(512), kLdsWs, s, wp);
-      else hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, -1>), dim3(blocks), dim3(512), kLdsWs, s, wp);
-    } else if (ws_pf == 5) {
-      hipLaunchKernelGGL((x3_conv1x1_ws_kernel<5, 0>), dim3(blocks), dim3(512), kLdsWs, s, wp);
-    } else if (ws_pf == 6) {
-      hipLaunchKernelGGL((x3_conv1x1_ws_kernel<6, 0>), dim3(blocks), dim3(512), kLdsWs, s, wp);
-    } else {
-      hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, 0>), dim3(blocks), dim3(512), kLdsWs, s, wp);
-    }
+    if (wp.dbg) hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, -1>), dim3(blocks), dim3(512), kLdsWs, s, wp);
+    else hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, 0>), dim3(blocks), dim3(512), kLdsWs, s, wp);
     return hipGetLastError();
   }
-  static const int xg = getenv("TCAMD_X3_XCD_GROUP") ? atoi(getenv("TCAMD_X3_XCD_GROUP")) : 1;
   const int mb = (M + pl.bm - 1) / pl.bm, ntl = N / kBN;
-  p.xcd_group = (xg && ntl > 1 && pl.splits == 1) ? 1 : 0;
+  p.xcd_group = (ntl > 1 && pl.splits == 1) ? 1 : 0;
   const dim3 g = p.xcd_group ? dim3((mb + 7) / 8 * 8 * ntl, 1, 1) : dim3(mb, pl.splits, ntl);
   if (pool) {
     if (split_out) launch_x3_1x1<true, true>(pl, g, s, p);
@@ -2697,9 +2611,9 @@ int tcamd_x3_fused_stamps(unsigned long long* out, int n) {
 }
 
 // K11x: the whole dense layer in one kernel (z stays in LDS).  v 1: the
-// 8-wave kernel (w2 in x3_w3f_fragments); v 2: the 4-wave kernel (w2 in
-// x3_w3_fragments, K9x's layout).  w1 in x3_w1_fragments; 16 <= W <= 56,
-// K in 64..224.
+// 8-wave kernel; v 3: v1 with the next chunk's 1x1 interleaved into each
+// tile's 3x3.  w1 in x3_w1_fragments, w2 in x3_w3f_fragments; 16 <= W <= 56,
+// K in 64..480.
 static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, int W, int K, const float* s1,
                                const float* t1, const void* w1_hi, const void* w1_lo, const float* b1,
                                const void* w2_hi, const void* w2_lo, float* y, int ldy, void* stream) {
@@ -2744,7 +2658,7 @@ static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, 
 #undef X3F_ROW
   const int nst = K / 32;
   if (nst < 2 || nst > 15 || (v != 1 && v != 3)) return hipErrorInvalidValue;
-  static const bool stamp = getenv("TCAMD_X3F_STAMP") && atoi(getenv("TCAMD_X3F_STAMP"));
+  const bool stamp = tcamd::knob(tcamd::Knob::X3fStamp) != 0;
   p.stamps = nullptr;
   if (stamp) {
     if (!g_x3f_stamps && hipMalloc((void**)&g_x3f_stamps, 8 * 1024 * sizeof(unsigned long long)) != hipSuccess)
@@ -2762,8 +2676,7 @@ static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, 
         }
     attr_set[dev_slot].store(true, std::memory_order_release);
   }
-  static const int dbg = getenv("TCAMD_X3F_DBG") ? atoi(getenv("TCAMD_X3F_DBG")) : 0;
-  p.dbg = dbg;
+  p.dbg = (int)tcamd::knob(tcamd::Knob::X3fDbg);
   p.tiles = (p.M + kT2 - 1) / kT2;
   const int grid = std::min(p.tiles, cu_count());
   p.tiles_per_block = (p.tiles + grid - 1) / grid;
@@ -2865,9 +2778,8 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
   p.K = K;
   p.ldy = ldy;
   p.imgs = imgs;
-  static const int dbg = getenv("TCAMD_X3_SMALLF_DBG") ? atoi(getenv("TCAMD_X3_SMALLF_DBG")) : 0;
-  p.dbg = dbg;
-  static const bool stamp = getenv("TCAMD_X3_SMALLF_STAMP") && atoi(getenv("TCAMD_X3_SMALLF_STAMP"));
+  p.dbg = (int)tcamd::knob(tcamd::Knob::X3SmallfDbg);
+  const bool stamp = tcamd::knob(tcamd::Knob::X3SmallfStamp) != 0;
   p.stamps = nullptr;
   if (stamp) {
     if (!g_x3s_stamps && hipMalloc((void**)&g_x3s_stamps, 8 * 4096 * sizeof(unsigned long long)) != hipSuccess)
@@ -2931,20 +2843,11 @@ int tcamd_x3_stem(const void* srcs, const void* w_hi, const void* w_lo, const fl
   p.bias = bias;
   p.y = y;
   p.ldy = ldy;
-  // v3 (persistent, TCAMD_X3_STEM_BPC blocks per CU) unless TCAMD_X3_STEM=1/2
-  // (v1: conv tile in LDS, v2: one block per tile; A/B runs)
-  static const int stem_v = getenv("TCAMD_X3_STEM") ? atoi(getenv("TCAMD_X3_STEM")) : 3;
-  const dim3 g(kSHo / kSPC, kSHo / kSPR, imgs);
-  if (stem_v == 1) {
-    hipLaunchKernelGGL(x3_stem_kernel<false>, g, dim3(256), 0, (hipStream_t)stream, p);
-  } else if (stem_v == 2) {
-    hipLaunchKernelGGL(x3_stem_kernel<true>, g, dim3(256), 0, (hipStream_t)stream, p);
-  } else {
-    static const int bpc = getenv("TCAMD_X3_STEM_BPC") ? std::max(1, atoi(getenv("TCAMD_X3_STEM_BPC"))) : 2;
-    const int ntiles = (int)(g.x * g.y) * imgs;
-    const int grid = std::min(ntiles, bpc * cu_count());
-    hipLaunchKernelGGL(x3_stem_p_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, ntiles);
-  }
+  // persistent: TCAMD_X3_STEM_BPC workgroups per CU walk the 4 x 14 tiles of every image
+  const int bpc = std::max(1, (int)tcamd::knob(tcamd::Knob::X3StemBpc));
+  const int ntiles = (kSHo / kSPC) * (kSHo / kSPR) * imgs;
+  const int grid = std::min(ntiles, bpc * cu_count());
+  hipLaunchKernelGGL(x3_stem_p_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, ntiles);
   return hipGetLastError();
 }
 

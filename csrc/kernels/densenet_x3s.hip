@@ -43,6 +43,7 @@
 #include <cstdlib>
 
 #include "kernels/common.h"
+#include "kernels/knobs.h"
 
 namespace {
 
@@ -411,7 +412,7 @@ __global__ void __launch_bounds__(256) x3c_base_kernel(X3cParams p) {
   }
 }
 
-// NW waves per block (4 or 8).  Part A: wave w takes taps w, w + NW, ... and
+// NW waves per block (4 launched; 8 measured slower).  Part A: wave w takes taps w, w + NW, ... and
 // band row tiles w, w + NW, ...; part B: each group of 4 waves (one per
 // output quarter) takes one later layer, NW / 4 layers per block
 template <int NW>
@@ -547,14 +548,8 @@ extern "C" {
 // run to run; with at most 2 chunks and TCAMD_X3S_SPLIT3=0 the layer is
 // bitwise reproducible (two adds onto a zero are order-free).
 int tcamd_x3s_steps_per_block(int M, int K) {
-  static const int target = [] {
-    const char* e = getenv("TCAMD_X3S_BLOCKS");
-    return e ? std::max(1, atoi(e)) : 384;
-  }();
-  static const int max_chunks = [] {
-    const char* e = getenv("TCAMD_X3S_MAX_CHUNKS");
-    return e ? std::max(1, atoi(e)) : 8;
-  }();
+  const int target = std::max(1, (int)tcamd::knob(tcamd::Knob::X3sBlocks));
+  const int max_chunks = std::max(1, (int)tcamd::knob(tcamd::Knob::X3sMaxChunks));
   const int tiles = (M + kTile - 1) / kTile * 4;
   const int nst = K / 16;
   const int chunks = std::max(1, std::min(std::min(target / std::max(tiles, 1), nst / 4), max_chunks));
@@ -596,7 +591,7 @@ int tcamd_x3s_dense_layer(const float* x, int ldx, int imgs, int H, int W, int K
   // weight bytes per block, y accumulated by float atomics (zeroed by S1).
   // bs1 forward 0.862 -> 0.682 ms (profiles/r3_x3s_small_m.md);
   // TCAMD_X3S_SPLIT3=0: all quarters in one block, y stored (bitwise reproducible)
-  static const int split3 = getenv("TCAMD_X3S_SPLIT3") ? atoi(getenv("TCAMD_X3S_SPLIT3")) : 1;
+  const bool split3 = tcamd::knob(tcamd::Knob::X3sSplit3) != 0;
   a.y_zero = split3 ? y : nullptr;
   a.ldy = ldy;
   const int chunks = (K / 16 + a.steps_per_block - 1) / a.steps_per_block;
@@ -657,13 +652,11 @@ int tcamd_x3c_layer(const void* layers, int l, int n, float* x, int ldx, int img
   X3cParams p;
   int e = x3c_check(layers, x, ldx, imgs, H, W, l, n, p);
   if (e != hipSuccess) return e;
-  // 4 waves per block; TCAMD_X3C_WAVES=8 (taps and band tiles over 8 waves,
-  // two later layers per part-B block) measured slower: bs1 0.430 -> 0.455 ms
-  static const int nw = getenv("TCAMD_X3C_WAVES") && atoi(getenv("TCAMD_X3C_WAVES")) == 8 ? 8 : 4;
-  const int per = nw / 4;  // later layers per part-B block
-  const int nB = l > 0 ? (p.M + kTile - 1) / kTile * ((n - l - 1 + per - 1) / per) : 0;
-  if (nw == 4) hipLaunchKernelGGL(x3c_layer_kernel<4>, dim3(p.nA + nB), dim3(256), 0, (hipStream_t)stream, p);
-  else hipLaunchKernelGGL(x3c_layer_kernel<8>, dim3(p.nA + nB), dim3(512), 0, (hipStream_t)stream, p);
+  // 4 waves per block, one later layer per part-B block (8 waves, taps and
+  // band tiles over 8 and two later layers per block, measured slower in
+  // round 3: bs1 0.430 -> 0.455 ms; removed in round 5)
+  const int nB = l > 0 ? (p.M + kTile - 1) / kTile * (n - l - 1) : 0;
+  hipLaunchKernelGGL(x3c_layer_kernel<4>, dim3(p.nA + nB), dim3(256), 0, (hipStream_t)stream, p);
   return hipGetLastError();
 }
 

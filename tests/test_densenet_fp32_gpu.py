@@ -481,6 +481,39 @@ def test_fp32_engine_k14x_blocks_match_fp32_module(fp32_engine, b):
     assert e_ref < 1e-3 and e_base < 1e-4
 
 
+_ROUTES = [{"fuse_min_tiles": 0}, {"fuse_big_k_min_tiles": 1}, {"fuse_v3": 0}, {"fuse_v3": 16},
+           {"small_m": 0}, {"use_chain": False}, {"chain_m": 0}, {"small_m": 0, "chain_m": 0},
+           {"smallf_min_blocks": 1, "smallf_tiles": 2}, {"smallf_min_blocks": 1, "smallf_tiles": 4}]
+
+
+@pytest.mark.parametrize("b", [2, 24])
+def test_fp32_engine_routing_knobs(fp32_engine, b):
+    """Every engine routing knob (the TCAMD_X3_* engine attributes: K11x on /
+    off, its big-K floor, v3 placement, K13x two-launch and chain, chain size,
+    K14x tiling) gives the default route's logits to fp32 parity, and the
+    fp32 module's within the engine bound."""
+    eng, model = fp32_engine
+    g = torch.Generator(device=DEV).manual_seed(500 + b)
+    x = torch.randn(b, 3, 224, 224, device=DEV, generator=g)
+    with torch.no_grad():
+        base = eng(x).clone()
+        ref = model.to(DEV).float()(x)
+    for route in _ROUTES:
+        keep = {k: getattr(eng, k) for k in route}
+        try:
+            for k, v in route.items():
+                setattr(eng, k, v)
+            with torch.no_grad():
+                got = eng(x).clone()
+        finally:
+            for k, v in keep.items():
+                setattr(eng, k, v)
+        torch.cuda.synchronize()
+        e_base, e_ref = _rel(got, base), _rel(got, ref)
+        print("engine b=%d %s: rel vs default route %.3g, vs fp32 module %.3g" % (b, route, e_base, e_ref))
+        assert e_base < 1e-4 and e_ref < 1e-3, route
+
+
 def test_fp32_engine_vs_fp64_and_graph_capture(fp32_engine):
     """Against an fp64 CPU reference the engine must stay fp32-class (rel-L2
     < 1e-4; measured 4.5e-5, torch's own fp32 forward 2.2e-6 on MI355X, the

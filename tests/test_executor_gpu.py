@@ -74,6 +74,37 @@ def test_executor_mixed_device_and_host_rows(model, instance):
     assert st["batches"] == before + 1 and st["wait_ns"] > 0
 
 
+def test_native_executor_matches_python_path(model, monkeypatch):
+    """TCAMD_NATIVE_EXEC=0 loads the model without the C++ executor (tcserve
+    then calls the Python execute_native per batch); both give the same logits
+    for the same batch."""
+    from triton_client_amd.server.gpu_models import DensenetOnnx
+
+    monkeypatch.setenv("TCAMD_NATIVE_EXEC", "0")
+    py = DensenetOnnx(engine="fp32", max_batch_size=8)
+    py.instance_count = 1
+    py.load()
+    try:
+        assert py.native_executor() is None and py.executor_stats() is None
+        assert model.native_executor() is not None
+        dev = torch.device("cuda", 0)
+        x = torch.randn(3, 3, 224, 224, generator=torch.Generator().manual_seed(11)).to(dev).contiguous()
+        outs = []
+        for m, run in ((model, lambda b: model._pgx.execute(0, ctypes.addressof(b))),
+                       (py, lambda b: py.execute_native(0, b))):
+            out = torch.full((3, 1000), float("nan"), device=dev)
+            torch.cuda.synchronize()
+            b, keep = _batch([(1, 0, x.data_ptr(), x.numel() * 4)], [(1, 0, out.data_ptr(), out.numel() * 4)], [3])
+            run(b)
+            torch.cuda.synchronize()
+            outs.append(out.cpu().numpy())
+        assert np.isfinite(outs[1]).all()
+        rel = np.linalg.norm(outs[0] - outs[1]) / np.linalg.norm(outs[1])
+        assert rel < 2e-5, rel  # same engine and bucket graph; float-atomic ordering noise only
+    finally:
+        py.unload()
+
+
 def test_executor_rejects_oversized_batch(model):
     x = torch.zeros(9, 3, 224, 224, device="cuda")
     out = torch.zeros(9, 1000, device="cuda")

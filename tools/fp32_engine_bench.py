@@ -26,12 +26,14 @@ def main():
                     help="fp32 engine: also capture graphs with K14x off and interleave the two (rounds)")
     ap.add_argument("--ab", default="",
                     help="fp32 engine A/B of one engine attribute, interleaved per round: ATTR=V1,V2 "
-                         "(e.g. fuse_v3=0,56; integer values)")
+                         "(e.g. fuse_v3=0,56; integer values), or of a native knob, captured into each "
+                         "variant's graphs (e.g. TCAMD_X3_MAX_SPLITS=2,4; triton_client_amd/utils/knobs.py)")
     ap.add_argument("--rounds", type=int, default=1)
     args = ap.parse_args()
     import torch
 
     from triton_client_amd.models import densenet_fp32, densenet_fused
+    from triton_client_amd.ops import hip
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
@@ -61,8 +63,10 @@ def main():
             gv = {}
             for vname, mb in variants:
                 graphs = []
+                native = attr.startswith("TCAMD_") and attr in hip.knobs()
+                prev = hip.knob_set(attr, mb) if native and mb is not None else None
                 for e, o, s in zip(engines, outs, sts):
-                    if mb is not None:
+                    if mb is not None and not native:
                         setattr(e, attr, mb)
                     with torch.cuda.stream(s), torch.no_grad():
                         e.forward_ptrs(b, out=o)
@@ -70,6 +74,8 @@ def main():
                         with torch.cuda.graph(g, stream=s):
                             e.forward_ptrs(b, out=o)
                     graphs.append(g)
+                if prev is not None:
+                    hip.knob_set(attr, prev)
                 gv[vname] = graphs
             torch.cuda.synchronize()
             for ns in streams:

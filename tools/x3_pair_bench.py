@@ -80,7 +80,7 @@ def bench(a):
         print("hw=%d k=%d chunk=%d: %.1f us per %d images" % (a.hw, K, c, us, a.imgs), flush=True)
     # K11x: the same layer in one kernel, z kept in LDS
     f1h, f1l = hip.x3_w1_fragments(w1h), hip.x3_w1_fragments(w1l)
-    v = int(os.environ.get("TCAMD_X3F_V", "3"))
+    v = int(os.environ.get("X3_PAIR_BENCH_V", "3"))
     frag = hip.x3_w3f_fragments
     fn = hip.x3_dense_fused if v == 1 else hip.x3_dense_fused3
     f3h, f3l = frag(w3h), frag(w3l)
@@ -108,8 +108,8 @@ def bench(a):
     runs = [("TCAMD_X3F_DBG", d) for d in a.fused_dbg.split(",") if d] + ([("TCAMD_X3F_STAMP", "1")] if a.stamp else [])
     runs = [(v, d, {}) for v, d in runs] + [("TCAMD_X3F_DBG", d, {"TCAMD_X3F_STAMP": "1"})
                                             for d in a.stamp_dbg.split(",") if d]
-    if a.both and os.environ.get("TCAMD_X3F_V", "3") == "3":
-        runs.append(("TCAMD_X3F_V", "1", {}))
+    if a.both and os.environ.get("X3_PAIR_BENCH_V", "3") == "3":
+        runs.append(("X3_PAIR_BENCH_V", "1", {}))
     if runs:
         import subprocess
         for var, d, extra in runs:

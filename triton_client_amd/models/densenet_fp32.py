@@ -131,7 +131,6 @@ class FusedDenseNetFP32:
         # layer); TCAMD_X3_CHAIN=0: two launches per layer up to small_m
         self.use_chain = os.environ.get("TCAMD_X3_CHAIN", "1") != "0"
         self.chain_m = int(os.environ.get("TCAMD_X3_CHAIN_M", "3136"))
-        self.chain_after_fused = os.environ.get("TCAMD_X3_CHAIN_AFTER_FUSED", "0") != "0"
         # K14x (whole dense layer in one kernel at 14x14 / 7x7) once it has at
         # least this many workgroups (row tiles of the images, 2-4 per 14x14
         # image, 1-4 per 7x7 image: x3_small_tiles); 0 disables it
@@ -234,14 +233,10 @@ class FusedDenseNetFP32:
             ch = self.chain[bi]
             if ch is not None and 0 < M <= ch[2]:
                 # the whole block runs as one chain (at bs1-2 a 28x28 K11x layer
-                # takes 13-15 us, a chain layer ~5.5); TCAMD_X3_CHAIN_AFTER_FUSED=1
-                # starts the chain after the layers K11x would take
-                f = sum(1 for L in layers if fused and L["cin"] <= fmax) if self.chain_after_fused else 0
-                for L in layers[:f]:
-                    self._fused_layer(fused, L, fp, ctot, b, hw, st)
-                tab, n = ch[1].data_ptr() + 8 * hip.X3C_LAYER_WORDS * f, len(layers) - f
-                if n:
-                    hip.x3c_base(tab, n, fp, ctot, b, hw, hw, stream=st)
+                # takes 13-15 us, a chain layer ~5.5; starting the chain after
+                # the layers K11x would take lost, round 3)
+                tab, n = ch[1].data_ptr(), len(layers)
+                hip.x3c_base(tab, n, fp, ctot, b, hw, hw, stream=st)
                 for i in range(n):
                     hip.x3c_layer(tab, i, n, fp, ctot, b, hw, hw, stream=st)
                 self._transition(bi, fp, ctot, b, hw, ws, wsb, st)

@@ -15,6 +15,7 @@ int (``torch.cuda.current_stream().cuda_stream`` works) or None for the
 library's per-device copy stream / the null stream.
 """
 
+import contextlib
 import ctypes
 import os
 import sys
@@ -235,6 +236,13 @@ _SIGS = {
         ctypes.c_int,
     ),
     "tcamd_k3_set_check": ([ctypes.c_int], ctypes.c_int),
+    "tcamd_knob_count": ([], ctypes.c_int),
+    "tcamd_knob_info": (
+        [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_longlong),
+         ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_char_p)],
+        ctypes.c_int,
+    ),
+    "tcamd_knob_set": ([ctypes.c_char_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_longlong)], ctypes.c_int),
     "tcamd_x3_cat": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "tcamd_x3_stem": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
@@ -891,6 +899,42 @@ def k3_set_check(on):
     workspace at exactly the size it needs with a 4 KiB canary behind it and
     fails if the canary changed.  Returns the previous setting."""
     return bool(_load().tcamd_k3_set_check(1 if on else 0))
+
+
+def knobs():
+    """The native knob registry (csrc/runtime/knobs.hip): {name: {"default",
+    "value", "doc"}} -- every tuning / diagnostic switch the kernels' host
+    entry points read, seeded from the environment variable of that name."""
+    lib_ = _load()
+    out = {}
+    for i in range(lib_.tcamd_knob_count()):
+        name, doc = ctypes.c_char_p(), ctypes.c_char_p()
+        d, v = ctypes.c_longlong(), ctypes.c_longlong()
+        if lib_.tcamd_knob_info(i, ctypes.byref(name), ctypes.byref(d), ctypes.byref(v), ctypes.byref(doc)) == 0:
+            out[name.value.decode()] = {"default": d.value, "value": v.value, "doc": doc.value.decode()}
+    return out
+
+
+def knob_set(name, value):
+    """Sets a native knob for this process (read at each launch; a captured HIP
+    graph keeps what it captured); returns the previous value."""
+    prev = ctypes.c_longlong()
+    if _load().tcamd_knob_set(name.encode(), int(value), ctypes.byref(prev)) != 0:
+        raise KeyError("unknown native knob %r (known: %s)" % (name, ", ".join(sorted(knobs()))))
+    return prev.value
+
+
+@contextlib.contextmanager
+def knob(**settings):
+    """``with hip.knob(TCAMD_X3_WS=0): ...`` -- native knobs set for the block, restored after."""
+    prev = {}
+    try:
+        for k, v in settings.items():
+            prev[k] = knob_set(k, v)
+        yield
+    finally:
+        for k, v in prev.items():
+            knob_set(k, v)
 
 
 def index_bytes(buf_ptr, nbytes, n_expected, offs_ptr, lens_ptr, status_ptr, stream=None):
