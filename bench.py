@@ -460,7 +460,7 @@ def main():
         _, in1 = make_input("data_1_in", 1)
         p1 = Point(srv, model, 1, args.bs1_concurrency, "data_1_in", in1, dev, cpu)
         points.append(p1)
-        n1 = 16 * args.bs1_concurrency
+        n1 = 64 * args.bs1_concurrency  # ~0.2 s at 20k infer/s: the batch groups of a closed loop need time to settle
         p1.run(n1 // 4)
         s10, b10 = p1.s.server_stats(), batch_stats(client, model)
         l1, e1, el1 = measure(p1, 4, n1 // 4)
@@ -474,6 +474,9 @@ def main():
         bd64["compute_us_per_request_weighted"] = round(wc1, 1)
         bd64["unattributed_us_per_request"] = round(
             bd64["server_us_per_request"] - bd64["queue_us_per_request"] - wc1, 1)
+        # executed batches by rows (a closed loop of 64 settles into groups: ~2 of ~32 or ~3 of ~21)
+        bd64["batch_rows_histogram"] = {str(k): int(b11[k][0] - b10.get(k, (0,))[0]) for k in sorted(b11)
+                                        if b11[k][0] - b10.get(k, (0,))[0] > 0}
         bs1["breakdown_rank0"] = bd64
         l1g = fanout.gather_arrays(l1.astype(np.int64)).astype(np.float64)
         bs1.update({"p50_latency_us": round(percentile_us(l1g, 50), 1),

@@ -19,6 +19,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <queue>
 #include <functional>
 #include <map>
 #include <memory>
@@ -2459,6 +2460,103 @@ int32_t tcserve_batch_policy_sim(int32_t max_batch, uint64_t delay_ns, const int
     for (int i = 0; i < instances; ++i)
       if (free_at[i]) nt = std::min(nt, free_at[i]);
     if (nt == UINT64_MAX) return -1;  // cannot happen: a queued request always has a deadline or a free instance
+    t = std::max(t, nt);
+  }
+  return nb;
+}
+
+int32_t tcserve_batch_policy_sim_closed(int32_t max_batch, uint64_t delay_ns, const int32_t* preferred,
+                                        int32_t n_pref, int32_t instances, int32_t flags, int32_t clients,
+                                        int32_t rows_per_req, uint64_t spread_ns, uint64_t turnaround_ns,
+                                        uint64_t resp_spacing_ns, uint64_t exec_base_ns, uint64_t exec_per_row_ns,
+                                        uint64_t horizon_ns, uint64_t* out_start_ns, int32_t* out_rows,
+                                        int32_t* out_instance, int32_t max_batches)
+{
+  if (instances < 1 || clients < 1 || n_pref < 0 || (n_pref && !preferred) || !out_start_ns || !out_rows ||
+      !out_instance)
+    return -1;
+  tcserve::BatchPolicyConfig pc;
+  pc.max_batch = max_batch;
+  pc.delay_ns = delay_ns;
+  for (int32_t i = 0; i < n_pref; ++i)
+    if (preferred[i] > 0) pc.preferred.push_back(preferred[i]);
+  std::sort(pc.preferred.begin(), pc.preferred.end());
+  pc.idle_dispatch = flags & 1;
+  pc.pipelined = (flags & 2) != 0;
+  pc.stagger = (flags & 4) != 0;
+  pc.instances = instances;
+  if (rows_per_req < 1 || rows_per_req > pc.Cap()) return -1;
+  // (arrival time, client), earliest first
+  using Ev = std::pair<uint64_t, int32_t>;
+  std::priority_queue<Ev, std::vector<Ev>, std::greater<Ev>> arrivals;
+  for (int32_t k = 0; k < clients; ++k) arrivals.push({spread_ns * static_cast<uint64_t>(k), k});
+  std::deque<int32_t> q;
+  std::vector<uint64_t> free_at(instances, 0), started(instances, 0);
+  std::vector<std::vector<int32_t>> members(instances);
+  std::vector<uint64_t> arrived(clients, 0);
+  int q_rows = 0, busy = 0, last_rows = 0, nb = 0;
+  double ema = 0;
+  uint64_t last_start = 0, t = 0;
+  while (true) {
+    for (int i = 0; i < instances; ++i)
+      if (free_at[i] && free_at[i] <= t) {
+        const double d = static_cast<double>(free_at[i] - started[i]);
+        ema = ema > 0 ? 0.9 * ema + 0.1 * d : d;
+        busy--;
+        for (size_t j = 0; j < members[i].size(); ++j)
+          arrivals.push({free_at[i] + turnaround_ns + resp_spacing_ns * j, members[i][j]});
+        members[i].clear();
+        free_at[i] = 0;
+      }
+    while (!arrivals.empty() && arrivals.top().first <= t) {
+      arrived[arrivals.top().second] = arrivals.top().first;
+      q.push_back(arrivals.top().second);
+      q_rows += rows_per_req;
+      arrivals.pop();
+    }
+    if (t >= horizon_ns) break;
+    uint64_t timer = UINT64_MAX;
+    while (!q.empty()) {
+      int idle = -1;
+      for (int i = 0; i < instances && idle < 0; ++i)
+        if (!free_at[i]) idle = i;
+      if (idle < 0) break;
+      tcserve::BatchPolicyState st;
+      st.now_ns = t;
+      st.q_rows = q_rows;
+      st.busy = busy;
+      st.last_rows = last_rows;
+      st.ema_exec_ns = ema;
+      st.last_start_ns = last_start;
+      st.front_arrive_ns = arrived[q.front()];
+      const uint64_t until = tcserve::WaitUntil(pc, st);
+      if (until) {
+        timer = until;
+        break;
+      }
+      const int limit = tcserve::TakeLimit(pc, q_rows);
+      int r = 0;
+      while (!q.empty() && (r == 0 || r + rows_per_req <= limit)) {
+        r += rows_per_req;
+        q_rows -= rows_per_req;
+        members[idle].push_back(q.front());
+        q.pop_front();
+      }
+      if (nb >= max_batches) return -2;
+      out_start_ns[nb] = t;
+      out_rows[nb] = r;
+      out_instance[nb] = idle;
+      nb++;
+      last_rows = r;
+      last_start = t;
+      started[idle] = t;
+      free_at[idle] = t + exec_base_ns + exec_per_row_ns * static_cast<uint64_t>(r);
+      busy++;
+    }
+    uint64_t nt = std::min(timer, horizon_ns);
+    if (!arrivals.empty()) nt = std::min(nt, arrivals.top().first);
+    for (int i = 0; i < instances; ++i)
+      if (free_at[i]) nt = std::min(nt, free_at[i]);
     t = std::max(t, nt);
   }
   return nb;

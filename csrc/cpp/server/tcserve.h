@@ -76,6 +76,16 @@ int32_t tcserve_batch_policy_sim(int32_t max_batch, uint64_t delay_ns, const int
                                  int32_t instances, int32_t flags, const uint64_t* arrive_ns, const int32_t* rows,
                                  int32_t n, uint64_t exec_base_ns, uint64_t exec_per_row_ns, uint64_t* out_start_ns,
                                  int32_t* out_rows, int32_t* out_first, int32_t* out_instance, int32_t max_batches);
+/// Closed-loop variant: `clients` clients each keep one request of rows_per_req rows in flight (client k
+/// first arrives at k * spread_ns; a finished batch's clients come back turnaround_ns after its end, the
+/// j-th of them j * resp_spacing_ns later).  Reports the batches started before horizon_ns; returns their
+/// count (-1 on bad arguments, -2 if max_batches was too small).
+int32_t tcserve_batch_policy_sim_closed(int32_t max_batch, uint64_t delay_ns, const int32_t* preferred,
+                                        int32_t n_pref, int32_t instances, int32_t flags, int32_t clients,
+                                        int32_t rows_per_req, uint64_t spread_ns, uint64_t turnaround_ns,
+                                        uint64_t resp_spacing_ns, uint64_t exec_base_ns, uint64_t exec_per_row_ns,
+                                        uint64_t horizon_ns, uint64_t* out_start_ns, int32_t* out_rows,
+                                        int32_t* out_instance, int32_t max_batches);
 /// Mirror of the Python shared-memory registries; kind 0 = system (ptr = host mapping), 1 = device.
 int32_t tcserve_shm_add(void* server, const char* name, int32_t kind, uint64_t ptr, uint64_t bytes, int32_t device);
 /// Unregister (name "" = all of kind).  Never blocks: returns how many of the removed regions

@@ -1730,6 +1730,8 @@ constexpr int x3s_zrows_max(int W, int T) {
 // producers' registers, 4 K-step stages, W1 loaded by the consumers.
 template <int W, int T>
 __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
+  // (6 X steps in flight measured the same as 3 at 16..128 images: the step
+  // is bound by the producers' conversion, not by X latency; round 5)
   constexpr int PF = 3, kSmS = 4;
   constexpr int kLdsSm = kSmS * kWsStage;
   constexpr int kRowsOut = (W + T - 1) / T;          // most output rows of a tile
@@ -1764,7 +1766,7 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
   const int TR = (zr1 - zr0) * W;  // z rows of the tile
   const int mz0 = img * W * W + zr0 * W;
   const int nst = p.K / kBK;
-  const int Q = nst, Qp = (Q + PF - 1) / PF * PF;
+  const int Q = nst;  // K steps = barrier rounds of both roles (no padding to a multiple of PF)
   // timeline diagnostic (dbg 64, block 0): shader-clock time of producer wave
   // 4 and consumer wave 0 reaching each step barrier, kept in LDS past the
   // stages (no memory op inside the counted-wait loop)
@@ -1828,10 +1830,11 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
     issue_x(PF, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     ws_barrier();  // B0
-    for (int q0 = 0; q0 < Qp; q0 += PF) {
+    for (int q0 = 0; q0 < Q; q0 += PF) {
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
         const int q = q0 + u;
+        if (q >= Q) break;  // block-uniform: both roles run Q barrier rounds
         const int slot = (u + 1) % PF;
         __builtin_amdgcn_s_waitcnt(ws_vmcnt(kOps * (PF - 1)));  // X of step q+1
         __builtin_amdgcn_sched_barrier(0);
@@ -1925,9 +1928,9 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
       stamp_c(q);
       ws_barrier();  // B(q+1)
     };
-    for (int q = 0; q < Qp; q += 2) {
+    for (int q = 0; q < Q; q += 2) {
       step(q, fa, fb);
-      if (q + 1 >= Qp) break;
+      if (q + 1 >= Q) break;
       step(q + 1, fb, fa);
     }
   }

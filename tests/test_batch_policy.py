@@ -6,7 +6,8 @@ discrete-event simulation, so batch composition and start spacing are exact.
 Rules covered: preferred-size batches go at once; otherwise the queue delay
 from the oldest request; idle-aware dispatch; pipelined dispatch of partial
 batches; staggered starts of full batches on several instances; the take
-limit (largest preferred size the queue fills, whole requests, FIFO)."""
+limit (largest preferred size the queue fills, whole requests, FIFO); and, in
+the closed-loop simulator, how a loop of one-row clients settles into groups."""
 
 import ctypes
 import os
@@ -139,3 +140,51 @@ def test_bad_arguments_are_rejected():
     P = ctypes.c_void_p
     assert f(128, 0, P(0), 0, 1, 1, P(a.ctypes.data), P(r.ctypes.data), 1, 0, 0, P(out.ctypes.data),
              P(o32.ctypes.data), P(o32.ctypes.data), P(o32.ctypes.data), 4) == -1
+
+
+def sim_closed(flags, clients=64, instances=2, exec_base_us=1600, exec_per_row_us=3, turnaround_us=150,
+               spacing_us=4, spread_us=10, horizon_us=100000, max_batch=128, delay_us=2000):
+    """tcserve_batch_policy_sim_closed: a closed loop of ``clients`` one-row
+    requests (each client re-sends ``turnaround_us`` after its batch ends, the
+    j-th response ``j * spacing_us`` later)."""
+    lib = ctypes.CDLL(native_frontend.LIB_PATH)
+    f = lib.tcserve_batch_policy_sim_closed
+    f.restype = ctypes.c_int32
+    cap = 20000
+    st, nr, inst = np.zeros(cap, np.uint64), np.zeros(cap, np.int32), np.zeros(cap, np.int32)
+    P, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32
+    nb = f(i32(max_batch), u64(delay_us * US), P(0), i32(0), i32(instances), i32(flags), i32(clients), i32(1),
+           u64(spread_us * US), u64(turnaround_us * US), u64(spacing_us * US), u64(exec_base_us * US),
+           u64(exec_per_row_us * US), u64(horizon_us * US), P(st.ctypes.data), P(nr.ctypes.data), P(inst.ctypes.data),
+           i32(cap))
+    assert nb > 0, nb
+    return [dict(start_us=int(st[i]) // US, rows=int(nr[i]), instance=int(inst[i])) for i in range(nb)]
+
+
+def test_closed_loop_pipelined_settles_into_one_group_per_instance():
+    # bs1 at concurrency 64 on 2 instances: with pipelined dispatch the loop
+    # splits into two groups of 32 that alternate between the instances (each
+    # returning group is taken as soon as it is back); with the idle rule
+    # alone, one instance takes almost everything and the other idles
+    tail = [b for b in sim_closed(IDLE | PIPE) if b["start_us"] > 50000]
+    assert {b["rows"] for b in tail} == {32}
+    assert all(x["instance"] != y["instance"] for x, y in zip(tail, tail[1:]))
+    idle = [b for b in sim_closed(IDLE) if b["start_us"] > 50000]
+    assert {b["instance"] for b in idle} == {0} and max(b["rows"] for b in idle) == 63
+    # rows served per ms of the steady state
+    rate = lambda bs: sum(b["rows"] for b in bs) / (bs[-1]["start_us"] - bs[0]["start_us"]) * 1000  # noqa: E731
+    assert rate(tail) > 1.3 * rate(idle)
+
+
+def test_closed_loop_rejects_bad_arguments():
+    lib = ctypes.CDLL(native_frontend.LIB_PATH)
+    f = lib.tcserve_batch_policy_sim_closed
+    f.restype = ctypes.c_int32
+    buf = np.zeros(4, np.uint64)
+    P, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32
+    args = [i32(8), u64(0), P(0), i32(0), i32(1), i32(IDLE), i32(4), i32(1), u64(0), u64(0), u64(0), u64(US), u64(0),
+            u64(100 * US), P(buf.ctypes.data), P(buf.ctypes.data), P(buf.ctypes.data)]
+    assert f(*args, i32(1)) == -2  # more batches than the output holds
+    bad = list(args)
+    bad[7] = i32(9)  # rows per request above max_batch
+    assert f(*bad, i32(4)) == -1

@@ -481,6 +481,24 @@ def test_fp32_engine_k14x_blocks_match_fp32_module(fp32_engine, b):
     assert e_ref < 1e-3 and e_base < 1e-4
 
 
+def test_k14x_routing_follows_stream_concurrency(fp32_engine):
+    """TCAMD_X3_SMALLF_MIN_BLOCKS unset: K14x takes the 14x14 / 7x7 blocks from
+    48 workgroups (images x row tiles) when the engine is one of several
+    concurrent streams, from 80 on one stream (profiles/r5_engine_ab.md)."""
+    eng, _ = fp32_engine
+    keep = eng.smallf_min_blocks, eng.concurrent_streams
+    try:
+        eng.smallf_min_blocks = None
+        eng.concurrent_streams = 1
+        assert [b for b in range(1, 33) if eng._small_fused(b, 14)] == list(range(20, 33))
+        eng.concurrent_streams = 2
+        assert [b for b in range(1, 33) if eng._small_fused(b, 14)] == list(range(12, 33))
+        assert [b for b in range(1, 33) if eng._small_fused(b, 7)] == list(range(12, 33))
+        assert not eng._small_fused(64, 28)
+    finally:
+        eng.smallf_min_blocks, eng.concurrent_streams = keep
+
+
 _ROUTES = [{"fuse_min_tiles": 0}, {"fuse_big_k_min_tiles": 1}, {"fuse_v3": 0}, {"fuse_v3": 16},
            {"small_m": 0}, {"use_chain": False}, {"chain_m": 0}, {"small_m": 0, "chain_m": 0},
            {"smallf_min_blocks": 1, "smallf_tiles": 2}, {"smallf_min_blocks": 1, "smallf_tiles": 4}]

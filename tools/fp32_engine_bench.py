@@ -46,6 +46,7 @@ def main():
             eng, _ = densenet_fp32.build(maxb, device=dev)
         else:
             eng, _ = densenet_fused.build(maxb, device=dev)
+        eng.concurrent_streams = max(streams)  # routing as a server with that many instances would pick
         engines = [eng] + [eng.with_workspace() for _ in range(max(streams) - 1)]
         imgs = torch.randn(maxb, 3, 224, 224, device=dev)
         for e in engines:

@@ -131,10 +131,16 @@ class FusedDenseNetFP32:
         # layer); TCAMD_X3_CHAIN=0: two launches per layer up to small_m
         self.use_chain = os.environ.get("TCAMD_X3_CHAIN", "1") != "0"
         self.chain_m = int(os.environ.get("TCAMD_X3_CHAIN_M", "3136"))
-        # K14x (whole dense layer in one kernel at 14x14 / 7x7) once it has at
-        # least this many workgroups (row tiles of the images, 2-4 per 14x14
-        # image, 1-4 per 7x7 image: x3_small_tiles); 0 disables it
-        self.smallf_min_blocks = int(os.environ.get("TCAMD_X3_SMALLF_MIN_BLOCKS", "128"))
+        # K14x (whole dense layer in one kernel at 14x14 / 7x7) once the launch
+        # has at least this many workgroups (images x row tiles: 2-4 per 14x14
+        # image, 1-4 per 7x7 image, x3_small_tiles); 0 disables it.  Unset:
+        # 48 when the engine is one of several concurrent streams (a server's
+        # model instances: concurrent_streams), else 80 -- K14x beats the
+        # K13x chain from bs12 on two streams (+6 / +13 / +19 % at bs12 / 14 /
+        # 16) but only from bs20 on one (profiles/r5_engine_ab.md)
+        env = os.environ.get("TCAMD_X3_SMALLF_MIN_BLOCKS")
+        self.smallf_min_blocks = int(env) if env else None
+        self.concurrent_streams = 1
         # tiles per image for K14x: 0 = the library's chip-filling choice
         self.smallf_tiles = int(os.environ.get("TCAMD_X3_SMALLF_TILES", "0"))
         self._alloc(max_batch)
@@ -295,10 +301,13 @@ class FusedDenseNetFP32:
                            pool=1, H=hw, W=hw, ws=ws, ws_bytes=wsb, stream=st, N=ctot // 2)
 
     def _small_fused(self, b, hw):
-        if self.smallf_min_blocks <= 0 or hw not in (7, 14):
+        thr = self.smallf_min_blocks
+        if thr is None:
+            thr = 48 if self.concurrent_streams > 1 else 80
+        if thr <= 0 or hw not in (7, 14):
             return False
         tiles = self.smallf_tiles or hip.x3_small_tiles(b, hw)
-        return (b + 7) // 8 * 8 * tiles >= self.smallf_min_blocks
+        return b * tiles >= thr
 
     def _fuse_max_k(self, M):
         """Largest K that K11x takes: past 224 only at >= 4 tiles per block, where

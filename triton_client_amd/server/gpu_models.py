@@ -107,6 +107,8 @@ class DensenetOnnx(Model):
         else:
             self.model = densenet.build(device=dev)
         self.scale = None
+        # the instances' streams run concurrently: engines route small batches for that
+        self.model.concurrent_streams = max(1, self.instance_count)
         for _ in range(max(1, self.instance_count)):
             self._slots.append(self._make_slot(dev))
         self._free = list(range(len(self._slots)))
