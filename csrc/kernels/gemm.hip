@@ -1,0 +1,411 @@
+// K17 — bf16 GEMM for the bert_large projections (gfx950).
+//
+//   C[M, N] = A[M, K] . B[N, K]^T (+ bias[N]) (GELU), fp32 accumulate,
+//   bf16 or fp32 out.  A = activations (tokens x hidden), B = a torch Linear
+//   weight [out, in]: both operands K-contiguous.
+//
+// Structure (the 256x256 ping-pong schedule of the CDNA4 playbook, built
+// for these operands):
+//   * one 256x256 output tile per 512-thread workgroup, 8 waves as 2 (M) x
+//     4 (N), each wave 128 x 64 outputs = 8 x 4 accumulators of
+//     v_mfma_f32_16x16x32_bf16 (128 VGPRs);
+//   * K in slabs of 32: A and B slabs [256 rows][32 k] bf16 (16 KB each)
+//     staged by LDS-DMA (global_load_lds_dwordx4, no VGPR staging) into a
+//     ring of 4 slab buffers (128 KB), 3 slabs ahead, swizzled on the source
+//     address (16-B chunk c of row r lands at chunk c ^ swz(r)) so every
+//     ds_read_b128 of a fragment is bank-conflict free;
+//   * per slab an R interval (the slab's fragments from LDS, the LDS-DMAs of
+//     slab s+3, the counted vmcnt that retires slab s+1, lgkmcnt(0),
+//     barrier) and an M interval (32 MFMAs, barrier);
+//     waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave
+//     reads while the other multiplies;
+//   * the counted vmcnt never drains the ring inside the loop (loads past the
+//     last slab re-read it into a free buffer, so the counts stay constant);
+//   * persistent: one workgroup per CU walks its tiles, and their K slabs are
+//     one continuous stream through the ring (no per-tile prologue wait);
+//     the bf16 epilogue stores 4-byte column pairs (a lane-pair swap);
+//   * XCD-aware tile order: the tiles of one M panel run on one XCD (its L2
+//     keeps the A panel).
+//
+// Reference analog: none (the reference client runs no model; this serves
+// the bert_large perf_analyzer config of BASELINE.json).
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+
+#include "kernels/common.h"
+#include "kernels/knobs.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+constexpr int kTile = 256;   // N per tile; M per tile: TM = 256 or 128
+constexpr int kSlabK = 32;   // k per slab
+constexpr int kBBytes = kTile * kSlabK * 2;  // B's slab: 16 KB
+constexpr int kRing = 4;
+constexpr int kMaxBiasN = 8192;  // bias copy behind the ring (<= 32 KB)
+constexpr int slab_bytes(int tm) { return tm * kSlabK * 2 + kBBytes; }  // A | B
+constexpr int ring_bytes(int tm) { return kRing * slab_bytes(tm); }     // 128 / 96 KB
+
+enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2 };
+
+struct K17Params {
+  const uint16_t* A;  // [M][lda] bf16
+  const uint16_t* B;  // [N][ldb] bf16
+  const float* bias;  // [N] fp32 (epi >= 1)
+  void* C;            // [M][ldc] bf16 or fp32
+  int M, N, K, lda, ldb, ldc;
+  int tiles_m, tiles_n;
+};
+
+__device__ __forceinline__ v4u lds16(const uint8_t* p) { return *reinterpret_cast<const v4u*>(p); }
+
+__device__ __forceinline__ f32x4 mma(v4u a, v4u b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+
+// GELU(x) = x/2 (1 + erf(x / sqrt 2)), erf by Abramowitz-Stegun 7.1.26
+// (|error| <= 1.5e-7, far below bf16's rounding), with the hardware
+// reciprocal and exp2 (v_rcp_f32, v_exp_f32: ~1 ulp): the epilogue runs
+// between barriers, so every instruction of it stalls the other wave group
+__device__ __forceinline__ float gelu(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * z);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float e = 1.0f - poly * __builtin_amdgcn_exp2f(-1.4426950408889634f * z * z);
+  return 0.5f * x * (1.0f + __builtin_copysignf(e, x));
+}
+
+// raw barrier (no vmcnt(0): the ring's LDS-DMAs stay in flight across it);
+// the empty asm keeps LDS reads from moving across
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// the counted wait that retires slab g + 1 (slabs g + 2 and g + 3 in flight):
+// 2 x the LDS-DMAs per slab and wave (TM = 256: 2 A + 2 B, TM = 128: 1 + 2)
+template <int TM>
+__device__ __forceinline__ void wait_ring() {
+  if constexpr (TM == 256) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+}
+
+// ... and before a tile's epilogue: slabs g + 1 AND g + 2 landed (only g + 3
+// in flight), so the next tile's first R interval needs no wait and the
+// epilogue's stores (which vmcnt counts in issue order with the LDS-DMAs)
+// get two intervals to retire before a wait covers them
+template <int TM>
+__device__ __forceinline__ void wait_ring_deep() {
+  if constexpr (TM == 256) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+}
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// 16-B chunk swizzle of a 64-B slab row: chunk c of row r sits at c ^ swz(r).
+// A fragment read (lane l: row l % 16, chunk l / 16) is then conflict-free
+// in each of ds_read_b128's four lane groups ({0-3, 12-15, 20-27}, ...:
+// MI355X_MICROARCH.md LDS table): within a group the rows that share a
+// bank-row quarter (equal r % 4) land on four different chunks.  (The
+// (r >> 2) & 3 swizzle of a contiguous-16-lane model is 2-way there.)
+__device__ __forceinline__ int swz(int r) { return ((r >> 3) & 1) << 1; }
+
+__device__ __forceinline__ uint32_t pk2(float lo, float hi) {
+  const bf16x2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+template <int TM, int EPI, bool OUTF32>
+__global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
+  constexpr int kAI = TM / 128;  // A LDS-DMAs per slab and wave
+  constexpr int kMT = TM / 32;   // 16-row MFMA tiles per wave (TM / 2 rows)
+  constexpr int kSlab = slab_bytes(TM), kLds = ring_bytes(TM);
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  // persistent: workgroup b takes tiles b, b + G, ... and the K slabs of all
+  // of them form ONE stream through the LDS ring (the next tile's first
+  // slabs load during this tile's last ones and its epilogue)
+  const int G = (int)gridDim.x, wg = (int)blockIdx.x;
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int T = (ntiles - wg + G - 1) / G;
+  const int nsl = p.K / kSlabK;
+
+  // XCD-aware tile order (bijective): tiles with equal t % 8 run on one XCD
+  // (G is a multiple of 8 or the whole grid); give each XCD a contiguous
+  // M-panel-major run of tile ids, so the tiles an XCD runs together share
+  // their A panel in its L2
+  auto origin = [&](int tl, int& m0, int& n0) {
+    const int t = wg + tl * G;
+    const int x = t & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+    const int id = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + (t >> 3);
+    const int tm = id / p.tiles_n;
+    m0 = tm * TM;
+    n0 = (id - tm * p.tiles_n) * kTile;
+  };
+
+  // ---- LDS-DMA: wave w's instruction i of an operand fills slab rows
+  // 16 (n w + i) .. + 15 (n = that operand's instructions per wave; 1 KB,
+  // lane-linear: row 16 (n w + i) + lane/4, chunk' lane%4) from global
+  // chunk c = chunk' ^ swz(row) of that row
+  int arow[kAI], acol[kAI], brow[2], bcol[2];
+#pragma unroll
+  for (int i = 0; i < kAI; ++i) {
+    arow[i] = 16 * (kAI * wave + i) + (lane >> 2);
+    acol[i] = 8 * ((lane & 3) ^ swz(arow[i]));
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    brow[i] = 16 * (2 * wave + i) + (lane >> 2);
+    bcol[i] = 8 * ((lane & 3) ^ swz(brow[i]));
+  }
+  // staging cursor: the slab stream position gs (its ring buffer gs % 4),
+  // the tile and slab it loads (past the end: the last slab again, into a
+  // buffer nobody reads, so every vmcnt count stays constant) and that
+  // tile's per-lane source rows
+  int gs = 0, st_tl = 0, st_s = 0;
+  const uint16_t* sa[kAI];
+  const uint16_t* sbp[2];
+  auto set_tile = [&](int tl) {
+    int m0, n0;
+    origin(tl, m0, n0);
+#pragma unroll
+    for (int i = 0; i < kAI; ++i) sa[i] = p.A + (size_t)min(m0 + arow[i], p.M - 1) * p.lda + acol[i];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) sbp[i] = p.B + (size_t)(n0 + brow[i]) * p.ldb + bcol[i];
+  };
+  set_tile(0);
+  auto stage = [&]() {
+    uint8_t* dst = lds + (gs & (kRing - 1)) * kSlab;
+    const int k0 = st_s * kSlabK;
+#pragma unroll
+    for (int i = 0; i < kAI; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(sa[i] + k0), (void*)(dst + (kAI * wave + i) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(sbp[i] + k0), (void*)(dst + TM * 64 + (2 * wave + i) * 1024), 16,
+                                       0, 0);
+    ++gs;
+    if (++st_s == nsl) {
+      if (st_tl + 1 < T) {
+        st_s = 0;
+        set_tile(++st_tl);
+      } else {
+        st_s = nsl - 1;
+      }
+    }
+  };
+  // fragment reads: 16-row tile at row R0 (a multiple of 16), lane row R0 +
+  // lane%16, k chunk lane/16 -> swizzled chunk (lane/16) ^ swz(lane % 16)
+  const int lane_off = (lane & 15) * 64 + (((lane >> 4) ^ swz(lane & 15)) << 4);
+  const int a_off = (wr * (TM / 2)) * 64 + lane_off;
+  const int b_off = TM * 64 + (wc * 64) * 64 + lane_off;
+
+  // the bias in LDS behind the ring: an ordinary global load used in the
+  // epilogue would make hipcc wait vmcnt(0) there, draining the ring's
+  // in-flight LDS-DMAs of the next tile
+  float* const bias_l = reinterpret_cast<float*>(lds + kLds);
+  if (EPI >= kEpiBias) {
+    for (int c = tid; c < p.N; c += 512) bias_l[c] = p.bias[c];
+    __syncthreads();
+  }
+  // prologue: slabs 0..2 in flight, slab 0 landed
+  for (int i = 0; i < 3; ++i) stage();
+  wait_ring<TM>();
+  bar();
+  // waves 4-7 run one barrier behind
+  if (__builtin_amdgcn_readfirstlane(wave) >= 4) bar();
+
+  const int col_l = lane & 15, row_l = (lane >> 4) * 4, par = lane & 1;
+  f32x4 acc[kMT][4];
+  v4u a[kMT], b[4];
+  int g = 0;
+  for (int tl = 0; tl < T; ++tl) {
+#pragma unroll
+    for (int i = 0; i < kMT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < nsl; ++s, ++g) {
+      const uint8_t* sb = lds + (g & (kRing - 1)) * kSlab;
+      // ---- R interval: this slab's fragments (the wave's TM / 2 rows x 64
+      // columns), the LDS-DMAs of slab g + 3, slab g + 1 landed ----
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = lds16(sb + b_off + j * 16 * 64);
+#pragma unroll
+      for (int i = 0; i < kMT; ++i) a[i] = lds16(sb + a_off + i * 16 * 64);
+      stage();
+      // this wave's LDS-DMAs of slab g + 1 landed (g + 2, g + 3 in flight);
+      // a tile's first slab: waited for before the last epilogue
+      if (s != 0 || tl == 0) wait_ring<TM>();
+      wait_lgkm0();
+      bar();
+      // ---- M interval: 4 kMT MFMAs ----
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < kMT; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma(a[i], b[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+    }
+
+    wait_ring_deep<TM>();
+    // ---- epilogue of tile tl (no barriers: the other wave group's interval
+    // just runs longer).  C/D map of 16x16x32: col = lane % 16, row =
+    // 4 (lane / 16) + e.  bf16: lanes 2c and 2c + 1 swap halves so each
+    // stores two rows of a column pair as 4-byte words ----
+    int m0, n0;
+    origin(tl, m0, n0);
+    float bj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bj[j] = EPI >= kEpiBias ? bias_l[n0 + wc * 64 + j * 16 + col_l] : 0.f;
+    const bool full = m0 + TM <= p.M;  // block-uniform
+#pragma unroll
+    for (int i = 0; i < kMT; ++i) {
+      const int row0 = m0 + wr * (TM / 2) + i * 16 + row_l;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wc * 64 + j * 16 + col_l;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[i][j][e] + bj[j];
+          if (EPI == kEpiBiasGelu) v[e] = gelu(v[e]);
+        }
+        if constexpr (OUTF32) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (full || row0 + e < p.M) reinterpret_cast<float*>(p.C)[(size_t)(row0 + e) * p.ldc + col] = v[e];
+        } else {
+          const uint32_t send = par ? pk2(v[0], v[1]) : pk2(v[2], v[3]);
+          // lane ^ 1 by DPP quad_perm [1, 0, 3, 2] (a VALU move, no LDS round trip)
+          const uint32_t recv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0xB1, 0xf, 0xf, false);
+          const float r0 = __uint_as_float(recv << 16), r1 = __uint_as_float(recv & 0xffff0000u);
+          // even lane: rows 0, 1 of columns (c, c + 1); odd lane: rows 2, 3 of (c - 1, c)
+          const uint32_t w0 = par ? pk2(r0, v[2]) : pk2(v[0], r0);
+          const uint32_t w1 = par ? pk2(r1, v[3]) : pk2(v[1], r1);
+          const int r = row0 + 2 * par, c = col - par;
+          uint32_t* out = reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(p.C) + (size_t)r * p.ldc + c);
+          if (full || r < p.M) out[0] = w0;
+          if (full || r + 1 < p.M) out[p.ldc / 2] = w1;
+        }
+      }
+    }
+  }
+  if (__builtin_amdgcn_readfirstlane(wave) < 4) bar();  // the same barrier count for all waves
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the re-reads past the last slab
+}
+
+bool a16(const void* q) { return ((uintptr_t)q & 15) == 0; }
+
+int cu_count() {
+  static std::atomic<int> n{0};
+  int v = n.load(std::memory_order_relaxed);
+  if (!v) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    n.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+
+template <int TM, int EPI, bool F32>
+hipError_t launch_tm(const K17Params& prm, int grid, hipStream_t s) {
+  constexpr int kLds = ring_bytes(TM);
+  const int lds_bytes = kLds + (EPI >= kEpiBias ? 4 * prm.N : 0);
+  static std::atomic<uint32_t> attr_done{0};  // one bit per device (<= 32)
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const uint32_t bit = 1u << (dev & 31);
+  if (!(attr_done.load(std::memory_order_acquire) & bit)) {
+    e = hipFuncSetAttribute((const void*)k17_gemm_kernel<TM, EPI, F32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kLds + 4 * kMaxBiasN);
+    if (e != hipSuccess) return e;
+    attr_done.fetch_or(bit, std::memory_order_acq_rel);
+  }
+  hipLaunchKernelGGL((k17_gemm_kernel<TM, EPI, F32>), dim3(grid), dim3(512), lds_bytes, s, prm);
+  return hipGetLastError();
+}
+
+template <int TM>
+hipError_t launch(const K17Params& prm, int grid, hipStream_t s, int epi, int out_f32) {
+  if (out_f32) {
+    if (epi == kEpiNone) return launch_tm<TM, kEpiNone, true>(prm, grid, s);
+    if (epi == kEpiBias) return launch_tm<TM, kEpiBias, true>(prm, grid, s);
+    return launch_tm<TM, kEpiBiasGelu, true>(prm, grid, s);
+  }
+  if (epi == kEpiNone) return launch_tm<TM, kEpiNone, false>(prm, grid, s);
+  if (epi == kEpiBias) return launch_tm<TM, kEpiBias, false>(prm, grid, s);
+  return launch_tm<TM, kEpiBiasGelu, false>(prm, grid, s);
+}
+
+std::atomic<int> g_k17_last_tm{0};
+std::atomic<long long> g_k17_calls{0};
+
+}  // namespace
+
+extern "C" {
+
+// K17: C = A . B^T (+ bias) (GELU) with bf16 A [M][lda], B [N][ldb] (K
+// contiguous), fp32 bias [N], C bf16 (out_f32 = 0) or fp32 [M][ldc].
+// epi: 0 none, 1 bias, 2 bias + GELU (N <= 8192).  N a multiple of 256, K of 32, lda /
+// ldb / ldc multiples of 8, 16-B aligned pointers; any M >= 1.
+int tcamd_k17_gemm(const void* A, const void* B, const float* bias, void* C, int M, int N, int K, int lda, int ldb,
+                   int ldc, int epi, int out_f32, void* stream) {
+  if (M <= 0) return hipSuccess;
+  if (!A || !B || !C || N <= 0 || N % kTile || K <= 0 || K % kSlabK || epi < 0 || epi > 2) return hipErrorInvalidValue;
+  if (lda < K || ldb < K || ldc < N || lda % 8 || ldb % 8 || ldc % 8) return hipErrorInvalidValue;
+  if (!a16(A) || !a16(B) || !a16(C) || (epi && (!bias || ((uintptr_t)bias & 3) || N > kMaxBiasN)))
+    return hipErrorInvalidValue;
+  if ((size_t)M * lda >= (1ull << 31) || (size_t)N * ldb >= (1ull << 31) || (size_t)M * ldc >= (1ull << 31))
+    return hipErrorInvalidValue;  // 32-bit element offsets in the slab sources
+  K17Params prm;
+  prm.A = (const uint16_t*)A;
+  prm.B = (const uint16_t*)B;
+  prm.bias = bias;
+  prm.C = C;
+  prm.M = M;
+  prm.N = N;
+  prm.K = K;
+  prm.lda = lda;
+  prm.ldb = ldb;
+  prm.ldc = ldc;
+  // tile height: 256 (most MFMA work per LDS read) unless 128-row tiles
+  // spread the work over the CUs markedly better (the last round of a
+  // persistent grid is the one that runs partly empty); TCAMD_K17_TM forces
+  const int ncu = cu_count();
+  auto rounds_eff = [&](int tm) {
+    const long t = (long)((M + tm - 1) / tm) * (N / kTile);
+    const long r = (t + ncu - 1) / ncu;
+    return (double)t / (double)(r * ncu) * (tm == 256 ? 1.0 : 0.85);  // 128-row tiles: ~15 % less per tile
+  };
+  int tm = (int)tcamd::knob(tcamd::Knob::K17Tm);
+  if (tm != 128 && tm != 256) tm = rounds_eff(128) > rounds_eff(256) ? 128 : 256;
+  prm.tiles_m = (M + tm - 1) / tm;
+  prm.tiles_n = N / kTile;
+  const int ntiles = prm.tiles_m * prm.tiles_n;
+  const int grid = ntiles <= ncu ? ntiles : ncu / 8 * 8;  // persistent: one workgroup per CU
+  g_k17_last_tm = tm;
+  g_k17_calls.fetch_add(1, std::memory_order_relaxed);
+  hipStream_t s = (hipStream_t)stream;
+  if (tm == 128) return launch<128>(prm, grid, s, epi, out_f32);
+  return launch<256>(prm, grid, s, epi, out_f32);
+}
+
+// tile height of the last tcamd_k17_gemm call (tests, tools)
+int tcamd_k17_last_tm() { return g_k17_last_tm; }
+
+// launches so far (tests: which projections a model routed through K17)
+long long tcamd_k17_calls() { return g_k17_calls.load(std::memory_order_relaxed); }
+
+}  // extern "C"

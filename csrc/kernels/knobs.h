@@ -30,6 +30,7 @@ enum class Knob : int {
   X3sSplit3,       // K13x 3x3 over input quarters (0 = one block, bitwise reproducible)
   PkBigLim,        // K2 pack: output offset past which a block takes the 64-bit byte path
   K3Mode,          // K3 index: 1 = general walk only
+  K17Tm,           // K17 GEMM tile height (0 = by the grid fill, 128, 256)
   kCount
 };
 

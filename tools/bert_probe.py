@@ -2,6 +2,7 @@
 ``rocprofv3 --kernel-trace --stats`` for the per-kernel split.
 
   python tools/bert_probe.py --batch 64 --iters 10
+  python tools/bert_probe.py --batch 1 8 64 --k17 --graphs   # K17 vs hipBLASLt projections, HIP graphs
 """
 
 import argparse
@@ -28,6 +29,8 @@ def main():
     ap.add_argument("--tunable", default="",
                     help="A/B against PyTorch TunableOp (hipBLASLt / rocBLAS solution search per GEMM shape); "
                          "the tuned results go to this CSV path")
+    ap.add_argument("--k17", action="store_true", help="A/B: the K17 projections (bert.K17) against hipBLASLt only")
+    ap.add_argument("--graphs", action="store_true", help="time HIP-graph replays of the forward (as served)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     model = bert.build(device=dev)
@@ -36,6 +39,8 @@ def main():
         mask = torch.ones(b, a.seq, device=dev, dtype=torch.int64)
         tt = torch.zeros(b, a.seq, device=dev, dtype=torch.int64)
         variants = {"default": 0}
+        if a.k17:
+            variants = {"library": 0, "k17": 0}
         tun = None
         if a.tuned_table:
             import torch.cuda.tunable as tun
@@ -55,21 +60,38 @@ def main():
                 tun.tuning_enable(False)
                 tun.enable(False)
         ts = {k: [] for k in variants}
+        graphs = {}
         with torch.no_grad():
             for name in variants:
                 if tun is not None:
                     tun.enable(name == "tunableop")
+                if a.k17:
+                    bert.K17 = name == "k17"
                 for _ in range(2):
                     model(ids, mask, tt)
+                if a.graphs:
+                    s = torch.cuda.Stream()
+                    s.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(s):
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, stream=s):
+                            model(ids, mask, tt)
+                    torch.cuda.current_stream().wait_stream(s)
+                    graphs[name] = g
             torch.cuda.synchronize()
             for _ in range(a.rounds):
                 for name in variants:
                     if tun is not None:
                         tun.enable(name == "tunableop")
+                    if a.k17:
+                        bert.K17 = name == "k17"
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
                     for _ in range(a.iters):
-                        model(ids, mask, tt)
+                        if a.graphs:
+                            graphs[name].replay()
+                        else:
+                            model(ids, mask, tt)
                     torch.cuda.synchronize()
                     ts[name].append((time.perf_counter() - t0) / a.iters)
         for name, v in ts.items():

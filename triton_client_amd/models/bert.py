@@ -36,14 +36,49 @@ TYPES = 2
 
 # fused paths on the GPU (bf16 CUDA tensors); TC_BERT_FUSED=0 runs plain torch ops
 FUSED = os.environ.get("TC_BERT_FUSED", "1") != "0"
+# K17 (the hand-written gfx950 GEMM) for the projections _k17_takes names;
+# off by default: inside the served HIP graphs it measured slower than
+# hipBLASLt at bs1 / bs8 and -1 % at bs64 (profiles/r5_k17_gemm.md)
+K17 = os.environ.get("TC_BERT_K17", "0") == "1"
+def _k17_takes(M, N, K, epilogue):
+    """The projections K17 (csrc/kernels/gemm.hip) matched or beat hipBLASLt on
+    as standalone launches (profiles/r5_k17_gemm.md): the QKV projection (no
+    epilogue) and the attention-out projection (N = K = 1024, bias) up to
+    3,072 tokens; the FFN projections stay on the library."""
+    if epilogue == "none":
+        return N % 256 == 0 and K % 32 == 0
+    return epilogue == "bias" and N * K <= 1024 * 1024 and N % 256 == 0 and K % 32 == 0 and M <= 3072
+
+
+def _k17(x2, lin, epilogue):
+    from triton_client_amd.ops import hip
+
+    M, K = x2.shape
+    N = lin.weight.shape[0]
+    out = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
+    bias = None
+    if epilogue != "none":
+        bias = getattr(lin, "bias_f32", None)
+        if bias is None or bias.device != x2.device:
+            bias = lin.bias_f32 = lin.bias.detach().float().contiguous()
+    hip.k17_gemm(x2.data_ptr(), lin.weight.data_ptr(), None if bias is None else bias.data_ptr(), out.data_ptr(), M, N,
+                 K, x2.stride(0), lin.weight.stride(0), N, epilogue=epilogue,
+                 stream=torch.cuda.current_stream(x2.device).cuda_stream)
+    return out
+
+
 def _proj(x, lin, epilogue="bias"):
-    """lin(x) (epilogue "bias"), gelu(lin(x)) ("bias_gelu") or x @ W^T ("none")
-    on hipBLASLt.  The four projections are plain library GEMMs: a hand-written
-    gfx950 GEMM (K15, rounds 3-4) reached 0.80-0.93x of hipBLASLt at 24,576
-    tokens and made the served forward slower, so it was retired
-    (profiles/r4_gemm_k15.md); config 4 is library-bound on these GEMMs."""
+    """lin(x) (epilogue "bias"), gelu(lin(x)) ("bias_gelu") or x @ W^T ("none").
+    On the GPU in bf16: hipBLASLt, or K17, the hand-written gfx950 GEMM, with
+    TC_BERT_K17=1 (_k17_takes).  Config 4 is library-bound on these GEMMs:
+    K15 (rounds 3-4) reached 0.80-0.93x of hipBLASLt; K17 (round 5) 0.76-1.06x
+    at 24,576 tokens and loses inside the served graphs at small batches."""
     x2 = x.reshape(-1, x.shape[-1])
     n = lin.weight.shape[0]
+    if (FUSED and K17 and x2.is_cuda and x2.dtype == torch.bfloat16 and lin.weight.dtype == torch.bfloat16
+            and x2.stride(1) == 1 and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0 and lin.weight.is_contiguous()
+            and _k17_takes(x2.shape[0], n, x2.shape[1], epilogue)):
+        return _k17(x2, lin, epilogue).view(*x.shape[:-1], n)
     if getattr(lin, "w3", None) is not None and x2.is_cuda and x2.dtype == torch.float32:
         y = _mm_x3(x2, lin.w3)
         if epilogue != "none":

@@ -243,6 +243,13 @@ _SIGS = {
         ctypes.c_int,
     ),
     "tcamd_knob_set": ([ctypes.c_char_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_longlong)], ctypes.c_int),
+    "tcamd_k17_gemm": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "tcamd_k17_last_tm": ([], ctypes.c_int),
+    "tcamd_k17_calls": ([], ctypes.c_longlong),
     "tcamd_x3_cat": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "tcamd_x3_stem": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
@@ -899,6 +906,28 @@ def k3_set_check(on):
     workspace at exactly the size it needs with a 4 KiB canary behind it and
     fails if the canary changed.  Returns the previous setting."""
     return bool(_load().tcamd_k3_set_check(1 if on else 0))
+
+
+K17_EPI = {"none": 0, "bias": 1, "bias_gelu": 2}
+
+
+def k17_gemm(a, b, bias, c, M, N, K, lda, ldb, ldc, epilogue="none", out_f32=False, stream=None):
+    """K17 (csrc/kernels/gemm.hip): C[M, N] = A[M, K] . B[N, K]^T (+ bias) (GELU)
+    with bf16 A and B (K contiguous, row strides lda / ldb), fp32 bias [N], C
+    bf16 or fp32 (``out_f32``) with row stride ldc; fp32 accumulate.  N a
+    multiple of 256, K of 32."""
+    _check(_load().tcamd_k17_gemm(a, b, _vp(bias), c, int(M), int(N), int(K), int(lda), int(ldb), int(ldc),
+                                  K17_EPI[epilogue], 1 if out_f32 else 0, _vp(stream)), "k17_gemm")
+
+
+def k17_last_tm():
+    """Tile height (128 / 256) the last k17_gemm picked (TCAMD_K17_TM forces one)."""
+    return int(_load().tcamd_k17_last_tm())
+
+
+def k17_calls():
+    """K17 launches so far in this process."""
+    return int(_load().tcamd_k17_calls())
 
 
 def knobs():
