@@ -91,24 +91,33 @@ __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
 }
 
-// the counted wait that retires slab g + 1 (slabs g + 2 and g + 3 in flight):
-// 2 x the LDS-DMAs per slab and wave (TM = 256: 2 A + 2 B, TM = 128: 1 + 2)
-template <int TM>
-__device__ __forceinline__ void wait_ring() {
-  if constexpr (TM == 256) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-}
+// A-operand LDS-DMAs per slab of a wave in group 0 (waves 0-3) / group 1
+// (waves 4-7): TM / 16 instructions of 16 rows, split 2 / 2 (256), 2 / 1
+// (192), 1 / 1 (128)
+constexpr int ai0(int tm) { return tm == 128 ? 1 : 2; }
+constexpr int ai1(int tm) { return tm == 256 ? 2 : 1; }
 
-// ... and before a tile's epilogue: slabs g + 1 AND g + 2 landed (only g + 3
-// in flight), so the next tile's first R interval needs no wait and the
-// epilogue's stores (which vmcnt counts in issue order with the LDS-DMAs)
-// get two intervals to retire before a wait covers them
-template <int TM>
-__device__ __forceinline__ void wait_ring_deep() {
-  if constexpr (TM == 256) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-}
+// the counted wait that retires slab g + 1 (slabs g + 2 and g + 3 in
+// flight: 2 x this wave's LDS-DMAs per slab), and the deeper one before a
+// tile's epilogue (slabs g + 1 AND g + 2 landed, only g + 3 in flight) so the
+// next tile's first R interval needs no wait and the epilogue's stores (which
+// vmcnt counts in issue order with the LDS-DMAs) get two intervals to retire
 __device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int TM>
+__device__ __forceinline__ void wait_ring(bool grp1) {
+  if (grp1) vm_wait<2 * (ai1(TM) + 2)>();
+  else vm_wait<2 * (ai0(TM) + 2)>();
+}
+template <int TM>
+__device__ __forceinline__ void wait_ring_deep(bool grp1) {
+  if (grp1) vm_wait<ai1(TM) + 2>();
+  else vm_wait<ai0(TM) + 2>();
+}
 
 // 16-B chunk swizzle of a 64-B slab row: chunk c of row r sits at c ^ swz(r).
 // A fragment read (lane l: row l % 16, chunk l / 16) is then conflict-free
@@ -125,12 +134,15 @@ __device__ __forceinline__ uint32_t pk2(float lo, float hi) {
 
 template <int TM, int EPI, bool OUTF32>
 __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
-  constexpr int kAI = TM / 128;  // A LDS-DMAs per slab and wave
-  constexpr int kMT = TM / 32;   // 16-row MFMA tiles per wave (TM / 2 rows)
+  constexpr int kAI = ai0(TM);  // the most A LDS-DMAs per slab of a wave
+  constexpr int kMT = TM / 32;  // 16-row MFMA tiles per wave (TM / 2 rows)
   constexpr int kSlab = slab_bytes(TM), kLds = ring_bytes(TM);
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
+  const bool grp1 = __builtin_amdgcn_readfirstlane(wave) >= 4;  // wave-uniform
+  const int nai = grp1 ? ai1(TM) : ai0(TM);                     // this wave's A LDS-DMAs per slab
+  const int arow0 = grp1 ? 64 * ai0(TM) + 16 * ai1(TM) * (wave - 4) : 16 * ai0(TM) * wave;
   // persistent: workgroup b takes tiles b, b + G, ... and the K slabs of all
   // of them form ONE stream through the LDS ring (the next tile's first
   // slabs load during this tile's last ones and its epilogue)
@@ -159,7 +171,7 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
   int arow[kAI], acol[kAI], brow[2], bcol[2];
 #pragma unroll
   for (int i = 0; i < kAI; ++i) {
-    arow[i] = 16 * (kAI * wave + i) + (lane >> 2);
+    arow[i] = arow0 + 16 * i + (lane >> 2);
     acol[i] = 8 * ((lane & 3) ^ swz(arow[i]));
   }
 #pragma unroll
@@ -188,7 +200,8 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
     const int k0 = st_s * kSlabK;
 #pragma unroll
     for (int i = 0; i < kAI; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(sa[i] + k0), (void*)(dst + (kAI * wave + i) * 1024), 16, 0, 0);
+      if (i < nai)
+        __builtin_amdgcn_global_load_lds((const void*)(sa[i] + k0), (void*)(dst + (arow0 / 16 + i) * 1024), 16, 0, 0);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(sbp[i] + k0), (void*)(dst + TM * 64 + (2 * wave + i) * 1024), 16,
@@ -219,10 +232,10 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
   }
   // prologue: slabs 0..2 in flight, slab 0 landed
   for (int i = 0; i < 3; ++i) stage();
-  wait_ring<TM>();
+  wait_ring<TM>(grp1);
   bar();
   // waves 4-7 run one barrier behind
-  if (__builtin_amdgcn_readfirstlane(wave) >= 4) bar();
+  if (grp1) bar();
 
   const int col_l = lane & 15, row_l = (lane >> 4) * 4, par = lane & 1;
   f32x4 acc[kMT][4];
@@ -244,7 +257,7 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
       stage();
       // this wave's LDS-DMAs of slab g + 1 landed (g + 2, g + 3 in flight);
       // a tile's first slab: waited for before the last epilogue
-      if (s != 0 || tl == 0) wait_ring<TM>();
+      if (s != 0 || tl == 0) wait_ring<TM>(grp1);
       wait_lgkm0();
       bar();
       // ---- M interval: 4 kMT MFMAs ----
@@ -257,7 +270,7 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
       bar();
     }
 
-    wait_ring_deep<TM>();
+    wait_ring_deep<TM>(grp1);
     // ---- epilogue of tile tl (no barriers: the other wave group's interval
     // just runs longer).  C/D map of 16x16x32: col = lane % 16, row =
     // 4 (lane / 16) + e.  bf16: lanes 2c and 2c + 1 swap halves so each
@@ -300,7 +313,7 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
       }
     }
   }
-  if (__builtin_amdgcn_readfirstlane(wave) < 4) bar();  // the same barrier count for all waves
+  if (!grp1) bar();  // the same barrier count for all waves
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the re-reads past the last slab
 }
 
@@ -380,17 +393,20 @@ int tcamd_k17_gemm(const void* A, const void* B, const float* bias, void* C, int
   prm.lda = lda;
   prm.ldb = ldb;
   prm.ldc = ldc;
-  // tile height: 256 (most MFMA work per LDS read) unless 128-row tiles
-  // spread the work over the CUs markedly better (the last round of a
-  // persistent grid is the one that runs partly empty); TCAMD_K17_TM forces
+  // tile height: the one whose persistent grid finishes first -- rounds of
+  // tiles per CU x tile time (a 192- / 128-row tile costs ~0.9 / ~0.72 of a
+  // 256-row one, measured: profiles/r5_k17_gemm.md); TCAMD_K17_TM forces one
   const int ncu = cu_count();
-  auto rounds_eff = [&](int tm) {
+  auto makespan = [&](int tm) {
     const long t = (long)((M + tm - 1) / tm) * (N / kTile);
-    const long r = (t + ncu - 1) / ncu;
-    return (double)t / (double)(r * ncu) * (tm == 256 ? 1.0 : 0.85);  // 128-row tiles: ~15 % less per tile
+    return (double)((t + ncu - 1) / ncu) * (tm == 256 ? 1.0 : tm == 192 ? 0.9 : 0.72);
   };
   int tm = (int)tcamd::knob(tcamd::Knob::K17Tm);
-  if (tm != 128 && tm != 256) tm = rounds_eff(128) > rounds_eff(256) ? 128 : 256;
+  if (tm != 128 && tm != 192 && tm != 256) {
+    tm = 256;
+    for (int c : {192, 128})
+      if (makespan(c) < makespan(tm) * 0.97) tm = c;
+  }
   prm.tiles_m = (M + tm - 1) / tm;
   prm.tiles_n = N / kTile;
   const int ntiles = prm.tiles_m * prm.tiles_n;
@@ -399,6 +415,7 @@ int tcamd_k17_gemm(const void* A, const void* B, const float* bias, void* C, int
   g_k17_calls.fetch_add(1, std::memory_order_relaxed);
   hipStream_t s = (hipStream_t)stream;
   if (tm == 128) return launch<128>(prm, grid, s, epi, out_f32);
+  if (tm == 192) return launch<192>(prm, grid, s, epi, out_f32);
   return launch<256>(prm, grid, s, epi, out_f32);
 }
 

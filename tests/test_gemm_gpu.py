@@ -40,7 +40,7 @@ def _case(M, N, K, lda=None, ldb=None, seed=0):
                                    (3072, 1024, 1024), (300, 256, 64), (1, 256, 32), (517, 512, 96),
                                    (256, 768, 160), (1000, 1280, 2048)])
 @pytest.mark.parametrize("epi", ["none", "bias", "bias_gelu"])
-@pytest.mark.parametrize("tm", [128, 256])
+@pytest.mark.parametrize("tm", [128, 192, 256])
 def test_k17_gemm_bf16_out(M, N, K, epi, tm):
     """Both tile heights (TCAMD_K17_TM; by default picked from how evenly the
     tiles fill the CUs)."""
@@ -68,7 +68,7 @@ def test_k17_gemm_bf16_out(M, N, K, epi, tm):
 
 @pytest.mark.parametrize("M,N,K,lda,ldb", [(384, 1024, 3072, 3072, 3072), (777, 512, 192, 256, 200)])
 @pytest.mark.parametrize("epi", ["none", "bias"])
-@pytest.mark.parametrize("tm", [128, 256])
+@pytest.mark.parametrize("tm", [128, 192, 256])
 def test_k17_gemm_fp32_out_strided(M, N, K, lda, ldb, epi, tm):
     """fp32 output (the fp32-parity bert's [x_hi|x_hi|x_lo] . [W_hi|W_lo|W_hi]
     GEMM, K = 3 x hidden) and row strides larger than K."""

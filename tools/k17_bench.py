@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--json", default="")
     ap.add_argument("--proj", default="", help="only these projections (comma-separated names)")
-    ap.add_argument("--arms", default="k17,hipblaslt", help="k17, k17_t128, k17_t256, hipblaslt (one arm: PMC passes)")
+    ap.add_argument("--arms", default="k17,hipblaslt", help="k17, k17_t128, k17_t192, k17_t256, hipblaslt (one arm: PMC passes)")
     a = ap.parse_args()
     import torch
 
@@ -69,8 +69,8 @@ def main():
             else:
                 def lib():
                     torch._addmm_activation(bias16, x, w.t(), use_gelu=True)
-            arms = {k: v for k, v in (("k17", k17), ("k17_t128", k17_tm(128)), ("k17_t256", k17_tm(256)),
-                                      ("hipblaslt", lib)) if k in a.arms.split(",")}
+            arms = {k: v for k, v in (("k17", k17), ("k17_t128", k17_tm(128)), ("k17_t192", k17_tm(192)),
+                                      ("k17_t256", k17_tm(256)), ("hipblaslt", lib)) if k in a.arms.split(",")}
             for f in arms.values():
                 f()
             torch.cuda.synchronize()
