@@ -72,16 +72,21 @@ __device__ __forceinline__ f32x4 mma(v4u a, v4u b, f32x4 c) {
                                                  0, 0);
 }
 
-// GELU(x) = x/2 (1 + erf(x / sqrt 2)), erf by Abramowitz-Stegun 7.1.26
-// (|error| <= 1.5e-7, far below bf16's rounding), with the hardware
-// reciprocal and exp2 (v_rcp_f32, v_exp_f32: ~1 ulp): the epilogue runs
-// between barriers, so every instruction of it stalls the other wave group
-__device__ __forceinline__ float gelu(float x) {
-  const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * z);
-  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
-  const float e = 1.0f - poly * __builtin_amdgcn_exp2f(-1.4426950408889634f * z * z);
-  return 0.5f * x * (1.0f + __builtin_copysignf(e, x));
+// GELU in its tanh form, x sigmoid(2 sqrt(2/pi) (x + 0.044715 x^3)) (the
+// form hipBLASLt's GELU epilogue -- bert's library path -- computes; within
+// 5e-4 of the erf form, far below bf16's rounding), on column pairs: the
+// multiplies/FMAs as packed f32 (v_pk_*: two columns per issue), exp2 and the
+// reciprocal on the transcendental unit.  The epilogue runs between barriers,
+// so every instruction of it stalls the other wave group: ~14 issue cycles
+// per element (the erf form with scalar f32 took ~34; FFN-up at 24,576
+// tokens 219.8 -> 200.3 us, profiles/r5_k17_gemm.md)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu2(f32x2 x) {
+  constexpr float kC1 = -2.3022081983f;            // -2 sqrt(2/pi) log2(e)
+  constexpr float kC3 = kC1 * 0.044715f;
+  const f32x2 w = x * __builtin_elementwise_fma(x * x, f32x2{kC3, kC3}, f32x2{kC1, kC1});
+  const f32x2 d = f32x2{__builtin_amdgcn_exp2f(w.x), __builtin_amdgcn_exp2f(w.y)} + 1.0f;
+  return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};  // x -> -inf: x * 0
 }
 
 // raw barrier (no vmcnt(0): the ring's LDS-DMAs stay in flight across it);
@@ -287,12 +292,16 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = n0 + wc * 64 + j * 16 + col_l;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = acc[i][j][e] + bj[j];
-          if (EPI == kEpiBiasGelu) v[e] = gelu(v[e]);
+        f32x2 v01 = f32x2{acc[i][j][0], acc[i][j][1]}, v23 = f32x2{acc[i][j][2], acc[i][j][3]};
+        if (EPI >= kEpiBias) {
+          v01 += bj[j];
+          v23 += bj[j];
         }
+        if (EPI == kEpiBiasGelu) {
+          v01 = gelu2(v01);
+          v23 = gelu2(v23);
+        }
+        const float v[4] = {v01.x, v01.y, v23.x, v23.y};
         if constexpr (OUTF32) {
 #pragma unroll
           for (int e = 0; e < 4; ++e)

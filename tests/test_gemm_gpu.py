@@ -24,7 +24,9 @@ def _hip():
 
 
 def _gelu(x):
-    return 0.5 * x * (1.0 + torch.erf(x / 2 ** 0.5))
+    """The tanh form K17 computes (as hipBLASLt's GELU epilogue does); the erf
+    form differs by up to 5e-4, which is 3e-2 of a -0.004 output at x = -3."""
+    return torch.nn.functional.gelu(x, approximate="tanh")
 
 
 def _case(M, N, K, lda=None, ldb=None, seed=0):

@@ -67,11 +67,13 @@ def main():
                     tun.enable(name == "tunableop")
                 if a.k17:
                     bert.K17 = name == "k17"
-                for _ in range(2):
-                    model(ids, mask, tt)
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):  # warm-up on the capture stream (K17 allocates its workspace there)
+                    for _ in range(2):
+                        model(ids, mask, tt)
+                torch.cuda.current_stream().wait_stream(s)
                 if a.graphs:
-                    s = torch.cuda.Stream()
-                    s.wait_stream(torch.cuda.current_stream())
                     with torch.cuda.stream(s):
                         g = torch.cuda.CUDAGraph()
                         with torch.cuda.graph(g, stream=s):
