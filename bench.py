@@ -70,6 +70,8 @@ def parse_args(argv=None):
     ap.add_argument("--concurrency", type=int, default=48, help="requests in flight per GPU")
     ap.add_argument("--window", type=int, default=16, help="requests per step = window x concurrency")
     ap.add_argument("--bs1-concurrency", type=int, default=64)
+    ap.add_argument("--bs1-lanes", type=int, default=1,
+                    help="client lanes (connection + worker thread each) sharing the bs=1 concurrency")
     ap.add_argument("--fanout", default="rccl", choices=["rccl", "p2p", "local"])
     ap.add_argument("--fanout-fallback", default="none", choices=["none", "local"],
                     help="none (default): a failed RCCL broadcast ends the run non-zero with the error; "
@@ -139,6 +141,46 @@ class Point:
 
     def close(self):
         self.s.close()
+
+
+class Lanes:
+    """`sum(conc)` requests in flight over several client lanes against one
+    server: each lane is its own Point (gRPC connection, I/O thread, engine
+    worker thread), the way perf_analyzer spreads a concurrency over its worker
+    threads.  run(n) runs n / lanes requests on every lane at once."""
+
+    def __init__(self, points):
+        self.points = points
+        self.conc = sum(p.conc for p in points)
+        self.s = points[0].s  # server statistics are per model, any lane reads them
+
+    def run(self, n):
+        import threading
+
+        import numpy as np
+
+        k = len(self.points)
+        out = [None] * k
+        errs = []
+
+        def go(i):
+            try:
+                out[i] = self.points[i].run(n // k)
+            except Exception as e:  # noqa: BLE001 -- re-raised below
+                errs.append(e)
+
+        th = [threading.Thread(target=go, args=(i,)) for i in range(k)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
+        return (np.concatenate([o[0] for o in out]), np.concatenate([o[1] for o in out]), max(o[2] for o in out))
+
+    def close(self):
+        for p in self.points:
+            p.close()
 
 
 def windows(end_ns, per, k):
@@ -458,14 +500,17 @@ def main():
 
         # ---- bs=1 on the same server -------------------------------------------------
         _, in1 = make_input("data_1_in", 1)
-        p1 = Point(srv, model, 1, args.bs1_concurrency, "data_1_in", in1, dev, cpu)
-        points.append(p1)
+        nl = max(1, args.bs1_lanes)
+        if args.bs1_concurrency % nl:
+            raise SystemExit("--bs1-concurrency must be a multiple of --bs1-lanes")
+        p1 = Lanes([Point(srv, model, 1, args.bs1_concurrency // nl, "data_1_in", in1, dev, cpu) for _ in range(nl)])
+        points.extend(p1.points)
         n1 = 64 * args.bs1_concurrency  # ~0.2 s at 20k infer/s: the batch groups of a closed loop need time to settle
         p1.run(n1 // 4)
         s10, b10 = p1.s.server_stats(), batch_stats(client, model)
         l1, e1, el1 = measure(p1, 4, n1 // 4)
         s11, b11 = p1.s.server_stats(), batch_stats(client, model)
-        bs1 = {"concurrency": args.bs1_concurrency, "infer_per_sec": round(world * n1 / el1, 1)}
+        bs1 = {"concurrency": args.bs1_concurrency, "client_lanes": nl, "infer_per_sec": round(world * n1 / el1, 1)}
         # where a bs=1 request's latency goes at this concurrency: rows per
         # batch, queueing, and the request-weighted device time of its batch
         bd64 = stats_delta(s10, s11)
