@@ -101,21 +101,24 @@ def test_k17_gemm_rejects_bad_shapes():
 
 
 def test_bert_projections_k17_vs_library(monkeypatch):
-    """bert's _proj routes the QKV (no epilogue, any batch) and the
-    attention-out projection (bias, <= 3,072 tokens) through K17
-    (TC_BERT_K17=1) and the rest through hipBLASLt; each routed projection
-    agrees with the library path to bf16 rounding."""
+    """bert's _proj routes the QKV (no epilogue) and FFN-up + GELU projections
+    from TC_BERT_K17_MIN_TOKENS tokens and the attention-out projection (bias,
+    <= 3,072 tokens) through K17 (TC_BERT_K17=1), the rest through hipBLASLt;
+    each routed projection agrees with the library path to bf16 rounding
+    (both compute the tanh form of GELU)."""
     hip = _hip()
     from triton_client_amd.models import bert
 
     g = torch.Generator(device=DEV).manual_seed(5)
-    for tokens in (384, 3072):
+    big = bert.K17_MIN_TOKENS
+    for tokens in (384, 3072, big):
         x = torch.randn(tokens, 1024, device=DEV, generator=g).to(torch.bfloat16)
-        for N, K, epi, routed in ((3072, 1024, "none", True), (1024, 1024, "bias", True),
-                                  (4096, 1024, "bias_gelu", False)):
+        for N, K, epi in ((3072, 1024, "none"), (1024, 1024, "bias"), (4096, 1024, "bias_gelu"),
+                          (1024, 4096, "bias")):
+            routed = tokens >= big if epi in ("none", "bias_gelu") else (K == 1024 and tokens <= 3072)
             lin = torch.nn.Linear(K, N).to(DEV, torch.bfloat16)
             xin = x if K == 1024 else torch.randn(tokens, K, device=DEV, generator=g).to(torch.bfloat16)
-            assert bert._k17_takes(tokens, N, K, epi) == routed
+            assert bert._k17_takes(tokens, N, K, epi) == routed, (tokens, N, K, epi)
             monkeypatch.setattr(bert, "K17", True)
             before = hip.k17_calls()
             got = bert._proj(xin, lin, epi).float()

@@ -37,17 +37,24 @@ TYPES = 2
 # fused paths on the GPU (bf16 CUDA tensors); TC_BERT_FUSED=0 runs plain torch ops
 FUSED = os.environ.get("TC_BERT_FUSED", "1") != "0"
 # K17 (the hand-written gfx950 GEMM) for the projections _k17_takes names;
-# off by default: inside the served HIP graphs it measured slower than
-# hipBLASLt at bs1 / bs8 and -1 % at bs64 (profiles/r5_k17_gemm.md)
+# off by default: inside the served HIP graphs the forward is slower with it
+# at every batch (bs1 +16 %, bs8 +6 %, bs64 +3-6 %, profiles/r5_k17_gemm.md)
+# although the large-M shapes match or beat hipBLASLt as standalone launches
 K17 = os.environ.get("TC_BERT_K17", "0") == "1"
+K17_MIN_TOKENS = int(os.environ.get("TC_BERT_K17_MIN_TOKENS", "12288"))
+
+
 def _k17_takes(M, N, K, epilogue):
     """The projections K17 (csrc/kernels/gemm.hip) matched or beat hipBLASLt on
     as standalone launches (profiles/r5_k17_gemm.md): the QKV projection (no
-    epilogue) and the attention-out projection (N = K = 1024, bias) up to
-    3,072 tokens; the FFN projections stay on the library."""
-    if epilogue == "none":
-        return N % 256 == 0 and K % 32 == 0
-    return epilogue == "bias" and N * K <= 1024 * 1024 and N % 256 == 0 and K % 32 == 0 and M <= 3072
+    epilogue) and FFN-up + GELU from TC_BERT_K17_MIN_TOKENS tokens (1.04-1.06x
+    and 0.99-1.00x at 24,576), the attention-out projection (N = K = 1024,
+    bias) up to 3,072 tokens; FFN-down stays on the library."""
+    if N % 256 or K % 32:
+        return False
+    if epilogue in ("none", "bias_gelu"):
+        return M >= K17_MIN_TOKENS
+    return epilogue == "bias" and N * K <= 1024 * 1024 and M <= 3072
 
 
 def _k17(x2, lin, epilogue):

@@ -70,7 +70,10 @@ KNOBS = [
     Knob("TC_BERT_FUSED", "python", 1, "models/bert.py FUSED",
          "K11 / K12 fused kernels on the GPU; 0 = plain torch ops", "tests/test_bert_kernels_gpu.py::test_bert_fused_layers_match_torch_ops"),
     Knob("TC_BERT_K17", "python", 0, "models/bert.py K17",
-         "1 = K17 (hand-written GEMM) for the QKV / attention-out projections (_k17_takes); 0 = hipBLASLt",
+         "1 = K17 (hand-written GEMM) for the projections _k17_takes names; 0 = hipBLASLt",
+         "tests/test_gemm_gpu.py::test_bert_projections_k17_vs_library"),
+    Knob("TC_BERT_K17_MIN_TOKENS", "python", 12288, "models/bert.py K17_MIN_TOKENS",
+         "with TC_BERT_K17=1: tokens from which QKV and FFN-up + GELU go to K17",
          "tests/test_gemm_gpu.py::test_bert_projections_k17_vs_library"),
     Knob("TC_BERT_TUNED_GEMMS", "python", 0, "models/bert.py use_tuned_gemms",
          "TunableOp with the committed gfx950 solution table (process-wide; measured neutral)",
