@@ -54,6 +54,16 @@ def test_bench_spawns_ranks_and_aggregates(gpus):
         assert "fanned out by gloo" in res["data"]
 
 
+def test_bench_bs1_over_two_client_lanes():
+    """--bs1-lanes 2: the bs=1 concurrency split over two client connections /
+    worker threads; the JSON says so and the breakdown still reads the
+    server's statistics."""
+    res, _ = _bench("--steps", "2", "--bs1-lanes", "2")
+    assert res["bs1"]["client_lanes"] == 2 and res["bs1"]["concurrency"] == 4
+    assert res["bs1"]["infer_per_sec"] > 0 and res["bs1"]["p99_latency_us"] >= res["bs1"]["p50_latency_us"] > 0
+    assert res["bs1"]["breakdown_rank0"]["avg_rows_per_batch"] >= 1
+
+
 @pytest.mark.slow
 def test_bench_eight_ranks_on_cpu():
     """The driver's N=8 launch, rehearsed on the CPU (verdict r4 #6): 8 ranks,
