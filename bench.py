@@ -690,11 +690,18 @@ def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout
         points.append(pt)
         per = max(64, 8 * c)
         pt.run(max(args.warmup, 1) * per)
+        s0, b0 = pt.s.server_stats(), batch_stats(client, model)
         lat, _, elapsed = measure(pt, args.steps, per)
+        s1, b1 = pt.s.server_stats(), batch_stats(client, model)
         all_lat = fanout.gather_arrays(lat.astype(np.int64)).astype(np.float64)
         row = {"concurrency": c, "infer_per_sec": round(world * args.steps * per / elapsed, 1),
                "p50_latency_us": round(percentile_us(all_lat, 50), 1),
                "p99_latency_us": round(percentile_us(all_lat, 99), 1), "ms_per_step": round(1e3 * elapsed / args.steps, 3)}
+        # rank 0's server over the timed window: rows per executed batch, queueing, device time per batch
+        bd = stats_delta(s0, s1)
+        bd["batch_rows_histogram"] = {str(k): int(b1[k][0] - b0.get(k, (0,))[0]) for k in sorted(b1)
+                                      if b1[k][0] - b0.get(k, (0,))[0] > 0}
+        row["breakdown_rank0"] = bd
         sweep.append(row)
         log("bert c%d: %.1f infer/s p99 %.0f us" % (c, row["infer_per_sec"], row["p99_latency_us"]))
     top = sweep[-1]
