@@ -39,7 +39,7 @@ from .types import DeviceView, OutputTensor, ServerError
 # padding rows cost full compute: under the headline load (bs8 requests, 128-row
 # preferred batches) batches average 109-124 rows, which power-of-two buckets
 # padded to 128 (3-15% of the device time spent on padding)
-BUCKETS = (1, 2, 4, 8, 16) + tuple(range(24, 129, 8)) + tuple(range(144, 257, 16))
+BUCKETS = (1, 2, 4, 8, 12, 16, 20) + tuple(range(24, 129, 8)) + tuple(range(144, 257, 16))
 
 
 class DensenetOnnx(Model):
