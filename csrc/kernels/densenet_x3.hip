@@ -2744,13 +2744,18 @@ int tcamd_x3_small_tiles(int imgs, int W) {
   const int opts14[2] = {2, 4}, opts7[3] = {1, 2, 4};
   const int* o = W == 14 ? opts14 : opts7;
   const int n = W == 14 ? 2 : 3;
+  const int padded = (imgs + 7) / 8 * 8;
   for (int i = 0; i < n; ++i)
-    if ((imgs + 7) / 8 * 8 * o[i] >= ncu) return o[i];
+    if (padded * o[i] >= ncu) return o[i];
+  // 14x14 images too few to fill the CUs with quarters: 2-row tiles (7 per
+  // image) while they still fit one round (bs8-32: -20..23 % per layer; at 7x7
+  // a 7-way split gains nothing; profiles/r5_k14x_tiles.md)
+  if (W == 14 && padded * 7 <= ncu) return 7;
   return o[n - 1];
 }
 
 // K14x: one dense layer of the 14x14 or 7x7 block in one kernel, `tiles`
-// tiles per image (14x14: 2 or 4, 7x7: 1, 2 or 4; <= 0: the chip-filling
+// tiles per image (14x14: 2, 4 or 7, 7x7: 1, 2, 4 or 7; <= 0: the chip-filling
 // default above); w1 in x3_w1_fragments, w2 in x3_w3f_fragments.  K a
 // multiple of 32 in 64..2048.
 int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K, const float* s1, const float* t1,
@@ -2765,7 +2770,7 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
     return hipErrorInvalidValue;
   if ((size_t)imgs * H * W >= (1u << 30) / 4) return hipErrorInvalidValue;
   if (tiles <= 0) tiles = tcamd_x3_small_tiles(imgs, W);
-  const int ti = tiles == 1 ? 0 : tiles == 2 ? 1 : tiles == 4 ? 2 : -1;
+  const int ti = tiles == 1 ? 0 : tiles == 2 ? 1 : tiles == 4 ? 2 : tiles == 7 ? 3 : -1;
   if (ti < 0 || (W == 14 && ti == 0)) return hipErrorInvalidValue;
   X3SmallParams p;
   p.x = x;
@@ -2789,11 +2794,12 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
       return hipErrorOutOfMemory;
     p.stamps = g_x3s_stamps;
   }
-  // [14x14 / 7x7][1 / 2 / 4 tiles per image]
-  const void* const fns[2][3] = {
-      {nullptr, (const void*)x3_dense_small_kernel<14, 2>, (const void*)x3_dense_small_kernel<14, 4>},
+  // [14x14 / 7x7][1 / 2 / 4 / 7 tiles per image]
+  const void* const fns[2][4] = {
+      {nullptr, (const void*)x3_dense_small_kernel<14, 2>, (const void*)x3_dense_small_kernel<14, 4>,
+       (const void*)x3_dense_small_kernel<14, 7>},
       {(const void*)x3_dense_small_kernel<7, 1>, (const void*)x3_dense_small_kernel<7, 2>,
-       (const void*)x3_dense_small_kernel<7, 4>}};
+       (const void*)x3_dense_small_kernel<7, 4>, (const void*)x3_dense_small_kernel<7, 7>}};
   constexpr int kLds = 4 * kWsStage + 1024;  // 4 K-step stages + the dbg-64 timeline
   static std::atomic<bool> attr_set[kMaxDevices];
   const int dev_slot = device_slot();

@@ -314,10 +314,10 @@ def test_x3_dense_fused(imgs, H, K, version):
 @pytest.mark.parametrize("imgs,H,K", [(1, 14, 64), (3, 14, 256), (8, 14, 288), (9, 14, 992), (17, 14, 640),
                                       (128, 14, 512), (16, 14, 96), (1, 7, 512), (5, 7, 992), (64, 7, 768),
                                       (130, 7, 544), (2, 7, 64), (40, 14, 416)])
-@pytest.mark.parametrize("tiles", [1, 2, 4])
+@pytest.mark.parametrize("tiles", [1, 2, 4, 7])
 def test_x3_dense_small(imgs, H, K, tiles):
     """K14x: the whole dense layer of a 14x14 or 7x7 block in one kernel over
-    row tiles of the images (tiles per image: 14x14 2 or 4, 7x7 1, 2 or 4;
+    row tiles of the images (tiles per image: 14x14 2, 4 or 7, 7x7 1, 2, 4 or 7;
     every tile recomputes the 1x1 of its halo rows), z in a zero-padded LDS
     image of the tile.  Ragged image counts (not multiples of 8: the grid
     groups the tiles of images 8g+j), uneven tiles (14 rows in 4 tiles, 7 in 2
@@ -367,16 +367,24 @@ def test_x3_dense_small(imgs, H, K, tiles):
 
 
 def test_x3_small_tiles_fill_the_chip():
-    """The default tiling: the fewest tiles per image that give every CU a workgroup."""
+    """The default tiling: the fewest tiles per image that give every CU a
+    workgroup; 14x14 images too few for that with quarters take 7 two-row
+    tiles while those still fit one round of the CUs."""
     _need_gpu()
     hip = _hip()
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    for imgs in (1, 8, 32, 64, 128, 256):
+    for imgs in (1, 8, 24, 32, 40, 64, 128, 256):
         for W, opts in ((14, (2, 4)), (7, (1, 2, 4))):
             t = hip.x3_small_tiles(imgs, W)
-            assert t in opts
-            fill = [o for o in opts if (imgs + 7) // 8 * 8 * o >= ncu]
-            assert t == (fill[0] if fill else opts[-1]), (imgs, W, t)
+            padded = (imgs + 7) // 8 * 8
+            fill = [o for o in opts if padded * o >= ncu]
+            if fill:
+                want = fill[0]
+            elif W == 14 and padded * 7 <= ncu:
+                want = 7
+            else:
+                want = opts[-1]
+            assert t == want, (imgs, W, t)
 
 
 def test_x3_dense_small_rejects_bad_shapes():
@@ -497,6 +505,29 @@ def test_k14x_routing_follows_stream_concurrency(fp32_engine):
         assert not eng._small_fused(64, 28)
     finally:
         eng.smallf_min_blocks, eng.concurrent_streams = keep
+
+
+def test_k14x_seven_tiles_fit_the_stream_share(fp32_engine):
+    """Small 14x14 batches take 7 two-row tiles per image when those fit one
+    round of the engine's share of the CUs (all of them on one stream, half
+    on two), else quarters; 7x7 never takes 7; TCAMD_X3_SMALLF_TILES wins."""
+    eng, _ = fp32_engine
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    keep = eng.smallf_tiles, eng.concurrent_streams
+    try:
+        eng.smallf_tiles = 0
+        for streams in (1, 2):
+            eng.concurrent_streams = streams
+            for b in (8, 16, 24, 32, 40):
+                padded = (b + 7) // 8 * 8
+                want = 7 if padded * 4 < ncu and padded * 7 <= ncu // streams else \
+                    (2 if padded * 2 >= ncu else 4)
+                assert eng._small_tiles(b, 14) == want, (streams, b)
+                assert eng._small_tiles(b, 7) != 7
+        eng.smallf_tiles = 2
+        assert eng._small_tiles(16, 14) == 2
+    finally:
+        eng.smallf_tiles, eng.concurrent_streams = keep
 
 
 _ROUTES = [{"fuse_min_tiles": 0}, {"fuse_big_k_min_tiles": 1}, {"fuse_v3": 0}, {"fuse_v3": 16},

@@ -233,7 +233,7 @@ class FusedDenseNetFP32:
                     hip.x3_dense_small(fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(),
                                        L["w1fh"].data_ptr(), L["w1fl"].data_ptr(), L["b1"].data_ptr(),
                                        L["w2fh"].data_ptr(), L["w2fl"].data_ptr(), fp + 4 * L["cin"], ctot, stream=st,
-                                       tiles=self.smallf_tiles)
+                                       tiles=self._small_tiles(b, hw))
                 self._transition(bi, fp, ctot, b, hw, ws, wsb, st)
                 continue
             ch = self.chain[bi]
@@ -300,13 +300,27 @@ class FusedDenseNetFP32:
                            T["wh"].data_ptr(), T["wl"].data_ptr(), y=self.feat[bi + 1].data_ptr(), ldy=nct,
                            pool=1, H=hw, W=hw, ws=ws, ws_bytes=wsb, stream=st, N=ctot // 2)
 
+    def _small_tiles(self, b, hw):
+        """K14x row tiles per image: TCAMD_X3_SMALLF_TILES, else the native
+        chip-filling choice, except that the 7-tile split of small 14x14 batches
+        must fit one round of this stream's share of the CUs (on 2 streams at
+        bs32 it oversubscribes them: -5.6 %, profiles/r5_k14x_tiles.md)."""
+        if self.smallf_tiles:
+            return self.smallf_tiles
+        t = hip.x3_small_tiles(b, hw)
+        if t == 7 and (b + 7) // 8 * 8 * 7 > _cu_count(self.device) // max(1, self.concurrent_streams):
+            t = 4
+        return t
+
     def _small_fused(self, b, hw):
         thr = self.smallf_min_blocks
         if thr is None:
             thr = 48 if self.concurrent_streams > 1 else 80
         if thr <= 0 or hw not in (7, 14):
             return False
-        tiles = self.smallf_tiles or hip.x3_small_tiles(b, hw)
+        # the thresholds count workgroups at up to 4 row tiles per image (the
+        # 7-tile split of small 14x14 batches came later and did not move them)
+        tiles = min(self._small_tiles(b, hw), 4)
         return b * tiles >= thr
 
     def _fuse_max_k(self, M):

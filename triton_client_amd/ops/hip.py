@@ -770,7 +770,7 @@ def x3_dense_fused(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo
 def x3_dense_small(x, ldx, imgs, H, W, K, s1, t1, w1f_hi, w1f_lo, b1, w2_hi, w2_lo, y, ldy, stream=None, tiles=0):
     """K14x: one fp32-parity dense layer of the 14x14 or 7x7 block in ONE
     kernel, ``tiles`` row tiles per image (each with the halo rows its 3x3
-    needs, recomputed; 14x14: 2 or 4, 7x7: 1, 2 or 4; 0 = the fewest that give
+    needs, recomputed; 14x14: 2, 4 or 7, 7x7: 1, 2, 4 or 7; 0 = the fewest that give
     every CU a workgroup, :func:`x3_small_tiles`), z kept in a zero-padded LDS
     image of the tile.  ``w1f_*`` in x3_w1_fragments, ``w2_*`` in
     x3_w3f_fragments; K a multiple of 32 in 64..2048."""
