@@ -491,14 +491,15 @@ def test_fp32_engine_k14x_blocks_match_fp32_module(fp32_engine, b):
 
 def test_k14x_routing_follows_stream_concurrency(fp32_engine):
     """TCAMD_X3_SMALLF_MIN_BLOCKS unset: K14x takes the 14x14 / 7x7 blocks from
-    48 workgroups (images x row tiles) when the engine is one of several
-    concurrent streams, from 80 on one stream (profiles/r5_engine_ab.md)."""
+    48 workgroups (images x row tiles, counted at up to 4 tiles per image)
+    when the engine is one of several concurrent streams, from 64 on one
+    stream (profiles/r5_engine_ab.md, r5_k14x_tiles.md)."""
     eng, _ = fp32_engine
     keep = eng.smallf_min_blocks, eng.concurrent_streams
     try:
         eng.smallf_min_blocks = None
         eng.concurrent_streams = 1
-        assert [b for b in range(1, 33) if eng._small_fused(b, 14)] == list(range(20, 33))
+        assert [b for b in range(1, 33) if eng._small_fused(b, 14)] == list(range(16, 33))
         eng.concurrent_streams = 2
         assert [b for b in range(1, 33) if eng._small_fused(b, 14)] == list(range(12, 33))
         assert [b for b in range(1, 33) if eng._small_fused(b, 7)] == list(range(12, 33))

@@ -315,7 +315,9 @@ class FusedDenseNetFP32:
     def _small_fused(self, b, hw):
         thr = self.smallf_min_blocks
         if thr is None:
-            thr = 48 if self.concurrent_streams > 1 else 80
+            # one stream: from 16 images (with 7-tile 14x14 layers K14x is 7 % faster
+            # there, 2 % slower at 12; profiles/r5_k14x_tiles.md)
+            thr = 48 if self.concurrent_streams > 1 else 64
         if thr <= 0 or hw not in (7, 14):
             return False
         # the thresholds count workgroups at up to 4 row tiles per image (the

@@ -61,7 +61,7 @@ KNOBS = [
          "largest block pixel count the chain takes", _DF + "test_fp32_engine_routing_knobs"),
     Knob("TCAMD_X3_SMALLF_MIN_BLOCKS", "python", "auto", "FP32DenseNet.smallf_min_blocks",
          "K14x for the 14x14 / 7x7 blocks from this many workgroups (images x row tiles); 0 = off; "
-         "auto = 48 with concurrent streams (server instances), 80 on one",
+         "auto = 48 with concurrent streams (server instances), 64 on one",
          _DF + "test_fp32_engine_k14x_blocks_match_fp32_module"),
     Knob("TCAMD_X3_SMALLF_TILES", "python", 0, "FP32DenseNet.smallf_tiles",
          "K14x row tiles per image; 0 = the chip-filling choice (x3_small_tiles)",
