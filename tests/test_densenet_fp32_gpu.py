@@ -531,7 +531,7 @@ def test_k14x_seven_tiles_fit_the_stream_share(fp32_engine):
         eng.smallf_tiles, eng.concurrent_streams = keep
 
 
-_ROUTES = [{"fuse_min_tiles": 0}, {"fuse_big_k_min_tiles": 1}, {"fuse_v3": 0}, {"fuse_v3": 16},
+_ROUTES = [{"fuse_min_tiles": 0}, {"fuse_big_k_min_tiles": 4}, {"fuse_v3": 0}, {"fuse_v3": 16},
            {"small_m": 0}, {"use_chain": False}, {"chain_m": 0}, {"small_m": 0, "chain_m": 0},
            {"smallf_min_blocks": 1, "smallf_tiles": 2}, {"smallf_min_blocks": 1, "smallf_tiles": 4}]
 

@@ -49,7 +49,7 @@ from .densenet_fused import _bn_affine
 
 IMG_ELEMS = 3 * 224 * 224
 FUSE_MAX_K = 224  # K11x at every batch: K 64..224
-FUSE_MAX_K_BIG = 480  # ... and up to K 480 (the late block-2 layers) once every block walks >= 4 tiles
+FUSE_MAX_K_BIG = 480  # ... and up to K 480 (the late block-2 layers) from fuse_big_k_min_tiles tiles per block
 
 
 def split_bf16(w):
@@ -118,7 +118,10 @@ class FusedDenseNetFP32:
         # tiles (its per-block prologue recomputes a (2W+2)-row halo of z, yet it
         # still beats the two-launch pair at bs1); 0 disables it (A/B runs)
         self.fuse_min_tiles = int(os.environ.get("TCAMD_X3_FUSE_MIN_TPB", "1"))
-        self.fuse_big_k_min_tiles = int(os.environ.get("TCAMD_X3_FUSE_BIGK_MIN_TPB", "4"))
+        # ... and past K = 224 from this many tiles per block: 1 (K11x for K 256..480
+        # at any batch: engine bs12-48 +1..6 % against the pair there, round 5;
+        # from bs64 every block has >= 4 tiles anyway; profiles/r5_engine_ab.md)
+        self.fuse_big_k_min_tiles = int(os.environ.get("TCAMD_X3_FUSE_BIGK_MIN_TPB", "1"))
         # K11x v3 (the next chunk's 1x1 interleaved into the 3x3) on blocks of
         # width >= fuse_v3 at >= 2 tiles per block; 0 = v1 everywhere.  Engine
         # bs128 x 2 streams 47.1k -> 47.6k img/s with v3 on both K11x blocks

@@ -48,7 +48,7 @@ KNOBS = [
     Knob("TCAMD_X3_FUSE_MIN_TPB", "python", 1, "FP32DenseNet.fuse_min_tiles",
          "K11x for a block when every workgroup gets this many 64-pixel tiles; 0 = the K8x + K9x pair",
          _DF + "test_fp32_engine_routing_knobs"),
-    Knob("TCAMD_X3_FUSE_BIGK_MIN_TPB", "python", 4, "FP32DenseNet.fuse_big_k_min_tiles",
+    Knob("TCAMD_X3_FUSE_BIGK_MIN_TPB", "python", 1, "FP32DenseNet.fuse_big_k_min_tiles",
          "K11x past K = 224 (to 480) from this many tiles per workgroup", _DF + "test_fp32_engine_routing_knobs"),
     Knob("TCAMD_X3_FUSE_V3", "python", 28, "FP32DenseNet.fuse_v3",
          "K11x v3 on blocks at least this wide (at >= 2 tiles per workgroup); 0 = v1 everywhere",
