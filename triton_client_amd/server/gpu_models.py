@@ -519,10 +519,11 @@ class BertLarge(Model):
     instance_count = 1
     supports_native = True
     # HIP-graph buckets: a batch runs the smallest one that holds it.  Steps of
-    # 8 rows from 8 up: closed-loop loads batch anything from 1 to 64 rows, and
+    # 4 rows from 8 to 32 (where c64's batches land), 8 above: closed-loop loads
+    # batch anything from 1 to 64 rows, and
     # with power-of-two buckets a 33-row batch paid for 64 (served c64: 33 rows
     # per batch at 11.5 ms vs 7.9 ms for a 32-row forward)
-    BUCKETS = (1, 2, 4, 8, 12, 16, 24, 32, 40, 48, 56, 64)
+    BUCKETS = (1, 2, 4, 8, 12, 16, 20, 24, 28, 32, 40, 48, 56, 64)
 
     def __init__(self, version=1, device_id=0, use_graphs=True, layers=24, **kw):
         super().__init__(version, **kw)
