@@ -313,7 +313,8 @@ def test_x3_dense_fused(imgs, H, K, version):
 
 @pytest.mark.parametrize("imgs,H,K", [(1, 14, 64), (3, 14, 256), (8, 14, 288), (9, 14, 992), (17, 14, 640),
                                       (128, 14, 512), (16, 14, 96), (1, 7, 512), (5, 7, 992), (64, 7, 768),
-                                      (130, 7, 544), (2, 7, 64), (40, 14, 416)])
+                                      (130, 7, 544), (2, 7, 64), (40, 14, 416), (37, 14, 736), (64, 14, 1024),
+                                      (37, 7, 320), (8, 7, 1024)])
 @pytest.mark.parametrize("tiles", [1, 2, 4, 7])
 def test_x3_dense_small(imgs, H, K, tiles):
     """K14x: the whole dense layer of a 14x14 or 7x7 block in one kernel over
@@ -463,12 +464,12 @@ def test_fp32_engine_matches_fp32_module(fp32_engine, b):
     assert err < 1e-3
 
 
-@pytest.mark.parametrize("b", [3, 9, 24])
+@pytest.mark.parametrize("b", [1, 3, 8, 9, 24, 32])  # (37 / 64 images: test_x3_dense_small, per layer)
 def test_fp32_engine_k14x_blocks_match_fp32_module(fp32_engine, b):
     """The engine with K14x forced on for the 14x14 and 7x7 blocks at every
-    batch (ragged image counts: the grid groups the tiles of images 8g+j; at
-    these batches the default tiling is 4 tiles per image), against the fp32
-    module, and against the same engine with K14x off."""
+    batch (ragged image counts: the grid groups the tiles of images 8g+j; up
+    to 32 images the 14x14 layers take 7 tiles per image, then 4), against
+    the fp32 module, and against the same engine with K14x off."""
     eng, model = fp32_engine
     g = torch.Generator(device=DEV).manual_seed(300 + b)
     x = torch.randn(b, 3, 224, 224, device=DEV, generator=g)
