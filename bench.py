@@ -70,6 +70,8 @@ def parse_args(argv=None):
     ap.add_argument("--concurrency", type=int, default=48, help="requests in flight per GPU")
     ap.add_argument("--window", type=int, default=16, help="requests per step = window x concurrency")
     ap.add_argument("--bs1-concurrency", type=int, default=64)
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="client lanes (connection + worker thread each) sharing the headline concurrency")
     ap.add_argument("--bs1-lanes", type=int, default=1,
                     help="client lanes (connection + worker thread each) sharing the bs=1 concurrency")
     ap.add_argument("--fanout", default="rccl", choices=["rccl", "p2p", "local"])
@@ -414,9 +416,9 @@ def main():
             client.register_cuda_shared_memory("fc6_1_out", shmod.get_raw_handle(ro), dev, nslots * ob)
             out_list = ["fc6_1_out@%d" % (i * ob) for i in range(nslots)]
 
-        def slots(c):
-            return {"data_0": in_list[:c] if isinstance(in_list, list) else in_list}, \
-                ({"fc6_1": out_list[:c]} if out_list else None)
+        def slots(c, lo=0):
+            return {"data_0": in_list[lo:c] if isinstance(in_list, list) else in_list}, \
+                ({"fc6_1": out_list[lo:c]} if out_list else None)
 
         fan = {"method": method, "replicas_verified": True, "bytes": in_total}
         if not cpu and world > 1:
@@ -437,9 +439,16 @@ def main():
 
         # ---- headline: bs=8 -------------------------------------------------------
         per = args.window * conc
-        ins, outs = slots(conc)
-        p8 = Point(srv, model, bs, conc, None, in_bytes, dev, cpu, inputs=ins, outputs=outs)
-        points.append(p8)
+        nl8 = max(1, args.lanes)
+        if conc % nl8 or per % nl8:
+            raise SystemExit("--concurrency (and window x concurrency) must be a multiple of --lanes")
+        # lane i drives concurrency slots [i c / n, (i + 1) c / n): its own connection and worker thread
+        lanes8 = []
+        for i in range(nl8):
+            ins, outs = slots((i + 1) * conc // nl8, i * conc // nl8)
+            lanes8.append(Point(srv, model, bs, conc // nl8, None, in_bytes, dev, cpu, inputs=ins, outputs=outs))
+        p8 = Lanes(lanes8)
+        points.extend(lanes8)
         lat_w, _, _ = p8.run(max(args.warmup, 1) * per)
         log("warmup done: p50 %.0f us" % percentile_us(lat_w.astype(np.float64), 50))
         st0 = p8.s.server_stats()
@@ -567,7 +576,7 @@ def main():
                 "engine": args.engine,
                 "compute": ("split-precision bf16x3 MFMA, fp32 accumulate (rel-L2 vs fp32 module ~4e-5)"
                             if args.engine == "fp32" else args.engine),
-                "loadgen": "native C++ (csrc/cpp/perf)",
+                "loadgen": "native C++ (csrc/cpp/perf)", "client_lanes": args.lanes,
                 "server_instances": args.instance_count,
                 "preferred_batch_rows": args.preferred,
                 "max_queue_delay_us": args.max_queue_delay_us,

@@ -55,11 +55,12 @@ def test_bench_spawns_ranks_and_aggregates(gpus):
 
 
 def test_bench_bs1_over_two_client_lanes():
-    """--bs1-lanes 2: the bs=1 concurrency split over two client connections /
-    worker threads; the JSON says so and the breakdown still reads the
-    server's statistics."""
-    res, _ = _bench("--steps", "2", "--bs1-lanes", "2")
+    """--lanes 2 / --bs1-lanes 2: the headline and bs=1 concurrencies split over
+    two client connections / worker threads (disjoint concurrency slots); the
+    JSON says so and the breakdowns still read the server's statistics."""
+    res, _ = _bench("--steps", "2", "--bs1-lanes", "2", "--lanes", "2")
     assert res["bs1"]["client_lanes"] == 2 and res["bs1"]["concurrency"] == 4
+    assert res["config"]["client_lanes"] == 2 and res["value"] > 0 and len(res["window_infer_per_sec_rank0"]) == 2
     assert res["bs1"]["infer_per_sec"] > 0 and res["bs1"]["p99_latency_us"] >= res["bs1"]["p50_latency_us"] > 0
     assert res["bs1"]["breakdown_rank0"]["avg_rows_per_batch"] >= 1
 
