@@ -51,3 +51,20 @@ def test_x3_w3f_fragments_matches_kernel_indexing():
     src = w[(16 * oh + col).reshape(-1), (t * 128 + 32 * kq + 8 * h + e).reshape(-1)]
     assert torch.equal(f[off], src)
     assert sorted(f.tolist()) == list(range(w.numel()))
+
+
+def test_k14x_seven_tile_split_fits_the_stream_share():
+    """DensenetFP32's K14x tiling rule (CPU, pure): the native choice's 7-tile
+    split of small 14x14 batches stays only while its grid (images padded to
+    8) fits one round of this stream's share of the CUs; other choices pass
+    through."""
+    from triton_client_amd.models.densenet_fp32 import stream_share_tiles
+
+    assert stream_share_tiles(7, 32, 256, 1) == 7   # 224 workgroups <= 256
+    assert stream_share_tiles(7, 33, 256, 1) == 4   # 280 > 256
+    assert stream_share_tiles(7, 16, 256, 2) == 7   # 112 <= 128
+    assert stream_share_tiles(7, 17, 256, 2) == 4   # 168 > 128
+    assert stream_share_tiles(7, 1, 256, 3) == 7    # 56 <= 85
+    assert stream_share_tiles(7, 16, 256, 3) == 4   # 112 > 85
+    for t in (1, 2, 4):
+        assert stream_share_tiles(t, 24, 256, 2) == t

@@ -310,10 +310,7 @@ class FusedDenseNetFP32:
         bs32 it oversubscribes them: -5.6 %, profiles/r5_k14x_tiles.md)."""
         if self.smallf_tiles:
             return self.smallf_tiles
-        t = hip.x3_small_tiles(b, hw)
-        if t == 7 and (b + 7) // 8 * 8 * 7 > _cu_count(self.device) // max(1, self.concurrent_streams):
-            t = 4
-        return t
+        return stream_share_tiles(hip.x3_small_tiles(b, hw), b, _cu_count(self.device), self.concurrent_streams)
 
     def _small_fused(self, b, hw):
         thr = self.smallf_min_blocks
@@ -349,6 +346,15 @@ class FusedDenseNetFP32:
 
 
 _CU = {}
+
+
+def stream_share_tiles(native_tiles, imgs, ncu, streams):
+    """K14x tiles per image given the native chip-filling choice: its 7-tile
+    split of small 14x14 batches only while the grid fits one round of this
+    stream's share of the CUs, else quarters."""
+    if native_tiles == 7 and (imgs + 7) // 8 * 8 * 7 > ncu // max(1, streams):
+        return 4
+    return native_tiles
 
 
 def _cu_count(dev):
