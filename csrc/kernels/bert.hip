@@ -93,6 +93,80 @@ __global__ void __launch_bounds__(256) add_layernorm_kernel(const uint16_t* x, c
   ln_store_row<E>(v, gamma, beta, out + base, lane, eps);
 }
 
+// ---- K11p: LN(x + bias + sum_z parts[z]) -----------------------------------
+// The consumer of a split-K projection (K18, csrc/kernels/gemm_tiles.hip):
+// the attention-out / FFN-down GEMM leaves fp32 partial slabs instead of a
+// bf16 y, and this pass -- which BERT needs anyway for the residual add +
+// LayerNorm -- sums them with the bias on the way in, so the split costs no
+// reduce launch and y never exists as its own tensor.  T = uint16_t (bf16
+// x / gamma / beta / out: the bf16 model) or float (the fp32-parity model).
+__device__ __forceinline__ void load8(const uint16_t* p, float* v) {
+  const v4u a = *reinterpret_cast<const v4u*>(p);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[2 * q] = __uint_as_float(a[q] << 16);
+    v[2 * q + 1] = __uint_as_float(a[q] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void load8(const float* p, float* v) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+}
+__device__ __forceinline__ void add8(const float* p, float* v) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  v[0] += a.x, v[1] += a.y, v[2] += a.z, v[3] += a.w, v[4] += b.x, v[5] += b.y, v[6] += b.z, v[7] += b.w;
+}
+__device__ __forceinline__ void store8(uint16_t* p, const float* v) {
+  *reinterpret_cast<v4u*>(p) = v4u{pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7])};
+}
+__device__ __forceinline__ void store8(float* p, const float* v) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+template <int E, typename T>
+__global__ void __launch_bounds__(256) add_ln_parts_kernel(const T* x, const float* parts, int nparts, long long pstride,
+                                                           const float* __restrict__ bias, const T* __restrict__ gamma,
+                                                           const T* __restrict__ beta, T* out, int rows, float eps) {
+  constexpr int H = 64 * E, C = E / 8;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const size_t base = (size_t)row * H;
+  float v[E];
+#pragma unroll
+  for (int c = 0; c < C; ++c) load8(x + base + (c * 64 + lane) * 8, v + 8 * c);
+  if (bias)
+#pragma unroll
+    for (int c = 0; c < C; ++c) add8(bias + (c * 64 + lane) * 8, v + 8 * c);
+  for (int zz = 0; zz < nparts; ++zz) {
+    const float* pz = parts + zz * pstride + base;
+#pragma unroll
+    for (int c = 0; c < C; ++c) add8(pz + (c * 64 + lane) * 8, v + 8 * c);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) s += v[e];
+  const float mean = wave_sum(s) * (1.0f / H);
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const float d = v[e] - mean;
+    ss += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(ss) * (1.0f / H) + eps);
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int off = (c * 64 + lane) * 8;
+    float g[8], bt[8], o[8];
+    load8(gamma + off, g);
+    load8(beta + off, bt);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (v[8 * c + e] - mean) * rstd * g[e] + bt[e];
+    store8(out + base + off, o);
+  }
+}
+
 // Embedding sum + LayerNorm: out[r] = LN(word[ids[r]] + pos[r % S] +
 // type[types[r]]) in one pass (torch: three gathers, two adds and a LayerNorm,
 // six launches and ~5 passes over [tokens, H]).  Ids outside the tables are
@@ -394,6 +468,38 @@ int tcamd_add_layernorm(const void* x, const void* y, const void* gamma, const v
     case 4096: hipLaunchKernelGGL(add_layernorm_kernel<64>, grid, block, 0, s, px, py, pg, pb, po, rows, eps); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// K11p: out = LayerNorm(x + bias + sum_{z < nparts} parts[z]) * gamma + beta
+// over rows of H elements (H in {512, 1024, 2048, 4096}); parts fp32, slab z
+// at parts + z * pstride (elements, [rows][H] each); bias fp32 [H] or null;
+// f32 = 0: x / gamma / beta / out bf16, 1: fp32.  16-B aligned pointers;
+// out may alias x.
+int tcamd_add_layernorm_parts(const void* x, const float* parts, int nparts, long long pstride, const float* bias,
+                              const void* gamma, const void* beta, void* out, int rows, int H, float eps, int f32,
+                              void* stream) {
+  if (rows <= 0) return hipSuccess;
+  if (nparts < 0 || (nparts > 0 && (!parts || pstride < (long long)rows * H)) ||
+      ((uintptr_t)x | (uintptr_t)parts | (uintptr_t)bias | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)out) % 16)
+    return hipErrorInvalidValue;
+  const dim3 grid((rows + 3) / 4), block(256);
+  hipStream_t s = (hipStream_t)stream;
+#define TC_K11P(E, T)                                                                                            \
+  hipLaunchKernelGGL((add_ln_parts_kernel<E, T>), grid, block, 0, s, (const T*)x, parts, nparts, pstride, bias, \
+                     (const T*)gamma, (const T*)beta, (T*)out, rows, eps)
+  switch (H * 2 + (f32 ? 1 : 0)) {
+    case 1024: TC_K11P(8, uint16_t); break;
+    case 1025: TC_K11P(8, float); break;
+    case 2048: TC_K11P(16, uint16_t); break;
+    case 2049: TC_K11P(16, float); break;
+    case 4096: TC_K11P(32, uint16_t); break;
+    case 4097: TC_K11P(32, float); break;
+    case 8192: TC_K11P(64, uint16_t); break;
+    case 8193: TC_K11P(64, float); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef TC_K11P
   return hipGetLastError();
 }
 

@@ -25,7 +25,16 @@
 //     one continuous stream through the ring (no per-tile prologue wait);
 //     the bf16 epilogue stores 4-byte column pairs (a lane-pair swap);
 //   * XCD-aware tile order: the tiles of one M panel run on one XCD (its L2
-//     keeps the A panel).
+//     keeps the A panel);
+//   * dynamic tile scheduling (round 6): a workgroup's first tile is its own
+//     id, every later one is claimed from a device counter (one returning
+//     atomic per tile, issued at the start of the tile before it, so its
+//     round trip hides behind a slab interval).  A workgroup that starts late --
+//     its CU still running the previous kernel's tail -- simply claims fewer
+//     tiles, instead of finishing a fixed tile list late (the in-graph loss of
+//     the fixed list: profiles/r5_k17_gemm.md).  The last workgroup to finish
+//     resets the counter, so a HIP graph replays the launch with no memset
+//     node; one counter per stream (kernels of one stream never overlap).
 //
 // Reference analog: none (the reference client runs no model; this serves
 // the bert_large perf_analyzer config of BASELINE.json).
@@ -35,6 +44,8 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
+#include <cstring>
+#include <mutex>
 
 #include "kernels/common.h"
 #include "kernels/knobs.h"
@@ -50,7 +61,8 @@ constexpr int kTile = 256;   // N per tile; M per tile: TM = 256 or 128
 constexpr int kSlabK = 32;   // k per slab
 constexpr int kBBytes = kTile * kSlabK * 2;  // B's slab: 16 KB
 constexpr int kRing = 4;
-constexpr int kMaxBiasN = 8192;  // bias copy behind the ring (<= 32 KB)
+constexpr int kMaxBiasN = 8188;  // bias copy behind the ring and the tile queue (<= 32 KB - 16 B)
+constexpr int kTq = 16;          // LDS tile queue of the dynamic scheduler (4 ints)
 constexpr int slab_bytes(int tm) { return tm * kSlabK * 2 + kBBytes; }  // A | B
 constexpr int ring_bytes(int tm) { return kRing * slab_bytes(tm); }     // 128 / 96 KB
 
@@ -63,6 +75,7 @@ struct K17Params {
   void* C;            // [M][ldc] bf16 or fp32
   int M, N, K, lda, ldb, ldc;
   int tiles_m, tiles_n;
+  int* sched;  // {next, done} claim counters (dynamic scheduling) or null (static tile list)
 };
 
 __device__ __forceinline__ v4u lds16(const uint8_t* p) { return *reinterpret_cast<const v4u*>(p); }
@@ -87,6 +100,19 @@ __device__ __forceinline__ f32x2 gelu2(f32x2 x) {
   const f32x2 w = x * __builtin_elementwise_fma(x * x, f32x2{kC3, kC3}, f32x2{kC1, kC1});
   const f32x2 d = f32x2{__builtin_amdgcn_exp2f(w.x), __builtin_amdgcn_exp2f(w.y)} + 1.0f;
   return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};  // x -> -inf: x * 0
+}
+
+// The dynamic scheduler's claim: a returning atomic add of 1 to *ctr, as
+// inline asm so hipcc does not wait for it -- its own waits would be a
+// vmcnt(0) at the use (the claim is loop-carried across the slab loop), which
+// drains the LDS-DMA ring.  The kernel's counted ring wait one slab later
+// retires it instead (VMEM ops return in issue order).  The destination VGPR
+// must stay untouched until then: tests/test_gemm_isa.py checks the built code
+// object for that (the register is read only by the consumer).
+__device__ __forceinline__ int claim_tile(int* ctr) {
+  int old;
+  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(old) : "v"(ctr), "v"(1) : "memory");
+  return old;
 }
 
 // raw barrier (no vmcnt(0): the ring's LDS-DMAs stay in flight across it);
@@ -148,20 +174,31 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
   const bool grp1 = __builtin_amdgcn_readfirstlane(wave) >= 4;  // wave-uniform
   const int nai = grp1 ? ai1(TM) : ai0(TM);                     // this wave's A LDS-DMAs per slab
   const int arow0 = grp1 ? 64 * ai0(TM) + 16 * ai1(TM) * (wave - 4) : 16 * ai0(TM) * wave;
-  // persistent: workgroup b takes tiles b, b + G, ... and the K slabs of all
-  // of them form ONE stream through the LDS ring (the next tile's first
-  // slabs load during this tile's last ones and its epilogue)
+  // persistent: workgroup b takes tiles seq[0], seq[1], ... and the K slabs
+  // of all of them form ONE stream through the LDS ring (the next tile's
+  // first slabs load during this tile's last ones and its epilogue).
+  // Static: seq[k] = b + k G.  Dynamic (p.sched): seq[0] = b, seq[k + 1] = G +
+  // a claimed counter value, claimed by thread 0 in the R interval of tile
+  // k's slab 0 and written to an LDS ring of 4 (tq) in slab 1's, which every
+  // wave reads behind at least one barrier (staging reaches tile k + 1 at
+  // slab nsl - 3; the host asks for nsl >= 6).
   const int G = (int)gridDim.x, wg = (int)blockIdx.x;
   const int ntiles = p.tiles_m * p.tiles_n;
-  const int T = (ntiles - wg + G - 1) / G;
   const int nsl = p.K / kSlabK;
+  const bool dyn = p.sched != nullptr;  // launch-uniform
+  int* const tq = reinterpret_cast<int*>(lds + kLds);
+  const bool claimer = dyn && tid == 0;
+  auto seq = [&](int k) -> int {
+    if (!dyn) return wg + k * G;
+    return k == 0 ? wg : __builtin_amdgcn_readfirstlane(tq[k & 3]);
+  };
 
   // XCD-aware tile order (bijective): tiles with equal t % 8 run on one XCD
   // (G is a multiple of 8 or the whole grid); give each XCD a contiguous
   // M-panel-major run of tile ids, so the tiles an XCD runs together share
-  // their A panel in its L2
-  auto origin = [&](int tl, int& m0, int& n0) {
-    const int t = wg + tl * G;
+  // their A panel in its L2 (dynamic claims keep the claim order, which
+  // interleaves the XCDs the same way)
+  auto origin = [&](int t, int& m0, int& n0) {
     const int x = t & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
     const int id = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + (t >> 3);
     const int tm = id / p.tiles_n;
@@ -191,15 +228,15 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
   int gs = 0, st_tl = 0, st_s = 0;
   const uint16_t* sa[kAI];
   const uint16_t* sbp[2];
-  auto set_tile = [&](int tl) {
+  auto set_tile = [&](int t) {
     int m0, n0;
-    origin(tl, m0, n0);
+    origin(t, m0, n0);
 #pragma unroll
     for (int i = 0; i < kAI; ++i) sa[i] = p.A + (size_t)min(m0 + arow[i], p.M - 1) * p.lda + acol[i];
 #pragma unroll
     for (int i = 0; i < 2; ++i) sbp[i] = p.B + (size_t)(n0 + brow[i]) * p.ldb + bcol[i];
   };
-  set_tile(0);
+  set_tile(wg);
   auto stage = [&]() {
     uint8_t* dst = lds + (gs & (kRing - 1)) * kSlab;
     const int k0 = st_s * kSlabK;
@@ -213,9 +250,11 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
                                        0, 0);
     ++gs;
     if (++st_s == nsl) {
-      if (st_tl + 1 < T) {
+      const int nxt = seq(st_tl + 1);
+      if (nxt < ntiles) {
         st_s = 0;
-        set_tile(++st_tl);
+        ++st_tl;
+        set_tile(nxt);
       } else {
         st_s = nsl - 1;
       }
@@ -230,7 +269,7 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
   // the bias in LDS behind the ring: an ordinary global load used in the
   // epilogue would make hipcc wait vmcnt(0) there, draining the ring's
   // in-flight LDS-DMAs of the next tile
-  float* const bias_l = reinterpret_cast<float*>(lds + kLds);
+  float* const bias_l = reinterpret_cast<float*>(lds + kLds + kTq);
   if (EPI >= kEpiBias) {
     for (int c = tid; c < p.N; c += 512) bias_l[c] = p.bias[c];
     __syncthreads();
@@ -246,7 +285,10 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
   f32x4 acc[kMT][4];
   v4u a[kMT], b[4];
   int g = 0;
-  for (int tl = 0; tl < T; ++tl) {
+  int cn;  // the claimed counter value (dynamic), in flight from slab 0 to slab 1
+  for (int tl = 0;; ++tl) {
+    const int tile = seq(tl);
+    if (tile >= ntiles) break;
 #pragma unroll
     for (int i = 0; i < kMT; ++i)
 #pragma unroll
@@ -259,10 +301,15 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
       for (int j = 0; j < 4; ++j) b[j] = lds16(sb + b_off + j * 16 * 64);
 #pragma unroll
       for (int i = 0; i < kMT; ++i) a[i] = lds16(sb + a_off + i * 16 * 64);
+      // dynamic: claim seq[tl + 1] ahead of this slab's LDS-DMAs (claim_tile)
+      if (claimer && s == 0) cn = claim_tile(p.sched);
       stage();
       // this wave's LDS-DMAs of slab g + 1 landed (g + 2, g + 3 in flight);
       // a tile's first slab: waited for before the last epilogue
       if (s != 0 || tl == 0) wait_ring<TM>(grp1);
+      // slab 1: that wait retired every VMEM op issued before slab 0's
+      // LDS-DMAs, the claim's return among them
+      if (claimer && s == 1) tq[(tl + 1) & 3] = G + cn;
       wait_lgkm0();
       bar();
       // ---- M interval: 4 kMT MFMAs ----
@@ -281,7 +328,7 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
     // 4 (lane / 16) + e.  bf16: lanes 2c and 2c + 1 swap halves so each
     // stores two rows of a column pair as 4-byte words ----
     int m0, n0;
-    origin(tl, m0, n0);
+    origin(tile, m0, n0);
     float bj[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) bj[j] = EPI >= kEpiBias ? bias_l[n0 + wc * 64 + j * 16 + col_l] : 0.f;
@@ -324,6 +371,12 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
   }
   if (!grp1) bar();  // the same barrier count for all waves
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the re-reads past the last slab
+  // dynamic: the last workgroup out (all claims of all workgroups returned
+  // before their done adds) resets the counters for the next launch
+  if (claimer && atomicAdd(p.sched + 1, 1) == G - 1) {
+    atomicExch(p.sched, 0);
+    atomicExch(p.sched + 1, 0);
+  }
 }
 
 bool a16(const void* q) { return ((uintptr_t)q & 15) == 0; }
@@ -343,7 +396,7 @@ int cu_count() {
 template <int TM, int EPI, bool F32>
 hipError_t launch_tm(const K17Params& prm, int grid, hipStream_t s) {
   constexpr int kLds = ring_bytes(TM);
-  const int lds_bytes = kLds + (EPI >= kEpiBias ? 4 * prm.N : 0);
+  const int lds_bytes = kLds + kTq + (EPI >= kEpiBias ? 4 * prm.N : 0);
   static std::atomic<uint32_t> attr_done{0};  // one bit per device (<= 32)
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -351,7 +404,7 @@ hipError_t launch_tm(const K17Params& prm, int grid, hipStream_t s) {
   const uint32_t bit = 1u << (dev & 31);
   if (!(attr_done.load(std::memory_order_acquire) & bit)) {
     e = hipFuncSetAttribute((const void*)k17_gemm_kernel<TM, EPI, F32>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            kLds + 4 * kMaxBiasN);
+                            kLds + kTq + 4 * kMaxBiasN);
     if (e != hipSuccess) return e;
     attr_done.fetch_or(bit, std::memory_order_acq_rel);
   }
@@ -373,6 +426,46 @@ hipError_t launch(const K17Params& prm, int grid, hipStream_t s, int epi, int ou
 
 std::atomic<int> g_k17_last_tm{0};
 std::atomic<long long> g_k17_calls{0};
+
+// the dynamic scheduler's claim counters: one {next, done} pair per stream on
+// a 128-B line of its own, in the code object's device memory (zero at load;
+// every launch leaves them zero again)
+constexpr int kSchedSlots = 64;
+__device__ int g_k17_sched[kSchedSlots * 32];
+
+struct SchedMap {
+  std::mutex mu;
+  int* base[32] = {};            // g_k17_sched's address per device
+  uintptr_t key[32][kSchedSlots];  // stream handle + 1 per slot (0 = free)
+  SchedMap() { std::memset(key, 0, sizeof(key)); }
+};
+SchedMap& sched_map() {
+  static SchedMap m;
+  return m;
+}
+
+// the counter pair of (device, stream), or null when the slots are used up
+// (the launch then runs the static tile list)
+int* sched_for(hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 32) return nullptr;
+  SchedMap& m = sched_map();
+  std::lock_guard<std::mutex> g(m.mu);
+  if (!m.base[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_k17_sched)) != hipSuccess || !p) return nullptr;
+    m.base[dev] = (int*)p;
+  }
+  const uintptr_t k = (uintptr_t)s + 1;
+  for (int i = 0; i < kSchedSlots; ++i)
+    if (m.key[dev][i] == k) return m.base[dev] + 32 * i;
+  for (int i = 0; i < kSchedSlots; ++i)
+    if (!m.key[dev][i]) {
+      m.key[dev][i] = k;
+      return m.base[dev] + 32 * i;
+    }
+  return nullptr;
+}
 
 }  // namespace
 
@@ -423,6 +516,10 @@ int tcamd_k17_gemm(const void* A, const void* B, const float* bias, void* C, int
   g_k17_last_tm = tm;
   g_k17_calls.fetch_add(1, std::memory_order_relaxed);
   hipStream_t s = (hipStream_t)stream;
+  // dynamic scheduling when some workgroup runs more than one tile and a
+  // tile has the >= 6 slabs the claim-ahead needs (TCAMD_K17_DYN=0: static)
+  prm.sched = nullptr;
+  if (ntiles > grid && K / kSlabK >= 6 && tcamd::knob(tcamd::Knob::K17Dyn) != 0) prm.sched = sched_for(s);
   if (tm == 128) return launch<128>(prm, grid, s, epi, out_f32);
   if (tm == 192) return launch<192>(prm, grid, s, epi, out_f32);
   return launch<256>(prm, grid, s, epi, out_f32);

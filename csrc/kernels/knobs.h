@@ -31,6 +31,7 @@ enum class Knob : int {
   PkBigLim,        // K2 pack: output offset past which a block takes the 64-bit byte path
   K3Mode,          // K3 index: 1 = general walk only
   K17Tm,           // K17 GEMM tile height (0 = by the grid fill, 128, 256)
+  K17Dyn,          // K17 dynamic (claimed) tile scheduling (0 = static tile lists)
   kCount
 };
 

@@ -40,6 +40,7 @@ constexpr KnobDef kDefs[] = {
     {"TCAMD_PK_BIG_LIM", (1ll << 31) - (1ll << 20), "K2 BYTES pack: output offset from which blocks take the 64-bit path"},
     {"TCAMD_K3_MODE", 0, "K3 BYTES index: 1 = general walk only (no windowed v3 walk)"},
     {"TCAMD_K17_TM", 0, "K17 GEMM: tile height 128, 192 or 256; 0 picks the one whose persistent grid finishes first"},
+    {"TCAMD_K17_DYN", 1, "K17 GEMM: claim tiles from a device counter (1) or walk a fixed tile list per workgroup (0)"},
 };
 static_assert(sizeof(kDefs) / sizeof(kDefs[0]) == (size_t)tcamd::Knob::kCount, "knob table != enum");
 

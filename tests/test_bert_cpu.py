@@ -63,3 +63,25 @@ def test_bert_flops():
 
     f = bert.flops_per_sequence()
     assert 2.0e11 < f < 3.0e11  # ~0.25 TFLOP per 384-token sequence
+
+
+def test_gemm_route_table():
+    """bert's projection routing (TC_BERT_GEMM): the measured table first,
+    hipBLASLt past it in auto mode, the hand-written kernels everywhere in
+    ours mode; the CPU forward never routes (it stays on torch ops)."""
+    from triton_client_amd.models import bert
+
+    for name, table in bert.GEMM_ROUTES.items():
+        tops = [t for t, _ in table]
+        assert tops == sorted(tops), name
+        for top, route in table:
+            for mode in ("auto", "ours"):
+                assert bert.gemm_route(name, top, mode) == route
+                assert bert.gemm_route(name, 1, mode) == table[0][1]
+            assert bert.gemm_route(name, top, "lib") == ("lib",)
+        assert bert.gemm_route(name, tops[-1] + 384, "auto") == ("lib",)
+        assert bert.gemm_route(name, 24576, "ours") == bert.OURS_LARGE[name]
+        assert bert.gemm_route(name, 24576, "ours")[0] in ("k17", "k18")
+    # split-K only where K11p can sum the slabs: the N = 1024 projections
+    for name in ("qkv", "ffn_up"):
+        assert all(r[0] != "k18" or r[2] == 1 for _, r in bert.GEMM_ROUTES[name])

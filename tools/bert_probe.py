@@ -2,7 +2,7 @@
 ``rocprofv3 --kernel-trace --stats`` for the per-kernel split.
 
   python tools/bert_probe.py --batch 64 --iters 10
-  python tools/bert_probe.py --batch 1 8 64 --k17 --graphs   # K17 vs hipBLASLt projections, HIP graphs
+  python tools/bert_probe.py --batch 1 8 64 --gemm lib,auto,ours --graphs   # projection routing A/B, HIP graphs
 """
 
 import argparse
@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--tunable", default="",
                     help="A/B against PyTorch TunableOp (hipBLASLt / rocBLAS solution search per GEMM shape); "
                          "the tuned results go to this CSV path")
-    ap.add_argument("--k17", action="store_true", help="A/B: the K17 projections (bert.K17) against hipBLASLt only")
+    ap.add_argument("--gemm", default="", help="A/B the projection routing modes (bert.GEMM), e.g. lib,auto,ours")
     ap.add_argument("--graphs", action="store_true", help="time HIP-graph replays of the forward (as served)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -39,8 +39,8 @@ def main():
         mask = torch.ones(b, a.seq, device=dev, dtype=torch.int64)
         tt = torch.zeros(b, a.seq, device=dev, dtype=torch.int64)
         variants = {"default": 0}
-        if a.k17:
-            variants = {"library": 0, "k17": 0}
+        if a.gemm:
+            variants = {m: 0 for m in a.gemm.split(",")}
         tun = None
         if a.tuned_table:
             import torch.cuda.tunable as tun
@@ -65,8 +65,8 @@ def main():
             for name in variants:
                 if tun is not None:
                     tun.enable(name == "tunableop")
-                if a.k17:
-                    bert.K17 = name == "k17"
+                if a.gemm:
+                    bert.GEMM = name
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):  # warm-up on the capture stream (K17 allocates its workspace there)
@@ -85,8 +85,8 @@ def main():
                 for name in variants:
                     if tun is not None:
                         tun.enable(name == "tunableop")
-                    if a.k17:
-                        bert.K17 = name == "k17"
+                    if a.gemm:
+                        bert.GEMM = name
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
                     for _ in range(a.iters):

@@ -11,8 +11,12 @@ Compute layout for MI355X: bf16 everywhere, fused QKV projection (one
 kernel (K12, csrc/kernels/bert.hip) that reads Q/K/V straight from the QKV
 GEMM's output (computed without its bias, which K12 applies), applies the
 key-padding mask and writes the [tokens, hidden] layout the output projection reads (torch SDPA is the fallback for sequences
-over 384 or off the GPU), plain GEMMs on hipBLASLt, the GELU
-in the FFN-up GEMM's epilogue (``torch._addmm_activation``) and every
+over 384 or off the GPU), the projections on the hand-written K18 GEMM
+(csrc/kernels/gemm_tiles.hip) at the token counts where it beat hipBLASLt
+(gemm_route: up to 768 tokens, the attention-out projection to 3,072; the
+N = 1024 projections split over K into fp32 slabs that the LayerNorm kernel
+sums) and on hipBLASLt above, the GELU
+in the FFN-up GEMM's epilogue and every
 residual add + LayerNorm as ONE hand-written HIP kernel (K11,
 csrc/kernels/bert.hip), as is the embedding sum + LayerNorm.  The serving wrapper captures one HIP graph per
 batch bucket.
@@ -36,25 +40,53 @@ TYPES = 2
 
 # fused paths on the GPU (bf16 CUDA tensors); TC_BERT_FUSED=0 runs plain torch ops
 FUSED = os.environ.get("TC_BERT_FUSED", "1") != "0"
-# K17 (the hand-written gfx950 GEMM) for the projections _k17_takes names;
-# off by default: inside the served HIP graphs the forward is slower with it
-# at every batch (bs1 +16 %, bs8 +6 %, bs64 +3-6 %, profiles/r5_k17_gemm.md)
-# although the large-M shapes match or beat hipBLASLt as standalone launches
-K17 = os.environ.get("TC_BERT_K17", "0") == "1"
-K17_MIN_TOKENS = int(os.environ.get("TC_BERT_K17_MIN_TOKENS", "12288"))
+# Who runs the four projection GEMMs: "auto" = the measured routing table
+# below (our K18 where it beat hipBLASLt, the library elsewhere), "ours" =
+# the hand-written kernels everywhere (K18 for small / mid token counts, K17
+# above), "lib" = hipBLASLt everywhere.
+GEMM = os.environ.get("TC_BERT_GEMM", "auto")
+
+# Measured routing (tools/gemm_sweep.py on MI355X, profiles/r6_bert_gemms.md:
+# each arm in a HIP graph over weight copies past the Infinity Cache, the
+# N = 1024 projections timed together with the residual add + LayerNorm that
+# follows them).  Per projection: (largest token count, route), first match
+# wins; route = ("k18", cfg, splits) -- splits > 1 leaves fp32 partial slabs
+# that K11p sums into the LayerNorm -- or ("k17",).  Past the last entry:
+# hipBLASLt (auto) or OURS_LARGE (ours).
+GEMM_ROUTES = {
+    "qkv": [(384, ("k18", 6, 1)), (768, ("k18", 3, 1))],
+    "out": [(384, ("k18", 9, 1)), (768, ("k18", 6, 1)), (1536, ("k18", 0, 1)), (3072, ("k18", 3, 1))],
+    "ffn_up": [(384, ("k18", 1, 1)), (768, ("k18", 3, 1))],
+    "ffn_down": [(384, ("k18", 6, 2)), (768, ("k18", 7, 2)), (1536, ("k18", 2, 2))],
+}
+OURS_LARGE = {"qkv": ("k17",), "out": ("k18", 3, 1), "ffn_up": ("k17",), "ffn_down": ("k18", 3, 1)}
+OURS_LARGE_FROM = 3072  # tokens from which "ours" uses OURS_LARGE instead of the last table entry
 
 
-def _k17_takes(M, N, K, epilogue):
-    """The projections K17 (csrc/kernels/gemm.hip) matched or beat hipBLASLt on
-    as standalone launches (profiles/r5_k17_gemm.md): the QKV projection (no
-    epilogue) and FFN-up + GELU from TC_BERT_K17_MIN_TOKENS tokens (1.04-1.06x
-    and 0.99-1.00x at 24,576), the attention-out projection (N = K = 1024,
-    bias) up to 3,072 tokens; FFN-down stays on the library."""
-    if N % 256 or K % 32:
-        return False
-    if epilogue in ("none", "bias_gelu"):
-        return M >= K17_MIN_TOKENS
-    return epilogue == "bias" and N * K <= 1024 * 1024 and M <= 3072
+def gemm_route(name, M, mode=None):
+    """The kernel that runs projection ``name`` at ``M`` tokens: ("lib",),
+    ("k17",) or ("k18", cfg, splits)."""
+    mode = mode or GEMM
+    if mode == "lib":
+        return ("lib",)
+    for top, route in GEMM_ROUTES[name]:
+        if M <= top:
+            return route
+    if mode == "ours":
+        return OURS_LARGE[name] if M >= OURS_LARGE_FROM else GEMM_ROUTES[name][-1][1]
+    return ("lib",)
+
+
+def _bias_f32(lin, dev):
+    b = getattr(lin, "bias_f32", None)
+    if b is None or b.device != dev:
+        b = lin.bias_f32 = lin.bias.detach().float().contiguous()
+    return b
+
+
+def _ours_ok(x2, lin):
+    return (FUSED and x2.is_cuda and x2.dtype == torch.bfloat16 and lin.weight.dtype == torch.bfloat16
+            and x2.stride(1) == 1 and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0 and lin.weight.is_contiguous())
 
 
 def _k17(x2, lin, epilogue):
@@ -63,29 +95,68 @@ def _k17(x2, lin, epilogue):
     M, K = x2.shape
     N = lin.weight.shape[0]
     out = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
-    bias = None
-    if epilogue != "none":
-        bias = getattr(lin, "bias_f32", None)
-        if bias is None or bias.device != x2.device:
-            bias = lin.bias_f32 = lin.bias.detach().float().contiguous()
+    bias = None if epilogue == "none" else _bias_f32(lin, x2.device)
     hip.k17_gemm(x2.data_ptr(), lin.weight.data_ptr(), None if bias is None else bias.data_ptr(), out.data_ptr(), M, N,
                  K, x2.stride(0), lin.weight.stride(0), N, epilogue=epilogue,
                  stream=torch.cuda.current_stream(x2.device).cuda_stream)
     return out
 
 
-def _proj(x, lin, epilogue="bias"):
+def _k18(x2, lin, epilogue, cfg, splits=1):
+    """K18 (csrc/kernels/gemm_tiles.hip); splits > 1: fp32 partial slabs
+    [splits, M, N] (no epilogue), for K11p to sum."""
+    from triton_client_amd.ops import hip
+
+    M, K = x2.shape
+    N = lin.weight.shape[0]
+    st = torch.cuda.current_stream(x2.device).cuda_stream
+    if splits > 1:
+        out = torch.empty(splits, M, N, device=x2.device, dtype=torch.float32)
+        hip.k18_gemm(x2.data_ptr(), lin.weight.data_ptr(), None, out.data_ptr(), M, N, K, x2.stride(0),
+                     lin.weight.stride(0), N, out_f32=True, cfg=cfg, splits=splits, split_stride=M * N, stream=st)
+        return out
+    out = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
+    bias = None if epilogue == "none" else _bias_f32(lin, x2.device)
+    hip.k18_gemm(x2.data_ptr(), lin.weight.data_ptr(), None if bias is None else bias.data_ptr(), out.data_ptr(), M,
+                 N, K, x2.stride(0), lin.weight.stride(0), N, epilogue=epilogue, cfg=cfg, stream=st)
+    return out
+
+
+def _route_ok(route, M, N, K):
+    """The shape constraints of the routed kernel (else the library runs it)."""
+    if route[0] == "k17":
+        return N % 256 == 0 and K % 32 == 0
+    if route[0] == "k18":
+        from triton_client_amd.ops import hip
+
+        tn = hip.k18_cfg(route[1])[1]
+        return N % tn == 0 and K % (64 * route[2]) == 0
+    return False
+
+
+class _Parts:
+    """A split-K projection's fp32 partial slabs [splits, tokens, N] (no bias)."""
+
+    def __init__(self, slabs):
+        self.slabs = slabs
+
+
+def _proj(x, lin, epilogue="bias", name=None, allow_split=False):
     """lin(x) (epilogue "bias"), gelu(lin(x)) ("bias_gelu") or x @ W^T ("none").
-    On the GPU in bf16: hipBLASLt, or K17, the hand-written gfx950 GEMM, with
-    TC_BERT_K17=1 (_k17_takes).  Config 4 is library-bound on these GEMMs:
-    K15 (rounds 3-4) reached 0.80-0.93x of hipBLASLt; K17 (round 5) 0.76-1.06x
-    at 24,576 tokens and loses inside the served graphs at small batches."""
+    On the GPU in bf16 the routing table picks K18 / K17 (the hand-written
+    gfx950 GEMMs) or hipBLASLt per projection and token count (gemm_route).
+    With ``allow_split`` a split-K route returns its fp32 partial slabs
+    [splits, tokens, N] as _Parts (the caller's K11p sums them with the bias)."""
     x2 = x.reshape(-1, x.shape[-1])
     n = lin.weight.shape[0]
-    if (FUSED and K17 and x2.is_cuda and x2.dtype == torch.bfloat16 and lin.weight.dtype == torch.bfloat16
-            and x2.stride(1) == 1 and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0 and lin.weight.is_contiguous()
-            and _k17_takes(x2.shape[0], n, x2.shape[1], epilogue)):
-        return _k17(x2, lin, epilogue).view(*x.shape[:-1], n)
+    if name is not None and _ours_ok(x2, lin):
+        route = gemm_route(name, x2.shape[0])
+        if _route_ok(route, x2.shape[0], n, x2.shape[1]):
+            if route[0] == "k17":
+                return _k17(x2, lin, epilogue).view(*x.shape[:-1], n)
+            splits = route[2] if allow_split and epilogue == "bias" else 1
+            y = _k18(x2, lin, epilogue, route[1], splits)
+            return _Parts(y) if splits > 1 else y.view(*x.shape[:-1], n)
     if getattr(lin, "w3", None) is not None and x2.is_cuda and x2.dtype == torch.float32:
         y = _mm_x3(x2, lin.w3)
         if epilogue != "none":
@@ -128,6 +199,26 @@ def prepare_x3(model):
                 lin.w3 = torch.cat([hi, lo, hi], dim=1).contiguous()
     model.precision = "fp32"
     return model
+
+
+def _proj_add_ln(x, a, lin, ln, name):
+    """LayerNorm(x + lin(a)): the attention-out / FFN-down projection and the
+    residual add + LayerNorm behind it.  A split-K route hands its fp32
+    partial slabs to K11p, which sums them with the bias and the residual on
+    its way into the LayerNorm (no reduce launch, no bf16 y)."""
+    y = _proj(a, lin, "bias", name=name, allow_split=True)
+    if isinstance(y, _Parts):
+        from triton_client_amd.ops import hip
+
+        p = y.slabs
+        out = torch.empty_like(x)
+        rows, H = p.shape[1], p.shape[2]
+        assert x.is_contiguous() and x.numel() == rows * H
+        hip.add_layernorm_parts(x.data_ptr(), p.data_ptr(), p.shape[0], rows * H, _bias_f32(lin, x.device).data_ptr(),
+                                ln.weight.data_ptr(), ln.bias.data_ptr(), out.data_ptr(), rows, H, ln.eps,
+                                stream=torch.cuda.current_stream(x.device).cuda_stream)
+        return out
+    return _add_ln(x, y, ln)
 
 
 def _add_ln(x, y, ln):
@@ -194,12 +285,12 @@ class _Layer(nn.Module):
         if _k12_ok(x, s):
             # plain GEMM (no bias epilogue: 152 vs 171 us at bs64 x 384,
             # profiles/r3_bert_gemm_layout.log); K12 applies the bias
-            qkv = _proj(x, self.qkv, "none")
+            qkv = _proj(x, self.qkv, "none", name="qkv")
             a = _attention(qkv, b, s, mask_i32, bias, qkv_bias=self.qkv.bias)
         else:
             a = _attention(_proj(x, self.qkv), b, s, mask_i32, bias)
-        x = _add_ln(x, _proj(a, self.out), self.ln1)
-        return _add_ln(x, _proj(_proj(x, self.ffn1, "bias_gelu"), self.ffn2), self.ln2)
+        x = _proj_add_ln(x, a, self.out, self.ln1, "out")
+        return _proj_add_ln(x, _proj(x, self.ffn1, "bias_gelu", name="ffn_up"), self.ffn2, self.ln2, "ffn_down")
 
 
 class BertLargeQA(nn.Module):

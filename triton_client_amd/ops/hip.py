@@ -249,6 +249,23 @@ _SIGS = {
         ctypes.c_int,
     ),
     "tcamd_k17_last_tm": ([], ctypes.c_int),
+    "tcamd_k18_gemm": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+         ctypes.c_longlong, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "tcamd_k18_cfg": (
+        [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+         ctypes.POINTER(ctypes.c_int)],
+        ctypes.c_int,
+    ),
+    "tcamd_k18_calls": ([], ctypes.c_longlong),
+    "tcamd_add_layernorm_parts": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_k17_calls": ([], ctypes.c_longlong),
     "tcamd_x3_cat": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "tcamd_x3_stem": (
@@ -918,6 +935,39 @@ def k17_gemm(a, b, bias, c, M, N, K, lda, ldb, ldc, epilogue="none", out_f32=Fal
     multiple of 256, K of 32."""
     _check(_load().tcamd_k17_gemm(a, b, _vp(bias), c, int(M), int(N), int(K), int(lda), int(ldb), int(ldc),
                                   K17_EPI[epilogue], 1 if out_f32 else 0, _vp(stream)), "k17_gemm")
+
+
+def k18_gemm(a, b, bias, c, M, N, K, lda, ldb, ldc, epilogue="none", out_f32=False, cfg=0, splits=1,
+             split_stride=0, stream=None):
+    """K18 (csrc/kernels/gemm_tiles.hip): the small / mid-M tiled GEMM.  As
+    k17_gemm, with the tile configuration ``cfg`` (k18_cfg) and, for
+    ``splits`` > 1, K split over workgroups: C is then fp32, no epilogue, and
+    split z writes its partial product at C + z * split_stride (elements)."""
+    _check(_load().tcamd_k18_gemm(a, b, _vp(bias), c, int(M), int(N), int(K), int(lda), int(ldb), int(ldc),
+                                  K17_EPI[epilogue], 1 if out_f32 else 0, int(cfg), int(splits), int(split_stride),
+                                  _vp(stream)), "k18_gemm")
+
+
+def k18_cfg(cfg):
+    """(tile rows, tile columns, threads, ring stages) of K18 configuration ``cfg``, or None past the table."""
+    v = [ctypes.c_int(0) for _ in range(4)]
+    if _load().tcamd_k18_cfg(int(cfg), *[ctypes.byref(x) for x in v]) != 0:
+        return None
+    return tuple(x.value for x in v)
+
+
+def k18_calls():
+    """K18 launches so far in this process."""
+    return int(_load().tcamd_k18_calls())
+
+
+def add_layernorm_parts(x, parts, nparts, pstride, bias, gamma, beta, out, rows, H, eps, f32=False, stream=None):
+    """K11p: out = LayerNorm(x + bias + sum of ``nparts`` fp32 partial slabs
+    (``parts`` + z * ``pstride`` elements, [rows][H] each)) * gamma + beta.
+    bias fp32 [H] or None; x / gamma / beta / out bf16, or fp32 with ``f32``."""
+    _check(_load().tcamd_add_layernorm_parts(x, _vp(parts), int(nparts), int(pstride), _vp(bias), gamma, beta, out,
+                                             int(rows), int(H), float(eps), 1 if f32 else 0, _vp(stream)),
+           "add_layernorm_parts")
 
 
 def k17_last_tm():

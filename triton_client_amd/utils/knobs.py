@@ -44,6 +44,8 @@ KNOBS = [
          "tests/test_kernels_gpu.py::test_pack_bytes_big_block_path"),
     Knob("TCAMD_K3_MODE", "native", 0, "K3 BYTES index", "", _KN + "test_k3_general_walk_mode"),
     Knob("TCAMD_K17_TM", "native", 0, "K17 GEMM tile height", "", "tests/test_gemm_gpu.py::test_k17_gemm_bf16_out"),
+    Knob("TCAMD_K17_DYN", "native", 1, "K17 GEMM tile scheduling", "",
+         "tests/test_gemm_gpu.py::test_k17_dynamic_schedule_every_tile_once"),
     # ---- python: fp32 DenseNet engine routing (models/densenet_fp32.py, engine attributes) ----
     Knob("TCAMD_X3_FUSE_MIN_TPB", "python", 1, "FP32DenseNet.fuse_min_tiles",
          "K11x for a block when every workgroup gets this many 64-pixel tiles; 0 = the K8x + K9x pair",
@@ -69,12 +71,9 @@ KNOBS = [
     # ---- python: BERT ----
     Knob("TC_BERT_FUSED", "python", 1, "models/bert.py FUSED",
          "K11 / K12 fused kernels on the GPU; 0 = plain torch ops", "tests/test_bert_kernels_gpu.py::test_bert_fused_layers_match_torch_ops"),
-    Knob("TC_BERT_K17", "python", 0, "models/bert.py K17",
-         "1 = K17 (hand-written GEMM) for the projections _k17_takes names; 0 = hipBLASLt",
-         "tests/test_gemm_gpu.py::test_bert_projections_k17_vs_library"),
-    Knob("TC_BERT_K17_MIN_TOKENS", "python", 12288, "models/bert.py K17_MIN_TOKENS",
-         "with TC_BERT_K17=1: tokens from which QKV and FFN-up + GELU go to K17",
-         "tests/test_gemm_gpu.py::test_bert_projections_k17_vs_library"),
+    Knob("TC_BERT_GEMM", "python", "auto", "models/bert.py GEMM",
+         "projection GEMMs: auto = the measured routing table (K18 where it beat hipBLASLt), ours = K18 / K17 "
+         "everywhere, lib = hipBLASLt everywhere", "tests/test_gemm_gpu.py::test_bert_projection_routes"),
     Knob("TC_BERT_TUNED_GEMMS", "python", 0, "models/bert.py use_tuned_gemms",
          "TunableOp with the committed gfx950 solution table (process-wide; measured neutral)",
          _KN + "test_bert_tuned_gemm_table"),
