@@ -157,17 +157,25 @@ class Lanes:
         self.s = points[0].s  # server statistics are per model, any lane reads them
 
     def run(self, n):
+        """Per-request latencies and completion times of all lanes on ONE
+        clock: each lane's end_ns counts from its own run's start, so every
+        lane's times are shifted to the earliest lane start (a lane's start =
+        its return time minus its elapsed run time) before they are merged --
+        the window statistics sort them as one timeline."""
         import threading
+        import time
 
         import numpy as np
 
         k = len(self.points)
         out = [None] * k
+        back = [0] * k
         errs = []
 
         def go(i):
             try:
                 out[i] = self.points[i].run(n // k)
+                back[i] = time.perf_counter_ns()
             except Exception as e:  # noqa: BLE001 -- re-raised below
                 errs.append(e)
 
@@ -178,11 +186,24 @@ class Lanes:
             t.join()
         if errs:
             raise errs[0]
-        return (np.concatenate([o[0] for o in out]), np.concatenate([o[1] for o in out]), max(o[2] for o in out))
+        return merge_lanes(out, back)
 
     def close(self):
         for p in self.points:
             p.close()
+
+
+def merge_lanes(out, back_ns):
+    """Lane results [(lat_ns, end_ns, elapsed_s)] and each lane's return time
+    (perf_counter ns) -> one (lat_ns, end_ns, elapsed_s) with every end_ns on
+    the clock of the earliest-starting lane."""
+    import numpy as np
+
+    starts = [b - int(o[2] * 1e9) for o, b in zip(out, back_ns)]
+    t0 = min(starts)
+    ends = [o[1].astype(np.int64) + (st - t0) for o, st in zip(out, starts)]
+    span = max(b - t0 for b in back_ns) * 1e-9
+    return np.concatenate([o[0] for o in out]), np.concatenate(ends).astype(np.uint64), span
 
 
 def windows(end_ns, per, k):

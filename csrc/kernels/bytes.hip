@@ -1604,7 +1604,13 @@ static hipError_t ix_canary_check(hipStream_t s) {
 }
 
 // Overrun check mode on / off (tests); returns the previous setting.
-extern "C" int tcamd_k3_set_check(int on) { return g_ix_check.exchange(on ? 1 : 0); }
+// under g_ix_mu: tcamd_index_bytes holds it for its whole call and reads the
+// flag several times (workspace sizing, after the walk, after the final
+// sync), so the mode never flips inside a call (round-5 advisor finding)
+extern "C" int tcamd_k3_set_check(int on) {
+  std::lock_guard<std::mutex> lk(g_ix_mu);
+  return g_ix_check.exchange(on ? 1 : 0);
+}
 
 static int index_locked(const void* buf, uint64_t nbytes, uint64_t n_expected, uint64_t* offs, uint32_t* lens,
                         int* status, hipStream_t s) {

@@ -103,3 +103,20 @@ def test_bench_bert_sweep_two_ranks():
     assert res["value"] == res["sweep"][-1]["infer_per_sec"]
     assert "fanned out by gloo" in res["data"]
     assert "bert c4" in err
+
+
+def test_merge_lanes_puts_lanes_on_one_clock():
+    """Lanes started at different times: their completion times are shifted to
+    the earliest lane's clock before the windows sort them (round-5 advisor
+    finding: mixed time bases skewed the per-window statistics)."""
+    import numpy as np
+
+    import bench
+
+    # lane 0 ran 0..1.0 s, lane 1 started 0.5 s later and ran 1.0 s
+    lane0 = (np.array([5, 6], dtype=np.uint64), np.array([400_000_000, 1_000_000_000], dtype=np.uint64), 1.0)
+    lane1 = (np.array([7, 8], dtype=np.uint64), np.array([100_000_000, 1_000_000_000], dtype=np.uint64), 1.0)
+    lat, end, span = bench.merge_lanes([lane0, lane1], [2_000_000_000, 2_500_000_000])
+    assert list(lat) == [5, 6, 7, 8]
+    assert list(end) == [400_000_000, 1_000_000_000, 600_000_000, 1_500_000_000]
+    assert abs(span - 1.5) < 1e-9

@@ -46,6 +46,16 @@ def test_gpu_order_and_pci_addresses(tmp_path, monkeypatch):
     assert placement.gpu_bdfs(root) == ["0000:10:00.0", "0000:20:00.0", "0000:30:00.0", "0000:40:00.0"]
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "2,0")
     assert placement.gpu_bdfs(root) == ["0000:30:00.0", "0000:10:00.0"]
+    # CUDA_VISIBLE_DEVICES is HIP's alias, used only when HIP_VISIBLE_DEVICES
+    # is unset: with both set it must not filter a second time
+    monkeypatch.setenv("CUDA_VISIBLE_DEVICES", "1")
+    assert placement.gpu_bdfs(root) == ["0000:30:00.0", "0000:10:00.0"]
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    assert placement.gpu_bdfs(root) == ["0000:20:00.0"]
+    # ROCR filters first, HIP indexes what is left
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "3,1,2")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "2,0")
+    assert placement.gpu_bdfs(root) == ["0000:30:00.0", "0000:40:00.0"]
 
 
 def test_two_socket_eight_gpus(tmp_path, monkeypatch):

@@ -138,7 +138,7 @@ class FusedDenseNetFP32:
         # has at least this many workgroups (images x row tiles: 2-4 per 14x14
         # image, 1-4 per 7x7 image, x3_small_tiles); 0 disables it.  Unset:
         # 48 when the engine is one of several concurrent streams (a server's
-        # model instances: concurrent_streams), else 80 -- K14x beats the
+        # model instances: concurrent_streams), else 64 -- K14x beats the
         # K13x chain from bs12 on two streams (+6 / +13 / +19 % at bs12 / 14 /
         # 16) but only from bs20 on one (profiles/r5_engine_ab.md)
         env = os.environ.get("TCAMD_X3_SMALLF_MIN_BLOCKS")

@@ -77,7 +77,8 @@ def _props(text):
 
 def gpu_bdfs(root="/"):
     """PCI addresses of the GPUs in the runtime's enumeration order, after
-    ``HIP_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES``."""
+    ``ROCR_VISIBLE_DEVICES`` and then ``HIP_VISIBLE_DEVICES`` (or its alias
+    ``CUDA_VISIBLE_DEVICES`` when that is unset)."""
     base = os.path.join(root, KFD_NODES)
     try:
         ids = sorted(int(n) for n in os.listdir(base) if n.isdigit())
@@ -90,7 +91,11 @@ def gpu_bdfs(root="/"):
             continue
         loc, dom = p.get("location_id", 0), p.get("domain", 0)
         out.append("%04x:%02x:%02x.%x" % (dom, (loc >> 8) & 0xFF, (loc >> 3) & 0x1F, loc & 0x7))
-    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+    # ROCR filters first; then HIP applies HIP_VISIBLE_DEVICES, and
+    # CUDA_VISIBLE_DEVICES only as its alias when HIP_VISIBLE_DEVICES is unset
+    # (never both: a second filter would map a rank to the wrong GPU)
+    hip_var = "HIP_VISIBLE_DEVICES" if os.environ.get("HIP_VISIBLE_DEVICES") else "CUDA_VISIBLE_DEVICES"
+    for var in ("ROCR_VISIBLE_DEVICES", hip_var):
         vis = os.environ.get(var)
         if vis:
             try:

@@ -51,10 +51,7 @@ def main(argv=None):
     from .app import default_models, serve
     from .core import InferenceServer
 
-    models = default_models(gpu=args.gpu)
-    if args.models:
-        keep = set(args.models.split(","))
-        models = [m for m in models if m.name in keep]
+    models = default_models(gpu=args.gpu, names=args.models.split(",") if args.models else None)
     opts = {}
     for m in models:
         if getattr(m, "instance_kind", "") == "KIND_GPU":

@@ -15,14 +15,23 @@ from .grpc_frontend import FaultInjector, GrpcFrontend
 from .http_frontend import HttpFrontend
 
 
-def default_models(gpu=False):
+def default_models(gpu=False, names=None):
+    """The model classes a server loads: the CPU zoo, plus the GPU zoo with
+    ``gpu``; ``names`` (an iterable of model names) selects a subset and may
+    also name the opt-in GPU models (OPT_IN_GPU_MODELS), which no default
+    list contains."""
     from .cpu_models import CPU_MODELS
 
     models = list(CPU_MODELS)
     if gpu:
-        from .gpu_models import GPU_MODELS
+        from .gpu_models import GPU_MODELS, OPT_IN_GPU_MODELS
 
         models += list(GPU_MODELS)
+        if names is not None:
+            models += [m for m in OPT_IN_GPU_MODELS if m.name in set(names)]
+    if names is not None:
+        keep = set(names)
+        models = [m for m in models if m.name in keep]
     return models
 
 

@@ -785,4 +785,7 @@ class BertLargeFP32(BertLarge):
         return bert.prepare_x3(bert.build(device=dev, dtype=torch.float32, layers=self.layers))
 
 
-GPU_MODELS = [DensenetOnnx, PreprocessInceptionEnsemble, BertLarge, BertLargeFP32]
+GPU_MODELS = [DensenetOnnx, PreprocessInceptionEnsemble, BertLarge]
+# loaded only when --models names them: bert_large_fp32 adds ~2 GB of bf16x3
+# weights and 28 captured HIP graphs per instance (round-5 advisor finding)
+OPT_IN_GPU_MODELS = [BertLargeFP32]
