@@ -141,6 +141,27 @@ class Point:
     def run(self, n):
         return self.s.run_timed(self.conc, n)
 
+    # ---- continuous closed loop (measure): no restart between warm-up and timing ----
+    def start(self):
+        self.s.loop_start(self.conc)
+
+    def marks(self):
+        return [self.s.loop_count()]
+
+    def wait_after(self, marks, n):
+        self.s.loop_wait(marks[0][0] + n)
+
+    def take(self, marks, n, t0_ns):
+        """The first n requests completed after ``marks``: latencies (ns) and
+        completion times (ns after t0_ns on the engine clock), completion order."""
+        st, en, ok = self.s.loop_records(marks[0][0], n)
+        if len(en) < n or not ok.all():
+            raise RuntimeError("the loop lost requests (%d of %d, %d failed)" % (len(en), n, int((ok == 0).sum())))
+        return en - st, en.astype("int64") - int(t0_ns)
+
+    def stop(self):
+        self.s.loop_stop()
+
     def close(self):
         self.s.close()
 
@@ -187,6 +208,42 @@ class Lanes:
         if errs:
             raise errs[0]
         return merge_lanes(out, back)
+
+    # ---- continuous closed loop: every lane at once ----
+    def start(self):
+        for p in self.points:
+            p.start()
+
+    def marks(self):
+        return [p.s.loop_count() for p in self.points]
+
+    def wait_after(self, marks, n):
+        k = len(self.points)
+        for p, m in zip(self.points, marks):  # equal concurrency per lane: each takes its share
+            p.s.loop_wait(m[0] + -(-n // k))
+
+    def take(self, marks, n, t0_ns):
+        """All lanes' completions since ``marks`` merged on the engine clock
+        (one steady clock in this process); the first n by completion time."""
+        import numpy as np
+
+        lat, end = [], []
+        for p, m in zip(self.points, marks):
+            cnt, _ = p.s.loop_count()
+            st, en, ok = p.s.loop_records(m[0], cnt - m[0])
+            if not ok.all():
+                raise RuntimeError("a lane's loop had failed requests")
+            lat.append(en - st)
+            end.append(en.astype(np.int64) - int(t0_ns))
+        lat, end = np.concatenate(lat), np.concatenate(end)
+        if len(end) < n:
+            raise RuntimeError("the lanes completed %d of %d requests" % (len(end), n))
+        order = np.argsort(end, kind="stable")[:n]
+        return lat[order], end[order]
+
+    def stop(self):
+        for p in self.points:
+            p.stop()
 
     def close(self):
         for p in self.points:
@@ -397,20 +454,36 @@ def main():
             state["client"].register_cuda_shared_memory(name, shmod.get_raw_handle(r), dev, nbytes)
         return method, nbytes
 
-    def measure(point, steps, per):
-        """W warmup already done; EXACTLY `steps` windows between barrier + sync."""
-        if world > 1:
-            fanout.barrier()
-        if not cpu:
-            torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        lat, end, _ = point.run(steps * per)
-        if not cpu:
-            torch.cuda.synchronize()
-        if world > 1:
-            fanout.barrier()
-        elapsed = time.perf_counter() - t0
-        return lat, end, fanout.max_over_ranks(elapsed)
+    def measure(point, warm_n, steps, per, snap=None):
+        """One continuous closed loop: `warm_n` untimed warm-up requests, then
+        EXACTLY `steps` windows of `per` requests between barrier + sync, in
+        the SAME loop (no restart, so the timed windows start in steady state
+        instead of with a refilling pipeline; round 5's first window carried
+        that refill's tail).  `snap()` (server statistics) is read right
+        before the timed start and right after the last timed completion.
+        Returns latencies, completion times (ns after the timed start),
+        elapsed (max over ranks) and the two snapshots."""
+        point.start()
+        try:
+            point.wait_after(point.marks(), warm_n)
+            s0 = snap() if snap else None  # outside the timed windows: its RPC would ride in window 0
+            if world > 1:
+                fanout.barrier()
+            if not cpu:
+                torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            m = point.marks()
+            point.wait_after(m, steps * per)
+            s1 = snap() if snap else None
+            if not cpu:
+                torch.cuda.synchronize()
+            if world > 1:
+                fanout.barrier()
+            elapsed = time.perf_counter() - t0
+            lat, end = point.take(m, steps * per, m[0][1])
+        finally:
+            point.stop()
+        return lat, end, fanout.max_over_ranks(elapsed), (s0, s1)
 
     try:
         log("waiting for server (log %s)" % srv_log)
@@ -470,13 +543,9 @@ def main():
             lanes8.append(Point(srv, model, bs, conc // nl8, None, in_bytes, dev, cpu, inputs=ins, outputs=outs))
         p8 = Lanes(lanes8)
         points.extend(lanes8)
-        lat_w, _, _ = p8.run(max(args.warmup, 1) * per)
-        log("warmup done: p50 %.0f us" % percentile_us(lat_w.astype(np.float64), 50))
-        st0 = p8.s.server_stats()
-        bst0 = batch_stats(client, model)
-        lat, end, elapsed = measure(p8, args.steps, per)
-        st1 = p8.s.server_stats()
-        bst1 = batch_stats(client, model)
+        lat, end, elapsed, ((st0, bst0), (st1, bst1)) = measure(
+            p8, max(args.warmup, 1) * per, args.steps, per,
+            snap=lambda: (p8.s.server_stats(), batch_stats(client, model)))
         wins = windows(end, per, args.steps)
         # the last window holds the closed loop's drain (no new issues), so the
         # stability rule looks at the three windows before it
@@ -513,12 +582,19 @@ def main():
                 pc = Point(srv, model, bs, c, None, in_bytes, dev, cpu, inputs=ins_c, outputs=outs_c)
                 points.append(pc)
                 perc = 16 * c
-                pc.run(perc)
-                lc_, _, elc = measure(pc, 4, perc)
+                lc_, _, elc, ((sp0, bp0), (sp1, bp1)) = measure(
+                    pc, perc, 4, perc, snap=lambda: (pc.s.server_stats(), batch_stats(client, model)))
                 lg = fanout.gather_arrays(lc_.astype(np.int64)).astype(np.float64)
                 row = {"concurrency": c, "infer_per_sec": round(world * 4 * perc * bs / elc, 1),
                        "p50_latency_us": round(percentile_us(lg, 50), 1),
                        "p99_latency_us": round(percentile_us(lg, 99), 1)}
+                # why a probe lands where it does: rows per executed batch
+                # (how the c x bs rows in flight split into batches over the
+                # instances), queueing and device time per batch (rank 0)
+                bdp = stats_delta(sp0, sp1)
+                bdp["batch_rows_histogram"] = {str(k): int(bp1[k][0] - bp0.get(k, (0,))[0]) for k in sorted(bp1)
+                                               if bp1[k][0] - bp0.get(k, (0,))[0] > 0}
+                row["breakdown_rank0"] = bdp
                 p99c["points"].append(row)
                 log("p99-constrained probe c%d: %.0f infer/s p99 %.0f us" % (c, row["infer_per_sec"],
                                                                              row["p99_latency_us"]))
@@ -536,10 +612,8 @@ def main():
         p1 = Lanes([Point(srv, model, 1, args.bs1_concurrency // nl, "data_1_in", in1, dev, cpu) for _ in range(nl)])
         points.extend(p1.points)
         n1 = 64 * args.bs1_concurrency  # ~0.2 s at 20k infer/s: the batch groups of a closed loop need time to settle
-        p1.run(n1 // 4)
-        s10, b10 = p1.s.server_stats(), batch_stats(client, model)
-        l1, e1, el1 = measure(p1, 4, n1 // 4)
-        s11, b11 = p1.s.server_stats(), batch_stats(client, model)
+        l1, e1, el1, ((s10, b10), (s11, b11)) = measure(
+            p1, n1 // 4, 4, n1 // 4, snap=lambda: (p1.s.server_stats(), batch_stats(client, model)))
         bs1 = {"concurrency": args.bs1_concurrency, "client_lanes": nl, "infer_per_sec": round(world * n1 / el1, 1)}
         # where a bs=1 request's latency goes at this concurrency: rows per
         # batch, queueing, and the request-weighted device time of its batch
@@ -641,8 +715,7 @@ def main():
             ins, outs = slots(conc)
             pb = Point(srv, model, bs, conc, None, in_bytes, dev, cpu, inputs=ins, outputs=outs)
             points.append(pb)
-            pb.run(per)
-            _, _, elb = measure(pb, max(2, args.steps // 4), per)
+            _, _, elb, _ = measure(pb, per, max(2, args.steps // 4), per)
             res["bf16_engine_infer_per_sec"] = round(world * max(2, args.steps // 4) * per * bs / elb, 1)
             res["bf16_engine_note"] = "same pipeline, bf16 K8-K10 kernels: ~3e-2 rel-L2 off fp32 (not the headline)"
         if rehearse:
@@ -719,10 +792,8 @@ def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout
         pt = Point(srv, model, 1, c, None, nbytes, local_rank, cpu, inputs=inputs, out_bytes=BERT_SEQ * 4)
         points.append(pt)
         per = max(64, 8 * c)
-        pt.run(max(args.warmup, 1) * per)
-        s0, b0 = pt.s.server_stats(), batch_stats(client, model)
-        lat, _, elapsed = measure(pt, args.steps, per)
-        s1, b1 = pt.s.server_stats(), batch_stats(client, model)
+        lat, _, elapsed, ((s0, b0), (s1, b1)) = measure(
+            pt, max(args.warmup, 1) * per, args.steps, per, snap=lambda: (pt.s.server_stats(), batch_stats(client, model)))
         all_lat = fanout.gather_arrays(lat.astype(np.int64)).astype(np.float64)
         row = {"concurrency": c, "infer_per_sec": round(world * args.steps * per / elapsed, 1),
                "p50_latency_us": round(percentile_us(all_lat, 50), 1),

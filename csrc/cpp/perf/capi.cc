@@ -1,6 +1,7 @@
 // C ABI of the perf engine for in-process use from Python (bench.py drives
 // the native load generator through ctypes; ctypes drops the GIL for the
 // duration of each call, so no Python runs on the request path).
+#include <algorithm>
 #include <cstring>
 
 #include "perf.h"
@@ -65,6 +66,66 @@ int tcperf_run_fixed_timed(void* h, int concurrency, uint64_t total, uint64_t* l
   tcperf::Error e = s->engine->RunFixed(static_cast<size_t>(concurrency), total, &lat, elapsed_s, &end);
   if (lat_ns) memcpy(lat_ns, lat.data(), std::min<size_t>(lat.size(), total) * sizeof(uint64_t));
   if (end_ns) memcpy(end_ns, end.data(), std::min<size_t>(end.size(), total) * sizeof(uint64_t));
+  if (!e.IsOk()) {
+    SetErr(err, errlen, e.Message());
+    return 1;
+  }
+  return 0;
+}
+
+// Continuous closed loop (steady-state measurement without a restart between
+// the warm-up and the timed windows): start, mark indices with
+// tcperf_loop_count, wait for a completion count, read records, stop.
+int tcperf_loop_start(void* h, int concurrency, char* err, int errlen)
+{
+  auto* s = static_cast<tcperf::Session*>(h);
+  tcperf::Error e = s->engine->StartLoop(static_cast<size_t>(concurrency));
+  if (!e.IsOk()) {
+    SetErr(err, errlen, e.Message());
+    return 1;
+  }
+  return 0;
+}
+
+// completions so far (a record index) and the engine clock (ns)
+uint64_t tcperf_loop_count(void* h, uint64_t* now_ns)
+{
+  auto* s = static_cast<tcperf::Session*>(h);
+  if (now_ns) *now_ns = tcperf::NowNs();
+  return s->engine->CompletedCount();
+}
+
+int tcperf_loop_wait(void* h, uint64_t target, double timeout_s, char* err, int errlen)
+{
+  auto* s = static_cast<tcperf::Session*>(h);
+  tcperf::Error e = s->engine->WaitCompleted(static_cast<size_t>(target), timeout_s);
+  if (!e.IsOk()) {
+    SetErr(err, errlen, e.Message());
+    return 1;
+  }
+  return 0;
+}
+
+// records [from, from + n) (n clipped to what exists): start / end ns on the
+// engine clock and an ok flag; returns the number copied
+uint64_t tcperf_loop_records(void* h, uint64_t from, uint64_t n, uint64_t* start_ns, uint64_t* end_ns, uint8_t* ok)
+{
+  auto* s = static_cast<tcperf::Session*>(h);
+  std::vector<tcperf::Record> recs;
+  s->engine->Snapshot(static_cast<size_t>(from), &recs);
+  const uint64_t m = std::min<uint64_t>(n, recs.size());
+  for (uint64_t i = 0; i < m; ++i) {
+    if (start_ns) start_ns[i] = recs[i].start_ns;
+    if (end_ns) end_ns[i] = recs[i].end_ns;
+    if (ok) ok[i] = recs[i].ok ? 1 : 0;
+  }
+  return m;
+}
+
+int tcperf_loop_stop(void* h, char* err, int errlen)
+{
+  auto* s = static_cast<tcperf::Session*>(h);
+  tcperf::Error e = s->engine->StopLoop();
   if (!e.IsOk()) {
     SetErr(err, errlen, e.Message());
     return 1;

@@ -410,6 +410,42 @@ Error LoadEngine::SetRequestRate(double rate)
   return Error::Success;
 }
 
+Error LoadEngine::StartLoop(size_t concurrency)
+{
+  if (concurrency == 0 || concurrency > slots_.size()) return Error("bad concurrency for the prepared slots");
+  Error e = StopLoop();
+  if (!e.IsOk()) return e;
+  return SetConcurrency(concurrency);
+}
+
+Error LoadEngine::StopLoop()
+{
+  Error e = SetConcurrency(0);
+  if (!e.IsOk()) return e;
+  std::unique_lock<std::mutex> lk(mu_);
+  const bool drained = fixed_cv_.wait_for(lk, std::chrono::seconds(30),
+                                          [&] { return in_flight_.load() == 0 && done_.empty(); });
+  lk.unlock();
+  for (auto& t : sync_threads_)
+    if (t.joinable()) t.join();
+  sync_threads_.clear();
+  return drained ? Error::Success : Error("requests still in flight 30 s after the loop stopped");
+}
+
+Error LoadEngine::WaitCompleted(size_t target, double timeout_s)
+{
+  std::unique_lock<std::mutex> lk(mu_);
+  bool failed = false;
+  const bool ok = fixed_cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] {
+    std::lock_guard<std::mutex> rl(rec_mu_);
+    failed = !first_error_.empty();
+    return failed || records_.size() >= target;
+  });
+  lk.unlock();
+  if (failed) return Error("request failed during the loop: " + FirstError());
+  return ok ? Error::Success : Error("loop timed out waiting for completions");
+}
+
 size_t LoadEngine::Snapshot(size_t since, std::vector<Record>* out)
 {
   std::lock_guard<std::mutex> lk(rec_mu_);

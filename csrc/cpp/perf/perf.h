@@ -290,6 +290,16 @@ class LoadEngine {
   Error RunFixed(size_t concurrency, uint64_t total, std::vector<uint64_t>* lat_ns, double* elapsed_s,
                  std::vector<uint64_t>* end_ns = nullptr);
   void Stop();
+  /// Continuous closed loop for steady-state measurement: quiesces any
+  /// previous load, then keeps `concurrency` requests in flight until
+  /// SetConcurrency(0) (or StopLoop).  Callers mark record indices with
+  /// CompletedCount and read the records with Snapshot.
+  Error StartLoop(size_t concurrency);
+  /// Stops issuing and waits (<= 30 s) until nothing is in flight.
+  Error StopLoop();
+  /// Waits until `target` records exist (all time, CompletedCount's index),
+  /// at most `timeout_s`; fails on a request error or the timeout.
+  Error WaitCompleted(size_t target, double timeout_s);
   /// Records completed since `since_index`; returns the new end index.
   size_t Snapshot(size_t since_index, std::vector<Record>* out);
   size_t CompletedCount();

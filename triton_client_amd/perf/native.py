@@ -46,6 +46,19 @@ def _load():
         lib.tcperf_profile.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.POINTER(ctypes.c_double),
                                        ctypes.c_char_p, ctypes.c_int]
         lib.tcperf_profile.restype = ctypes.c_int
+        lib.tcperf_loop_start.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        lib.tcperf_loop_start.restype = ctypes.c_int
+        lib.tcperf_loop_count.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+        lib.tcperf_loop_count.restype = ctypes.c_uint64
+        lib.tcperf_loop_wait.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_double, ctypes.c_char_p,
+                                         ctypes.c_int]
+        lib.tcperf_loop_wait.restype = ctypes.c_int
+        lib.tcperf_loop_records.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                            ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                            ctypes.POINTER(ctypes.c_uint8)]
+        lib.tcperf_loop_records.restype = ctypes.c_uint64
+        lib.tcperf_loop_stop.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
+        lib.tcperf_loop_stop.restype = ctypes.c_int
         lib.tcperf_describe.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
         lib.tcperf_describe.restype = ctypes.c_int
         lib.tcperf_session_destroy.argtypes = [ctypes.c_void_p]
@@ -99,6 +112,40 @@ class PerfSession:
         if rc != 0:
             raise PerfError(err.value.decode(errors="replace"))
         return lat, end, el.value
+
+    # ---- continuous closed loop (steady-state windows, no restart) ----
+    def loop_start(self, concurrency):
+        """Keep ``concurrency`` requests in flight until loop_stop."""
+        err = ctypes.create_string_buffer(1024)
+        if _load().tcperf_loop_start(self._h, int(concurrency), err, 1024) != 0:
+            raise PerfError(err.value.decode(errors="replace"))
+
+    def loop_count(self):
+        """(completions so far = a record index, engine clock ns)."""
+        now = ctypes.c_uint64(0)
+        n = _load().tcperf_loop_count(self._h, ctypes.byref(now))
+        return int(n), int(now.value)
+
+    def loop_wait(self, target, timeout_s=600.0):
+        """Block (GIL released) until ``target`` records exist."""
+        err = ctypes.create_string_buffer(1024)
+        if _load().tcperf_loop_wait(self._h, int(target), float(timeout_s), err, 1024) != 0:
+            raise PerfError(err.value.decode(errors="replace"))
+
+    def loop_records(self, start, n):
+        """Records [start, start + n): (start_ns, end_ns, ok) on the engine clock."""
+        st = np.zeros(int(n), dtype=np.uint64)
+        en = np.zeros(int(n), dtype=np.uint64)
+        ok = np.zeros(int(n), dtype=np.uint8)
+        p64 = ctypes.POINTER(ctypes.c_uint64)
+        m = _load().tcperf_loop_records(self._h, int(start), int(n), st.ctypes.data_as(p64), en.ctypes.data_as(p64),
+                                        ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+        return st[:m], en[:m], ok[:m]
+
+    def loop_stop(self):
+        err = ctypes.create_string_buffer(1024)
+        if _load().tcperf_loop_stop(self._h, err, 1024) != 0:
+            raise PerfError(err.value.decode(errors="replace"))
 
     def server_stats(self):
         out = (ctypes.c_uint64 * 8)()
