@@ -105,6 +105,9 @@ def parse_args(argv=None):
     ap.add_argument("--sweep", default="1,4,16,64,256", help="bert_large: concurrencies per GPU")
     ap.add_argument("--bert-instance-count", type=int, default=2)
     ap.add_argument("--bert-queue-delay-us", type=int, default=500)
+    ap.add_argument("--bert-precision", default="bf16", choices=["bf16", "fp32"],
+                    help="bert_large: bf16 (the config-4 default) or fp32 parity (serves bert_large_fp32: bf16x3 "
+                         "projections on the hand-written GEMMs, fp32 LayerNorm / attention)")
     return ap.parse_args(argv)
 
 
@@ -362,7 +365,7 @@ def main():
     cpu = args.cpu
     bert = args.model == "bert_large"
     if bert:
-        model = "bert_sink" if cpu else "bert_large"
+        model = "bert_sink" if cpu else ("bert_large_fp32" if args.bert_precision == "fp32" else "bert_large")
     else:
         model = "frontend_sink" if cpu else "densenet_onnx"
     bs, conc = args.batch, args.concurrency
@@ -787,6 +790,15 @@ def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout
                 raise RuntimeError("fan-out replicas differ across ranks")
             client.register_cuda_shared_memory(reg, shmod.get_raw_handle(r), local_rank, nbytes)
         inputs[name] = reg
+    fan = {"method": method, "replicas_verified": True, "bytes": nbytes}
+    if not cpu and world > 1:
+        # X1 vs X2 on the token-id region, as the densenet run does on its batch
+        rehearse = args.rehearse
+        fan["timings"] = fanout.time_fanout(regions[0], nbytes, ["p2p", "host"] if rehearse else
+                                            (["p2p"] if method == fanout.LOCAL_FALLBACK else ["rccl", "p2p"]))
+        fan["errors"] = fanout.fanout_errors(fan["timings"])
+        if not fanout.verify_replicas(regions[0], nbytes, over_cpu=method == fanout.LOCAL_FALLBACK):
+            raise RuntimeError("fan-out replicas differ across ranks after the fan-out timing")
     sweep = []
     for c in [int(v) for v in args.sweep.split(",") if v]:
         pt = Point(srv, model, 1, c, None, nbytes, local_rank, cpu, inputs=inputs, out_bytes=BERT_SEQ * 4)
@@ -817,7 +829,7 @@ def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32" if cpu else "bf16",
+        "dtype": "fp32" if (cpu or args.bert_precision == "fp32") else "bf16",
         "data": ("synthetic INT32 (host, fanned out by %s), CPU %s" % (method, model) if cpu else
                  "synthetic INT32 token ids / all-ones mask / zero segments (K1 on device, fanned out by %s), "
                  "random-init weights" % method),
@@ -827,7 +839,18 @@ def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout
                    "server_instances": args.bert_instance_count, "max_queue_delay_us": args.bert_queue_delay_us},
         "p99_latency_us": top["p99_latency_us"],
         "sweep": sweep,
+        "fanout": fan,
     }
+    if not cpu:
+        res["config"]["compute"] = ("fp32 parity: bf16x3 projections (x_hi W_hi + x_hi W_lo + x_lo W_hi, fp32 "
+                                    "accumulate), fp32 LayerNorm / softmax attention" if args.bert_precision == "fp32"
+                                    else "bf16 (fp32 accumulate)")
+        from triton_client_amd.models import bert as _bert
+
+        res["config"]["gemm_routing"] = _bert.GEMM
+    if args.rehearse and world > 1:
+        res["rehearsal"] = ("%d ranks on ONE GPU over gloo (launch/fan-out/aggregation rehearsal; "
+                            "not a scaling measurement)" % world)
     if rank == 0:
         print(json.dumps(res), flush=True)
     return 0

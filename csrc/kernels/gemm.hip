@@ -66,7 +66,9 @@ constexpr int kTq = 16;          // LDS tile queue of the dynamic scheduler (4 i
 constexpr int slab_bytes(int tm) { return tm * kSlabK * 2 + kBBytes; }  // A | B
 constexpr int ring_bytes(int tm) { return kRing * slab_bytes(tm); }     // 128 / 96 KB
 
-enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2 };
+// kEpiBiasGeluErf: the erf form of GELU (the fp32-parity bert, whose
+// reference module uses it; the bf16 model keeps the tanh form)
+enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiBiasGeluErf = 3 };
 
 struct K17Params {
   const uint16_t* A;  // [M][lda] bf16
@@ -347,6 +349,11 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
         if (EPI == kEpiBiasGelu) {
           v01 = gelu2(v01);
           v23 = gelu2(v23);
+        } else if (EPI == kEpiBiasGeluErf) {
+          v01 = f32x2{0.5f * v01.x * (1.0f + erff(v01.x * 0.70710678118654752f)),
+                      0.5f * v01.y * (1.0f + erff(v01.y * 0.70710678118654752f))};
+          v23 = f32x2{0.5f * v23.x * (1.0f + erff(v23.x * 0.70710678118654752f)),
+                      0.5f * v23.y * (1.0f + erff(v23.y * 0.70710678118654752f))};
         }
         const float v[4] = {v01.x, v01.y, v23.x, v23.y};
         if constexpr (OUTF32) {
@@ -417,6 +424,7 @@ hipError_t launch(const K17Params& prm, int grid, hipStream_t s, int epi, int ou
   if (out_f32) {
     if (epi == kEpiNone) return launch_tm<TM, kEpiNone, true>(prm, grid, s);
     if (epi == kEpiBias) return launch_tm<TM, kEpiBias, true>(prm, grid, s);
+    if (epi == kEpiBiasGeluErf) return launch_tm<TM, kEpiBiasGeluErf, true>(prm, grid, s);
     return launch_tm<TM, kEpiBiasGelu, true>(prm, grid, s);
   }
   if (epi == kEpiNone) return launch_tm<TM, kEpiNone, false>(prm, grid, s);
@@ -473,12 +481,14 @@ extern "C" {
 
 // K17: C = A . B^T (+ bias) (GELU) with bf16 A [M][lda], B [N][ldb] (K
 // contiguous), fp32 bias [N], C bf16 (out_f32 = 0) or fp32 [M][ldc].
-// epi: 0 none, 1 bias, 2 bias + GELU (N <= 8192).  N a multiple of 256, K of 32, lda /
+// epi: 0 none, 1 bias, 2 bias + GELU (tanh form), 3 bias + GELU (erf form,
+// fp32 C only) (N <= 8188).  N a multiple of 256, K of 32, lda /
 // ldb / ldc multiples of 8, 16-B aligned pointers; any M >= 1.
 int tcamd_k17_gemm(const void* A, const void* B, const float* bias, void* C, int M, int N, int K, int lda, int ldb,
                    int ldc, int epi, int out_f32, void* stream) {
   if (M <= 0) return hipSuccess;
-  if (!A || !B || !C || N <= 0 || N % kTile || K <= 0 || K % kSlabK || epi < 0 || epi > 2) return hipErrorInvalidValue;
+  if (!A || !B || !C || N <= 0 || N % kTile || K <= 0 || K % kSlabK || epi < 0 || epi > 3) return hipErrorInvalidValue;
+  if (epi == 3 && !out_f32) return hipErrorInvalidValue;  // erf GELU: the fp32-parity form only
   if (lda < K || ldb < K || ldc < N || lda % 8 || ldb % 8 || ldc % 8) return hipErrorInvalidValue;
   if (!a16(A) || !a16(B) || !a16(C) || (epi && (!bias || ((uintptr_t)bias & 3) || N > kMaxBiasN)))
     return hipErrorInvalidValue;

@@ -52,7 +52,9 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 constexpr int kBK = 64;         // k per stage
 constexpr int kRow = kBK * 2;   // bytes of one staged operand row
 
-enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2 };
+// kEpiBiasGeluErf: the erf form of GELU (the fp32-parity bert, whose
+// reference module uses it; the bf16 model keeps the tanh form)
+enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiBiasGeluErf = 3 };
 
 struct K18Params {
   const uint16_t* A;  // [M][lda] bf16
@@ -108,6 +110,11 @@ __device__ __forceinline__ f32x2 gelu2(f32x2 x) {
   const f32x2 w = x * __builtin_elementwise_fma(x * x, f32x2{kC3, kC3}, f32x2{kC1, kC1});
   const f32x2 d = f32x2{__builtin_amdgcn_exp2f(w.x), __builtin_amdgcn_exp2f(w.y)} + 1.0f;
   return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  return f32x2{0.5f * x.x * (1.0f + erff(x.x * 0.70710678118654752f)),
+               0.5f * x.y * (1.0f + erff(x.y * 0.70710678118654752f))};
 }
 
 // TM x TN output tile per workgroup of WM x WN waves, an NS-stage ring; EPI;
@@ -213,6 +220,9 @@ __global__ void __launch_bounds__(64 * WM * WN) k18_gemm_kernel(K18Params p) {
       if (EPI == kEpiBiasGelu) {
         v01 = gelu2(v01);
         v23 = gelu2(v23);
+      } else if (EPI == kEpiBiasGeluErf) {
+        v01 = gelu_erf2(v01);
+        v23 = gelu_erf2(v23);
       }
       const float v[4] = {v01.x, v01.y, v23.x, v23.y};
       if constexpr (F32) {
@@ -278,6 +288,7 @@ hipError_t launch_cfg(const K18Params& prm, int grid, hipStream_t s, int epi, bo
   if (f32) {
     if (epi == kEpiNone) return launch_k<TM, TN, WM, WN, NS, kEpiNone, true>(prm, grid, s);
     if (epi == kEpiBias) return launch_k<TM, TN, WM, WN, NS, kEpiBias, true>(prm, grid, s);
+    if (epi == kEpiBiasGeluErf) return launch_k<TM, TN, WM, WN, NS, kEpiBiasGeluErf, true>(prm, grid, s);
     return launch_k<TM, TN, WM, WN, NS, kEpiBiasGelu, true>(prm, grid, s);
   }
   if (epi == kEpiNone) return launch_k<TM, TN, WM, WN, NS, kEpiNone, false>(prm, grid, s);
@@ -294,7 +305,8 @@ extern "C" {
 // K18: C = A . B^T (+ bias) (GELU) with bf16 A [M][lda], B [N][ldb] (K
 // contiguous), fp32 bias [N], C bf16 (out_f32 = 0) or fp32 [M][ldc]; cfg
 // indexes the tile table above.  splits > 1 splits K over
-// workgroups: C is then fp32 (out_f32 = 1, epi = 0) and split z writes its
+// workgroups: C is then fp32 (out_f32 = 1, epi = 0); epi 3 (bias + erf
+// GELU) with fp32 C only and split z writes its
 // partial A[:, Kz] . B[:, Kz]^T at C + z * split_stride (elements, >= M * ldc).
 // N a multiple of the tile width, K of 64 x splits; lda / ldb / ldc multiples
 // of 8 (2 for fp32 C), 16-B aligned A / B / C; any M >= 1.
@@ -303,8 +315,9 @@ int tcamd_k18_gemm(const void* A, const void* B, const float* bias, void* C, int
   if (M <= 0) return hipSuccess;
   if (cfg < 0 || cfg >= kNumCfgs || splits < 1 || splits > 64) return hipErrorInvalidValue;
   const Cfg c = kCfgs[cfg];
-  if (!A || !B || !C || N <= 0 || N % c.tn || K <= 0 || K % (kBK * splits) || epi < 0 || epi > 2)
+  if (!A || !B || !C || N <= 0 || N % c.tn || K <= 0 || K % (kBK * splits) || epi < 0 || epi > 3)
     return hipErrorInvalidValue;
+  if (epi == kEpiBiasGeluErf && !out_f32) return hipErrorInvalidValue;  // the fp32-parity form only
   if (lda < K || ldb < K || ldc < N || lda % 8 || ldb % 8 || ldc % (out_f32 ? 2 : 8)) return hipErrorInvalidValue;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 || (epi && (!bias || (uintptr_t)bias % 4)))
     return hipErrorInvalidValue;

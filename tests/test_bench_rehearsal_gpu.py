@@ -43,4 +43,35 @@ def test_bench_two_ranks_rehearsed_on_one_gpu():
     assert fan["fanout_us"] > 0
     assert set(fan["timings"]) == {"p2p", "host"}
     assert all("us" in v for v in fan["timings"].values()), fan
+    # X2 is a pull: each destination timed its own copy; both ranks share GPU 0
+    assert set(fan["timings"]["p2p"]["per_peer"]) == {"1"}
+    assert fan["timings"]["p2p"]["per_peer"]["1"]["us"] > 0
+    assert fan["timings"]["p2p"]["peer_access"] is None
     assert res["value"] > 0 and res["p99_latency_us"] > 0
+    # every p99-constrained probe says how its rows split into batches
+    for p in res["p99_constrained"]["points"][1:]:
+        assert sum(p["breakdown_rank0"]["batch_rows_histogram"].values()) > 0
+
+
+@pytest.mark.timeout(900)
+def test_bert_sweep_two_ranks_rehearsed_on_one_gpu():
+    """The config-4 sweep through the multi-rank launch: both ranks' bert_large
+    servers on GPU 0, the token-id region fanned out and X1/X2-timed (per-peer
+    pull time), the sweep aggregated over ranks."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--rehearse", "--model", "bert_large",
+           "--sweep", "1,8", "--steps", "2", "--warmup", "1", "--bert-instance-count", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=850, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and "rehearsal" in res and res["config"]["model"] == "bert_large"
+    assert [p["concurrency"] for p in res["sweep"]] == [1, 8]
+    assert all(p["infer_per_sec"] > 0 for p in res["sweep"])
+    fan = res["fanout"]
+    assert set(fan["timings"]) == {"p2p", "host"} and not fan["errors"]
+    assert fan["timings"]["p2p"]["per_peer"]["1"]["us"] > 0

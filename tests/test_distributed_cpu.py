@@ -142,11 +142,12 @@ def test_fanout_rccl_failure_labelled_local_fallback(tmp_path):
 
 
 def _p2p_error_worker(rank, world, port, out_dir, fault_rank, peer_ok):
-    """time_fanout through the REAL _p2p_copy (only rank 0's device copies are
-    stubbed) with an injected fault on one rank: every rank reports the same
-    agreed error, nobody is left in the closing barrier, and the collective
-    sequence stays aligned (the next collective completes on every rank).
-    Without a fault, a failed peer-access enable is reported, not swallowed."""
+    """time_fanout through the REAL _p2p_copy (only each destination's device
+    pull is stubbed) with an injected fault on one rank: every rank reports the
+    same agreed error, nobody is left in the closing barrier, and the
+    collective sequence stays aligned (the next collective completes on every
+    rank).  Without a fault, every destination's pull time and a failed
+    peer-access enable are reported per peer, not swallowed."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     if fault_rank is not None:
         os.environ["TCAMD_FANOUT_FAULT"] = "p2p:%d" % fault_rank
@@ -155,11 +156,11 @@ def _p2p_error_worker(rank, world, port, out_dir, fault_rank, peer_ok):
 
     calls = []
 
-    def fake_copies(region, handles, nbytes):
-        calls.append(len(handles))
-        return {p: peer_ok for p in range(1, len(handles))}
+    def fake_pull(region, src_dev, handle, nbytes):
+        calls.append((src_dev, handle.decode()))
+        return 10.0 + rank, peer_ok
 
-    fanout._star_copies = fake_copies
+    fanout._pull_copy = fake_pull
 
     class Region:
         _device_id = rank
@@ -188,8 +189,9 @@ def test_time_fanout_agrees_on_a_one_rank_failure(tmp_path, fault_rank):
     for r in res:
         assert "p2p" in r["errors"], r
         assert r["after"] == 1.0
-    # rank 0 ran the (stubbed) star copies once per repetition: 1 warm-up + 2
-    assert res[0]["calls"] == [2, 2, 2] and res[1]["calls"] == []
+    # every destination pulled rank 0's region once per repetition (1 warm-up
+    # + 2); rank 0 copies nothing
+    assert res[0]["calls"] == [] and res[1]["calls"] == [[0, "h0"]] * 3
     assert "injected p2p fault on rank %d" % fault_rank in res[fault_rank]["errors"]["p2p"]
     assert res[1 - fault_rank]["errors"]["p2p"] == "failed on another rank"
 
@@ -198,11 +200,14 @@ def test_time_fanout_agrees_on_a_one_rank_failure(tmp_path, fault_rank):
 def test_time_fanout_reports_peer_access(tmp_path, peer_ok):
     """verdict r4 weak #7: a failed hipDeviceEnablePeerAccess is an explicit
     peer_access: false on every rank's X2 timing, never a swallowed exception."""
-    res = _p2p_results(tmp_path, 2, None, peer_ok)
+    res = _p2p_results(tmp_path, 3, None, peer_ok)
     for r in res:
         assert not r["errors"], r
-        assert r["timings"]["p2p"]["peer_access"] is peer_ok
-        assert ("note" in r["timings"]["p2p"]) is (not peer_ok)
+        t = r["timings"]["p2p"]
+        assert t["peer_access"] is peer_ok
+        assert ("note" in t) is (not peer_ok)
+        # each destination's own pull time and link state, per peer
+        assert t["per_peer"] == {"1": {"us": 11.0, "peer_access": peer_ok}, "2": {"us": 12.0, "peer_access": peer_ok}}
 
 
 @pytest.mark.parametrize("nbytes", [1, 2, 4096, 4097, 4816896, 231211008, 2 ** 31 + 12345])

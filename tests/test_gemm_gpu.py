@@ -315,3 +315,27 @@ def test_add_layernorm_parts(f32, nparts, with_bias):
     ref = torch.nn.functional.layer_norm(v, (H,), gamma.double(), beta.double(), eps=1e-12)
     err = ((out.double() - ref).norm() / ref.norm()).item()
     assert err < (1e-6 if f32 else 4e-3), err
+
+
+@pytest.mark.parametrize("kern", ["k17", "k18_c3", "k18_c6"])
+def test_gelu_erf_epilogue_fp32(kern):
+    """bias + erf-form GELU with fp32 output (the fp32-parity bert's FFN-up on
+    its bf16x3 operands) against fp64 of the same bf16 operands; the bf16
+    output form is refused."""
+    hip = _hip()
+    M, N, K = 300, 512, 3072
+    a, b, bias = _case(M, N, K, seed=9)
+    c = torch.full((M, N), 7.0, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    if kern == "k17":
+        hip.k17_gemm(a.data_ptr(), b.data_ptr(), bias.data_ptr(), c.data_ptr(), M, N, K, K, K, N,
+                     epilogue="bias_gelu_erf", out_f32=True, stream=st)
+    else:
+        hip.k18_gemm(a.data_ptr(), b.data_ptr(), bias.data_ptr(), c.data_ptr(), M, N, K, K, K, N,
+                     epilogue="bias_gelu_erf", out_f32=True, cfg=int(kern[-1]), stream=st)
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.gelu(a.double() @ b.double().t() + bias.double())
+    assert ((c.double() - ref).norm() / ref.norm()).item() < 1e-5
+    with pytest.raises(Exception):
+        hip.k18_gemm(a.data_ptr(), b.data_ptr(), bias.data_ptr(), c.data_ptr(), M, N, K, K, K, N,
+                     epilogue="bias_gelu_erf", out_f32=False, cfg=3, stream=st)

@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--cfgs", default="0,1,2,3,4,5,6,7,8,9")
     ap.add_argument("--splits", default="1,2,4,8")
     ap.add_argument("--no-k17", action="store_true")
+    ap.add_argument("--x3", action="store_true",
+                    help="the fp32-parity projections: bf16x3 operands (K tripled), fp32 output, erf GELU, fp32 "
+                         "LayerNorm (K11p) behind the N = 1024 ones; the library arm is torch.mm + bias (+ GELU)")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     import torch
@@ -45,20 +48,24 @@ def main():
     cfgs = [int(c) for c in a.cfgs.split(",") if c != ""]
     splits_all = [int(s) for s in a.splits.split(",")]
     for M in [int(v) for v in a.tokens.split(",")]:
-        for name, N, K, epi in SHAPES:
+        for name, N, K0, epi in SHAPES:
             if a.proj and name not in a.proj.split(","):
                 continue
-            L = a.layers or max(4, -(-320 * 2 ** 20 // (N * K * 2)))
+            K = 3 * K0 if a.x3 else K0
+            if a.x3 and epi == "bias_gelu":
+                epi = "bias_gelu_erf"
+            odt = torch.float32 if a.x3 else torch.bfloat16
+            L = a.layers or max(4, min(64, -(-320 * 2 ** 20 // (N * K * 2))))
             x = torch.empty(M, K, device=dev, dtype=torch.bfloat16).uniform_(-1, 1)
             ws = [(torch.empty(N, K, device=dev).uniform_(-1, 1) / K ** 0.5).to(torch.bfloat16) for _ in range(L)]
             bias = torch.randn(N, device=dev) * 0.1
             bias16 = bias.to(torch.bfloat16)
-            c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            c = torch.empty(M, N, device=dev, dtype=odt)
             ln = N == 1024  # followed by residual add + LayerNorm in the model
-            resid = torch.randn(M, N, device=dev).to(torch.bfloat16) if ln else None
-            gamma = torch.ones(N, device=dev, dtype=torch.bfloat16)
-            beta = torch.zeros(N, device=dev, dtype=torch.bfloat16)
-            lnout = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            resid = torch.randn(M, N, device=dev).to(odt) if ln else None
+            gamma = torch.ones(N, device=dev, dtype=odt)
+            beta = torch.zeros(N, device=dev, dtype=odt)
+            lnout = torch.empty(M, N, device=dev, dtype=odt)
             maxs = max(splits_all)
             part = torch.empty(maxs, M, N, device=dev) if ln else None
 
@@ -66,10 +73,23 @@ def main():
                 return torch.cuda.current_stream().cuda_stream
 
             def k11(y):
+                if a.x3:
+                    hip.add_layernorm_parts(resid.data_ptr(), y.data_ptr(), 1, M * N, None, gamma.data_ptr(),
+                                            beta.data_ptr(), lnout.data_ptr(), M, N, 1e-12, f32=True, stream=st())
+                    return
                 hip.add_layernorm(resid.data_ptr(), y.data_ptr(), gamma.data_ptr(), beta.data_ptr(), lnout.data_ptr(),
                                   M, N, 1e-12, stream=st())
 
             def lib_arm(w):
+                if a.x3:
+                    y = torch.mm(x, w.t(), out_dtype=torch.float32)
+                    if epi != "none":
+                        y += bias
+                    if epi == "bias_gelu_erf":
+                        y = torch.nn.functional.gelu(y)
+                    if ln:
+                        k11(y)
+                    return
                 if epi == "none":
                     torch.mm(x, w.t(), out=c)
                 elif epi == "bias":
@@ -79,9 +99,13 @@ def main():
                 if ln:
                     k11(c)
 
+            def k17_static_arm(w):
+                with hip.knob(TCAMD_K17_DYN=0):
+                    k17_arm(w)
+
             def k17_arm(w):
                 hip.k17_gemm(x.data_ptr(), w.data_ptr(), bias.data_ptr(), c.data_ptr(), M, N, K, K, K, N,
-                             epilogue=epi, stream=st())
+                             epilogue=epi, out_f32=a.x3, stream=st())
                 if ln:
                     k11(c)
 
@@ -89,7 +113,7 @@ def main():
                 def run(w):
                     if s == 1:
                         hip.k18_gemm(x.data_ptr(), w.data_ptr(), bias.data_ptr(), c.data_ptr(), M, N, K, K, K, N,
-                                     epilogue=epi, cfg=cfg, stream=st())
+                                     epilogue=epi, out_f32=a.x3, cfg=cfg, stream=st())
                         if ln:
                             k11(c)
                     else:
@@ -97,12 +121,13 @@ def main():
                                      out_f32=True, cfg=cfg, splits=s, split_stride=M * N, stream=st())
                         hip.add_layernorm_parts(resid.data_ptr(), part.data_ptr(), s, M * N, bias.data_ptr(),
                                                 gamma.data_ptr(), beta.data_ptr(), lnout.data_ptr(), M, N, 1e-12,
-                                                stream=st())
+                                                f32=a.x3, stream=st())
                 return run
 
             arms = {"hipblaslt": lib_arm}
             if not a.no_k17 and N % 256 == 0:
                 arms["k17"] = k17_arm
+                arms["k17_static"] = k17_static_arm
             for cfg in cfgs:
                 tm, tn, _, _ = hip.k18_cfg(cfg)
                 if N % tn:
@@ -134,7 +159,7 @@ def main():
                     ev1.record()
                     ev1.synchronize()
                     ts[k].append(ev0.elapsed_time(ev1) * 1e3 / L)
-            row = {"tokens": M, "proj": name, "N": N, "K": K, "epilogue": epi, "with_ln": ln}
+            row = {"tokens": M, "proj": name, "N": N, "K": K, "epilogue": epi, "with_ln": ln, "x3": a.x3}
             for k, v in ts.items():
                 row[k + "_us"] = round(sorted(v)[len(v) // 2], 2)
             best = min((k for k in arms if k != "hipblaslt"), key=lambda k: row[k + "_us"])

@@ -158,12 +158,8 @@ def _proj(x, lin, epilogue="bias", name=None, allow_split=False):
             y = _k18(x2, lin, epilogue, route[1], splits)
             return _Parts(y) if splits > 1 else y.view(*x.shape[:-1], n)
     if getattr(lin, "w3", None) is not None and x2.is_cuda and x2.dtype == torch.float32:
-        y = _mm_x3(x2, lin.w3)
-        if epilogue != "none":
-            y += lin.bias
-        if epilogue == "bias_gelu":
-            y = F.gelu(y)
-        return y.view(*x.shape[:-1], n)
+        y = _mm_x3(x2, lin, epilogue, name, allow_split)
+        return y if isinstance(y, _Parts) else y.view(*x.shape[:-1], n)
     if epilogue == "none":
         return torch.mm(x2, lin.weight.t()).view(*x.shape[:-1], n)
     if epilogue == "bias_gelu":
@@ -171,17 +167,68 @@ def _proj(x, lin, epilogue="bias", name=None, allow_split=False):
     return lin(x)
 
 
-def _mm_x3(x2, w3):
-    """fp32-parity GEMM: x2 fp32 [M, K] against w3 = [W_hi | W_lo | W_hi] bf16
-    [N, 3K] as ONE bf16 GEMM with fp32 output over [x_hi | x_hi | x_lo]
-    (csrc/kernels/bert.hip x3_cat): x_hi W_hi + x_hi W_lo + x_lo W_hi, ~1e-5
-    of an fp32 GEMM."""
+# fp32-parity projections (bf16x3, K tripled): the measured routing of the
+# x3 GEMMs (tools/gemm_sweep.py --x3, profiles/r6_gemm/), same format as
+# GEMM_ROUTES; past the table: X3_LARGE (K17, fp32 out) -- "lib" runs torch.mm.
+GEMM_ROUTES_X3 = {
+    "qkv": [(768, ("k18", 6, 1)), (3072, ("k18", 3, 1))],
+    "out": [(768, ("k18", 6, 2)), (3072, ("k18", 3, 1))],
+    "ffn_up": [(768, ("k18", 6, 1)), (3072, ("k18", 3, 1))],
+    "ffn_down": [(768, ("k18", 6, 4)), (3072, ("k18", 3, 2))],
+}
+X3_LARGE = {"qkv": ("k17",), "out": ("k17",), "ffn_up": ("k17",), "ffn_down": ("k17",)}
+
+
+def gemm_route_x3(name, M, mode=None):
+    """The kernel of the fp32-parity (bf16x3) projection ``name`` at ``M`` tokens."""
+    mode = mode or GEMM
+    if mode == "lib" or name is None:
+        return ("lib",)
+    for top, route in GEMM_ROUTES_X3[name]:
+        if M <= top:
+            return route
+    return X3_LARGE[name]
+
+
+def _mm_x3(x2, lin, epilogue="none", name=None, allow_split=False):
+    """fp32-parity projection: x2 fp32 [M, K] against w3 = [W_hi | W_lo | W_hi]
+    bf16 [N, 3K] as ONE bf16 GEMM over [x_hi | x_hi | x_lo] (csrc/kernels/bert.hip
+    x3_cat): x_hi W_hi + x_hi W_lo + x_lo W_hi, fp32 accumulate and output,
+    ~1e-5 of an fp32 GEMM.  The GEMM is K18 / K17 (gemm_route_x3) with the
+    bias and the erf GELU in its epilogue, or a split-K route's fp32 slabs
+    (_Parts) for K11p; torch.mm with TC_BERT_GEMM=lib."""
     from triton_client_amd.ops import hip
 
     M, K = x2.shape
+    w3 = lin.w3
+    N = w3.shape[0]
+    st = torch.cuda.current_stream(x2.device).cuda_stream
     xc = torch.empty(M, 3 * K, device=x2.device, dtype=torch.bfloat16)
-    hip.x3_cat(x2.contiguous().data_ptr(), xc.data_ptr(), M, K, stream=torch.cuda.current_stream(x2.device).cuda_stream)
-    return torch.mm(xc, w3.t(), out_dtype=torch.float32)
+    hip.x3_cat(x2.contiguous().data_ptr(), xc.data_ptr(), M, K, stream=st)
+    route = gemm_route_x3(name, M)
+    if route[0] != "lib" and FUSED and _route_ok(route, M, N, 3 * K):
+        epi = "bias_gelu_erf" if epilogue == "bias_gelu" else epilogue
+        bias = None if epi == "none" else lin.bias.detach()
+        if route[0] == "k18" and route[2] > 1 and allow_split and epilogue == "bias":
+            out = torch.empty(route[2], M, N, device=x2.device, dtype=torch.float32)
+            hip.k18_gemm(xc.data_ptr(), w3.data_ptr(), None, out.data_ptr(), M, N, 3 * K, 3 * K, 3 * K, N,
+                         out_f32=True, cfg=route[1], splits=route[2], split_stride=M * N, stream=st)
+            return _Parts(out)
+        out = torch.empty(M, N, device=x2.device, dtype=torch.float32)
+        bp = None if bias is None else bias.data_ptr()
+        if route[0] == "k17":
+            hip.k17_gemm(xc.data_ptr(), w3.data_ptr(), bp, out.data_ptr(), M, N, 3 * K, 3 * K, 3 * K, N,
+                         epilogue=epi, out_f32=True, stream=st)
+        else:
+            hip.k18_gemm(xc.data_ptr(), w3.data_ptr(), bp, out.data_ptr(), M, N, 3 * K, 3 * K, 3 * K, N,
+                         epilogue=epi, out_f32=True, cfg=route[1], stream=st)
+        return out
+    y = torch.mm(xc, w3.t(), out_dtype=torch.float32)
+    if epilogue != "none":
+        y += lin.bias
+    if epilogue == "bias_gelu":
+        y = F.gelu(y)
+    return y
 
 
 def prepare_x3(model):
@@ -214,15 +261,28 @@ def _proj_add_ln(x, a, lin, ln, name):
         out = torch.empty_like(x)
         rows, H = p.shape[1], p.shape[2]
         assert x.is_contiguous() and x.numel() == rows * H
-        hip.add_layernorm_parts(x.data_ptr(), p.data_ptr(), p.shape[0], rows * H, _bias_f32(lin, x.device).data_ptr(),
-                                ln.weight.data_ptr(), ln.bias.data_ptr(), out.data_ptr(), rows, H, ln.eps,
+        f32 = x.dtype == torch.float32
+        bias = lin.bias.detach() if f32 else _bias_f32(lin, x.device)
+        hip.add_layernorm_parts(x.data_ptr(), p.data_ptr(), p.shape[0], rows * H, bias.data_ptr(),
+                                ln.weight.data_ptr(), ln.bias.data_ptr(), out.data_ptr(), rows, H, ln.eps, f32=f32,
                                 stream=torch.cuda.current_stream(x.device).cuda_stream)
         return out
     return _add_ln(x, y, ln)
 
 
 def _add_ln(x, y, ln):
-    """LayerNorm(x + y): K11 on the GPU, torch ops elsewhere."""
+    """LayerNorm(x + y): K11 on the GPU (K11p's fp32 form for the fp32-parity
+    model: y as its one partial slab), torch ops elsewhere."""
+    if (FUSED and x.is_cuda and x.dtype == torch.float32 and y.dtype == torch.float32 and x.is_contiguous()
+            and y.is_contiguous() and x.shape[-1] in (512, 1024, 2048, 4096)):
+        from triton_client_amd.ops import hip
+
+        out = torch.empty_like(x)
+        rows, H = x.numel() // x.shape[-1], x.shape[-1]
+        hip.add_layernorm_parts(x.data_ptr(), y.data_ptr(), 1, rows * H, None, ln.weight.data_ptr(),
+                                ln.bias.data_ptr(), out.data_ptr(), rows, H, ln.eps, f32=True,
+                                stream=torch.cuda.current_stream(x.device).cuda_stream)
+        return out
     if FUSED and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and y.is_contiguous():
         from triton_client_amd.ops import hip
 
@@ -288,7 +348,7 @@ class _Layer(nn.Module):
             qkv = _proj(x, self.qkv, "none", name="qkv")
             a = _attention(qkv, b, s, mask_i32, bias, qkv_bias=self.qkv.bias)
         else:
-            a = _attention(_proj(x, self.qkv), b, s, mask_i32, bias)
+            a = _attention(_proj(x, self.qkv, name="qkv"), b, s, mask_i32, bias)
         x = _proj_add_ln(x, a, self.out, self.ln1, "out")
         return _proj_add_ln(x, _proj(x, self.ffn1, "bias_gelu", name="ffn_up"), self.ffn2, self.ln2, "ffn_down")
 

@@ -6,10 +6,13 @@ batch is replicated into every rank's HIP shared-memory input region:
 
 * ``rccl``  — X1: ``dist.broadcast`` straight into the region (the region is
   exposed to torch through a zero-copy kDLROCM DLPack view).
-* ``p2p``   — X2: a one-hop star over xGMI: ranks all-gather their regions'
-  IPC handles, rank 0 opens them and issues one hipMemcpyAsync per peer on
-  its own stream (each copy uses the direct rank0->peer link; no ring hops).
-  Ranks then barrier.
+* ``p2p``   — X2: a one-hop star over xGMI in which every destination
+  PULLS: rank 0 broadcasts its region's IPC handle, each other rank opens it
+  and copies rank 0's bytes into its own region with one hipMemcpyAsync on
+  its own stream -- its own GPU's copy engines over its own direct link to
+  rank 0 (no ring hops, and rank 0's engines are not the serial point of
+  seven copies).  Ranks then barrier.  The native load generator's star
+  (csrc/cpp/perf/multigpu.cc) pulls the same way.
 * ``local`` — every rank generates the identical data itself (K1 is a pure
   function of (seed, offset)), used when no process group exists.
 
@@ -242,13 +245,20 @@ def time_fanout(region, nbytes, methods, reps=5):
         med = max_over_ranks(med)
         out[m] = {"us": round(med * 1e6, 1), "GBps_per_peer": round(nbytes / med / 1e9, 2), "bytes": int(nbytes)}
         if m == "p2p":
-            # rank 0 knows whether every peer had direct access; MIN over ranks
-            # hands its answer to all of them
-            ok = all_ok(all(_PEER_ACCESS.values()) if dist.get_rank() == 0 else True)
-            out[m]["peer_access"] = ok
+            # every destination timed its own pull (last rep): per-peer copy
+            # time and whether its link to rank 0 had peer access
+            peers = [None] * dist.get_world_size()
+            dist.all_gather_object(peers, dict(_LAST_PULL), group=cpu_group())
+            out[m]["per_peer"] = {str(r): {"us": round(p["us"], 1), "peer_access": p["peer_access"]}
+                                  for r, p in enumerate(peers) if r != 0 and p}
+            acc = [p["peer_access"] for r, p in enumerate(peers) if r != 0 and p]
+            ok = all(a is not False for a in acc)
+            out[m]["peer_access"] = ok if any(a is not None for a in acc) else None
             if not ok:
-                out[m]["note"] = ("hipDeviceEnablePeerAccess failed for a peer: the copies ran over the "
+                out[m]["note"] = ("hipDeviceEnablePeerAccess failed for a peer: its pull ran over the "
                                   "runtime's staging path, not the xGMI star")
+            elif out[m]["peer_access"] is None:
+                out[m]["note"] = "every rank shares rank 0's GPU (rehearsal): no xGMI link was used"
     return out
 
 
@@ -258,68 +268,69 @@ def fanout_errors(timings):
     return {m: v["error"] for m, v in (timings or {}).items() if "error" in v}
 
 
-# rank 0's last X2 star: {peer rank: hipDeviceEnablePeerAccess succeeded}
-_PEER_ACCESS = {}
+# this rank's last X2 pull: {"us": copy time, "peer_access": bool or None
+# (None: same device as rank 0, no link to enable)}
+_LAST_PULL = {}
 
 
-def _star_copies(region, handles, nbytes):
-    """Rank 0's half of the X2 star: open every peer's region and copy into it
-    on one stream per peer.  Returns {peer rank: peer access enabled}; a peer
-    whose ``hipDeviceEnablePeerAccess`` failed is still copied to (the runtime
-    stages such copies), but the timing is then not the xGMI star and
-    :func:`time_fanout` labels it ``peer_access: false``.  Raises on a copy
-    failure."""
+def _pull_copy(region, src_dev, handle, nbytes):
+    """A destination rank's half of the X2 star: open rank 0's region (IPC
+    handle) on this rank's device and copy it into this rank's region on a
+    stream of its own -- this GPU's copy engines, over its direct link to rank
+    0.  ``hipDeviceEnablePeerAccess`` failing is recorded (the runtime then
+    stages the copy, and the timing is not the xGMI star) and reported as
+    ``peer_access: false``.  Returns (microseconds, peer_access)."""
+    import time
+
     from tritonclient.utils import hip_shared_memory as hipshm  # noqa: F401
     from triton_client_amd.ops import hip
 
-    src_dev = region._device_id
-    streams, opened, access = [], [], {}
+    dev = region._device_id
+    access = None
+    if dev != src_dev:
+        try:
+            hip.enable_peer(dev, src_dev)
+            access = True
+        except Exception as e:  # noqa: BLE001 - recorded and reported, never swallowed
+            access = False
+            print("[fanout] hipDeviceEnablePeerAccess(%d -> %d) failed: %s" % (dev, src_dev, str(e)[:200]),
+                  file=sys.stderr)
+    ptr = hip.ipc_open(handle, dev)
+    s = None
     try:
-        for peer in range(1, len(handles)):
-            dev, h = handles[peer]
-            try:
-                hip.enable_peer(src_dev, dev)
-                access[peer] = True
-            except Exception as e:  # noqa: BLE001 - recorded and reported, never swallowed
-                access[peer] = False
-                print("[fanout] hipDeviceEnablePeerAccess(%d -> %d) failed: %s" % (src_dev, dev, str(e)[:200]),
-                      file=sys.stderr)
-            ptr = hip.ipc_open(h, src_dev)
-            opened.append(ptr)
-            s = hip.Stream(src_dev)
-            streams.append(s)
-            hip.memcpy_async(ptr, region._base_addr, nbytes, s.handle)
-        for s in streams:
-            s.synchronize()
+        s = hip.Stream(dev)
+        t0 = time.perf_counter()
+        hip.memcpy_async(region._base_addr, ptr, nbytes, s.handle)
+        s.synchronize()
+        us = (time.perf_counter() - t0) * 1e6
     finally:
-        for s in streams:
+        if s is not None:
             s.close()
-        for p in opened:
-            hip.ipc_close(p, src_dev)
-    return access
+        hip.ipc_close(ptr, dev)
+    return us, access
 
 
 def _p2p_copy(region, nbytes, dist):
-    """The X2 star.  Returns this rank's exception (rank 0's copy failure, or
+    """The X2 star (pull).  Returns this rank's exception (its copy failure, or
     an injected fault) or None; every rank reaches the closing barrier either
     way, so the collective sequence stays aligned and the caller can agree on
     the outcome."""
     rank = dist.get_rank()
-    handles = [None] * dist.get_world_size()
-    dist.all_gather_object(handles, (region._device_id, region._hip_shm_handle))
+    src = [(region._device_id, region._hip_shm_handle) if rank == 0 else None]
+    dist.broadcast_object_list(src, src=0, group=cpu_group())
     err = None
-    if rank == 0:
+    _LAST_PULL.clear()
+    if rank != 0:
         try:
-            access = _star_copies(region, handles, nbytes)
-            _PEER_ACCESS.clear()
-            _PEER_ACCESS.update(access)
+            us, access = _pull_copy(region, src[0][0], src[0][1], nbytes)
+            _LAST_PULL.update({"us": us, "peer_access": access})
         except Exception as e:  # noqa: BLE001 - agreed on by the caller
             err = e
     try:
         _fault("p2p")  # test hook: recorded like a real copy error, before the barrier
     except RuntimeError as e:
         err = err or e
-    dist.barrier()
+    dist.barrier(group=cpu_group())
     return err
 
 
