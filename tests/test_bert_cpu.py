@@ -66,22 +66,23 @@ def test_bert_flops():
 
 
 def test_gemm_route_table():
-    """bert's projection routing (TC_BERT_GEMM): the measured table first,
-    hipBLASLt past it in auto mode, the hand-written kernels everywhere in
-    ours mode; the CPU forward never routes (it stays on torch ops)."""
+    """bert's projection routing (TC_BERT_GEMM): the measured tables (bf16 and
+    the fp32-parity bf16x3 ones) in auto mode, no library anywhere in ours
+    mode, the library everywhere in lib mode; the last entry covers every
+    larger token count."""
     from triton_client_amd.models import bert
 
-    for name, table in bert.GEMM_ROUTES.items():
-        tops = [t for t, _ in table]
-        assert tops == sorted(tops), name
-        for top, route in table:
-            for mode in ("auto", "ours"):
-                assert bert.gemm_route(name, top, mode) == route
-                assert bert.gemm_route(name, 1, mode) == table[0][1]
-            assert bert.gemm_route(name, top, "lib") == ("lib",)
-        assert bert.gemm_route(name, tops[-1] + 384, "auto") == ("lib",)
-        assert bert.gemm_route(name, 24576, "ours") == bert.OURS_LARGE[name]
-        assert bert.gemm_route(name, 24576, "ours")[0] in ("k17", "k18")
-    # split-K only where K11p can sum the slabs: the N = 1024 projections
-    for name in ("qkv", "ffn_up"):
-        assert all(r[0] != "k18" or r[2] == 1 for _, r in bert.GEMM_ROUTES[name])
+    for table, route in ((bert.GEMM_ROUTES, bert.gemm_route), (bert.GEMM_ROUTES_X3, bert.gemm_route_x3)):
+        for name, entries in table.items():
+            tops = [t for t, _ in entries]
+            assert tops == sorted(tops) and tops[-1] == bert.INF, name
+            for top, r in entries:
+                for M in (top, top - 1 if top > 1 else top):
+                    assert route(name, M, "auto") == r
+                    ours = route(name, M, "ours")
+                    assert ours[0] in ("k17", "k18") and (r[0] == "lib" or ours == r)
+                    assert route(name, M, "lib") == ("lib",)
+            assert route(name, 10 ** 6, "auto") == entries[-1][1]
+        # split-K only where K11p can sum the slabs: the N = 1024 projections
+        for name in ("qkv", "ffn_up"):
+            assert all(r[0] != "k18" or r[2] == 1 for _, r in table[name])

@@ -31,9 +31,10 @@ def main():
                          "the tuned results go to this CSV path")
     ap.add_argument("--gemm", default="", help="A/B the projection routing modes (bert.GEMM), e.g. lib,auto,ours")
     ap.add_argument("--graphs", action="store_true", help="time HIP-graph replays of the forward (as served)")
+    ap.add_argument("--fp32", action="store_true", help="the fp32-parity model (bert_large_fp32: bf16x3 projections)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    model = bert.build(device=dev)
+    model = (bert.prepare_x3(bert.build(device=dev, dtype=torch.float32)) if a.fp32 else bert.build(device=dev))
     for b in a.batch:
         ids = torch.randint(0, bert.VOCAB, (b, a.seq), device=dev)
         mask = torch.ones(b, a.seq, device=dev, dtype=torch.int64)
@@ -99,7 +100,7 @@ def main():
         for name, v in ts.items():
             dt = sorted(v)[len(v) // 2]
             tf = bert.flops_per_sequence(a.seq) * b / dt / 1e12
-            print({"batch": b, "variant": name, "ms": round(dt * 1e3, 3), "seq_per_s": round(b / dt, 1),
+            print({"batch": b, "variant": name, "fp32": a.fp32, "ms": round(dt * 1e3, 3), "seq_per_s": round(b / dt, 1),
                    "tflops": round(tf, 1)}, flush=True)
 
 

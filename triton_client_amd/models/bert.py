@@ -46,35 +46,57 @@ FUSED = os.environ.get("TC_BERT_FUSED", "1") != "0"
 # above), "lib" = hipBLASLt everywhere.
 GEMM = os.environ.get("TC_BERT_GEMM", "auto")
 
-# Measured routing (tools/gemm_sweep.py on MI355X, profiles/r6_bert_gemms.md:
-# each arm in a HIP graph over weight copies past the Infinity Cache, the
-# N = 1024 projections timed together with the residual add + LayerNorm that
-# follows them).  Per projection: (largest token count, route), first match
-# wins; route = ("k18", cfg, splits) -- splits > 1 leaves fp32 partial slabs
-# that K11p sums into the LayerNorm -- or ("k17",).  Past the last entry:
-# hipBLASLt (auto) or OURS_LARGE (ours).
+# Measured routing (tools/gemm_sweep.py on MI355X, profiles/r6_gemm/: each
+# arm in a HIP graph over weight copies past the Infinity Cache, the N = 1024
+# projections timed together with the residual add + LayerNorm that follows
+# them).  Per projection: (largest token count, route), first match wins, the
+# last entry covers every larger count; route = ("k18", cfg, splits) --
+# splits > 1 leaves fp32 partial slabs that K11p sums into the LayerNorm --
+# ("k17",) / ("k17", 0) (K17, claimed / static tile lists) or ("lib",)
+# (hipBLASLt: where it measured faster).
+INF = 1 << 30
 GEMM_ROUTES = {
-    "qkv": [(384, ("k18", 6, 1)), (768, ("k18", 3, 1))],
-    "out": [(384, ("k18", 9, 1)), (768, ("k18", 6, 1)), (1536, ("k18", 0, 1)), (3072, ("k18", 3, 1))],
-    "ffn_up": [(384, ("k18", 1, 1)), (768, ("k18", 3, 1))],
-    "ffn_down": [(384, ("k18", 6, 2)), (768, ("k18", 7, 2)), (1536, ("k18", 2, 2))],
+    "qkv": [(384, ("k18", 6, 1)), (768, ("k18", 3, 1)), (3072, ("lib",)), (6144, ("k17", 0)), (INF, ("lib",))],
+    "out": [(384, ("k18", 9, 1)), (768, ("k18", 6, 1)), (1536, ("k18", 0, 1)), (3072, ("k18", 3, 1)),
+            (INF, ("lib",))],
+    "ffn_up": [(384, ("k18", 1, 1)), (768, ("k18", 3, 1)), (INF, ("lib",))],
+    "ffn_down": [(384, ("k18", 6, 2)), (768, ("k18", 7, 2)), (1536, ("k18", 2, 2)), (INF, ("lib",))],
 }
-OURS_LARGE = {"qkv": ("k17",), "out": ("k18", 3, 1), "ffn_up": ("k17",), "ffn_down": ("k18", 3, 1)}
-OURS_LARGE_FROM = 3072  # tokens from which "ours" uses OURS_LARGE instead of the last table entry
+# the fp32-parity model's bf16x3 projections (K tripled, fp32 out, erf GELU;
+# tools/gemm_sweep.py --x3, whose library arm adds the bias and the GELU as
+# separate ops, as torch.mm must)
+GEMM_ROUTES_X3 = {
+    "qkv": [(384, ("k18", 6, 1)), (INF, ("lib",))],
+    "out": [(384, ("k18", 6, 2)), (768, ("k18", 2, 2)), (1536, ("k18", 3, 2)), (3072, ("k18", 3, 1)),
+            (INF, ("k17", 0))],
+    "ffn_up": [(384, ("k18", 1, 1)), (768, ("k18", 3, 1)), (1536, ("lib",)), (INF, ("k17", 0))],
+    "ffn_down": [(384, ("k18", 7, 4)), (768, ("k18", 3, 4)), (1536, ("k18", 3, 2)), (INF, ("lib",))],
+}
+OURS_FROM_K17 = 3072  # "ours" mode where the table says lib: K17 from this many tokens, K18 cfg 3 below
+
+
+def _route(table, name, M, mode):
+    if mode == "lib" or name is None:
+        return ("lib",)
+    for top, route in table[name]:
+        if M <= top:
+            break
+    if route[0] == "lib" and mode == "ours":
+        return ("k17",) if M >= OURS_FROM_K17 else ("k18", 3, 1)
+    return route
 
 
 def gemm_route(name, M, mode=None):
-    """The kernel that runs projection ``name`` at ``M`` tokens: ("lib",),
-    ("k17",) or ("k18", cfg, splits)."""
-    mode = mode or GEMM
-    if mode == "lib":
-        return ("lib",)
-    for top, route in GEMM_ROUTES[name]:
-        if M <= top:
-            return route
-    if mode == "ours":
-        return OURS_LARGE[name] if M >= OURS_LARGE_FROM else GEMM_ROUTES[name][-1][1]
-    return ("lib",)
+    """The kernel that runs bf16 projection ``name`` at ``M`` tokens: ("lib",),
+    ("k17"[, dyn]) or ("k18", cfg, splits).  mode (default TC_BERT_GEMM): auto
+    = the table, ours = the table with every library entry replaced by K17 /
+    K18, lib = hipBLASLt everywhere."""
+    return _route(GEMM_ROUTES, name, M, mode or GEMM)
+
+
+def gemm_route_x3(name, M, mode=None):
+    """The kernel of the fp32-parity (bf16x3) projection ``name`` at ``M`` tokens."""
+    return _route(GEMM_ROUTES_X3, name, M, mode or GEMM)
 
 
 def _bias_f32(lin, dev):
@@ -89,16 +111,26 @@ def _ours_ok(x2, lin):
             and x2.stride(1) == 1 and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0 and lin.weight.is_contiguous())
 
 
-def _k17(x2, lin, epilogue):
+def _k17_launch(route, *args, **kw):
+    """K17 with the route's scheduling: ("k17",) the TCAMD_K17_DYN default,
+    ("k17", 0) static tile lists (read at launch, so a captured graph keeps it)."""
     from triton_client_amd.ops import hip
 
+    if len(route) > 1:
+        with hip.knob(TCAMD_K17_DYN=int(route[1])):
+            hip.k17_gemm(*args, **kw)
+    else:
+        hip.k17_gemm(*args, **kw)
+
+
+def _k17(x2, lin, epilogue, route=("k17",)):
     M, K = x2.shape
     N = lin.weight.shape[0]
     out = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
     bias = None if epilogue == "none" else _bias_f32(lin, x2.device)
-    hip.k17_gemm(x2.data_ptr(), lin.weight.data_ptr(), None if bias is None else bias.data_ptr(), out.data_ptr(), M, N,
-                 K, x2.stride(0), lin.weight.stride(0), N, epilogue=epilogue,
-                 stream=torch.cuda.current_stream(x2.device).cuda_stream)
+    _k17_launch(route, x2.data_ptr(), lin.weight.data_ptr(), None if bias is None else bias.data_ptr(),
+                out.data_ptr(), M, N, K, x2.stride(0), lin.weight.stride(0), N, epilogue=epilogue,
+                stream=torch.cuda.current_stream(x2.device).cuda_stream)
     return out
 
 
@@ -153,7 +185,7 @@ def _proj(x, lin, epilogue="bias", name=None, allow_split=False):
         route = gemm_route(name, x2.shape[0])
         if _route_ok(route, x2.shape[0], n, x2.shape[1]):
             if route[0] == "k17":
-                return _k17(x2, lin, epilogue).view(*x.shape[:-1], n)
+                return _k17(x2, lin, epilogue, route).view(*x.shape[:-1], n)
             splits = route[2] if allow_split and epilogue == "bias" else 1
             y = _k18(x2, lin, epilogue, route[1], splits)
             return _Parts(y) if splits > 1 else y.view(*x.shape[:-1], n)
@@ -165,29 +197,6 @@ def _proj(x, lin, epilogue="bias", name=None, allow_split=False):
     if epilogue == "bias_gelu":
         return _linear_gelu(x, lin)
     return lin(x)
-
-
-# fp32-parity projections (bf16x3, K tripled): the measured routing of the
-# x3 GEMMs (tools/gemm_sweep.py --x3, profiles/r6_gemm/), same format as
-# GEMM_ROUTES; past the table: X3_LARGE (K17, fp32 out) -- "lib" runs torch.mm.
-GEMM_ROUTES_X3 = {
-    "qkv": [(768, ("k18", 6, 1)), (3072, ("k18", 3, 1))],
-    "out": [(768, ("k18", 6, 2)), (3072, ("k18", 3, 1))],
-    "ffn_up": [(768, ("k18", 6, 1)), (3072, ("k18", 3, 1))],
-    "ffn_down": [(768, ("k18", 6, 4)), (3072, ("k18", 3, 2))],
-}
-X3_LARGE = {"qkv": ("k17",), "out": ("k17",), "ffn_up": ("k17",), "ffn_down": ("k17",)}
-
-
-def gemm_route_x3(name, M, mode=None):
-    """The kernel of the fp32-parity (bf16x3) projection ``name`` at ``M`` tokens."""
-    mode = mode or GEMM
-    if mode == "lib" or name is None:
-        return ("lib",)
-    for top, route in GEMM_ROUTES_X3[name]:
-        if M <= top:
-            return route
-    return X3_LARGE[name]
 
 
 def _mm_x3(x2, lin, epilogue="none", name=None, allow_split=False):
@@ -217,8 +226,8 @@ def _mm_x3(x2, lin, epilogue="none", name=None, allow_split=False):
         out = torch.empty(M, N, device=x2.device, dtype=torch.float32)
         bp = None if bias is None else bias.data_ptr()
         if route[0] == "k17":
-            hip.k17_gemm(xc.data_ptr(), w3.data_ptr(), bp, out.data_ptr(), M, N, 3 * K, 3 * K, 3 * K, N,
-                         epilogue=epi, out_f32=True, stream=st)
+            _k17_launch(route, xc.data_ptr(), w3.data_ptr(), bp, out.data_ptr(), M, N, 3 * K, 3 * K, 3 * K, N,
+                        epilogue=epi, out_f32=True, stream=st)
         else:
             hip.k18_gemm(xc.data_ptr(), w3.data_ptr(), bp, out.data_ptr(), M, N, 3 * K, 3 * K, 3 * K, N,
                          epilogue=epi, out_f32=True, cfg=route[1], stream=st)
