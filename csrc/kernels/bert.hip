@@ -314,10 +314,29 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
 #pragma unroll
     for (int e = 0; e < 16; ++e) o[r][e] = 0.f;
 
-  for (int c0 = 0; c0 < S; c0 += 64) {
-    // S^T for keys [c0, c0 + 64): two 32-key row blocks; lane (query, h) holds
-    // keys 32 rb + 8 g + 4 h + e
-    f32x16 st[2];
+  // Chunk classes (round 6).  A key-padding mask is a run of valid keys, so
+  // most 64-key chunks are all valid or all padded: an all-valid chunk takes
+  // the unmasked math (no bias add, one FMA per score into the exponent), an
+  // all-padded chunk is skipped -- exactly: behind any valid key its scores
+  // are exp2(<= -14000) = 0 in fp32, and if it comes first the first valid
+  // chunk's rescale zeroes it.  Only a sequence with no valid key at all runs
+  // every chunk masked (softmax over the padded scores, as torch does).
+  const int nch = S / 64;
+  uint32_t todo = (1u << nch) - 1u, full = todo;
+  if constexpr (MASKED) {
+    full = 0u;
+    uint32_t empty = 0u;
+    for (int c = 0; c < nch; ++c) {
+      const uint64_t v = __ballot(kb[64 * c + lane] == 0.0f);
+      if (v == ~0ull) full |= 1u << c;
+      if (v == 0ull) empty |= 1u << c;
+    }
+    if (empty != todo) todo &= ~empty;
+  }
+
+  // S^T for keys [c0, c0 + 64): two 32-key row blocks; lane (query, h) holds
+  // keys 32 rb + 8 g + 4 h + e
+  auto qk = [&](f32x16 (&st)[2], int c0) {
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
 #pragma unroll
@@ -329,11 +348,14 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
         st[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(kf), as_bf8(qf[kk]), st[rb], 0, 0, 0);
       }
     }
-    // masked: x = s * scale * log2e + bias, max and exp2(x - m) on x;
-    // unmasked: max on the raw scores (scale > 0 commutes with max) and
-    // p = exp2(s * c - m * c) as one FMA per score
+  };
+  // online softmax of one chunk's scores and O^T += V^T P^T.  masked: x = s
+  // scale log2e + bias, max and exp2(x - m) on x; unmasked (or an all-valid
+  // chunk): max on the raw scores (scale > 0 commutes with max) and p =
+  // exp2(s c - m c) as one FMA per score
+  auto soft_pv = [&](f32x16 (&st)[2], int c0, bool bias_chunk) {
     float mx = -1.0e30f;
-    if constexpr (MASKED) {
+    if (bias_chunk) {
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
@@ -366,8 +388,8 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
         float pv[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          pv[e] = MASKED ? __builtin_amdgcn_exp2f(st[rb][4 * g + e] - m_new)
-                         : __builtin_amdgcn_exp2f(__builtin_fmaf(st[rb][4 * g + e], sl2, -m_new));
+          pv[e] = bias_chunk ? __builtin_amdgcn_exp2f(st[rb][4 * g + e] - m_new)
+                             : __builtin_amdgcn_exp2f(__builtin_fmaf(st[rb][4 * g + e], sl2, -m_new));
         ls2 += f32x2{pv[0], pv[1]} + f32x2{pv[2], pv[3]};
         const int kk2 = 2 * rb + (g >> 1), half = g & 1;
         pf[kk2][2 * half] = pack2(pv[0], pv[1]);
@@ -390,6 +412,31 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
         const v4u af = v4u{a0[0], a0[1], a1[0], a1[1]};
         o[rd] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(af), as_bf8(pf[kk2]), o[rd], 0, 0, 0);
       }
+  };
+  // two score buffers: the next chunk's QK^T MFMAs are issued before this
+  // chunk's softmax, so the matrix pipe works while the wave's VALU runs the
+  // exponentials (unrolled by two: no buffer copies)
+  f32x16 sa[2], sb[2];
+  int ca = __builtin_ctz(todo);
+  todo &= todo - 1u;
+  qk(sa, 64 * ca);
+  while (true) {
+    const bool more = todo != 0u;
+    const int cb = more ? __builtin_ctz(todo) : 0;
+    if (more) {
+      todo &= todo - 1u;
+      qk(sb, 64 * cb);
+    }
+    soft_pv(sa, 64 * ca, MASKED && !((full >> ca) & 1u));
+    if (!more) break;
+    const bool more2 = todo != 0u;
+    if (more2) {
+      ca = __builtin_ctz(todo);
+      todo &= todo - 1u;
+      qk(sa, 64 * ca);
+    }
+    soft_pv(sb, 64 * cb, MASKED && !((full >> cb) & 1u));
+    if (!more2) break;
   }
   const float inv = 1.0f / (l_part + __shfl_xor(l_part, 32, 64));
   uint16_t* orow = out + ((size_t)seq * S + q) * HD + head * kAD;
