@@ -13,6 +13,7 @@
 // `bert_large` perf_analyzer config of BASELINE.json).
 
 #include <algorithm>
+#include <type_traits>
 
 #include "kernels/common.h"
 
@@ -353,9 +354,10 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
   // scale log2e + bias, max and exp2(x - m) on x; unmasked (or an all-valid
   // chunk): max on the raw scores (scale > 0 commutes with max) and p =
   // exp2(s c - m c) as one FMA per score
-  auto soft_pv = [&](f32x16 (&st)[2], int c0, bool bias_chunk) {
+  auto soft_pv = [&](f32x16 (&st)[2], int c0, auto bias_tag) {
+    constexpr bool bias_chunk = decltype(bias_tag)::value;
     float mx = -1.0e30f;
-    if (bias_chunk) {
+    if constexpr (bias_chunk) {
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
@@ -413,31 +415,22 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
         o[rd] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(af), as_bf8(pf[kk2]), o[rd], 0, 0, 0);
       }
   };
-  // two score buffers: the next chunk's QK^T MFMAs are issued before this
-  // chunk's softmax, so the matrix pipe works while the wave's VALU runs the
-  // exponentials (unrolled by two: no buffer copies)
-  f32x16 sa[2], sb[2];
-  int ca = __builtin_ctz(todo);
-  todo &= todo - 1u;
-  qk(sa, 64 * ca);
-  while (true) {
-    const bool more = todo != 0u;
-    const int cb = more ? __builtin_ctz(todo) : 0;
-    if (more) {
-      todo &= todo - 1u;
-      qk(sb, 64 * cb);
-    }
-    soft_pv(sa, 64 * ca, MASKED && !((full >> ca) & 1u));
-    if (!more) break;
-    const bool more2 = todo != 0u;
-    if (more2) {
-      ca = __builtin_ctz(todo);
-      todo &= todo - 1u;
-      qk(sa, 64 * ca);
-    }
-    soft_pv(sb, 64 * cb, MASKED && !((full >> cb) & 1u));
-    if (!more2) break;
+  // all-valid chunks first (unmasked math), then the partial ones (masked
+  // math): the online softmax does not depend on the chunk order, and each
+  // loop keeps one compile-time path (a per-chunk branch inside the softmax
+  // cost registers and 10 % on the masked kernel, profiles/r6_k12.md)
+  f32x16 st[2];
+  for (uint32_t f = todo & full; f; f &= f - 1u) {
+    const int c0 = 64 * __builtin_ctz(f);
+    qk(st, c0);
+    soft_pv(st, c0, std::false_type{});
   }
+  if constexpr (MASKED)
+    for (uint32_t m = todo & ~full; m; m &= m - 1u) {
+      const int c0 = 64 * __builtin_ctz(m);
+      qk(st, c0);
+      soft_pv(st, c0, std::true_type{});
+    }
   const float inv = 1.0f / (l_part + __shfl_xor(l_part, 32, 64));
   uint16_t* orow = out + ((size_t)seq * S + q) * HD + head * kAD;
 #pragma unroll

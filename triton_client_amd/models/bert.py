@@ -56,7 +56,7 @@ GEMM = os.environ.get("TC_BERT_GEMM", "auto")
 # (hipBLASLt: where it measured faster).
 INF = 1 << 30
 GEMM_ROUTES = {
-    "qkv": [(384, ("k18", 6, 1)), (768, ("k18", 3, 1)), (3072, ("lib",)), (6144, ("k17", 0)), (INF, ("lib",))],
+    "qkv": [(384, ("k18", 6, 1)), (768, ("k18", 3, 1)), (4608, ("lib",)), (6144, ("k17", 0)), (INF, ("lib",))],
     "out": [(384, ("k18", 9, 1)), (768, ("k18", 6, 1)), (1536, ("k18", 0, 1)), (3072, ("k18", 3, 1)),
             (INF, ("lib",))],
     "ffn_up": [(384, ("k18", 1, 1)), (768, ("k18", 3, 1)), (INF, ("lib",))],
