@@ -262,6 +262,9 @@ constexpr Cfg kCfgs[] = {
     {64, 128, 256, 6},   // 7: 144 KB, 1 per CU, 5 in flight
     {128, 64, 256, 6},   // 8: 144 KB, 1 per CU, 5 in flight
     {32, 64, 256, 8},    // 9: 96 KB, 1 per CU, 7 in flight (4 waves of 16 x 32)
+    {128, 128, 512, 4},  // 10: 128 KB, 1 per CU, 3 in flight, 8 waves
+    {128, 64, 256, 5},   // 11: 120 KB, 1 per CU, 4 in flight
+    {256, 128, 512, 3},  // 12: 144 KB, 1 per CU, 8 waves of 128 x 32
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -351,7 +354,10 @@ int tcamd_k18_gemm(const void* A, const void* B, const float* bias, void* C, int
     case 6: return launch_cfg<64, 64, 2, 2, 5>(prm, (int)grid, s, epi, f32);
     case 7: return launch_cfg<64, 128, 2, 2, 6>(prm, (int)grid, s, epi, f32);
     case 8: return launch_cfg<128, 64, 2, 2, 6>(prm, (int)grid, s, epi, f32);
-    default: return launch_cfg<32, 64, 2, 2, 8>(prm, (int)grid, s, epi, f32);
+    case 9: return launch_cfg<32, 64, 2, 2, 8>(prm, (int)grid, s, epi, f32);
+    case 10: return launch_cfg<128, 128, 2, 4, 4>(prm, (int)grid, s, epi, f32);
+    case 11: return launch_cfg<128, 64, 2, 2, 5>(prm, (int)grid, s, epi, f32);
+    default: return launch_cfg<256, 128, 2, 4, 3>(prm, (int)grid, s, epi, f32);
   }
 }
 

@@ -208,7 +208,7 @@ K18_SHAPES = [(384, 3072, 1024), (384, 1024, 4096), (3072, 4096, 1024), (300, 25
 
 @pytest.mark.parametrize("M,N,K", K18_SHAPES)
 @pytest.mark.parametrize("epi", ["none", "bias", "bias_gelu"])
-@pytest.mark.parametrize("cfg", list(range(10)))
+@pytest.mark.parametrize("cfg", list(range(13)))
 def test_k18_gemm_bf16_out(M, N, K, epi, cfg):
     """Every tile configuration against the fp32 matmul of the same bf16
     operands; the ldc padding and the rows past M stay untouched."""
@@ -236,7 +236,7 @@ def test_k18_gemm_bf16_out(M, N, K, epi, cfg):
 
 @pytest.mark.parametrize("M,N,K,splits", [(384, 1024, 4096, 8), (384, 1024, 1024, 4), (3072, 1024, 4096, 2),
                                           (77, 256, 512, 8), (1000, 512, 3072, 3)])
-@pytest.mark.parametrize("cfg", [0, 1, 4, 5, 7, 9])
+@pytest.mark.parametrize("cfg", [0, 1, 4, 5, 7, 9, 10, 11, 12])
 def test_k18_split_k_partials(M, N, K, splits, cfg):
     """split-K: slab z holds A[:, Kz] . B[:, Kz]^T in fp32 (against fp64), and
     the slabs sum to the whole product."""
