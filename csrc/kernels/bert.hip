@@ -168,6 +168,41 @@ __global__ void __launch_bounds__(256) add_ln_parts_kernel(const T* x, const flo
   }
 }
 
+// ---- QA head: (start, end)[r] = x[r] . w[0 / 1] + b[0 / 1] -----------------
+// BERT's span head is a [2 x H] Linear over every token: as a library GEMM an
+// N = 2 launch plus a cast and two strided copies.  One wave per row: each
+// lane dots its 8-element chunks with both weight rows, a butterfly sums the
+// wave, lane 0 writes the two fp32 logits into their separate [rows] planes.
+template <int E, typename T>
+__global__ void __launch_bounds__(256) qa_head_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                      const float* __restrict__ b, float* __restrict__ start,
+                                                      float* __restrict__ end, int rows) {
+  constexpr int H = 64 * E, C = E / 8;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int off = (c * 64 + lane) * 8;
+    float xv[8], w0[8], w1[8];
+    load8(x + (size_t)row * H + off, xv);
+    load8(w + off, w0);
+    load8(w + H + off, w1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s0 += xv[e] * w0[e];
+      s1 += xv[e] * w1[e];
+    }
+  }
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  if (lane == 0) {
+    start[row] = s0 + b[0];
+    end[row] = s1 + b[1];
+  }
+}
+
 // Embedding sum + LayerNorm: out[r] = LN(word[ids[r]] + pos[r % S] +
 // type[types[r]]) in one pass (torch: three gathers, two adds and a LayerNorm,
 // six launches and ~5 passes over [tokens, H]).  Ids outside the tables are
@@ -540,6 +575,32 @@ int tcamd_add_layernorm_parts(const void* x, const float* parts, int nparts, lon
     default: return hipErrorInvalidValue;
   }
 #undef TC_K11P
+  return hipGetLastError();
+}
+
+// QA head: start[r] = x[r] . w[0] + b[0], end[r] = x[r] . w[1] + b[1] (fp32
+// out) over rows of H (512 / 1024 / 2048 / 4096) elements; x / w bf16 (f32 =
+// 0) or fp32, b fp32 [2]; 16-B aligned x / w.
+int tcamd_qa_head(const void* x, const void* w, const float* b, float* start, float* end, int rows, int H, int f32,
+                  void* stream) {
+  if (rows <= 0) return hipSuccess;
+  if (!x || !w || !b || !start || !end || ((uintptr_t)x | (uintptr_t)w) % 16) return hipErrorInvalidValue;
+  const dim3 grid((rows + 3) / 4), block(256);
+  hipStream_t s = (hipStream_t)stream;
+#define TC_QA(E, T) \
+  hipLaunchKernelGGL((qa_head_kernel<E, T>), grid, block, 0, s, (const T*)x, (const T*)w, b, start, end, rows)
+  switch (H * 2 + (f32 ? 1 : 0)) {
+    case 1024: TC_QA(8, uint16_t); break;
+    case 1025: TC_QA(8, float); break;
+    case 2048: TC_QA(16, uint16_t); break;
+    case 2049: TC_QA(16, float); break;
+    case 4096: TC_QA(32, uint16_t); break;
+    case 4097: TC_QA(32, float); break;
+    case 8192: TC_QA(64, uint16_t); break;
+    case 8193: TC_QA(64, float); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef TC_QA
   return hipGetLastError();
 }
 

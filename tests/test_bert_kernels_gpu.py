@@ -176,3 +176,24 @@ def test_attention_rejects_unsupported_shapes():
     for S in (100, 448):
         with pytest.raises(hip.HipError):
             hip.attention(x.data_ptr(), None, o.data_ptr(), 1, S, 16, 0.125)
+
+
+@pytest.mark.parametrize("f32", [False, True])
+@pytest.mark.parametrize("rows,H", [(1, 1024), (777, 1024), (5, 512)])
+def test_qa_head(f32, rows, H):
+    """The span head kernel (one launch: both logits planes in fp32) against
+    fp64 of the same operands."""
+    _need_gpu()
+    from triton_client_amd.ops import hip
+
+    g = torch.Generator(device=DEV).manual_seed(rows + H)
+    dt = torch.float32 if f32 else torch.bfloat16
+    x = torch.randn(rows, H, device=DEV, generator=g).to(dt)
+    w = (torch.randn(2, H, device=DEV, generator=g) * 0.05).to(dt)
+    b = torch.randn(2, device=DEV, generator=g)
+    out = torch.full((2, rows), float("nan"), device=DEV)
+    hip.qa_head(x.data_ptr(), w.data_ptr(), b.data_ptr(), out[0].data_ptr(), out[1].data_ptr(), rows, H, f32=f32)
+    torch.cuda.synchronize()
+    ref = (x.double() @ w.double().t() + b.double()).t()
+    err = ((out.double() - ref).norm() / ref.norm()).item()
+    assert err < 1e-5, err

@@ -339,6 +339,26 @@ def _attention(qkv, b, s, mask_i32, bias, qkv_bias=None):
     return a.transpose(1, 2).reshape(b, s, HIDDEN)
 
 
+def _qa_head(x, qa):
+    """(start, end) fp32 logits [b, s]: the QA head kernel (csrc/kernels/bert.hip qa_head) on the GPU
+    (one launch instead of an N = 2 library GEMM, a cast and two strided
+    copies), the Linear elsewhere."""
+    b, s, H = x.shape
+    if FUSED and x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.is_contiguous() and \
+            qa.weight.dtype == x.dtype and H % 512 == 0:
+        from triton_client_amd.ops import hip
+
+        bias = getattr(qa, "bias_f32", None)
+        if bias is None or bias.device != x.device:
+            bias = qa.bias_f32 = qa.bias.detach().float().contiguous()
+        out = torch.empty(2, b, s, device=x.device, dtype=torch.float32)
+        hip.qa_head(x.data_ptr(), qa.weight.data_ptr(), bias.data_ptr(), out[0].data_ptr(), out[1].data_ptr(), b * s, H,
+                    f32=x.dtype == torch.float32, stream=torch.cuda.current_stream(x.device).cuda_stream)
+        return out[0], out[1]
+    logits = qa(x).float()
+    return logits[..., 0], logits[..., 1]
+
+
 class _Layer(nn.Module):
     def __init__(self):
         super().__init__()
@@ -402,8 +422,7 @@ class BertLargeQA(nn.Module):
         mask_i32 = None if dense else attention_mask.to(torch.int32).contiguous()
         for layer in self.layers:
             x = layer(x, bias, mask_i32)
-        logits = self.qa(x).float()
-        return logits[..., 0], logits[..., 1]
+        return _qa_head(x, self.qa)
 
 
 def init_weights(model, seed=0):

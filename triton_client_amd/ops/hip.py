@@ -261,6 +261,11 @@ _SIGS = {
         ctypes.c_int,
     ),
     "tcamd_k18_calls": ([], ctypes.c_longlong),
+    "tcamd_qa_head": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+         ctypes.c_int, ctypes.c_int, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_add_layernorm_parts": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p,
          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_void_p],
@@ -959,6 +964,12 @@ def k18_cfg(cfg):
 def k18_calls():
     """K18 launches so far in this process."""
     return int(_load().tcamd_k18_calls())
+
+
+def qa_head(x, w, b, start, end, rows, H, f32=False, stream=None):
+    """BERT's span head: start[r] = x[r] . w[0] + b[0], end[r] = x[r] . w[1] +
+    b[1] in fp32; x [rows][H] and w [2][H] bf16 (or fp32 with ``f32``), b fp32 [2]."""
+    _check(_load().tcamd_qa_head(x, w, b, start, end, int(rows), int(H), 1 if f32 else 0, _vp(stream)), "qa_head")
 
 
 def add_layernorm_parts(x, parts, nparts, pstride, bias, gamma, beta, out, rows, H, eps, f32=False, stream=None):
