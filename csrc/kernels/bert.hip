@@ -274,6 +274,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+typedef short v4s __attribute__((ext_vector_type(4)));
 
 constexpr int kAD = 64;           // head dim
 constexpr int kAMaxS = 384;       // keys / queries per sequence (multiple of 64)
@@ -291,10 +292,9 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
                                                            uint16_t* __restrict__ out, int S, int heads, float scale,
                                                            const uint16_t* __restrict__ qkv_bias) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_a[];
-  const int ldv = S + 4;  // V^T row (elements)
   uint16_t* Ks = reinterpret_cast<uint16_t*>(lds_a);
-  uint16_t* Vt = Ks + S * kAD;
-  float* kb = reinterpret_cast<float*>(Vt + kAD * ldv);  // per-key log2-domain bias
+  uint16_t* Vs = Ks + S * kAD;
+  float* kb = reinterpret_cast<float*>(Vs + S * kAD);  // per-key log2-domain bias
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nthr = blockDim.x;
   const int seq = blockIdx.x / heads, head = blockIdx.x % heads;
@@ -302,21 +302,26 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
   const uint16_t* base = qkv + (size_t)seq * S * ld + head * kAD;
   constexpr float kLog2e = 1.4426950408889634f;
 
-  // ---- stage K (swizzled rows) and V^T ----
-  for (int e = tid; e < S * 8; e += nthr) {
-    const int key = e >> 3, c = e & 7;
-    const v4u v = *reinterpret_cast<const v4u*>(base + (size_t)key * ld + HD + 8 * c);
-    *reinterpret_cast<v4u*>(Ks + key * kAD + 8 * (c ^ ((key >> 1) & 7))) = v;
-  }
-  for (int e = tid; e < (S / 2) * 8; e += nthr) {
-    const int kp = e >> 3, c = e & 7, key = 2 * kp;
-    const v4u a = *reinterpret_cast<const v4u*>(base + (size_t)key * ld + 2 * HD + 8 * c);
-    const v4u b = *reinterpret_cast<const v4u*>(base + (size_t)(key + 1) * ld + 2 * HD + 8 * c);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t lo = (a[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-      const uint32_t hi = (b[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-      *reinterpret_cast<uint32_t*>(Vt + (8 * c + j) * ldv + key) = lo | (hi << 16);
+  // ---- stage K and V rows (128 B each) by LDS-DMA (round 6) ----
+  // Both row-major, 16-B chunks XOR-swizzled on the SOURCE address (the DMA
+  // writes lane-linear: one wave instruction = 8 rows), every instruction of
+  // the block in flight at once and one wait.  K chunk c of key k sits at
+  // c ^ ((k >> 1) & 7) (conflict-free b128 reads by 16 consecutive keys);
+  // V chunk c at c ^ (((k >> 1) & 1) << 2), which makes the transposing
+  // ds_read_b64_tr_b16 reads of the PV operand conflict-free.  (Round 5
+  // staged with per-thread 16-B loads and transposed V by 4-byte LDS writes:
+  // ~25 of 83 us at bs64 and half of bs1's 11 us went to that staging,
+  // profiles/r6_k12/.)
+  {
+    const int nw = nthr >> 6, nrb = S >> 3;  // waves, 8-row blocks per operand
+    const int r8 = lane >> 3, cs = lane & 7;
+    for (int j = wave; j < 2 * nrb; j += nw) {
+      const bool isv = j >= nrb;
+      const int row = 8 * (isv ? j - nrb : j) + r8;
+      const int c = isv ? cs ^ (((row >> 1) & 1) << 2) : cs ^ ((row >> 1) & 7);
+      const uint16_t* src = base + (size_t)row * ld + (isv ? 2 * HD : HD) + 8 * c;
+      uint8_t* dst = lds_a + (isv ? S * 128 : 0) + (j - (isv ? nrb : 0)) * 1024;
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)dst, 16, 0, 0);
     }
   }
   if (MASKED)
@@ -340,7 +345,8 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
       }
     }
   }
-  __syncthreads();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's K / V DMAs landed
+  __syncthreads();                                   // ... and every other wave's
 
   const float sl2 = scale * kLog2e;
   float m_run = -1.0e30f, l_part = 0.f;
@@ -370,6 +376,14 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
     if (empty != todo) todo &= ~empty;
   }
 
+  // transposed V reads: lane 4 q4 + p4 of 16-lane group g supplies row (key)
+  // 4 h + q4 of the 16-key step, dims 32 rd + 16 (g & 1) + 4 p4 .. + 3 (8 B of
+  // chunk 4 rd + 2 (g & 1) + p4 / 2, swizzled by its key -- bit 1 of the key
+  // is bit 1 of q4, the other terms are multiples of 4)
+  const int q4 = (lane >> 2) & 3, p4 = lane & 3, g1 = (lane >> 4) & 1;
+  const int vch = 2 * g1 + (p4 >> 1);
+  const uint8_t* vbase = lds_a + S * 128 + (4 * h + q4) * 128 + ((vch ^ (((q4 >> 1) & 1) << 2)) << 4) + 8 * (p4 & 1);
+  const int vrd = ((4 ^ (((q4 >> 1) & 1) << 2)) - (((q4 >> 1) & 1) << 2)) << 4;  // rd = 1: chunk + 4, swizzled
   // S^T for keys [c0, c0 + 64): two 32-key row blocks; lane (query, h) holds
   // keys 32 rb + 8 g + 4 h + e
   auto qk = [&](f32x16 (&st)[2], int c0) {
@@ -438,14 +452,18 @@ __global__ void __launch_bounds__(768, 1) attention_kernel(const uint16_t* __res
     for (int r = 0; r < 2; ++r)
 #pragma unroll
       for (int e = 0; e < 16; ++e) o[r][e] *= alpha;
-    // O^T += V^T P^T: A = V^T rows (dims 32 rd + col), keys in the permuted order
+    // O^T += V^T P^T: A = V^T rows (dims 32 rd + col), keys in the permuted
+    // order, read TRANSPOSED from the row-major V image: ds_read_b64_tr_b16
+    // gives lane i of a 16-lane group column i (= its dim) of 4 key rows
 #pragma unroll
     for (int kk2 = 0; kk2 < 4; ++kk2)
 #pragma unroll
       for (int rd = 0; rd < 2; ++rd) {
-        const uint16_t* vr = Vt + (32 * rd + col) * ldv + c0 + 16 * kk2 + 4 * h;
-        const v2u a0 = *reinterpret_cast<const v2u*>(vr);
-        const v2u a1 = *reinterpret_cast<const v2u*>(vr + 8);
+        const uint8_t* vr = vbase + (c0 + 16 * kk2) * 128 + rd * vrd;
+        const v2u a0 = __builtin_bit_cast(v2u, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                                   (__attribute__((address_space(3))) v4s*)(vr)));
+        const v2u a1 = __builtin_bit_cast(v2u, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                                   (__attribute__((address_space(3))) v4s*)(vr + 8 * 128)));
         const v4u af = v4u{a0[0], a0[1], a1[0], a1[1]};
         o[rd] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(af), as_bf8(pf[kk2]), o[rd], 0, 0, 0);
       }
@@ -638,7 +656,7 @@ int tcamd_attention_bias(const void* qkv, const void* qkv_bias, const int* mask,
   if (S <= 0 || S % 64 || S > kAMaxS || heads <= 0 || ((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)qkv_bias) % 16 ||
       (uintptr_t)mask % 16)
     return hipErrorInvalidValue;
-  const size_t lds = (size_t)S * kAD * 2 + (size_t)kAD * (S + 4) * 2 + (size_t)S * 4;
+  const size_t lds = (size_t)S * kAD * 2 * 2 + (size_t)S * 4;  // K rows | V rows | key bias
   static bool attr = false;
   if (!attr) {
     hipError_t e =

@@ -82,9 +82,14 @@ class ServerProcess:
 
         t0 = time.time()
         last = None
+        said = t0
         while time.time() - t0 < timeout:
             if self.proc.poll() is not None:
                 raise RuntimeError("server exited with %s (log: %s)" % (self.proc.returncode, self.log_path))
+            if time.time() - said >= 30:  # a long model load (graph captures) must not look hung
+                said = time.time()
+                print("[harness] waiting for the server (%s): %.0f s" % (model or "ready", said - t0), file=sys.stderr,
+                      flush=True)
             try:
                 c = httpclient.InferenceServerClient(self.http_url, connection_timeout=2, network_timeout=5)
                 ok = c.is_server_ready() and (model is None or c.is_model_ready(model))
