@@ -152,7 +152,7 @@ class Point:
         return [self.s.loop_count()]
 
     def wait_after(self, marks, n):
-        self.s.loop_wait(marks[0][0] + n)
+        self.s.loop_wait(marks[0][0] + n, log=log)
 
     def take(self, marks, n, t0_ns):
         """The first n requests completed after ``marks``: latencies (ns) and
@@ -223,7 +223,7 @@ class Lanes:
     def wait_after(self, marks, n):
         k = len(self.points)
         for p, m in zip(self.points, marks):  # equal concurrency per lane: each takes its share
-            p.s.loop_wait(m[0] + -(-n // k))
+            p.s.loop_wait(m[0] + -(-n // k), log=log)
 
     def take(self, marks, n, t0_ns):
         """All lanes' completions since ``marks`` merged on the engine clock

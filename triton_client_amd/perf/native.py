@@ -126,11 +126,23 @@ class PerfSession:
         n = _load().tcperf_loop_count(self._h, ctypes.byref(now))
         return int(n), int(now.value)
 
-    def loop_wait(self, target, timeout_s=600.0):
-        """Block (GIL released) until ``target`` records exist."""
-        err = ctypes.create_string_buffer(1024)
-        if _load().tcperf_loop_wait(self._h, int(target), float(timeout_s), err, 1024) != 0:
-            raise PerfError(err.value.decode(errors="replace"))
+    def loop_wait(self, target, timeout_s=600.0, heartbeat_s=30.0, log=None):
+        """Block (GIL released) until ``target`` records exist; every
+        ``heartbeat_s`` without reaching it, ``log`` (if given) gets the
+        progress, so a long window never looks like a hung run."""
+        import time
+
+        t0 = time.time()
+        while True:
+            step = min(heartbeat_s, max(0.0, timeout_s - (time.time() - t0)))
+            err = ctypes.create_string_buffer(1024)
+            if _load().tcperf_loop_wait(self._h, int(target), float(step), err, 1024) == 0:
+                return
+            msg = err.value.decode(errors="replace")
+            if "timed out" not in msg or time.time() - t0 >= timeout_s:
+                raise PerfError(msg)
+            if log is not None:
+                log("loop: %d of %d requests after %.0f s" % (self.loop_count()[0], int(target), time.time() - t0))
 
     def loop_records(self, start, n):
         """Records [start, start + n): (start_ns, end_ns, ok) on the engine clock."""
