@@ -105,6 +105,8 @@ def parse_args(argv=None):
     ap.add_argument("--sweep", default="1,4,16,64,256", help="bert_large: concurrencies per GPU")
     ap.add_argument("--bert-instance-count", type=int, default=2)
     ap.add_argument("--bert-queue-delay-us", type=int, default=500)
+    ap.add_argument("--loop-timeout", type=float, default=600.0,
+                    help="seconds a timed loop may wait for its requests before the run fails (server stacks dumped)")
     ap.add_argument("--bert-precision", default="bf16", choices=["bf16", "fp32"],
                     help="bert_large: bf16 (the config-4 default) or fp32 parity (serves bert_large_fp32: bf16x3 "
                          "projections on the hand-written GEMMs, fp32 LayerNorm / attention)")
@@ -151,8 +153,10 @@ class Point:
     def marks(self):
         return [self.s.loop_count()]
 
+    timeout_s = 600.0
+
     def wait_after(self, marks, n):
-        self.s.loop_wait(marks[0][0] + n, log=log)
+        self.s.loop_wait(marks[0][0] + n, timeout_s=self.timeout_s, log=log)
 
     def take(self, marks, n, t0_ns):
         """The first n requests completed after ``marks``: latencies (ns) and
@@ -223,7 +227,7 @@ class Lanes:
     def wait_after(self, marks, n):
         k = len(self.points)
         for p, m in zip(self.points, marks):  # equal concurrency per lane: each takes its share
-            p.s.loop_wait(m[0] + -(-n // k), log=log)
+            p.s.loop_wait(m[0] + -(-n // k), timeout_s=p.timeout_s, log=log)
 
     def take(self, marks, n, t0_ns):
         """All lanes' completions since ``marks`` merged on the engine clock
@@ -363,6 +367,7 @@ def main():
     from triton_client_amd.perf.loadgen import percentile_us
 
     cpu = args.cpu
+    Point.timeout_s = args.loop_timeout
     bert = args.model == "bert_large"
     if bert:
         model = "bert_sink" if cpu else ("bert_large_fp32" if args.bert_precision == "fp32" else "bert_large")
@@ -468,24 +473,37 @@ def main():
         elapsed (max over ranks) and the two snapshots."""
         point.start()
         try:
-            point.wait_after(point.marks(), warm_n)
-            s0 = snap() if snap else None  # outside the timed windows: its RPC would ride in window 0
-            if world > 1:
-                fanout.barrier()
-            if not cpu:
-                torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            m = point.marks()
-            point.wait_after(m, steps * per)
-            s1 = snap() if snap else None
-            if not cpu:
-                torch.cuda.synchronize()
-            if world > 1:
-                fanout.barrier()
-            elapsed = time.perf_counter() - t0
-            lat, end = point.take(m, steps * per, m[0][1])
+            return _measure(point, warm_n, steps, per, snap)
+        except Exception:
+            log("timed loop failed: asking the server for its thread stacks (log %s)" % srv_log)
+            try:
+                srv.dump_stacks()
+            except Exception as e:  # noqa: BLE001
+                log("stack dump failed: %s" % e)
+            raise
         finally:
-            point.stop()
+            try:
+                point.stop()
+            except Exception as e:  # noqa: BLE001 -- the loop's own error is the one to report
+                log("loop stop: %s" % e)
+
+    def _measure(point, warm_n, steps, per, snap):
+        point.wait_after(point.marks(), warm_n)
+        s0 = snap() if snap else None  # outside the timed windows: its RPC would ride in window 0
+        if world > 1:
+            fanout.barrier()
+        if not cpu:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        m = point.marks()
+        point.wait_after(m, steps * per)
+        s1 = snap() if snap else None
+        if not cpu:
+            torch.cuda.synchronize()
+        if world > 1:
+            fanout.barrier()
+        elapsed = time.perf_counter() - t0
+        lat, end = point.take(m, steps * per, m[0][1])
         return lat, end, fanout.max_over_ranks(elapsed), (s0, s1)
 
     try:

@@ -101,6 +101,14 @@ class ServerProcess:
             time.sleep(0.5)
         raise TimeoutError("server not ready after %ss: %s" % (timeout, last))
 
+    def dump_stacks(self, settle_s=2.0):
+        """SIGUSR1: the server writes every thread's Python stack to its log."""
+        import signal
+
+        if self.proc.poll() is None:
+            self.proc.send_signal(signal.SIGUSR1)
+            time.sleep(settle_s)
+
     def stop(self):
         if self.proc.poll() is None:
             self.proc.terminate()

@@ -48,6 +48,13 @@ def main(argv=None):
         # 4 -> 8 A/B set it by hand
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
 
+    # `kill -USR1 <server>` dumps every thread's Python stack into the server
+    # log (the bench asks for it when a timed loop stops completing)
+    import faulthandler
+    import signal
+
+    faulthandler.register(signal.SIGUSR1, all_threads=True)
+
     from .app import default_models, serve
     from .core import InferenceServer
 
