@@ -485,7 +485,11 @@ def main():
             try:
                 point.stop()
             except Exception as e:  # noqa: BLE001 -- the loop's own error is the one to report
-                log("loop stop: %s" % e)
+                log("loop stop: %s -- asking the server for its thread stacks" % e)
+                try:
+                    srv.dump_stacks()
+                except Exception as e2:  # noqa: BLE001
+                    log("stack dump failed: %s" % e2)
 
     def _measure(point, warm_n, steps, per, snap):
         point.wait_after(point.marks(), warm_n)
