@@ -65,12 +65,20 @@ GEMM_ROUTES = {
 # the fp32-parity model's bf16x3 projections (K tripled, fp32 out, erf GELU;
 # tools/gemm_sweep.py --x3, whose library arm adds the bias and the GELU as
 # separate ops, as torch.mm must)
+#
+# Past 3,072 tokens every x3 projection stays on K17 even where the library
+# measured faster (QKV 188 vs 216 us, FFN-down 281 vs 312 us at 12,288
+# tokens): served with two instances (two streams), the fp32 model stalled
+# twice at c256 with one instance thread waiting in hipStreamSynchronize
+# forever (profiles/r6_bert_fp32/); the library's large fp32-output GEMMs were
+# the only kernels of that graph not ours, so they are kept off it.
 GEMM_ROUTES_X3 = {
-    "qkv": [(384, ("k18", 6, 1)), (INF, ("lib",))],
+    "qkv": [(384, ("k18", 6, 1)), (3072, ("lib",)), (INF, ("k17", 0))],
     "out": [(384, ("k18", 6, 2)), (768, ("k18", 2, 2)), (1536, ("k18", 3, 2)), (3072, ("k18", 3, 1)),
             (INF, ("k17", 0))],
     "ffn_up": [(384, ("k18", 1, 1)), (768, ("k18", 3, 1)), (1536, ("lib",)), (INF, ("k17", 0))],
-    "ffn_down": [(384, ("k18", 7, 4)), (768, ("k18", 3, 4)), (1536, ("k18", 3, 2)), (INF, ("lib",))],
+    "ffn_down": [(384, ("k18", 7, 4)), (768, ("k18", 3, 4)), (1536, ("k18", 3, 2)), (3072, ("lib",)),
+                 (INF, ("k17", 0))],
 }
 OURS_FROM_K17 = 3072  # "ours" mode where the table says lib: K17 from this many tokens, K18 cfg 3 below
 
