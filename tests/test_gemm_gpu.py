@@ -164,6 +164,7 @@ def test_k17_dynamic_schedule_every_tile_once():
         refs.append((a.float() @ b.float().t()) + bias)
     outs = [[torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16) for _ in range(3)]
             for M, N, K in shapes]
+    torch.cuda.synchronize()  # the NaN fills ran on the current stream; the launches below use two others
     with hip.knob(TCAMD_K17_DYN=1):
         for rep in range(3):
             for i in range(len(shapes)):
