@@ -5,7 +5,8 @@ Two served precisions of the same BERT-large QA model (seed 0, random init):
 * ``bert_large`` (the config-4 serving default): bf16 weights and
   activations, hipBLASLt GEMMs with fp32 accumulation, K11 residual-add +
   LayerNorm, K12 attention (key-padding mask in kernel), one HIP graph per
-  (batch bucket, masked | dense) captured in the server.  Compared with an
+  batch bucket captured in the server (the per-bucket "dense" variant is off
+  since round 6: K12 runs an all-ones mask's chunks with the unmasked math).  Compared with an
   fp32 forward of the SAME weights (the bf16 parameters upcast), so the gap
   is the serving precision, not a weight rounding.
 * ``bert_large_fp32``: fp32-parity compute (every projection one bf16x3 GEMM,
@@ -13,8 +14,8 @@ Two served precisions of the same BERT-large QA model (seed 0, random init):
   fp32 weights.
 
 Both are served through the bench server's native gRPC front end at batch 1,
-7 (bucket 8: a padded graph) and 64, with padded rows (masked graph) and an
-all-full-length batch (dense graph).  The contract (our own: the reference
+7 (bucket 8: a padded graph) and 64, with padded rows and an
+all-full-length batch.  The contract (our own: the reference
 holds no bert fixture, parity with it is unpinned), per row of start and end
 logits:
 

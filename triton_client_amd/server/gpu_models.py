@@ -524,6 +524,12 @@ class BertLarge(Model):
     # with power-of-two buckets a 33-row batch paid for 64 (served c64: 33 rows
     # per batch at 11.5 ms vs 7.9 ms for a 32-row forward)
     BUCKETS = (1, 2, 4, 8, 12, 16, 20, 24, 28, 32, 40, 48, 56, 64)
+    # a second, unmasked ("dense") graph per bucket, picked per batch when no
+    # real row is padded.  Off since round 6: K12 classifies its key chunks
+    # (an all-ones mask runs the unmasked math: 9.9 vs 9.8 us at bs1), so the
+    # dense graph no longer pays, while picking it costs a device reduction and
+    # a host sync per batch on HIP-shm inputs (profiles/r6_k12/)
+    DENSE_VARIANT = False
 
     def __init__(self, version=1, device_id=0, use_graphs=True, layers=24, **kw):
         super().__init__(version, **kw)
@@ -578,11 +584,11 @@ class BertLarge(Model):
             slot["outs"][1][:b].copy_(en)
 
         slot["run"] = run
-        # two graphs per bucket: with the key-padding bias, and "dense" (no
-        # padding in any real row: attention without a mask, picked per batch)
+        # one graph per bucket with the key-padding mask (plus a "dense" one
+        # without it when DENSE_VARIANT: no padding in any real row)
         with torch.cuda.stream(slot["stream"]), torch.no_grad():
             for b in self.BUCKETS:
-                for dense in (False, True):
+                for dense in ((False, True) if self.DENSE_VARIANT else (False,)):
                     run(b, dense)
                     if self.use_graphs:
                         g = torch.cuda.CUDAGraph()
@@ -668,7 +674,7 @@ class BertLarge(Model):
                 hip.batched_copy(c_src, c_dst, c_n, sh)
             if bucket > total:  # padding rows: keep them deterministic (mask 1, ids 0)
                 hip.memset_async(base + total * row, 0, (bucket - total) * row, sh)
-        dense = self._mask_all_ones(slot, srcs[1], total)
+        dense = self.DENSE_VARIANT and self._mask_all_ones(slot, srcs[1], total)
         ev[1].record(stream)
         with self.torch.cuda.stream(stream), self.torch.no_grad():
             if self.use_graphs:
