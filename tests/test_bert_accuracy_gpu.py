@@ -5,8 +5,8 @@ Two served precisions of the same BERT-large QA model (seed 0, random init):
 * ``bert_large`` (the config-4 serving default): bf16 weights and
   activations, hipBLASLt GEMMs with fp32 accumulation, K11 residual-add +
   LayerNorm, K12 attention (key-padding mask in kernel), one HIP graph per
-  batch bucket captured in the server (the per-bucket "dense" variant is off
-  since round 6: K12 runs an all-ones mask's chunks with the unmasked math).  Compared with an
+  batch bucket captured in the server, plus an unmasked ("dense") one for the
+  buckets from 32 rows, run when no real row is padded.  Compared with an
   fp32 forward of the SAME weights (the bf16 parameters upcast), so the gap
   is the serving precision, not a weight rounding.
 * ``bert_large_fp32``: fp32-parity compute (every projection one bf16x3 GEMM,

@@ -34,11 +34,13 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--k12-only", action="store_true")
     ap.add_argument("--seq", type=int, default=384)
+    ap.add_argument("--pad", type=int, default=20, help="padded (masked) keys at the end of every sequence")
     a = ap.parse_args()
     b, s, h, d = a.batch, a.seq, 16, 64
     q, k, v = (torch.randn(b, h, s, d, device="cuda", dtype=torch.bfloat16) for _ in range(3))
     keep = torch.ones(b, s, device="cuda", dtype=torch.bool)
-    keep[:, s - 20:] = False
+    if a.pad:
+        keep[:, s - a.pad:] = False
     add = ((~keep)[:, None, None, :].to(torch.bfloat16) * -10000.0)
     cases = {
         "none": lambda: F.scaled_dot_product_attention(q, k, v),

@@ -524,12 +524,15 @@ class BertLarge(Model):
     # with power-of-two buckets a 33-row batch paid for 64 (served c64: 33 rows
     # per batch at 11.5 ms vs 7.9 ms for a 32-row forward)
     BUCKETS = (1, 2, 4, 8, 12, 16, 20, 24, 28, 32, 40, 48, 56, 64)
-    # a second, unmasked ("dense") graph per bucket, picked per batch when no
-    # real row is padded.  Off since round 6: K12 classifies its key chunks
-    # (an all-ones mask runs the unmasked math: 9.9 vs 9.8 us at bs1), so the
-    # dense graph no longer pays, while picking it costs a device reduction and
-    # a host sync per batch on HIP-shm inputs (profiles/r6_k12/)
-    DENSE_VARIANT = False
+    # a second, unmasked ("dense") graph for the buckets from DENSE_FROM rows,
+    # picked per batch when no real row is padded.  Below that every batch
+    # runs the masked graph: K12 classifies its key chunks, so an all-ones
+    # mask runs the unmasked math (bs1 9.8 vs 9.7-10.8 us), while picking the
+    # dense graph costs a device reduction and a host sync per batch on
+    # HIP-shm inputs (~40 us of compute_input at c1).  At 64 rows the
+    # unmasked kernel is still 4-8 % faster (78-80 vs 82-87 us,
+    # profiles/r6_k12/k12_allones.log), worth the sync.
+    DENSE_FROM = 32
 
     def __init__(self, version=1, device_id=0, use_graphs=True, layers=24, **kw):
         super().__init__(version, **kw)
@@ -584,11 +587,11 @@ class BertLarge(Model):
             slot["outs"][1][:b].copy_(en)
 
         slot["run"] = run
-        # one graph per bucket with the key-padding mask (plus a "dense" one
-        # without it when DENSE_VARIANT: no padding in any real row)
+        # one graph per bucket with the key-padding mask, plus a "dense" one
+        # without it from DENSE_FROM rows (no padding in any real row)
         with torch.cuda.stream(slot["stream"]), torch.no_grad():
             for b in self.BUCKETS:
-                for dense in ((False, True) if self.DENSE_VARIANT else (False,)):
+                for dense in ((False, True) if b >= self.DENSE_FROM else (False,)):
                     run(b, dense)
                     if self.use_graphs:
                         g = torch.cuda.CUDAGraph()
@@ -674,7 +677,7 @@ class BertLarge(Model):
                 hip.batched_copy(c_src, c_dst, c_n, sh)
             if bucket > total:  # padding rows: keep them deterministic (mask 1, ids 0)
                 hip.memset_async(base + total * row, 0, (bucket - total) * row, sh)
-        dense = self.DENSE_VARIANT and self._mask_all_ones(slot, srcs[1], total)
+        dense = bucket >= self.DENSE_FROM and self._mask_all_ones(slot, srcs[1], total)
         ev[1].record(stream)
         with self.torch.cuda.stream(stream), self.torch.no_grad():
             if self.use_graphs:
