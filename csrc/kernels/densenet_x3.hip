@@ -387,7 +387,6 @@ struct X3WsParams {
   X3Conv1x1Params c;
   int units_per_block;  // 16-pixel units per block
   int tile_rows;        // rows per tile (<= 128): a block's run split into equal tiles
-  int dbg;              // ablation (tools/x3_kbench.py): 1 = no MFMA, 2 = no z stores
 };
 
 // s_waitcnt immediates for gfx9-family (vmcnt 6 bits split [3:0]+[15:14],
@@ -406,9 +405,8 @@ __device__ __forceinline__ void ws_barrier() {
 __device__ __forceinline__ int ws_chunk(int row, int c) { return row * 64 + ((c ^ ((row >> 2) & 3)) << 4); }
 
 // kWsPF: X steps in flight in the producers' registers
-template <int kWsPF, int DBG>
+template <int kWsPF>
 __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
-  const int dbg = DBG < 0 ? wp.dbg : DBG;  // ablation flags (DBG -1 only)
   extern __shared__ __attribute__((aligned(16))) uint8_t ldsw[];
   const X3Conv1x1Params& p = wp.c;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -435,7 +433,7 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
     // K steps of a tile run in a block-rotated order: at any moment the blocks
     // then read different column offsets of their X rows (all blocks on the
     // same offset would camp on a subset of the HBM channels)
-    const int rot = (dbg & 4) ? 0 : (int)(blockIdx.x % (unsigned)nst);
+    const int rot = (int)(blockIdx.x % (unsigned)nst);
     auto kofs = [&](int ks) { ks += rot; return (ks >= nst ? ks - nst : ks) * kBK; };
     auto issue_x = [&](int q, int slot) {
       q = min(q, Q - 1);
@@ -567,27 +565,20 @@ __global__ void __launch_bounds__(512, 1) x3_conv1x1_ws_kernel(X3WsParams wp) {
     // pixel blocks wholly past the block's last row (the ragged last tile)
     // skip their MFMAs
     const int rv = min(TR, mend - (mbeg + tile * TR)) - 64 * wm;  // valid rows from this wave's first
-    if (!(dbg & 1)) {
-      if (rv > 32) {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 2; ++b) acc[a][b] = x3_32(ah[kk][a], al[kk][a], bh[kk][b], bl[kk][b], acc[a][b]);
-      } else if (rv > 0) {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int a = 0; a < 2; ++a) acc[a][0] = x3_32(ah[kk][a], al[kk][a], bh[kk][0], bl[kk][0], acc[a][0]);
-      }
-    } else {
+    if (rv > 32) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int a = 0; a < 2; ++a) acc[a][0][0] += __builtin_bit_cast(float, ah[kk][a][0] ^ al[kk][a][1] ^ bh[kk][a][2] ^ bl[kk][a][3]);
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) acc[a][b] = x3_32(ah[kk][a], al[kk][a], bh[kk][b], bl[kk][b], acc[a][b]);
+    } else if (rv > 0) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int a = 0; a < 2; ++a) acc[a][0] = x3_32(ah[kk][a], al[kk][a], bh[kk][0], bl[kk][0], acc[a][0]);
     }
-    if (ks == nst - 1 && !(dbg & 2)) {
+    if (ks == nst - 1) {
       // epilogue through this wave's 8 KB LDS slab: per 32-pixel block, the
       // bias+ReLU+split 64-channel rows land as [32 px][64 ch] hi and lo
       // (16-B chunks XOR-swizzled by pixel), then leave as 16-B-per-lane
@@ -650,7 +641,6 @@ struct X3Conv3x3Params {
   float* y;              // [M][ldy] fp32, offset to the layer's 32-channel slice
   int ldy, M, H, W;
   int tiles, tiles_per_block;
-  int dbg;  // v2 ablation (TCAMD_X3_K9_DBG): 1 no MFMA, 2 no partial exchange, 4 no operand reads
   // PART kernels: the band comes from the preceding 1x1's split-K partials
   // [splits][M][128] fp32 (z = relu(sum + bias), split hi/lo while staged)
   const float* part;
@@ -698,15 +688,13 @@ constexpr int kRowB = 2 * kC3 * 2;          // 512 B per ring row
 constexpr int kScrSlot = 32 * 8;            // floats per (group, ph, source) slot: 32 px x 8 channels
 constexpr int kLdsV2 = (kRing + 1) * kRowB + 4 * 2 * 3 * kScrSlot * 4;  // 131,584 + 24,576 B
 
-// DBG: 0 = production; -1 = ablation flags read from p.dbg (tools/gpu_x3_k9abl.sh).
 // PART: small-M layers (bs1/bs8 at 14x14 and below, bs1 everywhere) whose
 // 1x1 ran split-K: the band is summed from the fp32 partials, bias+ReLU'd
 // and split while it is staged, which replaces the split-K reduce launch
 // (one ~5 us launch per such layer, 28% of a bs1 forward).  Those layers have
 // one or two tiles per block, so the synchronous staging costs no overlap.
-template <int DBG, bool PART = false>
+template <bool PART = false>
 __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p) {
-  const int dbg = DBG < 0 ? p.dbg : DBG;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds2[];
   float* scr = reinterpret_cast<float*>(lds2 + (kRing + 1) * kRowB);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -832,11 +820,6 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p
       const int row = ok ? ((base + dy * W + dx) & (kRing - 1)) : kRing;
       const uint8_t* rp = lds2 + row * kRowB;
       const int sw = row & 15;
-      if (dbg & 4) {
-#pragma unroll
-        for (int kc = 0; kc < 2; ++kc) bq[slot][kc][0] = bq[slot][kc][1] = v4u{(uint32_t)row, 0u, 1u, 2u};
-        return;
-      }
 #pragma unroll
       for (int kc = 0; kc < 2; ++kc) {
         const uint8_t* q = rp + (((4 * kq + 2 * kc + h) ^ sw) << 4);
@@ -852,17 +835,8 @@ __global__ void __launch_bounds__(512, 1) x3_conv3x3_v2_kernel(X3Conv3x3Params p
       // registers), and each read's LDS latency hides behind a tap of MFMAs
       if (t + 1 < kTaps) rd(t + 1, (t + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);
-      if (dbg & 1) {
 #pragma unroll
-        for (int kc = 0; kc < 2; ++kc) acc[kc] += __builtin_bit_cast(float, bq[t & 1][kc][0][0] ^ bq[t & 1][kc][1][1]);
-      } else {
-#pragma unroll
-        for (int kc = 0; kc < 2; ++kc) acc = x3_32(wh[t][kc], wl[t][kc], bq[t & 1][kc][0], bq[t & 1][kc][1], acc);
-      }
-    }
-    if (dbg & 2) {
-      if (in) *reinterpret_cast<f32x4*>(p.y + (size_t)m * p.ldy + 8 * kq + 4 * h) = f32x4{acc[0], acc[1], acc[2], acc[3]};
-      continue;
+      for (int kc = 0; kc < 2; ++kc) acc = x3_32(wh[t][kc], wl[t][kc], bq[t & 1][kc][0], bq[t & 1][kc][1], acc);
     }
     // C layout (32x32): lane col = pixel, reg 4g+e -> channel 8g + 4h + e.
     // scratch slot (group g, ph, source kq != g) at index (g*2 + ph)*3 + (kq - g + 3) % 4
@@ -968,9 +942,6 @@ struct X3FusedParams {
   int ldx, K, ldy, M, H, W;
   int tiles, tiles_per_block;
   uint32_t mag_hw, mag_w;
-  int dbg;                 // ablation (TCAMD_X3F_DBG): v1 1 no 3x3 phase, 2 no tile-loop 1x1 chunks;
-                           // (STAMP builds of the removed 4-wave v2 also took 4 no W1 loads, 8 no X loads, 16 no conversion)
-  unsigned long long* stamps;  // STAMP builds: per block [8] phase cycle sums (wave 0)
 };
 
 // NST = K / 32 (2..7): the k loop of a chunk is straight-line code, so the
@@ -979,22 +950,8 @@ struct X3FusedParams {
 // (A stagger of the two waves of each SIMD in the 1x1 chunk -- waves 4-7
 // running a step's MFMAs before converting the next X step -- measured 5-20%
 // slower at 56x56 and 28x28 in round 4 and was dropped.)
-template <int NST, bool STAMP = false>
+template <int NST>
 __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p) {
-  // STAMP (diagnostic builds, TCAMD_X3F_STAMP=1): shader-clock cycles per
-  // phase, summed over the block's tiles by wave 0: [0] prologue, [1] B0 wait,
-  // [2] 3x3 reads+MFMA, [3] exchange (B1 + owner adds), [4] 1x1 chunks,
-  // [5] tiles, [6] total
-  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long st_t = STAMP ? __builtin_amdgcn_s_memtime() : 0;
-  const unsigned long long st_t0 = st_t;
-  auto stamp = [&](int i) {
-    if constexpr (STAMP) {
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      st_acc[i] += t - st_t;
-      st_t = t;
-    }
-  };
   extern __shared__ __attribute__((aligned(16))) uint8_t ldsf[];
   uint8_t* const ring = ldsf;
   float* const scr = reinterpret_cast<float*>(ldsf + kRingRowsF * kRowF1);
@@ -1145,23 +1102,21 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
       z_chunk(g0, min(64, b1 - g0));
     }
   }
-  stamp(0);
 
   const int c4 = lane >> 4;
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int m0 = tile * kT2;
     __syncthreads();  // B0: the ring holds band(tile); the scratch is free
-    stamp(1);
     // this iteration's chunk: its first X steps and W(0) go out now and land
     // while the 3x3 runs (issued and consumed in one tile iteration: a load
     // carried round the loop is one the compiler's waits cannot follow)
-    if (tile + 1 < t_end && !(p.dbg & 2)) {
+    if (tile + 1 < t_end) {
       prime(m0 + kT2 + W + 1);
       wload(0, 0);
     }
 
     // ---- 3x3 phase ----
-    if (!(p.dbg & 1)) {
+    {
     // Per pixel group pg (16 consecutive pixels; the host requires W >= 16,
     // so +16 pixels wraps an image row at most once) and tap
     // row dy: the band row R[pg][dy] (logical 0..191), or the zero rows for
@@ -1226,7 +1181,6 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
       const int t = step >> 2, pg = step & 3;
       acc[pg] = x3_16(w2h[t], w2l[t], bq[step % (kLead + 1)][0], bq[step % (kLead + 1)][1], acc[pg]);
     }
-    stamp(2);
     // C (16x16): lane (lane&15) = pixel of group pg, reg e -> channel 16oh + 4c + e,
     // c = lane>>4; owner of channels 16oh + 4c .. +4 is wave (kq = c, oh), whose
     // lanes 16c .. 16c+15 hold their own share and add the other three
@@ -1243,12 +1197,11 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
       for (int pg = 0; pg < 4; ++pg) *reinterpret_cast<f32x4*>(yw + pg * 64) = acc[pg];
     }
     }
-    stamp(3);
 
     // ---- 1x1 phase: the 64 rows band(tile+1) adds; its first barrier
     // publishes the partials (no exchange barrier of its own), its last one
     // makes them readable by the owners below ----
-    if (tile + 1 < t_end && !(p.dbg & 2)) {
+    if (tile + 1 < t_end) {
       const int g0 = m0 + kT2 + W + 1;
       z_chunk(g0, kT2);
     } else {
@@ -1256,7 +1209,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
     }
     // owners: own share + the three partials -> y (the stores are issued
     // after the chunk's last W1 / X wait and long retired by the next one)
-    if (!(p.dbg & 1) && c4 == kq) {
+    if (c4 == kq) {
       const float* sr = scr + (oh * 4 + kq) * 3 * 256 + (lane & 15) * 4;
       const float* yr = ysum + (oh * 4 + kq) * 256 + (lane & 15) * 4;
 #pragma unroll
@@ -1267,18 +1220,6 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
         const int m = m0 + 16 * pg + (lane & 15);
         if (m < p.M) *reinterpret_cast<f32x4*>(p.y + (size_t)m * p.ldy + 16 * oh + 4 * kq) = v;
       }
-    }
-    stamp(4);
-  }
-  if constexpr (STAMP) {
-    st_acc[5] = t_end - t_begin;
-    st_acc[6] = __builtin_amdgcn_s_memtime() - st_t0;
-    if (wave == 0 && lane < 8) {
-      unsigned long long v = st_acc[0];
-#pragma unroll
-      for (int i = 1; i < 8; ++i)
-        if (lane == i) v = st_acc[i];
-      p.stamps[blockIdx.x * 8 + lane] = v;
     }
   }
   // the last chunk's clamped tail DMAs (and, ablated, a primed chunk) must
@@ -1314,19 +1255,8 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused_kernel(X3FusedParams p)
 constexpr int kLdsF3 = kLdsF + 128 * 4;
 static_assert(kLdsF3 <= 160 * 1024, "K11x v3 LDS budget");
 
-template <int NST, bool STAMP = false>
+template <int NST>
 __global__ void __launch_bounds__(512, 1) x3_dense_fused3_kernel(X3FusedParams p) {
-  // STAMP: [0] prologue, [1] interleaved tiles, [2] last tile, [5] tiles, [6] total (wave 0's cycles)
-  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long st_t = STAMP ? __builtin_amdgcn_s_memtime() : 0;
-  const unsigned long long st_t0 = st_t;
-  auto stamp = [&](int i) {
-    if constexpr (STAMP) {
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      st_acc[i] += t - st_t;
-      st_t = t;
-    }
-  };
   extern __shared__ __attribute__((aligned(16))) uint8_t ldsf[];
   uint8_t* const ring = ldsf;
   float* const scr = reinterpret_cast<float*>(ldsf + kRingRowsF * kRowF1);
@@ -1334,20 +1264,7 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused3_kernel(X3FusedParams p
   float* const bn = reinterpret_cast<float*>(cvt + 4 * kCvtF);   // s1 [kMaxKF] | t1 [kMaxKF]
   float* const ysum = bn + 2 * kMaxKF;                            // [oh][owner][pg][16 px][4]
   float* const bias = ysum + kYsF;                                // b1 [128]
-  // STAMP timeline (block 0, tiles t_begin+2 and +3): per wave and barrier of
-  // the tile, the shader clock on arrival and on release -> stamps[4096 + ...]
-  int tl_tile = -1;
-  auto tl = [&](int k, int what) {
-    if constexpr (STAMP) {
-      if (blockIdx.x == 0 && tl_tile >= 0 && tl_tile < 2 && (threadIdx.x & 63) == 0)
-        p.stamps[4096 + ((threadIdx.x >> 6) * 2 + tl_tile) * 64 + 2 * k + what] = __builtin_amdgcn_s_memtime();
-    }
-  };
-  auto bar = [&](int k) {
-    tl(k, 0);
-    __syncthreads();
-    tl(k, 1);
-  };
+  auto bar = [](int) { __syncthreads(); };  // argument: the barrier's index within a tile
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int W = p.W, HW = p.H * p.W;
 
@@ -1506,7 +1423,6 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused3_kernel(X3FusedParams p
     else xload(0, xptr(g + 64), 0);
   }
   __syncthreads();  // B: ring = band(t_begin), stage 0 ready
-  stamp(0);
 
   // 3x3 row bases of a tile (see v1)
   int R[4][3];
@@ -1586,7 +1502,6 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused3_kernel(X3FusedParams p
 
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int m0 = tile * kT2;
-    if constexpr (STAMP) tl_tile = tile - t_begin - 2;
     rows3(m0);
 #pragma unroll
     for (int pg = 0; pg < 4; ++pg) acc3[pg] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1632,7 +1547,6 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused3_kernel(X3FusedParams p
       if (PF < nst) xload(0, xn, PF);
       else xload(0, xptr(g + 128), 0);
       bar(nst);  // B: ring = band(t+1), stage 0 ready
-      stamp(1);
     } else {
       // last tile of the block: 3x3 only (v1's phase)
       if (tile > t_begin) owner_sums(m0 - kT2);
@@ -1644,18 +1558,6 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused3_kernel(X3FusedParams p
       partials();
       __syncthreads();
       owner_sums(m0);
-      stamp(2);
-    }
-  }
-  if constexpr (STAMP) {
-    st_acc[5] = t_end - t_begin;
-    st_acc[6] = __builtin_amdgcn_s_memtime() - st_t0;
-    if (wave == 0 && lane < 8) {
-      unsigned long long v = st_acc[0];
-#pragma unroll
-      for (int i = 1; i < 8; ++i)
-        if (lane == i) v = st_acc[i];
-      p.stamps[blockIdx.x * 8 + lane] = v;
     }
   }
   // the clamped X prefetches of chunks past the block's last tile are still
@@ -1707,8 +1609,6 @@ struct X3SmallParams {
   const uint16_t* w2_lo;
   float* y;               // [pixels][ldy] fp32, offset to the layer's 32-channel slice
   int ldx, K, ldy, imgs;
-  int dbg;                // 1 = no 3x3 phase (timing ablation), 64 = step timeline (block 0)
-  unsigned long long* stamps;  // TCAMD_X3_SMALLF_STAMP: per block [8] s_memrealtime (100 MHz) marks
 };
 
 // Tile geometry of T tiles per W x W image: tile t owns output rows
@@ -1754,25 +1654,12 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
   const int g8 = blockIdx.x / (8 * T), rr = blockIdx.x % (8 * T);
   const int tile = rr >> 3, img = 8 * g8 + (rr & 7);
   if (img >= p.imgs) return;  // block-uniform, before any barrier
-  // diagnostic marks (wave 0): [0] entry [1] after B0 [2] 1x1 done [3] z
-  // handover [4] z complete [5] 3x3 MFMAs done [6] partials summed [7] exit
-  unsigned long long mk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  auto mark = [&](int i) {
-    if (p.stamps) mk[i] = __builtin_amdgcn_s_memrealtime();
-  };
-  mark(0);
   const int r0 = tile * W / T, r1 = (tile + 1) * W / T;
   const int zr0 = max(r0 - 1, 0), zr1 = min(r1 + 1, W);
   const int TR = (zr1 - zr0) * W;  // z rows of the tile
   const int mz0 = img * W * W + zr0 * W;
   const int nst = p.K / kBK;
   const int Q = nst;  // K steps = barrier rounds of both roles (no padding to a multiple of PF)
-  // timeline diagnostic (dbg 64, block 0): shader-clock time of producer wave
-  // 4 and consumer wave 0 reaching each step barrier, kept in LDS past the
-  // stages (no memory op inside the counted-wait loop)
-  const bool tl = (p.dbg & 64) && blockIdx.x == 0;
-  unsigned long long* const tls = reinterpret_cast<unsigned long long*>(ldss + kSmS * kWsStage);
-  const unsigned long long tl0 = __builtin_amdgcn_s_memtime();
   // consumer wave = 32-channel quarter of the 1x1 output x every 32-pixel
   // block: each W1 fragment is loaded by one wave only, for twice the X
   // operand reads, which go to LDS (256 B/clk) instead of the vector-memory path
@@ -1838,17 +1725,10 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
         const int slot = (u + 1) % PF;
         __builtin_amdgcn_s_waitcnt(ws_vmcnt(kOps * (PF - 1)));  // X of step q+1
         __builtin_amdgcn_sched_barrier(0);
-        if (tl && wave == 4 && lane == 0 && q < 32) tls[4 * q] = __builtin_amdgcn_s_memtime();
         write_x(q + 1, slot);
-        if (tl && wave == 4 && lane == 0 && q < 32) {
-          __builtin_amdgcn_s_waitcnt(0xc07f);  // the conversion's LDS writes done
-          tls[4 * q + 1] = __builtin_amdgcn_s_memtime();
-        }
         __builtin_amdgcn_sched_barrier(0);
         issue_x(q + 1 + PF, slot);
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this step's stage writes
-        if (tl && wave == 4 && lane == 0 && q < 32)  // producer wave 4 at the barrier (LDS, no vm op)
-          tls[4 * q + 2] = __builtin_amdgcn_s_memtime();
         ws_barrier();  // B(q+1)
       }
     }
@@ -1896,9 +1776,6 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
         for (int b = 0; b < kNB; ++b)
           if (32 * b < TR) acc[b] = x3_32(A.h[kk], A.l[kk], B.h[kk][b], B.l[kk][b], acc[b]);
     };
-    auto stamp_c = [&](int q) {
-      if (tl && wave == 0 && lane == 0 && q < 32) tls[4 * q + 3] = __builtin_amdgcn_s_memtime();
-    };
     // W of step q is loaded during step q-1 (two register sets, the loop
     // unrolled by 2 so each has a fixed name); the step's counted wait leaves
     // the next step's 4 fragment loads in flight.  The prefetch is
@@ -1915,7 +1792,6 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
     ld_a(0, fa);  // lands during the producers' prologue
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the copy is in LDS
     ws_barrier();  // B0
-    mark(1);
     auto step = [&](int q, const AOps& cur, AOps& nxt) {
       ld_a(q + 1, nxt);
       if (q < Q) {
@@ -1925,7 +1801,6 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
         mma(cur, B);
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-      stamp_c(q);
       ws_barrier();  // B(q+1)
     };
     for (int q = 0; q < Q; q += 2) {
@@ -1934,7 +1809,6 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
       step(q + 1, fb, fa);
     }
   }
-  mark(2);
   // BN2 bias of this consumer lane's channels, loaded BEFORE the 3x3
   // weights: a later load would make its wait drain the weight loads too
   f32x4 ob[4];
@@ -1956,7 +1830,6 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_waitcnt(ws_vmcnt_lgkm0(2 * kTaps));
   ws_barrier();
-  mark(3);
   // zero the padding of the tile image (columns 0 and W+1, rows outside the image)
   for (int i = tid; i < kNPad * 32; i += 512) {
     const int pos = i >> 5, piece = i & 31;
@@ -1992,8 +1865,6 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
 
   // ---- 3x3 phase: 8 waves = input-channel quarter kq x output half oh ----
   __syncthreads();  // z and its padding complete
-  mark(4);
-  if (p.dbg & 1) return;
   const int nout = (r1 - r0) * W;  // this tile's outputs (the last tile may have fewer rows)
   int base[kNPG];
 #pragma unroll
@@ -2030,7 +1901,6 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
   // C (16x16): lane (lane&15) = pixel of group pg, reg e -> channel 16oh + 4c + e
   // (c = lane>>4); wave (kq = c, oh) owns those 4 channels and adds the other
   // three waves' partials
-  mark(5);
   float* scr = reinterpret_cast<float*>(ldss + kNPad * kRowB);
   const int c4 = lane >> 4;
   constexpr int kSlot = kNPG * 64;
@@ -2050,23 +1920,6 @@ __device__ __forceinline__ void x3_small_body(const X3SmallParams& p) {
       for (int src = 0; src < 3; ++src) v += *reinterpret_cast<const f32x4*>(sr + src * kSlot + pg * 64);
       const int o = 16 * pg + (lane & 15);
       if (o < nout) *reinterpret_cast<f32x4*>(p.y + (size_t)(m0 + o) * p.ldy + 16 * oh + 4 * kq) = v;
-    }
-  }
-  mark(6);
-  if (tl && p.stamps) {
-    __syncthreads();
-    // [16384 + 4q + e]: cycles since kernel entry of: e 0 producer past its X
-    // wait, 1 producer after the conversion, 2 producer at the barrier, 3 consumer at the barrier
-    if (tid < 128) p.stamps[16384 + tid] = tls[tid] > tl0 ? tls[tid] - tl0 : 0;
-  }
-  if (p.stamps && wave == 0) {
-    mark(7);
-    if (lane < 8) {
-      unsigned long long v = mk[0];
-#pragma unroll
-      for (int i = 1; i < 8; ++i)
-        if (lane == i) v = mk[i];
-      p.stamps[blockIdx.x * 8 + lane] = v;  // a vector store (lane-indexed)
     }
   }
 }
@@ -2425,27 +2278,21 @@ static int x3_conv3x3_launch(const void* z_hi, const void* z_lo, const float* pa
   static std::atomic<bool> attr_set[kMaxDevices];
   const int dev_slot = device_slot();
   if (!attr_set[dev_slot].load(std::memory_order_acquire)) {
-    hipError_t e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<0>,
+    hipError_t e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsV2);
     if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<-1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kLdsV2);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      e = hipFuncSetAttribute((const void*)x3_conv3x3_v2_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               kLdsV2);
     if (e != hipSuccess) return e;
     attr_set[dev_slot].store(true, std::memory_order_release);
   }
-  p.dbg = (int)tcamd::knob(tcamd::Knob::X3K9Dbg);
   p.tiles = (p.M + kT2 - 1) / kT2;
   const int grid = std::min(p.tiles, 256);
   p.tiles_per_block = (p.tiles + grid - 1) / grid;
   const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
   if (part)
-    hipLaunchKernelGGL((x3_conv3x3_v2_kernel<0, true>), dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
-  else if (p.dbg)
-    hipLaunchKernelGGL(x3_conv3x3_v2_kernel<-1>, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
-  else hipLaunchKernelGGL(x3_conv3x3_v2_kernel<0>, dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
+    hipLaunchKernelGGL((x3_conv3x3_v2_kernel<true>), dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
+  else hipLaunchKernelGGL((x3_conv3x3_v2_kernel<false>), dim3(blocks), dim3(512), kLdsV2, (hipStream_t)stream, p);
   return hipGetLastError();
 }
 
@@ -2529,15 +2376,14 @@ static int x3_conv1x1_impl(const float* x, int ldx, int M, int K, int N, const f
       hipError_t e = hipGetDevice(&dev);
       if (e == hipSuccess) e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
       if (e == hipSuccess && n <= 0) e = hipErrorInvalidDevice;
-      for (const void* f : {(const void*)x3_conv1x1_ws_kernel<3, 0>, (const void*)x3_conv1x1_ws_kernel<3, -1>})
-        if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsWs);
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)x3_conv1x1_ws_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsWs);
       if (e != hipSuccess) return e;
       ncu = n;
       ncu_dev[dev_slot].store(ncu, std::memory_order_release);
     }
     X3WsParams wp;
     wp.c = p;
-    wp.dbg = (int)tcamd::knob(tcamd::Knob::X3WsDbg);
     const int units = (M + 15) / 16;
     wp.units_per_block = (units + ncu - 1) / ncu;
     // equal tiles: 392 rows -> 4 x 98 instead of 3 x 128 + 8 (every tile
@@ -2546,8 +2392,7 @@ static int x3_conv1x1_impl(const float* x, int ldx, int M, int K, int N, const f
     const int nt = (rpb + 127) / 128;
     wp.tile_rows = (rpb + nt - 1) / nt;
     const int blocks = (units + wp.units_per_block - 1) / wp.units_per_block;
-    if (wp.dbg) hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, -1>), dim3(blocks), dim3(512), kLdsWs, s, wp);
-    else hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3, 0>), dim3(blocks), dim3(512), kLdsWs, s, wp);
+    hipLaunchKernelGGL((x3_conv1x1_ws_kernel<3>), dim3(blocks), dim3(512), kLdsWs, s, wp);
     return hipGetLastError();
   }
   const int mb = (M + pl.bm - 1) / pl.bm, ntl = N / kBN;
@@ -2599,20 +2444,6 @@ int tcamd_x3_dense_layer(const float* x, int ldx, int imgs, int H, int W, int K,
 
 static int cu_count();
 
-static unsigned long long* g_x3f_stamps = nullptr;  // TCAMD_X3F_STAMP diagnostic builds
-static int g_x3f_stamp_blocks = 0;
-
-// Copies the last stamped K11x launch's per-block phase cycles ([blocks][8])
-// into out (host, n entries); returns the block count.
-int tcamd_x3_fused_stamps(unsigned long long* out, int n) {
-  if (!g_x3f_stamps || !out) return 0;
-  const int m = std::min(n, 8 * 1024);  // per-block sums [0, 8 x blocks) + the v3 timeline [4096, 5120)
-  if (hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpy(out, g_x3f_stamps, m * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
-    return -1;
-  return g_x3f_stamp_blocks;
-}
-
 // K11x: the whole dense layer in one kernel (z stays in LDS).  v 1: the
 // 8-wave kernel; v 3: v1 with the next chunk's 1x1 interleaved into each
 // tile's 3x3.  w1 in x3_w1_fragments, w2 in x3_w3f_fragments; 16 <= W <= 56,
@@ -2648,47 +2479,33 @@ static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, 
   p.mag_w = (uint32_t)((0x100000000ull + W - 1) / (uint64_t)W);
   // NST 2..15 (K 64..480; the BN1 affine table in LDS holds K <= 480).  v1
   // at NST 15 spills 12 B per lane; measured per K before the engine uses it
-#define X3F_ROW(KERN, ...)                                                                                   \
-  {(const void*)KERN<2, __VA_ARGS__>,  (const void*)KERN<3, __VA_ARGS__>,  (const void*)KERN<4, __VA_ARGS__>,  \
-   (const void*)KERN<5, __VA_ARGS__>,  (const void*)KERN<6, __VA_ARGS__>,  (const void*)KERN<7, __VA_ARGS__>,  \
-   (const void*)KERN<8, __VA_ARGS__>,  (const void*)KERN<9, __VA_ARGS__>,  (const void*)KERN<10, __VA_ARGS__>, \
-   (const void*)KERN<11, __VA_ARGS__>, (const void*)KERN<12, __VA_ARGS__>, (const void*)KERN<13, __VA_ARGS__>, \
-   (const void*)KERN<14, __VA_ARGS__>, (const void*)KERN<15, __VA_ARGS__>}
-  // [version 1 / 3][0 plain / 1 stamped][NST - 2]
-  static const void* const kFns[2][2][14] = {
-      {X3F_ROW(x3_dense_fused_kernel, false), X3F_ROW(x3_dense_fused_kernel, true)},
-      {X3F_ROW(x3_dense_fused3_kernel, false), X3F_ROW(x3_dense_fused3_kernel, true)}};
+#define X3F_ROW(KERN)                                                                                  \
+  {(const void*)KERN<2>,  (const void*)KERN<3>,  (const void*)KERN<4>,  (const void*)KERN<5>,  (const void*)KERN<6>, \
+   (const void*)KERN<7>,  (const void*)KERN<8>,  (const void*)KERN<9>,  (const void*)KERN<10>, (const void*)KERN<11>, \
+   (const void*)KERN<12>, (const void*)KERN<13>, (const void*)KERN<14>, (const void*)KERN<15>}
+  // [version 1 / 3][NST - 2]
+  static const void* const kFns[2][14] = {X3F_ROW(x3_dense_fused_kernel), X3F_ROW(x3_dense_fused3_kernel)};
 #undef X3F_ROW
   const int nst = K / 32;
   if (nst < 2 || nst > 15 || (v != 1 && v != 3)) return hipErrorInvalidValue;
-  const bool stamp = tcamd::knob(tcamd::Knob::X3fStamp) != 0;
-  p.stamps = nullptr;
-  if (stamp) {
-    if (!g_x3f_stamps && hipMalloc((void**)&g_x3f_stamps, 8 * 1024 * sizeof(unsigned long long)) != hipSuccess)
-      return hipErrorOutOfMemory;
-    p.stamps = g_x3f_stamps;
-  }
   static std::atomic<bool> attr_set[kMaxDevices];
   const int dev_slot = device_slot();
   if (!attr_set[dev_slot].load(std::memory_order_acquire)) {
-    for (const auto& byv : kFns)
-      for (const auto& fs : byv)
-        for (const void* f : fs) {
-          const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsF3);
-          if (e != hipSuccess) return e;
-        }
+    for (const auto& fs : kFns)
+      for (const void* f : fs) {
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsF3);
+        if (e != hipSuccess) return e;
+      }
     attr_set[dev_slot].store(true, std::memory_order_release);
   }
-  p.dbg = (int)tcamd::knob(tcamd::Knob::X3fDbg);
   p.tiles = (p.M + kT2 - 1) / kT2;
   const int grid = std::min(p.tiles, cu_count());
   p.tiles_per_block = (p.tiles + grid - 1) / grid;
   const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
   void* args[] = {&p};
-  const hipError_t e = hipLaunchKernel(kFns[v == 3][stamp ? 1 : 0][nst - 2], dim3(blocks), dim3(512), args,
+  const hipError_t e = hipLaunchKernel(kFns[v == 3][nst - 2], dim3(blocks), dim3(512), args,
                                        v == 3 ? kLdsF3 : kLdsF, (hipStream_t)stream);
   if (e != hipSuccess) return e;
-  g_x3f_stamp_blocks = blocks;
   return hipGetLastError();
 }
 
@@ -2706,33 +2523,6 @@ int tcamd_x3_dense_fused3(const float* x, int ldx, int imgs, int H, int W, int K
   return x3_dense_fused_impl(3, x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream);
 }
 
-
-static unsigned long long* g_x3s_stamps = nullptr;  // TCAMD_X3_SMALLF_STAMP builds
-static int g_x3s_stamp_blocks = 0;
-
-// Copies the last K14x launch's step timeline (TCAMD_X3_SMALLF_STAMP=1 and
-// TCAMD_X3_SMALLF_DBG & 64): [4q + e] shader-clock cycles since block 0's
-// entry: producer wave 4 past its X wait (e 0), after the conversion (1), at
-// the barrier after K step q (2); consumer wave 0 at that barrier (3).
-int tcamd_x3_small_timeline(unsigned long long* out, int n) {
-  if (!g_x3s_stamps || !out) return 0;
-  const int m = std::min(n, 128);
-  if (hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpy(out, g_x3s_stamps + 16384, m * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
-    return -1;
-  return m;
-}
-
-// Copies the last stamped K14x launch's per-block marks ([blocks][8],
-// s_memrealtime ticks of 10 ns; blocks past the image count stay 0).
-int tcamd_x3_small_stamps(unsigned long long* out, int n) {
-  if (!g_x3s_stamps || !out) return 0;
-  const int m = std::min(n, 8 * g_x3s_stamp_blocks);
-  if (hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpy(out, g_x3s_stamps, m * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
-    return -1;
-  return g_x3s_stamp_blocks;
-}
 
 static int cu_count();
 
@@ -2786,21 +2576,13 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
   p.K = K;
   p.ldy = ldy;
   p.imgs = imgs;
-  p.dbg = (int)tcamd::knob(tcamd::Knob::X3SmallfDbg);
-  const bool stamp = tcamd::knob(tcamd::Knob::X3SmallfStamp) != 0;
-  p.stamps = nullptr;
-  if (stamp) {
-    if (!g_x3s_stamps && hipMalloc((void**)&g_x3s_stamps, 8 * 4096 * sizeof(unsigned long long)) != hipSuccess)
-      return hipErrorOutOfMemory;
-    p.stamps = g_x3s_stamps;
-  }
   // [14x14 / 7x7][1 / 2 / 4 / 7 tiles per image]
   const void* const fns[2][4] = {
       {nullptr, (const void*)x3_dense_small_kernel<14, 2>, (const void*)x3_dense_small_kernel<14, 4>,
        (const void*)x3_dense_small_kernel<14, 7>},
       {(const void*)x3_dense_small_kernel<7, 1>, (const void*)x3_dense_small_kernel<7, 2>,
        (const void*)x3_dense_small_kernel<7, 4>, (const void*)x3_dense_small_kernel<7, 7>}};
-  constexpr int kLds = 4 * kWsStage + 1024;  // 4 K-step stages + the dbg-64 timeline
+  constexpr int kLds = 4 * kWsStage;  // 4 K-step stages
   static std::atomic<bool> attr_set[kMaxDevices];
   const int dev_slot = device_slot();
   if (!attr_set[dev_slot].load(std::memory_order_acquire)) {
@@ -2813,8 +2595,6 @@ int tcamd_x3_dense_small(const float* x, int ldx, int imgs, int H, int W, int K,
     attr_set[dev_slot].store(true, std::memory_order_release);
   }
   const int blocks = (imgs + 7) / 8 * 8 * tiles;
-  if (stamp && blocks > 4096) return hipErrorInvalidValue;
-  g_x3s_stamp_blocks = blocks;
   void* args[] = {&p};
   const hipError_t e = hipLaunchKernel(fns[W == 14 ? 0 : 1][ti], dim3(blocks), dim3(512), args, kLds,
                                        (hipStream_t)stream);

@@ -18,12 +18,6 @@ enum class Knob : int {
   X3MaxSplits,     // K8x split-K cap
   X3Ws,            // K8x warp-specialised persistent 1x1 (0 = tiled kernel only)
   X3WsMin,         // ... from this many pixels
-  X3WsDbg,         // K8x-ws timing ablation bits
-  X3K9Dbg,         // K9x timing ablation
-  X3fDbg,          // K11x timing ablation bits
-  X3fStamp,        // K11x phase-cycle stamps
-  X3SmallfDbg,     // K14x ablation (1) / step timeline (64)
-  X3SmallfStamp,   // K14x per-block marks
   X3StemBpc,       // K10x stem persistent blocks per CU
   X3sBlocks,       // K13x 1x1 target workgroups
   X3sMaxChunks,    // K13x 1x1 K-chunk cap

@@ -27,12 +27,6 @@ constexpr KnobDef kDefs[] = {
     {"TCAMD_X3_MAX_SPLITS", 4, "K8x 1x1: most K splits (bs1 0.975 ms at 4 vs 1.005 uncapped)"},
     {"TCAMD_X3_WS", 1, "K8x 1x1: warp-specialised persistent kernel for the dense-layer 1x1s (0: tiled only)"},
     {"TCAMD_X3_WS_MIN", 16384, "K8x 1x1: pixels from which the warp-specialised kernel runs"},
-    {"TCAMD_X3_WS_DBG", 0, "K8x-ws timing ablation bits (diagnostic: output is wrong while set)"},
-    {"TCAMD_X3_K9_DBG", 0, "K9x 3x3 timing ablation (diagnostic: output is wrong while set)"},
-    {"TCAMD_X3F_DBG", 0, "K11x timing ablation: 1 no 3x3 phase, 2 no tile-loop 1x1 (diagnostic)"},
-    {"TCAMD_X3F_STAMP", 0, "K11x: record per-block phase cycles and the v3 barrier timeline (stamped build)"},
-    {"TCAMD_X3_SMALLF_DBG", 0, "K14x: 1 no 3x3 phase (diagnostic), 64 step timeline of block 0"},
-    {"TCAMD_X3_SMALLF_STAMP", 0, "K14x: record per-block s_memrealtime marks"},
     {"TCAMD_X3_STEM_BPC", 2, "K10x stem: persistent workgroups per CU"},
     {"TCAMD_X3S_BLOCKS", 384, "K13x small-M 1x1: target workgroups (sets the K chunking)"},
     {"TCAMD_X3S_MAX_CHUNKS", 8, "K13x small-M 1x1: most K chunks (float atomics sum them)"},

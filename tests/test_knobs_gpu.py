@@ -141,69 +141,6 @@ def test_k8x_plan_knobs(hip, M, K):
         assert sizes[(("TCAMD_X3_MAX_SPLITS", 1),)] == 0
 
 
-def test_ablation_knobs_run_and_reset(hip):
-    """The timing ablations (diagnostic: they skip work, the output is wrong
-    while set) launch without a fault, and the next default launch is right."""
-    d = _layer(50000, 224, seed=1)
-    for v in (1, 2, 4):
-        with hip.knob(TCAMD_X3_WS_DBG=v):
-            _conv1x1(hip, d)
-    assert _rel(_conv1x1(hip, d)[0], _z_ref(d)) < 3e-5
-    for v in (1, 2, 4):
-        with hip.knob(TCAMD_X3_K9_DBG=v):
-            _conv3x3(hip, 24, 28, seed=2)
-    y, ref = _conv3x3(hip, 24, 28, seed=2)
-    assert _rel(y, ref) < 2e-5
-    d = _layer(16 * 28 * 28, 128, seed=3)
-    for v in (1, 2, 3):
-        for ver in (1, 3):
-            with hip.knob(TCAMD_X3F_DBG=v):
-                _fused(hip, d, 16, 28, ver)
-    ref = _layer_ref(d, 16, 28)
-    assert _rel(_fused(hip, d, 16, 28, 1), ref) < 3e-5 and _rel(_fused(hip, d, 16, 28, 3), ref) < 3e-5
-    d = _layer(16 * 14 * 14, 256, seed=4)
-    with hip.knob(TCAMD_X3_SMALLF_DBG=1):
-        _small(hip, d, 16, 14)
-    assert _rel(_small(hip, d, 16, 14), _layer_ref(d, 16, 14)) < 3e-5
-
-
-def test_k11x_stamps(hip):
-    """TCAMD_X3F_STAMP: the stamped K11x instantiations compute the same layer
-    and record per-block phase cycles (v3: plus block 0's barrier timeline)."""
-    imgs, H = 32, 56
-    d = _layer(imgs * H * H, 96, seed=5)
-    ref = _layer_ref(d, imgs, H)
-    for ver in (1, 3):
-        with hip.knob(TCAMD_X3F_STAMP=1):
-            got = _fused(hip, d, imgs, H, ver)
-            st = hip.x3_fused_stamps()
-            tl = hip.x3_fused_timeline() if ver == 3 else None
-        assert _rel(got, ref) < 3e-5
-        assert st is not None and st.shape[1] == 8 and st.shape[0] >= 1
-        assert (st[:, 6] > 0).all(), "total cycles missing"
-        assert (st[:, 5] >= 1).all(), "tile counts missing"
-        if ver == 3:
-            assert tl is not None and (tl > 0).any()
-
-
-def test_k14x_stamps_and_timeline(hip):
-    """TCAMD_X3_SMALLF_STAMP + TCAMD_X3_SMALLF_DBG=64: per-block marks and
-    block 0's step timeline, the layer still computed exactly."""
-    imgs, H, K = 16, 14, 256
-    d = _layer(imgs * H * H, K, seed=6)
-    with hip.knob(TCAMD_X3_SMALLF_STAMP=1, TCAMD_X3_SMALLF_DBG=64):
-        got = _small(hip, d, imgs, H, tiles=4)
-        st = hip.x3_small_stamps()
-        tl = hip.x3_small_timeline()
-    assert _rel(got, _layer_ref(d, imgs, H)) < 3e-5
-    assert st.shape == ((imgs + 7) // 8 * 8 * 4, 8)
-    live = st[:imgs * 4]
-    assert (live[:, 0] > 0).all()
-    steps = K // 32
-    assert (tl[:steps, 2] > 0).all() and (tl[:steps, 3] > 0).all(), tl[:steps]
-    assert (np.diff(tl[:steps, 3]) >= 0).all(), "consumer barrier times must be ordered"
-
-
 @pytest.mark.parametrize("bpc", [1, 2, 4, 8])
 def test_stem_blocks_per_cu(hip, bpc):
     """K10x stem with TCAMD_X3_STEM_BPC persistent workgroups per CU (fewer:

@@ -80,37 +80,10 @@ def main():
                 row["v%d_rel_vs_v%d" % (v, vers[0])] = float((outs[v].double() - ref).norm() / ref.norm())
             rows.append(row)
             print(json.dumps(row), flush=True)
-    if os.environ.get("TCAMD_X3F_STAMP") and 3 in vers:
-        timeline(a, hip, vers)
     if a.json:
         with open(a.json, "w") as f:
             for r in rows:
                 f.write(json.dumps(r) + "\n")
-
-
-def timeline(a, hip, vers):
-    """Barrier timeline of the last v3 launch (block 0, two steady tiles):
-    per barrier k, the cycles from the previous release to each wave's arrival
-    (work) and from its arrival to the release (wait)."""
-    import numpy as np
-
-    tl = hip.x3_fused_timeline()
-    if tl is None:
-        return
-    tl = tl.astype(np.int64)
-    for tile in range(2):
-        rel = tl[:, tile, :, 1]
-        arr = tl[:, tile, :, 0]
-        nb = int((rel[0] > 0).sum())
-        rows = []
-        for k in range(nb):
-            prev = rel[:, k - 1] if k else None
-            work = (arr[:, k] - prev) if prev is not None else None
-            wait = rel[:, k] - arr[:, k]
-            rows.append({"barrier": k, "span": int(rel[:, k].max() - (rel[:, k - 1].max() if k else arr[:, 0].min())),
-                         "work_per_wave": None if work is None else [int(v) for v in work],
-                         "wait_per_wave": [int(v) for v in wait]})
-        print(json.dumps({"timeline_tile": tile, "barriers": rows}), flush=True)
 
 
 if __name__ == "__main__":

@@ -3,11 +3,7 @@
 against the K8x + K9x pair, per K and batch, interleaved round by round in
 one process (median of the rounds).
 
-    python tools/k14x_bench.py --hw 14,7 --imgs 64,128 --ks 256,512,992 --tiles 1,2,4 [--timeline]
-
---timeline: block 0's step timeline of the default tiling (per step: producer
-past its X wait, after the conversion, at the barrier; consumer at the
-barrier; cycles), summarised as mean cycles per step.
+    python tools/k14x_bench.py --hw 14,7 --imgs 64,128 --ks 256,512,992 --tiles 1,2,4
 """
 import argparse
 import json
@@ -37,9 +33,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--json", default="")
-    ap.add_argument("--timeline", action="store_true")
     a = ap.parse_args()
-    import numpy as np
     import torch
 
     from triton_client_amd.ops import hip
@@ -98,17 +92,6 @@ def main():
                 row = {"hw": hw, "imgs": imgs, "K": K, "default_tiles": hip.x3_small_tiles(imgs, hw)}
                 for k, v in ts.items():
                     row[k + "_us"] = round(sorted(v)[len(v) // 2], 2)
-                if a.timeline:
-                    with hip.knob(TCAMD_X3_SMALLF_STAMP=1, TCAMD_X3_SMALLF_DBG=64):
-                        k14(0)()
-                        tl = hip.x3_small_timeline()
-                    n = min(K // 32, 32)
-                    d = np.diff(tl[:n, 3].astype(np.float64))
-                    row["timeline"] = {
-                        "cycles_per_step": round(float(d.mean()), 1) if len(d) else None,
-                        "producer_wait_to_converted": round(float((tl[1:n, 1] - tl[1:n, 0]).mean()), 1),
-                        "producer_barrier_minus_consumer": round(float((tl[1:n, 2] - tl[1:n, 3]).mean()), 1),
-                        "first_step_done": int(tl[0, 3])}
                 rows.append(row)
                 print(json.dumps(row), flush=True)
     if a.json:

@@ -22,10 +22,7 @@ def main():
     ap.add_argument("--chunks", default="128,64,32,16")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--ks", default="", help="comma list of K: loop over them (overrides --k)")
-    ap.add_argument("--fused-dbg", default="", help="comma list of K11x ablation masks (TCAMD_X3F_DBG) to time")
-    ap.add_argument("--stamp", action="store_true", help="also run a TCAMD_X3F_STAMP=1 child (phase cycles)")
     ap.add_argument("--both", action="store_true", help="also time K11x v1 in a child (default v3)")
-    ap.add_argument("--stamp-dbg", default="", help="comma list of ablation masks to run as stamped children")
     a = ap.parse_args()
     for K in ([int(v) for v in a.ks.split(",")] if a.ks else [a.k]):
         a.k = K
@@ -97,17 +94,7 @@ def bench(a):
     torch.cuda.synchronize()
     us = 1e6 * (time.perf_counter() - t0) / a.iters
     print("hw=%d k=%d fused v%d: %.1f us per %d images" % (a.hw, K, v, us, a.imgs), flush=True)
-    st = hip.x3_fused_stamps() if os.environ.get("TCAMD_X3F_STAMP") else None
-    if st is not None:
-        tiles = st[:, 5].astype(float)
-        full = tiles == tiles.max()
-        names = ["prologue", "B0 wait", "3x3", "exchange", "1x1 chunks"]
-        per_tile = ["%s %.0f" % (nm, st[full, i].mean() / tiles[full].mean()) for i, nm in enumerate(names) if i]
-        print("  stamps (cycles, %d blocks, %d tiles/block): prologue %.0f | per tile: %s | total %.0f" % (
-            st.shape[0], tiles.max(), st[full, 0].mean(), ", ".join(per_tile), st[full, 6].mean()), flush=True)
-    runs = [("TCAMD_X3F_DBG", d) for d in a.fused_dbg.split(",") if d] + ([("TCAMD_X3F_STAMP", "1")] if a.stamp else [])
-    runs = [(v, d, {}) for v, d in runs] + [("TCAMD_X3F_DBG", d, {"TCAMD_X3F_STAMP": "1"})
-                                            for d in a.stamp_dbg.split(",") if d]
+    runs = []
     if a.both and os.environ.get("X3_PAIR_BENCH_V", "3") == "3":
         runs.append(("X3_PAIR_BENCH_V", "1", {}))
     if runs:
@@ -118,9 +105,8 @@ def bench(a):
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--hw", str(a.hw), "--k", str(K),
                                   "--imgs", str(a.imgs), "--ldx", str(a.ldx), "--chunks", "", "--iters",
                                   str(a.iters)], env=env, capture_output=True, text=True, timeout=300)
-            line = [ln for ln in out.stdout.splitlines() if "fused" in ln or "stamps" in ln]
-            print("  %s=%s%s: %s" % (var, d, " +stamp" if extra else "", " / ".join(line) if line else out.stderr[-300:]),
-                  flush=True)
+            line = [ln for ln in out.stdout.splitlines() if "fused" in ln]
+            print("  %s=%s: %s" % (var, d, " / ".join(line) if line else out.stderr[-300:]), flush=True)
 
 
 if __name__ == "__main__":

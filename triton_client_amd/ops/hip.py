@@ -224,9 +224,6 @@ _SIGS = {
         ctypes.c_int,
     ),
     "tcamd_x3_small_tiles": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
-    "tcamd_x3_fused_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
-    "tcamd_x3_small_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
-    "tcamd_x3_small_timeline": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "tcamd_x3_dense_fused3": (
         [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -805,28 +802,6 @@ def x3_small_tiles(imgs, W):
     return int(_load().tcamd_x3_small_tiles(int(imgs), int(W)))
 
 
-def x3_small_timeline():
-    """Step timeline of the last K14x launch (STAMP process with TCAMD_X3_SMALLF_DBG
-    bit 64): int64 [32][4] cycles since block 0's entry: producer wave 4 past
-    its X wait, after the conversion, at the step barrier; consumer wave 0 at
-    the step barrier (0 = not reached)."""
-    out = np.zeros(128, dtype=np.uint64)
-    n = _load().tcamd_x3_small_timeline(out.ctypes.data, out.size)
-    if n < 0:
-        raise HipError(n, "x3_small_timeline")
-    return out.reshape(32, 4).astype(np.int64)
-
-
-def x3_small_stamps(max_blocks=4096):
-    """Per-block timeline marks of the last K14x launch (TCAMD_X3_SMALLF_STAMP=1
-    processes): int64 array [blocks][8] of s_memrealtime ticks (10 ns)."""
-    out = np.zeros(8 * max_blocks, dtype=np.uint64)
-    n = _load().tcamd_x3_small_stamps(out.ctypes.data, out.size)
-    if n < 0:
-        raise HipError(n, "x3_small_stamps")
-    return out[:8 * n].reshape(n, 8).astype(np.int64)
-
-
 def x3_dense_fused3(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None):
     """K11x v3: v1's roles and fragment layouts (``w2_*`` in x3_w3f_fragments),
     with the next chunk's 1x1 K steps interleaved into each tile's 3x3."""
@@ -839,30 +814,6 @@ def x3_cat(x, out, rows, K, stream=None):
     [hi | hi | lo] (csrc/kernels/bert.hip), for one bf16 GEMM against
     [W_hi | W_lo | W_hi] that accumulates the three split products."""
     _check(_load().tcamd_x3_cat(x, out, int(rows), int(K), _vp(stream)), "x3_cat")
-
-
-def x3_fused_stamps():
-    """Per-block phase cycle sums of the last K11x launch built with
-    TCAMD_X3F_STAMP=1: a [blocks, 8] uint64 array (columns: prologue, B0 wait,
-    3x3, exchange, 1x1 chunks, tiles, total), or None."""
-    import numpy as np
-
-    buf = np.zeros(8 * 1024, dtype=np.uint64)
-    n = _load().tcamd_x3_fused_stamps(buf.ctypes.data, buf.size)
-    if n <= 0:
-        return None
-    return buf[: 8 * n].reshape(n, 8)
-
-
-def x3_fused_timeline():
-    """K11x v3 STAMP builds: block 0's barrier timeline of two steady-state
-    tiles, [wave 8][tile 2][barrier 32][arrive, release] shader-clock stamps."""
-    import numpy as np
-
-    buf = np.zeros(8 * 1024, dtype=np.uint64)
-    if _load().tcamd_x3_fused_stamps(buf.ctypes.data, buf.size) <= 0:
-        return None
-    return buf[4096:5120].reshape(8, 2, 32, 2)
 
 
 def x3_stem_fragments(w):

@@ -30,12 +30,6 @@ KNOBS = [
     Knob("TCAMD_X3_MAX_SPLITS", "native", 4, "K8x 1x1 split-K cap", "", _KN + "test_k8x_plan_knobs"),
     Knob("TCAMD_X3_WS", "native", 1, "K8x warp-specialised 1x1", "", _KN + "test_k8x_plan_knobs"),
     Knob("TCAMD_X3_WS_MIN", "native", 16384, "K8x warp-specialised 1x1", "", _KN + "test_k8x_plan_knobs"),
-    Knob("TCAMD_X3_WS_DBG", "native", 0, "K8x-ws ablation", "", _KN + "test_ablation_knobs_run_and_reset"),
-    Knob("TCAMD_X3_K9_DBG", "native", 0, "K9x ablation", "", _KN + "test_ablation_knobs_run_and_reset"),
-    Knob("TCAMD_X3F_DBG", "native", 0, "K11x ablation", "", _KN + "test_ablation_knobs_run_and_reset"),
-    Knob("TCAMD_X3F_STAMP", "native", 0, "K11x stamps", "", _KN + "test_k11x_stamps"),
-    Knob("TCAMD_X3_SMALLF_DBG", "native", 0, "K14x ablation / timeline", "", _KN + "test_k14x_stamps_and_timeline"),
-    Knob("TCAMD_X3_SMALLF_STAMP", "native", 0, "K14x stamps", "", _KN + "test_k14x_stamps_and_timeline"),
     Knob("TCAMD_X3_STEM_BPC", "native", 2, "K10x stem grid", "", _KN + "test_stem_blocks_per_cu"),
     Knob("TCAMD_X3S_BLOCKS", "native", 384, "K13x 1x1 chunking", "", _KN + "test_k13x_chunking_and_split3"),
     Knob("TCAMD_X3S_MAX_CHUNKS", "native", 8, "K13x 1x1 chunking", "", _KN + "test_k13x_chunking_and_split3"),
