@@ -1565,6 +1565,314 @@ __global__ void __launch_bounds__(512, 1) x3_dense_fused3_kernel(X3FusedParams p
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---- K11w: K11x with split roles (warp-specialised) --------------------------
+// v1 / v3 give every wave both jobs: convert X (BN1 + ReLU + hi/lo split, ~5
+// VALU per element) and run the MFMAs, so each 32-k step is a serial chain of
+// conversion, LDS write, barrier, operand read and MFMA in every wave (v1:
+// ~960 cycles per step against 384 MFMA cycles per SIMD, r3/r5 cycle budgets).
+// K11w is 12 waves:
+//   * producers (waves 8-11, one per SIMD, no accumulators): keep kPfW K steps
+//     of X in flight in registers, and stage step g+1 (BN1 from LDS, split)
+//     into one of two LDS slots while the consumers multiply step g;
+//   * consumers (waves 0-7, v1's roles): the 1x1 MFMAs of every step
+//     (accumulators, W1 fragments by buffer loads one step ahead), the
+//     epilogue z -> ring, tile t's 3x3 (weights resident) and the owner sums.
+// Both roles run the same barrier sequence: Z (tables), P0 (step 0 staged),
+// one R per global K step (the producer's slot g+1 is full, the consumers'
+// slot g is free), and per tile T (band(t) complete in the ring) plus E after
+// the last tile's 3x3.  The chunk sequence of a block: the band of its first
+// tile in 64-row chunks, then the 64 rows each later tile adds.
+// LDS: v1's ring, scratch, y sums, 2 stages and BN1 table (160,160 B).
+// 768 threads: 168 VGPRs per wave (3 waves per SIMD).
+constexpr int kLdsFW = kRingRowsF * kRowF1 + kScrF * 4 + kYsF * 4 + 4 * kCvtF + 2 * kMaxKF * 4;
+static_assert(kLdsFW <= 160 * 1024, "K11w LDS budget");
+constexpr int kPfW = 3;  // producer X steps in flight
+
+template <int NST>
+__global__ void __launch_bounds__(768, 1) x3_dense_ws_kernel(X3FusedParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t ldsfw[];
+  uint8_t* const ring = ldsfw;
+  float* const scr = reinterpret_cast<float*>(ldsfw + kRingRowsF * kRowF1);
+  float* const ysum = scr + kScrF;                                    // [oh][owner][pg][16 px][4]
+  uint8_t* const cvt = reinterpret_cast<uint8_t*>(ysum + kYsF);       // [slot 2][plane 2][64 px][64 B]
+  float* const bn = reinterpret_cast<float*>(cvt + 4 * kCvtF);        // s1 [kMaxKF] | t1 [kMaxKF]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int W = p.W, HW = p.H * p.W;
+
+  const int t_begin = blockIdx.x * p.tiles_per_block;
+  const int t_end = min(p.tiles, t_begin + p.tiles_per_block);
+  if (t_begin >= t_end) return;  // block-uniform, before any barrier
+  const int b0 = t_begin * kT2 - W - 1, b1 = t_begin * kT2 + kT2 + W + 1;
+  const int npro = (b1 - b0 + 63) >> 6;         // chunks of the first band
+  const int nch = npro + (t_end - t_begin - 1);  // + one per later tile
+  const int G = nch * NST;                       // K steps (R barriers) of the block
+  auto chunk_g0 = [&](int c) { return c < npro ? b0 + 64 * c : (t_begin + c - npro) * kT2 + kT2 + W + 1; };
+
+  for (int i = tid; i < p.K; i += 768) {
+    bn[i] = p.s1[i];
+    bn[kMaxKF + i] = p.t1[i];
+  }
+  if (tid < 3 * kRowF1 / 16) *reinterpret_cast<v4u*>(ring + kZeroF * kRowF1 + tid * 16) = v4u{0, 0, 0, 0};
+  __syncthreads();  // Z
+
+  if (wave >= 8) {
+    // ------------------------------ producers ------------------------------
+    // thread = pixel px of the step x 8-k chunk cj: two float4 of X per step,
+    // one 16-B hi and one 16-B lo write (v1's stage layout: chunk c of pixel
+    // px at slot c ^ ((px >> 2) & 3))
+    const int pt = tid - 512;
+    const int px = pt >> 2, cj = pt & 3;
+    const int wo = px * 64 + ((cj ^ ((px >> 2) & 3)) << 4);
+    f32x4 xr[kPfW][2];
+    auto issue = [&](int s, int slot) {
+      s = min(s, G - 1);  // past the end: re-load the last step (static vmcnt)
+      const int c = s / NST, st = s - c * NST;
+      const int m = min(max(chunk_g0(c) + px, 0), p.M - 1);
+      const float* src = p.x + (size_t)m * p.ldx + st * 32 + 8 * cj;
+      // inline-asm loads: hipcc's own wait before a use of a register loaded
+      // across the round loop's back edge is a vmcnt(0), which drains the
+      // prefetch once per kPfW rounds; the counted s_waitcnt below covers them
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(xr[slot][0]) : "v"(src) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(xr[slot][1]) : "v"(src) : "memory");
+    };
+    // BN1 affine of the next step to convert, read from LDS one round ahead
+    // (off the convert -> stage write -> barrier chain)
+    f32x4 nb[4];
+    auto ldbn = [&](int s) {
+      const float* bs = bn + (s % NST) * 32 + 8 * cj;
+      nb[0] = ldf4(bs);
+      nb[1] = ldf4(bs + kMaxKF);
+      nb[2] = ldf4(bs + 4);
+      nb[3] = ldf4(bs + kMaxKF + 4);
+    };
+    auto convert = [&](int s, int slot) {
+      v2u h0, l0, h1, l1;
+      split4(bn_relu4(xr[slot][0], nb[0], nb[1]), h0, l0);
+      split4(bn_relu4(xr[slot][1], nb[2], nb[3]), h1, l1);
+      uint8_t* q = cvt + (s & 1) * 2 * kCvtF + wo;
+      *reinterpret_cast<v4u*>(q) = v4u{h0[0], h0[1], h1[0], h1[1]};
+      *reinterpret_cast<v4u*>(q + kCvtF) = v4u{l0[0], l0[1], l1[0], l1[1]};
+    };
+    __builtin_amdgcn_s_setprio(1);  // the producers' step is the chain every round waits on
+#pragma unroll
+    for (int u = 0; u < kPfW; ++u) issue(u, u);
+    ldbn(0);
+    __builtin_amdgcn_s_waitcnt(ws_vmcnt(2 * (kPfW - 1)));  // step 0 landed
+    __builtin_amdgcn_sched_barrier(0);
+    convert(0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    issue(kPfW, 0);
+    ldbn(1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ws_barrier();  // P0
+    for (int g0 = 0; g0 < G; g0 += kPfW) {
+#pragma unroll
+      for (int u = 0; u < kPfW; ++u) {
+        const int g = g0 + u;
+        if (g >= G) break;  // block-uniform
+        // unconditional (step G, past the end, converts a clamped copy into
+        // a slot no consumer reads): the vmcnt below counts kPfW - 1 steps
+        const int slot = (u + 1) % kPfW;
+        __builtin_amdgcn_s_waitcnt(ws_vmcnt(2 * (kPfW - 1)));  // X of step g+1
+        __builtin_amdgcn_sched_barrier(0);
+        convert(g + 1, slot);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(g + 1 + kPfW, slot);
+        ldbn(g + 2);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        ws_barrier();  // R(g)
+        if ((g + 1) % NST == 0) {
+          const int c = g / NST;
+          if (c >= npro - 1) {
+            ws_barrier();                 // T
+            if (c == nch - 1) ws_barrier();  // E
+          }
+        }
+      }
+    }
+    // the clamped re-loads past the last step land before the wave ends
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+
+  // ------------------------------- consumers -------------------------------
+  // 3x3 roles and resident weights: A[16oh + (lane&15)][tap t][32kq + 8(lane>>4) ..+8]
+  const int kq = wave & 3, oh = wave >> 2;
+  v4u w2h[kTaps], w2l[kTaps];
+#pragma unroll
+  for (int t = 0; t < kTaps; ++t) {
+    const size_t off = ((size_t)((t * 4 + kq) * 2 + oh) * 64 + lane) * 8;
+    w2h[t] = ld16(p.w2_hi + off);
+    w2l[t] = ld16(p.w2_lo + off);
+  }
+  // 1x1 roles: output-channel quarter q1 x pixel half ph of the 64-row chunk
+  const int q1 = wave & 3, ph = wave >> 2;
+  const int col = lane & 31, hh = lane >> 5;
+  v4u a1[2][2][2];  // [step parity][kc][plane]
+  const auto w1h = __builtin_amdgcn_make_buffer_rsrc((void*)p.w1_hi, (short)0, p.K * 256, 0x00020000);
+  const auto w1l = __builtin_amdgcn_make_buffer_rsrc((void*)p.w1_lo, (short)0, p.K * 256, 0x00020000);
+  const int w1v = (q1 * 64 + lane) * 16;
+  auto wload = [&](int slot, int st) {
+    st = min(st, NST - 1);
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      a1[slot][kc][0] = __builtin_amdgcn_raw_buffer_load_b128(w1h, w1v, (2 * st + kc) * 4096, 0);
+      a1[slot][kc][1] = __builtin_amdgcn_raw_buffer_load_b128(w1l, w1v, (2 * st + kc) * 4096, 0);
+    }
+  };
+  const int bpx = 32 * ph + col;
+  const int bsw = (bpx >> 2) & 3;
+  const int br_off[2] = {bpx * 64 + ((hh ^ bsw) << 4), bpx * 64 + (((2 + hh) ^ bsw) << 4)};
+  // z rows [g0, g0 + nrows) -> ring; W(0) was issued by the caller; gs = the
+  // chunk's first global step (its stage slot parity)
+  auto z_chunk = [&](int g0, int nrows, int gs) {
+    f32x16 acc;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 b = ldf4(p.b1 + 32 * q1 + 8 * g + 4 * hh);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[4 * g + e] = b[e];
+    }
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      wload((st + 1) & 1, st + 1);
+      const uint8_t* cb = cvt + ((gs + st) & 1) * 2 * kCvtF;
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc) {
+        const uint8_t* q = cb + br_off[kc];
+        acc = x3_32(a1[st & 1][kc][0], a1[st & 1][kc][1], ld16(q), ld16(q + kCvtF), acc);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      ws_barrier();  // R
+    }
+    // C (32x32): lane col = pixel, reg 4g+e -> channel 32q1 + 8g + 4hh + e
+    if (bpx < nrows) {
+      int pos;
+      (void)fast_divmod(g0 + bpx + W + 1, kRingF, kMagRingF, pos);
+      uint8_t* rp = ring + (pos + 1) * kRowF1 + 8 * hh;
+      const int mirror = pos == 0 ? kRingF * kRowF1 : (pos == kRingF - 1 ? -kRingF * kRowF1 : 0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[e] = fmaxf(acc[4 * g + e], 0.f);
+        v2u h, l;
+        split4(r, h, l);
+        uint8_t* q = rp + ((4 * q1 + g) << 4);
+        *reinterpret_cast<v2u*>(q) = h;
+        *reinterpret_cast<v2u*>(q + 256) = l;
+        if (mirror) {
+          *reinterpret_cast<v2u*>(q + mirror) = h;
+          *reinterpret_cast<v2u*>(q + mirror + 256) = l;
+        }
+      }
+    }
+  };
+
+  ws_barrier();  // P0
+  int gs = 0;
+  for (int c = 0; c < npro; ++c, gs += NST) {
+    wload(0, 0);
+    z_chunk(chunk_g0(c), min(64, b1 - chunk_g0(c)), gs);
+  }
+  const int c4 = lane >> 4;
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int m0 = tile * kT2;
+    __syncthreads();  // T: the ring holds band(tile); the scratch is free
+    // ---- 3x3 (as v1) ----
+    {
+      // band rows of tap rows dy 0/1/2 packed in bytes 0/1/2 (all < 256):
+      // 8 VGPRs fewer than v1's table, one v_bfe per operand read
+      uint32_t R[4];
+      bool lfm[4], rtm[4];
+      {
+        const int m = m0 + (lane & 15);
+        int r, xx, pm;
+        (void)fast_divmod(m, HW, p.mag_hw, r);
+        int yy = fast_divmod(r, W, p.mag_w, xx);
+        (void)fast_divmod(m + W + 1, kRingF, kMagRingF, pm);
+#pragma unroll
+        for (int pg = 0; pg < 4; ++pg) {
+          if (pg) {
+            xx += 16;
+            if (xx >= W) {
+              xx -= W;
+              if (++yy == p.H) yy = 0;
+            }
+            pm += 16;
+            if (pm >= kRingF) pm -= kRingF;
+          }
+          const bool in = m + 16 * pg < p.M;
+          const int rm = pm - W, rp = pm + W;
+          const int r0 = (in && yy > 0) ? (rm < 0 ? rm + kRingF : rm) : kZeroF;
+          const int r1 = in ? pm : kZeroF;
+          const int r2 = (in && yy < p.H - 1) ? (rp >= kRingF ? rp - kRingF : rp) : kZeroF;
+          R[pg] = (uint32_t)r0 | ((uint32_t)r1 << 8) | ((uint32_t)r2 << 16);
+          lfm[pg] = xx > 0;
+          rtm[pg] = xx < W - 1;
+        }
+      }
+      f32x4 acc[4];
+#pragma unroll
+      for (int pg = 0; pg < 4; ++pg) acc[pg] = f32x4{0.f, 0.f, 0.f, 0.f};
+      constexpr int kLead = 2;  // (3 in v1: one more operand set than 168 VGPRs hold)
+      v4u bq[kLead + 1][2];
+      const int chunk16 = (4 * kq + (lane >> 4)) << 4;
+      auto rd = [&](int step) {
+        const int t = step >> 2, pg = step & 3;
+        const int dy = t / 3, dx = t % 3 - 1;
+        const int a = (int)((R[pg] >> (8 * dy)) & 0xff) + dx;
+        int off = a * kRowF1 + chunk16;
+        if (dx < 0 && !lfm[pg]) off = kZeroF * kRowF1;
+        if (dx > 0 && !rtm[pg]) off = kZeroF * kRowF1;
+        const uint8_t* q = ring + kRowF1 + off;
+        bq[step % (kLead + 1)][0] = ld16(q);
+        bq[step % (kLead + 1)][1] = ld16(q + 256);
+      };
+#pragma unroll
+      for (int step = 0; step < kLead; ++step) rd(step);
+#pragma unroll
+      for (int step = 0; step < 4 * kTaps; ++step) {
+        if (step + kLead < 4 * kTaps) rd(step + kLead);
+        __builtin_amdgcn_sched_barrier(0);
+        const int t = step >> 2, pg = step & 3;
+        acc[pg] = x3_16(w2h[t], w2l[t], bq[step % (kLead + 1)][0], bq[step % (kLead + 1)][1], acc[pg]);
+      }
+      // the next chunk's W(0): issued after the operand reads (168 VGPRs do
+      // not hold it beside them), in flight during the partial stores
+      if (tile + 1 < t_end) wload(0, 0);
+      if (c4 != kq) {
+        float* sw = scr + ((oh * 4 + c4) * 3 + (kq - c4 + 3) % 4) * 256 + (lane & 15) * 4;
+#pragma unroll
+        for (int pg = 0; pg < 4; ++pg) *reinterpret_cast<f32x4*>(sw + pg * 64) = acc[pg];
+      } else {
+        float* yw = ysum + (oh * 4 + kq) * 256 + (lane & 15) * 4;
+#pragma unroll
+        for (int pg = 0; pg < 4; ++pg) *reinterpret_cast<f32x4*>(yw + pg * 64) = acc[pg];
+      }
+    }
+    if (tile + 1 < t_end) {
+      z_chunk(m0 + kT2 + W + 1, kT2, gs);
+      gs += NST;
+    } else {
+      __syncthreads();  // E
+    }
+    if (c4 == kq) {
+      const float* sr = scr + (oh * 4 + kq) * 3 * 256 + (lane & 15) * 4;
+      const float* yr = ysum + (oh * 4 + kq) * 256 + (lane & 15) * 4;
+#pragma unroll
+      for (int pg = 0; pg < 4; ++pg) {
+        f32x4 v = *reinterpret_cast<const f32x4*>(yr + pg * 64);
+#pragma unroll
+        for (int src = 0; src < 3; ++src) v += *reinterpret_cast<const f32x4*>(sr + src * 256 + pg * 64);
+        const int m = m0 + 16 * pg + (lane & 15);
+        if (m < p.M) *reinterpret_cast<f32x4*>(p.y + (size_t)m * p.ldy + 16 * oh + 4 * kq) = v;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // ============================================================================
 // K14x: the whole dense layer in one kernel for the 14x14 and 7x7 blocks
 // ============================================================================
@@ -2483,11 +2791,12 @@ static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, 
   {(const void*)KERN<2>,  (const void*)KERN<3>,  (const void*)KERN<4>,  (const void*)KERN<5>,  (const void*)KERN<6>, \
    (const void*)KERN<7>,  (const void*)KERN<8>,  (const void*)KERN<9>,  (const void*)KERN<10>, (const void*)KERN<11>, \
    (const void*)KERN<12>, (const void*)KERN<13>, (const void*)KERN<14>, (const void*)KERN<15>}
-  // [version 1 / 3][NST - 2]
-  static const void* const kFns[2][14] = {X3F_ROW(x3_dense_fused_kernel), X3F_ROW(x3_dense_fused3_kernel)};
+  // [version 1 / 3 / 5 (K11w)][NST - 2]
+  static const void* const kFns[3][14] = {X3F_ROW(x3_dense_fused_kernel), X3F_ROW(x3_dense_fused3_kernel),
+                                          X3F_ROW(x3_dense_ws_kernel)};
 #undef X3F_ROW
   const int nst = K / 32;
-  if (nst < 2 || nst > 15 || (v != 1 && v != 3)) return hipErrorInvalidValue;
+  if (nst < 2 || nst > 15 || (v != 1 && v != 3 && v != 5)) return hipErrorInvalidValue;
   static std::atomic<bool> attr_set[kMaxDevices];
   const int dev_slot = device_slot();
   if (!attr_set[dev_slot].load(std::memory_order_acquire)) {
@@ -2503,8 +2812,9 @@ static int x3_dense_fused_impl(int v, const float* x, int ldx, int imgs, int H, 
   p.tiles_per_block = (p.tiles + grid - 1) / grid;
   const int blocks = (p.tiles + p.tiles_per_block - 1) / p.tiles_per_block;
   void* args[] = {&p};
-  const hipError_t e = hipLaunchKernel(kFns[v == 3][nst - 2], dim3(blocks), dim3(512), args,
-                                       v == 3 ? kLdsF3 : kLdsF, (hipStream_t)stream);
+  const int vi = v == 1 ? 0 : (v == 3 ? 1 : 2);
+  const hipError_t e = hipLaunchKernel(kFns[vi][nst - 2], dim3(blocks), dim3(v == 5 ? 768 : 512), args,
+                                       v == 1 ? kLdsF : (v == 3 ? kLdsF3 : kLdsFW), (hipStream_t)stream);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }
@@ -2521,6 +2831,13 @@ int tcamd_x3_dense_fused3(const float* x, int ldx, int imgs, int H, int W, int K
                           const void* w1_hi, const void* w1_lo, const float* b1, const void* w2_hi,
                           const void* w2_lo, float* y, int ldy, void* stream) {
   return x3_dense_fused_impl(3, x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream);
+}
+
+// K11w: v1's layer with producer / consumer waves (768 threads); same inputs.
+int tcamd_x3_dense_fused_ws(const float* x, int ldx, int imgs, int H, int W, int K, const float* s1, const float* t1,
+                            const void* w1_hi, const void* w1_lo, const float* b1, const void* w2_hi,
+                            const void* w2_lo, float* y, int ldy, void* stream) {
+  return x3_dense_fused_impl(5, x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream);
 }
 
 

@@ -267,9 +267,10 @@ def test_x3c_chain(imgs, H, C0, n):
 @pytest.mark.parametrize("imgs,H,K", [(1, 56, 64), (8, 56, 224), (32, 56, 128), (64, 28, 224), (5, 28, 96),
                                       (3, 28, 192), (2, 16, 160), (128, 28, 128), (40, 56, 192), (16, 28, 480),
                                       (3, 28, 320), (24, 28, 256), (2, 20, 416)])
-@pytest.mark.parametrize("version", [1, 3])
+@pytest.mark.parametrize("version", [1, 3, 5])
 def test_x3_dense_fused(imgs, H, K, version):
-    """K11x (v1; v3: v1 with the next chunk's 1x1 interleaved into the 3x3): the whole dense layer in one kernel (z produced into the 3x3's LDS
+    """K11x (v1; v3: v1 with the next chunk's 1x1 interleaved into the 3x3;
+    5 = K11w, v1 on producer / consumer waves, bitwise v1's output): the whole dense layer in one kernel (z produced into the 3x3's LDS
     ring, never written to HBM): one block's band prologue only, several tiles
     per block, ragged tails, every block width, and every K-step instantiation
     (K = 64..480, 2..15 steps).  Against fp64
@@ -288,7 +289,7 @@ def test_x3_dense_fused(imgs, H, K, version):
     w2p = _split(w2.permute(0, 2, 3, 1).reshape(32, -1))
     f1h, f1l = (hip.x3_w1_fragments(u) for u in (w1h, w1l))
     frag = hip.x3_w3f_fragments
-    fused = {1: hip.x3_dense_fused, 3: hip.x3_dense_fused3}[version]
+    fused = {1: hip.x3_dense_fused, 3: hip.x3_dense_fused3, 5: hip.x3_dense_fused_ws}[version]
     f2h, f2l = (frag(u) for u in w2p)
     xc = x.clone()
     fused(x.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), f1h.data_ptr(), f1l.data_ptr(),
@@ -309,6 +310,13 @@ def test_x3_dense_fused(imgs, H, K, version):
                        y2.data_ptr() + 4 * K, ldx, stream=_st())
     torch.cuda.synchronize()
     assert _rel(x[:, K:K + 32], y2[:, K:K + 32]) < 2e-5
+    if version == 5:  # same products in the same order as v1
+        y1 = xc.clone()
+        hip.x3_dense_fused(y1.data_ptr(), ldx, imgs, H, H, K, s.data_ptr(), t.data_ptr(), f1h.data_ptr(),
+                           f1l.data_ptr(), b1.data_ptr(), f2h.data_ptr(), f2l.data_ptr(), y1.data_ptr() + 4 * K, ldx,
+                           stream=_st())
+        torch.cuda.synchronize()
+        assert torch.equal(x, y1)
 
 
 @pytest.mark.parametrize("imgs,H,K", [(1, 14, 64), (3, 14, 256), (8, 14, 288), (9, 14, 992), (17, 14, 640),

@@ -30,7 +30,7 @@ def main():
 
     dev = "cuda"
     st = torch.cuda.current_stream().cuda_stream
-    fns = {1: hip.x3_dense_fused, 3: hip.x3_dense_fused3}
+    fns = {1: hip.x3_dense_fused, 3: hip.x3_dense_fused3, 5: hip.x3_dense_fused_ws}
     vers = [int(v) for v in a.versions.split(",")]
     rows = []
     for imgs in [int(v) for v in a.imgs.split(",")]:

@@ -224,6 +224,14 @@ _SIGS = {
         ctypes.c_int,
     ),
     "tcamd_x3_small_tiles": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "tcamd_x3_dense_fused_ws": (
+        [
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+        ],
+        ctypes.c_int,
+    ),
     "tcamd_x3_dense_fused3": (
         [
             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -807,6 +815,14 @@ def x3_dense_fused3(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_l
     with the next chunk's 1x1 K steps interleaved into each tile's 3x3."""
     _check(_load().tcamd_x3_dense_fused3(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo, b1,
                                          w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_fused3")
+
+
+def x3_dense_fused_ws(x, ldx, imgs, H, W, K, s1, t1, w1_hi, w1_lo, b1, w2_hi, w2_lo, y, ldy, stream=None):
+    """K11w: v1's layer (same fragments, same products in the same order) on
+    768 threads: producer waves convert X into LDS stages, consumer waves run
+    the MFMAs (csrc/kernels/densenet_x3.hip)."""
+    _check(_load().tcamd_x3_dense_fused_ws(x, int(ldx), int(imgs), int(H), int(W), int(K), s1, t1, w1_hi, w1_lo,
+                                           b1, w2_hi, w2_lo, y, int(ldy), _vp(stream)), "x3_dense_fused_ws")
 
 
 def x3_cat(x, out, rows, K, stream=None):
