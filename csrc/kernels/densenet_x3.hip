@@ -1690,8 +1690,12 @@ __global__ void __launch_bounds__(768, 1) x3_dense_ws_kernel(X3FusedParams p) {
         }
       }
     }
-    // the clamped re-loads past the last step land before the wave ends
+    // the clamped re-loads past the last step land before the wave ends; the
+    // empty asm keeps their registers allocated until then (hipcc does not
+    // know the inline-asm loads are in flight and could reuse a dead one)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < kPfW; ++u) asm volatile("" ::"v"(xr[u][0]), "v"(xr[u][1]));
     return;
   }
 
