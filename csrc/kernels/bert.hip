@@ -525,6 +525,159 @@ __global__ void __launch_bounds__(256) x3_cat_kernel(const float* __restrict__ x
   }
 }
 
+
+// ---- K12x: fp32-parity attention (bf16x3 products, fp32 softmax) -----------
+// The fp32-parity bert's attention (it ran torch SDPA in fp32, 25 % of that
+// forward).  Block = (sequence, head, 64 queries), 4 waves x 16 queries; keys
+// in 64-key chunks staged into LDS split hi / lo (K row-major, V transposed);
+// every product is bf16x3 (hi*hi + hi*lo + lo*hi, fp32 accumulate), the
+// online softmax is fp32 with exp; masked keys get the reference's additive
+// -10000 (so a fully masked row averages like torch's).
+//   S^T = K Q^T on 16x16x32 MFMAs: lane (l & 15) = query, reg e -> key 4g + e
+//   (g = l >> 4), so the softmax state of a query is lane-local after two
+//   xor-shuffles over the lane groups, and the same registers are the B
+//   operand of O^T = V^T P^T: k position 8g + i <-> key 4g + i of the chunk's
+//   16-key tile 2ks (i < 4) or 2ks + 1 (i >= 4), read from V^T in LDS as two
+//   8-B runs.  O^T's C layout: lane = query, reg e -> head dim 16 dt + 4g + e.
+constexpr int kXR = 64 * 2 + 16;  // LDS row: 64 bf16 + 16 B (16 rows' b128 reads spread over all banks)
+constexpr int kLdsAX = 4 * 64 * kXR + 64 * 4;
+
+__device__ __forceinline__ void split_pk(float a, float b, uint32_t& hi, uint32_t& lo) {
+  hi = pack2(a, b);
+  lo = pack2(a - __uint_as_float(hi << 16), b - __uint_as_float(hi & 0xffff0000u));
+}
+
+__device__ __forceinline__ f32x4 mma_x3(v4u ah, v4u al, v4u bh, v4u bl, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf8(al), as_bf8(bh), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf8(ah), as_bf8(bl), c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf8(ah), as_bf8(bh), c, 0, 0, 0);
+}
+
+__global__ void __launch_bounds__(256) attention_x3_kernel(const float* __restrict__ qkv, const int* __restrict__ mask,
+                                                           float* __restrict__ out, int S, int heads, float scale) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t ldsa[];
+  uint8_t* const kh = ldsa;             // K hi [64 keys][kXR]
+  uint8_t* const kl = kh + 64 * kXR;    // K lo
+  uint8_t* const vth = kl + 64 * kXR;   // V^T hi [64 d][kXR]
+  uint8_t* const vtl = vth + 64 * kXR;  // V^T lo
+  float* const kb = reinterpret_cast<float*>(vtl + 64 * kXR);  // the chunk's key bias
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int seq = blockIdx.x / heads, h = blockIdx.x - seq * heads;
+  const int H = heads * 64, ld = 3 * H;
+  const float* const base = qkv + (size_t)seq * S * ld + h * 64;
+  const int g = lane >> 4, c = lane & 15;
+  const int q = blockIdx.y * 64 + wave * 16 + c;  // this lane's query
+
+  // Q^T operand, pre-scaled (1/8: exact), d = 32 ks + 8 g .. +8
+  v4u qh[2], ql[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const float4 a = *reinterpret_cast<const float4*>(base + (size_t)q * ld + 32 * ks + 8 * g);
+    const float4 b = *reinterpret_cast<const float4*>(base + (size_t)q * ld + 32 * ks + 8 * g + 4);
+    uint32_t hh[4], ll[4];
+    split_pk(a.x * scale, a.y * scale, hh[0], ll[0]);
+    split_pk(a.z * scale, a.w * scale, hh[1], ll[1]);
+    split_pk(b.x * scale, b.y * scale, hh[2], ll[2]);
+    split_pk(b.z * scale, b.w * scale, hh[3], ll[3]);
+    qh[ks] = v4u{hh[0], hh[1], hh[2], hh[3]};
+    ql[ks] = v4u{ll[0], ll[1], ll[2], ll[3]};
+  }
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  for (int c0 = 0; c0 < S; c0 += 64) {
+    __syncthreads();  // the previous chunk's LDS reads are done
+    // stage: thread -> (key, 4 head dims) x 4; K row-major, V transposed
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int i = it * 256 + tid, key = i >> 4, d4 = (i & 15) * 4;
+      const float* rp = base + (size_t)(c0 + key) * ld + d4;
+      const float4 kv = *reinterpret_cast<const float4*>(rp + H);
+      const float4 vv = *reinterpret_cast<const float4*>(rp + 2 * H);
+      uint32_t h0, l0, h1, l1;
+      split_pk(kv.x, kv.y, h0, l0);
+      split_pk(kv.z, kv.w, h1, l1);
+      *reinterpret_cast<uint2*>(kh + key * kXR + d4 * 2) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(kl + key * kXR + d4 * 2) = make_uint2(l0, l1);
+      split_pk(vv.x, vv.y, h0, l0);
+      split_pk(vv.z, vv.w, h1, l1);
+      uint16_t* const th = reinterpret_cast<uint16_t*>(vth + d4 * kXR) + key;
+      uint16_t* const tl = reinterpret_cast<uint16_t*>(vtl + d4 * kXR) + key;
+      constexpr int r = kXR / 2;  // row stride in bf16
+      th[0] = (uint16_t)h0;
+      th[r] = (uint16_t)(h0 >> 16);
+      th[2 * r] = (uint16_t)h1;
+      th[3 * r] = (uint16_t)(h1 >> 16);
+      tl[0] = (uint16_t)l0;
+      tl[r] = (uint16_t)(l0 >> 16);
+      tl[2 * r] = (uint16_t)l1;
+      tl[3 * r] = (uint16_t)(l1 >> 16);
+    }
+    if (tid < 64) kb[tid] = (mask && mask[seq * S + c0 + tid] == 0) ? -10000.f : 0.f;
+    __syncthreads();
+
+    // S^T tiles [16 keys][16 queries]
+    f32x4 st[4];
+    float mx = m;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      st[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const uint8_t* ar = kh + (kt * 16 + c) * kXR + (32 * ks + 8 * g) * 2;
+        st[kt] = mma_x3(*reinterpret_cast<const v4u*>(ar), *reinterpret_cast<const v4u*>(ar + 64 * kXR), qh[ks],
+                        ql[ks], st[kt]);
+      }
+      const f32x4 kbv = *reinterpret_cast<const f32x4*>(kb + kt * 16 + 4 * g);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        st[kt][e] += kbv[e];
+        mx = fmaxf(mx, st[kt][e]);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float corr = __expf(m - mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        st[kt][e] = __expf(st[kt][e] - mx);
+        sum += st[kt][e];
+      }
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    l = l * corr + sum;
+    m = mx;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+    // O^T += V^T P^T over the chunk's two 32-key steps
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint32_t ph[4], pl[4];
+      split_pk(st[2 * ks][0], st[2 * ks][1], ph[0], pl[0]);
+      split_pk(st[2 * ks][2], st[2 * ks][3], ph[1], pl[1]);
+      split_pk(st[2 * ks + 1][0], st[2 * ks + 1][1], ph[2], pl[2]);
+      split_pk(st[2 * ks + 1][2], st[2 * ks + 1][3], ph[3], pl[3]);
+      const v4u pbh = v4u{ph[0], ph[1], ph[2], ph[3]}, pbl = v4u{pl[0], pl[1], pl[2], pl[3]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int off = (dt * 16 + c) * kXR + (ks * 32 + 4 * g) * 2;
+        const uint2 a0 = *reinterpret_cast<const uint2*>(vth + off), a1 = *reinterpret_cast<const uint2*>(vth + off + 32);
+        const uint2 b0 = *reinterpret_cast<const uint2*>(vtl + off), b1 = *reinterpret_cast<const uint2*>(vtl + off + 32);
+        o[dt] = mma_x3(v4u{a0.x, a0.y, a1.x, a1.y}, v4u{b0.x, b0.y, b1.x, b1.y}, pbh, pbl, o[dt]);
+      }
+    }
+  }
+  const float inv = 1.f / l;
+  float* const op = out + ((size_t)seq * S + q) * H + h * 64 + 4 * g;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) *reinterpret_cast<f32x4*>(op + dt * 16) = o[dt] * inv;
+}
+
 }  // namespace
 
 extern "C" {
@@ -686,6 +839,19 @@ int tcamd_attention_bias(const void* qkv, const void* qkv_bias, const int* mask,
   else
     hipLaunchKernelGGL(attention_kernel<false>, grid, block, lds, (hipStream_t)stream, (const uint16_t*)qkv, mask,
                        (uint16_t*)out, S, heads, scale, (const uint16_t*)qkv_bias);
+  return hipGetLastError();
+}
+
+// K12x: fp32-parity attention over qkv [seqs * S][3 * heads * 64] fp32 (bias
+// included) -> out [seqs * S][heads * 64] fp32; mask int32 [seqs][S] (0 =
+// padded: additive -10000) or null.  S % 64 == 0; pointers 16-B aligned.
+int tcamd_attention_f32(const float* qkv, const int* mask, float* out, int seqs, int S, int heads, float scale,
+                        void* stream) {
+  if (seqs <= 0) return hipSuccess;
+  if (S <= 0 || S % 64 || heads <= 0 || ((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)mask) % 16)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(attention_x3_kernel, dim3(seqs * heads, S / 64), dim3(256), kLdsAX, (hipStream_t)stream, qkv,
+                     mask, out, S, heads, scale);
   return hipGetLastError();
 }
 

@@ -167,6 +167,41 @@ def test_attention_kernel_applies_qkv_bias(masked):
     assert err.item() < 1e-2, err.item()
 
 
+@pytest.mark.parametrize("seqs,S,masked", [(1, 64, False), (3, 128, True), (2, 384, True), (4, 384, False),
+                                           (1, 512, True)])
+def test_attention_f32_matches_fp64(seqs, S, masked):
+    """K12x (fp32-parity attention: bf16x3 QK^T and PV, fp32 softmax) against
+    fp64 softmax(QK^T/8 + key-padding bias) V on fp32 inputs; one sequence
+    fully masked (the reference's additive -10000 makes it a plain average)."""
+    _need_gpu()
+    from triton_client_amd.ops import hip
+
+    g = torch.Generator(device=DEV).manual_seed(seqs * 977 + S)
+    qkv = torch.randn(seqs * S, 3 * 1024, device=DEV, generator=g) * 1.5
+    mask = None
+    if masked:
+        mask = torch.ones(seqs, S, device=DEV, dtype=torch.int32)
+        for i in range(seqs):
+            mask[i, S - 7 * (i + 1) * (S // 64):] = 0
+        mask[0, 5] = 0
+        if seqs > 2:
+            mask[2] = 0
+    out = torch.full((seqs * S, 1024), float("nan"), device=DEV)
+    hip.attention_f32(qkv.data_ptr(), None if mask is None else mask.data_ptr(), out.data_ptr(), seqs, S, 16, 0.125)
+    torch.cuda.synchronize()
+    x = qkv.double().view(seqs, S, 3, 16, 64).permute(2, 0, 3, 1, 4)
+    sc = x[0] @ x[1].transpose(-1, -2) / 8.0
+    if mask is not None:
+        sc = sc + ((1.0 - mask.double()) * -10000.0)[:, None, None, :]
+    ref = (torch.softmax(sc, dim=-1) @ x[2]).transpose(1, 2).reshape(seqs, S, 1024)
+    got = out.double().view(seqs, S, 1024)
+    for i in range(seqs):
+        err = ((got[i] - ref[i]).norm() / ref[i].norm()).item()
+        # a fully masked sequence: every fp32 score carries the -10000 offset,
+        # which leaves ~10 fewer bits of it (as in the reference's fp32 path)
+        assert err < (2e-3 if mask is not None and not mask[i].any() else 2e-5), (i, err)
+
+
 def test_attention_rejects_unsupported_shapes():
     _need_gpu()
     from triton_client_amd.ops import hip

@@ -330,7 +330,8 @@ def _k12_ok(x, s):
 
 def _attention(qkv, b, s, mask_i32, bias, qkv_bias=None):
     """Multi-head attention over the QKV projection [b, s, 3H]: K12 on the GPU
-    (mask_i32: int32 [b, s] key-padding mask or None), SDPA elsewhere.
+    (bf16), K12x (fp32-parity; mask_i32: int32 [b, s] key-padding mask or
+    None), SDPA elsewhere.
     qkv_bias: the projection's bias when ``qkv`` was computed without it."""
     if _k12_ok(qkv, s):
         from triton_client_amd.ops import hip
@@ -342,6 +343,15 @@ def _attention(qkv, b, s, mask_i32, bias, qkv_bias=None):
         return out
     if qkv_bias is not None:
         qkv = qkv + qkv_bias
+    if FUSED and qkv.is_cuda and qkv.dtype == torch.float32 and s % 64 == 0 and qkv.is_contiguous():
+        # fp32-parity mode: K12x (bf16x3 products, fp32 softmax) instead of fp32 SDPA
+        from triton_client_amd.ops import hip
+
+        out = torch.empty(b, s, HIDDEN, device=qkv.device, dtype=torch.float32)
+        hip.attention_f32(qkv.data_ptr(), None if mask_i32 is None else mask_i32.data_ptr(), out.data_ptr(), b, s,
+                          HEADS, 1.0 / math.sqrt(HIDDEN // HEADS),
+                          stream=torch.cuda.current_stream(qkv.device).cuda_stream)
+        return out
     q, k, v = qkv.view(b, s, 3, HEADS, HIDDEN // HEADS).permute(2, 0, 3, 1, 4)
     a = F.scaled_dot_product_attention(q, k, v, attn_mask=bias)
     return a.transpose(1, 2).reshape(b, s, HIDDEN)

@@ -308,6 +308,11 @@ _SIGS = {
          ctypes.c_float, ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "tcamd_attention_f32": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+         ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_attention": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
          ctypes.c_void_p],
@@ -686,6 +691,15 @@ def attention(qkv, mask, out, seqs, S, heads, scale, stream=None, bias=None):
     b_k shifts every score of a query equally and cancels in the softmax)."""
     _check(_load().tcamd_attention_bias(qkv, _vp(bias), _vp(mask), out, int(seqs), int(S), int(heads), float(scale),
                                         _vp(stream)), "attention")
+
+
+def attention_f32(qkv, mask, out, seqs, S, heads, scale, stream=None):
+    """K12x: fp32-parity attention (bf16x3 products, fp32 online softmax) over
+    the fp32 QKV projection ``qkv`` [seqs*S][3*heads*64] (bias included) into
+    ``out`` [seqs*S][heads*64] fp32; ``mask`` int32 [seqs][S] (0 = padded key,
+    additive -10000 as the reference) or None.  S % 64 == 0."""
+    _check(_load().tcamd_attention_f32(qkv, _vp(mask), out, int(seqs), int(S), int(heads), float(scale), _vp(stream)),
+           "attention_f32")
 
 
 def x3_conv1x1_ws_bytes(M, K, N=128):
