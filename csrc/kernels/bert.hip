@@ -125,10 +125,14 @@ __device__ __forceinline__ void store8(float* p, const float* v) {
   reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
 }
 
+// out3 (fp32 model, or null): the row also as the next bf16x3 GEMM's operand,
+// bf16 [rows][3H] = [hi | hi | lo] (x3_cat's layout), so that GEMM needs no
+// x3_cat pass over the LayerNorm output.
 template <int E, typename T>
 __global__ void __launch_bounds__(256) add_ln_parts_kernel(const T* x, const float* parts, int nparts, long long pstride,
                                                            const float* __restrict__ bias, const T* __restrict__ gamma,
-                                                           const T* __restrict__ beta, T* out, int rows, float eps) {
+                                                           const T* __restrict__ beta, T* out, uint16_t* __restrict__ out3,
+                                                           int rows, float eps) {
   constexpr int H = 64 * E, C = E / 8;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -165,6 +169,18 @@ __global__ void __launch_bounds__(256) add_ln_parts_kernel(const T* x, const flo
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = (v[8 * c + e] - mean) * rstd * g[e] + bt[e];
     store8(out + base + off, o);
+    if (out3) {
+      v4u hi, lo;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        hi[q] = pack2(o[2 * q], o[2 * q + 1]);
+        lo[q] = pack2(o[2 * q] - __uint_as_float(hi[q] << 16), o[2 * q + 1] - __uint_as_float(hi[q] & 0xffff0000u));
+      }
+      uint16_t* r3 = out3 + 3 * base + off;
+      *reinterpret_cast<v4u*>(r3) = hi;
+      *reinterpret_cast<v4u*>(r3 + H) = hi;
+      *reinterpret_cast<v4u*>(r3 + 2 * H) = lo;
+    }
   }
 }
 
@@ -553,8 +569,11 @@ __device__ __forceinline__ f32x4 mma_x3(v4u ah, v4u al, v4u bh, v4u bl, f32x4 c)
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf8(ah), as_bf8(bh), c, 0, 0, 0);
 }
 
+// out3 (or null): write the output as the out-projection's bf16x3 operand,
+// bf16 [tokens][3H] = [hi | hi | lo], instead of fp32 into out
 __global__ void __launch_bounds__(256) attention_x3_kernel(const float* __restrict__ qkv, const int* __restrict__ mask,
-                                                           float* __restrict__ out, int S, int heads, float scale) {
+                                                           float* __restrict__ out, uint16_t* __restrict__ out3, int S,
+                                                           int heads, float scale) {
   extern __shared__ __attribute__((aligned(16))) uint8_t ldsa[];
   uint8_t* const kh = ldsa;             // K hi [64 keys][kXR]
   uint8_t* const kl = kh + 64 * kXR;    // K lo
@@ -673,6 +692,23 @@ __global__ void __launch_bounds__(256) attention_x3_kernel(const float* __restri
     }
   }
   const float inv = 1.f / l;
+  if (out3) {
+    uint16_t* const op = out3 + ((size_t)seq * S + q) * 3 * H + h * 64 + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      f32x4 r = o[dt] * inv;
+      // the rounded product (hipcc would contract r - hi into fma(o, inv, -hi)):
+      // the operand is then bitwise x3_cat of the fp32 output
+      asm volatile("" : "+v"(r));
+      uint32_t h0, l0, h1, l1;
+      split_pk(r[0], r[1], h0, l0);
+      split_pk(r[2], r[3], h1, l1);
+      *reinterpret_cast<uint2*>(op + dt * 16) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(op + H + dt * 16) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(op + 2 * H + dt * 16) = make_uint2(l0, l1);
+    }
+    return;
+  }
   float* const op = out + ((size_t)seq * S + q) * H + h * 64 + 4 * g;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) *reinterpret_cast<f32x4*>(op + dt * 16) = o[dt] * inv;
@@ -722,18 +758,19 @@ int tcamd_add_layernorm(const void* x, const void* y, const void* gamma, const v
 // at parts + z * pstride (elements, [rows][H] each); bias fp32 [H] or null;
 // f32 = 0: x / gamma / beta / out bf16, 1: fp32.  16-B aligned pointers;
 // out may alias x.
-int tcamd_add_layernorm_parts(const void* x, const float* parts, int nparts, long long pstride, const float* bias,
-                              const void* gamma, const void* beta, void* out, int rows, int H, float eps, int f32,
-                              void* stream) {
+int tcamd_add_layernorm_parts3(const void* x, const float* parts, int nparts, long long pstride, const float* bias,
+                               const void* gamma, const void* beta, void* out, void* out3, int rows, int H, float eps,
+                               int f32, void* stream) {
   if (rows <= 0) return hipSuccess;
-  if (nparts < 0 || (nparts > 0 && (!parts || pstride < (long long)rows * H)) ||
-      ((uintptr_t)x | (uintptr_t)parts | (uintptr_t)bias | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)out) % 16)
+  if (nparts < 0 || (nparts > 0 && (!parts || pstride < (long long)rows * H)) || (out3 && !f32) ||
+      ((uintptr_t)x | (uintptr_t)parts | (uintptr_t)bias | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)out |
+       (uintptr_t)out3) % 16)
     return hipErrorInvalidValue;
   const dim3 grid((rows + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
 #define TC_K11P(E, T)                                                                                            \
   hipLaunchKernelGGL((add_ln_parts_kernel<E, T>), grid, block, 0, s, (const T*)x, parts, nparts, pstride, bias, \
-                     (const T*)gamma, (const T*)beta, (T*)out, rows, eps)
+                     (const T*)gamma, (const T*)beta, (T*)out, (uint16_t*)out3, rows, eps)
   switch (H * 2 + (f32 ? 1 : 0)) {
     case 1024: TC_K11P(8, uint16_t); break;
     case 1025: TC_K11P(8, float); break;
@@ -747,6 +784,13 @@ int tcamd_add_layernorm_parts(const void* x, const float* parts, int nparts, lon
   }
 #undef TC_K11P
   return hipGetLastError();
+}
+
+int tcamd_add_layernorm_parts(const void* x, const float* parts, int nparts, long long pstride, const float* bias,
+                              const void* gamma, const void* beta, void* out, int rows, int H, float eps, int f32,
+                              void* stream) {
+  return tcamd_add_layernorm_parts3(x, parts, nparts, pstride, bias, gamma, beta, out, nullptr, rows, H, eps, f32,
+                                    stream);
 }
 
 // QA head: start[r] = x[r] . w[0] + b[0], end[r] = x[r] . w[1] + b[1] (fp32
@@ -845,13 +889,14 @@ int tcamd_attention_bias(const void* qkv, const void* qkv_bias, const int* mask,
 // K12x: fp32-parity attention over qkv [seqs * S][3 * heads * 64] fp32 (bias
 // included) -> out [seqs * S][heads * 64] fp32; mask int32 [seqs][S] (0 =
 // padded: additive -10000) or null.  S % 64 == 0; pointers 16-B aligned.
-int tcamd_attention_f32(const float* qkv, const int* mask, float* out, int seqs, int S, int heads, float scale,
+// x3: out is the out-projection's bf16x3 operand, bf16 [seqs * S][3 * heads * 64].
+int tcamd_attention_f32(const float* qkv, const int* mask, void* out, int seqs, int S, int heads, float scale, int x3,
                         void* stream) {
   if (seqs <= 0) return hipSuccess;
   if (S <= 0 || S % 64 || heads <= 0 || ((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)mask) % 16)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(attention_x3_kernel, dim3(seqs * heads, S / 64), dim3(256), kLdsAX, (hipStream_t)stream, qkv,
-                     mask, out, S, heads, scale);
+                     mask, x3 ? nullptr : (float*)out, x3 ? (uint16_t*)out : nullptr, S, heads, scale);
   return hipGetLastError();
 }
 

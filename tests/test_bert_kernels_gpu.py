@@ -202,6 +202,27 @@ def test_attention_f32_matches_fp64(seqs, S, masked):
         assert err < (2e-3 if mask is not None and not mask[i].any() else 2e-5), (i, err)
 
 
+def test_attention_f32_x3_operand():
+    """K12x with x3: the output written as the out projection's bf16x3 operand
+    is bitwise x3_cat of its fp32 output."""
+    _need_gpu()
+    from triton_client_amd.ops import hip
+
+    seqs, S = 2, 384
+    g = torch.Generator(device=DEV).manual_seed(5)
+    qkv = torch.randn(seqs * S, 3 * 1024, device=DEV, generator=g)
+    mask = torch.ones(seqs, S, device=DEV, dtype=torch.int32)
+    mask[1, 300:] = 0
+    out = torch.empty(seqs * S, 1024, device=DEV)
+    out3 = torch.empty(seqs * S, 3 * 1024, device=DEV, dtype=torch.bfloat16)
+    hip.attention_f32(qkv.data_ptr(), mask.data_ptr(), out.data_ptr(), seqs, S, 16, 0.125)
+    hip.attention_f32(qkv.data_ptr(), mask.data_ptr(), out3.data_ptr(), seqs, S, 16, 0.125, x3=True)
+    ref3 = torch.empty_like(out3)
+    hip.x3_cat(out.data_ptr(), ref3.data_ptr(), seqs * S, 1024)
+    torch.cuda.synchronize()
+    assert torch.equal(out3, ref3)
+
+
 def test_attention_rejects_unsupported_shapes():
     _need_gpu()
     from triton_client_amd.ops import hip

@@ -318,6 +318,34 @@ def test_add_layernorm_parts(f32, nparts, with_bias):
     assert err < (1e-6 if f32 else 4e-3), err
 
 
+@pytest.mark.parametrize("H", [1024, 4096])
+def test_add_layernorm_parts_x3_operand(H):
+    """K11p's fp32 form with out3: the LayerNorm output also as the next
+    bf16x3 GEMM's operand, bitwise what x3_cat makes of the fp32 output."""
+    hip = _hip()
+    g = torch.Generator(device=DEV).manual_seed(H)
+    rows = 333
+    x = torch.randn(rows, H, device=DEV, generator=g)
+    y = torch.randn(rows, H, device=DEV, generator=g) * 0.3
+    gamma = 1 + 0.1 * torch.randn(H, device=DEV, generator=g)
+    beta = 0.1 * torch.randn(H, device=DEV, generator=g)
+    out = torch.empty(rows, H, device=DEV)
+    out3 = torch.full((rows, 3 * H), 7.0, device=DEV, dtype=torch.bfloat16)
+    st = torch.cuda.current_stream().cuda_stream
+    hip.add_layernorm_parts(x.data_ptr(), y.data_ptr(), 1, rows * H, None, gamma.data_ptr(), beta.data_ptr(),
+                            out.data_ptr(), rows, H, 1e-12, f32=True, stream=st, out3=out3.data_ptr())
+    ref3 = torch.empty_like(out3)
+    hip.x3_cat(out.data_ptr(), ref3.data_ptr(), rows, H, stream=st)
+    plain = torch.empty_like(out)
+    hip.add_layernorm_parts(x.data_ptr(), y.data_ptr(), 1, rows * H, None, gamma.data_ptr(), beta.data_ptr(),
+                            plain.data_ptr(), rows, H, 1e-12, f32=True, stream=st)
+    torch.cuda.synchronize()
+    assert torch.equal(out3, ref3) and torch.equal(out, plain)
+    with pytest.raises(hip.HipError):  # bf16 model: no x3 operand
+        hip.add_layernorm_parts(x.data_ptr(), y.data_ptr(), 1, rows * H, None, gamma.data_ptr(), beta.data_ptr(),
+                                out.data_ptr(), rows, H, 1e-12, f32=False, stream=st, out3=out3.data_ptr())
+
+
 @pytest.mark.parametrize("kern", ["k17", "k18_c3", "k18_c6"])
 def test_gelu_erf_epilogue_fp32(kern):
     """bias + erf-form GELU with fp32 output (the fp32-parity bert's FFN-up on

@@ -181,14 +181,33 @@ class _Parts:
         self.slabs = slabs
 
 
+class _X3:
+    """An fp32 activation [..., K] that exists only as its bf16x3 GEMM operand
+    xc [rows, 3K] = [hi | hi | lo] (K12x writes the attention output so)."""
+
+    def __init__(self, xc, shape):
+        self.xc = xc
+        self.shape = shape
+
+
+def _x3_operand(x):
+    """The bf16x3 operand a producer already wrote for ``x`` (K12x's _X3, or
+    the ``_x3`` a K11p LayerNorm attaches to its fp32 output), else None."""
+    return x.xc if isinstance(x, _X3) else getattr(x, "_x3", None)
+
+
 def _proj(x, lin, epilogue="bias", name=None, allow_split=False):
     """lin(x) (epilogue "bias"), gelu(lin(x)) ("bias_gelu") or x @ W^T ("none").
     On the GPU in bf16 the routing table picks K18 / K17 (the hand-written
     gfx950 GEMMs) or hipBLASLt per projection and token count (gemm_route).
     With ``allow_split`` a split-K route returns its fp32 partial slabs
     [splits, tokens, N] as _Parts (the caller's K11p sums them with the bias)."""
-    x2 = x.reshape(-1, x.shape[-1])
     n = lin.weight.shape[0]
+    xc = _x3_operand(x)
+    if xc is not None and getattr(lin, "w3", None) is not None:
+        y = _mm_x3(None, lin, epilogue, name, allow_split, xc=xc)
+        return y if isinstance(y, _Parts) else y.view(*x.shape[:-1], n)
+    x2 = x.reshape(-1, x.shape[-1])
     if name is not None and _ours_ok(x2, lin):
         route = gemm_route(name, x2.shape[0])
         if _route_ok(route, x2.shape[0], n, x2.shape[1]):
@@ -207,21 +226,27 @@ def _proj(x, lin, epilogue="bias", name=None, allow_split=False):
     return lin(x)
 
 
-def _mm_x3(x2, lin, epilogue="none", name=None, allow_split=False):
+def _mm_x3(x2, lin, epilogue="none", name=None, allow_split=False, xc=None):
     """fp32-parity projection: x2 fp32 [M, K] against w3 = [W_hi | W_lo | W_hi]
     bf16 [N, 3K] as ONE bf16 GEMM over [x_hi | x_hi | x_lo] (csrc/kernels/bert.hip
     x3_cat): x_hi W_hi + x_hi W_lo + x_lo W_hi, fp32 accumulate and output,
     ~1e-5 of an fp32 GEMM.  The GEMM is K18 / K17 (gemm_route_x3) with the
     bias and the erf GELU in its epilogue, or a split-K route's fp32 slabs
-    (_Parts) for K11p; torch.mm with TC_BERT_GEMM=lib."""
+    (_Parts) for K11p; torch.mm with TC_BERT_GEMM=lib.  ``xc``: the operand a
+    producer (K11p, K12x) already wrote; then x2 is not read and no x3_cat runs."""
     from triton_client_amd.ops import hip
 
-    M, K = x2.shape
     w3 = lin.w3
     N = w3.shape[0]
-    st = torch.cuda.current_stream(x2.device).cuda_stream
-    xc = torch.empty(M, 3 * K, device=x2.device, dtype=torch.bfloat16)
-    hip.x3_cat(x2.contiguous().data_ptr(), xc.data_ptr(), M, K, stream=st)
+    if xc is None:
+        M, K = x2.shape
+        st = torch.cuda.current_stream(x2.device).cuda_stream
+        xc = torch.empty(M, 3 * K, device=x2.device, dtype=torch.bfloat16)
+        hip.x3_cat(x2.contiguous().data_ptr(), xc.data_ptr(), M, K, stream=st)
+    else:
+        M, K = xc.shape[0], xc.shape[1] // 3
+        st = torch.cuda.current_stream(xc.device).cuda_stream
+    x2 = xc
     route = gemm_route_x3(name, M)
     if route[0] != "lib" and FUSED and _route_ok(route, M, N, 3 * K):
         epi = "bias_gelu_erf" if epilogue == "bias_gelu" else epilogue
@@ -280,25 +305,42 @@ def _proj_add_ln(x, a, lin, ln, name):
         assert x.is_contiguous() and x.numel() == rows * H
         f32 = x.dtype == torch.float32
         bias = lin.bias.detach() if f32 else _bias_f32(lin, x.device)
+        xc = _x3_buffer(x, lin, rows, H)
         hip.add_layernorm_parts(x.data_ptr(), p.data_ptr(), p.shape[0], rows * H, bias.data_ptr(),
                                 ln.weight.data_ptr(), ln.bias.data_ptr(), out.data_ptr(), rows, H, ln.eps, f32=f32,
-                                stream=torch.cuda.current_stream(x.device).cuda_stream)
+                                stream=torch.cuda.current_stream(x.device).cuda_stream,
+                                out3=None if xc is None else xc.data_ptr())
+        if xc is not None:
+            out._x3 = xc
         return out
-    return _add_ln(x, y, ln)
+    return _add_ln(x, y, ln, x3=getattr(lin, "w3", None) is not None)
 
 
-def _add_ln(x, y, ln):
+def _x3_buffer(x, lin, rows, H):
+    """The bf16x3 operand buffer a fp32-parity LayerNorm fills beside its fp32
+    output (the next projection's input: no x3_cat pass), or None."""
+    if x.dtype != torch.float32 or getattr(lin, "w3", None) is None:
+        return None
+    return torch.empty(rows, 3 * H, device=x.device, dtype=torch.bfloat16)
+
+
+def _add_ln(x, y, ln, x3=False):
     """LayerNorm(x + y): K11 on the GPU (K11p's fp32 form for the fp32-parity
-    model: y as its one partial slab), torch ops elsewhere."""
+    model: y as its one partial slab; with ``x3`` it also writes the next
+    projection's bf16x3 operand, attached as ``out._x3``), torch ops elsewhere."""
     if (FUSED and x.is_cuda and x.dtype == torch.float32 and y.dtype == torch.float32 and x.is_contiguous()
             and y.is_contiguous() and x.shape[-1] in (512, 1024, 2048, 4096)):
         from triton_client_amd.ops import hip
 
         out = torch.empty_like(x)
         rows, H = x.numel() // x.shape[-1], x.shape[-1]
+        xc = torch.empty(rows, 3 * H, device=x.device, dtype=torch.bfloat16) if x3 else None
         hip.add_layernorm_parts(x.data_ptr(), y.data_ptr(), 1, rows * H, None, ln.weight.data_ptr(),
                                 ln.bias.data_ptr(), out.data_ptr(), rows, H, ln.eps, f32=True,
-                                stream=torch.cuda.current_stream(x.device).cuda_stream)
+                                stream=torch.cuda.current_stream(x.device).cuda_stream,
+                                out3=None if xc is None else xc.data_ptr())
+        if xc is not None:
+            out._x3 = xc
         return out
     if FUSED and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and y.is_contiguous():
         from triton_client_amd.ops import hip
@@ -328,10 +370,11 @@ def _k12_ok(x, s):
     return s <= hip.ATTENTION_MAX_SEQ
 
 
-def _attention(qkv, b, s, mask_i32, bias, qkv_bias=None):
+def _attention(qkv, b, s, mask_i32, bias, qkv_bias=None, x3_out=False):
     """Multi-head attention over the QKV projection [b, s, 3H]: K12 on the GPU
     (bf16), K12x (fp32-parity; mask_i32: int32 [b, s] key-padding mask or
-    None), SDPA elsewhere.
+    None), SDPA elsewhere.  ``x3_out`` (fp32-parity model): K12x writes the
+    out projection's bf16x3 operand and this returns it as an _X3.
     qkv_bias: the projection's bias when ``qkv`` was computed without it."""
     if _k12_ok(qkv, s):
         from triton_client_amd.ops import hip
@@ -347,11 +390,14 @@ def _attention(qkv, b, s, mask_i32, bias, qkv_bias=None):
         # fp32-parity mode: K12x (bf16x3 products, fp32 softmax) instead of fp32 SDPA
         from triton_client_amd.ops import hip
 
-        out = torch.empty(b, s, HIDDEN, device=qkv.device, dtype=torch.float32)
+        if x3_out:
+            out = torch.empty(b * s, 3 * HIDDEN, device=qkv.device, dtype=torch.bfloat16)
+        else:
+            out = torch.empty(b, s, HIDDEN, device=qkv.device, dtype=torch.float32)
         hip.attention_f32(qkv.data_ptr(), None if mask_i32 is None else mask_i32.data_ptr(), out.data_ptr(), b, s,
                           HEADS, 1.0 / math.sqrt(HIDDEN // HEADS),
-                          stream=torch.cuda.current_stream(qkv.device).cuda_stream)
-        return out
+                          stream=torch.cuda.current_stream(qkv.device).cuda_stream, x3=x3_out)
+        return _X3(out, (b, s, HIDDEN)) if x3_out else out
     q, k, v = qkv.view(b, s, 3, HEADS, HIDDEN // HEADS).permute(2, 0, 3, 1, 4)
     a = F.scaled_dot_product_attention(q, k, v, attn_mask=bias)
     return a.transpose(1, 2).reshape(b, s, HIDDEN)
@@ -395,7 +441,8 @@ class _Layer(nn.Module):
             qkv = _proj(x, self.qkv, "none", name="qkv")
             a = _attention(qkv, b, s, mask_i32, bias, qkv_bias=self.qkv.bias)
         else:
-            a = _attention(_proj(x, self.qkv, name="qkv"), b, s, mask_i32, bias)
+            a = _attention(_proj(x, self.qkv, name="qkv"), b, s, mask_i32, bias,
+                           x3_out=getattr(self.out, "w3", None) is not None and x.is_cuda)
         x = _proj_add_ln(x, a, self.out, self.ln1, "out")
         return _proj_add_ln(x, _proj(x, self.ffn1, "bias_gelu", name="ffn_up"), self.ffn2, self.ln2, "ffn_down")
 

@@ -276,6 +276,12 @@ _SIGS = {
          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "tcamd_add_layernorm_parts3": (
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p,
+         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+         ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "tcamd_k17_calls": ([], ctypes.c_longlong),
     "tcamd_x3_cat": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "tcamd_x3_stem": (
@@ -310,7 +316,7 @@ _SIGS = {
     ),
     "tcamd_attention_f32": (
         [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
-         ctypes.c_void_p],
+         ctypes.c_int, ctypes.c_void_p],
         ctypes.c_int,
     ),
     "tcamd_attention": (
@@ -693,13 +699,15 @@ def attention(qkv, mask, out, seqs, S, heads, scale, stream=None, bias=None):
                                         _vp(stream)), "attention")
 
 
-def attention_f32(qkv, mask, out, seqs, S, heads, scale, stream=None):
+def attention_f32(qkv, mask, out, seqs, S, heads, scale, stream=None, x3=False):
     """K12x: fp32-parity attention (bf16x3 products, fp32 online softmax) over
     the fp32 QKV projection ``qkv`` [seqs*S][3*heads*64] (bias included) into
-    ``out`` [seqs*S][heads*64] fp32; ``mask`` int32 [seqs][S] (0 = padded key,
-    additive -10000 as the reference) or None.  S % 64 == 0."""
-    _check(_load().tcamd_attention_f32(qkv, _vp(mask), out, int(seqs), int(S), int(heads), float(scale), _vp(stream)),
-           "attention_f32")
+    ``out`` [seqs*S][heads*64] fp32 -- or, with ``x3``, into the out
+    projection's bf16x3 operand, bf16 [seqs*S][3*heads*64] = [hi | hi | lo];
+    ``mask`` int32 [seqs][S] (0 = padded key, additive -10000 as the
+    reference) or None.  S % 64 == 0."""
+    _check(_load().tcamd_attention_f32(qkv, _vp(mask), out, int(seqs), int(S), int(heads), float(scale),
+                                       1 if x3 else 0, _vp(stream)), "attention_f32")
 
 
 def x3_conv1x1_ws_bytes(M, K, N=128):
@@ -953,12 +961,15 @@ def qa_head(x, w, b, start, end, rows, H, f32=False, stream=None):
     _check(_load().tcamd_qa_head(x, w, b, start, end, int(rows), int(H), 1 if f32 else 0, _vp(stream)), "qa_head")
 
 
-def add_layernorm_parts(x, parts, nparts, pstride, bias, gamma, beta, out, rows, H, eps, f32=False, stream=None):
+def add_layernorm_parts(x, parts, nparts, pstride, bias, gamma, beta, out, rows, H, eps, f32=False, stream=None,
+                        out3=None):
     """K11p: out = LayerNorm(x + bias + sum of ``nparts`` fp32 partial slabs
     (``parts`` + z * ``pstride`` elements, [rows][H] each)) * gamma + beta.
-    bias fp32 [H] or None; x / gamma / beta / out bf16, or fp32 with ``f32``."""
-    _check(_load().tcamd_add_layernorm_parts(x, _vp(parts), int(nparts), int(pstride), _vp(bias), gamma, beta, out,
-                                             int(rows), int(H), float(eps), 1 if f32 else 0, _vp(stream)),
+    bias fp32 [H] or None; x / gamma / beta / out bf16, or fp32 with ``f32``.
+    ``out3`` (f32 only, or None): the output also as a bf16x3 GEMM operand,
+    bf16 [rows][3H] = [hi | hi | lo] (x3_cat's layout)."""
+    _check(_load().tcamd_add_layernorm_parts3(x, _vp(parts), int(nparts), int(pstride), _vp(bias), gamma, beta, out,
+                                              _vp(out3), int(rows), int(H), float(eps), 1 if f32 else 0, _vp(stream)),
            "add_layernorm_parts")
 
 
