@@ -67,8 +67,11 @@ constexpr int slab_bytes(int tm) { return tm * kSlabK * 2 + kBBytes; }  // A | B
 constexpr int ring_bytes(int tm) { return kRing * slab_bytes(tm); }     // 128 / 96 KB
 
 // kEpiBiasGeluErf: the erf form of GELU (the fp32-parity bert, whose
-// reference module uses it; the bf16 model keeps the tanh form)
-enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiBiasGeluErf = 3 };
+// reference module uses it; the bf16 model keeps the tanh form).
+// kEpiBiasGeluErfX3: the same, written as the next bf16x3 GEMM's operand:
+// bf16 C [M][ldc >= 3N] = [hi | hi | lo] of each fp32 result (the FFN-down
+// input of the fp32-parity bert, which then needs no x3_cat pass)
+enum : int { kEpiNone = 0, kEpiBias = 1, kEpiBiasGelu = 2, kEpiBiasGeluErf = 3, kEpiBiasGeluErfX3 = 4 };
 
 struct K17Params {
   const uint16_t* A;  // [M][lda] bf16
@@ -349,29 +352,47 @@ __global__ void __launch_bounds__(512, 1) k17_gemm_kernel(K17Params p) {
         if (EPI == kEpiBiasGelu) {
           v01 = gelu2(v01);
           v23 = gelu2(v23);
-        } else if (EPI == kEpiBiasGeluErf) {
+        } else if (EPI == kEpiBiasGeluErf || EPI == kEpiBiasGeluErfX3) {
           v01 = f32x2{0.5f * v01.x * (1.0f + erff(v01.x * 0.70710678118654752f)),
                       0.5f * v01.y * (1.0f + erff(v01.y * 0.70710678118654752f))};
           v23 = f32x2{0.5f * v23.x * (1.0f + erff(v23.x * 0.70710678118654752f)),
                       0.5f * v23.y * (1.0f + erff(v23.y * 0.70710678118654752f))};
         }
-        const float v[4] = {v01.x, v01.y, v23.x, v23.y};
-        if constexpr (OUTF32) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (full || row0 + e < p.M) reinterpret_cast<float*>(p.C)[(size_t)(row0 + e) * p.ldc + col] = v[e];
-        } else {
-          const uint32_t send = par ? pk2(v[0], v[1]) : pk2(v[2], v[3]);
+        float v[4] = {v01.x, v01.y, v23.x, v23.y};
+        // bf16 stores of 4 rows of this column at column offset co
+        auto store_bf16 = [&](const float (&w)[4], int co) {
+          const uint32_t send = par ? pk2(w[0], w[1]) : pk2(w[2], w[3]);
           // lane ^ 1 by DPP quad_perm [1, 0, 3, 2] (a VALU move, no LDS round trip)
           const uint32_t recv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0xB1, 0xf, 0xf, false);
           const float r0 = __uint_as_float(recv << 16), r1 = __uint_as_float(recv & 0xffff0000u);
           // even lane: rows 0, 1 of columns (c, c + 1); odd lane: rows 2, 3 of (c - 1, c)
-          const uint32_t w0 = par ? pk2(r0, v[2]) : pk2(v[0], r0);
-          const uint32_t w1 = par ? pk2(r1, v[3]) : pk2(v[1], r1);
-          const int r = row0 + 2 * par, c = col - par;
+          const uint32_t w0 = par ? pk2(r0, w[2]) : pk2(w[0], r0);
+          const uint32_t w1 = par ? pk2(r1, w[3]) : pk2(w[1], r1);
+          const int r = row0 + 2 * par, c = col - par + co;
           uint32_t* out = reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(p.C) + (size_t)r * p.ldc + c);
           if (full || r < p.M) out[0] = w0;
           if (full || r + 1 < p.M) out[p.ldc / 2] = w1;
+        };
+        if constexpr (OUTF32) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (full || row0 + e < p.M) reinterpret_cast<float*>(p.C)[(size_t)(row0 + e) * p.ldc + col] = v[e];
+        } else if constexpr (EPI == kEpiBiasGeluErfX3) {
+          // hi = bf16(v) (exact in the bf16 stores), lo = v - hi (rounded by
+          // them); the asm keeps v the rounded GELU value (no contraction of
+          // v - hi into its product), as x3_cat would see it
+          asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+          float hv[4], lv[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            hv[e] = __uint_as_float(pk2(v[e], 0.f) << 16);
+            lv[e] = v[e] - hv[e];
+          }
+          store_bf16(hv, 0);
+          store_bf16(hv, p.N);
+          store_bf16(lv, 2 * p.N);
+        } else {
+          store_bf16(v, 0);
         }
       }
     }
@@ -429,6 +450,7 @@ hipError_t launch(const K17Params& prm, int grid, hipStream_t s, int epi, int ou
   }
   if (epi == kEpiNone) return launch_tm<TM, kEpiNone, false>(prm, grid, s);
   if (epi == kEpiBias) return launch_tm<TM, kEpiBias, false>(prm, grid, s);
+  if (epi == kEpiBiasGeluErfX3) return launch_tm<TM, kEpiBiasGeluErfX3, false>(prm, grid, s);
   return launch_tm<TM, kEpiBiasGelu, false>(prm, grid, s);
 }
 
@@ -482,13 +504,15 @@ extern "C" {
 // K17: C = A . B^T (+ bias) (GELU) with bf16 A [M][lda], B [N][ldb] (K
 // contiguous), fp32 bias [N], C bf16 (out_f32 = 0) or fp32 [M][ldc].
 // epi: 0 none, 1 bias, 2 bias + GELU (tanh form), 3 bias + GELU (erf form,
-// fp32 C only) (N <= 8188).  N a multiple of 256, K of 32, lda /
+// fp32 C only), 4 the erf form as a bf16x3 operand (bf16 C, ldc >= 3N:
+// [hi | hi | lo]) (N <= 8188).  N a multiple of 256, K of 32, lda /
 // ldb / ldc multiples of 8, 16-B aligned pointers; any M >= 1.
 int tcamd_k17_gemm(const void* A, const void* B, const float* bias, void* C, int M, int N, int K, int lda, int ldb,
                    int ldc, int epi, int out_f32, void* stream) {
   if (M <= 0) return hipSuccess;
-  if (!A || !B || !C || N <= 0 || N % kTile || K <= 0 || K % kSlabK || epi < 0 || epi > 3) return hipErrorInvalidValue;
+  if (!A || !B || !C || N <= 0 || N % kTile || K <= 0 || K % kSlabK || epi < 0 || epi > 4) return hipErrorInvalidValue;
   if (epi == 3 && !out_f32) return hipErrorInvalidValue;  // erf GELU: the fp32-parity form only
+  if (epi == 4 && (out_f32 || ldc < 3 * N)) return hipErrorInvalidValue;
   if (lda < K || ldb < K || ldc < N || lda % 8 || ldb % 8 || ldc % 8) return hipErrorInvalidValue;
   if (!a16(A) || !a16(B) || !a16(C) || (epi && (!bias || ((uintptr_t)bias & 3) || N > kMaxBiasN)))
     return hipErrorInvalidValue;

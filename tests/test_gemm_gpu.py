@@ -346,6 +346,31 @@ def test_add_layernorm_parts_x3_operand(H):
                                 out.data_ptr(), rows, H, 1e-12, f32=False, stream=st, out3=out3.data_ptr())
 
 
+@pytest.mark.parametrize("M", [300, 4100])
+def test_k17_gelu_erf_x3_operand(M):
+    """K17's bias_gelu_erf_x3 epilogue (the fp32-parity FFN-up writing the
+    FFN-down's bf16x3 operand) is bitwise x3_cat of its fp32-output form;
+    fp32 output and a short ldc are refused."""
+    hip = _hip()
+    N, K = 1024, 3072
+    a, b, bias = _case(M, N, K, seed=M)
+    st = torch.cuda.current_stream().cuda_stream
+    c = torch.empty(M, N, device=DEV)
+    hip.k17_gemm(a.data_ptr(), b.data_ptr(), bias.data_ptr(), c.data_ptr(), M, N, K, K, K, N,
+                 epilogue="bias_gelu_erf", out_f32=True, stream=st)
+    c3 = torch.full((M, 3 * N), 7.0, device=DEV, dtype=torch.bfloat16)
+    hip.k17_gemm(a.data_ptr(), b.data_ptr(), bias.data_ptr(), c3.data_ptr(), M, N, K, K, K, 3 * N,
+                 epilogue="bias_gelu_erf_x3", stream=st)
+    ref3 = torch.empty_like(c3)
+    hip.x3_cat(c.data_ptr(), ref3.data_ptr(), M, N, stream=st)
+    torch.cuda.synchronize()
+    assert torch.equal(c3, ref3)
+    for kw in ({"out_f32": True, "ldc": 3 * N}, {"out_f32": False, "ldc": 2 * N}):
+        with pytest.raises(hip.HipError):
+            hip.k17_gemm(a.data_ptr(), b.data_ptr(), bias.data_ptr(), c3.data_ptr(), M, N, K, K, K, kw["ldc"],
+                         epilogue="bias_gelu_erf_x3", out_f32=kw["out_f32"], stream=st)
+
+
 @pytest.mark.parametrize("kern", ["k17", "k18_c3", "k18_c6"])
 def test_gelu_erf_epilogue_fp32(kern):
     """bias + erf-form GELU with fp32 output (the fp32-parity bert's FFN-up on

@@ -196,17 +196,18 @@ def _x3_operand(x):
     return x.xc if isinstance(x, _X3) else getattr(x, "_x3", None)
 
 
-def _proj(x, lin, epilogue="bias", name=None, allow_split=False):
+def _proj(x, lin, epilogue="bias", name=None, allow_split=False, x3_out=False):
     """lin(x) (epilogue "bias"), gelu(lin(x)) ("bias_gelu") or x @ W^T ("none").
     On the GPU in bf16 the routing table picks K18 / K17 (the hand-written
     gfx950 GEMMs) or hipBLASLt per projection and token count (gemm_route).
     With ``allow_split`` a split-K route returns its fp32 partial slabs
-    [splits, tokens, N] as _Parts (the caller's K11p sums them with the bias)."""
+    [splits, tokens, N] as _Parts (the caller's K11p sums them with the bias).
+    ``x3_out`` (fp32-parity FFN-up): a K17 route writes the GELU output as the
+    next projection's bf16x3 operand and this returns it as an _X3."""
     n = lin.weight.shape[0]
     xc = _x3_operand(x)
     if xc is not None and getattr(lin, "w3", None) is not None:
-        y = _mm_x3(None, lin, epilogue, name, allow_split, xc=xc)
-        return y if isinstance(y, _Parts) else y.view(*x.shape[:-1], n)
+        return _x3_result(_mm_x3(None, lin, epilogue, name, allow_split, xc=xc, x3_out=x3_out), x, n)
     x2 = x.reshape(-1, x.shape[-1])
     if name is not None and _ours_ok(x2, lin):
         route = gemm_route(name, x2.shape[0])
@@ -217,8 +218,7 @@ def _proj(x, lin, epilogue="bias", name=None, allow_split=False):
             y = _k18(x2, lin, epilogue, route[1], splits)
             return _Parts(y) if splits > 1 else y.view(*x.shape[:-1], n)
     if getattr(lin, "w3", None) is not None and x2.is_cuda and x2.dtype == torch.float32:
-        y = _mm_x3(x2, lin, epilogue, name, allow_split)
-        return y if isinstance(y, _Parts) else y.view(*x.shape[:-1], n)
+        return _x3_result(_mm_x3(x2, lin, epilogue, name, allow_split, x3_out=x3_out), x, n)
     if epilogue == "none":
         return torch.mm(x2, lin.weight.t()).view(*x.shape[:-1], n)
     if epilogue == "bias_gelu":
@@ -226,7 +226,17 @@ def _proj(x, lin, epilogue="bias", name=None, allow_split=False):
     return lin(x)
 
 
-def _mm_x3(x2, lin, epilogue="none", name=None, allow_split=False, xc=None):
+def _x3_result(y, x, n):
+    """_mm_x3's result in the caller's shape [..., n] (split slabs as they are)."""
+    if isinstance(y, _Parts):
+        return y
+    if isinstance(y, _X3):
+        y.shape = (*x.shape[:-1], n)
+        return y
+    return y.view(*x.shape[:-1], n)
+
+
+def _mm_x3(x2, lin, epilogue="none", name=None, allow_split=False, xc=None, x3_out=False):
     """fp32-parity projection: x2 fp32 [M, K] against w3 = [W_hi | W_lo | W_hi]
     bf16 [N, 3K] as ONE bf16 GEMM over [x_hi | x_hi | x_lo] (csrc/kernels/bert.hip
     x3_cat): x_hi W_hi + x_hi W_lo + x_lo W_hi, fp32 accumulate and output,
@@ -256,8 +266,13 @@ def _mm_x3(x2, lin, epilogue="none", name=None, allow_split=False, xc=None):
             hip.k18_gemm(xc.data_ptr(), w3.data_ptr(), None, out.data_ptr(), M, N, 3 * K, 3 * K, 3 * K, N,
                          out_f32=True, cfg=route[1], splits=route[2], split_stride=M * N, stream=st)
             return _Parts(out)
-        out = torch.empty(M, N, device=x2.device, dtype=torch.float32)
         bp = None if bias is None else bias.data_ptr()
+        if route[0] == "k17" and x3_out and epi == "bias_gelu_erf":
+            out3 = torch.empty(M, 3 * N, device=x2.device, dtype=torch.bfloat16)
+            _k17_launch(route, xc.data_ptr(), w3.data_ptr(), bp, out3.data_ptr(), M, N, 3 * K, 3 * K, 3 * K, 3 * N,
+                        epilogue="bias_gelu_erf_x3", out_f32=False, stream=st)
+            return _X3(out3, (M, N))
+        out = torch.empty(M, N, device=x2.device, dtype=torch.float32)
         if route[0] == "k17":
             _k17_launch(route, xc.data_ptr(), w3.data_ptr(), bp, out.data_ptr(), M, N, 3 * K, 3 * K, 3 * K, N,
                         epilogue=epi, out_f32=True, stream=st)
@@ -444,7 +459,8 @@ class _Layer(nn.Module):
             a = _attention(_proj(x, self.qkv, name="qkv"), b, s, mask_i32, bias,
                            x3_out=getattr(self.out, "w3", None) is not None and x.is_cuda)
         x = _proj_add_ln(x, a, self.out, self.ln1, "out")
-        return _proj_add_ln(x, _proj(x, self.ffn1, "bias_gelu", name="ffn_up"), self.ffn2, self.ln2, "ffn_down")
+        return _proj_add_ln(x, _proj(x, self.ffn1, "bias_gelu", name="ffn_up", x3_out=True), self.ffn2, self.ln2,
+                            "ffn_down")
 
 
 class BertLargeQA(nn.Module):

@@ -919,7 +919,7 @@ def k3_set_check(on):
     return bool(_load().tcamd_k3_set_check(1 if on else 0))
 
 
-K17_EPI = {"none": 0, "bias": 1, "bias_gelu": 2, "bias_gelu_erf": 3}
+K17_EPI = {"none": 0, "bias": 1, "bias_gelu": 2, "bias_gelu_erf": 3, "bias_gelu_erf_x3": 4}
 
 
 def k17_gemm(a, b, bias, c, M, N, K, lda, ldb, ldc, epilogue="none", out_f32=False, stream=None):
