@@ -544,7 +544,7 @@ __global__ void __launch_bounds__(256) x3_cat_kernel(const float* __restrict__ x
 
 // ---- K12x: fp32-parity attention (bf16x3 products, fp32 softmax) -----------
 // The fp32-parity bert's attention (it ran torch SDPA in fp32, 25 % of that
-// forward).  Block = (sequence, head, 64 queries), 4 waves x 16 queries; keys
+// forward).  Block = (sequence, head, 16 NW queries), NW waves x 16 queries; keys
 // in 64-key chunks staged into LDS split hi / lo (K row-major, V transposed);
 // every product is bf16x3 (hi*hi + hi*lo + lo*hi, fp32 accumulate), the
 // online softmax is fp32 with exp; masked keys get the reference's additive
@@ -571,9 +571,11 @@ __device__ __forceinline__ f32x4 mma_x3(v4u ah, v4u al, v4u bh, v4u bl, f32x4 c)
 
 // out3 (or null): write the output as the out-projection's bf16x3 operand,
 // bf16 [tokens][3H] = [hi | hi | lo], instead of fp32 into out
-__global__ void __launch_bounds__(256) attention_x3_kernel(const float* __restrict__ qkv, const int* __restrict__ mask,
-                                                           float* __restrict__ out, uint16_t* __restrict__ out3, int S,
-                                                           int heads, float scale) {
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) attention_x3_kernel(const float* __restrict__ qkv,
+                                                               const int* __restrict__ mask, float* __restrict__ out,
+                                                               uint16_t* __restrict__ out3, int S, int heads,
+                                                               float scale) {
   extern __shared__ __attribute__((aligned(16))) uint8_t ldsa[];
   uint8_t* const kh = ldsa;             // K hi [64 keys][kXR]
   uint8_t* const kl = kh + 64 * kXR;    // K lo
@@ -585,7 +587,7 @@ __global__ void __launch_bounds__(256) attention_x3_kernel(const float* __restri
   const int H = heads * 64, ld = 3 * H;
   const float* const base = qkv + (size_t)seq * S * ld + h * 64;
   const int g = lane >> 4, c = lane & 15;
-  const int q = blockIdx.y * 64 + wave * 16 + c;  // this lane's query
+  const int q = blockIdx.y * (16 * NW) + wave * 16 + c;  // this lane's query
 
   // Q^T operand, pre-scaled (1/8: exact), d = 32 ks + 8 g .. +8
   v4u qh[2], ql[2];
@@ -608,31 +610,33 @@ __global__ void __launch_bounds__(256) attention_x3_kernel(const float* __restri
 
   for (int c0 = 0; c0 < S; c0 += 64) {
     __syncthreads();  // the previous chunk's LDS reads are done
-    // stage: thread -> (key, 4 head dims) x 4; K row-major, V transposed
+    // stage K row-major: thread -> (key, 4 head dims)
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int i = it * 256 + tid, key = i >> 4, d4 = (i & 15) * 4;
-      const float* rp = base + (size_t)(c0 + key) * ld + d4;
-      const float4 kv = *reinterpret_cast<const float4*>(rp + H);
-      const float4 vv = *reinterpret_cast<const float4*>(rp + 2 * H);
+    for (int it = 0; it < 1024 / (64 * NW); ++it) {
+      const int i = it * 64 * NW + tid, key = i >> 4, d4 = (i & 15) * 4;
+      const float4 kv = *reinterpret_cast<const float4*>(base + (size_t)(c0 + key) * ld + H + d4);
       uint32_t h0, l0, h1, l1;
       split_pk(kv.x, kv.y, h0, l0);
       split_pk(kv.z, kv.w, h1, l1);
       *reinterpret_cast<uint2*>(kh + key * kXR + d4 * 2) = make_uint2(h0, h1);
       *reinterpret_cast<uint2*>(kl + key * kXR + d4 * 2) = make_uint2(l0, l1);
-      split_pk(vv.x, vv.y, h0, l0);
-      split_pk(vv.z, vv.w, h1, l1);
-      uint16_t* const th = reinterpret_cast<uint16_t*>(vth + d4 * kXR) + key;
-      uint16_t* const tl = reinterpret_cast<uint16_t*>(vtl + d4 * kXR) + key;
-      constexpr int r = kXR / 2;  // row stride in bf16
-      th[0] = (uint16_t)h0;
-      th[r] = (uint16_t)(h0 >> 16);
-      th[2 * r] = (uint16_t)h1;
-      th[3 * r] = (uint16_t)(h1 >> 16);
-      tl[0] = (uint16_t)l0;
-      tl[r] = (uint16_t)(l0 >> 16);
-      tl[2 * r] = (uint16_t)l1;
-      tl[3 * r] = (uint16_t)(l1 >> 16);
+    }
+    // stage V transposed: thread -> (key pair, 8 head dims); each V^T row gets
+    // 4-B words of two keys, a wave's 32 key pairs one contiguous 128-B run
+    for (int u = tid; u < 256; u += 64 * NW) {
+      const int kp = u & 31, d8 = (u >> 5) * 8;
+      const float* r0 = base + (size_t)(c0 + 2 * kp) * ld + 2 * H + d8;
+      const float4 a0 = *reinterpret_cast<const float4*>(r0), a1 = *reinterpret_cast<const float4*>(r0 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(r0 + ld), b1 = *reinterpret_cast<const float4*>(r0 + ld + 4);
+      const float va[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float vb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint32_t hh, ll;
+        split_pk(va[j], vb[j], hh, ll);
+        *reinterpret_cast<uint32_t*>(vth + (d8 + j) * kXR + 4 * kp) = hh;
+        *reinterpret_cast<uint32_t*>(vtl + (d8 + j) * kXR + 4 * kp) = ll;
+      }
     }
     if (tid < 64) kb[tid] = (mask && mask[seq * S + c0 + tid] == 0) ? -10000.f : 0.f;
     __syncthreads();
@@ -895,8 +899,17 @@ int tcamd_attention_f32(const float* qkv, const int* mask, void* out, int seqs, 
   if (seqs <= 0) return hipSuccess;
   if (S <= 0 || S % 64 || heads <= 0 || ((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)mask) % 16)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(attention_x3_kernel, dim3(seqs * heads, S / 64), dim3(256), kLdsAX, (hipStream_t)stream, qkv,
-                     mask, x3 ? nullptr : (float*)out, x3 ? (uint16_t*)out : nullptr, S, heads, scale);
+  float* const o32 = x3 ? nullptr : (float*)out;
+  uint16_t* const o3 = x3 ? (uint16_t*)out : nullptr;
+  // 128 queries per block (half the K / V staging per query; bs64 x 384: 331
+  // -> 248 us) once that still gives every CU a block (bs1 keeps 64: 20.5 vs
+  // 21.2 us; profiles/r6_bert_fp32/k12x_ab*.log)
+  if (S % 128 == 0 && seqs * heads * (S / 128) >= 256)
+    hipLaunchKernelGGL(attention_x3_kernel<8>, dim3(seqs * heads, S / 128), dim3(512), kLdsAX, (hipStream_t)stream,
+                       qkv, mask, o32, o3, S, heads, scale);
+  else
+    hipLaunchKernelGGL(attention_x3_kernel<4>, dim3(seqs * heads, S / 64), dim3(256), kLdsAX, (hipStream_t)stream,
+                       qkv, mask, o32, o3, S, heads, scale);
   return hipGetLastError();
 }
 
