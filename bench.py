@@ -72,6 +72,11 @@ def parse_args(argv=None):
     ap.add_argument("--bs1-concurrency", type=int, default=64)
     ap.add_argument("--lanes", type=int, default=1,
                     help="client lanes (connection + worker thread each) sharing the headline concurrency")
+    ap.add_argument("--bs1-preferred", default="auto",
+                    help="preferred batch rows for the bs=1 point (comma list; auto = bs1 concurrency / instances; "
+                         "none = keep the headline's), set on the loaded model through the repository API's config "
+                         "override before that point: c64 on 2 instances 23.6k -> 26.3k infer/s, p99 3.5 -> 3.2 ms "
+                         "(profiles/r6_bench/bs1_preferred_ab.md)")
     ap.add_argument("--bs1-lanes", type=int, default=1,
                     help="client lanes (connection + worker thread each) sharing the bs=1 concurrency")
     ap.add_argument("--fanout", default="rccl", choices=["rccl", "p2p", "local"])
@@ -630,6 +635,19 @@ def main():
                              "p99_latency_us": best["p99_latency_us"]})
 
         # ---- bs=1 on the same server -------------------------------------------------
+        bs1_pref = args.bs1_preferred
+        if bs1_pref == "auto":
+            per = args.bs1_concurrency // max(1, args.instance_count)
+            bs1_pref = str(per) if per > 0 and args.bs1_concurrency % max(1, args.instance_count) == 0 else "none"
+        if bs1_pref not in ("", "none") and not cpu:
+            # a deployment tuned for this load: the batcher's preferred size
+            # (Triton's dynamic_batching.preferred_batch_size) = the closed
+            # loop's rows per instance, so the loop settles into one full group
+            # per instance instead of ~3 groups of ~21 rows; applied to the
+            # loaded model by a repository load with a config override
+            pref = [int(x) for x in bs1_pref.split(",")]
+            client.load_model(model, config=json.dumps({"dynamic_batching": {"preferred_batch_size": pref}}))
+            log("bs=1 point: preferred batch rows %s" % pref)
         _, in1 = make_input("data_1_in", 1)
         nl = max(1, args.bs1_lanes)
         if args.bs1_concurrency % nl:
@@ -639,7 +657,8 @@ def main():
         n1 = 64 * args.bs1_concurrency  # ~0.2 s at 20k infer/s: the batch groups of a closed loop need time to settle
         l1, e1, el1, ((s10, b10), (s11, b11)) = measure(
             p1, n1 // 4, 4, n1 // 4, snap=lambda: (p1.s.server_stats(), batch_stats(client, model)))
-        bs1 = {"concurrency": args.bs1_concurrency, "client_lanes": nl, "infer_per_sec": round(world * n1 / el1, 1)}
+        bs1 = {"concurrency": args.bs1_concurrency, "client_lanes": nl, "infer_per_sec": round(world * n1 / el1, 1),
+               "preferred_batch_rows": args.preferred if cpu or bs1_pref in ("", "none") else bs1_pref}
         # where a bs=1 request's latency goes at this concurrency: rows per
         # batch, queueing, and the request-weighted device time of its batch
         bd64 = stats_delta(s10, s11)

@@ -250,6 +250,28 @@ def test_load_unload_and_overrides(proto):
     assert c.is_model_ready("simple_identity")
 
 
+def test_config_override_retunes_preferred_batch_size(cpu_server):
+    """A repository load with a dynamic_batching override on a loaded model
+    (how bench.py's bs=1 point sets its preferred size): no reload, the
+    reported config carries the new preferred sizes, requests keep working."""
+    c = grpcclient.InferenceServerClient(cpu_server.grpc_url)
+    name = "add_sub_pipelined"
+    cfg = lambda: c.get_model_config(name, as_json=True)["config"]["dynamic_batching"]  # noqa: E731
+    assert [int(x) for x in cfg().get("preferred_batch_size", [])] == [8]
+    try:
+        c.load_model(name, config='{"dynamic_batching":{"preferred_batch_size":[4]}}')
+        assert c.is_model_ready(name)
+        assert [int(x) for x in cfg()["preferred_batch_size"]] == [4]
+        x = np.arange(16, dtype=np.int32).reshape(1, 16)
+        ins = [grpcclient.InferInput("INPUT0", [1, 16], "INT32").set_data_from_numpy(x),
+               grpcclient.InferInput("INPUT1", [1, 16], "INT32").set_data_from_numpy(x)]
+        r = c.infer(name, ins)
+        np.testing.assert_array_equal(r.as_numpy("OUTPUT0"), 2 * x)
+    finally:
+        c.load_model(name, config='{"dynamic_batching":{"preferred_batch_size":[8]}}')
+    assert [int(x) for x in cfg()["preferred_batch_size"]] == [8]
+
+
 def test_grpc_stream_sequence_and_decoupled(cpu_server):
     c = grpcclient.InferenceServerClient(cpu_server.grpc_url)
     q = queue.Queue()

@@ -621,6 +621,9 @@ class InferenceServer:
             cfg.version_policy.specific.versions[:] = sorted(e.version_filter)
         if e.config_override and "backend" in e.config_override:
             cfg.backend = e.config_override["backend"]
+        pref = _override_preferred(e)
+        if pref is not None and cfg.HasField("dynamic_batching"):
+            cfg.dynamic_batching.preferred_batch_size[:] = pref
         return cfg
 
     def model_config(self, name, version=""):
@@ -952,6 +955,16 @@ class DirectScheduler:
 
     def close(self):
         pass
+
+
+def _override_preferred(entry):
+    """dynamic_batching.preferred_batch_size of a repository load's config
+    override (a deployment retuning the batcher of a loaded model: the native
+    batcher takes it without reloading the model), or None."""
+    db = (entry.config_override or {}).get("dynamic_batching")
+    if not isinstance(db, dict) or "preferred_batch_size" not in db:
+        return None
+    return [int(x) for x in db["preferred_batch_size"]]
 
 
 class DynamicBatcher(DirectScheduler):

@@ -169,6 +169,11 @@ class NativeFrontend:
         if name in self._versions:
             self.unregister_model(name)
         self.register_model(name, inst)
+        from .core import _override_preferred
+
+        pref = _override_preferred(entry)
+        if pref is not None:
+            self.set_preferred(name, pref)
 
     def register_model(self, name, inst):
         """Serve ``inst`` (a loaded model exposing execute_native) on the fast path."""
