@@ -77,8 +77,11 @@ def parse_args(argv=None):
                          "none = keep the headline's), set on the loaded model through the repository API's config "
                          "override before that point: c64 on 2 instances 23.6k -> 26.3k infer/s, p99 3.5 -> 3.2 ms "
                          "(profiles/r6_bench/bs1_preferred_ab.md)")
-    ap.add_argument("--bs1-lanes", type=int, default=1,
-                    help="client lanes (connection + worker thread each) sharing the bs=1 concurrency")
+    ap.add_argument("--bs1-lanes", type=int, default=2,
+                    help="client lanes (connection + worker thread each) sharing the bs=1 concurrency; with the "
+                         "preferred size at rows per instance, 2 lanes return each 32-row group fast enough that every "
+                         "batch is full: c64 25.3-26.8k -> 28.6-29.2k infer/s, p99 3.1-3.4 -> 2.3-2.4 ms "
+                         "(profiles/r6_bench/bs1_preferred_ab.md)")
     ap.add_argument("--fanout", default="rccl", choices=["rccl", "p2p", "local"])
     ap.add_argument("--fanout-fallback", default="none", choices=["none", "local"],
                     help="none (default): a failed RCCL broadcast ends the run non-zero with the error; "
