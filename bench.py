@@ -111,6 +111,12 @@ def parse_args(argv=None):
     ap.add_argument("--server-log", default="")
     ap.add_argument("--model", default="densenet_onnx", choices=["densenet_onnx", "bert_large"])
     ap.add_argument("--sweep", default="1,4,16,64,256", help="bert_large: concurrencies per GPU")
+    ap.add_argument("--bert-lanes", type=int, default=1,
+                    help="bert_large sweep: client lanes per point (from 8 requests per lane)")
+    ap.add_argument("--bert-preferred", default="auto", choices=["auto", "none"],
+                    help="bert_large sweep: per point, the batcher's preferred size = concurrency / instances (capped "
+                         "at the model's max batch; a repository config override, as for the bs=1 point); none = the "
+                         "model's own setting for every point")
     ap.add_argument("--bert-instance-count", type=int, default=2)
     ap.add_argument("--bert-queue-delay-us", type=int, default=500)
     ap.add_argument("--loop-timeout", type=float, default=600.0,
@@ -845,15 +851,31 @@ def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout
             raise RuntimeError("fan-out replicas differ across ranks after the fan-out timing")
     sweep = []
     for c in [int(v) for v in args.sweep.split(",") if v]:
-        pt = Point(srv, model, 1, c, None, nbytes, local_rank, cpu, inputs=inputs, out_bytes=BERT_SEQ * 4)
-        points.append(pt)
+        # the batcher's preferred size for this load: one equal group per
+        # instance (e.g. c16 on 2 instances ran as 5- and 11-row batches)
+        n_inst = max(1, args.bert_instance_count)
+        # (from 8 rows per instance: c4's 2-row preference ran mostly 1-row batches)
+        pref = min(64, c // n_inst) if args.bert_preferred == "auto" and c % n_inst == 0 and c >= 8 * n_inst else None
+        if pref and not cpu:
+            client.load_model(model, config=json.dumps({"dynamic_batching": {"preferred_batch_size": [pref]}}))
+        nl = max(1, args.bert_lanes)
+        if nl > 1 and c % nl == 0 and c >= 8 * nl:  # read-only input regions: the lanes may share them
+            pt = Lanes([Point(srv, model, 1, c // nl, None, nbytes, local_rank, cpu, inputs=inputs,
+                              out_bytes=BERT_SEQ * 4) for _ in range(nl)])
+            points.extend(pt.points)
+        else:
+            pt = Point(srv, model, 1, c, None, nbytes, local_rank, cpu, inputs=inputs, out_bytes=BERT_SEQ * 4)
+        if isinstance(pt, Point):
+            points.append(pt)
         per = max(64, 8 * c)
         lat, _, elapsed, ((s0, b0), (s1, b1)) = measure(
             pt, max(args.warmup, 1) * per, args.steps, per, snap=lambda: (pt.s.server_stats(), batch_stats(client, model)))
         all_lat = fanout.gather_arrays(lat.astype(np.int64)).astype(np.float64)
         row = {"concurrency": c, "infer_per_sec": round(world * args.steps * per / elapsed, 1),
                "p50_latency_us": round(percentile_us(all_lat, 50), 1),
-               "p99_latency_us": round(percentile_us(all_lat, 99), 1), "ms_per_step": round(1e3 * elapsed / args.steps, 3)}
+               "p99_latency_us": round(percentile_us(all_lat, 99), 1), "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+               "preferred_batch_rows": pref if pref and not cpu else None,
+               "client_lanes": len(pt.points) if isinstance(pt, Lanes) else 1}
         # rank 0's server over the timed window: rows per executed batch, queueing, device time per batch
         bd = stats_delta(s0, s1)
         bd["batch_rows_histogram"] = {str(k): int(b1[k][0] - b0.get(k, (0,))[0]) for k in sorted(b1)
@@ -886,8 +908,9 @@ def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout
         "fanout": fan,
     }
     if not cpu:
-        res["config"]["compute"] = ("fp32 parity: bf16x3 projections (x_hi W_hi + x_hi W_lo + x_lo W_hi, fp32 "
-                                    "accumulate), fp32 LayerNorm / softmax attention" if args.bert_precision == "fp32"
+        res["config"]["compute"] = ("fp32 parity: bf16x3 projections and attention products (x_hi W_hi + x_hi W_lo + "
+                                    "x_lo W_hi, fp32 accumulate), fp32 LayerNorm / softmax"
+                                    if args.bert_precision == "fp32"
                                     else "bf16 (fp32 accumulate)")
         from triton_client_amd.models import bert as _bert
 

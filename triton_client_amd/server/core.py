@@ -480,6 +480,11 @@ class InferenceServer:
                 else:
                     entry.version_filter = None
                 entry.config_override = cfg_override
+                pref = _override_preferred(entry)
+                if pref is not None:  # the Python batcher of a loaded model (the native one: its frontend)
+                    for sched in entry.schedulers.values():
+                        if isinstance(sched, DynamicBatcher):
+                            sched.preferred = sorted(pref)
             wanted = set(entry.versions())
             for v in list(entry.instances):
                 if v not in wanted:
