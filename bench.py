@@ -857,7 +857,10 @@ def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout
         # (from 8 rows per instance: c4's 2-row preference ran mostly 1-row batches)
         pref = min(64, c // n_inst) if args.bert_preferred == "auto" and c % n_inst == 0 and c >= 8 * n_inst else None
         if pref and not cpu:
-            client.load_model(model, config=json.dumps({"dynamic_batching": {"preferred_batch_size": [pref]}}))
+            # with a delay long enough for a partial group to wait for the next
+            # group to come back (one batch), the loop converges on full groups
+            client.load_model(model, config=json.dumps({"dynamic_batching": {
+                "preferred_batch_size": [pref], "max_queue_delay_microseconds": max(args.bert_queue_delay_us, 20000)}}))
         nl = max(1, args.bert_lanes)
         if nl > 1 and c % nl == 0 and c >= 8 * nl:  # read-only input regions: the lanes may share them
             pt = Lanes([Point(srv, model, 1, c // nl, None, nbytes, local_rank, cpu, inputs=inputs,

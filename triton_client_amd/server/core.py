@@ -480,11 +480,11 @@ class InferenceServer:
                 else:
                     entry.version_filter = None
                 entry.config_override = cfg_override
-                pref = _override_preferred(entry)
-                if pref is not None:  # the Python batcher of a loaded model (the native one: its frontend)
-                    for sched in entry.schedulers.values():
-                        if isinstance(sched, DynamicBatcher):
-                            sched.preferred = sorted(pref)
+                for sched in entry.schedulers.values():  # the Python batchers (the native one: its frontend)
+                    if isinstance(sched, DynamicBatcher):
+                        db = _override_batching(entry, sched.inst.dynamic_batching or {})
+                        sched.preferred = sorted(db.get("preferred", []))
+                        sched.delay_s = db.get("max_queue_delay_us", 0) / 1e6
             wanted = set(entry.versions())
             for v in list(entry.instances):
                 if v not in wanted:
@@ -626,9 +626,12 @@ class InferenceServer:
             cfg.version_policy.specific.versions[:] = sorted(e.version_filter)
         if e.config_override and "backend" in e.config_override:
             cfg.backend = e.config_override["backend"]
-        pref = _override_preferred(e)
-        if pref is not None and cfg.HasField("dynamic_batching"):
-            cfg.dynamic_batching.preferred_batch_size[:] = pref
+        db = _override_batching(e, {})
+        if db and cfg.HasField("dynamic_batching"):
+            if "preferred" in db:
+                cfg.dynamic_batching.preferred_batch_size[:] = db["preferred"]
+            if "max_queue_delay_us" in db:
+                cfg.dynamic_batching.max_queue_delay_microseconds = db["max_queue_delay_us"]
         return cfg
 
     def model_config(self, name, version=""):
@@ -970,6 +973,21 @@ def _override_preferred(entry):
     if not isinstance(db, dict) or "preferred_batch_size" not in db:
         return None
     return [int(x) for x in db["preferred_batch_size"]]
+
+
+def _override_batching(entry, base):
+    """The model's batcher settings (``base``: its dynamic_batching dict) with
+    a config override's preferred_batch_size / max_queue_delay_microseconds
+    applied, or ``base`` itself without an override."""
+    db = (entry.config_override or {}).get("dynamic_batching")
+    if base is None or not isinstance(db, dict):
+        return base
+    out = dict(base)
+    if "preferred_batch_size" in db:
+        out["preferred"] = [int(x) for x in db["preferred_batch_size"]]
+    if "max_queue_delay_microseconds" in db:
+        out["max_queue_delay_us"] = int(db["max_queue_delay_microseconds"])
+    return out
 
 
 class DynamicBatcher(DirectScheduler):

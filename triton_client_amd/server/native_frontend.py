@@ -168,15 +168,15 @@ class NativeFrontend:
             return
         if name in self._versions:
             self.unregister_model(name)
-        self.register_model(name, inst)
-        from .core import _override_preferred
+        from .core import _override_batching
 
-        pref = _override_preferred(entry)
-        if pref is not None:
-            self.set_preferred(name, pref)
+        self.register_model(name, inst, _override_batching(entry, inst.dynamic_batching))
 
-    def register_model(self, name, inst):
-        """Serve ``inst`` (a loaded model exposing execute_native) on the fast path."""
+    def register_model(self, name, inst, dynamic_batching=None):
+        """Serve ``inst`` (a loaded model exposing execute_native) on the fast
+        path; ``dynamic_batching`` replaces the model's own batcher settings
+        (a repository load's config override)."""
+        db_cfg = inst.dynamic_batching if dynamic_batching is None else dynamic_batching
         ins, outs = inst.inputs, inst.outputs
 
         def flat(specs):
@@ -206,7 +206,7 @@ class NativeFrontend:
         else:
             cb = EXEC_FN(_exec)
             user = None
-        delay = int((inst.dynamic_batching or {}).get("max_queue_delay_us", 0)) if inst.dynamic_batching is not None else 0
+        delay = int((db_cfg or {}).get("max_queue_delay_us", 0)) if db_cfg is not None else 0
         err = ctypes.create_string_buffer(512)
         rc = _load().tcserve_add_model(
             self._h, name.encode(), str(inst.version).encode(), int(inst.max_batch_size), delay,
@@ -216,10 +216,10 @@ class NativeFrontend:
             cb, user, err, 512)
         if rc != 0:
             raise RuntimeError("tcserve: %s" % err.value.decode(errors="replace"))
-        pref = [int(x) for x in (inst.dynamic_batching or {}).get("preferred", [])]
+        pref = [int(x) for x in (db_cfg or {}).get("preferred", [])]
         if pref:
             self.set_preferred(name, pref)
-        db = inst.dynamic_batching or {}
+        db = db_cfg or {}
         self.set_idle_dispatch(name, bool(db.get("idle_dispatch", True)), pipelined=bool(db.get("pipelined", False)))
         with self._lock:
             self._cbs[name] = cb
