@@ -111,6 +111,8 @@ def parse_args(argv=None):
     ap.add_argument("--server-log", default="")
     ap.add_argument("--model", default="densenet_onnx", choices=["densenet_onnx", "bert_large"])
     ap.add_argument("--sweep", default="1,4,16,64,256", help="bert_large: concurrencies per GPU")
+    ap.add_argument("--bert-preferred-from", type=int, default=2,
+                    help="bert_large sweep: rows per instance from which --bert-preferred auto applies")
     ap.add_argument("--bert-lanes", type=int, default=1,
                     help="bert_large sweep: client lanes per point (from 8 requests per lane)")
     ap.add_argument("--bert-preferred", default="auto", choices=["auto", "none"],
@@ -854,8 +856,10 @@ def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout
         # the batcher's preferred size for this load: one equal group per
         # instance (e.g. c16 on 2 instances ran as 5- and 11-row batches)
         n_inst = max(1, args.bert_instance_count)
-        # (from 8 rows per instance: c4's 2-row preference ran mostly 1-row batches)
-        pref = min(64, c // n_inst) if args.bert_preferred == "auto" and c % n_inst == 0 and c >= 8 * n_inst else None
+        # (from 2 rows per instance: c4 1,312 -> 1,566 infer/s; without the longer
+        # queue delay the 2-row preference had run mostly 1-row batches)
+        pref = (min(64, c // n_inst) if args.bert_preferred == "auto" and c % n_inst == 0 and
+                c >= max(1, args.bert_preferred_from) * n_inst else None)
         if pref and not cpu:
             # with a delay long enough for a partial group to wait for the next
             # group to come back (one batch), the loop converges on full groups
