@@ -141,6 +141,28 @@ def spawn_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
+def bs1_preferred_rows(spec, concurrency, instances):
+    """--bs1-preferred: "auto" = one full group per instance (concurrency /
+    instances, when it divides), "none"/"" = keep the headline's setting, else
+    the comma list given.  Returns the list or None."""
+    if spec == "auto":
+        n = max(1, instances)
+        return [concurrency // n] if concurrency >= n and concurrency % n == 0 else None
+    if spec in ("", "none"):
+        return None
+    return [int(x) for x in spec.split(",")]
+
+
+def bert_point_preferred(mode, concurrency, instances, from_rows, max_batch=64):
+    """Preferred batch rows of one bert sweep point (--bert-preferred auto):
+    concurrency / instances, capped at the model's max batch, from
+    ``from_rows`` rows per instance; None otherwise."""
+    n = max(1, instances)
+    if mode != "auto" or concurrency % n or concurrency < max(1, from_rows) * n:
+        return None
+    return min(max_batch, concurrency // n)
+
+
 class Point:
     """One load point of the native engine against one server."""
 
@@ -646,19 +668,15 @@ def main():
                              "p99_latency_us": best["p99_latency_us"]})
 
         # ---- bs=1 on the same server -------------------------------------------------
-        bs1_pref = args.bs1_preferred
-        if bs1_pref == "auto":
-            per = args.bs1_concurrency // max(1, args.instance_count)
-            bs1_pref = str(per) if per > 0 and args.bs1_concurrency % max(1, args.instance_count) == 0 else "none"
-        if bs1_pref not in ("", "none") and not cpu:
+        bs1_rows = bs1_preferred_rows(args.bs1_preferred, args.bs1_concurrency, args.instance_count)
+        if bs1_rows and not cpu:
             # a deployment tuned for this load: the batcher's preferred size
             # (Triton's dynamic_batching.preferred_batch_size) = the closed
             # loop's rows per instance, so the loop settles into one full group
             # per instance instead of ~3 groups of ~21 rows; applied to the
             # loaded model by a repository load with a config override
-            pref = [int(x) for x in bs1_pref.split(",")]
-            client.load_model(model, config=json.dumps({"dynamic_batching": {"preferred_batch_size": pref}}))
-            log("bs=1 point: preferred batch rows %s" % pref)
+            client.load_model(model, config=json.dumps({"dynamic_batching": {"preferred_batch_size": bs1_rows}}))
+            log("bs=1 point: preferred batch rows %s" % bs1_rows)
         _, in1 = make_input("data_1_in", 1)
         nl = max(1, args.bs1_lanes)
         if args.bs1_concurrency % nl:
@@ -669,7 +687,7 @@ def main():
         l1, e1, el1, ((s10, b10), (s11, b11)) = measure(
             p1, n1 // 4, 4, n1 // 4, snap=lambda: (p1.s.server_stats(), batch_stats(client, model)))
         bs1 = {"concurrency": args.bs1_concurrency, "client_lanes": nl, "infer_per_sec": round(world * n1 / el1, 1),
-               "preferred_batch_rows": args.preferred if cpu or bs1_pref in ("", "none") else bs1_pref}
+               "preferred_batch_rows": args.preferred if cpu or not bs1_rows else ",".join(map(str, bs1_rows))}
         # where a bs=1 request's latency goes at this concurrency: rows per
         # batch, queueing, and the request-weighted device time of its batch
         bd64 = stats_delta(s10, s11)
@@ -858,8 +876,7 @@ def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout
         n_inst = max(1, args.bert_instance_count)
         # (from 2 rows per instance: c4 1,312 -> 1,566 infer/s; without the longer
         # queue delay the 2-row preference had run mostly 1-row batches)
-        pref = (min(64, c // n_inst) if args.bert_preferred == "auto" and c % n_inst == 0 and
-                c >= max(1, args.bert_preferred_from) * n_inst else None)
+        pref = bert_point_preferred(args.bert_preferred, c, n_inst, args.bert_preferred_from)
         if pref and not cpu:
             # with a delay long enough for a partial group to wait for the next
             # group to come back (one batch), the loop converges on full groups

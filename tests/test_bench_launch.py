@@ -120,3 +120,19 @@ def test_merge_lanes_puts_lanes_on_one_clock():
     assert list(lat) == [5, 6, 7, 8]
     assert list(end) == [400_000_000, 1_000_000_000, 600_000_000, 1_500_000_000]
     assert abs(span - 1.5) < 1e-9
+
+
+def test_batcher_preference_per_point():
+    """The preferred batch rows bench.py sets per load point: one full group
+    per instance (bs=1: concurrency / instances; bert: from --bert-preferred-from
+    rows per instance, capped at the model's max batch)."""
+    import bench
+
+    assert bench.bs1_preferred_rows("auto", 64, 2) == [32]
+    assert bench.bs1_preferred_rows("auto", 63, 2) is None
+    assert bench.bs1_preferred_rows("none", 64, 2) is None
+    assert bench.bs1_preferred_rows("16,32", 64, 2) == [16, 32]
+    got = [bench.bert_point_preferred("auto", c, 2, 2) for c in (1, 4, 16, 64, 256)]
+    assert got == [None, 2, 8, 32, 64]
+    assert bench.bert_point_preferred("auto", 4, 2, 8) is None
+    assert bench.bert_point_preferred("none", 64, 2, 2) is None
