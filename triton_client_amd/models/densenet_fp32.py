@@ -127,6 +127,8 @@ class FusedDenseNetFP32:
         # bs128 x 2 streams 47.1k -> 47.6k img/s with v3 on both K11x blocks
         # (profiles/r5_k11x_v3.md)
         self.fuse_v3 = int(os.environ.get("TCAMD_X3_FUSE_V3", "28"))
+        # ... from this many 64-pixel tiles per CU (engine attribute)
+        self.fuse_v3_tiles_per_cu = 2
         # K13x (small-M dense layer, csrc/kernels/densenet_x3s.hip) for the
         # unfused layers of a block with at most this many pixels; 0 disables it
         self.small_m = int(os.environ.get("TCAMD_X3_SMALL_M", "1600"))
@@ -290,7 +292,7 @@ class FusedDenseNetFP32:
         args = (fp, ctot, b, hw, hw, L["cin"], L["s1"].data_ptr(), L["t1"].data_ptr(), L["w1fh"].data_ptr(),
                 L["w1fl"].data_ptr(), L["b1"].data_ptr(), L["w2fh"].data_ptr(), L["w2fl"].data_ptr(),
                 fp + 4 * L["cin"], ctot)
-        if self.fuse_v3 and hw >= self.fuse_v3 and b * hw * hw >= 2 * 64 * _cu_count(self.device):
+        if self.fuse_v3 and hw >= self.fuse_v3 and b * hw * hw >= self.fuse_v3_tiles_per_cu * 64 * _cu_count(self.device):
             hip.x3_dense_fused3(*args, stream=st)
         else:
             hip.x3_dense_fused(*args, stream=st)
