@@ -870,13 +870,16 @@ def bert_sweep(args, srv, model, client, shmod, regions, points, measure, fanout
         if not fanout.verify_replicas(regions[0], nbytes, over_cpu=method == fanout.LOCAL_FALLBACK):
             raise RuntimeError("fan-out replicas differ across ranks after the fan-out timing")
     sweep = []
+    bert_max_batch = 64
+    if not cpu:
+        bert_max_batch = int(client.get_model_config(model, as_json=True)["config"].get("max_batch_size", 64))
     for c in [int(v) for v in args.sweep.split(",") if v]:
         # the batcher's preferred size for this load: one equal group per
         # instance (e.g. c16 on 2 instances ran as 5- and 11-row batches)
         n_inst = max(1, args.bert_instance_count)
         # (from 2 rows per instance: c4 1,312 -> 1,566 infer/s; without the longer
         # queue delay the 2-row preference had run mostly 1-row batches)
-        pref = bert_point_preferred(args.bert_preferred, c, n_inst, args.bert_preferred_from)
+        pref = bert_point_preferred(args.bert_preferred, c, n_inst, args.bert_preferred_from, bert_max_batch)
         if pref and not cpu:
             # with a delay long enough for a partial group to wait for the next
             # group to come back (one batch), the loop converges on full groups

@@ -509,7 +509,9 @@ class BertLarge(Model):
     name = "bert_large"
     platform = "pytorch_libtorch"
     backend = "pytorch"
-    max_batch_size = 64
+    # 128: a bs128 HIP-graph forward runs 4,292 seq/s against 4,095 at bs64
+    # (tools/bert_probe.py --graphs, profiles/r6_bert_batching/)
+    max_batch_size = 128
     SEQ = 384
     inputs = (TensorSpec("input_ids", "INT32", [384]), TensorSpec("attention_mask", "INT32", [384]),
               TensorSpec("token_type_ids", "INT32", [384]))
@@ -523,7 +525,7 @@ class BertLarge(Model):
     # batch anything from 1 to 64 rows, and
     # with power-of-two buckets a 33-row batch paid for 64 (served c64: 33 rows
     # per batch at 11.5 ms vs 7.9 ms for a 32-row forward)
-    BUCKETS = (1, 2, 4, 8, 12, 16, 20, 24, 28, 32, 40, 48, 56, 64)
+    BUCKETS = (1, 2, 4, 8, 12, 16, 20, 24, 28, 32, 40, 48, 56, 64, 80, 96, 112, 128)
     # a second, unmasked ("dense") graph for the buckets from DENSE_FROM rows,
     # picked per batch when no real row is padded.  Below that every batch
     # runs the masked graph: K12 classifies its key chunks, so an all-ones
