@@ -789,6 +789,12 @@ class BertLargeFP32(BertLarge):
     bf16 ``bert_large`` stays the config-4 serving default."""
 
     name = "bert_large_fp32"
+    # 64 rows, as before bert_large went to 128: a bs128 fp32-parity forward
+    # (~110 ms) outlasts the sweep's queue delay, so c256 ran partial 88-row
+    # batches at 1,142 infer/s against 1,200 with 64-row ones
+    # (profiles/r6_bert_batching/)
+    max_batch_size = 64
+    BUCKETS = tuple(b for b in BertLarge.BUCKETS if b <= 64)
 
     def _build_model(self, bert, dev):
         import torch
