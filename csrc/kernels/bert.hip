@@ -13,6 +13,7 @@
 // `bert_large` perf_analyzer config of BASELINE.json).
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "kernels/common.h"
@@ -556,7 +557,8 @@ __global__ void __launch_bounds__(256) x3_cat_kernel(const float* __restrict__ x
 //   16-key tile 2ks (i < 4) or 2ks + 1 (i >= 4), read from V^T in LDS as two
 //   8-B runs.  O^T's C layout: lane = query, reg e -> head dim 16 dt + 4g + e.
 constexpr int kXR = 64 * 2 + 16;  // LDS row: 64 bf16 + 16 B (16 rows' b128 reads spread over all banks)
-constexpr int kLdsAX = 4 * 64 * kXR + 64 * 4;
+constexpr int kBufAX = 4 * 64 * kXR + 64 * 4;  // one chunk: K hi | K lo | V^T hi | V^T lo | key bias
+constexpr int kLdsAX = 2 * kBufAX;             // double-buffered: chunk c + 1 is staged during chunk c
 
 __device__ __forceinline__ void split_pk(float a, float b, uint32_t& hi, uint32_t& lo) {
   hi = pack2(a, b);
@@ -577,11 +579,7 @@ __global__ void __launch_bounds__(64 * NW) attention_x3_kernel(const float* __re
                                                                uint16_t* __restrict__ out3, int S, int heads,
                                                                float scale) {
   extern __shared__ __attribute__((aligned(16))) uint8_t ldsa[];
-  uint8_t* const kh = ldsa;             // K hi [64 keys][kXR]
-  uint8_t* const kl = kh + 64 * kXR;    // K lo
-  uint8_t* const vth = kl + 64 * kXR;   // V^T hi [64 d][kXR]
-  uint8_t* const vtl = vth + 64 * kXR;  // V^T lo
-  float* const kb = reinterpret_cast<float*>(vtl + 64 * kXR);  // the chunk's key bias
+  // per buffer: K hi [64 keys][kXR] | K lo | V^T hi [64 d][kXR] | V^T lo | key bias [64]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int seq = blockIdx.x / heads, h = blockIdx.x - seq * heads;
   const int H = heads * 64, ld = 3 * H;
@@ -608,38 +606,63 @@ __global__ void __launch_bounds__(64 * NW) attention_x3_kernel(const float* __re
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
 
-  for (int c0 = 0; c0 < S; c0 += 64) {
-    __syncthreads();  // the previous chunk's LDS reads are done
-    // stage K row-major: thread -> (key, 4 head dims)
+  // staging of one 64-key chunk, split so that its global loads are in
+  // flight during the previous chunk's math: K row-major (thread -> key, 4
+  // head dims), V transposed (thread -> key pair, 4 head dims: 4-B words of
+  // two keys, a wave's 32 key pairs one contiguous 128-B run per V^T row)
+  constexpr int KIT = 1024 / (64 * NW), VIT = 512 / (64 * NW);
+  float4 kr[KIT], va[VIT], vb[VIT];
+  float mkb = 0.f;
+  auto stage_load = [&](int c0) {
 #pragma unroll
-    for (int it = 0; it < 1024 / (64 * NW); ++it) {
+    for (int it = 0; it < KIT; ++it) {
       const int i = it * 64 * NW + tid, key = i >> 4, d4 = (i & 15) * 4;
-      const float4 kv = *reinterpret_cast<const float4*>(base + (size_t)(c0 + key) * ld + H + d4);
-      uint32_t h0, l0, h1, l1;
-      split_pk(kv.x, kv.y, h0, l0);
-      split_pk(kv.z, kv.w, h1, l1);
-      *reinterpret_cast<uint2*>(kh + key * kXR + d4 * 2) = make_uint2(h0, h1);
-      *reinterpret_cast<uint2*>(kl + key * kXR + d4 * 2) = make_uint2(l0, l1);
+      kr[it] = *reinterpret_cast<const float4*>(base + (size_t)(c0 + key) * ld + H + d4);
     }
-    // stage V transposed: thread -> (key pair, 8 head dims); each V^T row gets
-    // 4-B words of two keys, a wave's 32 key pairs one contiguous 128-B run
-    for (int u = tid; u < 256; u += 64 * NW) {
-      const int kp = u & 31, d8 = (u >> 5) * 8;
-      const float* r0 = base + (size_t)(c0 + 2 * kp) * ld + 2 * H + d8;
-      const float4 a0 = *reinterpret_cast<const float4*>(r0), a1 = *reinterpret_cast<const float4*>(r0 + 4);
-      const float4 b0 = *reinterpret_cast<const float4*>(r0 + ld), b1 = *reinterpret_cast<const float4*>(r0 + ld + 4);
-      const float va[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      const float vb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+    for (int it = 0; it < VIT; ++it) {
+      const int u = it * 64 * NW + tid, kp = u & 31, d4 = (u >> 5) * 4;
+      const float* r0 = base + (size_t)(c0 + 2 * kp) * ld + 2 * H + d4;
+      va[it] = *reinterpret_cast<const float4*>(r0);
+      vb[it] = *reinterpret_cast<const float4*>(r0 + ld);
+    }
+    if (tid < 64) mkb = (mask && mask[seq * S + c0 + tid] == 0) ? -10000.f : 0.f;
+  };
+  auto stage_store = [&](uint8_t* buf) {
+#pragma unroll
+    for (int it = 0; it < KIT; ++it) {
+      const int i = it * 64 * NW + tid, key = i >> 4, d4 = (i & 15) * 4;
+      uint32_t h0, l0, h1, l1;
+      split_pk(kr[it].x, kr[it].y, h0, l0);
+      split_pk(kr[it].z, kr[it].w, h1, l1);
+      *reinterpret_cast<uint2*>(buf + key * kXR + d4 * 2) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(buf + 64 * kXR + key * kXR + d4 * 2) = make_uint2(l0, l1);
+    }
+#pragma unroll
+    for (int it = 0; it < VIT; ++it) {
+      const int u = it * 64 * NW + tid, kp = u & 31, d4 = (u >> 5) * 4;
+      const float a[4] = {va[it].x, va[it].y, va[it].z, va[it].w}, b[4] = {vb[it].x, vb[it].y, vb[it].z, vb[it].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
         uint32_t hh, ll;
-        split_pk(va[j], vb[j], hh, ll);
-        *reinterpret_cast<uint32_t*>(vth + (d8 + j) * kXR + 4 * kp) = hh;
-        *reinterpret_cast<uint32_t*>(vtl + (d8 + j) * kXR + 4 * kp) = ll;
+        split_pk(a[j], b[j], hh, ll);
+        *reinterpret_cast<uint32_t*>(buf + 128 * kXR + (d4 + j) * kXR + 4 * kp) = hh;
+        *reinterpret_cast<uint32_t*>(buf + 192 * kXR + (d4 + j) * kXR + 4 * kp) = ll;
       }
     }
-    if (tid < 64) kb[tid] = (mask && mask[seq * S + c0 + tid] == 0) ? -10000.f : 0.f;
-    __syncthreads();
+    if (tid < 64) reinterpret_cast<float*>(buf + 256 * kXR)[tid] = mkb;
+  };
+  stage_load(0);
+  stage_store(ldsa);
+  __syncthreads();
+  const int nch = S / 64;
+  for (int ci = 0; ci < nch; ++ci) {
+    uint8_t* const kh = ldsa + (ci & 1) * kBufAX;
+    uint8_t* const kl = kh + 64 * kXR;
+    uint8_t* const vth = kh + 128 * kXR;
+    uint8_t* const vtl = kh + 192 * kXR;
+    const float* const kb = reinterpret_cast<const float*>(kh + 256 * kXR);
+    if (ci + 1 < nch) stage_load(64 * (ci + 1));
 
     // S^T tiles [16 keys][16 queries]
     f32x4 st[4];
@@ -694,6 +717,10 @@ __global__ void __launch_bounds__(64 * NW) attention_x3_kernel(const float* __re
         o[dt] = mma_x3(v4u{a0.x, a0.y, a1.x, a1.y}, v4u{b0.x, b0.y, b1.x, b1.y}, pbh, pbl, o[dt]);
       }
     }
+    // chunk ci + 1 into the other buffer (read last in iteration ci - 1, which
+    // every wave left behind the previous barrier)
+    if (ci + 1 < nch) stage_store(ldsa + ((ci + 1) & 1) * kBufAX);
+    __syncthreads();
   }
   const float inv = 1.f / l;
   if (out3) {
@@ -901,6 +928,14 @@ int tcamd_attention_f32(const float* qkv, const int* mask, void* out, int seqs, 
     return hipErrorInvalidValue;
   float* const o32 = x3 ? nullptr : (float*)out;
   uint16_t* const o3 = x3 ? (uint16_t*)out : nullptr;
+  static std::atomic<bool> attr{false};  // 72.5 KB of dynamic LDS: past the 64 KB default
+  if (!attr.load(std::memory_order_acquire)) {
+    for (const void* fn : {(const void*)attention_x3_kernel<4>, (const void*)attention_x3_kernel<8>}) {
+      const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsAX);
+      if (e != hipSuccess) return e;
+    }
+    attr.store(true, std::memory_order_release);
+  }
   // 128 queries per block (half the K / V staging per query; bs64 x 384: 331
   // -> 248 us) once that still gives every CU a block (bs1 keeps 64: 20.5 vs
   // 21.2 us; profiles/r6_bert_fp32/k12x_ab*.log)
